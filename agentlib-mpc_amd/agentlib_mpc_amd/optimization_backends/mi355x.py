@@ -1,0 +1,199 @@
+"""The MI355X optimization backends (drop-in for the CasADi/IPOPT backends).
+
+``MI355XBackend``      <- ``CasADiFullBackend`` (type ``"casadi"``, `casadi_/full.py:169-179`)
+``MI355XBaseBackend``  <- ``CasADiBaseBackend`` (type ``"casadi_basic"``, `casadi_/basic.py:555-564`)
+``MI355XADMMBackend``  <- ``CasADiADMMBackend`` (type ``"casadi_admm"``, `casadi_/admm.py:341-424`)
+
+Same config schema (``CasadiBackendConfig``, `core/casadi_backend.py:40-92`),
+same ``setup_optimization(var_ref)`` / ``solve(now, current_vars) -> Results``
+contract (`core/casadi_backend.py:108-139`), same variable/parameter layout and
+``Results`` format.  The NLP is solved by the generated HIP interior-point
+kernel.  IPOPT options given in ``solver.options`` (``{"ipopt": {...}}`` or
+``"ipopt.<key>"``) are mapped onto the kernel options; the reference's
+defaults (`data_structures/casadi_utils.py:191-217`: ``max_iter=100``,
+``tol=1e-4``, acceptable tolerances) are applied unless overridden.
+
+Besides the per-agent ``solve``, ``solve_batch`` solves many agents of the
+same structure in one launch (the fleet path used by the ADMM drivers).
+"""
+
+from __future__ import annotations
+
+import time
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import pydantic
+
+from agentlib_mpc_amd.data_structures import admm_datatypes as adt
+from agentlib_mpc_amd.data_structures.mpc_datamodels import (
+    CasadiDiscretizationOptions, DiscretizationMethod, SolverOptions, stats_path,
+)
+from agentlib_mpc_amd.models.casadi_model import CasadiModel
+from agentlib_mpc_amd.optimization_backends import discretization as disc
+from agentlib_mpc_amd.optimization_backends.backend import (
+    ADMMBackend, BackendConfig, OptimizationBackend,
+)
+from agentlib_mpc_amd.optimization_backends.problem import CompiledProblem
+from agentlib_mpc_amd.optimization_backends.results import Results
+from agentlib_mpc_amd.optimization_backends.system import ADMMSystem, BaseSystem, FullSystem
+
+#: reference IPOPT defaults (`casadi_utils.py:197-206`)
+REFERENCE_IPOPT_DEFAULTS = {"max_iter": 100, "tol": 1e-4}
+
+
+class MI355XBackendConfig(BackendConfig):
+    discretization_options: CasadiDiscretizationOptions = pydantic.Field(
+        default_factory=CasadiDiscretizationOptions)
+    solver: SolverOptions = pydantic.Field(default_factory=SolverOptions)
+    build_batch_bat: Optional[Path] = None
+    do_jit: Optional[bool] = None
+    save_only_stats: bool = False
+
+
+def ipopt_options_to_kernel(options: dict) -> dict:
+    """Map IPOPT-style options (nested or dotted) onto kernel option names."""
+    opts = dict(REFERENCE_IPOPT_DEFAULTS)
+    nested = dict(options.get("ipopt", {}))
+    for k, v in options.items():
+        if k.startswith("ipopt."):
+            nested[k[len("ipopt."):]] = v
+    aliases = {"mu_linear_decrease_factor": "kappa_mu", "mu_superlinear_decrease_power": "theta_mu",
+               "barrier_tol_factor": "kappa_eps", "bound_mult_init_val": "bound_mult_init_val",
+               "constr_mult_init_max": "constr_mult_init_max",
+               "alpha_min_frac": "alpha_min_frac"}
+    ignored = {"print_level", "sb", "print_time", "linear_solver", "hessian_approximation",
+               "acceptable_obj_change_tol", "acceptable_dual_inf_tol", "acceptable_constr_viol_tol",
+               "acceptable_compl_inf_tol"}
+    for k, v in nested.items():
+        if k in ignored:
+            continue
+        opts[aliases.get(k, k)] = v
+    return opts
+
+
+class MI355XBackend(OptimizationBackend):
+    """Backend ``"casadi"`` replacement (full system with ``u_prev``)."""
+
+    system_type = FullSystem
+    discretization_types = {
+        DiscretizationMethod.collocation: disc.FullCollocation,
+        DiscretizationMethod.multiple_shooting: disc.FullMultipleShooting,
+    }
+    _supported_models = {"CasadiModel": CasadiModel}
+    config_type = MI355XBackendConfig
+
+    def __init__(self, config: dict):
+        super().__init__(config)
+        self.problem: Optional[CompiledProblem] = None
+        self.system = None
+        self._remembered: Optional[Dict[str, np.ndarray]] = None
+        self.solver_options = ipopt_options_to_kernel(self.config.solver.options)
+
+    # -- setup (`core/casadi_backend.py:108-131`) --------------------------------
+    def setup_optimization(self, var_ref):
+        self.var_ref = var_ref
+        self.system = self.system_type()
+        self.system.initialize(model=self.model, var_ref=var_ref)
+        opts = self.config.discretization_options
+        discretization = self.discretization_types[opts.method](options=opts)
+        nlp = discretization.transcribe(self.system)
+        self.problem = CompiledProblem(nlp, self.system)
+        self._remembered = None
+
+    def _native(self):
+        prob = self.problem.native
+        prob.set_options(**{k: v for k, v in self.solver_options.items()})
+        return prob
+
+    # -- solve (`core/casadi_backend.py:133-139`) --------------------------------
+    def solve(self, now: float, current_vars: dict) -> Results:
+        return self.solve_batch(now, [current_vars])[0]
+
+    def solve_batch(self, now, batch_vars: Sequence[dict], remembered: Optional[list] = None) -> List[Results]:
+        """Solve one NLP per entry of ``batch_vars`` (same structure) in one launch."""
+        import torch
+
+        if self.problem is None:
+            raise RuntimeError("setup_optimization() must be called before solve()")
+        prob = self.problem
+        inputs, P, LB, UB, W = [], [], [], [], []
+        for i, cv in enumerate(batch_vars):
+            mi = prob.mpc_inputs(cv, now)
+            rem = self._remembered if remembered is None else remembered[i]
+            mi.update(prob.initial_guess(mi, rem))
+            p, lbw, ubw, w0 = prob.nlp_inputs(mi)
+            inputs.append(mi)
+            P.append(p); LB.append(lbw); UB.append(ubw); W.append(w0)
+        native = self._native()
+        dev = torch.device("cuda")
+        t0 = time.perf_counter()
+        tp = torch.as_tensor(np.stack(P), dtype=torch.float64, device=dev)
+        tl = torch.as_tensor(np.stack(LB), dtype=torch.float64, device=dev)
+        tu = torch.as_tensor(np.stack(UB), dtype=torch.float64, device=dev)
+        tw = torch.as_tensor(np.stack(W), dtype=torch.float64, device=dev)
+        n = len(batch_vars)
+        from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+
+        lam_g = torch.empty((n, prob.nlp.ng_total), dtype=torch.float64, device=dev)
+        st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=dev)
+        native.solve(tp, tl, tu, tw, lam_g=lam_g, stats=st)
+        w = tw.cpu().numpy()
+        stats = stats_to_dicts(st.cpu().numpy().tobytes())
+        wall = time.perf_counter() - t0
+        results = []
+        for i in range(n):
+            s = stats[i]
+            s["t_wall_total"] = wall
+            outs = prob.outputs(w[i])
+            if remembered is None and i == n - 1:
+                self._remembered = outs
+            elif remembered is not None:
+                remembered[i] = outs
+            res = prob.make_results(inputs[i], w[i], s)
+            self.save_result_df(res, now)
+            results.append(res)
+        return results
+
+    # -- results file (`core/casadi_backend.py:263-307`) ---------------------------
+    def save_result_df(self, results: Results, now: float = 0):
+        if not self.config.save_results:
+            return
+        res_file = self.config.results_file
+        if not self.results_folder_exists():
+            if not self.config.save_only_stats:
+                results.write_columns(res_file)
+            results.write_stats_columns(stats_path(res_file))
+        with open(stats_path(res_file), "a") as f:
+            f.write(results.stats_line(str(now)))
+        if self.config.save_only_stats:
+            return
+        df = results.df
+        df.index = [str((now, x)) for x in df.index]
+        df.to_csv(res_file, mode="a", header=False)
+
+
+class MI355XBaseBackend(MI355XBackend):
+    """Backend ``"casadi_basic"`` replacement."""
+
+    system_type = BaseSystem
+    discretization_types = {
+        DiscretizationMethod.collocation: disc.BasicCollocation,
+        DiscretizationMethod.multiple_shooting: disc.BasicMultipleShooting,
+    }
+
+
+class MI355XADMMBackend(MI355XBackend, ADMMBackend):
+    """Backend ``"casadi_admm"`` replacement (consensus and exchange terms)."""
+
+    system_type = ADMMSystem
+    discretization_types = {
+        DiscretizationMethod.collocation: disc.ADMMCollocation,
+        DiscretizationMethod.multiple_shooting: disc.ADMMMultipleShooting,
+    }
+
+    @property
+    def coupling_grid(self) -> list:
+        """`casadi_/admm.py:360-362`: grid of the multipliers parameter group."""
+        return list(self.problem.nlp.par_groups[self.system.multipliers.name].grid)

@@ -1,0 +1,204 @@
+"""A transcribed problem: layout maps, host marshalling and the native solver.
+
+Host-side marshalling restates the reference input path:
+``CasADiBackend._get_current_mpc_inputs`` (`core/casadi_backend.py:141-253`),
+``Discretization._determine_initial_guess`` (`core/discretization.py:212-245`),
+the NLP input map ``_mpc_inputs_to_nlp_inputs`` (:277-348), the output map
+(:350-358), warm start ``_remember_solution`` (:247-251) and the result
+matrix ``_result_map`` / ``_create_result_format`` (:360-484).
+
+Everything here is O(#variables x grid) numpy bookkeeping; the solve itself
+is the native batched kernel (:class:`agentlib_mpc_amd.runtime.native.NativeProblem`).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pandas as pd
+
+from agentlib_mpc_amd.optimization_backends.discretization import StageNLP
+from agentlib_mpc_amd.optimization_backends.results import ResultLayout, Results
+from agentlib_mpc_amd.optimization_backends.system import (
+    OptimizationParameter, OptimizationVariable, System,
+)
+from agentlib_mpc_amd.runtime import codegen
+from agentlib_mpc_amd.utils import sampling
+
+GUESS_PREFIX = "guess_"
+
+
+class CompiledProblem:
+    def __init__(self, nlp: StageNLP, system: System):
+        self.nlp = nlp
+        self.system = system
+        self.gen = codegen.generate(nlp)
+        self._native = None
+        self.layout = self._result_layout()
+
+    # -- native ------------------------------------------------------------------
+    @property
+    def native(self):
+        if self._native is None:
+            from agentlib_mpc_amd.runtime.native import NativeProblem
+
+            self._native = NativeProblem(self.gen)
+        return self._native
+
+    def compile(self):
+        from agentlib_mpc_amd.runtime.native import compile_model
+
+        return compile_model(self.gen)
+
+    # -- inputs ------------------------------------------------------------------
+    def mpc_inputs(self, current_vars: dict, now: float) -> Dict[str, np.ndarray]:
+        """Sample runtime values/bounds onto the group grids (`casadi_backend.py:141-253`)."""
+        out: Dict[str, np.ndarray] = {}
+        for par in self.system.parameters:
+            grid = self.nlp.par_groups[par.name].grid if par.name in self.nlp.par_groups else []
+            mat = np.empty((par.dim, len(grid)))
+            for i, name in enumerate(par.full_names):
+                if name in par.ref_names:
+                    var = current_vars[name]
+                    if var.value is None:
+                        raise ValueError(f"Input for variable {name} is empty. Cannot solve optimization problem.")
+                    try:
+                        method = var.interpolation_method
+                    except AttributeError as e:
+                        raise TypeError(
+                            f"The variable {name} does not have an interpolationmethod. All Variables "
+                            "used in MPC need to be of type MPCVariable (subclass of AgentVariable).") from e
+                    mat[i, :] = sampling.sample(trajectory=var.value, grid=grid, current=now, method=method)
+                else:
+                    mat[i, :] = par.defaults[i]
+            out[par.name] = mat
+        for var in self.system.variables:
+            grid = self.nlp.var_groups[var.name].grid if var.name in self.nlp.var_groups else []
+            lb = np.empty((var.dim, len(grid)))
+            ub = np.empty((var.dim, len(grid)))
+            for i, name in enumerate(var.full_names):
+                if name in var.ref_names:
+                    av = current_vars[name]
+                    method = getattr(av, "interpolation_method", "linear")
+                    ub[i, :] = sampling.sample(trajectory=av.ub, grid=grid, current=now, method=method)
+                    lb[i, :] = sampling.sample(trajectory=av.lb, grid=grid, current=now, method=method)
+                else:
+                    lb[i, :] = var.default_lb[i]
+                    ub[i, :] = var.default_ub[i]
+            out[f"lb_{var.name}"] = lb
+            out[f"ub_{var.name}"] = ub
+        return out
+
+    def initial_guess(self, mpc_inputs: Dict[str, np.ndarray],
+                      remembered: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, np.ndarray]:
+        """`core/discretization.py:212-245` (no time shift of the previous optimum)."""
+        guesses = {}
+        for name, lay in self.nlp.var_groups.items():
+            g = None if remembered is None else remembered.get(name)
+            if g is None:
+                key = f"initial_{name}"
+                if key in mpc_inputs:
+                    meas = mpc_inputs[key]
+                    meas = meas[:, -1:] if meas.shape[1] > 1 else meas
+                    g = np.tile(meas, len(lay.grid))
+                else:
+                    with np.errstate(invalid="ignore"):
+                        g = 0.5 * (mpc_inputs[f"lb_{name}"] + mpc_inputs[f"ub_{name}"])
+                    g = np.nan_to_num(g, posinf=0, neginf=-0)
+            guesses[GUESS_PREFIX + name] = np.asarray(g, dtype=float)
+        return guesses
+
+    def nlp_inputs(self, mpc_inputs: Dict[str, np.ndarray]) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+        """Permutation of the MPC input matrices into (p, lbw, ubw, w0)."""
+        nlp = self.nlp
+        p = np.full(nlp.npar, np.nan)
+        for name, lay in nlp.par_groups.items():
+            if lay.dim:
+                p[lay.index] = mpc_inputs[name]
+        lbw = np.full(nlp.nw, np.nan)
+        ubw = np.full(nlp.nw, np.nan)
+        w0 = np.full(nlp.nw, np.nan)
+        for name, lay in nlp.var_groups.items():
+            if not lay.dim:
+                continue
+            idx = lay.index
+            lbw[idx] = mpc_inputs[f"lb_{name}"]
+            ubw[idx] = mpc_inputs[f"ub_{name}"]
+            w0[idx] = mpc_inputs[GUESS_PREFIX + name]
+            for t, cols in enumerate(lay.columns):
+                for i, c in enumerate(cols):
+                    if lay.lb_par[t][i] >= 0:
+                        lbw[c] = p[lay.lb_par[t][i]]
+                    if lay.ub_par[t][i] >= 0:
+                        ubw[c] = p[lay.ub_par[t][i]]
+                    if lay.guess_par[t][i] >= 0:
+                        w0[c] = p[lay.guess_par[t][i]]
+        if np.isnan(p).any() or np.isnan(lbw).any() or np.isnan(ubw).any():
+            raise ValueError("incomplete NLP inputs (NaN in parameters or bounds)")
+        return p, lbw, ubw, np.nan_to_num(w0)
+
+    def outputs(self, w: np.ndarray) -> Dict[str, np.ndarray]:
+        """``_nlp_outputs_to_mpc_outputs``: group matrices of the optimum."""
+        return {name: np.asarray(w)[lay.index] for name, lay in self.nlp.var_groups.items()}
+
+    # -- results -------------------------------------------------------------------
+    def _result_layout(self) -> ResultLayout:
+        nlp = self.nlp
+        full = set()
+        for lay in list(nlp.var_groups.values()) + list(nlp.par_groups.values()):
+            full.update(lay.grid)
+        full_grid = sorted(full)
+        pos = {t: i for i, t in enumerate(full_grid)}
+        columns, blocks, var_rows = [], [], {}
+        for par in self.system.parameters:
+            if not par.full_names or par.name not in nlp.par_groups:
+                continue
+            lay = nlp.par_groups[par.name]
+            columns += [("parameter", n) for n in par.full_names]
+            blocks.append(("parameter", par.name, par.dim, self._rows_cols(lay.grid, full_grid, pos)))
+        for var in self.system.variables:
+            if not var.full_names or var.name not in nlp.var_groups:
+                continue
+            lay = nlp.var_groups[var.name]
+            rc = self._rows_cols(lay.grid, full_grid, pos)
+            for key, header in (("var", "variable"), ("ub", "upper"), ("lb", "lower")):
+                columns += [(header, n) for n in var.full_names]
+                blocks.append((key, var.name, var.dim, rc))
+            rows = [r for r, _ in rc if full_grid[r] >= 0]
+            for n in var.full_names:
+                var_rows[n] = rows
+        return ResultLayout(full_grid=full_grid, columns=pd.MultiIndex.from_tuples(columns),
+                            variable_grid_indices=var_rows, blocks=blocks)
+
+    @staticmethod
+    def _rows_cols(grid, full_grid, pos):
+        """(row in full grid, first column of the group grid at that time)."""
+        first = {}
+        for j, t in enumerate(grid):
+            first.setdefault(t, j)
+        return [(pos[t], j) for t, j in sorted(first.items(), key=lambda kv: pos[kv[0]])]
+
+    def result_matrix(self, mpc_inputs: Dict[str, np.ndarray], w: np.ndarray) -> np.ndarray:
+        lay = self.layout
+        outs = self.outputs(w)
+        ncol = len(lay.columns)
+        mat = np.full((len(lay.full_grid), ncol), np.nan)
+        col = 0
+        for kind, name, dim, rc in lay.blocks:
+            if kind == "parameter":
+                src = mpc_inputs[name]
+            elif kind == "var":
+                src = outs[name]
+            else:
+                src = mpc_inputs[f"{kind}_{name}"]
+            for r, j in rc:
+                mat[r, col:col + dim] = src[:, j]
+            col += dim
+        return mat
+
+    def make_results(self, mpc_inputs, w, stats) -> Results:
+        lay = self.layout
+        return Results(matrix=self.result_matrix(mpc_inputs, w), grid=list(lay.full_grid),
+                       columns=lay.columns, stats=stats, variable_grid_indices=lay.variable_grid_indices)

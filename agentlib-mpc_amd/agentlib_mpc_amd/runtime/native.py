@@ -1,0 +1,271 @@
+"""ctypes binding of ``libmpcx.so`` (include/mpcx.h) and the code-object cache.
+
+The product path is native only: if the shared library or a model's code
+object cannot be loaded on a GPU box this module raises — there is no CPU
+fallback.  Device memory and streams come from PyTorch (plumbing only): all
+arrays passed to the C ABI are ``torch.float64`` CUDA(HIP) tensors.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import pathlib
+import shutil
+import subprocess
+import threading
+from typing import Dict, Optional
+
+PKG_DIR = pathlib.Path(__file__).resolve().parents[1]          # agentlib_mpc_amd/
+ROOT_DIR = PKG_DIR.parent                                       # agentlib-mpc_amd/
+REPO_DIR = ROOT_DIR.parent
+CSRC = ROOT_DIR / "csrc"
+INCLUDE = REPO_DIR / "include"
+BUILD_DIR = PKG_DIR / "_build"
+KERNEL_DIR = BUILD_DIR / "kernels"
+LIB_PATH = BUILD_DIR / "libmpcx.so"
+OFFLOAD_ARCH = os.environ.get("MPCX_OFFLOAD_ARCH", "gfx950")
+
+STATUS_NAMES = {
+    0: "Solve_Succeeded",
+    1: "Solved_To_Acceptable_Level",
+    -1: "Maximum_Iterations_Exceeded",
+    -2: "Restoration_Failed",
+    -3: "Error_In_Step_Computation",
+    -4: "Invalid_Number_Detected",
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+# C structs (must match include/mpcx.h)
+# ---------------------------------------------------------------------------
+class ProblemDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("n_stages", "nx", "nv", "ng", "nps", "npg", "abi", "reserved")]
+
+
+_OPT_DOUBLES = [
+    "tol", "dual_inf_tol", "constr_viol_tol", "compl_inf_tol", "acceptable_tol",
+    "mu_init", "mu_min", "kappa_eps", "kappa_mu", "theta_mu", "tau_min",
+    "bound_push", "bound_frac", "bound_relax_factor", "bound_mult_init_val",
+    "constr_mult_init_max", "kappa_sigma", "nlp_scaling_max_gradient", "nlp_scaling_min_value",
+    "delta_w_first", "delta_w_min", "delta_w_max", "kappa_w_plus_bar", "kappa_w_plus",
+    "kappa_w_minus", "delta_c_bar", "kappa_c", "theta_max_fact", "theta_min_fact", "eta_phi",
+    "delta", "s_phi", "s_theta", "gamma_phi", "gamma_theta", "alpha_min_frac",
+]
+_OPT_INTS = ["max_iter", "acceptable_iter", "warm_start_mult", "reserved"]
+
+
+class Options(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in _OPT_DOUBLES] + [(n, ctypes.c_int32) for n in _OPT_INTS]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")] + \
+               [(n, ctypes.c_int32) for n in ("iter_count", "status", "n_inertia_corrections",
+                                              "n_linesearch_fallbacks", "n_factorizations", "reserved")]
+
+
+STATS_BYTES = ctypes.sizeof(Stats)
+EXPORTED_SYMBOLS = [
+    "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
+    "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_batch_solve",
+    "mpcx_admm_group_sums", "mpcx_admm_mean_from_sums", "mpcx_admm_consensus_multipliers",
+    "mpcx_admm_exchange_update", "mpcx_admm_residual_partials", "mpcx_admm_shift",
+]
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise NativeError("hipcc not found; cannot build MI355X kernels")
+
+
+def build_library(force: bool = False) -> pathlib.Path:
+    """Compile libmpcx.so (host runtime + ADMM kernels) for gfx950, in-tree."""
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    srcs = [CSRC / "mpcx_runtime.cpp", CSRC / "admm_kernels.hip"]
+    deps = srcs + [INCLUDE / "mpcx.h", CSRC / "mpcx_internal.h"]
+    if LIB_PATH.exists() and not force:
+        if LIB_PATH.stat().st_mtime >= max(p.stat().st_mtime for p in deps):
+            return LIB_PATH
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17",
+           "-Wno-unused-result", "-Wno-unused-value", f"-I{INCLUDE}", f"-I{CSRC}",
+           *map(str, srcs), "-o", str(tmp)]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise NativeError(f"building libmpcx.so failed:\n{res.stderr[-4000:]}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def load_library():
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            raise NativeError(
+                f"{LIB_PATH} is missing: run __graft_entry__.build() (or "
+                "agentlib_mpc_amd.runtime.native.build_library()) first. There is no CPU fallback.")
+        lib = ctypes.CDLL(str(LIB_PATH))
+        vp, i32, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_double
+        lib.mpcx_version.restype = ctypes.c_int
+        lib.mpcx_default_options.argtypes = [ctypes.POINTER(Options)]
+        lib.mpcx_default_options.restype = None
+        lib.mpcx_problem_create.argtypes = [ctypes.POINTER(ProblemDesc), ctypes.c_char_p, ctypes.POINTER(vp)]
+        lib.mpcx_problem_destroy.argtypes = [vp]
+        lib.mpcx_set_options.argtypes = [vp, ctypes.POINTER(Options)]
+        lib.mpcx_reserve.argtypes = [vp, i32]
+        lib.mpcx_workspace_bytes_per_agent.argtypes = [vp]
+        lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
+        lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp]
+        lib.mpcx_admm_group_sums.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp]
+        lib.mpcx_admm_mean_from_sums.argtypes = [i32, i32, vp, vp, vp, vp]
+        lib.mpcx_admm_consensus_multipliers.argtypes = [i32, i32, vp, i32, vp, vp, vp, f64, vp, vp, vp]
+        lib.mpcx_admm_exchange_update.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp]
+        lib.mpcx_admm_residual_partials.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, vp, f64, i32, vp, vp]
+        lib.mpcx_admm_shift.argtypes = [i32, i32, i32, vp, vp]
+        for name in EXPORTED_SYMBOLS:
+            getattr(lib, name)  # raises AttributeError if a symbol is missing
+        _lib = lib
+        return lib
+
+
+def default_options() -> Options:
+    opts = Options()
+    load_library().mpcx_default_options(ctypes.byref(opts))
+    return opts
+
+
+# ---------------------------------------------------------------------------
+# code objects
+# ---------------------------------------------------------------------------
+def _kernel_deps_hash() -> str:
+    h = hashlib.sha1()
+    for p in (CSRC / "mpcx_ipm.hip", CSRC / "mpcx_internal.h", INCLUDE / "mpcx.h"):
+        h.update(p.read_bytes())
+    return h.hexdigest()[:10]
+
+
+def code_object_path(gen_key: str) -> pathlib.Path:
+    return KERNEL_DIR / f"mpcx_{gen_key}_{_kernel_deps_hash()}_{OFFLOAD_ARCH}.hsaco"
+
+
+def compile_model(gen, verbose: bool = False) -> pathlib.Path:
+    """Compile a generated model source to a gfx950 code object (cached)."""
+    KERNEL_DIR.mkdir(parents=True, exist_ok=True)
+    out = code_object_path(gen.key)
+    if out.exists():
+        return out
+    src = out.with_suffix(".hip")
+    src.write_text(gen.source)
+    tmp = out.with_suffix(".tmp")
+    cmd = [_hipcc(), "--genco", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17",
+           f"-I{INCLUDE}", f"-I{CSRC}", str(src), "-o", str(tmp)]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise NativeError(f"compiling {src} failed:\n{res.stderr[-4000:]}")
+    if verbose and res.stderr:
+        print(res.stderr)
+    os.replace(tmp, out)
+    return out
+
+
+class NativeProblem:
+    """Owns one ``mpcx_handle`` (code object + workspace) for a problem structure."""
+
+    def __init__(self, gen, hsaco: Optional[pathlib.Path] = None):
+        self.lib = load_library()
+        self.gen = gen
+        d = gen.dims
+        self.desc = ProblemDesc(n_stages=d["N"], nx=d["NX"], nv=d["NV"], ng=d["NG"],
+                                nps=d["NPS"], npg=d["NPG"], abi=3, reserved=0)
+        path = hsaco or code_object_path(gen.key)
+        if not pathlib.Path(path).exists():
+            path = compile_model(gen)
+        handle = ctypes.c_void_p()
+        rc = self.lib.mpcx_problem_create(ctypes.byref(self.desc), str(path).encode(), ctypes.byref(handle))
+        if rc != 0:
+            raise NativeError(f"mpcx_problem_create failed ({rc}) for {path}")
+        self.handle = handle
+        self.options = default_options()
+        self.nw = d["NX"] + d["N"] * (d["NV"] + d["NX"])
+        self.ng_total = d["N"] * d["NG"]
+        self.npar = d["NPG"] + d["N"] * d["NPS"]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                self.lib.mpcx_problem_destroy(h)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+            self.handle = None
+
+    def set_options(self, **kw):
+        for k, v in kw.items():
+            if not hasattr(self.options, k):
+                raise KeyError(f"unknown solver option {k!r}")
+            setattr(self.options, k, v)
+        rc = self.lib.mpcx_set_options(self.handle, ctypes.byref(self.options))
+        if rc != 0:
+            raise NativeError(f"mpcx_set_options failed ({rc})")
+
+    def workspace_bytes_per_agent(self) -> int:
+        return int(self.lib.mpcx_workspace_bytes_per_agent(self.handle))
+
+    def reserve(self, n_agents: int):
+        rc = self.lib.mpcx_reserve(self.handle, int(n_agents))
+        if rc != 0:
+            raise NativeError(f"mpcx_reserve failed ({rc})")
+
+    def solve(self, p, lbw, ubw, w, lbg=None, ubg=None, lam_g=None, lam_w=None, stats=None,
+              stream=None):
+        """Launch the batched solve on device tensors (stream-ordered, async)."""
+        import torch
+
+        n = int(p.shape[0])
+        for name, t, cols in (("p", p, self.npar), ("lbw", lbw, self.nw), ("ubw", ubw, self.nw),
+                              ("w", w, self.nw)):
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or tuple(t.shape) != (n, cols):
+                raise ValueError(f"{name} must be a contiguous float64 device tensor of shape {(n, cols)}")
+        if (lbg is None) != (ubg is None):
+            raise ValueError("lbg and ubg must be given together")
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        rc = self.lib.mpcx_batch_solve(self.handle, n, ptr(p), ptr(lbw), ptr(ubw), ptr(lbg), ptr(ubg),
+                                       ptr(w), ptr(lam_g), ptr(lam_w), ptr(stats), ctypes.c_void_p(stream))
+        if rc != 0:
+            raise NativeError(f"mpcx_batch_solve failed ({rc})")
+
+
+def stats_to_dicts(raw_bytes) -> list:
+    """Decode a uint8 tensor/bytes of n * sizeof(mpcx_stats) into dicts."""
+    buf = bytes(raw_bytes)
+    n = len(buf) // STATS_BYTES
+    arr = (Stats * n).from_buffer_copy(buf)
+    out = []
+    for s in arr:
+        out.append({
+            "obj": s.obj, "primal_inf": s.primal_inf, "dual_inf": s.dual_inf,
+            "compl_inf": s.compl_inf, "mu": s.mu, "obj_scale": s.obj_scale,
+            "iter_count": s.iter_count, "status": s.status,
+            "return_status": STATUS_NAMES.get(s.status, str(s.status)),
+            "success": s.status in (0, 1),
+            "n_inertia_corrections": s.n_inertia_corrections,
+            "n_linesearch_fallbacks": s.n_linesearch_fallbacks,
+            "n_factorizations": s.n_factorizations,
+        })
+    return out

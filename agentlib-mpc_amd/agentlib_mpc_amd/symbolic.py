@@ -1,0 +1,682 @@
+"""Scalar symbolic expressions: the tracer, AD and code generator of this backend.
+
+The reference builds its NLPs with CasADi ``MX``/``SX`` symbols and lets
+``nlpsol(..., {"expand": True})`` turn them into straight-line scalar graphs
+(`agentlib_mpc/data_structures/casadi_utils.py:191-217`).  CasADi is not part of
+this framework; models written against the ``CasadiModel`` API
+(`agentlib_mpc/models/casadi_model.py:36-152`) are traced into the hash-consed
+DAG below instead.  It supports the operator subset the reference models use
+(``+ - * / **``, unary minus, ``exp log sqrt tanh sin cos fabs fmax fmin
+if_else`` and comparisons), symbolic forward differentiation (for gradients,
+Jacobians and Lagrangian Hessians) and emission of straight-line C/HIP code.
+
+Nodes are interned: building the same (op, args) twice returns the same object,
+so common sub-expressions are shared automatically and code generation emits
+each node once.
+"""
+
+from __future__ import annotations
+
+import math
+import numbers
+from typing import Dict, Iterable, List, Sequence, Tuple, Union
+
+import numpy as np
+
+__all__ = [
+    "Expr", "SX", "sym", "const", "as_expr", "exp", "log", "sqrt", "tanh", "sin",
+    "cos", "fabs", "fmax", "fmin", "if_else", "sum1", "diff", "gradient",
+    "jacobian", "hessian", "substitute", "free_symbols", "evaluate", "CodeGen",
+    "inf",
+]
+
+inf = math.inf
+
+_UNARY = {"neg", "exp", "log", "sqrt", "tanh", "sin", "cos", "fabs", "sq"}
+_BINARY = {"add", "sub", "mul", "div", "pow", "fmax", "fmin", "lt", "le", "eq", "ne"}
+
+
+class Expr:
+    """A node of the scalar expression DAG (interned)."""
+
+    __slots__ = ("op", "args", "value", "name", "uid", "__weakref__")
+    _table: Dict[tuple, "Expr"] = {}
+    _counter = 0
+
+    def __new__(cls, op: str, args: tuple = (), value=None, name: str = None):
+        if op == "sym":
+            key = None  # symbols are never merged
+        elif op == "const":
+            v = float(value)
+            # -0.0 and 0.0 compare equal; keep one representative
+            key = ("const", 0.0 if v == 0.0 else v) if not math.isnan(v) else None
+        else:
+            key = (op, tuple(a.uid for a in args))
+        if key is not None:
+            hit = cls._table.get(key)
+            if hit is not None:
+                return hit
+        obj = object.__new__(cls)
+        obj.op = op
+        obj.args = args
+        obj.value = None if value is None else float(value)
+        obj.name = name
+        Expr._counter += 1
+        obj.uid = Expr._counter
+        if key is not None:
+            cls._table[key] = obj
+        return obj
+
+    # -- python protocol -------------------------------------------------------
+    def __repr__(self):
+        return to_string(self)
+
+    def __hash__(self):
+        return self.uid
+
+    # nodes are immutable and interned: copies are the node itself
+    def __copy__(self):
+        return self
+
+    def __deepcopy__(self, memo):
+        return self
+
+    def is_const(self, v=None) -> bool:
+        return self.op == "const" and (v is None or self.value == v)
+
+    @property
+    def shape(self):
+        return (1, 1)
+
+    def __float__(self):
+        if self.op == "const":
+            return self.value
+        raise TypeError(f"Cannot convert non-constant expression {self} to float")
+
+    # arithmetic
+    def __add__(self, o):
+        return add(self, o)
+
+    def __radd__(self, o):
+        return add(o, self)
+
+    def __sub__(self, o):
+        return sub(self, o)
+
+    def __rsub__(self, o):
+        return sub(o, self)
+
+    def __mul__(self, o):
+        return mul(self, o)
+
+    def __rmul__(self, o):
+        return mul(o, self)
+
+    def __truediv__(self, o):
+        return div(self, o)
+
+    def __rtruediv__(self, o):
+        return div(o, self)
+
+    def __pow__(self, o, modulo=None):
+        return power(self, o)
+
+    def __rpow__(self, o):
+        return power(o, self)
+
+    def __neg__(self):
+        return neg(self)
+
+    def __pos__(self):
+        return self
+
+    def __abs__(self):
+        return fabs(self)
+
+    # comparisons build expressions (as CasADi does); equality of python
+    # objects is identity because nodes are interned
+    def __lt__(self, o):
+        return _cmp("lt", self, o)
+
+    def __le__(self, o):
+        return _cmp("le", self, o)
+
+    def __gt__(self, o):
+        return _cmp("lt", o, self)
+
+    def __ge__(self, o):
+        return _cmp("le", o, self)
+
+    def __eq__(self, o):  # noqa: D105 - identity semantics kept for dict keys
+        if isinstance(o, Expr):
+            return self is o
+        return NotImplemented
+
+    __array_priority__ = 1000
+
+
+SX = Expr
+
+
+def const(v: float) -> Expr:
+    return Expr("const", value=v)
+
+
+ZERO = const(0.0)
+ONE = const(1.0)
+
+
+def sym(name: str) -> Expr:
+    return Expr("sym", name=name)
+
+
+def as_expr(x) -> Expr:
+    if isinstance(x, Expr):
+        return x
+    if hasattr(x, "sym") and isinstance(getattr(x, "sym"), Expr):
+        return x.sym
+    if isinstance(x, (numbers.Real, np.floating, np.integer, bool)):
+        return const(float(x))
+    if isinstance(x, np.ndarray) and x.size == 1:
+        return const(float(x.reshape(-1)[0]))
+    raise TypeError(f"Cannot convert {type(x)} to a symbolic expression")
+
+
+def _binary(op, a, b):
+    return Expr(op, (a, b))
+
+
+def add(a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        return const(a.value + b.value)
+    if a.is_const(0.0):
+        return b
+    if b.is_const(0.0):
+        return a
+    if b.op == "neg":
+        return sub(a, b.args[0])
+    return _binary("add", a, b)
+
+
+def sub(a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        return const(a.value - b.value)
+    if b.is_const(0.0):
+        return a
+    if a.is_const(0.0):
+        return neg(b)
+    if a is b:
+        return ZERO
+    if b.op == "neg":
+        return add(a, b.args[0])
+    return _binary("sub", a, b)
+
+
+def mul(a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        return const(a.value * b.value)
+    # CasADi's SX simplifier also drops multiplications by structural zeros
+    if a.is_const(0.0) or b.is_const(0.0):
+        return ZERO
+    if a.is_const(1.0):
+        return b
+    if b.is_const(1.0):
+        return a
+    if a.is_const(-1.0):
+        return neg(b)
+    if b.is_const(-1.0):
+        return neg(a)
+    if a is b:
+        return Expr("sq", (a,))
+    return _binary("mul", a, b)
+
+
+def div(a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        return const(a.value / b.value) if b.value != 0 else const(math.copysign(math.inf, a.value) if a.value else math.nan)
+    if a.is_const(0.0):
+        return ZERO
+    if b.is_const(1.0):
+        return a
+    if b.is_const(-1.0):
+        return neg(a)
+    return _binary("div", a, b)
+
+
+def neg(a) -> Expr:
+    a = as_expr(a)
+    if a.op == "const":
+        return const(-a.value)
+    if a.op == "neg":
+        return a.args[0]
+    return Expr("neg", (a,))
+
+
+def power(a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        return const(a.value ** b.value)
+    if b.op == "const":
+        if b.value == 0.0:
+            return ONE
+        if b.value == 1.0:
+            return a
+        if b.value == 2.0:
+            return Expr("sq", (a,))
+        if b.value == -1.0:
+            return div(ONE, a)
+        if b.value == 0.5:
+            return sqrt(a)
+    return _binary("pow", a, b)
+
+
+def _unary_fold(op, fn):
+    def f(a) -> Expr:
+        a = as_expr(a)
+        if a.op == "const":
+            return const(fn(a.value))
+        return Expr(op, (a,))
+
+    f.__name__ = op
+    return f
+
+
+def _safe(fn):
+    def g(v):
+        try:
+            return fn(v)
+        except (ValueError, OverflowError):
+            return math.nan
+
+    return g
+
+
+exp = _unary_fold("exp", _safe(math.exp))
+log = _unary_fold("log", _safe(lambda v: math.log(v) if v > 0 else (-math.inf if v == 0 else math.nan)))
+sqrt = _unary_fold("sqrt", _safe(math.sqrt))
+tanh = _unary_fold("tanh", math.tanh)
+sin = _unary_fold("sin", math.sin)
+cos = _unary_fold("cos", math.cos)
+fabs = _unary_fold("fabs", abs)
+
+
+def sq(a) -> Expr:
+    a = as_expr(a)
+    if a.op == "const":
+        return const(a.value * a.value)
+    return Expr("sq", (a,))
+
+
+def fmax(a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        return const(max(a.value, b.value))
+    return _binary("fmax", a, b)
+
+
+def fmin(a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        return const(min(a.value, b.value))
+    return _binary("fmin", a, b)
+
+
+def _cmp(op, a, b) -> Expr:
+    a, b = as_expr(a), as_expr(b)
+    if a.op == "const" and b.op == "const":
+        fn = {"lt": a.value < b.value, "le": a.value <= b.value,
+              "eq": a.value == b.value, "ne": a.value != b.value}[op]
+        return const(1.0 if fn else 0.0)
+    return _binary(op, a, b)
+
+
+def if_else(cond, a, b, short_circuit: bool = False) -> Expr:
+    """``cond ? a : b`` with the CasADi argument order (`ca.if_else`)."""
+    cond, a, b = as_expr(cond), as_expr(a), as_expr(b)
+    if cond.op == "const":
+        return a if cond.value != 0 else b
+    if a is b:
+        return a
+    return Expr("if_else", (cond, a, b))
+
+
+def sum1(items: Iterable) -> Expr:
+    out = ZERO
+    for it in items:
+        out = add(out, it)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# traversal helpers
+# ---------------------------------------------------------------------------
+
+def topo_order(outputs: Sequence[Expr]) -> List[Expr]:
+    """Post-order (children first) list of all nodes reachable from outputs."""
+    seen = set()
+    order: List[Expr] = []
+    for root in outputs:
+        root = as_expr(root)
+        if root.uid in seen:
+            continue
+        stack = [(root, False)]
+        while stack:
+            node, expanded = stack.pop()
+            if expanded:
+                order.append(node)
+                continue
+            if node.uid in seen:
+                continue
+            seen.add(node.uid)
+            stack.append((node, True))
+            for a in reversed(node.args):
+                if a.uid not in seen:
+                    stack.append((a, False))
+    return order
+
+
+def free_symbols(outputs: Sequence[Expr]) -> List[Expr]:
+    return [n for n in topo_order(outputs) if n.op == "sym"]
+
+
+def depends_on(e: Expr, syms: Iterable[Expr]) -> bool:
+    ids = {s.uid for s in syms}
+    return any(n.uid in ids for n in topo_order([e]))
+
+
+def substitute(outputs: Sequence[Expr], mapping: Dict[Expr, Union[Expr, float]]) -> List[Expr]:
+    """Replace symbols (or any node) by other expressions, rebuilding the DAG."""
+    repl = {k.uid: as_expr(v) for k, v in mapping.items()}
+    memo: Dict[int, Expr] = {}
+    outs = [as_expr(o) for o in outputs]
+    for node in topo_order(outs):
+        if node.uid in repl:
+            memo[node.uid] = repl[node.uid]
+            continue
+        if node.op in ("sym", "const"):
+            memo[node.uid] = node
+            continue
+        new_args = [memo[a.uid] for a in node.args]
+        memo[node.uid] = _rebuild(node.op, new_args)
+    return [memo[o.uid] for o in outs]
+
+
+def _rebuild(op: str, args: List[Expr]) -> Expr:
+    if op == "add":
+        return add(*args)
+    if op == "sub":
+        return sub(*args)
+    if op == "mul":
+        return mul(*args)
+    if op == "div":
+        return div(*args)
+    if op == "neg":
+        return neg(args[0])
+    if op == "pow":
+        return power(*args)
+    if op == "sq":
+        return sq(args[0])
+    if op in ("lt", "le", "eq", "ne"):
+        return _cmp(op, *args)
+    if op == "fmax":
+        return fmax(*args)
+    if op == "fmin":
+        return fmin(*args)
+    if op == "if_else":
+        return if_else(*args)
+    return {"exp": exp, "log": log, "sqrt": sqrt, "tanh": tanh, "sin": sin,
+            "cos": cos, "fabs": fabs}[op](args[0])
+
+
+# ---------------------------------------------------------------------------
+# differentiation
+# ---------------------------------------------------------------------------
+
+def diff(e, x: Expr, _memo: Dict[int, Expr] = None) -> Expr:
+    """Symbolic derivative d e / d x (x must be a symbol)."""
+    e = as_expr(e)
+    if _memo is None:
+        _memo = {}
+    for node in topo_order([e]):
+        if node.uid in _memo:
+            continue
+        _memo[node.uid] = _diff_node(node, x, _memo)
+    return _memo[e.uid]
+
+
+def _diff_node(n: Expr, x: Expr, m: Dict[int, Expr]) -> Expr:
+    op = n.op
+    if op == "sym":
+        return ONE if n is x else ZERO
+    if op == "const":
+        return ZERO
+    a = n.args[0]
+    da = m[a.uid]
+    if op == "neg":
+        return neg(da)
+    if op == "add":
+        return add(da, m[n.args[1].uid])
+    if op == "sub":
+        return sub(da, m[n.args[1].uid])
+    if op == "mul":
+        b = n.args[1]
+        db = m[b.uid]
+        return add(mul(da, b), mul(a, db))
+    if op == "div":
+        b = n.args[1]
+        db = m[b.uid]
+        # (da*b - a*db)/b^2 == da/b - (a/b)*db/b
+        t1 = div(da, b)
+        t2 = mul(div(n, b), db) if not db.is_const(0.0) else ZERO
+        return sub(t1, t2)
+    if op == "sq":
+        return mul(mul(const(2.0), a), da)
+    if op == "pow":
+        b = n.args[1]
+        db = m[b.uid]
+        if b.op == "const":
+            return mul(mul(b, power(a, const(b.value - 1.0))), da)
+        # d(a^b) = a^b (db log a + b da / a)
+        return mul(n, add(mul(db, log(a)), div(mul(b, da), a)))
+    if op == "exp":
+        return mul(n, da)
+    if op == "log":
+        return div(da, a)
+    if op == "sqrt":
+        return div(da, mul(const(2.0), n))
+    if op == "tanh":
+        return mul(sub(ONE, sq(n)), da)
+    if op == "sin":
+        return mul(cos(a), da)
+    if op == "cos":
+        return neg(mul(sin(a), da))
+    if op == "fabs":
+        # sign(a) * da, sign as if_else to keep it straight-line
+        return mul(if_else(_cmp("lt", a, ZERO), const(-1.0), ONE), da)
+    if op in ("fmax", "fmin"):
+        b = n.args[1]
+        db = m[b.uid]
+        cond = _cmp("le", b, a) if op == "fmax" else _cmp("le", a, b)
+        return if_else(cond, da, db)
+    if op == "if_else":
+        c, t, f = n.args
+        return if_else(c, m[t.uid], m[f.uid])
+    if op in ("lt", "le", "eq", "ne"):
+        return ZERO
+    raise NotImplementedError(op)
+
+
+def gradient(f, xs: Sequence[Expr]) -> List[Expr]:
+    f = as_expr(f)
+    return [diff(f, x) for x in xs]
+
+
+def jacobian(fs: Sequence, xs: Sequence[Expr]) -> List[List[Expr]]:
+    return [[diff(as_expr(f), x) for x in xs] for f in fs]
+
+
+def hessian(f, xs: Sequence[Expr]) -> List[List[Expr]]:
+    g = gradient(f, xs)
+    return [[diff(gi, xj) for xj in xs] for gi in g]
+
+
+# ---------------------------------------------------------------------------
+# numeric evaluation (vectorised over a leading batch axis)
+# ---------------------------------------------------------------------------
+
+def evaluate(outputs: Sequence, values: Dict[Expr, Union[float, np.ndarray]]) -> List[np.ndarray]:
+    """Evaluate expressions with numpy; values may be arrays (broadcast)."""
+    outs = [as_expr(o) for o in outputs]
+    vals: Dict[int, object] = {}
+    for k, v in values.items():
+        vals[as_expr(k).uid] = np.asarray(v, dtype=float)
+    with np.errstate(all="ignore"):
+        for n in topo_order(outs):
+            if n.uid in vals:
+                continue
+            op = n.op
+            if op == "const":
+                vals[n.uid] = np.float64(n.value)
+                continue
+            if op == "sym":
+                raise KeyError(f"No value for symbol {n.name}")
+            a = [vals[x.uid] for x in n.args]
+            vals[n.uid] = _NUMPY_OPS[op](*a)
+    return [np.asarray(vals[o.uid], dtype=float) for o in outs]
+
+
+_NUMPY_OPS = {
+    "add": np.add, "sub": np.subtract, "mul": np.multiply, "div": np.divide,
+    "neg": np.negative, "pow": np.power, "sq": np.square, "exp": np.exp,
+    "log": np.log, "sqrt": np.sqrt, "tanh": np.tanh, "sin": np.sin, "cos": np.cos,
+    "fabs": np.abs, "fmax": np.fmax, "fmin": np.fmin,
+    "lt": lambda a, b: (a < b).astype(float), "le": lambda a, b: (a <= b).astype(float),
+    "eq": lambda a, b: (a == b).astype(float), "ne": lambda a, b: (a != b).astype(float),
+    "if_else": lambda c, t, f: np.where(c != 0, t, f),
+}
+
+
+def to_string(e: Expr, _depth: int = 0) -> str:
+    if e.op == "const":
+        return repr(e.value)
+    if e.op == "sym":
+        return e.name
+    if _depth > 12:
+        return "..."
+    a = [to_string(x, _depth + 1) for x in e.args]
+    infix = {"add": "+", "sub": "-", "mul": "*", "div": "/", "lt": "<", "le": "<=",
+             "eq": "==", "ne": "!="}
+    if e.op in infix:
+        return f"({a[0]}{infix[e.op]}{a[1]})"
+    if e.op == "neg":
+        return f"(-{a[0]})"
+    if e.op == "pow":
+        return f"pow({a[0]},{a[1]})"
+    return f"{e.op}({', '.join(a)})"
+
+
+def count_ops(outputs: Sequence[Expr]) -> Dict[str, int]:
+    """Floating point operation count of the DAG (shared nodes counted once)."""
+    counts: Dict[str, int] = {}
+    for n in topo_order([as_expr(o) for o in outputs]):
+        if n.op in ("sym", "const"):
+            continue
+        counts[n.op] = counts.get(n.op, 0) + 1
+    return counts
+
+
+def flop_count(outputs: Sequence[Expr]) -> int:
+    c = count_ops(outputs)
+    # transcendental functions are priced as a handful of flops
+    weights = {"exp": 8, "log": 8, "sqrt": 4, "tanh": 10, "sin": 8, "cos": 8,
+               "pow": 16, "div": 4}
+    return int(sum(v * weights.get(k, 1) for k, v in c.items()))
+
+
+# ---------------------------------------------------------------------------
+# code generation
+# ---------------------------------------------------------------------------
+
+def _c_literal(v: float) -> str:
+    if math.isnan(v):
+        return "__builtin_nan(\"\")"
+    if math.isinf(v):
+        return "(__builtin_inf())" if v > 0 else "(-__builtin_inf())"
+    r = repr(float(v))
+    if "e" not in r and "." not in r and "inf" not in r:
+        r += ".0"
+    return r
+
+
+class CodeGen:
+    """Emit straight-line C for a set of outputs.
+
+    ``inputs`` maps symbols to C l-value expressions; ``emit`` returns the body
+    lines assigning each output expression to the given C target.
+    """
+
+    def __init__(self, inputs: Dict[Expr, str], prefix: str = "t"):
+        self.inputs = {k.uid: v for k, v in inputs.items()}
+        self.prefix = prefix
+
+    def emit(self, assignments: Sequence[Tuple[str, Expr]], indent: str = "  ") -> List[str]:
+        outs = [as_expr(e) for _, e in assignments]
+        order = topo_order(outs)
+        # reference counts: inline leaf-ish nodes used once
+        names: Dict[int, str] = {}
+        lines: List[str] = []
+        for n in order:
+            if n.op == "const":
+                names[n.uid] = _c_literal(n.value)
+                continue
+            if n.op == "sym":
+                if n.uid not in self.inputs:
+                    raise KeyError(f"Symbol {n.name} has no input binding in code generation")
+                names[n.uid] = self.inputs[n.uid]
+                continue
+            a = [names[x.uid] for x in n.args]
+            expr = _c_op(n.op, a)
+            var = f"{self.prefix}{n.uid}"
+            lines.append(f"{indent}const double {var} = {expr};")
+            names[n.uid] = var
+        for target, e in assignments:
+            lines.append(f"{indent}{target} = {names[as_expr(e).uid]};")
+        return lines
+
+
+def _c_op(op: str, a: List[str]) -> str:
+    if op == "add":
+        return f"{a[0]} + {a[1]}"
+    if op == "sub":
+        return f"{a[0]} - {a[1]}"
+    if op == "mul":
+        return f"{a[0]} * {a[1]}"
+    if op == "div":
+        return f"{a[0]} / {a[1]}"
+    if op == "neg":
+        return f"-({a[0]})"
+    if op == "sq":
+        return f"{a[0]} * {a[0]}"
+    if op == "pow":
+        return f"pow({a[0]}, {a[1]})"
+    if op in ("exp", "log", "sqrt", "tanh", "sin", "cos", "fabs"):
+        return f"{op}({a[0]})"
+    if op == "fmax":
+        return f"fmax({a[0]}, {a[1]})"
+    if op == "fmin":
+        return f"fmin({a[0]}, {a[1]})"
+    if op == "lt":
+        return f"(({a[0]}) < ({a[1]}) ? 1.0 : 0.0)"
+    if op == "le":
+        return f"(({a[0]}) <= ({a[1]}) ? 1.0 : 0.0)"
+    if op == "eq":
+        return f"(({a[0]}) == ({a[1]}) ? 1.0 : 0.0)"
+    if op == "ne":
+        return f"(({a[0]}) != ({a[1]}) ? 1.0 : 0.0)"
+    if op == "if_else":
+        return f"(({a[0]}) != 0.0 ? ({a[1]}) : ({a[2]}))"
+    raise NotImplementedError(op)

@@ -1,0 +1,189 @@
+/* mpcx.h — C ABI of the MI355X batched MPC / ADMM solver (libmpcx.so).
+ *
+ * Drop-in boundary for AgentLib-MPC's optimization backend hot path.  The
+ * reference has no C ABI: its backends call CasADi/IPOPT from Python.  Each
+ * entry point below replaces one reference interface (file:line relative to
+ * the reference repository):
+ *
+ *   mpcx_problem_create   <- Discretization.initialize / SolverFactory.create_solver
+ *                            (optimization_backends/casadi_/core/discretization.py:156-162,
+ *                             data_structures/casadi_utils.py:282-300): load the generated
+ *                             code object of one transcribed NLP structure.
+ *   mpcx_batch_solve      <- self._optimizer(**nlp_inputs)
+ *                            (optimization_backends/casadi_/core/discretization.py:203), i.e.
+ *                            ca.nlpsol("mpc", "ipopt", ...)(p, x0, lbx, ubx, lbg, ubg),
+ *                            batched over agents; outputs x, lam_g, lam_x and the
+ *                            IPOPT-style stats (success, return_status, iter_count, obj).
+ *   mpcx_admm_group_sums + mpcx_admm_mean_from_sums
+ *                         <- ConsensusVariable.update_mean_trajectory
+ *                            (data_structures/admm_datatypes.py:221-236) and
+ *                            ADMM._set_mean_coupling_values (modules/dmpc/admm/admm.py:528-548)
+ *   mpcx_admm_consensus_multipliers
+ *                         <- ConsensusVariable.update_multipliers (admm_datatypes.py:238-267),
+ *                            ADMM.update_lambda (admm.py:612-633)
+ *   mpcx_admm_exchange_update
+ *                         <- ExchangeVariable.update_diff_trajectories / update_multiplier
+ *                            (admm_datatypes.py:292-324), admm.py:550-570, 635-655
+ *   mpcx_admm_residual_partials
+ *                         <- ADMMCoordinator._check_convergence norms
+ *                            (modules/dmpc/admm/admm_coordinator.py:354-435)
+ *
+ * Conventions: all array arguments are DEVICE pointers (HBM-resident, fp64),
+ * agent-major ([n_agents][len]).  Functions return 0 on success and a
+ * negative mpcx_err code otherwise; nothing throws across the ABI.  Calls are
+ * stream-ordered on the hipStream_t passed as `stream` (NULL = default
+ * stream) and do not synchronise.  One host thread per handle.
+ */
+#ifndef MPCX_H
+#define MPCX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCX_API_VERSION 3
+
+typedef enum mpcx_err {
+  MPCX_OK = 0,
+  MPCX_ERR_ARG = -1,
+  MPCX_ERR_HIP = -2,
+  MPCX_ERR_MODULE = -3,
+  MPCX_ERR_DIMS = -4,
+  MPCX_ERR_OOM = -5,
+} mpcx_err;
+
+/* per-agent solver status (IPOPT return_status equivalents) */
+typedef enum mpcx_status {
+  MPCX_SOLVE_SUCCEEDED = 0,          /* "Solve_Succeeded" */
+  MPCX_SOLVED_TO_ACCEPTABLE = 1,     /* "Solved_To_Acceptable_Level" */
+  MPCX_MAX_ITER_EXCEEDED = -1,       /* "Maximum_Iterations_Exceeded" */
+  MPCX_RESTORATION_FAILED = -2,      /* "Restoration_Failed" (line search gave up) */
+  MPCX_ERROR_IN_STEP = -3,           /* "Error_In_Step_Computation" */
+  MPCX_INVALID_NUMBER = -4,          /* "Invalid_Number_Detected" */
+} mpcx_status;
+
+/* Dimensions of one stage-structured NLP (must match the code object). */
+typedef struct mpcx_problem_desc {
+  int32_t n_stages;      /* N: prediction horizon */
+  int32_t nx;            /* differential states per stage boundary */
+  int32_t nv;            /* stage-local variables */
+  int32_t ng;            /* constraints per stage */
+  int32_t nps;           /* parameters per stage */
+  int32_t npg;           /* global parameters */
+  int32_t abi;           /* code object ABI version (MPCX_KERNEL_ABI) */
+  int32_t reserved;
+} mpcx_problem_desc;
+
+/* IPOPT-named options (defaults: mpcx_default_options). */
+typedef struct mpcx_options {
+  double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol;
+  double acceptable_tol;
+  double mu_init, mu_min, kappa_eps, kappa_mu, theta_mu, tau_min;
+  double bound_push, bound_frac, bound_relax_factor, bound_mult_init_val;
+  double constr_mult_init_max, kappa_sigma;
+  double nlp_scaling_max_gradient, nlp_scaling_min_value;
+  double delta_w_first, delta_w_min, delta_w_max;
+  double kappa_w_plus_bar, kappa_w_plus, kappa_w_minus, delta_c_bar, kappa_c;
+  double theta_max_fact, theta_min_fact, eta_phi, delta, s_phi, s_theta;
+  double gamma_phi, gamma_theta, alpha_min_frac;
+  int32_t max_iter, acceptable_iter;
+  int32_t warm_start_mult; /* 1: use lam_g/lam_w inputs as initial multipliers */
+  int32_t reserved;
+} mpcx_options;
+
+/* Per-agent result statistics (IPOPT stats() subset). */
+typedef struct mpcx_stats {
+  double obj;          /* objective at the solution (unscaled) */
+  double primal_inf;   /* unscaled max constraint violation */
+  double dual_inf;     /* unscaled max dual infeasibility */
+  double compl_inf;    /* max complementarity */
+  double mu;           /* final barrier parameter */
+  double obj_scale;    /* gradient-based objective scaling factor */
+  int32_t iter_count;
+  int32_t status;      /* mpcx_status */
+  int32_t n_inertia_corrections;
+  int32_t n_linesearch_fallbacks;
+  int32_t n_factorizations;
+  int32_t reserved;
+} mpcx_stats;
+
+typedef struct mpcx_handle mpcx_handle;
+
+int mpcx_version(void);
+void mpcx_default_options(mpcx_options* opts);
+
+/* Load a generated code object (hsaco) for one problem structure. */
+int mpcx_problem_create(const mpcx_problem_desc* desc, const char* code_object_path,
+                        mpcx_handle** out);
+int mpcx_problem_destroy(mpcx_handle* h);
+int mpcx_set_options(mpcx_handle* h, const mpcx_options* opts);
+/* Pre-allocate workspace for up to n_agents (keeps the solve path allocation-free). */
+int mpcx_reserve(mpcx_handle* h, int32_t n_agents);
+/* Workspace bytes per agent (for capacity planning on 288 GB HBM). */
+int64_t mpcx_workspace_bytes_per_agent(const mpcx_handle* h);
+
+/* Batched solve.  Shapes (agent-major, fp64, device):
+ *   p      [n_agents][np]            np = npg + n_stages*nps   (reference p order)
+ *   lbw/ubw[n_agents][nw]            nw = nx + n_stages*(nv+nx) (reference x order)
+ *   lbg/ubg[n_agents][ng_total] or NULL (then computed from the generated bound
+ *                                     expressions in p)        ng_total = n_stages*ng
+ *   w_io   [n_agents][nw]            initial guess in, solution out
+ *   lam_g  [n_agents][ng_total] or NULL   constraint multipliers out (in if warm_start_mult)
+ *   lam_w  [n_agents][nw] or NULL         bound multipliers out (z_U - z_L)
+ *   stats  [n_agents]  or NULL
+ */
+int mpcx_batch_solve(mpcx_handle* h, int32_t n_agents, const double* p, const double* lbw,
+                     const double* ubw, const double* lbg, const double* ubg, double* w_io,
+                     double* lam_g, double* lam_w, mpcx_stats* stats, void* stream);
+
+/* ---- ADMM kernels (agent-batched, see header comment for reference mapping) ----
+ * Local trajectories are rows of `locals` [n_rows][T].  The participants of one
+ * coupling alias ("group") are the contiguous rows group_start[g] ..
+ * group_start[g+1]-1 (device array); max_group_rows = max over g of the group
+ * size (host value, sizes the launch grid).  `active` [n_rows] (0/1, NULL = all) masks participants
+ * that did not report this round (coordinator: agents not "ready").
+ * Multi-GPU: every rank calls mpcx_admm_group_sums on its rows, the [n_groups][T+1]
+ * sums are all-reduced (RCCL), then mpcx_admm_mean_from_sums finalises.
+ */
+/* sums[g][t] += sum over active rows of group g of locals[row][t]; sums[g][T] += count.
+ * `sums` must be zeroed by the caller. */
+int mpcx_admm_group_sums(int32_t n_groups, int32_t T, const int32_t* group_start,
+                         int32_t max_group_rows,
+                         const double* locals, const int32_t* active, double* sums,
+                         void* stream);
+/* mean[g][:] <- sums[g][:T]/sums[g][T]; delta_mean <- old mean - new mean (groups with
+ * count 0 keep mean and delta_mean). */
+int mpcx_admm_mean_from_sums(int32_t n_groups, int32_t T, const double* sums, double* mean,
+                             double* delta_mean, void* stream);
+/* consensus: r = mean[g] - x_i ; lambda_i <- lambda_i - rho * r  (active rows; inactive r = 0) */
+int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, const int32_t* group_start,
+                                    int32_t max_group_rows,
+                                    const double* locals, const int32_t* active,
+                                    const double* mean, double rho, double* multipliers,
+                                    double* primal_residual, void* stream);
+/* exchange: diff_i <- x_i - mean[g] (active rows); lambda[g] <- lambda[g] + rho*mean[g];
+ * primal_residual[g] <- mean[g].  rho = 0 updates diffs only. */
+int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* group_start,
+                              int32_t max_group_rows,
+                              const double* locals, const int32_t* active, const double* mean,
+                              double* diff, double* multiplier, double* primal_residual,
+                              double rho, void* stream);
+/* Per-group partial sums of squares, ADDED to out[n_groups][4] (zeroed by caller):
+ *   {sum r^2, sum (rho*delta_mean)^2, sum x_local^2 (active rows), sum lambda^2}.
+ * consensus: r/lambda are [n_rows][T]; exchange: r/lambda are [n_groups][T]. */
+int mpcx_admm_residual_partials(int32_t n_groups, int32_t T, const int32_t* group_start,
+                                int32_t max_group_rows,
+                                const double* primal_residual, const double* delta_mean,
+                                const double* locals, const double* multipliers,
+                                const int32_t* active, double rho, int32_t exchange,
+                                double* out, void* stream);
+/* Shift rows by one control interval (admm_datatypes.py:275-282, 326-331):
+ * x[i][:] <- x[i][shift:] ++ x[i][T-shift:] */
+int mpcx_admm_shift(int32_t n_rows, int32_t T, int32_t shift, double* x, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCX_H */

@@ -1,0 +1,447 @@
+"""ORACLE (test infrastructure only) — IPOPT-style primal-dual interior point method.
+
+This is the CPU restatement of the solver the reference calls through
+``ca.nlpsol("mpc", "ipopt", nlp, opts)`` (`agentlib_mpc/data_structures/casadi_utils.py:191-217`,
+`282-300`; solve at `optimization_backends/casadi_/core/discretization.py:203`).
+IPOPT itself is a third-party dependency absent from `/root/reference`
+(bundled in the ``casadi>=3.6.6`` wheel, `pyproject.toml:30`, unpinned); this
+module restates its published algorithm (Wächter & Biegler, Math. Prog. 106,
+2006): barrier problem with slacks for inequalities, monotone Fiacco-McCormick
+barrier update, primal-dual Newton step on the KKT system with inertia
+correction (Algorithm IC), fraction-to-the-boundary rule and the filter line
+search, gradient-based NLP scaling, bound relaxation and least-squares
+constraint-multiplier initialisation, with IPOPT's default constants.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may use this package, and only as the checker.  The
+dense KKT here is factored with ``scipy.linalg.ldl`` (Bunch-Kaufman), whose
+D blocks give the inertia exactly as MUMPS does inside IPOPT.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Callable, Dict, Optional
+
+import numpy as np
+import scipy.linalg
+
+INF = 1e19  # IPOPT nlp_lower/upper_bound_inf
+
+
+@dataclasses.dataclass
+class IPMOptions:
+    tol: float = 1e-8
+    max_iter: int = 3000
+    dual_inf_tol: float = 1.0
+    constr_viol_tol: float = 1e-4
+    compl_inf_tol: float = 1e-4
+    mu_init: float = 0.1
+    mu_min: float = 1e-11
+    kappa_eps: float = 10.0
+    kappa_mu: float = 0.2
+    theta_mu: float = 1.5
+    tau_min: float = 0.99
+    bound_push: float = 1e-2
+    bound_frac: float = 1e-2
+    bound_relax_factor: float = 1e-8
+    bound_mult_init_val: float = 1.0
+    constr_mult_init_max: float = 1e3
+    kappa_sigma: float = 1e10
+    s_max: float = 100.0
+    nlp_scaling_max_gradient: float = 100.0
+    nlp_scaling_min_value: float = 1e-8
+    # inertia correction
+    delta_w_first: float = 1e-4
+    delta_w_min: float = 1e-20
+    delta_w_max: float = 1e40
+    kappa_w_plus_bar: float = 100.0
+    kappa_w_plus: float = 8.0
+    kappa_w_minus: float = 1.0 / 3.0
+    delta_c_bar: float = 1e-8
+    kappa_c: float = 0.25
+    # filter line search
+    theta_max_fact: float = 1e4
+    theta_min_fact: float = 1e-4
+    eta_phi: float = 1e-8
+    delta: float = 1.0
+    s_phi: float = 2.3
+    s_theta: float = 1.1
+    gamma_phi: float = 1e-8
+    gamma_theta: float = 1e-5
+    alpha_min_frac: float = 0.05
+    max_filter: int = 64
+
+
+@dataclasses.dataclass
+class NLPFunctions:
+    """Callables of one NLP instance (parameters already bound)."""
+
+    n: int
+    m: int
+    f: Callable[[np.ndarray], float]
+    grad_f: Callable[[np.ndarray], np.ndarray]
+    g: Callable[[np.ndarray], np.ndarray]
+    jac_g: Callable[[np.ndarray], np.ndarray]            # dense (m, n)
+    hess_l: Callable[[np.ndarray, float, np.ndarray], np.ndarray]  # (x, sigma, lam) -> (n, n)
+
+
+@dataclasses.dataclass
+class IPMResult:
+    x: np.ndarray
+    lam_g: np.ndarray
+    lam_x: np.ndarray
+    f: float
+    iterations: int
+    status: str
+    success: bool
+    history: list
+
+
+def _relax(b, lower: bool, factor: float):
+    out = b.copy()
+    fin = np.abs(b) < INF
+    d = factor * np.maximum(1.0, np.abs(b[fin]))
+    out[fin] = b[fin] - d if lower else b[fin] + d
+    return out
+
+
+def solve(nlp: NLPFunctions, x0, lbx, ubx, lbg, ubg, opts: IPMOptions = None,
+          record: bool = False) -> IPMResult:
+    o = opts or IPMOptions()
+    with np.errstate(divide='ignore', invalid='ignore'):
+        return _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record)
+
+
+def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
+    n, m = nlp.n, nlp.m
+    x = np.array(x0, dtype=float).copy()
+    lbx = np.maximum(np.asarray(lbx, float), -INF)
+    ubx = np.minimum(np.asarray(ubx, float), INF)
+    lbg = np.maximum(np.asarray(lbg, float), -INF)
+    ubg = np.minimum(np.asarray(ubg, float), INF)
+
+    fixed = lbx == ubx
+    x[fixed] = lbx[fixed]
+    free = ~fixed
+    # constraint classification
+    eq = lbg == ubg
+    ineq = ~eq
+
+    # --- NLP scaling (gradient based, at the user starting point) ----------
+    gf0 = nlp.grad_f(x)
+    gmax = np.max(np.abs(gf0[free])) if free.any() else 0.0
+    obj_scale = 1.0
+    if gmax > o.nlp_scaling_max_gradient:
+        obj_scale = max(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / gmax)
+    J0 = nlp.jac_g(x)
+    rowmax = np.max(np.abs(J0[:, free]), axis=1) if m else np.zeros(0)
+    g_scale = np.ones(m)
+    big = rowmax > o.nlp_scaling_max_gradient
+    g_scale[big] = np.maximum(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / rowmax[big])
+
+    def F(xx):
+        return obj_scale * nlp.f(xx)
+
+    def GF(xx):
+        v = obj_scale * nlp.grad_f(xx)
+        v[fixed] = 0.0
+        return v
+
+    def G(xx):
+        return g_scale * nlp.g(xx)
+
+    def JG(xx):
+        J = g_scale[:, None] * nlp.jac_g(xx)
+        J[:, fixed] = 0.0
+        return J
+
+    def H(xx, lam):
+        Hm = nlp.hess_l(xx, obj_scale, lam * g_scale)
+        Hm[fixed, :] = 0.0
+        Hm[:, fixed] = 0.0
+        return Hm
+
+    # scaled, relaxed bounds
+    xL = np.where(free & (lbx > -INF), _relax(lbx, True, o.bound_relax_factor), -np.inf)
+    xU = np.where(free & (ubx < INF), _relax(ubx, False, o.bound_relax_factor), np.inf)
+    sLb = np.where(lbg > -INF, lbg * g_scale, -np.inf)
+    sUb = np.where(ubg < INF, ubg * g_scale, np.inf)
+    sL = np.where(ineq, np.where(np.isfinite(sLb), _relax(np.where(np.isfinite(sLb), sLb, 0), True, o.bound_relax_factor), -np.inf), sLb)
+    sU = np.where(ineq, np.where(np.isfinite(sUb), _relax(np.where(np.isfinite(sUb), sUb, 0), False, o.bound_relax_factor), np.inf), sUb)
+    hasL, hasU = np.isfinite(xL), np.isfinite(xU)
+    shasL, shasU = ineq & np.isfinite(sL), ineq & np.isfinite(sU)
+    free_slack = ineq & ~shasL & ~shasU
+
+    def push(v, lo, hi, hl, hu):
+        v = v.copy()
+        pl = np.where(hl, o.bound_push * np.maximum(1.0, np.abs(np.where(hl, lo, 0))), 0.0)
+        pu = np.where(hu, o.bound_push * np.maximum(1.0, np.abs(np.where(hu, hi, 0))), 0.0)
+        both = hl & hu
+        width = np.where(both, np.where(both, hi, 0) - np.where(both, lo, 0), np.inf)
+        pl = np.where(both, np.minimum(pl, o.bound_frac * width), pl)
+        pu = np.where(both, np.minimum(pu, o.bound_frac * width), pu)
+        lo_p = np.where(hl, lo + pl, -np.inf)
+        hi_p = np.where(hu, hi - pu, np.inf)
+        v = np.maximum(v, lo_p)
+        v = np.minimum(v, hi_p)
+        # degenerate interval: middle
+        bad = both & (lo_p > hi_p)
+        v[bad] = 0.5 * (lo[bad] + hi[bad])
+        return v
+
+    x = np.where(free, push(x, xL, xU, hasL, hasU), x)
+    gx = G(x)
+    s = np.where(ineq, push(gx, sL, sU, shasL, shasU), np.where(eq, lbg * g_scale, 0.0))
+
+    zL = np.where(hasL, o.bound_mult_init_val, 0.0)
+    zU = np.where(hasU, o.bound_mult_init_val, 0.0)
+    vL = np.where(shasL, o.bound_mult_init_val, 0.0)
+    vU = np.where(shasU, o.bound_mult_init_val, 0.0)
+
+    fx = F(x)
+    gfx = GF(x)
+    Jx = JG(x)
+
+    # --- least-squares multiplier estimate ---------------------------------
+    lam = np.zeros(m)
+    if m and o.constr_mult_init_max > 0:
+        K = np.zeros((n + m, n + m))
+        K[:n, :n] = np.eye(n)
+        K[:n, n:] = Jx.T
+        K[n:, :n] = Jx
+        dd = np.where(ineq, -1.0, 0.0)
+        dd[free_slack] = -1.0
+        K[n:, n:] = np.diag(dd)
+        rhs = np.concatenate([-(gfx - zL + zU), np.where(ineq, vL - vU, 0.0)])
+        try:
+            sol = np.linalg.solve(K, rhs)
+            lam_ls = sol[n:]
+            if np.max(np.abs(lam_ls), initial=0.0) <= o.constr_mult_init_max:
+                lam = lam_ls
+        except np.linalg.LinAlgError:
+            pass
+
+    mu = o.mu_init
+    tau = max(o.tau_min, 1.0 - mu)
+    delta_w_last = 0.0
+
+    def residuals(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu_):
+        rd = gfx + Jx.T @ lam - zL + zU
+        rd[fixed] = 0.0
+        rs = np.where(ineq & ~free_slack, -lam - vL + vU, 0.0)
+        c = np.where(ineq, gx - s, gx - np.where(eq, lbg * g_scale, 0.0))
+        cl = np.where(hasL, (x - np.where(hasL, xL, 0)) * zL - mu_, 0.0)
+        cu = np.where(hasU, (np.where(hasU, xU, 0) - x) * zU - mu_, 0.0)
+        csl = np.where(shasL, (s - np.where(shasL, sL, 0)) * vL - mu_, 0.0)
+        csu = np.where(shasU, (np.where(shasU, sU, 0) - s) * vU - mu_, 0.0)
+        return rd, rs, c, np.concatenate([cl, cu, csl, csu])
+
+    def opt_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu_):
+        rd, rs, c, comp = residuals(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu_)
+        nz = np.sum(hasL) + np.sum(hasU) + np.sum(shasL) + np.sum(shasU)
+        zsum = np.sum(np.abs(zL)) + np.sum(np.abs(zU)) + np.sum(np.abs(vL)) + np.sum(np.abs(vU))
+        s_d = max(o.s_max, (np.sum(np.abs(lam)) + zsum) / max(1, m + nz)) / o.s_max
+        s_c = max(o.s_max, zsum / max(1, nz)) / o.s_max if nz else 1.0
+        dual = max(np.max(np.abs(rd), initial=0.0), np.max(np.abs(rs), initial=0.0))
+        primal = np.max(np.abs(c), initial=0.0)
+        compl = np.max(np.abs(comp), initial=0.0)
+        return max(dual / s_d, primal, compl / s_c), dual, primal, compl
+
+    def theta_of(gx, s):
+        c = np.where(ineq, gx - s, gx - np.where(eq, lbg * g_scale, 0.0))
+        return float(np.sum(np.abs(c)))
+
+    def phi_of(fx, x, s, mu_):
+        val = fx
+        val -= mu_ * np.sum(np.log(x[hasL] - xL[hasL]))
+        val -= mu_ * np.sum(np.log(xU[hasU] - x[hasU]))
+        val -= mu_ * np.sum(np.log(s[shasL] - sL[shasL]))
+        val -= mu_ * np.sum(np.log(sU[shasU] - s[shasU]))
+        return float(val)
+
+    theta0 = theta_of(gx, s)
+    theta_max = o.theta_max_fact * max(1.0, theta0)
+    theta_min = o.theta_min_fact * max(1.0, theta0)
+    filt = []
+    history = []
+    status = "Maximum_Iterations_Exceeded"
+    it = 0
+    while True:
+        err0, dual, primal, compl = opt_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, 0.0)
+        # unscaled checks
+        rd_u = (gfx + Jx.T @ lam - zL + zU) / obj_scale
+        c_u = np.where(ineq, gx - s, gx - np.where(eq, lbg * g_scale, 0.0)) / g_scale if m else np.zeros(0)
+        if record:
+            history.append(dict(iter=it, mu=mu, err=err0, f=fx / obj_scale, x=x.copy()))
+        if (err0 <= o.tol and np.max(np.abs(rd_u[free]), initial=0) <= o.dual_inf_tol
+                and np.max(np.abs(c_u), initial=0) <= o.constr_viol_tol
+                and compl <= o.compl_inf_tol):
+            status = "Solve_Succeeded"
+            break
+        if it >= o.max_iter:
+            break
+        # barrier update
+        while True:
+            err_mu = opt_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu)[0]
+            if err_mu > o.kappa_eps * mu or mu <= o.mu_min:
+                break
+            mu = max(o.tol / 10.0, min(o.kappa_mu * mu, mu ** o.theta_mu))
+            mu = max(mu, o.mu_min)
+            tau = max(o.tau_min, 1.0 - mu)
+            filt = []
+        Hx = H(x, lam)
+        # primal-dual matrices
+        dxL = np.where(hasL, x - np.where(hasL, xL, 0), 1.0)
+        dxU = np.where(hasU, np.where(hasU, xU, 0) - x, 1.0)
+        dsL = np.where(shasL, s - np.where(shasL, sL, 0), 1.0)
+        dsU = np.where(shasU, np.where(shasU, sU, 0) - s, 1.0)
+        Sx = np.where(hasL, zL / dxL, 0) + np.where(hasU, zU / dxU, 0)
+        Ss = np.where(shasL, vL / dsL, 0) + np.where(shasU, vU / dsU, 0)
+        gphi_x = gfx - np.where(hasL, mu / dxL, 0) + np.where(hasU, mu / dxU, 0)
+        gphi_s = -np.where(shasL, mu / dsL, 0) + np.where(shasU, mu / dsU, 0)
+        rhs_x = -(gphi_x + Jx.T @ lam)
+        rhs_x[fixed] = 0.0
+        r_s = np.where(ineq, gphi_s - lam, 0.0)
+        c = np.where(ineq, gx - s, gx - np.where(eq, lbg * g_scale, 0.0))
+
+        def factor_solve(dw, dc):
+            K = np.zeros((n + m, n + m))
+            W = Hx + np.diag(Sx + dw)
+            W[fixed, :] = 0.0
+            W[:, fixed] = 0.0
+            W[fixed, fixed] = 1.0
+            K[:n, :n] = W
+            K[:n, n:] = Jx.T
+            K[n:, :n] = Jx
+            Dd = np.where(ineq, 1.0 / (Ss + dw) + dc, dc)
+            Dd[free_slack] = 1.0
+            K[n:, n:] = -np.diag(Dd)
+            rhs_l = -c - np.where(ineq & ~free_slack, r_s / (Ss + dw), 0.0)
+            _, Dm, _ = scipy.linalg.ldl(K, lower=True)
+            ev = _block_eigs(Dm)
+            npos = int(np.sum(ev > 0))
+            nneg = int(np.sum(ev < 0))
+            nzero = len(ev) - npos - nneg
+            sol = np.linalg.solve(K, np.concatenate([rhs_x, rhs_l])) if nzero == 0 else None
+            return npos, nneg, nzero, sol
+
+        dw, dc = 0.0, 0.0
+        npos, nneg, nzero, sol = factor_solve(dw, dc)
+        if not (npos == n and nneg == m and nzero == 0):
+            if nzero > 0:
+                dc = o.delta_c_bar * mu ** o.kappa_c
+            dw = o.delta_w_first if delta_w_last == 0 else max(o.delta_w_min, o.kappa_w_minus * delta_w_last)
+            while True:
+                npos, nneg, nzero, sol = factor_solve(dw, dc)
+                if npos == n and nneg == m and nzero == 0:
+                    delta_w_last = dw
+                    break
+                dw = o.kappa_w_plus_bar * dw if delta_w_last == 0 else o.kappa_w_plus * dw
+                if dw > o.delta_w_max:
+                    raise RuntimeError("inertia correction failed")
+        dx = sol[:n]
+        dlam = sol[n:]
+        dx[fixed] = 0.0
+        ds = np.where(ineq & ~free_slack, (dlam - r_s) / (Ss + dw), 0.0)
+        dzL = np.where(hasL, mu / dxL - zL - (zL / dxL) * dx, 0.0)
+        dzU = np.where(hasU, mu / dxU - zU + (zU / dxU) * dx, 0.0)
+        dvL = np.where(shasL, mu / dsL - vL - (vL / dsL) * ds, 0.0)
+        dvU = np.where(shasU, mu / dsU - vU + (vU / dsU) * ds, 0.0)
+
+        def ftb(v, dv, mask):
+            a = 1.0
+            sel = mask & (dv < 0)
+            if np.any(sel):
+                a = min(a, float(np.min(-tau * v[sel] / dv[sel])))
+            return a
+
+        a_max = min(ftb(dxL, dx, hasL), ftb(dxU, -dx, hasU), ftb(dsL, ds, shasL), ftb(dsU, -ds, shasU))
+        a_z = min(ftb(zL, dzL, hasL), ftb(zU, dzU, hasU), ftb(vL, dvL, shasL), ftb(vU, dvU, shasU))
+
+        theta = theta_of(gx, s)
+        phi = phi_of(fx, x, s, mu)
+        gphi_d = float(gphi_x @ dx + gphi_s @ ds)
+        if gphi_d < 0 and theta <= theta_min:
+            a_min = o.alpha_min_frac * min(o.gamma_theta, o.gamma_phi * theta / (-gphi_d),
+                                           o.delta * theta ** o.s_theta / (-gphi_d) ** o.s_phi)
+        elif gphi_d < 0:
+            a_min = o.alpha_min_frac * min(o.gamma_theta, o.gamma_phi * theta / (-gphi_d))
+        else:
+            a_min = o.alpha_min_frac * o.gamma_theta
+        alpha = a_max
+        accepted = False
+        ftype = False
+        while True:
+            xt = x + alpha * dx
+            st = s + alpha * ds
+            gxt = G(xt)
+            fxt = F(xt)
+            th_t = theta_of(gxt, st)
+            ph_t = phi_of(fxt, xt, st, mu)
+            ok = th_t <= theta_max and not any(th_t >= a and ph_t >= b for a, b in filt)
+            if ok:
+                switching = gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
+                if theta <= theta_min and switching:
+                    ok = ph_t <= phi + o.eta_phi * alpha * gphi_d
+                    ftype = True
+                else:
+                    ok = th_t <= (1 - o.gamma_theta) * theta or ph_t <= phi - o.gamma_phi * theta
+                    ftype = False
+            if ok:
+                accepted = True
+                break
+            alpha *= 0.5
+            if alpha < a_min:
+                break
+        if not accepted:
+            # fallback instead of IPOPT's restoration phase: take the last trial
+            filt = []
+            ftype = True
+        if not ftype:
+            filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
+            if len(filt) > o.max_filter:
+                filt.pop(0)
+        x, s = xt, st
+        lam = lam + alpha * dlam
+        zL = zL + a_z * dzL
+        zU = zU + a_z * dzU
+        vL = vL + a_z * dvL
+        vU = vU + a_z * dvU
+        # safeguard (kappa_sigma)
+        dxL = np.where(hasL, x - np.where(hasL, xL, 0), 1.0)
+        dxU = np.where(hasU, np.where(hasU, xU, 0) - x, 1.0)
+        dsL = np.where(shasL, s - np.where(shasL, sL, 0), 1.0)
+        dsU = np.where(shasU, np.where(shasU, sU, 0) - s, 1.0)
+        zL = np.where(hasL, np.maximum(np.minimum(zL, o.kappa_sigma * mu / dxL), mu / (o.kappa_sigma * dxL)), 0)
+        zU = np.where(hasU, np.maximum(np.minimum(zU, o.kappa_sigma * mu / dxU), mu / (o.kappa_sigma * dxU)), 0)
+        vL = np.where(shasL, np.maximum(np.minimum(vL, o.kappa_sigma * mu / dsL), mu / (o.kappa_sigma * dsL)), 0)
+        vU = np.where(shasU, np.maximum(np.minimum(vU, o.kappa_sigma * mu / dsU), mu / (o.kappa_sigma * dsU)), 0)
+        fx, gx = fxt, gxt
+        gfx = GF(x)
+        Jx = JG(x)
+        it += 1
+
+    lam_g = lam * g_scale / obj_scale
+    lam_x = (zU - zL) / obj_scale
+    return IPMResult(x=x, lam_g=lam_g, lam_x=lam_x, f=fx / obj_scale, iterations=it,
+                     status=status, success=status == "Solve_Succeeded", history=history)
+
+
+def _block_eigs(D: np.ndarray) -> np.ndarray:
+    """Eigenvalues of the 1x1/2x2 block-diagonal D of scipy's ldl."""
+    n = D.shape[0]
+    ev = []
+    i = 0
+    while i < n:
+        if i + 1 < n and D[i + 1, i] != 0.0:
+            ev.extend(np.linalg.eigvalsh(D[i:i + 2, i:i + 2]))
+            i += 2
+        else:
+            ev.append(D[i, i])
+            i += 1
+    ev = np.asarray(ev)
+    scale = max(1.0, np.max(np.abs(ev), initial=0.0))
+    ev[np.abs(ev) <= 1e-14 * scale] = 0.0
+    return ev

@@ -1,0 +1,451 @@
+"""ORACLE (test infrastructure only) — hand restatement of the reference NLPs.
+
+Each builder writes out the reference transcription for one benchmark
+configuration with explicit variable / parameter / constraint ordering,
+independent of the product's tracer and transcriber:
+
+* ``one_room``   — backend ``casadi`` direct collocation
+  (`optimization_backends/casadi_/full.py:36-98`, `basic.py:251-392`) on the
+  model of `examples/one_room_mpc/physical/simple_mpc.py:95-138` (C1, C3).
+* ``admm_room`` / ``admm_ahu`` — backend ``casadi_admm`` collocation
+  (`casadi_/admm.py:119-195`, ADMM terms :90-116) on
+  `examples/4_Room_ADMM_Coordinator/models/{room,rlt}_model.py` (C2).
+* ``exchange_room`` / ``exchange_supply`` — backend ``casadi_admm`` multiple
+  shooting with Euler (`casadi_/admm.py:198-310`) on
+  `examples/exchange_admm/models/{room,rlt}_model.py` (C4).
+
+Derivatives come from torch fp64 autograd.  Initial guesses follow
+`core/discretization.py:212-245` (cold start).
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Callable, Dict, List
+
+import numpy as np
+import torch
+
+from oracle.ipm import NLPFunctions
+
+torch.set_default_dtype(torch.float64)
+
+
+def collocation(d: int, method: str = "legendre"):
+    if method == "legendre":
+        r, _ = np.polynomial.legendre.leggauss(d)
+        roots = np.sort((r + 1) / 2)
+    else:
+        c = np.zeros(d + 1)
+        c[d], c[d - 1] = 1.0, -1.0
+        r = np.sort(np.real(np.polynomial.legendre.legroots(c)))
+        r[-1] = 1.0
+        roots = (r + 1) / 2
+    tau = np.concatenate([[0.0], roots])
+    C = np.zeros((d + 1, d + 1))
+    D = np.zeros(d + 1)
+    B = np.zeros(d + 1)
+    for j in range(d + 1):
+        # Lagrange basis polynomial l_j on tau
+        coeffs = np.array([1.0])
+        for r_ in range(d + 1):
+            if r_ != j:
+                coeffs = np.convolve(coeffs, np.array([1.0, -tau[r_]]) / (tau[j] - tau[r_]))
+        D[j] = np.polyval(coeffs, 1.0)
+        der = np.polyder(coeffs)
+        C[j] = [np.polyval(der, t) for t in tau]
+        B[j] = np.polyval(np.polyint(coeffs), 1.0)
+    return tau, B, C, D
+
+
+@dataclasses.dataclass
+class OracleProblem:
+    name: str
+    n: int
+    m: int
+    np_: int
+    f: Callable  # torch (w, p) -> scalar
+    g: Callable  # torch (w, p) -> (m,)
+    lbg: Callable  # numpy p -> (m,)
+    ubg: Callable
+    w_names: List[str]
+
+    def functions(self, p: np.ndarray) -> NLPFunctions:
+        pt = torch.as_tensor(p)
+
+        def f(w):
+            return float(self.f(torch.as_tensor(w), pt))
+
+        def grad(w):
+            wt = torch.as_tensor(w).clone().requires_grad_(True)
+            return torch.autograd.grad(self.f(wt, pt), wt)[0].numpy()
+
+        def g(w):
+            return self.g(torch.as_tensor(w), pt).numpy()
+
+        def jac(w):
+            return torch.func.jacrev(lambda ww: self.g(ww, pt))(torch.as_tensor(w)).numpy().reshape(self.m, self.n)
+
+        def hess(w, sigma, lam):
+            lt = torch.as_tensor(lam)
+            L = lambda ww: sigma * self.f(ww, pt) + (lt * self.g(ww, pt)).sum()  # noqa: E731
+            return torch.func.hessian(L)(torch.as_tensor(w)).numpy()
+
+        return NLPFunctions(n=self.n, m=self.m, f=f, grad_f=grad, g=g, jac_g=jac, hess_l=hess)
+
+
+# ---------------------------------------------------------------------------
+# C1 / C3: one room, backend "casadi", collocation
+# ---------------------------------------------------------------------------
+
+def one_room(N=15, ts=300.0, d=2, method="legendre") -> OracleProblem:
+    tau, B, C, D = collocation(d, method)
+    nb = 1 + 3 * d + 1          # u, (T, T_slack, T_out) per point, T_end
+    n = 1 + N * nb
+    m = N * (1 + 3 * d)         # cont, (col, path, out) per point
+    npg = 1 + 1 + 4             # T0, u_prev, (cp, C, s_T, r_mDot)
+    nps = 3 * d                 # (T_in, load, T_upper) per point
+    names = ["T@0"]
+    for k in range(N):
+        names.append(f"mDot@{k}")
+        for j in range(d):
+            names += [f"T@{k},{j}", f"T_slack@{k},{j}", f"T_out@{k},{j}"]
+        names.append(f"T@{k + 1}")
+
+    def unpack(w, p):
+        cp, Cz, s_T, r = p[2], p[3], p[4], p[5]
+        return cp, Cz, s_T, r
+
+    def f(w, p):
+        cp, Cz, s_T, r = unpack(w, p)
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = 1 + k * nb
+            u = w[o]
+            for j in range(d):
+                zs = w[o + 1 + 3 * j + 1]
+                tot = tot + B[j + 1] * (r * u + s_T * zs ** 2) * ts
+        return tot
+
+    def g(w, p):
+        cp, Cz, s_T, r = unpack(w, p)
+        out = []
+        xk = w[0]
+        for k in range(N):
+            o = 1 + k * nb
+            u = w[o]
+            Tj = [w[o + 1 + 3 * j] for j in range(d)]
+            x_end = w[o + nb - 1]
+            out.append(x_end - (D[0] * xk + sum(D[j + 1] * Tj[j] for j in range(d))))
+            for j in range(d):
+                ps = npg + k * nps + 3 * j
+                T_in, load = p[ps], p[ps + 1]
+                ode = cp * u / Cz * (T_in - Tj[j]) + load / Cz
+                xp = C[0, j + 1] * xk + sum(C[r_ + 1, j + 1] * Tj[r_] for r_ in range(d))
+                out.append(ts * ode - xp)
+                out.append(Tj[j] + w[o + 1 + 3 * j + 1])
+                out.append(w[o + 1 + 3 * j + 2] - Tj[j])
+            xk = x_end
+        return torch.stack(out)
+
+    def lbg(p):
+        return np.zeros(m)
+
+    def ubg(p):
+        u = np.zeros(m)
+        for k in range(N):
+            for j in range(d):
+                u[k * (1 + 3 * d) + 1 + 3 * j + 1] = p[npg + k * nps + 3 * j + 2]
+        return u
+
+    return OracleProblem("one_room", n, m, npg + N * nps, f, g, lbg, ubg, names)
+
+
+def one_room_inputs(prob: OracleProblem, N=15, d=2, T0=298.16, load=150.0, T_in=290.15,
+                    T_upper=295.15, s_T=0.001, r_mDot=0.01, u_prev=0.02, cp=1000.0, C=100000.0,
+                    T_lb=288.15, T_ub=303.15, u_lb=0.0, u_ub=0.05):
+    p = [T0, u_prev, cp, C, s_T, r_mDot]
+    for k in range(N):
+        for j in range(d):
+            p += [T_in, load, T_upper]
+    p = np.array(p, float)
+    n = prob.n
+    lbw = np.full(n, -np.inf)
+    ubw = np.full(n, np.inf)
+    w0 = np.zeros(n)
+    for i, name in enumerate(prob.w_names):
+        base = name.split("@")[0]
+        if base == "T":
+            lbw[i], ubw[i], w0[i] = T_lb, T_ub, T0
+        elif base == "mDot":
+            lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
+    lbw[0] = ubw[0] = w0[0] = T0
+    return p, lbw, ubw, w0
+
+
+# ---------------------------------------------------------------------------
+# C2: 4 rooms + air handler, backend "casadi_admm", collocation (d=3)
+# ---------------------------------------------------------------------------
+
+def admm_room(N=10, ts=60.0, d=3) -> OracleProblem:
+    tau, B, C, D = collocation(d)
+    nb = 2 * d + 1               # (T, mDot) per point, T_end
+    n = 1 + N * nb
+    m = N * (1 + 2 * d)          # cont, (col, path) per point
+    npg = 1 + 4 + 1              # T0, (cp, cZ, q_T, q_mDot), rho  [u_prev is empty]
+    nps = 6 * d                  # (zbar, lam, d, T_set, T_upper, T_in) per point
+    names = ["T@0"]
+    for k in range(N):
+        for j in range(d):
+            names += [f"T@{k},{j}", f"mDot@{k},{j}"]
+        names.append(f"T@{k + 1}")
+
+    def f(w, p):
+        cp, cZ, qT, qm, rho = p[1], p[2], p[3], p[4], p[5]
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = 1 + k * nb
+            for j in range(d):
+                T, u = w[o + 2 * j], w[o + 2 * j + 1]
+                ps = npg + k * nps + 6 * j
+                zbar, lam, Tset = p[ps], p[ps + 1], p[ps + 3]
+                cost = (0.0001 * qT * (T - Tset) ** 2 + 0.0001 * qm * (1 / 0.167) ** 2 * u ** 2
+                        + lam * u + rho / 2 * (zbar - u) ** 2)
+                tot = tot + B[j + 1] * cost * ts
+        return tot
+
+    def g(w, p):
+        cp, cZ = p[1], p[2]
+        out = []
+        xk = w[0]
+        for k in range(N):
+            o = 1 + k * nb
+            Tj = [w[o + 2 * j] for j in range(d)]
+            x_end = w[o + nb - 1]
+            out.append(x_end - (D[0] * xk + sum(D[j + 1] * Tj[j] for j in range(d))))
+            for j in range(d):
+                ps = npg + k * nps + 6 * j
+                dist, T_in = p[ps + 2], p[ps + 5]
+                u = w[o + 2 * j + 1]
+                ode = cp * u / cZ * (T_in - Tj[j]) + dist / cZ
+                xp = C[0, j + 1] * xk + sum(C[r + 1, j + 1] * Tj[r] for r in range(d))
+                out.append(ts * ode - xp)
+                out.append(Tj[j])
+            xk = x_end
+        return torch.stack(out)
+
+    def ubg(p):
+        u = np.zeros(m)
+        for k in range(N):
+            for j in range(d):
+                u[k * (1 + 2 * d) + 1 + 2 * j + 1] = p[npg + k * nps + 6 * j + 4]
+        return u
+
+    return OracleProblem("admm_room", n, m, npg + N * nps, f, g, lambda p: np.zeros(m), ubg, names)
+
+
+def admm_room_inputs(prob, N=10, d=3, T0=296.0, dist=150.0, T_set=296.0, T_upper=303.15, T_in=290.15,
+                     rho=0.4, zbar=None, lam=None, cp=1000.0, cZ=60000.0, qT=1.0, qm=1.0,
+                     T_lb=288.15, T_ub=303.15, u_lb=0.0, u_ub=0.05, guess=None):
+    npts = N * d
+    zbar = np.full(npts, 0.02) if zbar is None else np.asarray(zbar, float)
+    lam = np.zeros(npts) if lam is None else np.asarray(lam, float)
+    p = [T0, cp, cZ, qT, qm, rho]
+    for k in range(N):
+        for j in range(d):
+            i = k * d + j
+            p += [zbar[i], lam[i], dist, T_set, T_upper, T_in]
+    p = np.array(p, float)
+    lbw = np.zeros(prob.n)
+    ubw = np.zeros(prob.n)
+    w0 = np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        if name.startswith("T@"):
+            lbw[i], ubw[i], w0[i] = T_lb, T_ub, T0
+        else:
+            lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
+    lbw[0] = ubw[0] = w0[0] = T0
+    if guess is not None:
+        w0 = np.array(guess, float)
+    return p, lbw, ubw, w0
+
+
+def admm_ahu(N=10, ts=60.0, d=3, rooms=4) -> OracleProblem:
+    tau, B, C, D = collocation(d)
+    nb = rooms + rooms * d       # controls, couplings per point
+    n = N * nb
+    m = N * d * (1 + rooms)      # (sum constraint, output eqs) per point
+    npg = rooms + 1 + 1          # u_prev (4 controls), mDot_max, rho  [no states]
+    nps = 2 * rooms * d          # (zbar_i..., lam_i...) per point
+    names = []
+    for k in range(N):
+        names += [f"mDot_{i + 1}@{k}" for i in range(rooms)]
+        for j in range(d):
+            names += [f"mDot_out_{i + 1}@{k},{j}" for i in range(rooms)]
+
+    def f(w, p):
+        rho = p[rooms + 1]
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = k * nb
+            for j in range(d):
+                ps = npg + k * nps + 2 * rooms * j
+                cost = w.new_zeros(())
+                for i in range(rooms):
+                    y = w[o + rooms + rooms * j + i]
+                    cost = cost + p[ps + rooms + i] * y + rho / 2 * (p[ps + i] - y) ** 2
+                tot = tot + B[j + 1] * cost * ts
+        return tot
+
+    def g(w, p):
+        out = []
+        for k in range(N):
+            o = k * nb
+            u = [w[o + i] for i in range(rooms)]
+            for j in range(d):
+                out.append(sum(u))
+                for i in range(rooms):
+                    out.append(w[o + rooms + rooms * j + i] - 1 * u[i])
+        return torch.stack(out)
+
+    def ubg(p):
+        u = np.zeros(m)
+        u[0::1 + rooms] = p[rooms]
+        return u
+
+    return OracleProblem("admm_ahu", n, m, npg + N * nps, f, g, lambda p: np.zeros(m), ubg, names)
+
+
+def admm_ahu_inputs(prob, N=10, d=3, rooms=4, mDot_max=0.1, rho=0.4, zbar=None, lam=None,
+                    u_lb=0.0, u_ub=0.075):
+    npts = N * d
+    zbar = np.full((rooms, npts), 0.01) if zbar is None else np.asarray(zbar, float)
+    lam = np.zeros((rooms, npts)) if lam is None else np.asarray(lam, float)
+    p = [0.01] * rooms + [mDot_max, rho]   # u_prev = control values (rlt_admm.json)
+    for k in range(N):
+        for j in range(d):
+            i = k * d + j
+            p += list(zbar[:, i]) + list(lam[:, i])
+    p = np.array(p, float)
+    lbw = np.full(prob.n, -np.inf)
+    ubw = np.full(prob.n, np.inf)
+    w0 = np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        if "_out_" not in name:
+            lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
+    return p, lbw, ubw, w0
+
+
+# ---------------------------------------------------------------------------
+# C4: exchange ADMM, backend "casadi_admm", multiple shooting + Euler
+# ---------------------------------------------------------------------------
+
+def exchange_room(N=10, ts=120.0) -> OracleProblem:
+    nb = 3                       # mDot, mDot_out, T_end
+    n = 1 + N * nb
+    m = N * 2                    # cont, output eq
+    npg = 1 + 1 + 4 + 4 + 1      # T0, u_prev, params, params (again), rho
+    nps = 6                      # d, T_set, T_upper, T_in, exchange diff, exchange lambda
+    names = ["T@0"]
+    for k in range(N):
+        names += [f"mDot@{k}", f"mDot_out@{k}", f"T@{k + 1}"]
+
+    def pars(p):
+        return p[6], p[7], p[8], p[9], p[10]  # second parameter copy + rho
+
+    def f(w, p):
+        cp, cZ, qT, qm, rho = pars(p)
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = 1 + k * nb
+            T = w[o - 1] if k == 0 else w[o - 1]
+            u, y = w[o], w[o + 1]
+            ps = npg + k * nps
+            Tset, diff, lam = p[ps + 1], p[ps + 4], p[ps + 5]
+            cost = qT * (T - Tset) ** 2 + qm * (1 / 0.167) ** 2 * u ** 2 + lam * y + rho / 2 * (diff - y) ** 2
+            tot = tot + cost * ts
+        return tot
+
+    def g(w, p):
+        cp, cZ, qT, qm, rho = pars(p)
+        out = []
+        for k in range(N):
+            o = 1 + k * nb
+            T = w[o - 1]
+            u, y, T1 = w[o], w[o + 1], w[o + 2]
+            ps = npg + k * nps
+            dist, T_in = p[ps], p[ps + 3]
+            ode = cp * u / cZ * (T_in - T) + dist / cZ
+            out.append(T1 - (T + ode * ts))
+            out.append(y - u)
+        return torch.stack(out)
+
+    return OracleProblem("exchange_room", n, m, npg + N * nps, f, g,
+                         lambda p: np.zeros(m), lambda p: np.zeros(m), names)
+
+
+def exchange_room_inputs(prob, N=10, T0=296.0, dist=150.0, T_set=296.0, T_upper=296.15, T_in=290.15,
+                         rho=1e4, diff=None, lam=None, u_prev=0.02, cp=1000.0, cZ=60000.0,
+                         qT=1.0, qm=0.0, T_lb=288.15, T_ub=303.15, u_lb=0.0, u_ub=0.05,
+                         y_lb=0.0, y_ub=0.05):
+    diff = np.zeros(N) if diff is None else np.asarray(diff, float)
+    lam = np.zeros(N) if lam is None else np.asarray(lam, float)
+    p = [T0, u_prev, cp, cZ, qT, qm, cp, cZ, qT, qm, rho]
+    for k in range(N):
+        p += [dist, T_set, T_upper, T_in, diff[k], lam[k]]
+    p = np.array(p, float)
+    lbw = np.zeros(prob.n)
+    ubw = np.zeros(prob.n)
+    w0 = np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        base = name.split("@")[0]
+        if base == "T":
+            lbw[i], ubw[i], w0[i] = T_lb, T_ub, T0
+        elif base == "mDot":
+            lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
+        else:
+            lbw[i], ubw[i], w0[i] = y_lb, y_ub, 0.5 * (y_lb + y_ub)
+    lbw[0] = ubw[0] = w0[0] = T0
+    return p, lbw, ubw, w0
+
+
+def exchange_supply(N=10, ts=120.0) -> OracleProblem:
+    n = 2 * N
+    m = N
+    npg = 1 + 1 + 1 + 1          # u_prev, penalty, penalty (again), rho   [no states]
+    nps = 2                      # exchange diff, exchange lambda
+    names = []
+    for k in range(N):
+        names += [f"mDot@{k}", f"mDot_out@{k}"]
+
+    def f(w, p):
+        pen, rho = p[2], p[3]
+        tot = w.new_zeros(())
+        for k in range(N):
+            u, y = w[2 * k], w[2 * k + 1]
+            diff, lam = p[npg + k * nps], p[npg + k * nps + 1]
+            tot = tot + (pen * u + lam * y + rho / 2 * (diff - y) ** 2) * ts
+        return tot
+
+    def g(w, p):
+        return torch.stack([w[2 * k + 1] - (-w[2 * k]) for k in range(N)])
+
+    return OracleProblem("exchange_supply", n, m, npg + N * nps, f, g,
+                         lambda p: np.zeros(m), lambda p: np.zeros(m), names)
+
+
+def exchange_supply_inputs(prob, N=10, penalty=0.1, rho=1e4, diff=None, lam=None, u_prev=0.01,
+                           u_lb=0.0, u_ub=0.1, y_lb=-0.1, y_ub=0.0):
+    diff = np.zeros(N) if diff is None else np.asarray(diff, float)
+    lam = np.zeros(N) if lam is None else np.asarray(lam, float)
+    p = [u_prev, penalty, penalty, rho]
+    for k in range(N):
+        p += [diff[k], lam[k]]
+    p = np.array(p, float)
+    lbw = np.zeros(prob.n)
+    ubw = np.zeros(prob.n)
+    w0 = np.zeros(prob.n)
+    for k in range(N):
+        lbw[2 * k], ubw[2 * k], w0[2 * k] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
+        lbw[2 * k + 1], ubw[2 * k + 1], w0[2 * k + 1] = y_lb, y_ub, 0.5 * (y_lb + y_ub)
+    return p, lbw, ubw, w0

@@ -1,0 +1,99 @@
+"""Layout parity (CPU): the product transcription vs the oracle restatement.
+
+Checks that the product builds the NLP in the reference ordering
+(`casadi_/full.py:36-98`, `casadi_/admm.py:119-310`): the
+same (p, lbx, ubx, x0) vectors from the same MPC inputs, and the same f(w, p),
+g(w, p), lbg(p), ubg(p) at random points — bit-for-bit up to fp64 rounding.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from agentlib_mpc_amd import symbolic as sx
+from tests import configs
+
+EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
+    "one_room": (121, 105, 96),
+    "admm_room": (71, 70, None),
+    "admm_ahu": (160, 150, None),
+    "exchange_room": (31, 20, 71),
+    "exchange_supply": (20, 10, None),
+}
+
+
+@pytest.mark.parametrize("name", list(configs.CASES))
+def test_dims_and_inputs_match_oracle(name):
+    case = configs.CASES[name]()
+    nlp = case.backend.problem.nlp
+    nw, ng, npar = EXPECTED_DIMS[name]
+    assert nlp.nw == nw and nlp.ng_total == ng
+    if npar is not None:
+        assert nlp.npar == npar
+    assert (nlp.nw, nlp.ng_total, nlp.npar) == (case.oracle.n, case.oracle.m, case.oracle.np_)
+    (p, lbw, ubw, w0), _ = configs.product_nlp_inputs(case)
+    op, olb, oub, ow0 = case.oracle_inputs
+    np.testing.assert_array_equal(p, op)
+    np.testing.assert_array_equal(lbw, olb)
+    np.testing.assert_array_equal(ubw, oub)
+    np.testing.assert_array_equal(w0, ow0)
+
+
+@pytest.mark.parametrize("name", list(configs.CASES))
+def test_functions_match_oracle(name):
+    case = configs.CASES[name]()
+    nlp = case.backend.problem.nlp
+    rng = np.random.default_rng(20261015)
+    (p, lbw, ubw, w0), _ = configs.product_nlp_inputs(case)
+    for trial in range(3):
+        w = w0 + rng.normal(scale=0.05, size=w0.shape) * np.maximum(1.0, np.abs(w0)) * 1e-2
+        pp = p * (1 + 0.1 * rng.normal(size=p.shape))
+        vals = {s: v for s, v in zip(nlp.w_syms, w)}
+        vals.update({s: v for s, v in zip(nlp.p_syms, pp)})
+        f, *g = sx.evaluate([nlp.f_expr] + nlp.g_exprs, vals)
+        lb = sx.evaluate(nlp.g_lb, vals) if nlp.g_lb else []
+        ub = sx.evaluate(nlp.g_ub, vals) if nlp.g_ub else []
+        of = float(case.oracle.f(torch.as_tensor(w), torch.as_tensor(pp)))
+        og = case.oracle.g(torch.as_tensor(w), torch.as_tensor(pp)).numpy()
+        np.testing.assert_allclose(float(f), of, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(np.array(g, float), og, rtol=1e-11, atol=1e-9)
+        np.testing.assert_allclose(np.array(lb, float), case.oracle.lbg(pp), rtol=0, atol=0)
+        np.testing.assert_allclose(np.array(ub, float), case.oracle.ubg(pp), rtol=0, atol=0)
+
+
+def test_stage_function_reproduces_full_nlp():
+    """The generic stage function evaluated stage by stage == the full NLP."""
+    case = configs.one_room()
+    nlp = case.backend.problem.nlp
+    st = nlp.stage
+    (p, lbw, ubw, w0), _ = configs.product_nlp_inputs(case)
+    rng = np.random.default_rng(1)
+    w = w0 + rng.normal(scale=0.01, size=w0.shape)
+    vals = {s: v for s, v in zip(nlp.w_syms, w)}
+    vals.update({s: v for s, v in zip(nlp.p_syms, p)})
+    full = sx.evaluate([nlp.f_expr] + nlp.g_exprs, vals)
+    np_ = nlp.nv + nlp.nx
+    ftot, gs = 0.0, []
+    for k in range(nlp.N):
+        loc = w[k * np_: k * np_ + len(st.local)]
+        sv = {s: v for s, v in zip(st.local, loc)}
+        sv.update({s: v for s, v in zip(st.PS, p[nlp.npg + k * nlp.nps: nlp.npg + (k + 1) * nlp.nps])})
+        sv.update({s: v for s, v in zip(st.PG, p[:nlp.npg])})
+        sv[st.TK] = k * nlp.ts
+        out = sx.evaluate([st.cost] + st.g, sv)
+        ftot += float(out[0])
+        gs += [float(v) for v in out[1:]]
+    np.testing.assert_allclose(ftot, float(full[0]), rtol=1e-13)
+    np.testing.assert_allclose(gs, np.array(full[1:], float), rtol=1e-13, atol=1e-12)
+
+
+def test_result_layout_matches_reference_shape():
+    """C1 result matrix: 46 rows x 21 columns."""
+    case = configs.one_room()
+    lay = case.backend.problem.layout
+    assert len(lay.full_grid) == 46
+    assert len(lay.columns) == 21
+    assert [c for c in lay.columns if c[0] == "parameter"][:3] == [
+        ("parameter", "T_in"), ("parameter", "load"), ("parameter", "T_upper")]
+    assert len(lay.variable_grid_indices["mDot"]) == 15
+    assert len(lay.variable_grid_indices["T"]) == 46  # (d+1)N+1 (test_casadi_backend.py:127-132)

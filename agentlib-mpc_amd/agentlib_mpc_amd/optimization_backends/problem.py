@@ -202,3 +202,54 @@ class CompiledProblem:
         lay = self.layout
         return Results(matrix=self.result_matrix(mpc_inputs, w), grid=list(lay.full_grid),
                        columns=lay.columns, stats=stats, variable_grid_indices=lay.variable_grid_indices)
+
+
+def fleet_nlp_inputs(prob: CompiledProblem, template_vars: dict, overrides: Dict[str, np.ndarray],
+                     now: float = 0.0):
+    """NLP inputs of a fleet of agents sharing one structure.
+
+    ``overrides`` maps a scalar MPC variable name to per-agent values (shape
+    [n_agents]) for its ``value`` (parameters/states/controls) — vectorised
+    equivalent of building ``current_vars`` per agent and calling
+    ``mpc_inputs`` + ``initial_guess`` + ``nlp_inputs`` (cold start).
+    Returns (p, lbw, ubw, w0) as [n_agents, .] float64 arrays.
+    """
+    n = len(next(iter(overrides.values())))
+    mi = prob.mpc_inputs(template_vars, now)
+    batched = {k: np.repeat(v[None], n, axis=0) for k, v in mi.items()}
+    for par in prob.system.parameters:
+        for i, name in enumerate(par.full_names):
+            if name in overrides and name in par.ref_names:
+                batched[par.name][:, i, :] = np.asarray(overrides[name], float)[:, None]
+    nlp = prob.nlp
+    p = np.empty((n, nlp.npar))
+    for name, lay in nlp.par_groups.items():
+        if lay.dim:
+            p[:, lay.index] = batched[name]
+    lbw = np.empty((n, nlp.nw))
+    ubw = np.empty((n, nlp.nw))
+    w0 = np.empty((n, nlp.nw))
+    for name, lay in nlp.var_groups.items():
+        if not lay.dim:
+            continue
+        idx = lay.index
+        lb, ub = batched[f"lb_{name}"], batched[f"ub_{name}"]
+        lbw[:, idx] = lb
+        ubw[:, idx] = ub
+        key = f"initial_{name}"
+        if key in batched:
+            meas = batched[key][:, :, -1:]
+            guess = np.repeat(meas, len(lay.grid), axis=2)
+        else:
+            with np.errstate(invalid="ignore"):
+                guess = np.nan_to_num(0.5 * (lb + ub), posinf=0, neginf=-0)
+        w0[:, idx] = guess
+        for t, cols in enumerate(lay.columns):
+            for i, c in enumerate(cols):
+                if lay.lb_par[t][i] >= 0:
+                    lbw[:, c] = p[:, lay.lb_par[t][i]]
+                if lay.ub_par[t][i] >= 0:
+                    ubw[:, c] = p[:, lay.ub_par[t][i]]
+                if lay.guess_par[t][i] >= 0:
+                    w0[:, c] = p[:, lay.guess_par[t][i]]
+    return p, lbw, ubw, w0

@@ -68,7 +68,7 @@ class Options(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")] + \
                [(n, ctypes.c_int32) for n in ("iter_count", "status", "n_inertia_corrections",
-                                              "n_linesearch_fallbacks", "n_factorizations", "reserved")]
+                                              "n_linesearch_fallbacks", "n_factorizations", "n_trials")]
 
 
 STATS_BYTES = ctypes.sizeof(Stats)
@@ -267,5 +267,6 @@ def stats_to_dicts(raw_bytes) -> list:
             "n_inertia_corrections": s.n_inertia_corrections,
             "n_linesearch_fallbacks": s.n_linesearch_fallbacks,
             "n_factorizations": s.n_factorizations,
+            "n_trials": s.n_trials,
         })
     return out

@@ -202,11 +202,10 @@ struct Inertia {
 __device__ __noinline__ void bk_factor(double* A, int* perm, int* piv, int lane, Inertia& in) {
   const double alpha = 0.6403882032022076;  // (1 + sqrt(17)) / 8
   for (int i = lane; i < NB; i += WAVE) perm[i] = i;
-  // block scale for the zero-pivot test
-  double amax = 0.0;
-  for (int t = lane; t < NB * NB; t += WAVE) amax = fmax(amax, fabs(A[(t / NB) * LDB + t % NB]));
-  amax = wmax(amax);
-  const double ztol = 1e-14 * fmax(1.0, amax);
+  // zero pivots: absolute threshold (same constant as oracle/ipm.py ZERO_PIVOT);
+  // the barrier terms make the block norm unbounded near active bounds, so a
+  // norm-relative test would misclassify legitimate -delta_c pivots
+  const double ztol = 1e-20;
   sync();
   int k = 0;
 #pragma unroll 1
@@ -270,7 +269,7 @@ __device__ __noinline__ void bk_factor(double* A, int* perm, int* piv, int lane,
     } else {
       const double a11 = A[k * LDB + k], a21 = A[(k + 1) * LDB + k], a22 = A[(k + 1) * LDB + k + 1];
       const double det = a11 * a22 - a21 * a21;
-      if (fabs(det) <= ztol * ztol) {
+      if (fabs(det) <= 1e-40) {
         in.zero += 2;  // treated as singular
       } else {
         if (det < 0) { in.pos++; in.neg++; }
@@ -940,7 +939,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   const Scal sc = init_agent(a, args, agent);
   const double obj_scale = sc.obj_scale;
   double fx = sc.fx;
-  int n_fact = 0, n_ic = 0, n_fallback = 0;
+  int n_fact = 0, n_ic = 0, n_fallback = 0, n_trials = 0;
   if (M > 0 && o.constr_mult_init_max > 0.0) {
     ls_multipliers(a, o, obj_scale, L);
     n_fact++;
@@ -968,7 +967,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     if (it >= o.max_iter) break;
     // barrier parameter update (monotone Fiacco-McCormick)
 #pragma unroll 1
-    for (;;) {
+    for (int mu_up = 0; mu_up < 64; ++mu_up) {
       const OptErr em = opt_error(a, mu, obj_scale);
       if (em.err > o.kappa_eps * mu || mu <= o.mu_min) break;
       mu = fmax(o.tol / 10.0, fmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
@@ -1020,9 +1019,11 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     double alpha = st.amax;
     Trial tr{0.0, 0.0, 0.0};
     bool accepted = false, ftype = false;
+    if (!(amin > 0.0)) amin = o.alpha_min_frac * o.gamma_theta;  // NaN guard
 #pragma unroll 1
-    for (;;) {
+    for (int ls = 0; ls < 64; ++ls) {
       tr = trial_point(a, alpha, mu, obj_scale);
+      n_trials++;
       bool okt = (tr.theta <= theta_max) && (tr.phi == tr.phi);
       for (int j = 0; j < nfilt && okt; ++j)
         if (tr.theta >= L.fth[j] && tr.phi >= L.fph[j]) okt = false;
@@ -1080,7 +1081,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     st.n_inertia_corrections = n_ic;
     st.n_linesearch_fallbacks = n_fallback;
     st.n_factorizations = n_fact;
-    st.reserved = 0;
+    st.n_trials = n_trials;
     args.stats[agent] = st;
   }
 }

@@ -106,7 +106,7 @@ typedef struct mpcx_stats {
   int32_t n_inertia_corrections;
   int32_t n_linesearch_fallbacks;
   int32_t n_factorizations;
-  int32_t reserved;
+  int32_t n_trials;    /* line-search trial points evaluated */
 } mpcx_stats;
 
 typedef struct mpcx_handle mpcx_handle;

@@ -28,6 +28,8 @@ import numpy as np
 import scipy.linalg
 
 INF = 1e19  # IPOPT nlp_lower/upper_bound_inf
+DEBUG = False
+ZERO_PIVOT = 1e-20  # same constant as csrc/mpcx_ipm.hip
 
 
 @dataclasses.dataclass
@@ -321,6 +323,8 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
             rhs_l = -c - np.where(ineq & ~free_slack, r_s / (Ss + dw), 0.0)
             _, Dm, _ = scipy.linalg.ldl(K, lower=True)
             ev = _block_eigs(Dm)
+            if DEBUG:
+                print("factor dw=%g dc=%g: ev min/max" % (dw, dc), np.sort(np.abs(ev))[:4], np.max(np.abs(ev)), "npos", int(np.sum(ev>0)), "nneg", int(np.sum(ev<0)), "n", n, "m", m)
             npos = int(np.sum(ev > 0))
             nneg = int(np.sum(ev < 0))
             nzero = len(ev) - npos - nneg
@@ -442,6 +446,8 @@ def _block_eigs(D: np.ndarray) -> np.ndarray:
             ev.append(D[i, i])
             i += 1
     ev = np.asarray(ev)
-    scale = max(1.0, np.max(np.abs(ev), initial=0.0))
-    ev[np.abs(ev) <= 1e-14 * scale] = 0.0
+    # a pivot is "zero" only when it is numerically null in absolute terms: the
+    # barrier terms make the matrix norm grow without bound near active bounds,
+    # so a threshold relative to it would misclassify legitimate -delta_c pivots
+    ev[np.abs(ev) <= ZERO_PIVOT] = 0.0
     return ev

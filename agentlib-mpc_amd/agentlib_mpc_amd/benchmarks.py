@@ -154,6 +154,13 @@ BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
 
 def compile_all(verbose: bool = False):
     """Generate and compile the code objects of all benchmark structures."""
+    from agentlib_mpc_amd.runtime import native
+
+    current = native._kernel_deps_hash()
+    if native.KERNEL_DIR.exists():  # drop code objects of older kernel sources
+        for f in native.KERNEL_DIR.iterdir():
+            if current not in f.name:
+                f.unlink()
     paths = {}
     for name, fn in BUILDERS.items():
         be, _ = fn()

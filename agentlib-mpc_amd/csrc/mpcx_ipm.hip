@@ -60,11 +60,17 @@ constexpr long O_ST = O_XT + NW, O_GT = O_ST + M, O_LB = O_GT + M, O_UB = O_LB +
 constexpr long O_SDG = O_UB + M;                 // [NL][N]      stage cost gradient
 constexpr long O_SDJ = O_SDG + (long)NL * N;     // [NG*NL][N]   stage jacobian
 constexpr long O_SDH = O_SDJ + (long)NG * NL * N;// [NL*NL][N]   stage hessian
-constexpr long O_FAC = O_SDH + (long)NL * NL * N;// [N][NB*LDB]  block factors
+constexpr long O_FAC = O_SDH + (long)NL * NL * N;// [N][NB*LDB]  blocks, then block inverses
 constexpr long O_RHS = O_FAC + (long)N * NB * LDB;
 constexpr long O_SOL = O_RHS + (long)N * NB;
-constexpr long O_PIV = O_SOL + (long)N * NB;     // ints: perm[N][NB], piv[N][NB]
-constexpr long WS_DOUBLES = O_PIV + (long)N * NB;  // 2 ints per double slot
+constexpr long O_CPL = O_SOL + (long)N * NB;     // [N][NB*NX] couplings to x_k (block chain)
+constexpr long O_KX = O_CPL + (long)N * NB * (NX > 0 ? NX : 1);  // [N*NP] primal KKT diagonal
+constexpr long O_KD = O_KX + (long)N * NP;       // [M] dual KKT diagonal
+constexpr int LPK = (NV + NG + 2 * NX) * (NV + NG + 2 * NX + 1) / 2;
+constexpr long O_LF = O_KD + M;                  // [N][LPK] stage-local factors
+constexpr long O_LPV = O_LF + (long)N * LPK;     // [N][2*NI] ints (perm, piv)
+constexpr long O_LZ = O_LPV + (long)N * (NV + NG);
+constexpr long WS_DOUBLES = O_LZ + (long)N * (NV + NG);
 
 using Args = mpcx_kernel_args;
 
@@ -101,8 +107,21 @@ __device__ __forceinline__ void wargmax(double& v, int& idx) {
   }
 }
 __device__ __forceinline__ void sync() { __syncthreads(); }
+// Wavefront-scope sync for LDS-only hand-offs between lanes: a workgroup is one
+// wavefront and the LDS executes one wave's DS instructions in issue order, so
+// only compiler ordering is needed (no s_barrier, no vmcnt drain).
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ bool isfin(double v) { return fabs(v) < INFINITY; }
+
+// LDS-qualified pointers: keeps ds_* addressing inside the noinline phases
+// (a generic pointer would compile to flat_* accesses)
+typedef __attribute__((address_space(3))) double ldsd;
+typedef __attribute__((address_space(3))) int ldsi;
 
 // ---------------------------------------------------------------------------
 // per-agent views
@@ -138,8 +157,12 @@ struct Agent {
   __device__ double* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
   __device__ double* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
   __device__ double* sol(int k) const { return ws + O_SOL + (long)k * NB; }
-  __device__ int* perm(int k) const { return reinterpret_cast<int*>(ws + O_PIV) + k * NB; }
-  __device__ int* piv(int k) const { return reinterpret_cast<int*>(ws + O_PIV) + N * NB + k * NB; }
+  __device__ double* cpl(int k) const { return ws + O_CPL + (long)k * NB * (NX > 0 ? NX : 1); }
+  __device__ double* kx() const { return ws + O_KX; }
+  __device__ double* kd() const { return ws + O_KD; }
+  __device__ double* lf(int k) const { return ws + O_LF + (long)k * LPK; }
+  __device__ int* lpv(int k) const { return reinterpret_cast<int*>(ws + O_LPV) + (long)k * 2 * (NV + NG); }
+  __device__ double* lz(int k) const { return ws + O_LZ + (long)k * (NV + NG); }
 };
 
 __device__ __forceinline__ bool is_fixed(const Agent& a, int i) { return a.xL()[i] == a.xU()[i]; }
@@ -193,45 +216,46 @@ __device__ __forceinline__ double acc_jtl(const Agent& a, int i, const double* l
 }
 
 // ---------------------------------------------------------------------------
-// dense Bunch-Kaufman LDL^T of the LDS block (full symmetric storage)
+// dense Bunch-Kaufman LDL^T in LDS (full symmetric storage, wave-wide)
 // ---------------------------------------------------------------------------
 struct Inertia {
   int pos, neg, zero;
 };
 
-__device__ __noinline__ void bk_factor(double* A, int* perm, int* piv, int lane, Inertia& in) {
-  const double alpha = 0.6403882032022076;  // (1 + sqrt(17)) / 8
-  for (int i = lane; i < NB; i += WAVE) perm[i] = i;
-  // zero pivots: absolute threshold (same constant as oracle/ipm.py ZERO_PIVOT);
-  // the barrier terms make the block norm unbounded near active bounds, so a
-  // norm-relative test would misclassify legitimate -delta_c pivots
-  const double ztol = 1e-20;
-  sync();
+// zero pivots: absolute threshold (same constant as oracle/ipm.py ZERO_PIVOT);
+// the barrier terms make the block norm unbounded near active bounds, so a
+// norm-relative test would misclassify legitimate -delta_c pivots
+constexpr double ZERO_PIVOT = 1e-20;
+constexpr double BK_ALPHA = 0.6403882032022076;  // (1 + sqrt(17)) / 8
+
+template <int NN, int LD>
+__device__ __noinline__ void bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int lane, Inertia& in) {
+  constexpr int NN2 = NN * NN;
+  for (int i = lane; i < NN; i += WAVE) perm[i] = i;
+  wsync();
   int k = 0;
 #pragma unroll 1
-  while (k < NB) {
-    const double akk = fabs(A[k * LDB + k]);
+  while (k < NN) {
+    const double akk = fabs(A[k * LD + k]);
     double lam = -1.0;
     int r = -1;
-    for (int i = k + 1 + lane; i < NB; i += WAVE) {
-      const double t = fabs(A[i * LDB + k]);
+    for (int i = k + 1 + lane; i < NN; i += WAVE) {
+      const double t = fabs(A[i * LD + k]);
       if (t > lam) { lam = t; r = i; }
     }
     wargmax(lam, r);
     if (r < 0) lam = 0.0;
     int size = 1, kp = k;
-    if (fmax(akk, lam) == 0.0) {
-      size = 1; kp = k;
-    } else if (akk >= alpha * lam) {
+    if (fmax(akk, lam) == 0.0 || akk >= BK_ALPHA * lam) {
       size = 1; kp = k;
     } else {
       double sg = 0.0;
-      for (int j = k + lane; j < NB; j += WAVE)
-        if (j != r) sg = fmax(sg, fabs(A[r * LDB + j]));
+      for (int j = k + lane; j < NN; j += WAVE)
+        if (j != r) sg = fmax(sg, fabs(A[r * LD + j]));
       const double sigma = wmax(sg);
-      if (akk * sigma >= alpha * lam * lam) {
+      if (akk * sigma >= BK_ALPHA * lam * lam) {
         size = 1; kp = k;
-      } else if (fabs(A[r * LDB + r]) >= alpha * sigma) {
+      } else if (fabs(A[r * LD + r]) >= BK_ALPHA * sigma) {
         size = 1; kp = r;
       } else {
         size = 2; kp = r;
@@ -239,118 +263,117 @@ __device__ __noinline__ void bk_factor(double* A, int* perm, int* piv, int lane,
     }
     const int kk = k + size - 1;
     if (kp != kk) {
-      for (int j = lane; j < NB; j += WAVE) {
-        const double t = A[kp * LDB + j]; A[kp * LDB + j] = A[kk * LDB + j]; A[kk * LDB + j] = t;
+      for (int j = lane; j < NN; j += WAVE) {
+        const double t = A[kp * LD + j]; A[kp * LD + j] = A[kk * LD + j]; A[kk * LD + j] = t;
       }
-      sync();
-      for (int i = lane; i < NB; i += WAVE) {
-        const double t = A[i * LDB + kp]; A[i * LDB + kp] = A[i * LDB + kk]; A[i * LDB + kk] = t;
+      wsync();
+      for (int i = lane; i < NN; i += WAVE) {
+        const double t = A[i * LD + kp]; A[i * LD + kp] = A[i * LD + kk]; A[i * LD + kk] = t;
       }
       if (lane == 0) { const int t = perm[kp]; perm[kp] = perm[kk]; perm[kk] = t; }
-      sync();
+      wsync();
     }
-    const int nt = NB - k - size;
     if (size == 1) {
-      const double d = A[k * LDB + k];
-      if (fabs(d) <= ztol) {
+      const double d = A[k * LD + k];
+      if (fabs(d) <= ZERO_PIVOT) {
         in.zero++;
-        for (int i = k + 1 + lane; i < NB; i += WAVE) A[i * LDB + k] = 0.0;
+        for (int i = k + 1 + lane; i < NN; i += WAVE) A[i * LD + k] = 0.0;
       } else {
         if (d > 0) in.pos++; else in.neg++;
         const double rd = 1.0 / d;
-        for (int t = lane; t < nt * nt; t += WAVE) {
-          const int i = k + 1 + t / nt, j = k + 1 + t % nt;
-          A[i * LDB + j] -= A[i * LDB + k] * A[j * LDB + k] * rd;
+        for (int t = lane; t < NN2; t += WAVE) {
+          const int i = t / NN, j = t % NN;
+          if (i > k && j > k) A[i * LD + j] -= A[i * LD + k] * A[j * LD + k] * rd;
         }
-        sync();
-        for (int i = k + 1 + lane; i < NB; i += WAVE) A[i * LDB + k] *= rd;
+        wsync();
+        for (int i = k + 1 + lane; i < NN; i += WAVE) A[i * LD + k] *= rd;
       }
       if (lane == 0) piv[k] = 1;
     } else {
-      const double a11 = A[k * LDB + k], a21 = A[(k + 1) * LDB + k], a22 = A[(k + 1) * LDB + k + 1];
+      const double a11 = A[k * LD + k], a21 = A[(k + 1) * LD + k], a22 = A[(k + 1) * LD + k + 1];
       const double det = a11 * a22 - a21 * a21;
-      if (fabs(det) <= 1e-40) {
-        in.zero += 2;  // treated as singular
+      if (fabs(det) <= ZERO_PIVOT * ZERO_PIVOT) {
+        in.zero += 2;
       } else {
         if (det < 0) { in.pos++; in.neg++; }
         else if (a11 + a22 > 0) in.pos += 2;
         else in.neg += 2;
       }
       const double rdet = 1.0 / det;
-      for (int t = lane; t < nt * nt; t += WAVE) {
-        const int i = k + 2 + t / nt, j = k + 2 + t % nt;
-        const double ai1 = A[i * LDB + k], ai2 = A[i * LDB + k + 1];
-        const double l1 = (ai1 * a22 - ai2 * a21) * rdet, l2 = (ai2 * a11 - ai1 * a21) * rdet;
-        A[i * LDB + j] -= l1 * A[j * LDB + k] + l2 * A[j * LDB + k + 1];
+      for (int t = lane; t < NN2; t += WAVE) {
+        const int i = t / NN, j = t % NN;
+        if (i > k + 1 && j > k + 1) {
+          const double ai1 = A[i * LD + k], ai2 = A[i * LD + k + 1];
+          const double l1 = (ai1 * a22 - ai2 * a21) * rdet, l2 = (ai2 * a11 - ai1 * a21) * rdet;
+          A[i * LD + j] -= l1 * A[j * LD + k] + l2 * A[j * LD + k + 1];
+        }
       }
-      sync();
-      for (int i = k + 2 + lane; i < NB; i += WAVE) {
-        const double ai1 = A[i * LDB + k], ai2 = A[i * LDB + k + 1];
-        A[i * LDB + k] = (ai1 * a22 - ai2 * a21) * rdet;
-        A[i * LDB + k + 1] = (ai2 * a11 - ai1 * a21) * rdet;
+      wsync();
+      for (int i = k + 2 + lane; i < NN; i += WAVE) {
+        const double ai1 = A[i * LD + k], ai2 = A[i * LD + k + 1];
+        A[i * LD + k] = (ai1 * a22 - ai2 * a21) * rdet;
+        A[i * LD + k + 1] = (ai2 * a11 - ai1 * a21) * rdet;
       }
       if (lane == 0) { piv[k] = 2; piv[k + 1] = 0; }
     }
-    sync();
+    wsync();
     k += size;
   }
 }
 
-// v <- A^{-1} v using factor F (L, D in F; perm, piv); v and y in LDS
-__device__ __noinline__ void bk_solve(const double* F, const int* perm, const int* piv, double* v, double* y,
-                         int lane) {
-  for (int i = lane; i < NB; i += WAVE) y[i] = v[perm[i]];
-  sync();
-  // forward: L z = y
+// Explicit inverse of a factored block, A^{-1} = P^T L^{-T} D^{-1} L^{-1} P,
+// written in the ORIGINAL index order to `out` (ld LD).  W, Y: LDS scratch.
+template <int NN, int LD>
+__device__ __noinline__ void bk_inverse(const ldsd* A, const ldsi* perm, const ldsi* piv, ldsd* W,
+                                        ldsd* Y, double* out, int lane) {
+  constexpr int NN2 = NN * NN;
+  for (int t = lane; t < NN2; t += WAVE) {
+    const int i = t / NN, j = t % NN;
+    W[i * LD + j] = (i == j) ? 1.0 : 0.0;
+  }
+  wsync();
   int k = 0;
-  while (k < NB) {
+#pragma unroll 1
+  while (k < NN) {
     const int sz = piv[k];
-    const double y0 = y[k];
-    if (sz == 1) {
-      for (int i = k + 1 + lane; i < NB; i += WAVE) y[i] -= F[i * LDB + k] * y0;
-    } else {
-      const double y1 = y[k + 1];
-      for (int i = k + 2 + lane; i < NB; i += WAVE) y[i] -= F[i * LDB + k] * y0 + F[i * LDB + k + 1] * y1;
+    for (int t = lane; t < NN2; t += WAVE) {
+      const int i = t / NN, j = t % NN;
+      if (i >= k + sz && j <= k + sz - 1) {
+        double v = A[i * LD + k] * W[k * LD + j];
+        if (sz == 2) v += A[i * LD + k + 1] * W[(k + 1) * LD + j];
+        W[i * LD + j] -= v;
+      }
     }
-    sync();
+    wsync();
     k += sz;
   }
-  // diagonal
-  for (int i = lane; i < NB; i += WAVE) {
+  for (int t = lane; t < NN2; t += WAVE) {
+    const int i = t / NN, j = t % NN;
     const int sz = piv[i];
     if (sz == 1) {
-      const double d = F[i * LDB + i];
-      y[i] = (d != 0.0) ? y[i] / d : 0.0;
+      const double d = A[i * LD + i];
+      Y[i * LD + j] = (d != 0.0) ? W[i * LD + j] / d : 0.0;
     } else if (sz == 2) {
-      const double a11 = F[i * LDB + i], a21 = F[(i + 1) * LDB + i], a22 = F[(i + 1) * LDB + i + 1];
+      const double a11 = A[i * LD + i], a21 = A[(i + 1) * LD + i], a22 = A[(i + 1) * LD + i + 1];
       const double det = a11 * a22 - a21 * a21;
-      const double y0 = y[i], y1 = y[i + 1];
-      y[i] = (a22 * y0 - a21 * y1) / det;
-      y[i + 1] = (a11 * y1 - a21 * y0) / det;
+      const double w0 = W[i * LD + j], w1 = W[(i + 1) * LD + j];
+      Y[i * LD + j] = (a22 * w0 - a21 * w1) / det;
+      Y[(i + 1) * LD + j] = (a11 * w1 - a21 * w0) / det;
     }
   }
-  sync();
-  // backward: L^T u = y (column sweep from the end)
-  k = NB - 1;
-  while (k >= 0) {
-    const int start = (piv[k] == 0) ? k - 1 : k;
-    const int sz = k - start + 1;
-    const double u0 = y[start];
-    const double u1 = (sz == 2) ? y[start + 1] : 0.0;
-    for (int j = lane; j < start; j += WAVE) {
-      double t = F[start * LDB + j] * u0;
-      if (sz == 2) t += F[(start + 1) * LDB + j] * u1;
-      y[j] -= t;
-    }
-    sync();
-    k = start - 1;
+  wsync();
+  for (int t = lane; t < NN2; t += WAVE) {
+    const int i = t / NN, j = t % NN;
+    double acc = 0.0;
+    const int mx = i > j ? i : j;
+    for (int m = (mx > 0 ? mx - 1 : 0); m < NN; ++m) acc += W[m * LD + i] * Y[m * LD + j];
+    out[perm[i] * LD + perm[j]] = acc;
   }
-  for (int i = lane; i < NB; i += WAVE) v[perm[i]] = y[i];
-  sync();
+  wsync();
 }
 
 // ---------------------------------------------------------------------------
-// KKT assembly
+// KKT entries
 // ---------------------------------------------------------------------------
 enum Mode { NEWTON = 0, LSQ = 1 };
 
@@ -389,151 +412,735 @@ __device__ __forceinline__ double dual_diag(const Agent& a, int c, const KKTDiag
   return 1.0 / (sigma_s(a, c) + kd.dw) + kd.dc;
 }
 
-// coupling of block k to x_k (columns c < NX of stage k's local vector)
+// ---------------------------------------------------------------------------
+// LDS layout
+// ---------------------------------------------------------------------------
+// Stage-parallel path: stage k's local system, ordered [V_k, lambda_k | x_k, x_{k+1}],
+// is held packed-lower in LDS; SR stages are resident per round, G lanes per stage.
+constexpr int NI = NV + NG;               // stage interior (eliminated in parallel)
+constexpr int NXP = NX > 0 ? NX : 1;
+constexpr int NXX = NXP * NXP;
+constexpr int NLOC = NI + 2 * NX;         // local system size
+constexpr int PK = NLOC * (NLOC + 1) / 2; // packed lower triangle
+constexpr int PKS = PK | 1;               // odd stride between stage slots
+static_assert(NI > 0, "stage interior must be non-empty");
+
+__host__ __device__ constexpr int pow2floor(int v) { int p = 1; while (p * 2 <= v) p *= 2; return p; }
+__host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+constexpr int SLOT_BYTES = 8 * (PKS + NLOC) + 8 * NI;  // F + z + perm/piv
+constexpr int OTHER_BYTES = 8 * (N * 3 * NXX + N * NXX + 3 * N * NXP + 3 * NXX + 2 * MAXF) + 8 * NXP + 64;
+#ifndef MPCX_LDS_TARGET
+#define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
+#endif
+constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / SLOT_BYTES));
+constexpr int ROUNDS = (N + SR0 - 1) / SR0;
+constexpr int SR = (N + ROUNDS - 1) / ROUNDS;   // stages per round (balanced)
+constexpr int G = pow2floor(WAVE / SR);         // lanes per stage
+
+constexpr int SQ = NX > 0 ? NB : 1;   // the fallback exists only when stages are coupled
+constexpr int SQL = NX > 0 ? LDB : 1;
+struct SeqLds {               // sequential block chain (fallback)
+  double A[SQ * SQL];
+  double W[SQ * SQL];
+  double Y[SQ * SQL];
+  double B[SQ * NXP];
+  double BP[SQ * NXP];
+  double P[NXX];
+  double v[SQ];
+  double y[SQ];
+  double t[SQ];
+  int perm[SQ];
+  int piv[SQ];
+};
+struct ParLds {
+  double F[SR * PKS];
+  double z[SR * NLOC];
+  int perm[SR * NI];
+  int piv[SR * NI];
+};
+union LinLds {
+  SeqLds s;
+  ParLds p;
+};
+
+struct Lds {
+  LinLds u;
+  double S[N * 3 * NXX];   // local Schur blocks per stage: S00 (x_k), S11 (x_{k+1}), S10
+  double Dinv[N * NXX];    // inverses of the state-chain pivots
+  double zx0[N * NXP];     // forward-eliminated local rhs, x_k part
+  double zx1[N * NXP];     // ... x_{k+1} part
+  double xs[N * NXP];      // state-chain rhs, then solution (x_1 .. x_N)
+  double C[NXX];
+  double CW[NXX];
+  double CY[NXX];
+  int cperm[NXP];
+  int cpiv[NXP];
+  int seq;                 // 1: last factorisation used the sequential chain
+  double fth[MAXF];
+  double fph[MAXF];
+#ifdef MPCX_PROFILE
+  double sprof[6];
+#endif
+};
+
+__shared__ Lds gL;
+#ifdef MPCX_PROFILE
+#define SPROF_DECL unsigned long long _st = __builtin_amdgcn_s_memtime();
+#define SPROF(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); if (a.lane == 0) gL.sprof[i] += (double)(_n - _st); _st = _n; } while (0)
+#else
+#define SPROF_DECL
+#define SPROF(i) do { } while (0)
+#endif  // one agent per workgroup: the agent's LDS scratch
+#define LDSP(x) ((ldsd*)(x))
+#define LDSI(x) ((ldsi*)(x))
+
+// per-variable / per-constraint diagonal terms of the KKT matrix, once per factorisation
+// (workspace: NaN in kx marks a fixed variable)
+__device__ __noinline__ void kkt_diagonals(const Agent& a, const KKTDiag& kd) {
+  for (int q = a.lane; q < N * NP; q += WAVE) {
+    const int i = NX + q;
+    a.kx()[q] = is_fixed(a, i) ? NAN : (kd.mode == LSQ ? 1.0 : sigma_x(a, i) + kd.dw);
+  }
+  for (int c = a.lane; c < M; c += WAVE) a.kd()[c] = dual_diag(a, c, kd);
+  sync();
+}
+
+__device__ __forceinline__ bool kfixed(const Agent& a, int k, int q) {
+  const double v = a.kx()[k * NP + q];
+  return v != v;
+}
+
+// ---------------------------------------------------------------------------
+// sequential block chain (fallback when a stage interior is singular)
+// ---------------------------------------------------------------------------
+// entry (i, j) of KKT block k = [V_k, X_{k+1}, lambda_k] (before the Schur update)
+__device__ __forceinline__ double kkt_entry(const Agent& a, int k, int i, int j, Mode mode) {
+  if (i < NP && j < NP) {
+    if (kfixed(a, k, i) || kfixed(a, k, j)) return (i == j) ? 1.0 : 0.0;
+    if (mode == LSQ) return (i == j) ? 1.0 : 0.0;
+    double v = a.sdh()[((NX + i) * NL + NX + j) * N + k];
+    if (NX > 0 && i >= NV && j >= NV && k + 1 < N) v += a.sdh()[((i - NV) * NL + (j - NV)) * N + k + 1];
+    if (i == j) v += a.kx()[k * NP + i];
+    return v;
+  }
+  if (i >= NP && j >= NP) return (i == j) ? -a.kd()[k * NG + i - NP] : 0.0;
+  const int r = (i >= NP) ? i - NP : j - NP;
+  const int q = (i >= NP) ? j : i;
+  if (kfixed(a, k, q)) return 0.0;
+  return a.gs()[k * NG + r] * a.sdj()[(r * NL + NX + q) * N + k];
+}
+
+// coupling of block k (row) to x_k = X0 of stage k (column c < NX)
 __device__ __forceinline__ double coupling(const Agent& a, int k, int row, int c, Mode mode) {
-  if (is_fixed(a, k * NP + c)) return 0.0;
+  if (k == 0 || kfixed(a, k - 1, NV + c)) return 0.0;
   if (row < NP) {
-    if (mode == LSQ) return 0.0;
-    if (is_fixed(a, NX + k * NP + row)) return 0.0;
+    if (mode == LSQ || kfixed(a, k, row)) return 0.0;
     return a.sdh()[((NX + row) * NL + c) * N + k];
   }
   const int r = row - NP;
   return a.gs()[k * NG + r] * a.sdj()[(r * NL + c) * N + k];
 }
 
-__device__ __noinline__ void assemble(const Agent& a, int k, const KKTDiag& kd, double* A) {
-  const int lane = a.lane;
-  const int w0 = NX + k * NP;
-  for (int t = lane; t < NP * NP; t += WAVE) {
-    const int p = t / NP, q = t % NP;
-    double v;
-    if (is_fixed(a, w0 + p) || is_fixed(a, w0 + q)) {
-      v = (p == q) ? 1.0 : 0.0;
-    } else if (kd.mode == LSQ) {
-      v = (p == q) ? 1.0 : 0.0;
-    } else {
-      v = a.sdh()[((NX + p) * NL + NX + q) * N + k];
-      if (NX > 0 && p >= NV && q >= NV && k + 1 < N) v += a.sdh()[((p - NV) * NL + (q - NV)) * N + k + 1];
-      if (p == q) v += sigma_x(a, w0 + p) + kd.dw;
+constexpr int NB2 = NB * NB;
+constexpr int EPL = (NB2 + WAVE - 1) / WAVE;  // block elements per lane
+
+__device__ __noinline__ void seq_assemble(const Agent& a, Mode mode) {
+#pragma unroll 4
+  for (int t = a.lane; t < N * NB2; t += WAVE) {
+    const int k = t / NB2, e = t % NB2, i = e / NB, j = e % NB;
+    a.fac(k)[i * LDB + j] = kkt_entry(a, k, i, j, mode);
+  }
+  if (NX > 0) {
+#pragma unroll 4
+    for (int t = a.lane; t < N * NB * NX; t += WAVE) {
+      const int k = t / (NB * NX), e = t % (NB * NX);
+      a.cpl(k)[e] = coupling(a, k, e / NX, e % NX, mode);
     }
-    A[p * LDB + q] = v;
   }
-  for (int t = lane; t < NG * NP; t += WAVE) {
-    const int r = t / NP, q = t % NP;
-    const double v = is_fixed(a, w0 + q) ? 0.0 : a.gs()[k * NG + r] * a.sdj()[(r * NL + NX + q) * N + k];
-    A[(NP + r) * LDB + q] = v;
-    A[q * LDB + NP + r] = v;
-  }
-  for (int t = lane; t < NG * NG; t += WAVE) {
-    const int r = t / NG, c = t % NG;
-    A[(NP + r) * LDB + NP + c] = (r == c) ? -dual_diag(a, k * NG + r, kd) : 0.0;
-  }
+  sync();
 }
 
-// Factor the whole chain; returns inertia.  Shared scratch in LDS.
-struct Lds {
-  double A[NB * LDB];
-  double B[NB * (NX > 0 ? NX : 1)];
-  double BP[NB * (NX > 0 ? NX : 1)];
-  double P[(NX > 0 ? NX : 1) * (NX > 0 ? NX : 1)];
-  double v[NB];
-  double y[NB];
-  double t[NB];
-  int perm[NB];
-  int piv[NB];
-  double fth[MAXF];
-  double fph[MAXF];
-};
-
-__device__ __noinline__ Inertia factor_chain(const Agent& a, const KKTDiag& kd, Lds& L) {
+// Block LDL^T through the state columns: D_k = A_k - B_k [D_{k-1}^{-1}]_{xx} B_k^T;
+// each block's explicit inverse is stored (solves become mat-vecs).
+__device__ __noinline__ Inertia seq_factor(const Agent& a, Mode mode) {
+  SeqLds& L = gL.u.s;
+  if constexpr (NX == 0) return Inertia{0, 0, 1};
   const int lane = a.lane;
   Inertia in{0, 0, 0};
+  seq_assemble(a, mode);
+  double pre[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int t = lane + e * WAVE;
+    pre[e] = (t < NB2) ? a.fac(0)[(t / NB) * LDB + t % NB] : 0.0;
+  }
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
-    assemble(a, k, kd, L.A);
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int t = lane + e * WAVE;
+      if (t < NB2) L.A[(t / NB) * LDB + t % NB] = pre[e];
+    }
+    if (NX > 0 && k > 0)
+      for (int t = lane; t < NB * NX; t += WAVE) L.B[t] = a.cpl(k)[t];
+    sync();
+    if (k + 1 < N) {  // prefetch block k+1 (consumed at the top of the next step)
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const int t = lane + e * WAVE;
+        pre[e] = (t < NB2) ? a.fac(k + 1)[(t / NB) * LDB + t % NB] : 0.0;
+      }
+    }
     if (NX > 0 && k > 0) {
-      for (int t = lane; t < NB * NX; t += WAVE) L.B[t] = coupling(a, k, t / NX, t % NX, kd.mode);
-      sync();
       for (int t = lane; t < NB * NX; t += WAVE) {
         const int i = t / NX, d = t % NX;
         double s = 0.0;
         for (int c = 0; c < NX; ++c) s += L.B[i * NX + c] * L.P[c * NX + d];
         L.BP[t] = s;
       }
-      sync();
-      for (int t = lane; t < NB * NB; t += WAVE) {
+      wsync();
+      for (int t = lane; t < NB2; t += WAVE) {
         const int i = t / NB, j = t % NB;
         double s = 0.0;
         for (int d = 0; d < NX; ++d) s += L.BP[i * NX + d] * L.B[j * NX + d];
         L.A[i * LDB + j] -= s;
       }
+      wsync();
     }
+    bk_factor<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), lane, in);
+    bk_inverse<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), LDSP(L.W), LDSP(L.Y), a.fac(k), lane);
     sync();
-    bk_factor(L.A, L.perm, L.piv, lane, in);
-    // store factor
-    double* F = a.fac(k);
-    for (int t = lane; t < NB * LDB; t += WAVE) F[t] = L.A[t];
-    for (int i = lane; i < NB; i += WAVE) { a.perm(k)[i] = L.perm[i]; a.piv(k)[i] = L.piv[i]; }
-    // P_k = [A_k^{-1}]_{X1,X1}
-    if (NX > 0 && k + 1 < N) {
-#pragma unroll 1
-      for (int c = 0; c < NX; ++c) {
-        for (int i = lane; i < NB; i += WAVE) L.v[i] = (i == NV + c) ? 1.0 : 0.0;
-        sync();
-        bk_solve(L.A, L.perm, L.piv, L.v, L.y, lane);
-        for (int d = lane; d < NX; d += WAVE) L.t[d * NX + c] = L.v[NV + d];
-        sync();
-      }
-      for (int t = lane; t < NX * NX; t += WAVE) L.P[t] = L.t[t];
-    }
+    if (NX > 0 && k + 1 < N)
+      for (int t = lane; t < NX * NX; t += WAVE)
+        L.P[t] = a.fac(k)[(NV + t / NX) * LDB + NV + t % NX];
     sync();
   }
   return in;
 }
 
-// Solve the chain with rhs blocks a.rhs(k) -> a.sol(k)
-__device__ __noinline__ void solve_chain(const Agent& a, Mode mode, Lds& L) {
+__device__ __noinline__ void seq_solve(const Agent& a) {
+  SeqLds& L = gL.u.s;
+  if constexpr (NX == 0) return;
   const int lane = a.lane;
-  // forward
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
-    for (int i = lane; i < NB; i += WAVE) L.v[i] = a.rhs(k)[i];
-    sync();
-    if (NX > 0 && k > 0) {
-      for (int t = lane; t < NB * NX; t += WAVE) L.B[t] = coupling(a, k, t / NX, t % NX, mode);
-      sync();
-      const double* wp = a.sol(k - 1);
-      for (int i = lane; i < NB; i += WAVE) {
-        double s = 0.0;
-        for (int c = 0; c < NX; ++c) s += L.B[i * NX + c] * wp[NV + c];
-        L.v[i] -= s;
-      }
-      sync();
+    for (int i = lane; i < NB; i += WAVE) {
+      double v = a.rhs(k)[i];
+      if (NX > 0 && k > 0)
+        for (int c = 0; c < NX; ++c) v -= a.cpl(k)[i * NX + c] * L.y[NV + c];
+      L.v[i] = v;
     }
-    bk_solve(a.fac(k), a.perm(k), a.piv(k), L.v, L.y, lane);
-    for (int i = lane; i < NB; i += WAVE) a.sol(k)[i] = L.v[i];
-    sync();
+    wsync();
+    const double* Ai = a.fac(k);
+    for (int i = lane; i < NB; i += WAVE) {
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < NB; ++j) acc += Ai[i * LDB + j] * L.v[j];
+      a.sol(k)[i] = acc;
+      L.t[i] = acc;
+    }
+    wsync();
+    for (int i = lane; i < NB; i += WAVE) L.y[i] = L.t[i];
+    wsync();
   }
-  // backward
   if (NX > 0) {
 #pragma unroll 1
     for (int k = N - 2; k >= 0; --k) {
-      const double* un = a.sol(k + 1);
-      for (int t = lane; t < NB * NX; t += WAVE) L.B[t] = coupling(a, k + 1, t / NX, t % NX, mode);
-      for (int i = lane; i < NB; i += WAVE) L.v[i] = 0.0;
-      sync();
       for (int c = lane; c < NX; c += WAVE) {
         double s = 0.0;
-#pragma unroll 4
-        for (int i = 0; i < NB; ++i) s += L.B[i * NX + c] * un[i];
-        L.v[NV + c] = s;
+        for (int i = 0; i < NB; ++i) s += a.cpl(k + 1)[i * NX + c] * L.y[i];
+        L.t[c] = s;
       }
-      sync();
-      bk_solve(a.fac(k), a.perm(k), a.piv(k), L.v, L.y, lane);
-      for (int i = lane; i < NB; i += WAVE) a.sol(k)[i] -= L.v[i];
-      sync();
+      wsync();
+      const double* Ai = a.fac(k);
+      for (int i = lane; i < NB; i += WAVE) {
+        double u = a.sol(k)[i];
+        for (int c = 0; c < NX; ++c) u -= Ai[i * LDB + NV + c] * L.t[c];
+        a.sol(k)[i] = u;
+        L.v[i] = u;
+      }
+      wsync();
+      for (int i = lane; i < NB; i += WAVE) L.y[i] = L.v[i];
+      wsync();
     }
   }
+  sync();
+}
+
+// ---------------------------------------------------------------------------
+// stage-parallel elimination (default path)
+// ---------------------------------------------------------------------------
+// The KKT matrix, permuted to [all stage interiors | all states], has a block-
+// diagonal interior part.  Every stage's interior is Bunch-Kaufman factored in
+// parallel (G lanes per stage) with the two state blocks it touches appended as
+// trailing rows, which leaves the stage's local Schur complement on (x_k, x_{k+1})
+// in those rows.  The states then form a block-tridiagonal chain of nx x nx
+// pivots: the only sequential part.  Inertia = sum of interior and chain
+// inertias (Haynsworth).  A singular interior falls back to the block chain.
+
+__device__ __forceinline__ int pko(int i) { return (i * (i + 1)) >> 1; }
+
+__device__ __forceinline__ double gmax(double v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+__device__ __forceinline__ void gargmax(double& v, int& idx) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o, WAVE);
+    const int oi = __shfl_xor(idx, o, WAVE);
+    if (ov > v || (ov == v && oi >= 0 && (idx < 0 || oi < idx))) { v = ov; idx = oi; }
+  }
+}
+
+// local index -> (kind, index in the stage vector [X0, V, X1] of length NL)
+// kinds: 0 primal V, 1 dual, 2 x_k, 3 x_{k+1}
+__device__ __forceinline__ int lkind(int i) {
+  return i < NV ? 0 : (i < NI ? 1 : (i < NI + NX ? 2 : 3));
+}
+
+// entry (i >= j) of stage k's local system
+__device__ __forceinline__ double local_entry(const Agent& a, int k, int i, int j, Mode mode) {
+  const int ki = lkind(i), kj = lkind(j);
+  if (ki == 1 && kj == 1) return (i == j) ? -a.kd()[k * NG + i - NV] : 0.0;
+  if (ki == 1 || kj == 1) {
+    const int r = (ki == 1 ? i : j) - NV;
+    const int q = (ki == 1 ? j : i);
+    const int kq = (ki == 1 ? kj : ki);
+    int nl;
+    if (kq == 0) { if (kfixed(a, k, q)) return 0.0; nl = NX + q; }
+    else if (kq == 2) { if (k == 0 || kfixed(a, k - 1, NV + q - NI)) return 0.0; nl = q - NI; }
+    else { if (kfixed(a, k, NV + q - NI - NX)) return 0.0; nl = NX + NV + (q - NI - NX); }
+    return a.gs()[k * NG + r] * a.sdj()[(r * NL + nl) * N + k];
+  }
+  // primal-primal
+  int nli, nlj;
+  bool fi, fj;
+  if (ki == 0) { fi = kfixed(a, k, i); nli = NX + i; }
+  else if (ki == 2) { fi = (k == 0) || kfixed(a, k - 1, NV + i - NI); nli = i - NI; }
+  else { fi = kfixed(a, k, NV + i - NI - NX); nli = NX + NV + (i - NI - NX); }
+  if (kj == 0) { fj = kfixed(a, k, j); nlj = NX + j; }
+  else if (kj == 2) { fj = (k == 0) || kfixed(a, k - 1, NV + j - NI); nlj = j - NI; }
+  else { fj = kfixed(a, k, NV + j - NI - NX); nlj = NX + NV + (j - NI - NX); }
+  if (fi || fj) return (i == j && ki == 0) ? 1.0 : 0.0;   // fixed states: chain pivot 1
+  if (mode == LSQ) return (i == j && ki != 2) ? 1.0 : 0.0;
+  double v = a.sdh()[(nli * NL + nlj) * N + k];
+  if (i == j && ki == 0) v += a.kx()[k * NP + i];
+  if (i == j && ki == 3) v += a.kx()[k * NP + NV + (i - NI - NX)];
+  return v;
+}
+
+// Bunch-Kaufman over the NI interior pivots of one stage (G lanes, packed lower
+// storage); the trailing 2*NX rows receive the updates but never pivot.
+// Sets bad on a zero pivot (singular interior).
+__device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, Inertia& in, int& bad) {
+  int k = 0;
+#pragma unroll 1
+  while (k < NI) {
+    const double akk = fabs(F[pko(k) + k]);
+    double lam = -1.0;
+    int r = -1;
+    for (int i = k + 1 + g; i < NI; i += G) {
+      const double t = fabs(F[pko(i) + k]);
+      if (t > lam) { lam = t; r = i; }
+    }
+    gargmax(lam, r);
+    if (r < 0) lam = 0.0;
+    if (fmax(akk, lam) == 0.0) {
+      if constexpr (NX > 0) { bad = 1; break; }
+      in.zero++;  // independent stages: the zero column is a zero eigenvalue
+      if (g == 0) piv[k] = 1;
+      wsync();
+      k += 1;
+      continue;
+    }
+    int size = 1, kp = k;
+    if (akk < BK_ALPHA * lam) {
+      double sg = 0.0;
+      for (int j = k + g; j < NI; j += G)
+        if (j != r) sg = fmax(sg, fabs(F[j < r ? pko(r) + j : pko(j) + r]));
+      const double sigma = gmax(sg);
+      if (akk * sigma >= BK_ALPHA * lam * lam) {
+        kp = k;
+      } else if (fabs(F[pko(r) + r]) >= BK_ALPHA * sigma) {
+        kp = r;
+      } else {
+        size = 2; kp = r;
+      }
+    }
+    const int p = k + size - 1, q = kp;
+    if (q != p) {  // symmetric interchange p <-> q (p < q < NI) in packed storage
+      const int op = pko(p), oq = pko(q);
+      for (int j = g; j < NLOC; j += G) {
+        if (j == p) {
+          const double t = F[op + p]; F[op + p] = F[oq + q]; F[oq + q] = t;
+        } else if (j < p) {
+          const double t = F[op + j]; F[op + j] = F[oq + j]; F[oq + j] = t;
+        } else if (j < q) {
+          const int oj = pko(j);
+          const double t = F[oj + p]; F[oj + p] = F[oq + j]; F[oq + j] = t;
+        } else if (j > q) {
+          const int oj = pko(j);
+          const double t = F[oj + p]; F[oj + p] = F[oj + q]; F[oj + q] = t;
+        }
+      }
+      if (g == 0) { const int t = perm[p]; perm[p] = perm[q]; perm[q] = t; }
+      wsync();
+    }
+    if (size == 1) {
+      const double d = F[pko(k) + k];
+      if (fabs(d) <= ZERO_PIVOT) {
+        if constexpr (NX > 0) { bad = 1; break; }
+        in.zero++;
+      } else if (d > 0) {
+        in.pos++;
+      } else {
+        in.neg++;
+      }
+      const double rd = 1.0 / d;
+      const int m = NLOC - 1 - k;  // rows k+1 .. NLOC-1, paired for balance
+      for (int base = 0; base < m; base += 2 * G) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int o = base + (h == 0 ? g : 2 * G - 1 - g);
+          if (o < m) {
+            const int i = k + 1 + o, ri = pko(i);
+            const double lik = F[ri + k] * rd;
+            int pj = pko(k + 1);
+            for (int j = k + 1; j <= i; ++j) { F[ri + j] -= lik * F[pj + k]; pj += j + 1; }
+          }
+        }
+      }
+      wsync();
+      for (int i = k + 1 + g; i < NLOC; i += G) F[pko(i) + k] *= rd;
+      if (g == 0) piv[k] = 1;
+    } else {
+      const int ok = pko(k), ok1 = pko(k + 1);
+      const double a11 = F[ok + k], a21 = F[ok1 + k], a22 = F[ok1 + k + 1];
+      const double det = a11 * a22 - a21 * a21;
+      if (fabs(det) <= ZERO_PIVOT * ZERO_PIVOT) {
+        if constexpr (NX > 0) { bad = 1; break; }
+        in.zero += 2;
+      } else if (det < 0) {
+        in.pos++; in.neg++;
+      } else if (a11 + a22 > 0) {
+        in.pos += 2;
+      } else {
+        in.neg += 2;
+      }
+      const double rdet = 1.0 / det;
+      const int m = NLOC - 2 - k;  // rows k+2 .. NLOC-1
+      for (int base = 0; base < m; base += 2 * G) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int o = base + (h == 0 ? g : 2 * G - 1 - g);
+          if (o < m) {
+            const int i = k + 2 + o, ri = pko(i);
+            const double ai1 = F[ri + k], ai2 = F[ri + k + 1];
+            const double l1 = (ai1 * a22 - ai2 * a21) * rdet, l2 = (ai2 * a11 - ai1 * a21) * rdet;
+            int pj = pko(k + 2);
+            for (int j = k + 2; j <= i; ++j) { F[ri + j] -= l1 * F[pj + k] + l2 * F[pj + k + 1]; pj += j + 1; }
+          }
+        }
+      }
+      wsync();
+      for (int i = k + 2 + g; i < NLOC; i += G) {
+        const int ri = pko(i);
+        const double ai1 = F[ri + k], ai2 = F[ri + k + 1];
+        F[ri + k] = (ai1 * a22 - ai2 * a21) * rdet;
+        F[ri + k + 1] = (ai2 * a11 - ai1 * a21) * rdet;
+      }
+      if (g == 0) { piv[k] = 2; piv[k + 1] = 0; }
+    }
+    wsync();
+    k += size;
+  }
+}
+
+// State chain over x_1..x_N: D_j = S11^(j-1) + S00^(j) - S10^(j-1) D_{j-1}^{-1} S10^(j-1)^T
+// (chain index j-1 <-> x_j; S10^(k) couples x_{k+1} (row) and x_k (col)).
+__device__ __noinline__ void chain_factor(const Agent& a, Inertia& in) {
+  Lds& L = gL;
+  const int lane = a.lane;
+  if constexpr (NX == 1) {
+    double dprev = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < N; ++j) {
+      double d;
+      if (kfixed(a, j, NV)) {
+        d = 1.0;
+      } else {
+        d = L.S[j * 3 + 1] + (j + 1 < N ? L.S[(j + 1) * 3] : 0.0);
+        if (j > 0) { const double t = L.S[j * 3 + 2]; d -= t * t * dprev; }
+      }
+      if (fabs(d) <= ZERO_PIVOT) { in.zero++; dprev = 0.0; }
+      else { if (d > 0) in.pos++; else in.neg++; dprev = 1.0 / d; }
+      if (lane == 0) L.Dinv[j] = dprev;
+    }
+  } else if constexpr (NX > 1) {
+#pragma unroll 1
+    for (int j = 0; j < N; ++j) {
+      // CW = T_j Dinv_{j-1}   (T_j = S10 of stage j)
+      if (j > 0)
+        for (int e = lane; e < NXX; e += WAVE) {
+          const int r = e / NX, c = e % NX;
+          double s = 0.0;
+          for (int m = 0; m < NX; ++m) s += L.S[(j * 3 + 2) * NXX + r * NX + m] * L.Dinv[(j - 1) * NXX + m * NX + c];
+          L.CW[e] = s;
+        }
+      wsync();
+      for (int e = lane; e < NXX; e += WAVE) {
+        const int r = e / NX, c = e % NX;
+        double v = L.S[(j * 3 + 1) * NXX + e] + (j + 1 < N ? L.S[((j + 1) * 3) * NXX + e] : 0.0);
+        if (j > 0)
+          for (int m = 0; m < NX; ++m) v -= L.CW[r * NX + m] * L.S[(j * 3 + 2) * NXX + c * NX + m];
+        const bool fr = kfixed(a, j, NV + r), fc = kfixed(a, j, NV + c);
+        if (fr || fc) v = (r == c) ? 1.0 : 0.0;
+        L.C[e] = v;
+      }
+      wsync();
+      bk_factor<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), lane, in);
+      bk_inverse<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), LDSP(L.CW), LDSP(L.CY), L.Dinv + j * NXX, lane);
+    }
+  }
+  sync();
+}
+
+__device__ __noinline__ void chain_solve(const Agent& a) {
+  Lds& L = gL;
+  const int lane = a.lane;
+  // rhs: rho_j = z1^(j) + z0^(j+1); forward y_j = rho_j - T_j Dinv_{j-1} y_{j-1}
+  if constexpr (NX == 1) {
+    if (lane == 0) {
+      double y = 0.0;
+#pragma unroll 1
+      for (int j = 0; j < N; ++j) {
+        double r = L.zx1[j] + (j + 1 < N ? L.zx0[j + 1] : 0.0);
+        if (j > 0) r -= L.S[j * 3 + 2] * L.Dinv[j - 1] * y;
+        y = r;
+        L.xs[j] = y;
+      }
+      double x = 0.0;
+#pragma unroll 1
+      for (int j = N - 1; j >= 0; --j) {
+        double r = L.xs[j];
+        if (j + 1 < N) r -= L.S[(j + 1) * 3 + 2] * x;
+        x = L.Dinv[j] * r;
+        L.xs[j] = x;
+      }
+    }
+  } else if constexpr (NX > 1) {
+    for (int c = lane; c < NX; c += WAVE) L.xs[c] = L.zx1[c] + (N > 1 ? L.zx0[NX + c] : 0.0);
+    wsync();
+#pragma unroll 1
+    for (int j = 1; j < N; ++j) {
+      for (int r = lane; r < NX; r += WAVE) {  // CY = Dinv_{j-1} y_{j-1}
+        double s = 0.0;
+        for (int m = 0; m < NX; ++m) s += L.Dinv[(j - 1) * NXX + r * NX + m] * L.xs[(j - 1) * NX + m];
+        L.CY[r] = s;
+      }
+      wsync();
+      for (int r = lane; r < NX; r += WAVE) {
+        double v = L.zx1[j * NX + r] + (j + 1 < N ? L.zx0[(j + 1) * NX + r] : 0.0);
+        for (int m = 0; m < NX; ++m) v -= L.S[(j * 3 + 2) * NXX + r * NX + m] * L.CY[m];
+        L.xs[j * NX + r] = v;
+      }
+      wsync();
+    }
+#pragma unroll 1
+    for (int j = N - 1; j >= 0; --j) {
+      for (int r = lane; r < NX; r += WAVE) {  // CY = y_j - T_{j+1}^T x_{j+1}
+        double v = L.xs[j * NX + r];
+        if (j + 1 < N)
+          for (int m = 0; m < NX; ++m) v -= L.S[((j + 1) * 3 + 2) * NXX + m * NX + r] * L.xs[(j + 1) * NX + m];
+        L.CY[r] = v;
+      }
+      wsync();
+      for (int r = lane; r < NX; r += WAVE) {
+        double s = 0.0;
+        for (int m = 0; m < NX; ++m) s += L.Dinv[j * NXX + r * NX + m] * L.CY[m];
+        L.xs[j * NX + r] = s;
+      }
+      wsync();
+    }
+  }
+  sync();
+}
+
+// Factor the KKT matrix; returns the inertia.
+__device__ __noinline__ Inertia factor_chain(const Agent& a, const KKTDiag& kd) {
+  Lds& L = gL;
+  const int lane = a.lane, g = lane % G, slot = lane / G;
+  SPROF_DECL
+  kkt_diagonals(a, kd);
+  ParLds& P = L.u.p;
+  double* F = P.F + slot * PKS;
+  int* perm = P.perm + slot * NI;
+  int* piv = P.piv + slot * NI;
+  Inertia gi{0, 0, 0};
+  int bad = 0;
+#pragma unroll 1
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int k = r * SR + slot;
+    const bool act = slot < SR && k < N;
+    if (act) {
+#pragma unroll 2
+      for (int t = g; t < PK; t += G) {
+        int i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+        if (pko(i + 1) <= t) ++i;
+        if (pko(i) > t) --i;
+        F[t] = local_entry(a, k, i, t - pko(i), kd.mode);
+      }
+      for (int i = g; i < NI; i += G) perm[i] = i;
+    }
+    wsync();
+    SPROF(0);
+    if (act) interior_bk(LDSP(F), LDSI(perm), LDSI(piv), g, gi, bad);
+    wsync();
+    SPROF(1);
+    if constexpr (NX > 0) {
+      if (wsumi(g == 0 ? bad : 0) > 0) {  // singular stage interior: block chain instead
+        if (lane == 0) L.seq = 1;
+        sync();
+        return seq_factor(a, kd.mode);
+      }
+    }
+    if (act) {
+      if (NX > 0) {  // local Schur complement of the two state blocks
+        for (int e = g; e < 3 * NXX; e += G) {
+          const int blk = e / NXX, rr = (e % NXX) / NX, cc = e % NX;
+          int ri, ci;
+          if (blk == 0) { ri = NI + rr; ci = NI + cc; }
+          else if (blk == 1) { ri = NI + NX + rr; ci = NI + NX + cc; }
+          else { ri = NI + NX + rr; ci = NI + cc; }
+          L.S[(k * 3 + blk) * NXX + rr * NX + cc] = (ri >= ci) ? F[pko(ri) + ci] : F[pko(ci) + ri];
+        }
+      }
+      if (ROUNDS > 1) {
+        for (int t = g; t < PK; t += G) a.lf(k)[t] = F[t];
+        for (int i = g; i < NI; i += G) { a.lpv(k)[i] = perm[i]; a.lpv(k)[NI + i] = piv[i]; }
+      }
+    }
+    sync();
+    SPROF(2);
+  }
+  Inertia in{wsumi(g == 0 ? gi.pos : 0), wsumi(g == 0 ? gi.neg : 0), wsumi(g == 0 ? gi.zero : 0)};
+  if (lane == 0) L.seq = 0;
+  if (NX > 0) chain_factor(a, in);
+  sync();
+  SPROF(3);
+  return in;
+}
+
+// Solve with rhs blocks a.rhs(k) ([V, X1, lambda] per stage) -> a.sol(k).
+__device__ __noinline__ void solve_chain(const Agent& a, Mode mode) {
+  Lds& L = gL;
+  (void)mode;
+  if (L.seq) { seq_solve(a); return; }
+  const int lane = a.lane, g = lane % G, slot = lane / G;
+  ParLds& P = L.u.p;
+  double* F = P.F + slot * PKS;
+  double* z = P.z + slot * NLOC;
+  int* perm = P.perm + slot * NI;
+  int* piv = P.piv + slot * NI;
+  SPROF_DECL
+  // forward elimination of every stage interior
+#pragma unroll 1
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int k = r * SR + slot;
+    const bool act = slot < SR && k < N;
+    if (act) {
+      if (ROUNDS > 1) {
+        for (int t = g; t < PK; t += G) F[t] = a.lf(k)[t];
+        for (int i = g; i < NI; i += G) { perm[i] = a.lpv(k)[i]; piv[i] = a.lpv(k)[NI + i]; }
+      }
+      wsync();
+      const double* rk = a.rhs(k);
+      for (int p = g; p < NLOC; p += G) {
+        double v;
+        if (p < NI) { const int o = perm[p]; v = (o < NV) ? rk[o] : rk[NP + o - NV]; }
+        else if (p < NI + NX) v = 0.0;
+        else v = rk[NV + p - NI - NX];
+        z[p] = v;
+      }
+      wsync();
+#pragma unroll 1
+      for (int p = 0; p < NI; ++p) {
+        const int pv = piv[p];
+        if (pv == 1) {
+          const double zp = z[p];
+          for (int i = p + 1 + g; i < NLOC; i += G) z[i] -= F[pko(i) + p] * zp;
+        } else if (pv == 2) {
+          const double z0 = z[p], z1 = z[p + 1];
+          for (int i = p + 2 + g; i < NLOC; i += G) { const int ri = pko(i); z[i] -= F[ri + p] * z0 + F[ri + p + 1] * z1; }
+        }
+        wsync();
+      }
+      for (int c = g; c < NX; c += G) { L.zx0[k * NX + c] = z[NI + c]; L.zx1[k * NX + c] = z[NI + NX + c]; }
+      if (ROUNDS > 1)
+        for (int i = g; i < NI; i += G) a.lz(k)[i] = z[i];
+    }
+    sync();
+  }
+  SPROF(4);
+  if (NX > 0) chain_solve(a);
+  // back substitution of every stage interior
+#pragma unroll 1
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int k = r * SR + slot;
+    const bool act = slot < SR && k < N;
+    if (act) {
+      if (ROUNDS > 1) {
+        for (int t = g; t < PK; t += G) F[t] = a.lf(k)[t];
+        for (int i = g; i < NI; i += G) { perm[i] = a.lpv(k)[i]; piv[i] = a.lpv(k)[NI + i]; z[i] = a.lz(k)[i]; }
+        wsync();
+      }
+      for (int p = g; p < NI; p += G) {
+        const int pv = piv[p];
+        if (pv == 1) {
+          z[p] = z[p] / F[pko(p) + p];
+        } else if (pv == 2) {
+          const double a11 = F[pko(p) + p], a21 = F[pko(p + 1) + p], a22 = F[pko(p + 1) + p + 1];
+          const double det = a11 * a22 - a21 * a21;
+          const double z0 = z[p], z1 = z[p + 1];
+          z[p] = (a22 * z0 - a21 * z1) / det;
+          z[p + 1] = (a11 * z1 - a21 * z0) / det;
+        }
+      }
+      for (int c = g; c < NX; c += G) {
+        z[NI + c] = (k > 0) ? L.xs[(k - 1) * NX + c] : 0.0;
+        z[NI + NX + c] = L.xs[k * NX + c];
+      }
+      wsync();
+      if (NX > 0)
+        for (int i = g; i < NI; i += G) {
+          double s = 0.0;
+          for (int c = 0; c < 2 * NX; ++c) s += F[pko(NI + c) + i] * z[NI + c];
+          z[i] -= s;
+        }
+      wsync();
+#pragma unroll 1
+      for (int m = NI - 1; m > 0; --m) {
+        const double um = z[m];
+        const int skip = (piv[m - 1] == 2) ? m - 1 : -1;
+        const int om = pko(m);
+        for (int i = g; i < m; i += G)
+          if (i != skip) z[i] -= F[om + i] * um;
+        wsync();
+      }
+      double* sk = a.sol(k);
+      for (int p = g; p < NI; p += G) {
+        const int o = perm[p];
+        sk[o < NV ? o : NP + o - NV] = z[p];
+      }
+      for (int c = g; c < NX; c += G) sk[NV + c] = L.xs[k * NX + c];
+    }
+  }
+  sync();
+  SPROF(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -725,10 +1332,10 @@ __device__ __noinline__ Scal init_agent(const Agent& a, const Args& args, int ag
 }
 
 // least-squares estimate of the constraint multipliers (IPOPT constr_mult_init_max)
-__device__ __noinline__ void ls_multipliers(const Agent& a, const mpcx_options& o, double obj_scale, Lds& L) {
+__device__ __noinline__ void ls_multipliers(const Agent& a, const mpcx_options& o, double obj_scale) {
   const int lane = a.lane;
   KKTDiag kd{0.0, 0.0, LSQ};
-  const Inertia in = factor_chain(a, kd, L);
+  const Inertia in = factor_chain(a, kd);
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
     for (int q = lane; q < NP; q += WAVE) {
@@ -742,7 +1349,7 @@ __device__ __noinline__ void ls_multipliers(const Agent& a, const mpcx_options& 
   }
   sync();
   if (in.zero != 0) return;
-  solve_chain(a, LSQ, L);
+  solve_chain(a, LSQ);
   double lmax = 0.0;
   for (int c = lane; c < M; c += WAVE) lmax = fmax(lmax, fabs(a.sol(c / NG)[NP + c % NG]));
   lmax = wmax(lmax);
@@ -922,13 +1529,23 @@ __device__ __noinline__ void accept_step(const Agent& a, const mpcx_options& o, 
 
 using namespace mpcx_kernel;
 
+// Diagnostic build only (-DMPCX_PROFILE): per-phase shader-clock cycles of each
+// agent are written to lam_w[agent][0..15] instead of the bound multipliers.
+#ifdef MPCX_PROFILE
+#define PROF_DECL unsigned long long _pt = __builtin_amdgcn_s_memtime(); double _prof[16] = {0};
+#define PROF(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); _prof[i] += (double)(_n - _pt); _pt = _n; } while (0)
+#else
+#define PROF_DECL
+#define PROF(i) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // the kernel: one agent NLP per workgroup (one wavefront)
 // ---------------------------------------------------------------------------
 extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(Args args) {
   const int agent = blockIdx.x;
   if (agent >= args.n_agents) return;
-  __shared__ Lds L;
+  Lds& L = gL;
   const mpcx_options& o = args.opt;
   Agent a;
   a.ws = args.ws + (long)agent * args.ws_stride;
@@ -936,14 +1553,21 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   a.lane = threadIdx.x;
   const int lane = a.lane;
 
+  PROF_DECL
+#ifdef MPCX_PROFILE
+  if (lane < 6) gL.sprof[lane] = 0.0;
+  sync();
+#endif
   const Scal sc = init_agent(a, args, agent);
+  PROF(0);
   const double obj_scale = sc.obj_scale;
   double fx = sc.fx;
   int n_fact = 0, n_ic = 0, n_fallback = 0, n_trials = 0;
   if (M > 0 && o.constr_mult_init_max > 0.0) {
-    ls_multipliers(a, o, obj_scale, L);
+    ls_multipliers(a, o, obj_scale);
     n_fact++;
   }
+  PROF(1);
 
   double mu = o.mu_init;
   double tau = fmax(o.tau_min, 1.0 - mu);
@@ -975,16 +1599,19 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
       tau = fmax(o.tau_min, 1.0 - mu);
       nfilt = 0;
     }
+    PROF(2);
     eval_hess(a, a.x(), obj_scale);
     sync();
+    PROF(3);
     rhs_primal(a, mu, obj_scale);
+    PROF(4);
     // factorisation with inertia correction (IPOPT Algorithm IC)
     double dw = 0.0, dc = 0.0;
     bool ok = false;
 #pragma unroll 1
     for (int attempt = 0; attempt < 60; ++attempt) {
       KKTDiag kd{dw, dc, NEWTON};
-      const Inertia in = factor_chain(a, kd, L);
+      const Inertia in = factor_chain(a, kd);
       n_fact++;
       if (in.pos == N * NP && in.neg == M && in.zero == 0) {
         if (attempt > 0) dw_last = dw;
@@ -1000,10 +1627,13 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
         if (dw > o.delta_w_max) break;
       }
     }
+    PROF(5);
     if (!ok) { status = MPCX_ERROR_IN_STEP; break; }
     rhs_dual(a, mu, dw);
-    solve_chain(a, NEWTON, L);
+    solve_chain(a, NEWTON);
+    PROF(6);
     const StepInfo st = recover_step(a, mu, tau, dw, obj_scale);
+    PROF(7);
     // filter line search
     const double theta = theta_of(a, a.gv(), a.s());
     const double phi = fx - mu * barrier_of(a, a.x(), a.s());
@@ -1052,11 +1682,13 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
       nfilt++;
       sync();
     }
+    PROF(8);
     accept_step(a, o, mu, alpha, st.az);
     fx = tr.f;
     eval_gj(a, a.x());
     sync();
     it++;
+    PROF(9);
   }
 
   // ---- outputs ----------------------------------------------------------------
@@ -1066,6 +1698,12 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     if (args.lam_w != nullptr)
       args.lam_w[(long)agent * NW + i] = (i < NX) ? 0.0 : (a.zU()[i] - a.zL()[i]) / obj_scale;
   }
+#ifdef MPCX_PROFILE
+  PROF(2);
+  for (int i = 0; i < 6; ++i) _prof[10 + i] = gL.sprof[i];
+  if (args.lam_w != nullptr && lane == 0)
+    for (int i = 0; i < 16 && i < NW; ++i) args.lam_w[(long)agent * NW + i] = _prof[i];
+#endif
   if (args.lam_g != nullptr)
     for (int c = lane; c < M; c += WAVE) args.lam_g[(long)agent * M + c] = a.lam()[c] * a.gs()[c] / obj_scale;
   if (args.stats != nullptr && lane == 0) {

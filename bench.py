@@ -71,27 +71,23 @@ def flops_model(gen, stats):
     return float(tot.sum())
 
 
-def cpu_baseline(n_sample=3):
-    """Oracle (torch-autograd IPM restatement) on a bounded sample, 1 core."""
-    import torch
+def cpu_baseline(p, lbw, ubw, w0, tol, repeats=3):
+    """C restatement of the oracle IPM (oracle/c/ipm_oracle.c), OpenMP over the
+    host cores allotted to this process (OMP_NUM_THREADS), on the rank-0 fleet."""
+    from oracle import cbuild
 
-    from oracle import ipm, nlps
-
-    torch.set_num_threads(1)
-    prob = nlps.one_room()
-    vals = fleet_values(n_sample, 20261015 + 2)
-    t0 = time.perf_counter()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    cbuild.build()
     ok = 0
-    for i in range(n_sample):
-        p, lbw, ubw, w0 = nlps.one_room_inputs(prob, T0=vals["T"][i], load=vals["load"][i],
-                                               T_in=vals["T_in"][i], T_upper=vals["T_upper"][i],
-                                               u_prev=vals["mDot"][i])
-        r = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p), ipm.IPMOptions(tol=1e-8))
-        ok += int(r.success)
+    t0 = time.perf_counter()
+    for _ in range(repeats):
+        _, _, n_ok = cbuild.solve_room_fleet(p, lbw, ubw, w0, tol=tol, threads=threads)
+        ok += n_ok
     dt = time.perf_counter() - t0
-    return {"value": ok / dt, "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"{n_sample} C3 agents (first of the rank-0 fleet), oracle/ipm.py dense "
-                      f"IPOPT restatement with torch fp64 autograd, tol=1e-8, {dt:.1f} s"}
+    return {"value": ok / dt, "unit": "solves/s", "cores": threads, "kind": "port",
+            "sample": f"{repeats} x the rank-0 C3 fleet ({p.shape[0]} agents, same inputs, tol={tol}) "
+                      f"with oracle/c/ipm_oracle.c (IPOPT restatement, block-tridiagonal LDL^T, "
+                      f"gcc -O3 -march=native, OpenMP {threads} threads): {dt:.2f} s wall"}
 
 
 def main():
@@ -216,7 +212,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline()
+                out["cpu_baseline"] = cpu_baseline(p, lbw, ubw, w0, args.tol)
             except Exception as e:  # pragma: no cover
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out))

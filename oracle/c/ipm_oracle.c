@@ -1,0 +1,775 @@
+/* ORACLE (test infrastructure only) — C restatement of the IPOPT algorithm for
+ * stage-structured MPC NLPs, used as the all-cores CPU baseline
+ * and cross-checked against oracle/ipm.py.
+ *
+ * Algorithm: IPOPT (Waechter & Biegler 2006) exactly as oracle/ipm.py restates it
+ * (reference solver call: agentlib_mpc/data_structures/casadi_utils.py:191-217,
+ * optimization_backends/casadi_/core/discretization.py:203).  The KKT system is
+ * solved with a structure-exploiting block-tridiagonal LDL^T (Bunch-Kaufman on
+ * each stage block, Riccati-style Schur complement through the state), which is
+ * what an efficient CPU implementation (fatrop-like) does; one agent per OpenMP
+ * thread.
+ *
+ * The model functions are hand-derived for the one_room model
+ * (examples/one_room_mpc/physical/simple_mpc.py:98-138) transcribed by
+ * direct collocation (optimization_backends/casadi_/full.py:36-98,
+ * basic.py:251-392): no dependency on the product's code generator.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define MAXD 9
+#define MAXNB 64
+
+/* --------------------------------------------------------------------------
+ * one_room collocation stage (d collocation points)
+ * local L = [X0, u, (T_j, Z_j, Y_j)_{j=1..d}, X1]; PS = (T_in, load, T_upper)_j
+ * PG = [T0, u_prev, cp, C, s_T, r_mDot]
+ * g = [cont, (col_j, path_j, out_j)_j]
+ * -------------------------------------------------------------------------- */
+typedef struct {
+  int N, d, nx, nv, ng, nps, npg;
+  double ts;
+  double B[MAXD + 1], C[MAXD + 1][MAXD + 1], D[MAXD + 1];
+} room_t;
+
+static void room_fg(const room_t* m, const double* L, const double* PS, const double* PG,
+                    double* f, double* g) {
+  const int d = m->d;
+  const double ts = m->ts, cp = PG[2], Cz = PG[3], sT = PG[4], r = PG[5];
+  const double X0 = L[0], u = L[1], X1 = L[2 + 3 * d];
+  double fk = 0.0, xe = m->D[0] * X0;
+  for (int j = 0; j < d; ++j) {
+    const double Z = L[2 + 3 * j + 1];
+    fk += m->B[j + 1] * (r * u + sT * Z * Z) * ts;
+    xe += m->D[j + 1] * L[2 + 3 * j];
+  }
+  *f = fk;
+  g[0] = X1 - xe;
+  for (int j = 0; j < d; ++j) {
+    const double T = L[2 + 3 * j], Z = L[2 + 3 * j + 1], Y = L[2 + 3 * j + 2];
+    double xp = m->C[0][j + 1] * X0;
+    for (int q = 0; q < d; ++q) xp += m->C[q + 1][j + 1] * L[2 + 3 * q];
+    const double ode = cp * u / Cz * (PS[3 * j] - T) + PS[3 * j + 1] / Cz;
+    g[1 + 3 * j] = ts * ode - xp;
+    g[2 + 3 * j] = T + Z;
+    g[3 + 3 * j] = Y - T;
+  }
+}
+
+static void room_bounds(const room_t* m, const double* PS, double* lb, double* ub) {
+  for (int i = 0; i < m->ng; ++i) lb[i] = ub[i] = 0.0;
+  for (int j = 0; j < m->d; ++j) ub[2 + 3 * j] = PS[3 * j + 2];
+}
+
+/* gradient (nl) and dense jacobian (ng x nl) */
+static void room_gj(const room_t* m, const double* L, const double* PS, const double* PG,
+                    double* grad, double* jac) {
+  const int d = m->d, nl = 2 * m->nx + m->nv;
+  const double ts = m->ts, cp = PG[2], Cz = PG[3], sT = PG[4], r = PG[5];
+  const double u = L[1];
+  memset(grad, 0, sizeof(double) * nl);
+  memset(jac, 0, sizeof(double) * m->ng * nl);
+  for (int j = 0; j < d; ++j) {
+    grad[1] += m->B[j + 1] * r * ts;
+    grad[2 + 3 * j + 1] = m->B[j + 1] * 2.0 * sT * L[2 + 3 * j + 1] * ts;
+  }
+  jac[0 * nl + nl - 1] = 1.0;
+  jac[0 * nl + 0] = -m->D[0];
+  for (int j = 0; j < d; ++j) jac[0 * nl + 2 + 3 * j] = -m->D[j + 1];
+  for (int j = 0; j < d; ++j) {
+    double* row = jac + (1 + 3 * j) * nl;
+    const double T = L[2 + 3 * j];
+    row[1] = ts * cp / Cz * (PS[3 * j] - T);
+    row[0] = -m->C[0][j + 1];
+    for (int q = 0; q < d; ++q) row[2 + 3 * q] = -m->C[q + 1][j + 1];
+    row[2 + 3 * j] += -ts * cp * u / Cz;
+    row = jac + (2 + 3 * j) * nl;
+    row[2 + 3 * j] = 1.0;
+    row[2 + 3 * j + 1] = 1.0;
+    row = jac + (3 + 3 * j) * nl;
+    row[2 + 3 * j + 2] = 1.0;
+    row[2 + 3 * j] = -1.0;
+  }
+}
+
+static void room_hess(const room_t* m, const double* L, const double* PS, const double* PG,
+                      double sigma, const double* lam, double* H) {
+  const int d = m->d, nl = 2 * m->nx + m->nv;
+  const double ts = m->ts, cp = PG[2], Cz = PG[3], sT = PG[4];
+  (void)L; (void)PS;
+  memset(H, 0, sizeof(double) * nl * nl);
+  for (int j = 0; j < d; ++j) {
+    const int z = 2 + 3 * j + 1, t = 2 + 3 * j;
+    H[z * nl + z] = sigma * m->B[j + 1] * 2.0 * sT * ts;
+    const double c = lam[1 + 3 * j] * (-ts * cp / Cz);
+    H[1 * nl + t] += c;
+    H[t * nl + 1] += c;
+  }
+}
+
+void oracle_room_init(room_t* m, int N, int d, double ts, const double* B, const double* Cm,
+                      const double* D) {
+  m->N = N; m->d = d; m->nx = 1; m->nv = 1 + 3 * d; m->ng = 1 + 3 * d;
+  m->nps = 3 * d; m->npg = 6; m->ts = ts;
+  for (int i = 0; i <= d; ++i) {
+    m->B[i] = B[i];
+    m->D[i] = D[i];
+    for (int j = 0; j <= d; ++j) m->C[i][j] = Cm[i * (d + 1) + j];
+  }
+}
+
+/* --------------------------------------------------------------------------
+ * IPM
+ * -------------------------------------------------------------------------- */
+typedef struct {
+  double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol;
+  int max_iter;
+} opts_t;
+
+typedef struct {
+  double obj;
+  int iter, status, n_fact, n_trials;
+} ostats_t;
+
+typedef struct {
+  int pos, neg, zero;
+} inertia_t;
+
+#define ZERO_PIVOT 1e-20
+
+/* Bunch-Kaufman LDL^T in place (full symmetric n x n, row-major ld) */
+static void bk_factor(double* A, int n, int ld, int* perm, int* piv, inertia_t* in) {
+  const double alpha = 0.6403882032022076;
+  for (int i = 0; i < n; ++i) perm[i] = i;
+  int k = 0;
+  while (k < n) {
+    const double akk = fabs(A[k * ld + k]);
+    double lam = 0.0;
+    int r = -1;
+    for (int i = k + 1; i < n; ++i) {
+      const double t = fabs(A[i * ld + k]);
+      if (t > lam) { lam = t; r = i; }
+    }
+    int size = 1, kp = k;
+    if (fmax(akk, lam) == 0.0 || akk >= alpha * lam) {
+      size = 1; kp = k;
+    } else {
+      double sigma = 0.0;
+      for (int j = k; j < n; ++j)
+        if (j != r) sigma = fmax(sigma, fabs(A[r * ld + j]));
+      if (akk * sigma >= alpha * lam * lam) { size = 1; kp = k; }
+      else if (fabs(A[r * ld + r]) >= alpha * sigma) { size = 1; kp = r; }
+      else { size = 2; kp = r; }
+    }
+    const int kk = k + size - 1;
+    if (kp != kk) {
+      for (int j = 0; j < n; ++j) { double t = A[kp * ld + j]; A[kp * ld + j] = A[kk * ld + j]; A[kk * ld + j] = t; }
+      for (int i = 0; i < n; ++i) { double t = A[i * ld + kp]; A[i * ld + kp] = A[i * ld + kk]; A[i * ld + kk] = t; }
+      int t = perm[kp]; perm[kp] = perm[kk]; perm[kk] = t;
+    }
+    if (size == 1) {
+      const double dv = A[k * ld + k];
+      if (fabs(dv) <= ZERO_PIVOT) {
+        in->zero++;
+        for (int i = k + 1; i < n; ++i) A[i * ld + k] = 0.0;
+      } else {
+        if (dv > 0) in->pos++; else in->neg++;
+        const double rd = 1.0 / dv;
+        for (int i = k + 1; i < n; ++i) {
+          const double aik = A[i * ld + k] * rd;
+          for (int j = k + 1; j < n; ++j) A[i * ld + j] -= aik * A[j * ld + k];
+        }
+        for (int i = k + 1; i < n; ++i) A[i * ld + k] *= rd;
+      }
+      piv[k] = 1;
+    } else {
+      const double a11 = A[k * ld + k], a21 = A[(k + 1) * ld + k], a22 = A[(k + 1) * ld + k + 1];
+      const double det = a11 * a22 - a21 * a21;
+      if (fabs(det) <= 1e-40) in->zero += 2;
+      else if (det < 0) { in->pos++; in->neg++; }
+      else if (a11 + a22 > 0) in->pos += 2;
+      else in->neg += 2;
+      const double rdet = 1.0 / det;
+      for (int i = k + 2; i < n; ++i) {
+        const double ai1 = A[i * ld + k], ai2 = A[i * ld + k + 1];
+        const double l1 = (ai1 * a22 - ai2 * a21) * rdet, l2 = (ai2 * a11 - ai1 * a21) * rdet;
+        for (int j = k + 2; j < n; ++j) A[i * ld + j] -= l1 * A[j * ld + k] + l2 * A[j * ld + k + 1];
+      }
+      for (int i = k + 2; i < n; ++i) {
+        const double ai1 = A[i * ld + k], ai2 = A[i * ld + k + 1];
+        A[i * ld + k] = (ai1 * a22 - ai2 * a21) * rdet;
+        A[i * ld + k + 1] = (ai2 * a11 - ai1 * a21) * rdet;
+      }
+      piv[k] = 2; piv[k + 1] = 0;
+    }
+    k += size;
+  }
+}
+
+static void bk_solve(const double* F, int n, int ld, const int* perm, const int* piv, double* v) {
+  double y[MAXNB];
+  for (int i = 0; i < n; ++i) y[i] = v[perm[i]];
+  for (int k = 0; k < n;) {
+    if (piv[k] == 1) {
+      for (int i = k + 1; i < n; ++i) y[i] -= F[i * ld + k] * y[k];
+      k += 1;
+    } else {
+      for (int i = k + 2; i < n; ++i) y[i] -= F[i * ld + k] * y[k] + F[i * ld + k + 1] * y[k + 1];
+      k += 2;
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    if (piv[i] == 1) {
+      y[i] = F[i * ld + i] != 0.0 ? y[i] / F[i * ld + i] : 0.0;
+    } else if (piv[i] == 2) {
+      const double a11 = F[i * ld + i], a21 = F[(i + 1) * ld + i], a22 = F[(i + 1) * ld + i + 1];
+      const double det = a11 * a22 - a21 * a21, y0 = y[i], y1 = y[i + 1];
+      y[i] = (a22 * y0 - a21 * y1) / det;
+      y[i + 1] = (a11 * y1 - a21 * y0) / det;
+    }
+  }
+  for (int k = n - 1; k >= 0;) {
+    const int start = piv[k] == 0 ? k - 1 : k;
+    for (int j = 0; j < start; ++j) {
+      y[j] -= F[start * ld + j] * y[start];
+      if (start < k) y[j] -= F[(start + 1) * ld + j] * y[start + 1];
+    }
+    k = start - 1;
+  }
+  for (int i = 0; i < n; ++i) v[perm[i]] = y[i];
+}
+
+/* per-agent solver state */
+typedef struct {
+  const room_t* m;
+  int N, NX, NV, NG, NL, NP, NB, NW, M;
+  const double *p;
+  double *x, *s, *lam, *zL, *zU, *vL, *vU, *xL, *xU, *sL, *sU, *gs, *gv, *lb, *ub;
+  double *dx, *ds, *dl, *xt, *st, *gt, *sdg, *sdj, *sdh, *fac, *rhs, *sol;
+  int *perm, *piv;
+  double obj_scale;
+} ws_t;
+
+static int fixedv(const ws_t* w, int i) { return w->xL[i] == w->xU[i]; }
+static int isfin(double v) { return fabs(v) < INFINITY; }
+
+static double eval_fg(ws_t* w, const double* xv, double* gout) {
+  double f = 0.0;
+  for (int k = 0; k < w->N; ++k) {
+    double fk;
+    room_fg(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, &fk, gout + k * w->NG);
+    f += fk;
+  }
+  return f;
+}
+static void eval_gj(ws_t* w, const double* xv) {
+  for (int k = 0; k < w->N; ++k)
+    room_gj(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, w->sdg + k * w->NL,
+            w->sdj + k * w->NG * w->NL);
+}
+static void eval_hess(ws_t* w, const double* xv, double sigma) {
+  double lk[MAXNB];
+  for (int k = 0; k < w->N; ++k) {
+    for (int r = 0; r < w->NG; ++r) lk[r] = w->lam[k * w->NG + r] * w->gs[k * w->NG + r];
+    room_hess(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, sigma, lk,
+              w->sdh + k * w->NL * w->NL);
+  }
+}
+static double acc_grad(const ws_t* w, int i) {
+  const int b = (i - w->NX) / w->NP, off = (i - w->NX) % w->NP;
+  double v = w->sdg[b * w->NL + w->NX + off];
+  if (w->NX > 0 && off >= w->NV && b + 1 < w->N) v += w->sdg[(b + 1) * w->NL + off - w->NV];
+  return v;
+}
+static double acc_jtl(const ws_t* w, int i, const double* lamv) {
+  const int b = (i - w->NX) / w->NP, off = (i - w->NX) % w->NP;
+  double v = 0.0;
+  for (int r = 0; r < w->NG; ++r)
+    v += w->sdj[(b * w->NG + r) * w->NL + w->NX + off] * w->gs[b * w->NG + r] * lamv[b * w->NG + r];
+  if (w->NX > 0 && off >= w->NV && b + 1 < w->N)
+    for (int r = 0; r < w->NG; ++r)
+      v += w->sdj[((b + 1) * w->NG + r) * w->NL + off - w->NV] * w->gs[(b + 1) * w->NG + r] *
+           lamv[(b + 1) * w->NG + r];
+  return v;
+}
+static int ccls(const ws_t* w, int c) {
+  if (w->lb[c] == w->ub[c]) return 0;
+  if (!isfin(w->sL[c]) && !isfin(w->sU[c])) return 2;
+  return 1;
+}
+static double sigma_x(const ws_t* w, int i) {
+  double s = 0.0;
+  if (fixedv(w, i)) return 0.0;
+  if (isfin(w->xL[i])) s += w->zL[i] / (w->x[i] - w->xL[i]);
+  if (isfin(w->xU[i])) s += w->zU[i] / (w->xU[i] - w->x[i]);
+  return s;
+}
+static double sigma_s(const ws_t* w, int c) {
+  double s = 0.0;
+  if (isfin(w->sL[c])) s += w->vL[c] / (w->s[c] - w->sL[c]);
+  if (isfin(w->sU[c])) s += w->vU[c] / (w->sU[c] - w->s[c]);
+  return s;
+}
+
+/* coupling of block k to x_k */
+static double coupling(const ws_t* w, int k, int row, int c, int lsq) {
+  if (fixedv(w, k * w->NP + c)) return 0.0;
+  if (row < w->NP) {
+    if (lsq || fixedv(w, w->NX + k * w->NP + row)) return 0.0;
+    return w->sdh[k * w->NL * w->NL + (w->NX + row) * w->NL + c];
+  }
+  const int r = row - w->NP;
+  return w->gs[k * w->NG + r] * w->sdj[(k * w->NG + r) * w->NL + c];
+}
+
+static inertia_t factor_chain(ws_t* w, double dw, double dc, int lsq) {
+  const int NB = w->NB, NP = w->NP, NV = w->NV, NX = w->NX, NG = w->NG, NL = w->NL, N = w->N;
+  inertia_t in = {0, 0, 0};
+  double P[16], Bm[MAXNB * 4], v[MAXNB];
+  for (int k = 0; k < N; ++k) {
+    double* A = w->fac + k * NB * NB;
+    const int w0 = NX + k * NP;
+    for (int p = 0; p < NP; ++p)
+      for (int q = 0; q < NP; ++q) {
+        double val;
+        if (fixedv(w, w0 + p) || fixedv(w, w0 + q)) val = p == q ? 1.0 : 0.0;
+        else if (lsq) val = p == q ? 1.0 : 0.0;
+        else {
+          val = w->sdh[k * NL * NL + (NX + p) * NL + NX + q];
+          if (NX > 0 && p >= NV && q >= NV && k + 1 < N) val += w->sdh[(k + 1) * NL * NL + (p - NV) * NL + q - NV];
+          if (p == q) val += sigma_x(w, w0 + p) + dw;
+        }
+        A[p * NB + q] = val;
+      }
+    for (int r = 0; r < NG; ++r)
+      for (int q = 0; q < NP; ++q) {
+        const double val = fixedv(w, w0 + q) ? 0.0 : w->gs[k * NG + r] * w->sdj[(k * NG + r) * NL + NX + q];
+        A[(NP + r) * NB + q] = val;
+        A[q * NB + NP + r] = val;
+      }
+    for (int r = 0; r < NG; ++r)
+      for (int c = 0; c < NG; ++c) {
+        double dd = 0.0;
+        if (r == c) {
+          const int cc = k * NG + r, cl = ccls(w, cc);
+          if (lsq) dd = cl == 0 ? 0.0 : 1.0;
+          else if (cl == 0) dd = dc;
+          else if (cl == 2) dd = 1.0;
+          else dd = 1.0 / (sigma_s(w, cc) + dw) + dc;
+        }
+        A[(NP + r) * NB + NP + c] = -dd;
+      }
+    if (NX > 0 && k > 0) {
+      for (int i = 0; i < NB; ++i)
+        for (int c = 0; c < NX; ++c) Bm[i * NX + c] = coupling(w, k, i, c, lsq);
+      for (int i = 0; i < NB; ++i)
+        for (int j = 0; j < NB; ++j) {
+          double s = 0.0;
+          for (int c = 0; c < NX; ++c)
+            for (int e = 0; e < NX; ++e) s += Bm[i * NX + c] * P[c * NX + e] * Bm[j * NX + e];
+          A[i * NB + j] -= s;
+        }
+    }
+    bk_factor(A, NB, NB, w->perm + k * NB, w->piv + k * NB, &in);
+    if (NX > 0 && k + 1 < N) {
+      for (int c = 0; c < NX; ++c) {
+        for (int i = 0; i < NB; ++i) v[i] = i == NV + c ? 1.0 : 0.0;
+        bk_solve(A, NB, NB, w->perm + k * NB, w->piv + k * NB, v);
+        for (int e = 0; e < NX; ++e) P[e * NX + c] = v[NV + e];
+      }
+    }
+  }
+  return in;
+}
+
+static void solve_chain(ws_t* w, int lsq) {
+  const int NB = w->NB, NV = w->NV, NX = w->NX, N = w->N;
+  double v[MAXNB];
+  for (int k = 0; k < N; ++k) {
+    for (int i = 0; i < NB; ++i) v[i] = w->rhs[k * NB + i];
+    if (NX > 0 && k > 0)
+      for (int i = 0; i < NB; ++i)
+        for (int c = 0; c < NX; ++c) v[i] -= coupling(w, k, i, c, lsq) * w->sol[(k - 1) * NB + NV + c];
+    bk_solve(w->fac + k * NB * NB, NB, NB, w->perm + k * NB, w->piv + k * NB, v);
+    memcpy(w->sol + k * NB, v, sizeof(double) * NB);
+  }
+  if (NX > 0)
+    for (int k = N - 2; k >= 0; --k) {
+      for (int i = 0; i < NB; ++i) v[i] = 0.0;
+      for (int c = 0; c < NX; ++c) {
+        double s = 0.0;
+        for (int i = 0; i < NB; ++i) s += coupling(w, k + 1, i, c, lsq) * w->sol[(k + 1) * NB + i];
+        v[NV + c] = s;
+      }
+      bk_solve(w->fac + k * NB * NB, NB, NB, w->perm + k * NB, w->piv + k * NB, v);
+      for (int i = 0; i < NB; ++i) w->sol[k * NB + i] -= v[i];
+    }
+}
+
+static double theta_of(const ws_t* w, const double* gval, const double* sv) {
+  double t = 0.0;
+  for (int c = 0; c < w->M; ++c)
+    t += fabs(ccls(w, c) == 0 ? gval[c] - w->gs[c] * w->lb[c] : gval[c] - sv[c]);
+  return t;
+}
+static double barrier_of(const ws_t* w, const double* xv, const double* sv) {
+  double t = 0.0;
+  for (int i = w->NX; i < w->NW; ++i) {
+    if (fixedv(w, i)) continue;
+    if (isfin(w->xL[i])) t += log(xv[i] - w->xL[i]);
+    if (isfin(w->xU[i])) t += log(w->xU[i] - xv[i]);
+  }
+  for (int c = 0; c < w->M; ++c) {
+    if (ccls(w, c) != 1) continue;
+    if (isfin(w->sL[c])) t += log(sv[c] - w->sL[c]);
+    if (isfin(w->sU[c])) t += log(w->sU[c] - sv[c]);
+  }
+  return t;
+}
+static double opt_error(const ws_t* w, double mu, double* dual_u, double* primal_u, double* compl_) {
+  double dmax = 0, du = 0, pmax = 0, pu = 0, cmax = 0, lsum = 0, zsum = 0;
+  int nz = 0;
+  for (int i = w->NX; i < w->NW; ++i) {
+    if (fixedv(w, i)) continue;
+    const double rd = w->obj_scale * acc_grad(w, i) + acc_jtl(w, i, w->lam) - w->zL[i] + w->zU[i];
+    dmax = fmax(dmax, fabs(rd));
+    du = fmax(du, fabs(rd) / w->obj_scale);
+    if (isfin(w->xL[i])) { cmax = fmax(cmax, fabs((w->x[i] - w->xL[i]) * w->zL[i] - mu)); zsum += fabs(w->zL[i]); nz++; }
+    if (isfin(w->xU[i])) { cmax = fmax(cmax, fabs((w->xU[i] - w->x[i]) * w->zU[i] - mu)); zsum += fabs(w->zU[i]); nz++; }
+  }
+  for (int c = 0; c < w->M; ++c) {
+    const int cl = ccls(w, c);
+    double cv;
+    if (cl == 0) cv = w->gv[c] - w->gs[c] * w->lb[c];
+    else {
+      cv = w->gv[c] - w->s[c];
+      if (cl == 1) {
+        dmax = fmax(dmax, fabs(-w->lam[c] - w->vL[c] + w->vU[c]));
+        if (isfin(w->sL[c])) { cmax = fmax(cmax, fabs((w->s[c] - w->sL[c]) * w->vL[c] - mu)); zsum += fabs(w->vL[c]); nz++; }
+        if (isfin(w->sU[c])) { cmax = fmax(cmax, fabs((w->sU[c] - w->s[c]) * w->vU[c] - mu)); zsum += fabs(w->vU[c]); nz++; }
+      }
+    }
+    pmax = fmax(pmax, fabs(cv));
+    pu = fmax(pu, fabs(cv) / w->gs[c]);
+    lsum += fabs(w->lam[c]);
+  }
+  const double s_d = fmax(100.0, (lsum + zsum) / fmax(1.0, (double)(w->M + nz))) / 100.0;
+  const double s_c = nz > 0 ? fmax(100.0, zsum / nz) / 100.0 : 1.0;
+  if (dual_u) *dual_u = du;
+  if (primal_u) *primal_u = pu;
+  if (compl_) *compl_ = cmax;
+  return fmax(fmax(dmax / s_d, pmax), cmax / s_c);
+}
+static double push_into(double v, double lo, double hi) {
+  const int hl = isfin(lo), hu = isfin(hi);
+  double pl = hl ? 1e-2 * fmax(1.0, fabs(lo)) : 0.0, pu = hu ? 1e-2 * fmax(1.0, fabs(hi)) : 0.0;
+  if (hl && hu) { pl = fmin(pl, 1e-2 * (hi - lo)); pu = fmin(pu, 1e-2 * (hi - lo)); }
+  const double lop = hl ? lo + pl : -INFINITY, hip = hu ? hi - pu : INFINITY;
+  if (hl && hu && lop > hip) return 0.5 * (lo + hi);
+  return fmin(fmax(v, lop), hip);
+}
+
+static void solve_one(const room_t* m, const double* p, const double* lbw, const double* ubw,
+                      double* wio, const opts_t* o, ostats_t* st, double* mem, int* imem) {
+  ws_t W;
+  ws_t* w = &W;
+  w->m = m; w->N = m->N; w->NX = m->nx; w->NV = m->nv; w->NG = m->ng;
+  w->NL = 2 * m->nx + m->nv; w->NP = m->nv + m->nx; w->NB = w->NP + w->NG;
+  w->NW = w->NX + w->N * w->NP; w->M = w->N * w->NG; w->p = p;
+  const int NW = w->NW, M = w->M, NX = w->NX, NP = w->NP, NG = w->NG, NB = w->NB, N = w->N;
+  double* q = mem;
+#define TAKE(ptr, n) do { ptr = q; q += (n); } while (0)
+  TAKE(w->x, NW); TAKE(w->s, M); TAKE(w->lam, M); TAKE(w->zL, NW); TAKE(w->zU, NW);
+  TAKE(w->vL, M); TAKE(w->vU, M); TAKE(w->xL, NW); TAKE(w->xU, NW); TAKE(w->sL, M); TAKE(w->sU, M);
+  TAKE(w->gs, M); TAKE(w->gv, M); TAKE(w->lb, M); TAKE(w->ub, M); TAKE(w->dx, NW); TAKE(w->ds, M);
+  TAKE(w->dl, M); TAKE(w->xt, NW); TAKE(w->st, M); TAKE(w->gt, M);
+  TAKE(w->sdg, N * w->NL); TAKE(w->sdj, N * NG * w->NL); TAKE(w->sdh, N * w->NL * w->NL);
+  TAKE(w->fac, N * NB * NB); TAKE(w->rhs, N * NB); TAKE(w->sol, N * NB);
+#undef TAKE
+  w->perm = imem; w->piv = imem + N * NB;
+  const double INF_B = 1e19;
+  for (int i = 0; i < NW; ++i) {
+    double lo = lbw[i] <= -INF_B ? -INFINITY : lbw[i], hi = ubw[i] >= INF_B ? INFINITY : ubw[i];
+    if (i < NX) hi = lo;
+    w->xL[i] = lo; w->xU[i] = hi; w->x[i] = lo == hi ? lo : wio[i];
+  }
+  for (int k = 0; k < N; ++k) room_bounds(m, p + m->npg + k * m->nps, w->lb + k * NG, w->ub + k * NG);
+  eval_gj(w, w->x);
+  double gmax = 0.0;
+  for (int i = NX; i < NW; ++i) if (!fixedv(w, i)) gmax = fmax(gmax, fabs(acc_grad(w, i)));
+  w->obj_scale = gmax > 100.0 ? fmax(1e-8, 100.0 / gmax) : 1.0;
+  for (int c = 0; c < M; ++c) {
+    const int k = c / NG, r = c % NG;
+    double rm = 0.0;
+    for (int j = 0; j < w->NL; ++j) if (!fixedv(w, k * NP + j)) rm = fmax(rm, fabs(w->sdj[(k * NG + r) * w->NL + j]));
+    w->gs[c] = rm > 100.0 ? fmax(1e-8, 100.0 / rm) : 1.0;
+  }
+  for (int i = 0; i < NW; ++i) {
+    double lo = w->xL[i], hi = w->xU[i];
+    w->zL[i] = w->zU[i] = 0.0;
+    if (i >= NX && lo != hi) {
+      if (isfin(lo)) lo -= 1e-8 * fmax(1.0, fabs(lo));
+      if (isfin(hi)) hi += 1e-8 * fmax(1.0, fabs(hi));
+      w->xL[i] = lo; w->xU[i] = hi;
+      w->x[i] = push_into(w->x[i], lo, hi);
+      w->zL[i] = isfin(lo) ? 1.0 : 0.0;
+      w->zU[i] = isfin(hi) ? 1.0 : 0.0;
+    }
+  }
+  double fx = w->obj_scale * eval_fg(w, w->x, w->gv);
+  for (int c = 0; c < M; ++c) {
+    const double gsc = w->gs[c];
+    w->gv[c] *= gsc;
+    const double lo = w->lb[c], hi = w->ub[c];
+    if (lo == hi) {
+      w->sL[c] = w->sU[c] = w->s[c] = gsc * lo; w->vL[c] = w->vU[c] = 0.0;
+    } else {
+      const double sl = isfin(lo) ? gsc * lo - 1e-8 * fmax(1.0, fabs(gsc * lo)) : -INFINITY;
+      const double su = isfin(hi) ? gsc * hi + 1e-8 * fmax(1.0, fabs(gsc * hi)) : INFINITY;
+      w->sL[c] = sl; w->sU[c] = su; w->s[c] = push_into(w->gv[c], sl, su);
+      w->vL[c] = isfin(sl) ? 1.0 : 0.0; w->vU[c] = isfin(su) ? 1.0 : 0.0;
+    }
+    w->lam[c] = 0.0;
+  }
+  eval_gj(w, w->x);
+  int n_fact = 0, n_trials = 0;
+  {
+    inertia_t in = factor_chain(w, 0.0, 0.0, 1);
+    n_fact++;
+    for (int k = 0; k < N; ++k) {
+      for (int qq = 0; qq < NP; ++qq) {
+        const int i = NX + k * NP + qq;
+        w->rhs[k * NB + qq] = fixedv(w, i) ? 0.0 : -(w->obj_scale * acc_grad(w, i) - w->zL[i] + w->zU[i]);
+      }
+      for (int r = 0; r < NG; ++r) {
+        const int c = k * NG + r;
+        w->rhs[k * NB + NP + r] = ccls(w, c) == 1 ? w->vL[c] - w->vU[c] : 0.0;
+      }
+    }
+    if (in.zero == 0) {
+      solve_chain(w, 1);
+      double lmax = 0.0;
+      for (int c = 0; c < M; ++c) lmax = fmax(lmax, fabs(w->sol[(c / NG) * NB + NP + c % NG]));
+      if (lmax <= 1e3) for (int c = 0; c < M; ++c) w->lam[c] = w->sol[(c / NG) * NB + NP + c % NG];
+    }
+  }
+  double mu = 0.1, tau = fmax(0.99, 1.0 - mu), dw_last = 0.0;
+  const double theta0 = theta_of(w, w->gv, w->s);
+  const double theta_max = 1e4 * fmax(1.0, theta0), theta_min = 1e-4 * fmax(1.0, theta0);
+  double fth[64], fph[64];
+  int nfilt = 0, status = -1, it = 0;
+  for (;;) {
+    double du, pu, cmpl;
+    const double err = opt_error(w, 0.0, &du, &pu, &cmpl);
+    if (err != err || fx != fx) { status = -4; break; }
+    if (err <= o->tol && du <= o->dual_inf_tol && pu <= o->constr_viol_tol && cmpl <= o->compl_inf_tol) { status = 0; break; }
+    if (it >= o->max_iter) break;
+    for (int g = 0; g < 64; ++g) {
+      if (opt_error(w, mu, 0, 0, 0) > 10.0 * mu || mu <= 1e-11) break;
+      mu = fmax(o->tol / 10.0, fmin(0.2 * mu, pow(mu, 1.5)));
+      mu = fmax(mu, 1e-11);
+      tau = fmax(0.99, 1.0 - mu);
+      nfilt = 0;
+    }
+    eval_hess(w, w->x, w->obj_scale);
+    for (int i = NX; i < NW; ++i) {
+      double r = 0.0;
+      if (!fixedv(w, i)) {
+        double gphi = w->obj_scale * acc_grad(w, i);
+        if (isfin(w->xL[i])) gphi -= mu / (w->x[i] - w->xL[i]);
+        if (isfin(w->xU[i])) gphi += mu / (w->xU[i] - w->x[i]);
+        r = -(gphi + acc_jtl(w, i, w->lam));
+      }
+      w->rhs[((i - NX) / NP) * NB + (i - NX) % NP] = r;
+    }
+    double dw = 0.0, dc = 0.0;
+    int ok = 0;
+    for (int attempt = 0; attempt < 60; ++attempt) {
+      inertia_t in = factor_chain(w, dw, dc, 0);
+      n_fact++;
+      if (in.pos == N * NP && in.neg == M && in.zero == 0) { if (attempt > 0) dw_last = dw; ok = 1; break; }
+      if (attempt == 0) {
+        if (in.zero > 0) dc = 1e-8 * pow(mu, 0.25);
+        dw = dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+      } else {
+        dw = dw_last == 0.0 ? 100.0 * dw : 8.0 * dw;
+        if (dw > 1e40) break;
+      }
+    }
+    if (!ok) { status = -3; break; }
+    for (int c = 0; c < M; ++c) {
+      const int cl = ccls(w, c);
+      double rr;
+      if (cl == 0) rr = -(w->gv[c] - w->gs[c] * w->lb[c]);
+      else {
+        rr = -(w->gv[c] - w->s[c]);
+        if (cl == 1) {
+          double gps = 0.0;
+          if (isfin(w->sL[c])) gps -= mu / (w->s[c] - w->sL[c]);
+          if (isfin(w->sU[c])) gps += mu / (w->sU[c] - w->s[c]);
+          rr -= (gps - w->lam[c]) / (sigma_s(w, c) + dw);
+        }
+      }
+      w->rhs[(c / NG) * NB + NP + c % NG] = rr;
+    }
+    solve_chain(w, 0);
+    double amax = 1.0, az = 1.0, gphid = 0.0;
+    for (int i = 0; i < NW; ++i) {
+      double d = 0.0;
+      if (i >= NX && !fixedv(w, i)) d = w->sol[((i - NX) / NP) * NB + (i - NX) % NP];
+      w->dx[i] = d;
+      if (i < NX || fixedv(w, i)) continue;
+      double gphi = w->obj_scale * acc_grad(w, i);
+      if (isfin(w->xL[i])) {
+        const double sl = w->x[i] - w->xL[i];
+        gphi -= mu / sl;
+        if (d < 0) amax = fmin(amax, -tau * sl / d);
+        const double dz = mu / sl - w->zL[i] - (w->zL[i] / sl) * d;
+        if (dz < 0) az = fmin(az, -tau * w->zL[i] / dz);
+      }
+      if (isfin(w->xU[i])) {
+        const double su = w->xU[i] - w->x[i];
+        gphi += mu / su;
+        if (d > 0) amax = fmin(amax, tau * su / d);
+        const double dz = mu / su - w->zU[i] + (w->zU[i] / su) * d;
+        if (dz < 0) az = fmin(az, -tau * w->zU[i] / dz);
+      }
+      gphid += gphi * d;
+    }
+    for (int c = 0; c < M; ++c) {
+      const double dlam = w->sol[(c / NG) * NB + NP + c % NG];
+      w->dl[c] = dlam;
+      double dsv = 0.0;
+      if (ccls(w, c) == 1) {
+        double gps = 0.0;
+        if (isfin(w->sL[c])) gps -= mu / (w->s[c] - w->sL[c]);
+        if (isfin(w->sU[c])) gps += mu / (w->sU[c] - w->s[c]);
+        const double rs = gps - w->lam[c];
+        dsv = (dlam - rs) / (sigma_s(w, c) + dw);
+        gphid += gps * dsv;
+        if (isfin(w->sL[c])) {
+          const double sl = w->s[c] - w->sL[c];
+          if (dsv < 0) amax = fmin(amax, -tau * sl / dsv);
+          const double dv = mu / sl - w->vL[c] - (w->vL[c] / sl) * dsv;
+          if (dv < 0) az = fmin(az, -tau * w->vL[c] / dv);
+        }
+        if (isfin(w->sU[c])) {
+          const double su = w->sU[c] - w->s[c];
+          if (dsv > 0) amax = fmin(amax, tau * su / dsv);
+          const double dv = mu / su - w->vU[c] + (w->vU[c] / su) * dsv;
+          if (dv < 0) az = fmin(az, -tau * w->vU[c] / dv);
+        }
+      }
+      w->ds[c] = dsv;
+    }
+    const double theta = theta_of(w, w->gv, w->s);
+    const double phi = fx - mu * barrier_of(w, w->x, w->s);
+    double amin;
+    if (gphid < 0 && theta <= theta_min)
+      amin = 0.05 * fmin(fmin(1e-5, 1e-8 * theta / -gphid), pow(theta, 1.1) / pow(-gphid, 2.3));
+    else if (gphid < 0) amin = 0.05 * fmin(1e-5, 1e-8 * theta / -gphid);
+    else amin = 0.05 * 1e-5;
+    if (!(amin > 0)) amin = 0.05 * 1e-5;
+    double alpha = amax, ft = 0.0;
+    int accepted = 0, ftype = 0;
+    for (int ls = 0; ls < 64; ++ls) {
+      for (int i = 0; i < NW; ++i) w->xt[i] = w->x[i] + alpha * w->dx[i];
+      for (int c = 0; c < M; ++c) w->st[c] = w->s[c] + alpha * w->ds[c];
+      ft = w->obj_scale * eval_fg(w, w->xt, w->gt);
+      n_trials++;
+      for (int c = 0; c < M; ++c) w->gt[c] *= w->gs[c];
+      const double tht = theta_of(w, w->gt, w->st), pht = ft - mu * barrier_of(w, w->xt, w->st);
+      int okt = tht <= theta_max && pht == pht;
+      for (int j = 0; j < nfilt && okt; ++j) if (tht >= fth[j] && pht >= fph[j]) okt = 0;
+      if (okt) {
+        const int sw = gphid < 0 && alpha * pow(-gphid, 2.3) > pow(theta, 1.1);
+        if (theta <= theta_min && sw) { okt = pht <= phi + 1e-8 * alpha * gphid; ftype = 1; }
+        else { okt = tht <= (1 - 1e-5) * theta || pht <= phi - 1e-8 * theta; ftype = 0; }
+      }
+      if (okt) { accepted = 1; break; }
+      alpha *= 0.5;
+      if (alpha < amin) break;
+    }
+    if (!accepted) { nfilt = 0; ftype = 1; }
+    if (!ftype) {
+      if (nfilt == 32) { for (int j = 1; j < 32; ++j) { fth[j - 1] = fth[j]; fph[j - 1] = fph[j]; } nfilt--; }
+      fth[nfilt] = (1 - 1e-5) * theta; fph[nfilt] = phi - 1e-8 * theta; nfilt++;
+    }
+    for (int i = NX; i < NW; ++i) {
+      if (fixedv(w, i)) continue;
+      const double d = w->dx[i], xo = w->x[i], xn = w->xt[i];
+      w->x[i] = xn;
+      if (isfin(w->xL[i])) {
+        const double sl0 = xo - w->xL[i], sl = xn - w->xL[i];
+        const double zn = w->zL[i] + az * (mu / sl0 - w->zL[i] - (w->zL[i] / sl0) * d);
+        w->zL[i] = fmax(fmin(zn, 1e10 * mu / sl), mu / (1e10 * sl));
+      }
+      if (isfin(w->xU[i])) {
+        const double su0 = w->xU[i] - xo, su = w->xU[i] - xn;
+        const double zn = w->zU[i] + az * (mu / su0 - w->zU[i] + (w->zU[i] / su0) * d);
+        w->zU[i] = fmax(fmin(zn, 1e10 * mu / su), mu / (1e10 * su));
+      }
+    }
+    for (int c = 0; c < M; ++c) {
+      w->lam[c] += alpha * w->dl[c];
+      w->gv[c] = w->gt[c];
+      if (ccls(w, c) != 1) { w->s[c] = w->st[c]; continue; }
+      const double so = w->s[c], sn = w->st[c], dsv = w->ds[c];
+      w->s[c] = sn;
+      if (isfin(w->sL[c])) {
+        const double sl0 = so - w->sL[c], sl = sn - w->sL[c];
+        const double vn = w->vL[c] + az * (mu / sl0 - w->vL[c] - (w->vL[c] / sl0) * dsv);
+        w->vL[c] = fmax(fmin(vn, 1e10 * mu / sl), mu / (1e10 * sl));
+      }
+      if (isfin(w->sU[c])) {
+        const double su0 = w->sU[c] - so, su = w->sU[c] - sn;
+        const double vn = w->vU[c] + az * (mu / su0 - w->vU[c] + (w->vU[c] / su0) * dsv);
+        w->vU[c] = fmax(fmin(vn, 1e10 * mu / su), mu / (1e10 * su));
+      }
+    }
+    fx = ft;
+    eval_gj(w, w->x);
+    it++;
+  }
+  for (int i = 0; i < NW; ++i) wio[i] = w->x[i];
+  st->obj = fx / w->obj_scale;
+  st->iter = it;
+  st->status = status;
+  st->n_fact = n_fact;
+  st->n_trials = n_trials;
+}
+
+/* Solve n_agents one_room NLPs (agent-major arrays); returns #converged. */
+int oracle_room_solve_fleet(const room_t* m, int n_agents, const double* p, const double* lbw,
+                            const double* ubw, double* w_io, ostats_t* stats, double tol,
+                            int max_iter, int threads) {
+  opts_t o = {tol, 1.0, 1e-4, 1e-4, max_iter};
+  const int NW = m->nx + m->N * (m->nv + m->nx), NPAR = m->npg + m->N * m->nps;
+  const int NB = m->nv + m->nx + m->ng, NL = 2 * m->nx + m->nv, M = m->N * m->ng;
+  const long dbl = 8L * NW + 14L * M + (long)m->N * (NL + m->ng * NL + NL * NL + NB * NB + 2 * NB) + 64;
+  int ok = 0;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel reduction(+ : ok)
+  {
+    double* mem = (double*)malloc(sizeof(double) * dbl);
+    int* imem = (int*)malloc(sizeof(int) * 2 * m->N * NB);
+#pragma omp for schedule(dynamic, 4)
+    for (int a = 0; a < n_agents; ++a) {
+      solve_one(m, p + (long)a * NPAR, lbw + (long)a * NW, ubw + (long)a * NW, w_io + (long)a * NW,
+                &o, &stats[a], mem, imem);
+      ok += stats[a].status == 0;
+    }
+    free(mem);
+    free(imem);
+  }
+  return ok;
+}
+
+int oracle_room_sizeof(void) { return (int)sizeof(room_t); }

@@ -1,0 +1,96 @@
+"""ORACLE (test infrastructure only) — build + ctypes binding of oracle/c/ipm_oracle.c.
+
+The C restatement is the CPU baseline of bench.py (all host cores, OpenMP,
+one agent NLP per thread) and is cross-checked against oracle/ipm.py in
+tests/test_oracle.py.  Built with gcc -O3 -march=native -fopenmp into
+oracle/c/build/ (git-ignored; travels to the GPU box with the snapshot).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+import subprocess
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+SRC = HERE / "c" / "ipm_oracle.c"
+OUT = HERE / "c" / "build" / "liboracle_ipm.so"
+
+MAXD = 9
+
+
+class RoomT(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("N", "d", "nx", "nv", "ng", "nps", "npg")] + [
+        ("ts", ctypes.c_double),
+        ("B", ctypes.c_double * (MAXD + 1)),
+        ("C", (ctypes.c_double * (MAXD + 1)) * (MAXD + 1)),
+        ("D", ctypes.c_double * (MAXD + 1)),
+    ]
+
+
+class OStats(ctypes.Structure):
+    _fields_ = [("obj", ctypes.c_double)] + [(n, ctypes.c_int) for n in ("iter", "status", "n_fact", "n_trials")]
+
+
+def build(force: bool = False, march: str = "native") -> pathlib.Path:
+    OUT.parent.mkdir(parents=True, exist_ok=True)
+    if OUT.exists() and not force and OUT.stat().st_mtime >= SRC.stat().st_mtime:
+        return OUT
+    cmd = ["gcc", "-O3", f"-march={march}", "-fopenmp", "-shared", "-fPIC", "-std=c11", str(SRC),
+           "-o", str(OUT) + ".tmp", "-lm"]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0 and march == "native":
+        return build(force=True, march="x86-64-v2")
+    if res.returncode != 0:
+        raise RuntimeError(res.stderr)
+    os.replace(str(OUT) + ".tmp", OUT)
+    return OUT
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not OUT.exists():
+            build()
+        _lib = ctypes.CDLL(str(OUT))
+        vp = ctypes.c_void_p
+        _lib.oracle_room_init.argtypes = [ctypes.POINTER(RoomT), ctypes.c_int, ctypes.c_int, ctypes.c_double, vp, vp, vp]
+        _lib.oracle_room_solve_fleet.argtypes = [ctypes.POINTER(RoomT), ctypes.c_int, vp, vp, vp, vp,
+                                                 ctypes.POINTER(OStats), ctypes.c_double, ctypes.c_int, ctypes.c_int]
+        _lib.oracle_room_solve_fleet.restype = ctypes.c_int
+        assert _lib.oracle_room_sizeof() == ctypes.sizeof(RoomT)
+    return _lib
+
+
+def room_model(N=15, d=2, ts=300.0) -> RoomT:
+    from oracle.nlps import collocation
+
+    _, B, C, D = collocation(d)
+    m = RoomT()
+    Bc = np.ascontiguousarray(B, dtype=np.float64)
+    Cc = np.ascontiguousarray(C, dtype=np.float64)
+    Dc = np.ascontiguousarray(D, dtype=np.float64)
+    lib().oracle_room_init(ctypes.byref(m), N, d, ts, Bc.ctypes.data, Cc.ctypes.data, Dc.ctypes.data)
+    return m
+
+
+def solve_room_fleet(p, lbw, ubw, w0, N=15, d=2, tol=1e-8, max_iter=500, threads=0):
+    """Returns (w, stats list of dicts, n_converged)."""
+    m = room_model(N, d)
+    p = np.ascontiguousarray(p, dtype=np.float64)
+    lbw = np.ascontiguousarray(lbw, dtype=np.float64)
+    ubw = np.ascontiguousarray(ubw, dtype=np.float64)
+    w = np.array(w0, dtype=np.float64, order="C", copy=True)
+    n = p.shape[0]
+    st = (OStats * n)()
+    ok = lib().oracle_room_solve_fleet(ctypes.byref(m), n, p.ctypes.data, lbw.ctypes.data, ubw.ctypes.data,
+                                       w.ctypes.data, st, tol, max_iter, threads)
+    stats = [{"obj": s.obj, "iter": s.iter, "status": s.status, "n_fact": s.n_fact, "n_trials": s.n_trials}
+             for s in st]
+    return w, stats, ok

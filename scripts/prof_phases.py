@@ -1,0 +1,48 @@
+"""Diagnostic: per-phase cycle breakdown of mpcx_ipm_solve (MPCX_PROFILE build)."""
+import os, sys, subprocess, json
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "agentlib-mpc_amd")]
+import numpy as np
+
+def build_profile_hsaco(gen):
+    from agentlib_mpc_amd.runtime import native
+    src = native.KERNEL_DIR / f"prof_{gen.key}.hip"
+    out = src.with_suffix(".hsaco")
+    src.parent.mkdir(parents=True, exist_ok=True)
+    src.write_text("#define MPCX_PROFILE 1\n" + gen.source)
+    subprocess.run([native._hipcc(), "--genco", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    f"-I{native.INCLUDE}", f"-I{native.CSRC}", str(src), "-o", str(out)], check=True)
+    return out
+
+def main():
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import NativeProblem
+    import bench
+    be, cv = bm.one_room(solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
+    path = build_profile_hsaco(be.problem.gen)
+    if len(sys.argv) > 1 and sys.argv[1] == "build":
+        print(path); return
+    import torch
+    n = int(os.environ.get("AGENTS", "4096"))
+    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261017))
+    nat = NativeProblem(be.problem.gen, hsaco=path)
+    nat.set_options(tol=1e-8, max_iter=500)
+    d = torch.device("cuda")
+    T = lambda a: torch.as_tensor(a, device=d).contiguous()
+    tp, tl, tu, tw = T(p), T(lbw), T(ubw), T(w0)
+    lw = torch.zeros_like(tw)
+    for _ in range(2):
+        tw.copy_(T(w0)); nat.solve(tp, tl, tu, tw, lam_w=lw)
+    torch.cuda.synchronize()
+    prof = lw[:, :16].cpu().numpy()
+    names = ["init", "ls_mult", "opt_err+mu", "hess", "rhs_x", "factor", "solve", "recover", "linesearch", "accept+gj",
+             "f:assemble", "f:interior_bk", "f:schur+store", "f:chain", "s:forward", "s:chain+back"]
+    tot = prof[:, :10].sum(axis=1).mean()
+    print(json.dumps({k: float(v) for k, v in zip(names, prof.mean(axis=0))}))
+    for k, v in zip(names, prof.mean(axis=0)):
+        print(f"{k:12s} {v/1e3:10.1f} kcyc  {100*v/tot:5.1f}%")
+    print("total kcycles/agent", tot / 1e3)
+
+if __name__ == "__main__":
+    main()

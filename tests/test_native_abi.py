@@ -1,0 +1,59 @@
+"""The C-ABI library (CPU, no GPU calls): it builds for gfx950, loads, and exports
+every entry point declared in include/mpcx.h; generated kernels compile."""
+
+import ctypes
+import pathlib
+import re
+
+import pytest
+
+from agentlib_mpc_amd.runtime import native
+
+HEADER = pathlib.Path(__file__).resolve().parents[1] / "include" / "mpcx.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|void|int64_t)\s+(mpcx_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    assert "mpcx_batch_solve" in names and "mpcx_problem_create" in names
+    assert set(names) == set(native.EXPORTED_SYMBOLS)
+
+
+def test_library_builds_loads_and_exports_all_symbols():
+    path = native.build_library()
+    lib = ctypes.CDLL(str(path))
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.mpcx_version() == 3
+
+
+def test_struct_sizes_match_header():
+    # mpcx_options: 36 doubles + 4 int32; mpcx_stats: 6 doubles + 6 int32
+    assert ctypes.sizeof(native.Options) == 36 * 8 + 4 * 4
+    assert ctypes.sizeof(native.Stats) == 6 * 8 + 6 * 4
+    assert ctypes.sizeof(native.ProblemDesc) == 8 * 4
+
+
+def test_default_options_are_ipopt_defaults():
+    o = native.default_options()
+    assert o.mu_init == 0.1 and o.kappa_mu == 0.2 and o.theta_mu == 1.5
+    assert o.bound_push == 1e-2 and o.kappa_sigma == 1e10 and o.tau_min == 0.99
+
+
+def test_generated_kernel_compiles(tmp_path, monkeypatch):
+    from agentlib_mpc_amd import benchmarks as bm
+
+    be, _ = bm.exchange_supply()
+    path = be.problem.compile()
+    assert path.exists() and path.stat().st_size > 0
+
+
+def test_product_path_has_no_cpu_fallback(monkeypatch):
+    monkeypatch.setattr(native, "LIB_PATH", pathlib.Path("/nonexistent/libmpcx.so"))
+    monkeypatch.setattr(native, "_lib", None)
+    with pytest.raises(native.NativeError):
+        native.load_library()

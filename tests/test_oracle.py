@@ -1,0 +1,71 @@
+"""The oracle itself (CPU): numpy IPM vs an independent scipy solver, and the
+C restatement (CPU baseline) vs the numpy IPM."""
+
+import numpy as np
+import pytest
+from scipy.optimize import Bounds, NonlinearConstraint, minimize
+
+from oracle import cbuild, ipm, nlps
+from tests import configs
+
+
+def _scipy_trust_constr(prob, p, lbw, ubw, w0):
+    fn = prob.functions(p)
+    free = lbw < ubw
+    x0 = np.where(free, w0, lbw)
+    cons = NonlinearConstraint(fn.g, prob.lbg(p), prob.ubg(p), jac=fn.jac_g,
+                               hess=lambda w, v: fn.hess_l(w, 0.0, v))
+    keep = np.flatnonzero(free)
+
+    # fix fixed variables through bounds with a tiny width (trust-constr needs lb<ub)
+    lb = np.where(free, lbw, lbw - 1e-12)
+    ub = np.where(free, ubw, ubw + 1e-12)
+    r = minimize(fn.f, x0, jac=fn.grad_f, hess=lambda w: fn.hess_l(w, 1.0, np.zeros(prob.m)),
+                 constraints=[cons], bounds=Bounds(lb, ub), method="trust-constr",
+                 options={"gtol": 1e-11, "xtol": 1e-13, "maxiter": 3000})
+    return r
+
+
+@pytest.mark.slow
+def test_oracle_ipm_vs_scipy_trust_constr():
+    prob = nlps.one_room(N=6)
+    p, lbw, ubw, w0 = nlps.one_room_inputs(prob, N=6)
+    res = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p), ipm.IPMOptions(tol=1e-10))
+    assert res.success
+    sc = _scipy_trust_constr(prob, p, lbw, ubw, w0)
+    # trust-constr's own barrier stops at ~1e-6 relative accuracy: the IPM must be at
+    # least as optimal and agree to that accuracy
+    assert res.f <= sc.fun + 1e-9
+    np.testing.assert_allclose(sc.fun, res.f, rtol=1e-5)
+    np.testing.assert_allclose(sc.x, res.x, rtol=1e-4, atol=1e-5)
+
+
+def test_oracle_kkt_residuals_small():
+    case = configs.exchange_supply(diff=-0.01, lam=20.0)
+    p, lbw, ubw, w0 = case.oracle_inputs
+    fn = case.oracle.functions(p)
+    res = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), ipm.IPMOptions(tol=1e-10))
+    assert res.success
+    # stationarity of the Lagrangian with the returned multipliers
+    r = fn.grad_f(res.x) + fn.jac_g(res.x).T @ res.lam_g + res.lam_x
+    assert np.max(np.abs(r)) < 1e-7 * max(1.0, np.max(np.abs(fn.grad_f(res.x))))
+    assert np.max(np.abs(fn.g(res.x) - case.oracle.lbg(p))) < 1e-9
+
+
+def test_c_oracle_matches_numpy_oracle():
+    prob = nlps.one_room()
+    rng = np.random.default_rng(11)
+    P, LB, UB, W0, refs = [], [], [], [], []
+    for i in range(3):
+        kw = dict(T0=float(rng.uniform(291, 301)), load=float(rng.uniform(50, 250)),
+                  T_upper=float(rng.uniform(294.15, 296.15)))
+        p, lbw, ubw, w0 = nlps.one_room_inputs(prob, **kw)
+        P.append(p); LB.append(lbw); UB.append(ubw); W0.append(w0)
+        refs.append(ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p),
+                              ipm.IPMOptions(tol=1e-10)))
+    cbuild.build()
+    w, st, ok = cbuild.solve_room_fleet(np.array(P), np.array(LB), np.array(UB), np.array(W0), tol=1e-10)
+    assert ok == 3
+    for i, r in enumerate(refs):
+        np.testing.assert_allclose(w[i], r.x, rtol=1e-9, atol=1e-9)
+        assert st[i]["iter"] == r.iterations

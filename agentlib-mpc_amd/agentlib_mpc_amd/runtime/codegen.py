@@ -13,6 +13,12 @@ emitted as four ``__device__`` functions:
 * ``gen_stage_gj``      cost gradient and dense constraint Jacobian,
 * ``gen_stage_hess``    Hessian of the stage Lagrangian ``σ f + λᵀ g``.
 
+``gen_stage_gj`` and ``gen_stage_hess`` also write their entries straight
+into ``lp``, the packed lower triangle of the stage's local KKT system in the
+kernel's local order ``[V, λ, x_k, x_{k+1}, rhs]`` (Jacobian rows scaled by
+the constraint scaling ``G[r]``), so the factorisation assembles a stage by a
+contiguous copy instead of gathering strided derivative entries.
+
 The file ends by including the generic kernel `csrc/mpcx_ipm.hip`, so each
 model gets one fully specialised code object (all dimensions compile-time).
 """
@@ -26,7 +32,7 @@ from typing import Dict, List
 from agentlib_mpc_amd import symbolic as sx
 from agentlib_mpc_amd.optimization_backends.discretization import StageNLP
 
-KERNEL_ABI_VERSION = 3
+KERNEL_ABI_VERSION = 4
 
 
 @dataclasses.dataclass
@@ -80,14 +86,36 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     cg = sx.CodeGen(bind, prefix="b")
     bd_lines = cg.emit([(f"lb[{i} * S]", e) for i, e in enumerate(st.g_lb)]
                        + [(f"ub[{i} * S]", e) for i, e in enumerate(st.g_ub)])
+    # local order of the kernel's stage system: [V (nv), lambda (ng), x_k (nx), x_{k+1} (nx), rhs]
+    nx, nv = nlp.nx, nlp.nv
+    ni = nv + ng
+
+    def lidx(n: int) -> int:
+        if n < nx:
+            return ni + n
+        if n < nx + nv:
+            return n - nx
+        return ni + nx + (n - nx - nv)
+
+    def pk(i: int, j: int) -> int:
+        i, j = max(i, j), min(i, j)
+        return i * (i + 1) // 2 + j
+
     # -- gradient + jacobian (structural zeros are never written) --
     gj_assign = [(f"grad[{j} * S]", e) for j, e in enumerate(grad) if not e.is_const(0.0)]
     gj_assign += [(f"jac[{i * nl + j} * S]", jac[i][j]) for i in range(ng) for j in range(nl)
                   if not jac[i][j].is_const(0.0)]
-    cg = sx.CodeGen(bind, prefix="c")
-    gj_lines = cg.emit(gj_assign)
-    # -- hessian: lower triangle, mirrored --
+    gsym = [sx.sym(f"G[{r}]") for r in range(ng)]
+    gb = dict(bind)
+    for r, s_ in enumerate(gsym):
+        gb[s_] = f"G[{r}]"
+    lp_j = [(f"lp[{pk(nv + i, lidx(j))}]", sx.mul(gsym[i], jac[i][j])) for i in range(ng) for j in range(nl)
+            if not jac[i][j].is_const(0.0)]
+    cg = sx.CodeGen(gb, prefix="c")
+    gj_lines = cg.emit(gj_assign + lp_j)
+    # -- hessian: lower triangle, mirrored; once into the packed local system --
     h_assign = []
+    lp_h = []
     for i in range(nl):
         for j in range(i + 1):
             e = hess[i][j]
@@ -96,8 +124,9 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
             h_assign.append((f"hess[{i * nl + j} * S]", e))
             if i != j:
                 h_assign.append((f"hess[{j * nl + i} * S]", e))
+            lp_h.append((f"lp[{pk(lidx(i), lidx(j))}]", e))
     cg = sx.CodeGen(hb, prefix="h")
-    h_lines = cg.emit(h_assign)
+    h_lines = cg.emit(h_assign + lp_h)
 
     dims = dict(N=nlp.N, NX=nlp.nx, NV=nlp.nv, NG=ng, NPS=nlp.nps, NPG=nlp.npg)
     ts = nlp.ts if ts is None else ts
@@ -127,9 +156,9 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         *fg_lines, "}", "",
         "__device__ __forceinline__ void gen_stage_bounds(const double* __restrict__ PS, const double* __restrict__ PG, const double TK, double* __restrict__ lb, double* __restrict__ ub, const int S) {",
         *bd_lines, "}", "",
-        f"__device__ __forceinline__ void gen_stage_gj({sig}, double* __restrict__ grad, double* __restrict__ jac, const int S) {{",
+        f"__device__ __forceinline__ void gen_stage_gj({sig}, double* __restrict__ grad, double* __restrict__ jac, const int S, const double* __restrict__ G, double* __restrict__ lp) {{",
         *gj_lines, "}", "",
-        f"__device__ __forceinline__ void gen_stage_hess({sig}, const double sigma, const double* __restrict__ lam, double* __restrict__ hess, const int S) {{",
+        f"__device__ __forceinline__ void gen_stage_hess({sig}, const double sigma, const double* __restrict__ lam, double* __restrict__ hess, const int S, double* __restrict__ lp) {{",
         *h_lines, "}", "",
         '#include "mpcx_ipm.hip"',
         "",

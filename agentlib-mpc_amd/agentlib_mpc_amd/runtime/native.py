@@ -190,7 +190,7 @@ class NativeProblem:
         self.gen = gen
         d = gen.dims
         self.desc = ProblemDesc(n_stages=d["N"], nx=d["NX"], nv=d["NV"], ng=d["NG"],
-                                nps=d["NPS"], npg=d["NPG"], abi=3, reserved=0)
+                                nps=d["NPS"], npg=d["NPG"], abi=4, reserved=0)
         path = hsaco or code_object_path(gen.key)
         if not pathlib.Path(path).exists():
             path = compile_model(gen)

@@ -9,20 +9,25 @@
 // IPOPT's (barrier + slacks, monotone mu, inertia-corrected Newton steps,
 // fraction-to-boundary, filter line search, gradient scaling, bound relaxation,
 // least-squares multiplier init) and follows the oracle restatement
-// oracle/ipm.py step for step.  What differs is the linear algebra: the KKT
-// system of a stage-structured NLP is a block-tridiagonal chain; each block
-// (stage-local primals, the state at the stage end, the stage constraint
-// multipliers) is factored in LDS by a Bunch-Kaufman LDL^T and the chain is
-// eliminated Riccati-style (Schur complement through the nx state columns).
-// Inertia = sum of the block inertias (Haynsworth), exactly what IPOPT reads
-// from MUMPS.
+// oracle/ipm.py step for step.  What differs is the linear algebra: permuted to
+// [stage interiors | states], the KKT matrix of a stage-structured NLP has a
+// block-diagonal interior part.  Every stage's interior (controls, collocation
+// states, outputs, constraint multipliers) is Bunch-Kaufman factored in LDS in
+// parallel with the other stages, bordered by the two state blocks it touches
+// and by the right-hand side; the local Schur complements on the states form a
+// block-tridiagonal chain of nx x nx pivots, the only sequential part.
+// Inertia = interior inertias + chain inertia (Haynsworth), exactly what IPOPT
+// reads from MUMPS.  A stage whose interior is singular sends the agent to the
+// sequential block chain (Riccati through the state columns) instead.
 //
-// Mapping: one agent per workgroup of one wavefront (64 lanes).  Lanes run
-// over stages for function/derivative evaluation (generated straight-line
-// code), over matrix entries for factorisation, and over variables for the
-// vector work (wave shuffles for the reductions).  Per-agent state lives in a
-// workspace slab in HBM (L2/MALL resident while the agent is active); the
-// active KKT block lives in LDS.
+// Mapping: one agent per workgroup of one wavefront (64 lanes).  Lanes own
+// variables/constraints (i = lane + 64*slot) for the vector phases, stages for
+// the generated evaluations, and lane groups of G own stages during the
+// factorisation.  The iterate lives in an HBM workspace slab; everything a
+// phase hands to lanes of another mapping goes through LDS where it fits
+// (parameters, trial point, step, factors), otherwise through the slab plus a
+// workgroup barrier.  Phases issue all their global loads before the first
+// dependent use: the kernel is latency-bound, not flop-bound.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include "mpcx.h"
@@ -41,9 +46,12 @@ constexpr int NP = NV + NX;        // primal unknowns per KKT block [V, X1]
 constexpr int NB = NP + NG;        // KKT block size
 constexpr int NW = NX + N * NP;    // NLP variables (reference order)
 constexpr int M = N * NG;          // NLP constraints
+constexpr int MM = M > 0 ? M : 1;
 constexpr int NPAR = NPG + N * NPS;
 constexpr int LDB = (NB % 2 == 0) ? NB + 1 : NB;
 constexpr int WAVE = 64;
+constexpr int VS = (NW + WAVE - 1) / WAVE;  // variable slots per lane
+constexpr int CS = (M + WAVE - 1) / WAVE;   // constraint slots per lane
 constexpr int MAXF = 32;           // filter entries kept in LDS
 constexpr double INF_BOUND = 1e19;
 constexpr double TS = MPCX_TS;
@@ -51,31 +59,49 @@ constexpr double TS = MPCX_TS;
 #define MPCX_MIN_WAVES 4
 #endif
 
+// address-space qualified pointers: global_* / ds_* addressing inside the
+// noinline phases (generic pointers compile to flat_*, which drain both
+// counters and block load/store reordering)
+typedef __attribute__((address_space(1))) double gdbl;
+typedef __attribute__((address_space(1))) int gint;
+typedef __attribute__((address_space(3))) double ldsd;
+typedef __attribute__((address_space(3))) int ldsi;
+
+// stage-local system [V_k, lambda_k | x_k, x_{k+1} | rhs]
+constexpr int NI = NV + NG;               // stage interior (eliminated in parallel)
+constexpr int NXP = NX > 0 ? NX : 1;
+constexpr int NXX = NXP * NXP;
+constexpr int NLOC = NI + 2 * NX;         // local system size
+constexpr int RB = NLOC;                  // border row holding the right-hand side
+constexpr int NTR = 2 * NX + 1;           // trailing rows: x_k, x_{k+1}, border
+constexpr int PKB = (NLOC + 1) * (NLOC + 2) / 2;  // packed lower triangle incl. border
+constexpr int PKS = PKB | 1;              // odd stride between stage slots
+static_assert(NI > 0, "stage interior must be non-empty");
+static_assert(NLOC < 64, "local fixed-variable masks are 64-bit");
+
 // workspace layout (doubles per agent)
 constexpr long O_X = 0, O_S = O_X + NW, O_LAM = O_S + M, O_ZL = O_LAM + M, O_ZU = O_ZL + NW;
 constexpr long O_VL = O_ZU + NW, O_VU = O_VL + M, O_XL = O_VU + M, O_XU = O_XL + NW;
 constexpr long O_SL = O_XU + NW, O_SU = O_SL + M, O_GS = O_SU + M, O_GV = O_GS + M;
-constexpr long O_DX = O_GV + M, O_DS = O_DX + NW, O_DL = O_DS + M, O_XT = O_DL + M;
-constexpr long O_ST = O_XT + NW, O_GT = O_ST + M, O_LB = O_GT + M, O_UB = O_LB + M;
+constexpr long O_DX = O_GV + M, O_DS = O_DX + NW, O_DL = O_DS + M, O_LB = O_DL + M, O_UB = O_LB + M;
 constexpr long O_SDG = O_UB + M;                 // [NL][N]      stage cost gradient
 constexpr long O_SDJ = O_SDG + (long)NL * N;     // [NG*NL][N]   stage jacobian
 constexpr long O_SDH = O_SDJ + (long)NG * NL * N;// [NL*NL][N]   stage hessian
-constexpr long O_FAC = O_SDH + (long)NL * NL * N;// [N][NB*LDB]  blocks, then block inverses
-constexpr long O_RHS = O_FAC + (long)N * NB * LDB;
-constexpr long O_SOL = O_RHS + (long)N * NB;
-constexpr long O_CPL = O_SOL + (long)N * NB;     // [N][NB*NX] couplings to x_k (block chain)
-constexpr long O_KX = O_CPL + (long)N * NB * (NX > 0 ? NX : 1);  // [N*NP] primal KKT diagonal
-constexpr long O_KD = O_KX + (long)N * NP;       // [M] dual KKT diagonal
-constexpr int LPK = (NV + NG + 2 * NX) * (NV + NG + 2 * NX + 1) / 2;
-constexpr long O_LF = O_KD + M;                  // [N][LPK] stage-local factors
-constexpr long O_LPV = O_LF + (long)N * LPK;     // [N][2*NI] ints (perm, piv)
-constexpr long O_LZ = O_LPV + (long)N * (NV + NG);
-constexpr long WS_DOUBLES = O_LZ + (long)N * (NV + NG);
+constexpr long O_RHS = O_SDH + (long)NL * NL * N;// [N][NB]      KKT right-hand side
+constexpr long O_TR = O_RHS + (long)N * NB;      // [N][NI][NTR] back-substitution operators
+constexpr long O_PRM = O_TR + (long)N * NI * NTR;// [N][NI] ints interior pivot order
+constexpr long O_KX = O_PRM + (long)N * NI;      // [N*NP] primal KKT diagonal   (block chain)
+constexpr long O_KD = O_KX + (long)N * NP;       // [M] dual KKT diagonal        (block chain)
+constexpr long O_SOL = O_KD + M;                 // [N][NB] solution             (block chain)
+constexpr long O_FAC = O_SOL + (long)N * NB;     // [N][NB*LDB] block inverses   (block chain)
+constexpr long O_CPL = O_FAC + (long)N * NB * LDB;  // [N][NB*NX] couplings      (block chain)
+constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [N][PKS] packed local systems (evaluators, rhs)
+constexpr long WS_DOUBLES = O_LP + (long)N * PKS;
 
 using Args = mpcx_kernel_args;
 
 // ---------------------------------------------------------------------------
-// wave helpers
+// wave and lane-group helpers
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
@@ -116,107 +142,253 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// DPP lane exchange inside aligned groups (quad_perm xor1 / xor2, half-row and
+// row mirrors): register-speed, no LDS round trip
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+template <int GG>
+__device__ __forceinline__ double gmax(double v) {
+  if constexpr (GG >= 2) v = fmax(v, dpp_f64<0xB1>(v));
+  if constexpr (GG >= 4) v = fmax(v, dpp_f64<0x4E>(v));
+  if constexpr (GG >= 8) v = fmax(v, dpp_f64<0x141>(v));
+  if constexpr (GG >= 16) v = fmax(v, dpp_f64<0x140>(v));
+  if constexpr (GG >= 32) v = fmax(v, __shfl_xor(v, 16, WAVE));
+  if constexpr (GG >= 64) v = fmax(v, __shfl_xor(v, 32, WAVE));
+  return v;
+}
+__device__ __forceinline__ void amax_merge(double& v, int& idx, double ov, int oi) {
+  if (ov > v || (ov == v && oi >= 0 && (idx < 0 || oi < idx))) { v = ov; idx = oi; }
+}
+template <int GG>
+__device__ __forceinline__ void gargmax(double& v, int& idx) {
+  if constexpr (GG >= 2) amax_merge(v, idx, dpp_f64<0xB1>(v), dpp_i32<0xB1>(idx));
+  if constexpr (GG >= 4) amax_merge(v, idx, dpp_f64<0x4E>(v), dpp_i32<0x4E>(idx));
+  if constexpr (GG >= 8) amax_merge(v, idx, dpp_f64<0x141>(v), dpp_i32<0x141>(idx));
+  if constexpr (GG >= 16) amax_merge(v, idx, dpp_f64<0x140>(v), dpp_i32<0x140>(idx));
+  if constexpr (GG >= 32) amax_merge(v, idx, __shfl_xor(v, 16, WAVE), __shfl_xor(idx, 16, WAVE));
+  if constexpr (GG >= 64) amax_merge(v, idx, __shfl_xor(v, 32, WAVE), __shfl_xor(idx, 32, WAVE));
+}
+
 __device__ __forceinline__ bool isfin(double v) { return fabs(v) < INFINITY; }
-
-// LDS-qualified pointers: keeps ds_* addressing inside the noinline phases
-// (a generic pointer would compile to flat_* accesses)
-typedef __attribute__((address_space(3))) double ldsd;
-typedef __attribute__((address_space(3))) int ldsi;
+__device__ __forceinline__ double absn(double v) {  // |v| with NaN -> +inf (total order for pivoting)
+  const double t = fabs(v);
+  return t == t ? t : INFINITY;
+}
 
 // ---------------------------------------------------------------------------
-// per-agent views
+// LDS layout
 // ---------------------------------------------------------------------------
-struct Agent {
-  double* ws;
-  const double* p;
-  int lane;
-  __device__ double* x() const { return ws + O_X; }
-  __device__ double* s() const { return ws + O_S; }
-  __device__ double* lam() const { return ws + O_LAM; }
-  __device__ double* zL() const { return ws + O_ZL; }
-  __device__ double* zU() const { return ws + O_ZU; }
-  __device__ double* vL() const { return ws + O_VL; }
-  __device__ double* vU() const { return ws + O_VU; }
-  __device__ double* xL() const { return ws + O_XL; }
-  __device__ double* xU() const { return ws + O_XU; }
-  __device__ double* sL() const { return ws + O_SL; }
-  __device__ double* sU() const { return ws + O_SU; }
-  __device__ double* gs() const { return ws + O_GS; }
-  __device__ double* gv() const { return ws + O_GV; }
-  __device__ double* dx() const { return ws + O_DX; }
-  __device__ double* ds() const { return ws + O_DS; }
-  __device__ double* dl() const { return ws + O_DL; }
-  __device__ double* xt() const { return ws + O_XT; }
-  __device__ double* st() const { return ws + O_ST; }
-  __device__ double* gt() const { return ws + O_GT; }
-  __device__ double* lb() const { return ws + O_LB; }
-  __device__ double* ub() const { return ws + O_UB; }
-  __device__ double* sdg() const { return ws + O_SDG; }
-  __device__ double* sdj() const { return ws + O_SDJ; }
-  __device__ double* sdh() const { return ws + O_SDH; }
-  __device__ double* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
-  __device__ double* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
-  __device__ double* sol(int k) const { return ws + O_SOL + (long)k * NB; }
-  __device__ double* cpl(int k) const { return ws + O_CPL + (long)k * NB * (NX > 0 ? NX : 1); }
-  __device__ double* kx() const { return ws + O_KX; }
-  __device__ double* kd() const { return ws + O_KD; }
-  __device__ double* lf(int k) const { return ws + O_LF + (long)k * LPK; }
-  __device__ int* lpv(int k) const { return reinterpret_cast<int*>(ws + O_LPV) + (long)k * 2 * (NV + NG); }
-  __device__ double* lz(int k) const { return ws + O_LZ + (long)k * (NV + NG); }
+__host__ __device__ constexpr int pow2floor(int v) { int p = 1; while (p * 2 <= v) p *= 2; return p; }
+__host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // packed system + perm/piv
+constexpr int OTHER_BYTES = 8 * (N * 3 * NXX + N * NXX + 3 * N * NXP + 3 * NXX + 2 * MAXF + NPAR + N) +
+                            8 * NXP + 64;
+#ifndef MPCX_LDS_TARGET
+#define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
+#endif
+constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / SLOT_BYTES));
+constexpr int ROUNDS = (N + SR0 - 1) / SR0;
+constexpr int SR = (N + ROUNDS - 1) / ROUNDS;   // stages per round (balanced)
+constexpr int G = pow2floor(WAVE / SR);         // lanes per stage
+
+constexpr int SQ = NX > 0 ? NB : 1;   // the block-chain fallback exists only when stages are coupled
+constexpr int SQL = NX > 0 ? LDB : 1;
+struct SeqLds {
+  double A[SQ * SQL];
+  double W[SQ * SQL];
+  double Y[SQ * SQL];
+  double B[SQ * NXP];
+  double BP[SQ * NXP];
+  double P[NXX];
+  double v[SQ];
+  double y[SQ];
+  double t[SQ];
+  int perm[SQ];
+  int piv[SQ];
+};
+struct ParLds {
+  double F[SR * PKS];
+  int perm[SR * NI];
+  int piv[SR * NI];
+};
+struct TrialLds {
+  double xt[NW];
+  double gt[MM];
+};
+union LinLds {
+  SeqLds s;
+  ParLds p;
+  double sol[N * NB];   // Newton step, block order [V, X1, lambda] per stage
+  TrialLds t;           // line-search trial point (x, scaled g)
 };
 
-__device__ __forceinline__ bool is_fixed(const Agent& a, int i) { return a.xL()[i] == a.xU()[i]; }
+struct Lds {
+  LinLds u;
+  double par[NPAR];        // agent parameters (read by every evaluation)
+  double S[N * 3 * NXX];   // local Schur blocks per stage: S00 (x_k), S11 (x_{k+1}), S10
+  double Dinv[N * NXX];    // inverses of the state-chain pivots
+  double zx[N * 2 * NXP];  // forward-eliminated rhs of (x_k, x_{k+1}) per stage
+  double xs[N * NXP];      // state-chain rhs, then solution (x_1 .. x_N)
+  double C[NXX];
+  double CW[NXX];
+  double CY[NXX];
+  unsigned long long fixm[N];  // per stage: local primal indices that are fixed variables
+  int cperm[NXP];
+  int cpiv[NXP];
+  int seq;                 // 1: last factorisation used the block chain
+  double fth[MAXF];
+  double fph[MAXF];
+#ifdef MPCX_PROFILE
+  double sprof[6];
+#endif
+};
+
+__shared__ Lds gL;  // one agent per workgroup: the agent's LDS scratch
+#define LDSP(x) ((ldsd*)(x))
+#define LDSI(x) ((ldsi*)(x))
+#ifdef MPCX_PROFILE
+#define SPROF_DECL unsigned long long _st = __builtin_amdgcn_s_memtime();
+#define SPROF(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); if (a.lane == 0) gL.sprof[i] += (double)(_n - _st); _st = _n; } while (0)
+#else
+#define SPROF_DECL
+#define SPROF(i) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
-// evaluation (lane k evaluates stage k)
+// per-agent views (by value: two global pointers and the lane)
 // ---------------------------------------------------------------------------
-// f and unscaled g at point xv; returns wave-summed f
-__device__ __noinline__ double eval_fg(const Agent& a, const double* xv, double* gout) {
+struct Agent {
+  gdbl* ws;
+  int lane;
+  __device__ gdbl* x() const { return ws + O_X; }
+  __device__ gdbl* s() const { return ws + O_S; }
+  __device__ gdbl* lam() const { return ws + O_LAM; }
+  __device__ gdbl* zL() const { return ws + O_ZL; }
+  __device__ gdbl* zU() const { return ws + O_ZU; }
+  __device__ gdbl* vL() const { return ws + O_VL; }
+  __device__ gdbl* vU() const { return ws + O_VU; }
+  __device__ gdbl* xL() const { return ws + O_XL; }
+  __device__ gdbl* xU() const { return ws + O_XU; }
+  __device__ gdbl* sL() const { return ws + O_SL; }
+  __device__ gdbl* sU() const { return ws + O_SU; }
+  __device__ gdbl* gs() const { return ws + O_GS; }
+  __device__ gdbl* gv() const { return ws + O_GV; }
+  __device__ gdbl* dx() const { return ws + O_DX; }
+  __device__ gdbl* ds() const { return ws + O_DS; }
+  __device__ gdbl* dl() const { return ws + O_DL; }
+  __device__ gdbl* lb() const { return ws + O_LB; }
+  __device__ gdbl* ub() const { return ws + O_UB; }
+  __device__ gdbl* sdg() const { return ws + O_SDG; }
+  __device__ gdbl* sdj() const { return ws + O_SDJ; }
+  __device__ gdbl* sdh() const { return ws + O_SDH; }
+  __device__ gdbl* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
+  __device__ gdbl* tr(int k) const { return ws + O_TR + (long)k * NI * NTR; }
+  __device__ gint* prm(int k) const { return reinterpret_cast<gint*>(ws + O_PRM) + (long)k * NI; }
+  __device__ gdbl* kx() const { return ws + O_KX; }
+  __device__ gdbl* kd() const { return ws + O_KD; }
+  __device__ gdbl* sol(int k) const { return ws + O_SOL + (long)k * NB; }
+  __device__ gdbl* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
+  __device__ gdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
+  __device__ gdbl* lp(int k) const { return ws + O_LP + (long)k * PKS; }
+};
+
+// constraint classes: 0 equality, 1 inequality with a finite bound, 2 free
+__device__ __forceinline__ int cls_of(double lo, double hi, double sl, double su) {
+  if (lo == hi) return 0;
+  if (!isfin(sl) && !isfin(su)) return 2;
+  return 1;
+}
+
+// ---------------------------------------------------------------------------
+// evaluation (lane k evaluates stage k; parameters from LDS)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ const double* par_stage(int k) { return (const double*)(gL.par + NPG + k * NPS); }
+__device__ __forceinline__ const double* par_global() { return (const double*)gL.par; }
+
+// f and unscaled g at the trial point in LDS (xt -> gt); returns wave-summed f
+__device__ __noinline__ double eval_fg_lds(const Agent a) {
   double f = 0.0;
   for (int k = a.lane; k < N; k += WAVE) {
     double fk = 0.0;
-    gen_stage_fg(xv + k * NP, a.p + NPG + k * NPS, a.p, k * TS, &fk, gout + k * NG, 1);
+    gen_stage_fg((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS, &fk,
+                 (double*)(gL.u.t.gt + k * NG), 1);
     f += fk;
   }
   return wsum(f);
 }
 
-__device__ __noinline__ void eval_gj(const Agent& a, const double* xv) {
+// f and unscaled g at a point in the workspace
+__device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* gout) {
+  double f = 0.0;
+  for (int k = a.lane; k < N; k += WAVE) {
+    double fk = 0.0;
+    gen_stage_fg((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, &fk, (double*)(gout + k * NG), 1);
+    f += fk;
+  }
+  return wsum(f);
+}
+
+__device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv) {
   for (int k = a.lane; k < N; k += WAVE)
-    gen_stage_gj(xv + k * NP, a.p + NPG + k * NPS, a.p, k * TS, a.sdg() + k, a.sdj() + k, N);
+    gen_stage_gj((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, (double*)(a.sdg() + k),
+                 (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG), (double*)a.lp(k));
+}
+
+// derivatives at the accepted trial point (still in LDS)
+__device__ __noinline__ void eval_gj_lds(const Agent a) {
+  for (int k = a.lane; k < N; k += WAVE)
+    gen_stage_gj((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS,
+                 (double*)(a.sdg() + k), (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG),
+                 (double*)a.lp(k));
 }
 
 // Hessian of sigma*f + sum lam_i * gs_i * g_i (scaled Lagrangian)
-__device__ __noinline__ void eval_hess(const Agent& a, const double* xv, double sigma) {
+__device__ __noinline__ void eval_hess(const Agent a, double sigma) {
   for (int k = a.lane; k < N; k += WAVE) {
     double lk[NG > 0 ? NG : 1];
 #pragma unroll
     for (int r = 0; r < NG; ++r) lk[r] = a.lam()[k * NG + r] * a.gs()[k * NG + r];
-    gen_stage_hess(xv + k * NP, a.p + NPG + k * NPS, a.p, k * TS, sigma, lk, a.sdh() + k, N);
+    gen_stage_hess((const double*)(a.x() + k * NP), par_stage(k), par_global(), k * TS, sigma, lk,
+                   (double*)(a.sdh() + k), N, (double*)a.lp(k));
   }
 }
 
-// gradient of the (unscaled) objective w.r.t. w[i], i >= NX
-__device__ __forceinline__ double acc_grad(const Agent& a, int i) {
+// gradient of the (unscaled) objective w.r.t. w[i], i >= NX (stage derivatives of
+// stage b and, for a state, the X0 part of stage b+1)
+__device__ __forceinline__ double acc_grad(const Agent a, int i) {
   const int b = (i - NX) / NP, off = (i - NX) % NP;
   double v = a.sdg()[(NX + off) * N + b];
   if (NX > 0 && off >= NV && b + 1 < N) v += a.sdg()[(off - NV) * N + b + 1];
   return v;
 }
-// (J~^T lam~)[i] with J~ = gs*J
-__device__ __forceinline__ double acc_jtl(const Agent& a, int i, const double* lamv) {
+// (J~^T lam)[i] with J~ = gs*J
+__device__ __forceinline__ double acc_jtl(const Agent a, int i, const gdbl* lamv) {
   const int b = (i - NX) / NP, off = (i - NX) % NP;
   double v = 0.0;
+#pragma unroll
   for (int r = 0; r < NG; ++r)
     v += a.sdj()[(r * NL + NX + off) * N + b] * a.gs()[b * NG + r] * lamv[b * NG + r];
-  if (NX > 0 && off >= NV && b + 1 < N)
+  if (NX > 0 && off >= NV && b + 1 < N) {
+#pragma unroll
     for (int r = 0; r < NG; ++r)
       v += a.sdj()[(r * NL + off - NV) * N + b + 1] * a.gs()[(b + 1) * NG + r] * lamv[(b + 1) * NG + r];
+  }
   return v;
 }
 
 // ---------------------------------------------------------------------------
-// dense Bunch-Kaufman LDL^T in LDS (full symmetric storage, wave-wide)
+// dense Bunch-Kaufman LDL^T in LDS (full symmetric storage, wave-wide):
+// block-chain fallback and the nx x nx state-chain pivots
 // ---------------------------------------------------------------------------
 struct Inertia {
   int pos, neg, zero;
@@ -229,8 +401,9 @@ constexpr double ZERO_PIVOT = 1e-20;
 constexpr double BK_ALPHA = 0.6403882032022076;  // (1 + sqrt(17)) / 8
 
 template <int NN, int LD>
-__device__ __noinline__ void bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int lane, Inertia& in) {
+__device__ __noinline__ Inertia bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int lane) {
   constexpr int NN2 = NN * NN;
+  Inertia in{0, 0, 0};
   for (int i = lane; i < NN; i += WAVE) perm[i] = i;
   wsync();
   int k = 0;
@@ -319,13 +492,14 @@ __device__ __noinline__ void bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int lane,
     wsync();
     k += size;
   }
+  return in;
 }
 
 // Explicit inverse of a factored block, A^{-1} = P^T L^{-T} D^{-1} L^{-1} P,
 // written in the ORIGINAL index order to `out` (ld LD).  W, Y: LDS scratch.
-template <int NN, int LD>
+template <int NN, int LD, typename OutT>
 __device__ __noinline__ void bk_inverse(const ldsd* A, const ldsi* perm, const ldsi* piv, ldsd* W,
-                                        ldsd* Y, double* out, int lane) {
+                                        ldsd* Y, OutT* out, int lane) {
   constexpr int NN2 = NN * NN;
   for (int t = lane; t < NN2; t += WAVE) {
     const int i = t / NN, j = t % NN;
@@ -382,141 +556,52 @@ struct KKTDiag {
   Mode mode;
 };
 
-__device__ __forceinline__ double sigma_x(const Agent& a, int i) {
-  const double xv = a.x()[i], lo = a.xL()[i], hi = a.xU()[i];
-  double s = 0.0;
+__device__ __forceinline__ double sigma_x_v(double xv, double lo, double hi, double zl, double zu) {
   if (lo == hi) return 0.0;
-  if (isfin(lo)) s += a.zL()[i] / (xv - lo);
-  if (isfin(hi)) s += a.zU()[i] / (hi - xv);
-  return s;
-}
-__device__ __forceinline__ double sigma_s(const Agent& a, int c) {
-  const double sv = a.s()[c], lo = a.sL()[c], hi = a.sU()[c];
   double s = 0.0;
-  if (isfin(lo)) s += a.vL()[c] / (sv - lo);
-  if (isfin(hi)) s += a.vU()[c] / (hi - sv);
+  if (isfin(lo)) s += zl / (xv - lo);
+  if (isfin(hi)) s += zu / (hi - xv);
   return s;
 }
-// constraint classes: 0 equality, 1 inequality with a finite bound, 2 free
-__device__ __forceinline__ int ccls(const Agent& a, int c) {
-  const double lo = a.lb()[c], hi = a.ub()[c];
-  if (lo == hi) return 0;
-  if (!isfin(a.sL()[c]) && !isfin(a.sU()[c])) return 2;
-  return 1;
+__device__ __forceinline__ double sigma_s_v(double sv, double sl, double su, double vl, double vu) {
+  double s = 0.0;
+  if (isfin(sl)) s += vl / (sv - sl);
+  if (isfin(su)) s += vu / (su - sv);
+  return s;
 }
-__device__ __forceinline__ double dual_diag(const Agent& a, int c, const KKTDiag& kd) {
-  const int cl = ccls(a, c);
+__device__ __forceinline__ double dual_diag_v(int cl, double sig, const KKTDiag kd) {
   if (kd.mode == LSQ) return cl == 0 ? 0.0 : 1.0;
   if (cl == 0) return kd.dc;
   if (cl == 2) return 1.0;
-  return 1.0 / (sigma_s(a, c) + kd.dw) + kd.dc;
-}
-
-// ---------------------------------------------------------------------------
-// LDS layout
-// ---------------------------------------------------------------------------
-// Stage-parallel path: stage k's local system, ordered [V_k, lambda_k | x_k, x_{k+1}],
-// is held packed-lower in LDS; SR stages are resident per round, G lanes per stage.
-constexpr int NI = NV + NG;               // stage interior (eliminated in parallel)
-constexpr int NXP = NX > 0 ? NX : 1;
-constexpr int NXX = NXP * NXP;
-constexpr int NLOC = NI + 2 * NX;         // local system size
-constexpr int PK = NLOC * (NLOC + 1) / 2; // packed lower triangle
-constexpr int PKS = PK | 1;               // odd stride between stage slots
-static_assert(NI > 0, "stage interior must be non-empty");
-
-__host__ __device__ constexpr int pow2floor(int v) { int p = 1; while (p * 2 <= v) p *= 2; return p; }
-__host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
-__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
-
-constexpr int SLOT_BYTES = 8 * (PKS + NLOC) + 8 * NI;  // F + z + perm/piv
-constexpr int OTHER_BYTES = 8 * (N * 3 * NXX + N * NXX + 3 * N * NXP + 3 * NXX + 2 * MAXF) + 8 * NXP + 64;
-#ifndef MPCX_LDS_TARGET
-#define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
-#endif
-constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / SLOT_BYTES));
-constexpr int ROUNDS = (N + SR0 - 1) / SR0;
-constexpr int SR = (N + ROUNDS - 1) / ROUNDS;   // stages per round (balanced)
-constexpr int G = pow2floor(WAVE / SR);         // lanes per stage
-
-constexpr int SQ = NX > 0 ? NB : 1;   // the fallback exists only when stages are coupled
-constexpr int SQL = NX > 0 ? LDB : 1;
-struct SeqLds {               // sequential block chain (fallback)
-  double A[SQ * SQL];
-  double W[SQ * SQL];
-  double Y[SQ * SQL];
-  double B[SQ * NXP];
-  double BP[SQ * NXP];
-  double P[NXX];
-  double v[SQ];
-  double y[SQ];
-  double t[SQ];
-  int perm[SQ];
-  int piv[SQ];
-};
-struct ParLds {
-  double F[SR * PKS];
-  double z[SR * NLOC];
-  int perm[SR * NI];
-  int piv[SR * NI];
-};
-union LinLds {
-  SeqLds s;
-  ParLds p;
-};
-
-struct Lds {
-  LinLds u;
-  double S[N * 3 * NXX];   // local Schur blocks per stage: S00 (x_k), S11 (x_{k+1}), S10
-  double Dinv[N * NXX];    // inverses of the state-chain pivots
-  double zx0[N * NXP];     // forward-eliminated local rhs, x_k part
-  double zx1[N * NXP];     // ... x_{k+1} part
-  double xs[N * NXP];      // state-chain rhs, then solution (x_1 .. x_N)
-  double C[NXX];
-  double CW[NXX];
-  double CY[NXX];
-  int cperm[NXP];
-  int cpiv[NXP];
-  int seq;                 // 1: last factorisation used the sequential chain
-  double fth[MAXF];
-  double fph[MAXF];
-#ifdef MPCX_PROFILE
-  double sprof[6];
-#endif
-};
-
-__shared__ Lds gL;
-#ifdef MPCX_PROFILE
-#define SPROF_DECL unsigned long long _st = __builtin_amdgcn_s_memtime();
-#define SPROF(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); if (a.lane == 0) gL.sprof[i] += (double)(_n - _st); _st = _n; } while (0)
-#else
-#define SPROF_DECL
-#define SPROF(i) do { } while (0)
-#endif  // one agent per workgroup: the agent's LDS scratch
-#define LDSP(x) ((ldsd*)(x))
-#define LDSI(x) ((ldsi*)(x))
-
-// per-variable / per-constraint diagonal terms of the KKT matrix, once per factorisation
-// (workspace: NaN in kx marks a fixed variable)
-__device__ __noinline__ void kkt_diagonals(const Agent& a, const KKTDiag& kd) {
-  for (int q = a.lane; q < N * NP; q += WAVE) {
-    const int i = NX + q;
-    a.kx()[q] = is_fixed(a, i) ? NAN : (kd.mode == LSQ ? 1.0 : sigma_x(a, i) + kd.dw);
-  }
-  for (int c = a.lane; c < M; c += WAVE) a.kd()[c] = dual_diag(a, c, kd);
-  sync();
-}
-
-__device__ __forceinline__ bool kfixed(const Agent& a, int k, int q) {
-  const double v = a.kx()[k * NP + q];
-  return v != v;
+  return 1.0 / (sig + kd.dw) + kd.dc;
 }
 
 // ---------------------------------------------------------------------------
 // sequential block chain (fallback when a stage interior is singular)
 // ---------------------------------------------------------------------------
+// per-variable / per-constraint diagonal terms (workspace; NaN in kx marks a fixed variable)
+__device__ __noinline__ void kkt_diagonals(const Agent a, const KKTDiag kd) {
+  for (int q = a.lane; q < N * NP; q += WAVE) {
+    const int i = NX + q;
+    const double lo = a.xL()[i], hi = a.xU()[i];
+    a.kx()[q] = (lo == hi) ? NAN
+                           : (kd.mode == LSQ ? 1.0 : sigma_x_v(a.x()[i], lo, hi, a.zL()[i], a.zU()[i]) + kd.dw);
+  }
+  for (int c = a.lane; c < M; c += WAVE) {
+    const double sl = a.sL()[c], su = a.sU()[c];
+    const int cl = cls_of(a.lb()[c], a.ub()[c], sl, su);
+    a.kd()[c] = dual_diag_v(cl, sigma_s_v(a.s()[c], sl, su, a.vL()[c], a.vU()[c]), kd);
+  }
+  sync();
+}
+
+__device__ __forceinline__ bool kfixed(const Agent a, int k, int q) {
+  const double v = a.kx()[k * NP + q];
+  return v != v;
+}
+
 // entry (i, j) of KKT block k = [V_k, X_{k+1}, lambda_k] (before the Schur update)
-__device__ __forceinline__ double kkt_entry(const Agent& a, int k, int i, int j, Mode mode) {
+__device__ __forceinline__ double kkt_entry(const Agent a, int k, int i, int j, Mode mode) {
   if (i < NP && j < NP) {
     if (kfixed(a, k, i) || kfixed(a, k, j)) return (i == j) ? 1.0 : 0.0;
     if (mode == LSQ) return (i == j) ? 1.0 : 0.0;
@@ -533,7 +618,7 @@ __device__ __forceinline__ double kkt_entry(const Agent& a, int k, int i, int j,
 }
 
 // coupling of block k (row) to x_k = X0 of stage k (column c < NX)
-__device__ __forceinline__ double coupling(const Agent& a, int k, int row, int c, Mode mode) {
+__device__ __forceinline__ double coupling(const Agent a, int k, int row, int c, Mode mode) {
   if (k == 0 || kfixed(a, k - 1, NV + c)) return 0.0;
   if (row < NP) {
     if (mode == LSQ || kfixed(a, k, row)) return 0.0;
@@ -546,14 +631,12 @@ __device__ __forceinline__ double coupling(const Agent& a, int k, int row, int c
 constexpr int NB2 = NB * NB;
 constexpr int EPL = (NB2 + WAVE - 1) / WAVE;  // block elements per lane
 
-__device__ __noinline__ void seq_assemble(const Agent& a, Mode mode) {
-#pragma unroll 4
+__device__ __noinline__ void seq_assemble(const Agent a, Mode mode) {
   for (int t = a.lane; t < N * NB2; t += WAVE) {
     const int k = t / NB2, e = t % NB2, i = e / NB, j = e % NB;
     a.fac(k)[i * LDB + j] = kkt_entry(a, k, i, j, mode);
   }
   if (NX > 0) {
-#pragma unroll 4
     for (int t = a.lane; t < N * NB * NX; t += WAVE) {
       const int k = t / (NB * NX), e = t % (NB * NX);
       a.cpl(k)[e] = coupling(a, k, e / NX, e % NX, mode);
@@ -564,88 +647,92 @@ __device__ __noinline__ void seq_assemble(const Agent& a, Mode mode) {
 
 // Block LDL^T through the state columns: D_k = A_k - B_k [D_{k-1}^{-1}]_{xx} B_k^T;
 // each block's explicit inverse is stored (solves become mat-vecs).
-__device__ __noinline__ Inertia seq_factor(const Agent& a, Mode mode) {
-  SeqLds& L = gL.u.s;
-  if constexpr (NX == 0) return Inertia{0, 0, 1};
-  const int lane = a.lane;
-  Inertia in{0, 0, 0};
-  seq_assemble(a, mode);
-  double pre[EPL];
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) {
-    const int t = lane + e * WAVE;
-    pre[e] = (t < NB2) ? a.fac(0)[(t / NB) * LDB + t % NB] : 0.0;
-  }
-#pragma unroll 1
-  for (int k = 0; k < N; ++k) {
+__device__ __noinline__ Inertia seq_factor(const Agent a, const KKTDiag kd) {
+  if constexpr (NX == 0) {
+    return Inertia{0, 0, 1};
+  } else {
+    SeqLds& L = gL.u.s;
+    const int lane = a.lane;
+    Inertia in{0, 0, 0};
+    kkt_diagonals(a, kd);
+    seq_assemble(a, kd.mode);
+    double pre[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       const int t = lane + e * WAVE;
-      if (t < NB2) L.A[(t / NB) * LDB + t % NB] = pre[e];
+      pre[e] = (t < NB2) ? a.fac(0)[(t / NB) * LDB + t % NB] : 0.0;
     }
-    if (NX > 0 && k > 0)
-      for (int t = lane; t < NB * NX; t += WAVE) L.B[t] = a.cpl(k)[t];
-    sync();
-    if (k + 1 < N) {  // prefetch block k+1 (consumed at the top of the next step)
+#pragma unroll 1
+    for (int k = 0; k < N; ++k) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
         const int t = lane + e * WAVE;
-        pre[e] = (t < NB2) ? a.fac(k + 1)[(t / NB) * LDB + t % NB] : 0.0;
+        if (t < NB2) L.A[(t / NB) * LDB + t % NB] = pre[e];
       }
+      if (k > 0)
+        for (int t = lane; t < NB * NX; t += WAVE) L.B[t] = a.cpl(k)[t];
+      sync();
+      if (k + 1 < N) {  // prefetch block k+1 (consumed at the top of the next step)
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const int t = lane + e * WAVE;
+          pre[e] = (t < NB2) ? a.fac(k + 1)[(t / NB) * LDB + t % NB] : 0.0;
+        }
+      }
+      if (k > 0) {
+        for (int t = lane; t < NB * NX; t += WAVE) {
+          const int i = t / NX, d = t % NX;
+          double s = 0.0;
+          for (int c = 0; c < NX; ++c) s += L.B[i * NX + c] * L.P[c * NX + d];
+          L.BP[t] = s;
+        }
+        wsync();
+        for (int t = lane; t < NB2; t += WAVE) {
+          const int i = t / NB, j = t % NB;
+          double s = 0.0;
+          for (int d = 0; d < NX; ++d) s += L.BP[i * NX + d] * L.B[j * NX + d];
+          L.A[i * LDB + j] -= s;
+        }
+        wsync();
+      }
+      const Inertia bi = bk_factor<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), lane);
+      in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
+      bk_inverse<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), LDSP(L.W), LDSP(L.Y), a.fac(k), lane);
+      sync();
+      if (k + 1 < N)
+        for (int t = lane; t < NX * NX; t += WAVE)
+          L.P[t] = a.fac(k)[(NV + t / NX) * LDB + NV + t % NX];
+      sync();
     }
-    if (NX > 0 && k > 0) {
-      for (int t = lane; t < NB * NX; t += WAVE) {
-        const int i = t / NX, d = t % NX;
-        double s = 0.0;
-        for (int c = 0; c < NX; ++c) s += L.B[i * NX + c] * L.P[c * NX + d];
-        L.BP[t] = s;
-      }
-      wsync();
-      for (int t = lane; t < NB2; t += WAVE) {
-        const int i = t / NB, j = t % NB;
-        double s = 0.0;
-        for (int d = 0; d < NX; ++d) s += L.BP[i * NX + d] * L.B[j * NX + d];
-        L.A[i * LDB + j] -= s;
-      }
-      wsync();
-    }
-    bk_factor<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), lane, in);
-    bk_inverse<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), LDSP(L.W), LDSP(L.Y), a.fac(k), lane);
-    sync();
-    if (NX > 0 && k + 1 < N)
-      for (int t = lane; t < NX * NX; t += WAVE)
-        L.P[t] = a.fac(k)[(NV + t / NX) * LDB + NV + t % NX];
-    sync();
+    return in;
   }
-  return in;
 }
 
-__device__ __noinline__ void seq_solve(const Agent& a) {
-  SeqLds& L = gL.u.s;
-  if constexpr (NX == 0) return;
-  const int lane = a.lane;
+// block-chain solve: rhs a.rhs(k) -> gL.u.sol
+__device__ __noinline__ void seq_solve(const Agent a) {
+  if constexpr (NX > 0) {
+    SeqLds& L = gL.u.s;
+    const int lane = a.lane;
 #pragma unroll 1
-  for (int k = 0; k < N; ++k) {
-    for (int i = lane; i < NB; i += WAVE) {
-      double v = a.rhs(k)[i];
-      if (NX > 0 && k > 0)
-        for (int c = 0; c < NX; ++c) v -= a.cpl(k)[i * NX + c] * L.y[NV + c];
-      L.v[i] = v;
+    for (int k = 0; k < N; ++k) {
+      for (int i = lane; i < NB; i += WAVE) {
+        double v = a.rhs(k)[i];
+        if (k > 0)
+          for (int c = 0; c < NX; ++c) v -= a.cpl(k)[i * NX + c] * L.y[NV + c];
+        L.v[i] = v;
+      }
+      wsync();
+      const gdbl* Ai = a.fac(k);
+      for (int i = lane; i < NB; i += WAVE) {
+        double acc = 0.0;
+        for (int j = 0; j < NB; ++j) acc += Ai[i * LDB + j] * L.v[j];
+        a.sol(k)[i] = acc;
+        L.t[i] = acc;
+      }
+      wsync();
+      for (int i = lane; i < NB; i += WAVE) L.y[i] = L.t[i];
+      wsync();
     }
-    wsync();
-    const double* Ai = a.fac(k);
-    for (int i = lane; i < NB; i += WAVE) {
-      double acc = 0.0;
-#pragma unroll 8
-      for (int j = 0; j < NB; ++j) acc += Ai[i * LDB + j] * L.v[j];
-      a.sol(k)[i] = acc;
-      L.t[i] = acc;
-    }
-    wsync();
-    for (int i = lane; i < NB; i += WAVE) L.y[i] = L.t[i];
-    wsync();
-  }
-  if (NX > 0) {
 #pragma unroll 1
     for (int k = N - 2; k >= 0; --k) {
       for (int c = lane; c < NX; c += WAVE) {
@@ -654,7 +741,7 @@ __device__ __noinline__ void seq_solve(const Agent& a) {
         L.t[c] = s;
       }
       wsync();
-      const double* Ai = a.fac(k);
+      const gdbl* Ai = a.fac(k);
       for (int i = lane; i < NB; i += WAVE) {
         double u = a.sol(k)[i];
         for (int c = 0; c < NX; ++c) u -= Ai[i * LDB + NV + c] * L.t[c];
@@ -665,93 +752,177 @@ __device__ __noinline__ void seq_solve(const Agent& a) {
       for (int i = lane; i < NB; i += WAVE) L.y[i] = L.v[i];
       wsync();
     }
+    sync();  // block-chain scratch is dead; sol(.) visible to every lane
+    for (int t = lane; t < N * NB; t += WAVE) gL.u.sol[t] = a.sol(t / NB)[t % NB];
+    wsync();
   }
-  sync();
 }
 
 // ---------------------------------------------------------------------------
 // stage-parallel elimination (default path)
 // ---------------------------------------------------------------------------
 // The KKT matrix, permuted to [all stage interiors | all states], has a block-
-// diagonal interior part.  Every stage's interior is Bunch-Kaufman factored in
-// parallel (G lanes per stage) with the two state blocks it touches appended as
-// trailing rows, which leaves the stage's local Schur complement on (x_k, x_{k+1})
-// in those rows.  The states then form a block-tridiagonal chain of nx x nx
-// pivots: the only sequential part.  Inertia = sum of interior and chain
-// inertias (Haynsworth).  A singular interior falls back to the block chain.
-
+// diagonal interior part.  Each stage's interior is Bunch-Kaufman factored by
+// G lanes with the two state blocks it touches and the right-hand side appended
+// as trailing rows: the elimination leaves the local Schur complement on
+// (x_k, x_{k+1}) and the forward-eliminated rhs in those rows.  A backward sweep
+// over the trailing rows then yields u0 = A_II^{-1} r_I and Z = A_II^{-1} A_IX,
+// so the final solve is u = u0 - Z x: one parallel pass.  The states form a
+// block-tridiagonal chain of nx x nx pivots (the only sequential part).
 __device__ __forceinline__ int pko(int i) { return (i * (i + 1)) >> 1; }
 
-__device__ __forceinline__ double gmax(double v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, WAVE));
-  return v;
-}
-__device__ __forceinline__ void gargmax(double& v, int& idx) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) {
-    const double ov = __shfl_xor(v, o, WAVE);
-    const int oi = __shfl_xor(idx, o, WAVE);
-    if (ov > v || (ov == v && oi >= 0 && (idx < 0 || oi < idx))) { v = ov; idx = oi; }
-  }
-}
-
-// local index -> (kind, index in the stage vector [X0, V, X1] of length NL)
-// kinds: 0 primal V, 1 dual, 2 x_k, 3 x_{k+1}
+// local index kinds: 0 primal V, 1 dual, 2 x_k, 3 x_{k+1}, 4 border (rhs)
 __device__ __forceinline__ int lkind(int i) {
-  return i < NV ? 0 : (i < NI ? 1 : (i < NI + NX ? 2 : 3));
+  return i < NV ? 0 : (i < NI ? 1 : (i < NI + NX ? 2 : (i < NLOC ? 3 : 4)));
+}
+// index into the stage vector [X0, V, X1] of a primal local index
+__device__ __forceinline__ int lnl(int i, int kind) {
+  return kind == 0 ? NX + i : (kind == 2 ? i - NI : NX + NV + (i - NI - NX));
+}
+// NLP variable index of a primal local index of stage k
+__device__ __forceinline__ int lvar(int k, int i, int kind) {
+  if (kind == 0) return NX + k * NP + i;
+  if (kind == 3) return NX + k * NP + NV + (i - NI - NX);
+  return k == 0 ? (i - NI) : NX + (k - 1) * NP + NV + (i - NI);  // x_k
+}
+// block-order index ([V, X1, lambda]) of a local index of kind 0, 1, 3
+__device__ __forceinline__ int lblk(int i, int kind) {
+  return kind == 0 ? i : (kind == 1 ? NP + i - NV : NV + (i - NI - NX));
 }
 
-// entry (i >= j) of stage k's local system
-__device__ __forceinline__ double local_entry(const Agent& a, int k, int i, int j, Mode mode) {
-  const int ki = lkind(i), kj = lkind(j);
-  if (ki == 1 && kj == 1) return (i == j) ? -a.kd()[k * NG + i - NV] : 0.0;
-  if (ki == 1 || kj == 1) {
-    const int r = (ki == 1 ? i : j) - NV;
-    const int q = (ki == 1 ? j : i);
-    const int kq = (ki == 1 ? kj : ki);
-    int nl;
-    if (kq == 0) { if (kfixed(a, k, q)) return 0.0; nl = NX + q; }
-    else if (kq == 2) { if (k == 0 || kfixed(a, k - 1, NV + q - NI)) return 0.0; nl = q - NI; }
-    else { if (kfixed(a, k, NV + q - NI - NX)) return 0.0; nl = NX + NV + (q - NI - NX); }
-    return a.gs()[k * NG + r] * a.sdj()[(r * NL + nl) * N + k];
+// assemble stage k's bordered local system into F (packed lower), G lanes: generic
+// gather from the strided derivative arrays (least-squares multiplier system)
+__device__ __noinline__ void local_assemble_generic(const Agent a, int k, int g, ldsd* F, const KKTDiag kd) {
+  const unsigned long long fm = gL.fixm[k];
+  const gdbl* ws = a.ws;
+  // pass 1: derivative / rhs entries (one or two independent loads per entry)
+#pragma unroll 4
+  for (int t = g; t < PKB; t += G) {
+    int i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+    if (pko(i + 1) <= t) ++i;
+    if (pko(i) > t) --i;
+    const int j = t - pko(i);
+    const int ki = lkind(i), kj = lkind(j);
+    const bool pi = (ki == 0 || ki == 2 || ki == 3), pj = (kj == 0 || kj == 2 || kj == 3);
+    const bool fi = pi && ((fm >> i) & 1ull), fj = pj && ((fm >> j) & 1ull);
+    const bool pp = pi && pj;
+    const bool dp = (ki == 1 && pj) || (kj == 1 && pi);
+    const bool bd = (ki == 4) && (kj == 0 || kj == 1 || kj == 3);
+    long off = 0, goff = O_GS;
+    if (pp) {
+      off = O_SDH + ((long)lnl(i, ki) * NL + lnl(j, kj)) * N + k;
+    } else if (dp) {
+      const int r = (ki == 1 ? i : j) - NV, q = (ki == 1 ? j : i), kq = (ki == 1 ? kj : ki);
+      off = O_SDJ + ((long)r * NL + lnl(q, kq)) * N + k;
+      goff = O_GS + k * NG + r;
+    } else if (bd) {
+      off = O_RHS + (long)k * NB + lblk(j, kj);
+    }
+    const double d = ws[off];
+    const double gsv = ws[goff];
+    double v = 0.0;
+    if (pp) v = (fi || fj) ? ((i == j && ki == 0) ? 1.0 : 0.0) : (kd.mode == LSQ ? 0.0 : d);
+    else if (dp) v = (fi || fj) ? 0.0 : gsv * d;
+    else if (bd) v = d;
+    F[t] = v;
   }
-  // primal-primal
-  int nli, nlj;
-  bool fi, fj;
-  if (ki == 0) { fi = kfixed(a, k, i); nli = NX + i; }
-  else if (ki == 2) { fi = (k == 0) || kfixed(a, k - 1, NV + i - NI); nli = i - NI; }
-  else { fi = kfixed(a, k, NV + i - NI - NX); nli = NX + NV + (i - NI - NX); }
-  if (kj == 0) { fj = kfixed(a, k, j); nlj = NX + j; }
-  else if (kj == 2) { fj = (k == 0) || kfixed(a, k - 1, NV + j - NI); nlj = j - NI; }
-  else { fj = kfixed(a, k, NV + j - NI - NX); nlj = NX + NV + (j - NI - NX); }
-  if (fi || fj) return (i == j && ki == 0) ? 1.0 : 0.0;   // fixed states: chain pivot 1
-  if (mode == LSQ) return (i == j && ki != 2) ? 1.0 : 0.0;
-  double v = a.sdh()[(nli * NL + nlj) * N + k];
-  if (i == j && ki == 0) v += a.kx()[k * NP + i];
-  if (i == j && ki == 3) v += a.kx()[k * NP + NV + (i - NI - NX)];
-  return v;
+  wsync();
+  // pass 2: diagonal terms (barrier Sigma + delta_w, dual diagonal)
+  for (int i = g; i < NLOC; i += G) {
+    const int ki = lkind(i);
+    const bool prim = (ki == 0 || ki == 3);
+    const bool fixd = (fm >> i) & 1ull;
+    const int vi = prim ? lvar(k, i, ki) : 0;
+    const int c = (ki == 1) ? k * NG + i - NV : 0;
+    const double xv = ws[O_X + vi], lo = ws[O_XL + vi], hi = ws[O_XU + vi];
+    const double zl = ws[O_ZL + vi], zu = ws[O_ZU + vi];
+    const double lbv = ws[O_LB + c], ubv = ws[O_UB + c], sv = ws[O_S + c];
+    const double sl = ws[O_SL + c], su = ws[O_SU + c], vl = ws[O_VL + c], vu = ws[O_VU + c];
+    const int ii = pko(i) + i;
+    if (prim && !fixd) F[ii] += (kd.mode == LSQ) ? 1.0 : sigma_x_v(xv, lo, hi, zl, zu) + kd.dw;
+    if (ki == 1) F[ii] = -dual_diag_v(cls_of(lbv, ubv, sl, su), sigma_s_v(sv, sl, su, vl, vu), kd);
+  }
+  wsync();
+}
+
+// diagonal terms (barrier Sigma + delta_w, dual diagonal) and fixed variables
+__device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd* F, const KKTDiag kd,
+                                               unsigned long long fm) {
+  const gdbl* ws = a.ws;
+  for (int i = g; i < NLOC; i += G) {
+    const int ki = lkind(i);
+    const bool prim = (ki == 0 || ki == 3);
+    const bool fixd = (fm >> i) & 1ull;
+    const int vi = prim ? lvar(k, i, ki) : 0;
+    const int c = (ki == 1) ? k * NG + i - NV : 0;
+    const double xv = ws[O_X + vi], lo = ws[O_XL + vi], hi = ws[O_XU + vi];
+    const double zl = ws[O_ZL + vi], zu = ws[O_ZU + vi];
+    const double lbv = ws[O_LB + c], ubv = ws[O_UB + c], sv = ws[O_S + c];
+    const double sl = ws[O_SL + c], su = ws[O_SU + c], vl = ws[O_VL + c], vu = ws[O_VU + c];
+    const int ii = pko(i) + i;
+    if (prim && !fixd) F[ii] += (kd.mode == LSQ) ? 1.0 : sigma_x_v(xv, lo, hi, zl, zu) + kd.dw;
+    if (ki == 1) F[ii] = -dual_diag_v(cls_of(lbv, ubv, sl, su), sigma_s_v(sv, sl, su, vl, vu), kd);
+  }
+  wsync();
+}
+
+// Newton system of stage k: contiguous copy of the packed image the evaluators
+// and the rhs phases wrote, then fixed variables and diagonal terms
+constexpr int EPG = (PKB + G - 1) / G;  // packed entries per lane
+__device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F, const KKTDiag kd) {
+  const unsigned long long fm = gL.fixm[k];
+  const gdbl* src = a.lp(k);
+  double v[EPG];
+#pragma unroll
+  for (int e = 0; e < EPG; ++e) {
+    const int t = g + e * G;
+    v[e] = src[t < PKB ? t : 0];
+  }
+#pragma unroll
+  for (int e = 0; e < EPG; ++e) {
+    const int t = g + e * G;
+    if (t < PKB) F[t] = v[e];
+  }
+  wsync();
+  if (fm != 0ull) {  // fixed variables: identity row (V) or empty row (states, chained as 1)
+#pragma unroll 1
+    for (int q = 0; q < NLOC; ++q) {
+      if (!((fm >> q) & 1ull)) continue;
+      for (int j = g; j <= RB; j += G) {
+        if (j == q) F[pko(q) + q] = (lkind(q) == 0) ? 1.0 : 0.0;
+        else if (j < q) F[pko(q) + j] = 0.0;
+        else F[pko(j) + q] = 0.0;
+      }
+      wsync();
+    }
+  }
+  local_diagonal(a, k, g, F, kd, fm);
 }
 
 // Bunch-Kaufman over the NI interior pivots of one stage (G lanes, packed lower
-// storage); the trailing 2*NX rows receive the updates but never pivot.
-// Sets bad on a zero pivot (singular interior).
-__device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, Inertia& in, int& bad) {
+// storage); the trailing 2*NX state rows and the border row receive the updates
+// but never pivot.  bad: singular interior (zero pivot) with coupled stages.
+struct BKOut {
+  int pos, neg, zero, bad;
+};
+__device__ __noinline__ BKOut interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g) {
+  Inertia in{0, 0, 0};
+  int bad = 0;
   int k = 0;
 #pragma unroll 1
   while (k < NI) {
-    const double akk = fabs(F[pko(k) + k]);
+    double akk = absn(F[pko(k) + k]);
     double lam = -1.0;
     int r = -1;
     for (int i = k + 1 + g; i < NI; i += G) {
-      const double t = fabs(F[pko(i) + k]);
+      const double t = absn(F[pko(i) + k]);
       if (t > lam) { lam = t; r = i; }
     }
-    gargmax(lam, r);
+    gargmax<G>(lam, r);
     if (r < 0) lam = 0.0;
     if (fmax(akk, lam) == 0.0) {
       if constexpr (NX > 0) { bad = 1; break; }
-      in.zero++;  // independent stages: the zero column is a zero eigenvalue
+      in.zero++;  // independent stages: a zero column is a zero eigenvalue
       if (g == 0) piv[k] = 1;
       wsync();
       k += 1;
@@ -761,11 +932,11 @@ __device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, 
     if (akk < BK_ALPHA * lam) {
       double sg = 0.0;
       for (int j = k + g; j < NI; j += G)
-        if (j != r) sg = fmax(sg, fabs(F[j < r ? pko(r) + j : pko(j) + r]));
-      const double sigma = gmax(sg);
+        if (j != r) sg = fmax(sg, absn(F[j < r ? pko(r) + j : pko(j) + r]));
+      const double sigma = gmax<G>(sg);
       if (akk * sigma >= BK_ALPHA * lam * lam) {
         kp = k;
-      } else if (fabs(F[pko(r) + r]) >= BK_ALPHA * sigma) {
+      } else if (absn(F[pko(r) + r]) >= BK_ALPHA * sigma) {
         kp = r;
       } else {
         size = 2; kp = r;
@@ -774,7 +945,7 @@ __device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, 
     const int p = k + size - 1, q = kp;
     if (q != p) {  // symmetric interchange p <-> q (p < q < NI) in packed storage
       const int op = pko(p), oq = pko(q);
-      for (int j = g; j < NLOC; j += G) {
+      for (int j = g; j <= RB; j += G) {
         if (j == p) {
           const double t = F[op + p]; F[op + p] = F[oq + q]; F[oq + q] = t;
         } else if (j < p) {
@@ -801,7 +972,7 @@ __device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, 
         in.neg++;
       }
       const double rd = 1.0 / d;
-      const int m = NLOC - 1 - k;  // rows k+1 .. NLOC-1, paired for balance
+      const int m = RB - k;  // rows k+1 .. RB, paired (short with long) for balance
       for (int base = 0; base < m; base += 2 * G) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -809,13 +980,23 @@ __device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, 
           if (o < m) {
             const int i = k + 1 + o, ri = pko(i);
             const double lik = F[ri + k] * rd;
-            int pj = pko(k + 1);
-            for (int j = k + 1; j <= i; ++j) { F[ri + j] -= lik * F[pj + k]; pj += j + 1; }
+            for (int j0 = k + 1; j0 <= i; j0 += 4) {
+              double av[4], bv[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int j = (j0 + u <= i) ? j0 + u : i;
+                av[u] = F[ri + j];
+                bv[u] = F[pko(j) + k];
+              }
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (j0 + u <= i) F[ri + j0 + u] = av[u] - lik * bv[u];
+            }
           }
         }
       }
       wsync();
-      for (int i = k + 1 + g; i < NLOC; i += G) F[pko(i) + k] *= rd;
+      for (int i = k + 1 + g; i <= RB; i += G) F[pko(i) + k] *= rd;
       if (g == 0) piv[k] = 1;
     } else {
       const int ok = pko(k), ok1 = pko(k + 1);
@@ -832,7 +1013,7 @@ __device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, 
         in.neg += 2;
       }
       const double rdet = 1.0 / det;
-      const int m = NLOC - 2 - k;  // rows k+2 .. NLOC-1
+      const int m = RB - 1 - k;  // rows k+2 .. RB
       for (int base = 0; base < m; base += 2 * G) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -841,13 +1022,25 @@ __device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, 
             const int i = k + 2 + o, ri = pko(i);
             const double ai1 = F[ri + k], ai2 = F[ri + k + 1];
             const double l1 = (ai1 * a22 - ai2 * a21) * rdet, l2 = (ai2 * a11 - ai1 * a21) * rdet;
-            int pj = pko(k + 2);
-            for (int j = k + 2; j <= i; ++j) { F[ri + j] -= l1 * F[pj + k] + l2 * F[pj + k + 1]; pj += j + 1; }
+            for (int j0 = k + 2; j0 <= i; j0 += 4) {
+              double av[4], b1[4], b2[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int j = (j0 + u <= i) ? j0 + u : i;
+                const int oj = pko(j);
+                av[u] = F[ri + j];
+                b1[u] = F[oj + k];
+                b2[u] = F[oj + k + 1];
+              }
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (j0 + u <= i) F[ri + j0 + u] = av[u] - (l1 * b1[u] + l2 * b2[u]);
+            }
           }
         }
       }
       wsync();
-      for (int i = k + 2 + g; i < NLOC; i += G) {
+      for (int i = k + 2 + g; i <= RB; i += G) {
         const int ri = pko(i);
         const double ai1 = F[ri + k], ai2 = F[ri + k + 1];
         F[ri + k] = (ai1 * a22 - ai2 * a21) * rdet;
@@ -858,19 +1051,41 @@ __device__ __noinline__ void interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g, 
     wsync();
     k += size;
   }
+  return BKOut{in.pos, in.neg, in.zero, bad};
 }
 
-// State chain over x_1..x_N: D_j = S11^(j-1) + S00^(j) - S10^(j-1) D_{j-1}^{-1} S10^(j-1)^T
-// (chain index j-1 <-> x_j; S10^(k) couples x_{k+1} (row) and x_k (col)).
-__device__ __noinline__ void chain_factor(const Agent& a, Inertia& in) {
+// After interior_bk: back-substitute the trailing rows through L^T, giving
+// u0 = L^-T D^-1 z (border row) and Z^T = L^-T L_B^T (state rows).
+__device__ __noinline__ void trailing_backsolve(ldsd* F, const ldsi* piv, int g) {
+#pragma unroll 1
+  for (int m = NI - 1; m > 0; --m) {
+    const int skip = (piv[m - 1] == 2) ? m - 1 : -1;
+    const int om = pko(m);
+    double vt[NTR];
+#pragma unroll
+    for (int t = 0; t < NTR; ++t) vt[t] = F[pko(NI + t) + m];
+    for (int i = g; i < m; i += G) {
+      if (i == skip) continue;
+      const double lmi = F[om + i];
+#pragma unroll
+      for (int t = 0; t < NTR; ++t) F[pko(NI + t) + i] -= lmi * vt[t];
+    }
+    wsync();
+  }
+}
+
+// State chain over x_1..x_N: D_j = S11^(j-1)... in chain index j (x_{j+1}):
+// D_j = S11^(j) + S00^(j+1) - S10^(j) D_{j-1}^{-1} S10^(j)^T,  S10^(j) couples x_{j+1}, x_j.
+__device__ __noinline__ Inertia chain_factor(const Agent a) {
   Lds& L = gL;
+  Inertia in{0, 0, 0};
   const int lane = a.lane;
   if constexpr (NX == 1) {
     double dprev = 0.0;
 #pragma unroll 1
     for (int j = 0; j < N; ++j) {
       double d;
-      if (kfixed(a, j, NV)) {
+      if ((L.fixm[j] >> (NI + NX)) & 1ull) {
         d = 1.0;
       } else {
         d = L.S[j * 3 + 1] + (j + 1 < N ? L.S[(j + 1) * 3] : 0.0);
@@ -883,7 +1098,6 @@ __device__ __noinline__ void chain_factor(const Agent& a, Inertia& in) {
   } else if constexpr (NX > 1) {
 #pragma unroll 1
     for (int j = 0; j < N; ++j) {
-      // CW = T_j Dinv_{j-1}   (T_j = S10 of stage j)
       if (j > 0)
         for (int e = lane; e < NXX; e += WAVE) {
           const int r = e / NX, c = e % NX;
@@ -897,28 +1111,30 @@ __device__ __noinline__ void chain_factor(const Agent& a, Inertia& in) {
         double v = L.S[(j * 3 + 1) * NXX + e] + (j + 1 < N ? L.S[((j + 1) * 3) * NXX + e] : 0.0);
         if (j > 0)
           for (int m = 0; m < NX; ++m) v -= L.CW[r * NX + m] * L.S[(j * 3 + 2) * NXX + c * NX + m];
-        const bool fr = kfixed(a, j, NV + r), fc = kfixed(a, j, NV + c);
+        const bool fr = (L.fixm[j] >> (NI + NX + r)) & 1ull, fc = (L.fixm[j] >> (NI + NX + c)) & 1ull;
         if (fr || fc) v = (r == c) ? 1.0 : 0.0;
         L.C[e] = v;
       }
       wsync();
-      bk_factor<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), lane, in);
-      bk_inverse<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), LDSP(L.CW), LDSP(L.CY), L.Dinv + j * NXX, lane);
+      const Inertia bi = bk_factor<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), lane);
+      in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
+      bk_inverse<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), LDSP(L.CW), LDSP(L.CY), LDSP(L.Dinv + j * NXX), lane);
     }
   }
-  sync();
+  wsync();
+  return in;
 }
 
-__device__ __noinline__ void chain_solve(const Agent& a) {
+__device__ __noinline__ void chain_solve(const Agent a) {
   Lds& L = gL;
   const int lane = a.lane;
-  // rhs: rho_j = z1^(j) + z0^(j+1); forward y_j = rho_j - T_j Dinv_{j-1} y_{j-1}
+  // rho_j = z[x_{j+1}] of stage j + z[x_{j+1}] of stage j+1; forward y_j = rho_j - T_j Dinv_{j-1} y_{j-1}
   if constexpr (NX == 1) {
     if (lane == 0) {
       double y = 0.0;
 #pragma unroll 1
       for (int j = 0; j < N; ++j) {
-        double r = L.zx1[j] + (j + 1 < N ? L.zx0[j + 1] : 0.0);
+        double r = L.zx[j * 2 + 1] + (j + 1 < N ? L.zx[(j + 1) * 2] : 0.0);
         if (j > 0) r -= L.S[j * 3 + 2] * L.Dinv[j - 1] * y;
         y = r;
         L.xs[j] = y;
@@ -933,7 +1149,7 @@ __device__ __noinline__ void chain_solve(const Agent& a) {
       }
     }
   } else if constexpr (NX > 1) {
-    for (int c = lane; c < NX; c += WAVE) L.xs[c] = L.zx1[c] + (N > 1 ? L.zx0[NX + c] : 0.0);
+    for (int c = lane; c < NX; c += WAVE) L.xs[c] = L.zx[NX + c] + (N > 1 ? L.zx[2 * NX + c] : 0.0);
     wsync();
 #pragma unroll 1
     for (int j = 1; j < N; ++j) {
@@ -944,7 +1160,7 @@ __device__ __noinline__ void chain_solve(const Agent& a) {
       }
       wsync();
       for (int r = lane; r < NX; r += WAVE) {
-        double v = L.zx1[j * NX + r] + (j + 1 < N ? L.zx0[(j + 1) * NX + r] : 0.0);
+        double v = L.zx[j * 2 * NX + NX + r] + (j + 1 < N ? L.zx[(j + 1) * 2 * NX + r] : 0.0);
         for (int m = 0; m < NX; ++m) v -= L.S[(j * 3 + 2) * NXX + r * NX + m] * L.CY[m];
         L.xs[j * NX + r] = v;
       }
@@ -967,19 +1183,18 @@ __device__ __noinline__ void chain_solve(const Agent& a) {
       wsync();
     }
   }
-  sync();
+  wsync();
 }
 
-// Factor the KKT matrix; returns the inertia.
-__device__ __noinline__ Inertia factor_chain(const Agent& a, const KKTDiag& kd) {
+// Factor the KKT matrix bordered by the rhs in a.rhs(); returns the inertia.
+__device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   Lds& L = gL;
   const int lane = a.lane, g = lane % G, slot = lane / G;
   SPROF_DECL
-  kkt_diagonals(a, kd);
   ParLds& P = L.u.p;
-  double* F = P.F + slot * PKS;
-  int* perm = P.perm + slot * NI;
-  int* piv = P.piv + slot * NI;
+  ldsd* F = LDSP(P.F + slot * PKS);
+  ldsi* perm = LDSI(P.perm + slot * NI);
+  ldsi* piv = LDSI(P.piv + slot * NI);
   Inertia gi{0, 0, 0};
   int bad = 0;
 #pragma unroll 1
@@ -987,235 +1202,156 @@ __device__ __noinline__ Inertia factor_chain(const Agent& a, const KKTDiag& kd) 
     const int k = r * SR + slot;
     const bool act = slot < SR && k < N;
     if (act) {
-#pragma unroll 2
-      for (int t = g; t < PK; t += G) {
-        int i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-        if (pko(i + 1) <= t) ++i;
-        if (pko(i) > t) --i;
-        F[t] = local_entry(a, k, i, t - pko(i), kd.mode);
-      }
       for (int i = g; i < NI; i += G) perm[i] = i;
+      if (kd.mode == LSQ) local_assemble_generic(a, k, g, F, kd);
+      else local_assemble(a, k, g, F, kd);
     }
     wsync();
     SPROF(0);
-    if (act) interior_bk(LDSP(F), LDSI(perm), LDSI(piv), g, gi, bad);
+    if (act) {
+      const BKOut bo = interior_bk(F, perm, piv, g);
+      gi.pos += bo.pos; gi.neg += bo.neg; gi.zero += bo.zero; bad |= bo.bad;
+    }
     wsync();
     SPROF(1);
     if constexpr (NX > 0) {
       if (wsumi(g == 0 ? bad : 0) > 0) {  // singular stage interior: block chain instead
         if (lane == 0) L.seq = 1;
         sync();
-        return seq_factor(a, kd.mode);
+        return seq_factor(a, kd);
       }
     }
     if (act) {
-      if (NX > 0) {  // local Schur complement of the two state blocks
+      if (NX > 0) {  // local Schur complement of the state blocks, eliminated rhs of the states
         for (int e = g; e < 3 * NXX; e += G) {
           const int blk = e / NXX, rr = (e % NXX) / NX, cc = e % NX;
-          int ri, ci;
-          if (blk == 0) { ri = NI + rr; ci = NI + cc; }
-          else if (blk == 1) { ri = NI + NX + rr; ci = NI + NX + cc; }
-          else { ri = NI + NX + rr; ci = NI + cc; }
+          const int ri = NI + (blk == 0 ? 0 : NX) + rr, ci = NI + (blk == 1 ? NX : 0) + cc;
           L.S[(k * 3 + blk) * NXX + rr * NX + cc] = (ri >= ci) ? F[pko(ri) + ci] : F[pko(ci) + ri];
         }
+        for (int c = g; c < 2 * NX; c += G) L.zx[k * 2 * NX + c] = F[pko(RB) + NI + c];
       }
-      if (ROUNDS > 1) {
-        for (int t = g; t < PK; t += G) a.lf(k)[t] = F[t];
-        for (int i = g; i < NI; i += G) { a.lpv(k)[i] = perm[i]; a.lpv(k)[NI + i] = piv[i]; }
+      trailing_backsolve(F, piv, g);
+      // back-substitution operators, p-major, each lane stores (and later reads) its own p
+      for (int p = g; p < NI; p += G) {
+#pragma unroll
+        for (int t = 0; t < NTR; ++t) a.tr(k)[p * NTR + t] = F[pko(NI + t) + p];
+        a.prm(k)[p] = perm[p];
       }
     }
-    sync();
+    wsync();
     SPROF(2);
   }
   Inertia in{wsumi(g == 0 ? gi.pos : 0), wsumi(g == 0 ? gi.neg : 0), wsumi(g == 0 ? gi.zero : 0)};
   if (lane == 0) L.seq = 0;
-  if (NX > 0) chain_factor(a, in);
-  sync();
+  if (NX > 0) {
+    const Inertia ci = chain_factor(a);
+    in.pos += ci.pos; in.neg += ci.neg; in.zero += ci.zero;
+  }
   SPROF(3);
   return in;
 }
 
-// Solve with rhs blocks a.rhs(k) ([V, X1, lambda] per stage) -> a.sol(k).
-__device__ __noinline__ void solve_chain(const Agent& a, Mode mode) {
+// Newton step into gL.u.sol (block order per stage) from the last factorisation.
+__device__ __noinline__ void solve(const Agent a) {
   Lds& L = gL;
-  (void)mode;
   if (L.seq) { seq_solve(a); return; }
-  const int lane = a.lane, g = lane % G, slot = lane / G;
-  ParLds& P = L.u.p;
-  double* F = P.F + slot * PKS;
-  double* z = P.z + slot * NLOC;
-  int* perm = P.perm + slot * NI;
-  int* piv = P.piv + slot * NI;
   SPROF_DECL
-  // forward elimination of every stage interior
-#pragma unroll 1
-  for (int r = 0; r < ROUNDS; ++r) {
-    const int k = r * SR + slot;
-    const bool act = slot < SR && k < N;
-    if (act) {
-      if (ROUNDS > 1) {
-        for (int t = g; t < PK; t += G) F[t] = a.lf(k)[t];
-        for (int i = g; i < NI; i += G) { perm[i] = a.lpv(k)[i]; piv[i] = a.lpv(k)[NI + i]; }
-      }
-      wsync();
-      const double* rk = a.rhs(k);
-      for (int p = g; p < NLOC; p += G) {
-        double v;
-        if (p < NI) { const int o = perm[p]; v = (o < NV) ? rk[o] : rk[NP + o - NV]; }
-        else if (p < NI + NX) v = 0.0;
-        else v = rk[NV + p - NI - NX];
-        z[p] = v;
-      }
-      wsync();
-#pragma unroll 1
-      for (int p = 0; p < NI; ++p) {
-        const int pv = piv[p];
-        if (pv == 1) {
-          const double zp = z[p];
-          for (int i = p + 1 + g; i < NLOC; i += G) z[i] -= F[pko(i) + p] * zp;
-        } else if (pv == 2) {
-          const double z0 = z[p], z1 = z[p + 1];
-          for (int i = p + 2 + g; i < NLOC; i += G) { const int ri = pko(i); z[i] -= F[ri + p] * z0 + F[ri + p + 1] * z1; }
-        }
-        wsync();
-      }
-      for (int c = g; c < NX; c += G) { L.zx0[k * NX + c] = z[NI + c]; L.zx1[k * NX + c] = z[NI + NX + c]; }
-      if (ROUNDS > 1)
-        for (int i = g; i < NI; i += G) a.lz(k)[i] = z[i];
-    }
-    sync();
-  }
-  SPROF(4);
+  const int lane = a.lane, g = lane % G, slot = lane / G;
   if (NX > 0) chain_solve(a);
-  // back substitution of every stage interior
+  SPROF(4);
 #pragma unroll 1
   for (int r = 0; r < ROUNDS; ++r) {
     const int k = r * SR + slot;
-    const bool act = slot < SR && k < N;
-    if (act) {
-      if (ROUNDS > 1) {
-        for (int t = g; t < PK; t += G) F[t] = a.lf(k)[t];
-        for (int i = g; i < NI; i += G) { perm[i] = a.lpv(k)[i]; piv[i] = a.lpv(k)[NI + i]; z[i] = a.lz(k)[i]; }
-        wsync();
-      }
-      for (int p = g; p < NI; p += G) {
-        const int pv = piv[p];
-        if (pv == 1) {
-          z[p] = z[p] / F[pko(p) + p];
-        } else if (pv == 2) {
-          const double a11 = F[pko(p) + p], a21 = F[pko(p + 1) + p], a22 = F[pko(p + 1) + p + 1];
-          const double det = a11 * a22 - a21 * a21;
-          const double z0 = z[p], z1 = z[p + 1];
-          z[p] = (a22 * z0 - a21 * z1) / det;
-          z[p + 1] = (a11 * z1 - a21 * z0) / det;
-        }
-      }
-      for (int c = g; c < NX; c += G) {
-        z[NI + c] = (k > 0) ? L.xs[(k - 1) * NX + c] : 0.0;
-        z[NI + NX + c] = L.xs[k * NX + c];
-      }
-      wsync();
-      if (NX > 0)
-        for (int i = g; i < NI; i += G) {
-          double s = 0.0;
-          for (int c = 0; c < 2 * NX; ++c) s += F[pko(NI + c) + i] * z[NI + c];
-          z[i] -= s;
-        }
-      wsync();
-#pragma unroll 1
-      for (int m = NI - 1; m > 0; --m) {
-        const double um = z[m];
-        const int skip = (piv[m - 1] == 2) ? m - 1 : -1;
-        const int om = pko(m);
-        for (int i = g; i < m; i += G)
-          if (i != skip) z[i] -= F[om + i] * um;
-        wsync();
-      }
-      double* sk = a.sol(k);
-      for (int p = g; p < NI; p += G) {
-        const int o = perm[p];
-        sk[o < NV ? o : NP + o - NV] = z[p];
-      }
-      for (int c = g; c < NX; c += G) sk[NV + c] = L.xs[k * NX + c];
+    if (!(slot < SR && k < N)) continue;
+    double xk[NXP], xk1[NXP];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) {
+      xk[c] = (k > 0) ? L.xs[(k - 1) * NX + c] : 0.0;
+      xk1[c] = L.xs[k * NX + c];
     }
+    for (int p = g; p < NI; p += G) {
+      const gdbl* t = a.tr(k) + p * NTR;
+      double u = t[2 * NX];
+#pragma unroll
+      for (int c = 0; c < NX; ++c) u -= xk[c] * t[c] + xk1[c] * t[NX + c];
+      const int o = a.prm(k)[p];
+      L.u.sol[k * NB + (o < NV ? o : NP + o - NV)] = u;
+    }
+    for (int c = g; c < NX; c += G) L.u.sol[k * NB + NV + c] = xk1[c];
   }
-  sync();
+  wsync();
   SPROF(5);
 }
 
 // ---------------------------------------------------------------------------
-// scalar helpers on vectors (all lanes return the same value)
+// vector phases (lane i + 64*slot owns variable / constraint; loads first)
 // ---------------------------------------------------------------------------
-__device__ __noinline__ double theta_of(const Agent& a, const double* gval, const double* sv) {
-  double t = 0.0;
-  for (int c = a.lane; c < M; c += WAVE) {
-    const double cv = (ccls(a, c) == 0) ? gval[c] - a.gs()[c] * a.lb()[c] : gval[c] - sv[c];
-    t += fabs(cv);
-  }
-  return wsum(t);
-}
-__device__ __noinline__ double barrier_of(const Agent& a, const double* xv, const double* sv) {
-  double t = 0.0;
-  for (int i = NX + a.lane; i < NW; i += WAVE) {
-    const double lo = a.xL()[i], hi = a.xU()[i];
-    if (lo == hi) continue;
-    if (isfin(lo)) t += log(xv[i] - lo);
-    if (isfin(hi)) t += log(hi - xv[i]);
-  }
-  for (int c = a.lane; c < M; c += WAVE) {
-    if (ccls(a, c) != 1) continue;
-    if (isfin(a.sL()[c])) t += log(sv[c] - a.sL()[c]);
-    if (isfin(a.sU()[c])) t += log(a.sU()[c] - sv[c]);
-  }
-  return wsum(t);
-}
-
+// optimality error parts; complementarity kept as (max, min) of the products so
+// that E_mu for any mu is max(pmx - mu, mu - pmn) without another pass
 struct OptErr {
-  double err, dual, primal, compl_, dual_u, primal_u;
+  double dual, dual_u, primal, primal_u, pmx, pmn, s_d, s_c;
+  int ncompl;
+  __device__ double compl_at(double mu) const { return ncompl > 0 ? fmax(pmx - mu, mu - pmn) : 0.0; }
+  __device__ double err_at(double mu) const { return fmax(fmax(dual / s_d, primal), compl_at(mu) / s_c); }
 };
 
 // scaled optimality error E_mu (IPOPT eq. 5) + unscaled parts
-__device__ __noinline__ OptErr opt_error(const Agent& a, double mu, double obj_scale) {
-  double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, pmax_u = 0.0, cmax = 0.0;
+__device__ __noinline__ OptErr opt_error(const Agent a, double obj_scale) {
+  const int lane = a.lane;
+  double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, pmax_u = 0.0, pmx = -INFINITY, pmn = INFINITY;
   double lsum = 0.0, zsum = 0.0;
   int nz = 0;
-  for (int i = NX + a.lane; i < NW; i += WAVE) {
-    if (is_fixed(a, i)) continue;
-    const double rd = obj_scale * acc_grad(a, i) + acc_jtl(a, i, a.lam()) - a.zL()[i] + a.zU()[i];
-    dmax = fmax(dmax, fabs(rd));
-    dmax_u = fmax(dmax_u, fabs(rd) / obj_scale);
-    const double lo = a.xL()[i], hi = a.xU()[i];
-    if (isfin(lo)) { cmax = fmax(cmax, fabs((a.x()[i] - lo) * a.zL()[i] - mu)); zsum += fabs(a.zL()[i]); nz++; }
-    if (isfin(hi)) { cmax = fmax(cmax, fabs((hi - a.x()[i]) * a.zU()[i] - mu)); zsum += fabs(a.zU()[i]); nz++; }
-  }
-  for (int c = a.lane; c < M; c += WAVE) {
-    const int cl = ccls(a, c);
-    const double gsc = a.gs()[c];
-    double cv;
-    if (cl == 0) {
-      cv = a.gv()[c] - gsc * a.lb()[c];
-    } else {
-      cv = a.gv()[c] - a.s()[c];
-      if (cl == 1) {
-        const double rs = -a.lam()[c] - a.vL()[c] + a.vU()[c];
-        dmax = fmax(dmax, fabs(rs));
-        if (isfin(a.sL()[c])) { cmax = fmax(cmax, fabs((a.s()[c] - a.sL()[c]) * a.vL()[c] - mu)); zsum += fabs(a.vL()[c]); nz++; }
-        if (isfin(a.sU()[c])) { cmax = fmax(cmax, fabs((a.sU()[c] - a.s()[c]) * a.vU()[c] - mu)); zsum += fabs(a.vU()[c]); nz++; }
-      }
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    const bool on = i >= NX && i < NW;
+    const int ii = on ? i : NX;
+    const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
+    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii, a.lam());
+    if (on && lo != hi) {
+      const double rd = obj_scale * gr + jt - zl + zu;
+      dmax = fmax(dmax, fabs(rd));
+      dmax_u = fmax(dmax_u, fabs(rd) / obj_scale);
+      if (isfin(lo)) { const double pr = (xv - lo) * zl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zl); nz++; }
+      if (isfin(hi)) { const double pr = (hi - xv) * zu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zu); nz++; }
     }
-    pmax = fmax(pmax, fabs(cv));
-    pmax_u = fmax(pmax_u, fabs(cv) / gsc);
-    lsum += fabs(a.lam()[c]);
   }
-  dmax = wmax(dmax); dmax_u = wmax(dmax_u); pmax = wmax(pmax); pmax_u = wmax(pmax_u);
-  cmax = wmax(cmax); lsum = wsum(lsum); zsum = wsum(zsum); nz = wsumi(nz);
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const bool on = c < M;
+    const int cc = on ? c : 0;
+    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double gsc = a.gs()[cc], gvv = a.gv()[cc], sv = a.s()[cc], lm = a.lam()[cc];
+    const double vl = a.vL()[cc], vu = a.vU()[cc];
+    if (on) {
+      const int cl = cls_of(lbv, ubv, slo, sup);
+      double cv;
+      if (cl == 0) {
+        cv = gvv - gsc * lbv;
+      } else {
+        cv = gvv - sv;
+        if (cl == 1) {
+          const double rs = -lm - vl + vu;
+          dmax = fmax(dmax, fabs(rs));
+          if (isfin(slo)) { const double pr = (sv - slo) * vl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vl); nz++; }
+          if (isfin(sup)) { const double pr = (sup - sv) * vu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vu); nz++; }
+        }
+      }
+      pmax = fmax(pmax, fabs(cv));
+      pmax_u = fmax(pmax_u, fabs(cv) / gsc);
+      lsum += fabs(lm);
+    }
+  }
+  OptErr e;
+  e.dual = wmax(dmax); e.dual_u = wmax(dmax_u); e.primal = wmax(pmax); e.primal_u = wmax(pmax_u);
+  e.pmx = wmax(pmx); e.pmn = wmin(pmn);
+  lsum = wsum(lsum); zsum = wsum(zsum); nz = wsumi(nz);
+  e.ncompl = nz;
   const double smax = 100.0;
   // IPOPT: s_d over all multipliers (y_c, y_d, z_L, z_U, v_L, v_U)
-  const double s_d = fmax(smax, (lsum + zsum) / fmax(1.0, (double)(M + nz))) / smax;
-  const double s_c = nz > 0 ? fmax(smax, zsum / (double)nz) / smax : 1.0;
-  OptErr e;
-  e.err = fmax(fmax(dmax / s_d, pmax), cmax / s_c);
-  e.dual = dmax; e.primal = pmax; e.compl_ = cmax; e.dual_u = dmax_u; e.primal_u = pmax_u;
+  e.s_d = fmax(smax, (lsum + zsum) / fmax(1.0, (double)(M + nz))) / smax;
+  e.s_c = nz > 0 ? fmax(smax, zsum / (double)nz) / smax : 1.0;
   return e;
 }
 
@@ -1233,20 +1369,20 @@ __device__ __forceinline__ double push_into(double v, double lo, double hi, doub
 __device__ __forceinline__ double relax_lo(double b, double f) { return b - f * fmax(1.0, fabs(b)); }
 __device__ __forceinline__ double relax_hi(double b, double f) { return b + f * fmax(1.0, fabs(b)); }
 
-// ---------------------------------------------------------------------------
-// IPM phases (noinline: keeps the register budget of each phase separate)
-// ---------------------------------------------------------------------------
 struct Scal {
   double obj_scale, fx;
 };
 
-__device__ __noinline__ Scal init_agent(const Agent& a, const Args& args, int agent) {
+__device__ __noinline__ Scal init_agent(const Agent a, const Args& args, int agent) {
   const mpcx_options& o = args.opt;
   const int lane = a.lane;
-  const double* lbw = args.lbw + (long)agent * NW;
-  const double* ubw = args.ubw + (long)agent * NW;
-  const double* wio = args.w + (long)agent * NW;
+  const gdbl* lbw = (const gdbl*)args.lbw + (long)agent * NW;
+  const gdbl* ubw = (const gdbl*)args.ubw + (long)agent * NW;
+  const gdbl* wio = (const gdbl*)args.w + (long)agent * NW;
+  const gdbl* pin = (const gdbl*)args.p + (long)agent * NPAR;
+  for (int t = lane; t < NPAR; t += WAVE) gL.par[t] = pin[t];
   for (long t = lane; t < (long)(NL + NG * NL + NL * NL) * N; t += WAVE) a.ws[O_SDG + t] = 0.0;
+  for (long t = lane; t < (long)N * PKS; t += WAVE) a.ws[O_LP + t] = 0.0;  // structural zeros stay zero
   for (int i = lane; i < NW; i += WAVE) {
     double lo = lbw[i], hi = ubw[i];
     if (lo <= -INF_BOUND) lo = -INFINITY;
@@ -1257,36 +1393,40 @@ __device__ __noinline__ Scal init_agent(const Agent& a, const Args& args, int ag
     a.x()[i] = (lo == hi) ? lo : wio[i];
   }
   if (args.lbg != nullptr) {
+    const gdbl* lbg = (const gdbl*)args.lbg + (long)agent * M;
+    const gdbl* ubg = (const gdbl*)args.ubg + (long)agent * M;
     for (int c = lane; c < M; c += WAVE) {
-      a.lb()[c] = args.lbg[(long)agent * M + c];
-      a.ub()[c] = args.ubg[(long)agent * M + c];
+      a.lb()[c] = lbg[c];
+      a.ub()[c] = ubg[c];
     }
   } else {
+    wsync();
     for (int k = lane; k < N; k += WAVE)
-      gen_stage_bounds(a.p + NPG + k * NPS, a.p, k * TS, a.lb() + k * NG, a.ub() + k * NG, 1);
+      gen_stage_bounds(par_stage(k), par_global(), k * TS, (double*)(a.lb() + k * NG), (double*)(a.ub() + k * NG), 1);
   }
   sync();
   for (int c = lane; c < M; c += WAVE) {
     if (a.lb()[c] <= -INF_BOUND) a.lb()[c] = -INFINITY;
     if (a.ub()[c] >= INF_BOUND) a.ub()[c] = INFINITY;
   }
+  for (int c = lane; c < M; c += WAVE) a.gs()[c] = 1.0;
   sync();
   // gradient based scaling at the user starting point
-  eval_gj(a, a.x());
+  eval_gj_ws(a, a.x());
   sync();
-  double gmax = 0.0;
+  double gmx = 0.0;
   for (int i = NX + lane; i < NW; i += WAVE)
-    if (!is_fixed(a, i)) gmax = fmax(gmax, fabs(acc_grad(a, i)));
-  gmax = wmax(gmax);
+    if (a.xL()[i] != a.xU()[i]) gmx = fmax(gmx, fabs(acc_grad(a, i)));
+  gmx = wmax(gmx);
   Scal sc;
   sc.obj_scale = 1.0;
-  if (gmax > o.nlp_scaling_max_gradient)
-    sc.obj_scale = fmax(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / gmax);
+  if (gmx > o.nlp_scaling_max_gradient)
+    sc.obj_scale = fmax(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / gmx);
   for (int c = lane; c < M; c += WAVE) {
     const int k = c / NG, r = c % NG;
     double rm = 0.0;
     for (int j = 0; j < NL; ++j)
-      if (!is_fixed(a, k * NP + j)) rm = fmax(rm, fabs(a.sdj()[(r * NL + j) * N + k]));
+      if (a.xL()[k * NP + j] != a.xU()[k * NP + j]) rm = fmax(rm, fabs(a.sdj()[(r * NL + j) * N + k]));
     a.gs()[c] = (rm > o.nlp_scaling_max_gradient) ? fmax(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / rm) : 1.0;
   }
   // bound relaxation + initial point
@@ -1306,7 +1446,18 @@ __device__ __noinline__ Scal init_agent(const Agent& a, const Args& args, int ag
     }
   }
   sync();
-  sc.fx = sc.obj_scale * eval_fg(a, a.x(), a.gv());
+  // fixed-variable masks of the stage-local systems (bounds never change fixedness)
+  for (int k = lane; k < N; k += WAVE) {
+    unsigned long long m = 0ull;
+    for (int i = 0; i < NLOC; ++i) {
+      const int ki = lkind(i);
+      if (ki == 1) continue;
+      const int vi = lvar(k, i, ki);
+      if (a.xL()[vi] == a.xU()[vi]) m |= 1ull << i;
+    }
+    gL.fixm[k] = m;
+  }
+  sc.fx = sc.obj_scale * eval_fg_ws(a, a.x(), a.gv());
   sync();
   for (int c = lane; c < M; c += WAVE) {
     const double gsc = a.gs()[c];
@@ -1326,130 +1477,178 @@ __device__ __noinline__ Scal init_agent(const Agent& a, const Args& args, int ag
     a.lam()[c] = 0.0;
   }
   sync();
-  eval_gj(a, a.x());
+  eval_gj_ws(a, a.x());
   sync();
   return sc;
 }
 
-// least-squares estimate of the constraint multipliers (IPOPT constr_mult_init_max)
-__device__ __noinline__ void ls_multipliers(const Agent& a, const mpcx_options& o, double obj_scale) {
+// sum |c(x) - s| (scaled) at the current point
+__device__ __noinline__ double theta_now(const Agent a) {
+  double t = 0.0;
+  for (int c = a.lane; c < M; c += WAVE) {
+    const int cl = cls_of(a.lb()[c], a.ub()[c], a.sL()[c], a.sU()[c]);
+    const double cv = (cl == 0) ? a.gv()[c] - a.gs()[c] * a.lb()[c] : a.gv()[c] - a.s()[c];
+    t += fabs(cv);
+  }
+  return wsum(t);
+}
+
+__device__ __noinline__ void rhs_primal(const Agent a, double mu, double obj_scale) {
   const int lane = a.lane;
-  KKTDiag kd{0.0, 0.0, LSQ};
-  const Inertia in = factor_chain(a, kd);
-#pragma unroll 1
-  for (int k = 0; k < N; ++k) {
-    for (int q = lane; q < NP; q += WAVE) {
-      const int i = NX + k * NP + q;
-      a.rhs(k)[q] = is_fixed(a, i) ? 0.0 : -(obj_scale * acc_grad(a, i) - a.zL()[i] + a.zU()[i]);
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    const bool on = i >= NX && i < NW;
+    const int ii = on ? i : NX;
+    const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii];
+    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii, a.lam());
+    if (on) {
+      double r = 0.0;
+      if (lo != hi) {
+        double gphi = obj_scale * gr;
+        if (isfin(lo)) gphi -= mu / (xv - lo);
+        if (isfin(hi)) gphi += mu / (hi - xv);
+        r = -(gphi + jt);
+      }
+      const int b = (i - NX) / NP, off = (i - NX) % NP;
+      a.rhs(b)[off] = r;
+      a.lp(b)[pko(RB) + (off < NV ? off : NI + NX + off - NV)] = r;
     }
-    for (int r = lane; r < NG; r += WAVE) {
-      const int c = k * NG + r;
-      a.rhs(k)[NP + r] = (ccls(a, c) == 1) ? a.vL()[c] - a.vU()[c] : 0.0;
+  }
+}
+
+// dual rows of the rhs (depend on delta_w); ends with the barrier that hands
+// the whole rhs to the factorisation lanes
+__device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw) {
+  const int lane = a.lane;
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const bool on = c < M;
+    const int cc = on ? c : 0;
+    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double gvv = a.gv()[cc], gsc = a.gs()[cc], sv = a.s()[cc], lm = a.lam()[cc];
+    const double vl = a.vL()[cc], vu = a.vU()[cc];
+    if (on) {
+      const int cl = cls_of(lbv, ubv, slo, sup);
+      double rr;
+      if (cl == 0) {
+        rr = -(gvv - gsc * lbv);
+      } else {
+        rr = -(gvv - sv);
+        if (cl == 1) {
+          double gphis = 0.0;
+          if (isfin(slo)) gphis -= mu / (sv - slo);
+          if (isfin(sup)) gphis += mu / (sup - sv);
+          rr -= (gphis - lm) / (sigma_s_v(sv, slo, sup, vl, vu) + dw);
+        }
+      }
+      a.rhs(c / NG)[NP + c % NG] = rr;
+      a.lp(c / NG)[pko(RB) + NV + c % NG] = rr;
     }
   }
   sync();
-  if (in.zero != 0) return;
-  solve_chain(a, LSQ);
-  double lmax = 0.0;
-  for (int c = lane; c < M; c += WAVE) lmax = fmax(lmax, fabs(a.sol(c / NG)[NP + c % NG]));
-  lmax = wmax(lmax);
-  if (lmax <= o.constr_mult_init_max)
-    for (int c = lane; c < M; c += WAVE) a.lam()[c] = a.sol(c / NG)[NP + c % NG];
-  sync();
 }
 
-__device__ __noinline__ void rhs_primal(const Agent& a, double mu, double obj_scale) {
+// least-squares estimate of the constraint multipliers (IPOPT constr_mult_init_max)
+__device__ __noinline__ void ls_multipliers(const Agent a, const double constr_mult_init_max, double obj_scale) {
   const int lane = a.lane;
   for (int i = NX + lane; i < NW; i += WAVE) {
-    double r = 0.0;
-    if (!is_fixed(a, i)) {
-      const double lo = a.xL()[i], hi = a.xU()[i], xv = a.x()[i];
-      double gphi = obj_scale * acc_grad(a, i);
-      if (isfin(lo)) gphi -= mu / (xv - lo);
-      if (isfin(hi)) gphi += mu / (hi - xv);
-      r = -(gphi + acc_jtl(a, i, a.lam()));
-    }
+    const double r = (a.xL()[i] == a.xU()[i]) ? 0.0 : -(obj_scale * acc_grad(a, i) - a.zL()[i] + a.zU()[i]);
     a.rhs((i - NX) / NP)[(i - NX) % NP] = r;
   }
-  sync();
-}
-
-__device__ __forceinline__ double slack_rs(const Agent& a, int c, double mu) {
-  const double sv = a.s()[c];
-  double gphis = 0.0;
-  if (isfin(a.sL()[c])) gphis -= mu / (sv - a.sL()[c]);
-  if (isfin(a.sU()[c])) gphis += mu / (a.sU()[c] - sv);
-  return gphis - a.lam()[c];
-}
-
-__device__ __noinline__ void rhs_dual(const Agent& a, double mu, double dw) {
-  const int lane = a.lane;
   for (int c = lane; c < M; c += WAVE) {
-    const int cl = ccls(a, c);
-    double rr;
-    if (cl == 0) {
-      rr = -(a.gv()[c] - a.gs()[c] * a.lb()[c]);
-    } else {
-      rr = -(a.gv()[c] - a.s()[c]);
-      if (cl == 1) rr -= slack_rs(a, c, mu) / (sigma_s(a, c) + dw);
-    }
-    a.rhs(c / NG)[NP + c % NG] = rr;
+    const int cl = cls_of(a.lb()[c], a.ub()[c], a.sL()[c], a.sU()[c]);
+    a.rhs(c / NG)[NP + c % NG] = (cl == 1) ? a.vL()[c] - a.vU()[c] : 0.0;
   }
+  sync();
+  KKTDiag kd{0.0, 0.0, LSQ};
+  const Inertia in = factor(a, kd);
+  if (in.zero != 0) return;
+  solve(a);
+  double lmax = 0.0;
+  for (int c = lane; c < M; c += WAVE) lmax = fmax(lmax, fabs(gL.u.sol[(c / NG) * NB + NP + c % NG]));
+  lmax = wmax(lmax);
+  if (lmax <= constr_mult_init_max)
+    for (int c = lane; c < M; c += WAVE) a.lam()[c] = gL.u.sol[(c / NG) * NB + NP + c % NG];
   sync();
 }
 
 struct StepInfo {
-  double amax, az, gphid;
+  double amax, az, gphid, theta, barrier;
 };
 
-// full step from the chain solution + fraction-to-the-boundary step sizes
-__device__ __noinline__ StepInfo recover_step(const Agent& a, double mu, double tau, double dw,
-                                              double obj_scale) {
+// full step from the Newton solution (LDS) + fraction-to-the-boundary step
+// sizes + constraint violation and barrier at the current point
+__device__ __noinline__ StepInfo recover_step(const Agent a, double mu, double tau, double dw, double obj_scale) {
   const int lane = a.lane;
-  double amax = 1.0, az = 1.0, gphid = 0.0;
-  for (int i = lane; i < NW; i += WAVE) {
-    double d = 0.0;
-    if (i >= NX && !is_fixed(a, i)) d = a.sol((i - NX) / NP)[(i - NX) % NP];
+  double amax = 1.0, az = 1.0, gphid = 0.0, theta = 0.0, bar = 0.0;
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    const bool on = i < NW;
+    const int ii = (i >= NX && on) ? i : NX;
+    const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
+    const double gr = acc_grad(a, ii);
+    const double sv = gL.u.sol[((ii - NX) / NP) * NB + (ii - NX) % NP];
+    if (!on) continue;
+    const bool free_ = i >= NX && lo != hi;
+    const double d = free_ ? sv : 0.0;
     a.dx()[i] = d;
-    if (i < NX || is_fixed(a, i)) continue;
-    const double lo = a.xL()[i], hi = a.xU()[i], xv = a.x()[i];
-    double gphi = obj_scale * acc_grad(a, i);
+    if (!free_) continue;
+    double gphi = obj_scale * gr;
     if (isfin(lo)) {
-      const double sl = xv - lo;
-      gphi -= mu / sl;
-      if (d < 0) amax = fmin(amax, -tau * sl / d);
-      const double dz = mu / sl - a.zL()[i] - (a.zL()[i] / sl) * d;
-      if (dz < 0) az = fmin(az, -tau * a.zL()[i] / dz);
+      const double s_l = xv - lo;
+      gphi -= mu / s_l;
+      if (d < 0) amax = fmin(amax, -tau * s_l / d);
+      const double dz = mu / s_l - zl - (zl / s_l) * d;
+      if (dz < 0) az = fmin(az, -tau * zl / dz);
+      bar += log(s_l);
     }
     if (isfin(hi)) {
-      const double su = hi - xv;
-      gphi += mu / su;
-      if (d > 0) amax = fmin(amax, tau * su / d);
-      const double dz = mu / su - a.zU()[i] + (a.zU()[i] / su) * d;
-      if (dz < 0) az = fmin(az, -tau * a.zU()[i] / dz);
+      const double s_u = hi - xv;
+      gphi += mu / s_u;
+      if (d > 0) amax = fmin(amax, tau * s_u / d);
+      const double dz = mu / s_u - zu + (zu / s_u) * d;
+      if (dz < 0) az = fmin(az, -tau * zu / dz);
+      bar += log(s_u);
     }
     gphid += gphi * d;
   }
-  for (int c = lane; c < M; c += WAVE) {
-    const double dlam = a.sol(c / NG)[NP + c % NG];
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const bool on = c < M;
+    const int cc = on ? c : 0;
+    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double sv = a.s()[cc], lm = a.lam()[cc], vl = a.vL()[cc], vu = a.vU()[cc];
+    const double gvv = a.gv()[cc], gsc = a.gs()[cc];
+    const double dlam = gL.u.sol[(cc / NG) * NB + NP + cc % NG];
+    if (!on) continue;
     a.dl()[c] = dlam;
+    const int cl = cls_of(lbv, ubv, slo, sup);
+    theta += fabs((cl == 0) ? gvv - gsc * lbv : gvv - sv);
     double dsv = 0.0;
-    if (ccls(a, c) == 1) {
-      const double sv = a.s()[c];
-      const double rs = slack_rs(a, c, mu);
-      dsv = (dlam - rs) / (sigma_s(a, c) + dw);
-      gphid += (rs + a.lam()[c]) * dsv;
-      if (isfin(a.sL()[c])) {
-        const double sl = sv - a.sL()[c];
-        if (dsv < 0) amax = fmin(amax, -tau * sl / dsv);
-        const double dv = mu / sl - a.vL()[c] - (a.vL()[c] / sl) * dsv;
-        if (dv < 0) az = fmin(az, -tau * a.vL()[c] / dv);
+    if (cl == 1) {
+      double gphis = 0.0;
+      if (isfin(slo)) gphis -= mu / (sv - slo);
+      if (isfin(sup)) gphis += mu / (sup - sv);
+      const double rs = gphis - lm;
+      dsv = (dlam - rs) / (sigma_s_v(sv, slo, sup, vl, vu) + dw);
+      gphid += (rs + lm) * dsv;
+      if (isfin(slo)) {
+        const double s_l = sv - slo;
+        if (dsv < 0) amax = fmin(amax, -tau * s_l / dsv);
+        const double dv = mu / s_l - vl - (vl / s_l) * dsv;
+        if (dv < 0) az = fmin(az, -tau * vl / dv);
+        bar += log(s_l);
       }
-      if (isfin(a.sU()[c])) {
-        const double su = a.sU()[c] - sv;
-        if (dsv > 0) amax = fmin(amax, tau * su / dsv);
-        const double dv = mu / su - a.vU()[c] + (a.vU()[c] / su) * dsv;
-        if (dv < 0) az = fmin(az, -tau * a.vU()[c] / dv);
+      if (isfin(sup)) {
+        const double s_u = sup - sv;
+        if (dsv > 0) amax = fmin(amax, tau * s_u / dsv);
+        const double dv = mu / s_u - vu + (vu / s_u) * dsv;
+        if (dv < 0) az = fmin(az, -tau * vu / dv);
+        bar += log(s_u);
       }
     }
     a.ds()[c] = dsv;
@@ -1458,71 +1657,176 @@ __device__ __noinline__ StepInfo recover_step(const Agent& a, double mu, double 
   st.amax = wmin(amax);
   st.az = wmin(az);
   st.gphid = wsum(gphid);
-  sync();
+  st.theta = wsum(theta);
+  st.barrier = wsum(bar);
   return st;
 }
 
 struct Trial {
   double f, theta, phi;
 };
+struct LSOpt {  // line-search options by value (registers, not kernarg loads)
+  double alpha_min_frac, gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi;
+};
+struct LSResult {
+  Trial tr;
+  double alpha;
+  int accepted, ftype, trials;
+};
 
-__device__ __noinline__ Trial trial_point(const Agent& a, double alpha, double mu, double obj_scale) {
+// filter line search; trial points live in LDS (xt, scaled gt)
+__device__ __noinline__ LSResult line_search(const Agent a, const LSOpt o, double mu, double obj_scale,
+                                             double alpha0, double gphid, double theta, double phi,
+                                             double theta_min, double theta_max, int nfilt) {
   const int lane = a.lane;
-  for (int i = lane; i < NW; i += WAVE) a.xt()[i] = a.x()[i] + alpha * a.dx()[i];
-  for (int c = lane; c < M; c += WAVE) a.st()[c] = a.s()[c] + alpha * a.ds()[c];
-  sync();
-  Trial t;
-  t.f = obj_scale * eval_fg(a, a.xt(), a.gt());
-  sync();
-  for (int c = lane; c < M; c += WAVE) a.gt()[c] *= a.gs()[c];
-  sync();
-  t.theta = theta_of(a, a.gt(), a.st());
-  t.phi = t.f - mu * barrier_of(a, a.xt(), a.st());
-  return t;
+  double xr[VS], dxr[VS], lor[VS], hir[VS];
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    const int ii = i < NW ? i : 0;
+    xr[sl] = a.x()[ii]; dxr[sl] = a.dx()[ii]; lor[sl] = a.xL()[ii]; hir[sl] = a.xU()[ii];
+  }
+  double sr[CS], dsr[CS], slr[CS], sur[CS], gsr[CS], lbr[CS];
+  int clr[CS];
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const int cc = c < M ? c : 0;
+    sr[sl] = a.s()[cc]; dsr[sl] = a.ds()[cc]; slr[sl] = a.sL()[cc]; sur[sl] = a.sU()[cc];
+    gsr[sl] = a.gs()[cc]; lbr[sl] = a.lb()[cc];
+    clr[sl] = cls_of(lbr[sl], a.ub()[cc], slr[sl], sur[sl]);
+  }
+  double amin;
+  if (gphid < 0 && theta <= theta_min)
+    amin = o.alpha_min_frac * fmin(fmin(o.gamma_theta, o.gamma_phi * theta / (-gphid)),
+                                   o.delta * pow(theta, o.s_theta) / pow(-gphid, o.s_phi));
+  else if (gphid < 0)
+    amin = o.alpha_min_frac * fmin(o.gamma_theta, o.gamma_phi * theta / (-gphid));
+  else
+    amin = o.alpha_min_frac * o.gamma_theta;
+  if (!(amin > 0.0)) amin = o.alpha_min_frac * o.gamma_theta;  // NaN guard
+  LSResult res;
+  res.alpha = alpha0;
+  res.accepted = 0;
+  res.ftype = 0;
+  res.trials = 0;
+  Trial tr{0.0, 0.0, 0.0};
+  double alpha = alpha0;
+#pragma unroll 1
+  for (int ls = 0; ls < 64; ++ls) {
+#pragma unroll
+    for (int sl = 0; sl < VS; ++sl) {
+      const int i = lane + sl * WAVE;
+      if (i < NW) gL.u.t.xt[i] = xr[sl] + alpha * dxr[sl];
+    }
+    wsync();
+    tr.f = obj_scale * eval_fg_lds(a);
+    wsync();
+    double th = 0.0, bar = 0.0;
+#pragma unroll
+    for (int sl = 0; sl < VS; ++sl) {
+      const int i = lane + sl * WAVE;
+      if (i >= NX && i < NW && lor[sl] != hir[sl]) {
+        const double xt = xr[sl] + alpha * dxr[sl];
+        if (isfin(lor[sl])) bar += log(xt - lor[sl]);
+        if (isfin(hir[sl])) bar += log(hir[sl] - xt);
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < CS; ++sl) {
+      const int c = lane + sl * WAVE;
+      if (c < M) {
+        const double gt = gL.u.t.gt[c] * gsr[sl];
+        gL.u.t.gt[c] = gt;
+        const double st = sr[sl] + alpha * dsr[sl];
+        th += fabs(clr[sl] == 0 ? gt - gsr[sl] * lbr[sl] : gt - st);
+        if (clr[sl] == 1) {
+          if (isfin(slr[sl])) bar += log(st - slr[sl]);
+          if (isfin(sur[sl])) bar += log(sur[sl] - st);
+        }
+      }
+    }
+    tr.theta = wsum(th);
+    tr.phi = tr.f - mu * wsum(bar);
+    res.trials++;
+    bool okt = (tr.theta <= theta_max) && (tr.phi == tr.phi);
+    for (int j = 0; j < nfilt && okt; ++j)
+      if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
+    bool ftype = false;
+    if (okt) {
+      const bool switching = gphid < 0 && alpha * pow(-gphid, o.s_phi) > o.delta * pow(theta, o.s_theta);
+      if (theta <= theta_min && switching) {
+        okt = tr.phi <= phi + o.eta_phi * alpha * gphid;
+        ftype = true;
+      } else {
+        okt = tr.theta <= (1.0 - o.gamma_theta) * theta || tr.phi <= phi - o.gamma_phi * theta;
+        ftype = false;
+      }
+    }
+    res.alpha = alpha;
+    res.ftype = ftype;
+    if (okt) { res.accepted = 1; break; }
+    alpha *= 0.5;
+    if (alpha < amin) break;
+  }
+  res.tr = tr;
+  return res;
 }
 
-__device__ __noinline__ void accept_step(const Agent& a, const mpcx_options& o, double mu,
-                                         double alpha, double az) {
+// take the last trial point (xt, gt in LDS) and the multiplier steps
+__device__ __noinline__ void accept_step(const Agent a, const double kappa_sigma, double mu, double alpha, double az) {
   const int lane = a.lane;
-  for (int i = NX + lane; i < NW; i += WAVE) {
-    if (is_fixed(a, i)) continue;
-    const double d = a.dx()[i];
-    const double lo = a.xL()[i], hi = a.xU()[i], xold = a.x()[i];
-    const double xn = a.xt()[i];
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    const bool on = i >= NX && i < NW;
+    const int ii = on ? i : NX;
+    const double lo = a.xL()[ii], hi = a.xU()[ii], xold = a.x()[ii], d = a.dx()[ii];
+    const double zl = a.zL()[ii], zu = a.zU()[ii];
+    const double xn = gL.u.t.xt[ii];
+    if (!on || lo == hi) continue;
     a.x()[i] = xn;
     if (isfin(lo)) {
       const double sl0 = xold - lo;
-      const double dz = mu / sl0 - a.zL()[i] - (a.zL()[i] / sl0) * d;
-      const double zn = a.zL()[i] + az * dz, sl = xn - lo;
-      a.zL()[i] = fmax(fmin(zn, o.kappa_sigma * mu / sl), mu / (o.kappa_sigma * sl));
+      const double dz = mu / sl0 - zl - (zl / sl0) * d;
+      const double zn = zl + az * dz, s_l = xn - lo;
+      a.zL()[i] = fmax(fmin(zn, kappa_sigma * mu / s_l), mu / (kappa_sigma * s_l));
     }
     if (isfin(hi)) {
       const double su0 = hi - xold;
-      const double dz = mu / su0 - a.zU()[i] + (a.zU()[i] / su0) * d;
-      const double zn = a.zU()[i] + az * dz, su = hi - xn;
-      a.zU()[i] = fmax(fmin(zn, o.kappa_sigma * mu / su), mu / (o.kappa_sigma * su));
+      const double dz = mu / su0 - zu + (zu / su0) * d;
+      const double zn = zu + az * dz, s_u = hi - xn;
+      a.zU()[i] = fmax(fmin(zn, kappa_sigma * mu / s_u), mu / (kappa_sigma * s_u));
     }
   }
-  for (int c = lane; c < M; c += WAVE) {
-    a.lam()[c] += alpha * a.dl()[c];
-    a.gv()[c] = a.gt()[c];
-    if (ccls(a, c) != 1) { a.s()[c] = a.st()[c]; continue; }
-    const double sold = a.s()[c], sn = a.st()[c], dsv = a.ds()[c];
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const bool on = c < M;
+    const int cc = on ? c : 0;
+    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double lm = a.lam()[cc], dl = a.dl()[cc], sold = a.s()[cc], dsv = a.ds()[cc];
+    const double vl = a.vL()[cc], vu = a.vU()[cc];
+    const double gt = gL.u.t.gt[cc];
+    if (!on) continue;
+    a.lam()[c] = lm + alpha * dl;
+    a.gv()[c] = gt;
+    const double sn = sold + alpha * dsv;
     a.s()[c] = sn;
-    if (isfin(a.sL()[c])) {
-      const double sl0 = sold - a.sL()[c];
-      const double dv = mu / sl0 - a.vL()[c] - (a.vL()[c] / sl0) * dsv;
-      const double vn = a.vL()[c] + az * dv, sl = sn - a.sL()[c];
-      a.vL()[c] = fmax(fmin(vn, o.kappa_sigma * mu / sl), mu / (o.kappa_sigma * sl));
+    if (cls_of(lbv, ubv, slo, sup) != 1) continue;
+    if (isfin(slo)) {
+      const double sl0 = sold - slo;
+      const double dv = mu / sl0 - vl - (vl / sl0) * dsv;
+      const double vn = vl + az * dv, s_l = sn - slo;
+      a.vL()[c] = fmax(fmin(vn, kappa_sigma * mu / s_l), mu / (kappa_sigma * s_l));
     }
-    if (isfin(a.sU()[c])) {
-      const double su0 = a.sU()[c] - sold;
-      const double dv = mu / su0 - a.vU()[c] + (a.vU()[c] / su0) * dsv;
-      const double vn = a.vU()[c] + az * dv, su = a.sU()[c] - sn;
-      a.vU()[c] = fmax(fmin(vn, o.kappa_sigma * mu / su), mu / (o.kappa_sigma * su));
+    if (isfin(sup)) {
+      const double su0 = sup - sold;
+      const double dv = mu / su0 - vu + (vu / su0) * dsv;
+      const double vn = vu + az * dv, s_u = sup - sn;
+      a.vU()[c] = fmax(fmin(vn, kappa_sigma * mu / s_u), mu / (kappa_sigma * s_u));
     }
   }
-  sync();
 }
 
 }  // namespace mpcx_kernel
@@ -1545,11 +1849,9 @@ using namespace mpcx_kernel;
 extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(Args args) {
   const int agent = blockIdx.x;
   if (agent >= args.n_agents) return;
-  Lds& L = gL;
   const mpcx_options& o = args.opt;
   Agent a;
-  a.ws = args.ws + (long)agent * args.ws_stride;
-  a.p = args.p + (long)agent * NPAR;
+  a.ws = (gdbl*)args.ws + (long)agent * args.ws_stride;
   a.lane = threadIdx.x;
   const int lane = a.lane;
 
@@ -1564,7 +1866,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   double fx = sc.fx;
   int n_fact = 0, n_ic = 0, n_fallback = 0, n_trials = 0;
   if (M > 0 && o.constr_mult_init_max > 0.0) {
-    ls_multipliers(a, o, obj_scale);
+    ls_multipliers(a, o.constr_mult_init_max, obj_scale);
     n_fact++;
   }
   PROF(1);
@@ -1572,7 +1874,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   double mu = o.mu_init;
   double tau = fmax(o.tau_min, 1.0 - mu);
   double dw_last = 0.0;
-  const double theta0 = theta_of(a, a.gv(), a.s());
+  const double theta0 = theta_now(a);
   const double theta_max = o.theta_max_fact * fmax(1.0, theta0);
   const double theta_min = o.theta_min_fact * fmax(1.0, theta0);
   int nfilt = 0;
@@ -1581,10 +1883,11 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   OptErr e0;
 #pragma unroll 1
   for (;;) {
-    e0 = opt_error(a, 0.0, obj_scale);
-    if (!(e0.err == e0.err) || !(fx == fx)) { status = MPCX_INVALID_NUMBER; break; }
-    if (e0.err <= o.tol && e0.dual_u <= o.dual_inf_tol && e0.primal_u <= o.constr_viol_tol &&
-        e0.compl_ <= o.compl_inf_tol) {
+    e0 = opt_error(a, obj_scale);
+    const double err0 = e0.err_at(0.0);
+    if (!(err0 == err0) || !(fx == fx)) { status = MPCX_INVALID_NUMBER; break; }
+    if (err0 <= o.tol && e0.dual_u <= o.dual_inf_tol && e0.primal_u <= o.constr_viol_tol &&
+        e0.compl_at(0.0) <= o.compl_inf_tol) {
       status = MPCX_SOLVE_SUCCEEDED;
       break;
     }
@@ -1592,16 +1895,14 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     // barrier parameter update (monotone Fiacco-McCormick)
 #pragma unroll 1
     for (int mu_up = 0; mu_up < 64; ++mu_up) {
-      const OptErr em = opt_error(a, mu, obj_scale);
-      if (em.err > o.kappa_eps * mu || mu <= o.mu_min) break;
+      if (e0.err_at(mu) > o.kappa_eps * mu || mu <= o.mu_min) break;
       mu = fmax(o.tol / 10.0, fmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
       mu = fmax(mu, o.mu_min);
       tau = fmax(o.tau_min, 1.0 - mu);
       nfilt = 0;
     }
     PROF(2);
-    eval_hess(a, a.x(), obj_scale);
-    sync();
+    eval_hess(a, obj_scale);
     PROF(3);
     rhs_primal(a, mu, obj_scale);
     PROF(4);
@@ -1610,8 +1911,9 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     bool ok = false;
 #pragma unroll 1
     for (int attempt = 0; attempt < 60; ++attempt) {
+      rhs_dual(a, mu, dw);
       KKTDiag kd{dw, dc, NEWTON};
-      const Inertia in = factor_chain(a, kd);
+      const Inertia in = factor(a, kd);
       n_fact++;
       if (in.pos == N * NP && in.neg == M && in.zero == 0) {
         if (attempt > 0) dw_last = dw;
@@ -1629,89 +1931,61 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     }
     PROF(5);
     if (!ok) { status = MPCX_ERROR_IN_STEP; break; }
-    rhs_dual(a, mu, dw);
-    solve_chain(a, NEWTON);
+    solve(a);
     PROF(6);
     const StepInfo st = recover_step(a, mu, tau, dw, obj_scale);
     PROF(7);
     // filter line search
-    const double theta = theta_of(a, a.gv(), a.s());
-    const double phi = fx - mu * barrier_of(a, a.x(), a.s());
-    const double gphid = st.gphid;
-    double amin;
-    if (gphid < 0 && theta <= theta_min)
-      amin = o.alpha_min_frac * fmin(fmin(o.gamma_theta, o.gamma_phi * theta / (-gphid)),
-                                     o.delta * pow(theta, o.s_theta) / pow(-gphid, o.s_phi));
-    else if (gphid < 0)
-      amin = o.alpha_min_frac * fmin(o.gamma_theta, o.gamma_phi * theta / (-gphid));
-    else
-      amin = o.alpha_min_frac * o.gamma_theta;
-    double alpha = st.amax;
-    Trial tr{0.0, 0.0, 0.0};
-    bool accepted = false, ftype = false;
-    if (!(amin > 0.0)) amin = o.alpha_min_frac * o.gamma_theta;  // NaN guard
-#pragma unroll 1
-    for (int ls = 0; ls < 64; ++ls) {
-      tr = trial_point(a, alpha, mu, obj_scale);
-      n_trials++;
-      bool okt = (tr.theta <= theta_max) && (tr.phi == tr.phi);
-      for (int j = 0; j < nfilt && okt; ++j)
-        if (tr.theta >= L.fth[j] && tr.phi >= L.fph[j]) okt = false;
-      if (okt) {
-        const bool switching = gphid < 0 && alpha * pow(-gphid, o.s_phi) > o.delta * pow(theta, o.s_theta);
-        if (theta <= theta_min && switching) {
-          okt = tr.phi <= phi + o.eta_phi * alpha * gphid;
-          ftype = true;
-        } else {
-          okt = tr.theta <= (1.0 - o.gamma_theta) * theta || tr.phi <= phi - o.gamma_phi * theta;
-          ftype = false;
-        }
-      }
-      if (okt) { accepted = true; break; }
-      alpha *= 0.5;
-      if (alpha < amin) break;
-    }
-    if (!accepted) { nfilt = 0; ftype = true; n_fallback++; }
+    const double theta = st.theta;
+    const double phi = fx - mu * st.barrier;
+    const LSOpt lso{o.alpha_min_frac, o.gamma_theta, o.gamma_phi, o.delta, o.s_theta, o.s_phi, o.eta_phi};
+    const LSResult ls = line_search(a, lso, mu, obj_scale, st.amax, st.gphid, theta, phi, theta_min,
+                                    theta_max, nfilt);
+    n_trials += ls.trials;
+    bool ftype = ls.ftype;
+    if (!ls.accepted) { nfilt = 0; ftype = true; n_fallback++; }
     if (!ftype) {
       if (nfilt == MAXF) {
         if (lane == 0)
-          for (int j = 1; j < MAXF; ++j) { L.fth[j - 1] = L.fth[j]; L.fph[j - 1] = L.fph[j]; }
+          for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
         nfilt--;
       }
-      if (lane == 0) { L.fth[nfilt] = (1.0 - o.gamma_theta) * theta; L.fph[nfilt] = phi - o.gamma_phi * theta; }
+      if (lane == 0) { gL.fth[nfilt] = (1.0 - o.gamma_theta) * theta; gL.fph[nfilt] = phi - o.gamma_phi * theta; }
       nfilt++;
-      sync();
+      wsync();
     }
     PROF(8);
-    accept_step(a, o, mu, alpha, st.az);
-    fx = tr.f;
-    eval_gj(a, a.x());
+    accept_step(a, o.kappa_sigma, mu, ls.alpha, st.az);
+    fx = ls.tr.f;
+    eval_gj_lds(a);
     sync();
     it++;
     PROF(9);
   }
 
   // ---- outputs ----------------------------------------------------------------
-  double* wio = args.w + (long)agent * NW;
+  gdbl* wio = (gdbl*)args.w + (long)agent * NW;
   for (int i = lane; i < NW; i += WAVE) {
     wio[i] = a.x()[i];
     if (args.lam_w != nullptr)
-      args.lam_w[(long)agent * NW + i] = (i < NX) ? 0.0 : (a.zU()[i] - a.zL()[i]) / obj_scale;
+      ((gdbl*)args.lam_w)[(long)agent * NW + i] = (i < NX) ? 0.0 : (a.zU()[i] - a.zL()[i]) / obj_scale;
   }
 #ifdef MPCX_PROFILE
   PROF(2);
   for (int i = 0; i < 6; ++i) _prof[10 + i] = gL.sprof[i];
+  sync();
   if (args.lam_w != nullptr && lane == 0)
-    for (int i = 0; i < 16 && i < NW; ++i) args.lam_w[(long)agent * NW + i] = _prof[i];
+    for (int i = 0; i < 16 && i < NW; ++i) ((gdbl*)args.lam_w)[(long)agent * NW + i] = _prof[i];
 #endif
   if (args.lam_g != nullptr)
-    for (int c = lane; c < M; c += WAVE) args.lam_g[(long)agent * M + c] = a.lam()[c] * a.gs()[c] / obj_scale;
+    for (int c = lane; c < M; c += WAVE)
+      ((gdbl*)args.lam_g)[(long)agent * M + c] = a.lam()[c] * a.gs()[c] / obj_scale;
   if (args.stats != nullptr && lane == 0) {
     mpcx_stats st;
     st.obj = fx / obj_scale;
     st.primal_inf = e0.primal_u;
     st.dual_inf = e0.dual_u;
-    st.compl_inf = e0.compl_;
+    st.compl_inf = e0.compl_at(0.0);
     st.mu = mu;
     st.obj_scale = obj_scale;
     st.iter_count = it;

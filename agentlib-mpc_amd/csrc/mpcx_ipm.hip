@@ -905,6 +905,7 @@ __device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F
 struct BKOut {
   int pos, neg, zero, bad;
 };
+constexpr int CPL = (RB + G - 1) / G;  // trailing columns per lane (at most RB of them)
 __device__ __noinline__ BKOut interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g) {
   Inertia in{0, 0, 0};
   int bad = 0;
@@ -914,9 +915,11 @@ __device__ __noinline__ BKOut interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g)
     double akk = absn(F[pko(k) + k]);
     double lam = -1.0;
     int r = -1;
-    for (int i = k + 1 + g; i < NI; i += G) {
-      const double t = absn(F[pko(i) + k]);
-      if (t > lam) { lam = t; r = i; }
+#pragma unroll
+    for (int u = 0; u < (NI + G - 1) / G; ++u) {
+      const int i = k + 1 + g + u * G;
+      const double t = absn(F[pko(i < NI ? i : k) + k]);
+      if (i < NI && t > lam) { lam = t; r = i; }
     }
     gargmax<G>(lam, r);
     if (r < 0) lam = 0.0;
@@ -961,6 +964,10 @@ __device__ __noinline__ BKOut interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g)
       if (g == 0) { const int t = perm[p]; perm[p] = perm[q]; perm[q] = t; }
       wsync();
     }
+    // trailing update, column-oriented: lane g owns columns j = k+size+g+u*G and keeps
+    // their multipliers in registers; rows in batches of 4 (all reads, then writes);
+    // predicated-off writes go to the unused (rhs, rhs) corner instead of branching
+    const int DUMMY = pko(RB) + RB;
     if (size == 1) {
       const double d = F[pko(k) + k];
       if (fabs(d) <= ZERO_PIVOT) {
@@ -972,31 +979,38 @@ __device__ __noinline__ BKOut interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g)
         in.neg++;
       }
       const double rd = 1.0 / d;
-      const int m = RB - k;  // rows k+1 .. RB, paired (short with long) for balance
-      for (int base = 0; base < m; base += 2 * G) {
+      int jj[CPL];
+      double lj[CPL];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int o = base + (h == 0 ? g : 2 * G - 1 - g);
-          if (o < m) {
-            const int i = k + 1 + o, ri = pko(i);
-            const double lik = F[ri + k] * rd;
-            for (int j0 = k + 1; j0 <= i; j0 += 4) {
-              double av[4], bv[4];
+      for (int u = 0; u < CPL; ++u) {
+        const int j = k + 1 + g + u * G;
+        jj[u] = j;
+        lj[u] = (j <= RB) ? F[pko(j <= RB ? j : RB) + k] * rd : 0.0;
+      }
+#pragma unroll 1
+      for (int i0 = k + 1; i0 <= RB; i0 += 4) {
+        double aik[4], av[4][CPL];
+        int rr[4];
 #pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                const int j = (j0 + u <= i) ? j0 + u : i;
-                av[u] = F[ri + j];
-                bv[u] = F[pko(j) + k];
-              }
+        for (int b = 0; b < 4; ++b) {
+          const int ii = (i0 + b <= RB) ? i0 + b : RB;
+          rr[b] = pko(ii);
+          aik[b] = F[rr[b] + k];
 #pragma unroll
-              for (int u = 0; u < 4; ++u)
-                if (j0 + u <= i) F[ri + j0 + u] = av[u] - lik * bv[u];
-            }
+          for (int u = 0; u < CPL; ++u) av[b][u] = F[rr[b] + (jj[u] <= ii ? jj[u] : ii)];
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+#pragma unroll
+          for (int u = 0; u < CPL; ++u) {
+            const bool on = (i0 + b <= RB) && (jj[u] <= i0 + b);
+            F[on ? rr[b] + jj[u] : DUMMY] = av[b][u] - aik[b] * lj[u];
           }
         }
       }
       wsync();
-      for (int i = k + 1 + g; i <= RB; i += G) F[pko(i) + k] *= rd;
+#pragma unroll
+      for (int u = 0; u < CPL; ++u) F[jj[u] <= RB ? pko(jj[u]) + k : DUMMY] = lj[u];
       if (g == 0) piv[k] = 1;
     } else {
       const int ok = pko(k), ok1 = pko(k + 1);
@@ -1013,38 +1027,45 @@ __device__ __noinline__ BKOut interior_bk(ldsd* F, ldsi* perm, ldsi* piv, int g)
         in.neg += 2;
       }
       const double rdet = 1.0 / det;
-      const int m = RB - 1 - k;  // rows k+2 .. RB
-      for (int base = 0; base < m; base += 2 * G) {
+      int jj[CPL];
+      double l1[CPL], l2[CPL];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int o = base + (h == 0 ? g : 2 * G - 1 - g);
-          if (o < m) {
-            const int i = k + 2 + o, ri = pko(i);
-            const double ai1 = F[ri + k], ai2 = F[ri + k + 1];
-            const double l1 = (ai1 * a22 - ai2 * a21) * rdet, l2 = (ai2 * a11 - ai1 * a21) * rdet;
-            for (int j0 = k + 2; j0 <= i; j0 += 4) {
-              double av[4], b1[4], b2[4];
+      for (int u = 0; u < CPL; ++u) {
+        const int j = k + 2 + g + u * G;
+        jj[u] = j;
+        const int oj = pko(j <= RB ? j : RB);
+        const double aj1 = F[oj + k], aj2 = F[oj + k + 1];
+        l1[u] = (j <= RB) ? (aj1 * a22 - aj2 * a21) * rdet : 0.0;
+        l2[u] = (j <= RB) ? (aj2 * a11 - aj1 * a21) * rdet : 0.0;
+      }
+#pragma unroll 1
+      for (int i0 = k + 2; i0 <= RB; i0 += 4) {
+        double ai1[4], ai2[4], av[4][CPL];
+        int rr[4];
 #pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                const int j = (j0 + u <= i) ? j0 + u : i;
-                const int oj = pko(j);
-                av[u] = F[ri + j];
-                b1[u] = F[oj + k];
-                b2[u] = F[oj + k + 1];
-              }
+        for (int b = 0; b < 4; ++b) {
+          const int ii = (i0 + b <= RB) ? i0 + b : RB;
+          rr[b] = pko(ii);
+          ai1[b] = F[rr[b] + k];
+          ai2[b] = F[rr[b] + k + 1];
 #pragma unroll
-              for (int u = 0; u < 4; ++u)
-                if (j0 + u <= i) F[ri + j0 + u] = av[u] - (l1 * b1[u] + l2 * b2[u]);
-            }
+          for (int u = 0; u < CPL; ++u) av[b][u] = F[rr[b] + (jj[u] <= ii ? jj[u] : ii)];
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+#pragma unroll
+          for (int u = 0; u < CPL; ++u) {
+            const bool on = (i0 + b <= RB) && (jj[u] <= i0 + b);
+            F[on ? rr[b] + jj[u] : DUMMY] = av[b][u] - (ai1[b] * l1[u] + ai2[b] * l2[u]);
           }
         }
       }
       wsync();
-      for (int i = k + 2 + g; i <= RB; i += G) {
-        const int ri = pko(i);
-        const double ai1 = F[ri + k], ai2 = F[ri + k + 1];
-        F[ri + k] = (ai1 * a22 - ai2 * a21) * rdet;
-        F[ri + k + 1] = (ai2 * a11 - ai1 * a21) * rdet;
+#pragma unroll
+      for (int u = 0; u < CPL; ++u) {
+        const int oj = jj[u] <= RB ? pko(jj[u]) : pko(RB);
+        F[jj[u] <= RB ? oj + k : DUMMY] = l1[u];
+        F[jj[u] <= RB ? oj + k + 1 : DUMMY] = l2[u];
       }
       if (g == 0) { piv[k] = 2; piv[k + 1] = 0; }
     }
@@ -1064,11 +1085,18 @@ __device__ __noinline__ void trailing_backsolve(ldsd* F, const ldsi* piv, int g)
     double vt[NTR];
 #pragma unroll
     for (int t = 0; t < NTR; ++t) vt[t] = F[pko(NI + t) + m];
-    for (int i = g; i < m; i += G) {
-      if (i == skip) continue;
-      const double lmi = F[om + i];
+    const int DUMMY = pko(RB) + RB;
 #pragma unroll
-      for (int t = 0; t < NTR; ++t) F[pko(NI + t) + i] -= lmi * vt[t];
+    for (int u = 0; u < (NI + G - 1) / G; ++u) {
+      const int i = g + u * G;
+      const bool on = i < m && i != skip;
+      const int ic = i < m ? i : 0;
+      const double lmi = F[om + ic];
+      double cur[NTR];
+#pragma unroll
+      for (int t = 0; t < NTR; ++t) cur[t] = F[pko(NI + t) + ic];
+#pragma unroll
+      for (int t = 0; t < NTR; ++t) F[on ? pko(NI + t) + ic : DUMMY] = cur[t] - lmi * vt[t];
     }
     wsync();
   }

@@ -1,0 +1,433 @@
+"""Fleet ADMM drivers: coordinated (consensus/exchange) and decentralised ADMM over
+device-resident fleets of agents, partitioned by agent across GPUs.
+
+The reference runs one agentlib module per agent and moves trajectories between
+them as JSON messages; every agent solves its own NLP through ``backend.solve``
+(SURVEY §3.C/§3.D).  Here all agents of one problem structure ("class") are
+solved by ONE batched kernel launch, their coupling trajectories never leave
+HBM, and the consensus/exchange arithmetic runs as HIP kernels.  Semantics
+follow, step for step:
+
+* coordinated ADMM — ``ADMMCoordinator._fast_process``
+  (`modules/dmpc/admm/admm_coordinator.py:259-321`): mean update from the last
+  locals, shift (:323-337), then per iteration trigger → local solves
+  (``CoordinatedADMM.optimize``, `admm_coordinated.py:133-193`) → mean update →
+  multiplier update (:339-347) → residual check with optional penalty variation
+  (:354-435, :467-479); ρ reset after the round (:665).
+* decentralised ADMM — ``LocalADMM.process`` (`modules/dmpc/admm/admm.py:873-937`):
+  shift and send locals and multipliers (:329-375), mean / mean-diff from the
+  shifted locals, then ``max_iterations`` × (solve → mean → multiplier update).
+
+Multi-GPU: one process per GPU, each holding a contiguous slice of every
+class's agents.  Aliases whose participants live on several ranks are "global
+groups"; their per-(group, t) moments (and the residual partial sums of the
+rank-local groups) travel in ONE ``all_reduce(SUM)`` per ADMM iteration
+(`include/mpcx.h`, ``mpcx_admm_moments``).  No other collective is on the data
+path.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import math
+import time
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+
+from agentlib_mpc_amd.data_structures import admm_datatypes as adt
+from agentlib_mpc_amd.runtime.native import ADMM_TOTALS, STATS_BYTES
+
+CONSENSUS = "consensus"
+EXCHANGE = "exchange"
+NMOM = 5
+_STATUS_WORD = 13  # int32 index of mpcx_stats.status (6 doubles + iter_count)
+
+
+@dataclasses.dataclass
+class Slot:
+    """One coupling of one class: where its trajectory lives in w and p."""
+
+    name: str
+    kind: str
+    aliases: List[str]
+    initial: np.ndarray           # [n] initial value of the local trajectory
+    w_cols: np.ndarray            # [T] columns of the local trajectory in w
+    mean_cols: np.ndarray         # [T] columns of the mean (consensus) / mean diff (exchange) in p
+    mult_cols: np.ndarray         # [T] columns of the multiplier in p
+
+
+def _local_cols(lay, comp: int) -> List[int]:
+    """w columns of ``Results[name]`` (first occurrence of every grid time >= 0)."""
+    seen, cols = set(), []
+    for j, t in enumerate(lay.grid):
+        if t >= 0 and t not in seen:
+            seen.add(t)
+            cols.append(lay.columns[j][comp])
+    return cols
+
+
+class FleetClass:
+    """All agents (on this rank) that share one problem structure.
+
+    ``backend`` is a set-up :class:`MI355XADMMBackend`; ``inputs`` the cold-start
+    NLP inputs ``(p, lbw, ubw, w0)`` as [n, .] arrays (e.g. from
+    :func:`~agentlib_mpc_amd.optimization_backends.problem.fleet_nlp_inputs`).
+    ``aliases`` maps a coupling/exchange variable name to its alias — one string
+    for all agents or one per agent (default: the variable name).  ``initial``
+    maps it to the initial local value (scalar or per agent), which the reference
+    takes from the module config (`admm_coordinated.py:226-238`, `admm.py:700-780`).
+    """
+
+    def __init__(self, name: str, backend, inputs, aliases: Optional[Dict[str, Union[str, Sequence[str]]]] = None,
+                 initial: Optional[Dict[str, Union[float, Sequence[float]]]] = None):
+        self.name = name
+        self.backend = backend
+        p, lbw, ubw, w0 = (np.ascontiguousarray(a, dtype=np.float64) for a in inputs)
+        self.p0, self.lbw, self.ubw, self.w0 = p, lbw, ubw, w0
+        self.n = p.shape[0]
+        prob = backend.problem
+        nlp = prob.nlp
+        sysm = backend.system
+        aliases = aliases or {}
+        initial = initial or {}
+        self.slots: List[Slot] = []
+        ref = backend.var_ref
+        specs = [(c.name, CONSENSUS, c.mean, c.multiplier, "local_couplings", "global_couplings", "multipliers")
+                 for c in getattr(ref, "couplings", [])]
+        specs += [(c.name, EXCHANGE, c.mean_diff, c.multiplier, "local_exchange", "average_diff",
+                   "exchange_multipliers") for c in getattr(ref, "exchange", [])]
+        groups = {q.name: q for q in sysm.quantities}
+        for name, kind, mean_name, mult_name, vg, mg, lg in specs:
+            comp = groups[vg].full_names.index(name)
+            w_cols = _local_cols(nlp.var_groups[vg], comp)
+            mlay, llay = nlp.par_groups[mg], nlp.par_groups[lg]
+            mean_cols = [c[groups[mg].full_names.index(mean_name)] for c in mlay.columns]
+            mult_cols = [c[groups[lg].full_names.index(mult_name)] for c in llay.columns]
+            if not (len(w_cols) == len(mean_cols) == len(mult_cols)):
+                raise ValueError(f"{name}: trajectory lengths differ (local {len(w_cols)}, mean "
+                                 f"{len(mean_cols)}, multiplier {len(mult_cols)})")
+            al = aliases.get(name, name)
+            al = [al] * self.n if isinstance(al, str) else list(al)
+            if len(al) != self.n:
+                raise ValueError(f"{name}: {len(al)} aliases for {self.n} agents")
+            init = np.broadcast_to(np.asarray(initial.get(name, 0.0), float), (self.n,)).copy()
+            self.slots.append(Slot(name, kind, al, init, np.asarray(w_cols, np.int32),
+                                   np.asarray(mean_cols, np.int32), np.asarray(mult_cols, np.int32)))
+        if not self.slots:
+            raise ValueError(f"class {name}: backend has no couplings or exchange variables")
+        self.rho_col = int(nlp.par_groups[sysm.penalty_factor.name].columns[0][0])
+        self.T = len(self.slots[0].w_cols)
+        opts = backend.config.discretization_options
+        self.horizon = int(opts.prediction_horizon)
+        self.time_step = float(opts.time_step)
+        self.coupling_grid = list(backend.coupling_grid)
+
+    @property
+    def native(self):
+        return self.backend._native()
+
+
+@dataclasses.dataclass
+class IterationRecord:
+    primal_residual: float
+    dual_residual: float
+    penalty: float
+    converged_solves: Optional[int] = None
+
+
+class ADMMFleet:
+    """Device-resident ADMM over fleets of agents (one or more classes).
+
+    ``ops`` is the device backend (default :class:`~agentlib_mpc_amd.admm.ops.NativeADMMOps`);
+    ``comm`` a ``torch.distributed`` process group (or ``None`` for one GPU / the
+    default group when the default group is initialised and ``comm="default"``).
+    """
+
+    def __init__(self, classes: Sequence[FleetClass], device=None, ops=None, comm=None):
+        import torch
+
+        self.torch = torch
+        self.classes = list(classes)
+        if ops is None:
+            from agentlib_mpc_amd.admm.ops import NativeADMMOps
+
+            ops = NativeADMMOps()
+        self.ops = ops
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.dist = None
+        if comm is not None:
+            import torch.distributed as dist
+
+            self.dist = dist
+            self.group = None if comm == "default" else comm
+            self.world = dist.get_world_size(self.group)
+        else:
+            self.world = 1
+        T = {c.T for c in self.classes}
+        if len(T) != 1:
+            raise ValueError(f"all coupling trajectories must have one length, got {sorted(T)}")
+        self.T = T.pop()
+        self._build_groups()
+        self._allocate()
+        self.history: List[IterationRecord] = []
+        self.rounds = 0
+
+    # ------------------------------------------------------------------ setup
+    def _build_groups(self):
+        kinds: Dict[str, str] = {}
+        parts = []  # (alias, class idx, slot idx, agent idx)
+        for ci, c in enumerate(self.classes):
+            for si, s in enumerate(c.slots):
+                for a, al in enumerate(s.aliases):
+                    if kinds.setdefault(al, s.kind) != s.kind:
+                        raise ValueError(f"alias {al!r} mixes consensus and exchange participants")
+                    parts.append((al, ci, si, a))
+        local_aliases = sorted(kinds)
+        if self.world > 1:
+            gathered = [None] * self.world
+            self.dist.all_gather_object(gathered, sorted(kinds.items()), group=self.group)
+            count: Dict[str, int] = {}
+            all_kinds: Dict[str, str] = {}
+            for lst in gathered:
+                for al, k in lst:
+                    count[al] = count.get(al, 0) + 1
+                    if all_kinds.setdefault(al, k) != k:
+                        raise ValueError(f"alias {al!r} mixes consensus and exchange participants")
+            global_aliases = sorted(al for al, n in count.items() if n > 1)
+            self.global_kinds = {al: all_kinds[al] for al in global_aliases}
+        else:
+            global_aliases = []
+            self.global_kinds = {}
+        gset = set(global_aliases)
+        order = global_aliases + [al for al in local_aliases if al not in gset]
+        self.n_global = len(global_aliases)
+        self.aliases = order
+        gid = {al: i for i, al in enumerate(order)}
+        G = len(order)
+        self.G = G
+        kind_of = dict(self.global_kinds)
+        kind_of.update(kinds)
+        self.exchange_flags = np.array([1 if kind_of[al] == EXCHANGE else 0 for al in order], np.int32)
+        parts.sort(key=lambda x: gid[x[0]])  # stable: class, slot, agent order inside a group
+        counts = np.zeros(G, np.int64)
+        rows = {}
+        for r, (al, ci, si, a) in enumerate(parts):
+            counts[gid[al]] += 1
+            rows[(ci, si, a)] = r
+        self.R = len(parts)
+        self.gstart = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+        self.max_rows = int(counts.max()) if G else 0
+        self.slot_rows = {}
+        self.slot_groups = {}
+        for ci, c in enumerate(self.classes):
+            for si, s in enumerate(c.slots):
+                self.slot_rows[(ci, si)] = np.array([rows[(ci, si, a)] for a in range(c.n)], np.int32)
+                self.slot_groups[(ci, si)] = np.array([gid[al] for al in s.aliases], np.int32)
+
+    def _allocate(self):
+        t = self.torch
+        dev, f64, i32 = self.device, t.float64, t.int32
+        T, G, R = self.T, self.G, max(self.R, 1)
+        self.X = t.zeros((R, T), dtype=f64, device=dev)          # local trajectories
+        self.LAMR = t.zeros((R, T), dtype=f64, device=dev)       # consensus multipliers per participant
+        self.DIFF = t.zeros((R, T), dtype=f64, device=dev)       # exchange mean diffs per participant
+        self.MEAN = t.zeros((max(G, 1), T), dtype=f64, device=dev)
+        self.DMEAN = t.zeros((max(G, 1), T), dtype=f64, device=dev)
+        self.GMULT = t.zeros((max(G, 1), T), dtype=f64, device=dev)  # exchange multiplier per alias
+        self.EXCH = t.as_tensor(self.exchange_flags if G else np.zeros(1, np.int32), dtype=i32, device=dev)
+        self.GSTART = t.as_tensor(self.gstart, dtype=i32, device=dev)
+        self.S = NMOM * T + 1
+        self.MOM = t.zeros(self.ops.moments_size(max(G, 1), T), dtype=f64, device=dev)
+        self.totals_off = self.n_global * self.S
+        self.reduce_len = self.n_global * self.S + ADMM_TOTALS
+        for ci, c in enumerate(self.classes):
+            c.P = t.as_tensor(c.p0, device=dev).contiguous()
+            c.LB = t.as_tensor(c.lbw, device=dev).contiguous()
+            c.UB = t.as_tensor(c.ubw, device=dev).contiguous()
+            c.W = t.as_tensor(c.w0, device=dev).contiguous()
+            c.LAMG = t.zeros((c.n, c.backend.problem.nlp.ng_total), dtype=f64, device=dev)
+            c.ST = t.zeros(c.n * STATS_BYTES, dtype=t.uint8, device=dev)
+            c.dev_slots = []
+            for si, s in enumerate(c.slots):
+                c.dev_slots.append({
+                    "w_cols": t.as_tensor(s.w_cols, dtype=i32, device=dev),
+                    "mean_cols": t.as_tensor(s.mean_cols, dtype=i32, device=dev),
+                    "mult_cols": t.as_tensor(s.mult_cols, dtype=i32, device=dev),
+                    "rows": t.as_tensor(self.slot_rows[(ci, si)], dtype=i32, device=dev),
+                    "groups": t.as_tensor(self.slot_groups[(ci, si)], dtype=i32, device=dev),
+                })
+        # initial local trajectories (registration, `admm_coordinator.py:528-560`;
+        # `admm.py:356-375`): the configured value repeated over the coupling grid
+        x0 = np.zeros((R, T))
+        for ci, c in enumerate(self.classes):
+            for si, s in enumerate(c.slots):
+                x0[self.slot_rows[(ci, si)]] = s.initial[:, None]
+        self.X.copy_(t.as_tensor(x0, device=dev))
+        self._ok_count = t.zeros(1, dtype=t.int64, device=dev)
+
+    def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
+                   ubw: Optional[np.ndarray] = None):
+        """New measurements/forecasts for the next control step (host -> HBM)."""
+        c = next(c for c in self.classes if c.name == class_name)
+        c.P.copy_(self.torch.as_tensor(p))
+        if lbw is not None:
+            c.LB.copy_(self.torch.as_tensor(lbw))
+        if ubw is not None:
+            c.UB.copy_(self.torch.as_tensor(ubw))
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            self.torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ steps
+    def _solve_all(self, rho: float):
+        """Inject mean/diff, multipliers and rho into every agent's p; solve; gather locals."""
+        ops, T = self.ops, self.T
+        for ci, c in enumerate(self.classes):
+            for si, s in enumerate(c.slots):
+                d = c.dev_slots[si]
+                if s.kind == CONSENSUS:
+                    ops.scatter_rows(T, self.MEAN, d["groups"], c.P, d["mean_cols"])
+                    ops.scatter_rows(T, self.LAMR, d["rows"], c.P, d["mult_cols"])
+                else:
+                    ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
+                    ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
+            ops.fill_column(c.P, c.rho_col, rho)
+            ops.solve(c)
+            for si, s in enumerate(c.slots):
+                d = c.dev_slots[si]
+                ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows"])
+            st = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)[:, _STATUS_WORD]
+            self._ok_count += ((st == 0) | (st == 1)).sum()
+
+    def _update_means(self, rho: float, apply_multipliers: bool) -> Optional[np.ndarray]:
+        """Mean (+ exchange diffs) from the current locals; with ``apply_multipliers``
+        also the multiplier update. Returns the residual totals when requested."""
+        ops, T, G = self.ops, self.T, self.G
+        if G == 0:
+            return None
+        self.MOM.zero_()
+        ops.moments(G, self.n_global, T, self.GSTART, self.max_rows, self.X, self.LAMR, self.MEAN, self.MOM)
+        totals = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS]
+        exch = self.EXCH if self.exchange_flags.any() else None
+        gm = self.GMULT if exch is not None else None
+        ops.finalize(self.n_global, G, self.n_global, T, self.MOM, exch, gm, rho, self.MEAN, self.DMEAN, totals)
+        if self.world > 1:
+            self.dist.all_reduce(self.MOM[:self.reduce_len], group=self.group)
+        ops.finalize(0, self.n_global, self.n_global, T, self.MOM, exch, gm, rho, self.MEAN, self.DMEAN, totals)
+        if apply_multipliers:
+            ops.consensus_multipliers(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, rho, self.LAMR)
+            # consensus rows of exchange groups are never read; exchange rows of consensus groups neither
+            ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT, rho)
+        else:
+            ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT, 0.0)
+        return totals
+
+    def _shift_all(self, shift: int):
+        ops, T = self.ops, self.T
+        ops.shift(T, shift, self.LAMR)
+        ops.shift(T, shift, self.DIFF)
+        ops.shift(T, shift, self.GMULT)
+
+    # ------------------------------------------------------------------ algorithms
+    def run_coordinated(self, penalty_factor: float, admm_iter_max: int = 20, primal_tol: float = 1e-3,
+                        dual_tol: float = 1e-3, use_relative_tolerances: bool = True, abs_tol: float = 1e-3,
+                        rel_tol: float = 1e-3, penalty_change_threshold: float = -1.0,
+                        penalty_change_factor: float = 2.0) -> dict:
+        """One control step of the coordinator (`admm_coordinator.py:259-321`)."""
+        rho = float(penalty_factor)
+        self._update_means(rho, apply_multipliers=False)
+        shift = int(len(self.classes[0].coupling_grid) / self.classes[0].horizon)
+        self.ops.shift(self.T, shift, self.MEAN)
+        self._shift_all(shift)
+        converged = False
+        it = 0
+        records = []
+        t0 = time.perf_counter()
+        self._ok_count.zero_()
+        for it in range(1, admm_iter_max + 1):
+            self._solve_all(rho)
+            tot = self._update_means(rho, apply_multipliers=True).cpu().numpy()
+            prim, dual = math.sqrt(max(tot[0], 0.0)), math.sqrt(max(tot[1], 0.0))
+            records.append(IterationRecord(prim, dual, rho))
+            if use_relative_tolerances:
+                scale_p = max(math.sqrt(max(tot[2], 0.0)), math.sqrt(max(tot[3], 0.0)))
+                eps_pri = math.sqrt(tot[6]) * abs_tol + rel_tol * scale_p
+                eps_dual = math.sqrt(tot[5]) * abs_tol + rel_tol * math.sqrt(max(tot[4], 0.0))
+                conv = prim < eps_pri and dual < eps_dual
+            else:
+                conv = prim < primal_tol and dual < dual_tol
+            # varying penalty (`admm_coordinator.py:467-479`) before the stopping test,
+            # as _check_convergence does
+            if penalty_change_threshold > 1:
+                if prim > penalty_change_threshold * dual:
+                    rho *= penalty_change_factor
+                elif dual > penalty_change_threshold * prim:
+                    rho /= penalty_change_factor
+            if conv:
+                converged = True
+                break
+        self._sync()
+        wall = time.perf_counter() - t0
+        self.history.extend(records)
+        self.rounds += 1
+        return {"iterations": it, "converged": converged, "records": records, "wall_s": wall,
+                "converged_solves": int(self._ok_count.item())}
+
+    def run_local(self, penalty_factor: float, max_iterations: int, record_residuals: bool = True) -> dict:
+        """One control step of decentralised ADMM (``LocalADMM.process``, `admm.py:873-937`)."""
+        rho = float(penalty_factor)
+        grid = self.classes[0].coupling_grid
+        ts = self.classes[0].time_step
+        shift = next(i for i, t in enumerate(grid) if t >= ts)
+        self.ops.shift(self.T, shift, self.X)   # _shift_and_send_coupling_outputs
+        self.ops.shift(self.T, shift, self.LAMR)  # _shift_multipliers
+        self.ops.shift(self.T, shift, self.GMULT)
+        self._update_means(rho, apply_multipliers=False)  # _set_mean_coupling_values
+        hist = self.torch.zeros((max(max_iterations, 1), ADMM_TOTALS), dtype=self.torch.float64,
+                                device=self.device)
+        t0 = time.perf_counter()
+        self._ok_count.zero_()
+        for it in range(max_iterations):
+            self._solve_all(rho)
+            tot = self._update_means(rho, apply_multipliers=True)
+            if record_residuals and tot is not None:
+                hist[it].copy_(tot)
+        h = hist.cpu().numpy()
+        wall = time.perf_counter() - t0
+        records = [IterationRecord(math.sqrt(max(r[0], 0.0)), math.sqrt(max(r[1], 0.0)), rho)
+                   for r in h[:max_iterations]] if record_residuals else []
+        self.history.extend(records)
+        self.rounds += 1
+        return {"iterations": max_iterations, "converged": None, "records": records, "wall_s": wall,
+                "converged_solves": int(self._ok_count.item())}
+
+    # ------------------------------------------------------------------ outputs
+    def solutions(self, class_name: str) -> np.ndarray:
+        c = next(c for c in self.classes if c.name == class_name)
+        return c.W.cpu().numpy()
+
+    def stats(self, class_name: str) -> list:
+        from agentlib_mpc_amd.runtime.native import stats_to_dicts
+
+        c = next(c for c in self.classes if c.name == class_name)
+        return stats_to_dicts(c.ST.cpu().numpy().tobytes())
+
+    def trajectories(self) -> Dict[str, np.ndarray]:
+        """Mean trajectory per alias (``ConsensusVariable.mean_trajectory``)."""
+        m = self.MEAN.cpu().numpy()
+        return {al: m[i].copy() for i, al in enumerate(self.aliases)}
+
+    def locals_of(self, class_name: str, slot: str) -> np.ndarray:
+        ci = next(i for i, c in enumerate(self.classes) if c.name == class_name)
+        si = next(i for i, s in enumerate(self.classes[ci].slots) if s.name == slot)
+        return self.X.cpu().numpy()[self.slot_rows[(ci, si)]]
+
+    def multipliers_of(self, class_name: str, slot: str) -> np.ndarray:
+        ci = next(i for i, c in enumerate(self.classes) if c.name == class_name)
+        si = next(i for i, s in enumerate(self.classes[ci].slots) if s.name == slot)
+        s = self.classes[ci].slots[si]
+        if s.kind == CONSENSUS:
+            return self.LAMR.cpu().numpy()[self.slot_rows[(ci, si)]]
+        return self.GMULT.cpu().numpy()[self.slot_groups[(ci, si)]]

@@ -1,0 +1,84 @@
+"""Device operations of the ADMM fleet driver: the C-ABI kernels of `libmpcx.so`.
+
+:class:`NativeADMMOps` is the product implementation — every call is one
+stream-ordered launch through `include/mpcx.h` on device tensors (torch is
+only the allocator).  The fleet driver (`admm/fleet.py`) is written against
+this small interface so that its host-side orchestration (partitioning,
+collectives, stopping rules) can also be exercised by CPU tests with a
+test-side implementation; there is no CPU implementation in the package.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+from agentlib_mpc_amd.runtime import native
+
+
+def _p(t) -> Optional[ctypes.c_void_p]:
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class NativeADMMOps:
+    """ADMM arithmetic + NLP solves on the GPU (C ABI, HIP kernels)."""
+
+    def __init__(self, stream=None):
+        self.lib = native.load_library()
+        self._stream = stream
+
+    @property
+    def stream(self):
+        import torch
+
+        s = self._stream if self._stream is not None else torch.cuda.current_stream()
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def _chk(self, rc, name):
+        if rc != 0:
+            raise native.NativeError(f"{name} failed ({rc})")
+
+    # -- NLP solves ---------------------------------------------------------------------
+    def solve(self, cls) -> None:
+        cls.native.solve(cls.P, cls.LB, cls.UB, cls.W, lam_g=cls.LAMG, stats=cls.ST,
+                         stream=self.stream.value)
+
+    # -- moves ---------------------------------------------------------------------------
+    def gather_rows(self, T, src, cols, dst, dst_rows):
+        self._chk(self.lib.mpcx_gather_rows(src.shape[0], T, _p(src), src.shape[1], _p(cols), _p(dst),
+                                            _p(dst_rows), self.stream), "mpcx_gather_rows")
+
+    def scatter_rows(self, T, src, src_rows, dst, cols):
+        self._chk(self.lib.mpcx_scatter_rows(dst.shape[0], T, _p(src), _p(src_rows), _p(dst), dst.shape[1],
+                                             _p(cols), self.stream), "mpcx_scatter_rows")
+
+    def fill_column(self, dst, col, value):
+        self._chk(self.lib.mpcx_fill_column(dst.shape[0], _p(dst), dst.shape[1], col, float(value),
+                                            self.stream), "mpcx_fill_column")
+
+    # -- ADMM arithmetic -------------------------------------------------------------------
+    def moments_size(self, n_groups, T) -> int:
+        return int(self.lib.mpcx_admm_moments_size(n_groups, T))
+
+    def moments(self, n_groups, n_global, T, gstart, max_rows, X, LAM, center, out):
+        self._chk(self.lib.mpcx_admm_moments(n_groups, n_global, T, _p(gstart), max_rows, _p(X), _p(LAM),
+                                             _p(center), _p(out), self.stream), "mpcx_admm_moments")
+
+    def finalize(self, g0, g1, n_global, T, mom, exchange, gmult, rho, mean, dmean, totals):
+        self._chk(self.lib.mpcx_admm_finalize(g0, g1, n_global, T, _p(mom), _p(exchange), _p(gmult),
+                                              float(rho), _p(mean), _p(dmean), _p(totals), self.stream),
+                  "mpcx_admm_finalize")
+
+    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho, LAM):
+        self._chk(self.lib.mpcx_admm_consensus_multipliers(n_groups, T, _p(gstart), max_rows, _p(X),
+                                                           _p(mean), float(rho), _p(LAM), None,
+                                                           self.stream),
+                  "mpcx_admm_consensus_multipliers")
+
+    def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, rho):
+        self._chk(self.lib.mpcx_admm_exchange_update(n_groups, T, _p(gstart), max_rows, _p(X), _p(mean),
+                                                     _p(diff), _p(gmult), float(rho), self.stream),
+                  "mpcx_admm_exchange_update")
+
+    def shift(self, T, shift, x):
+        self._chk(self.lib.mpcx_admm_shift(x.shape[0], T, shift, _p(x), self.stream), "mpcx_admm_shift")

@@ -168,3 +168,73 @@ def compile_all(verbose: bool = False):
         if verbose:
             print(f"[mpcx] {name}: {paths[name].name}")
     return paths
+
+
+# ---------------------------------------------------------------------------
+# ADMM fleets (C2 scaled, C4)
+# ---------------------------------------------------------------------------
+C2_ROOMS = [  # (d, T0) of examples/4_Room_ADMM_Coordinator/configs/room_{1..4}_admm.json
+    (150.0, 296.0), (100.0, 298.0), (50.0, 301.0), (10.0, 303.0)]
+C4_ROOMS = C2_ROOMS  # examples/exchange_admm/configs/room_{1..4}_admm.json
+
+
+def _class_inputs(be, cv, overrides, n):
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+
+    if not overrides:
+        overrides = {next(iter(cv)): np.full(n, cv[next(iter(cv))].value, float)}
+    return fleet_nlp_inputs(be.problem, cv, {k: np.asarray(v, float) for k, v in overrides.items()})
+
+
+def c2_fleet_classes(n_blocks=1, N=10, rho=0.4, seed=None, block_offset=0, solver_options=TIGHT):
+    """Coordinated consensus fleet: ``n_blocks`` x (4 rooms + 1 air handler) of
+    `examples/4_Room_ADMM_Coordinator` (block 0 = the example's values; further
+    blocks d~U(10,150), T0~U(296,303) from ``default_rng([seed, block])``).
+    Returns the FleetClass list [rooms, air handlers]."""
+    from agentlib_mpc_amd.admm.fleet import FleetClass
+
+    d, T0, aliases = [], [], []
+    for b in range(block_offset, block_offset + n_blocks):
+        rng = np.random.default_rng([seed, b]) if seed is not None else None
+        for i, (d_i, t_i) in enumerate(C2_ROOMS):
+            if b == 0 or rng is None:
+                d.append(d_i); T0.append(t_i)
+            else:
+                d.append(rng.uniform(10.0, 150.0)); T0.append(rng.uniform(296.0, 303.0))
+            aliases.append(f"mDot{i + 1}_coupling_b{b}")
+    be_r, cv_r = admm_room(N=N, rho=rho, solver_options=solver_options)
+    nr = 4 * n_blocks
+    rooms = FleetClass("room", be_r, _class_inputs(be_r, cv_r, {"T": T0, "d": d}, nr),
+                       aliases={"mDot": aliases}, initial={"mDot": 0.02})
+    be_a, cv_a = admm_ahu(N=N, rho=rho, solver_options=solver_options)
+    blocks = range(block_offset, block_offset + n_blocks)
+    ahu = FleetClass("ahu", be_a, _class_inputs(be_a, cv_a, {}, n_blocks),
+                     aliases={f"mDot_out_{i + 1}": [f"mDot{i + 1}_coupling_b{b}" for b in blocks]
+                              for i in range(4)},
+                     initial={f"mDot_out_{i + 1}": 0.01 for i in range(4)})
+    return [rooms, ahu]
+
+
+def c4_fleet_classes(n_rooms=4, n_supply=1, N=10, rho=1e4, seed=None, solver_options=TIGHT):
+    """Exchange fleet of `examples/exchange_admm` (one alias ``mDot_coupling``):
+    rooms (first four = the example's values, further d~U(10,150), T0~U(296,303))
+    and supply units (penalty 0.1)."""
+    from agentlib_mpc_amd.admm.fleet import FleetClass
+
+    rng = np.random.default_rng(seed)
+    d, T0 = [], []
+    for i in range(n_rooms):
+        if i < 4 and seed is None:
+            d.append(C4_ROOMS[i][0]); T0.append(C4_ROOMS[i][1])
+        else:
+            d.append(rng.uniform(10.0, 150.0)); T0.append(rng.uniform(296.0, 303.0))
+    classes = []
+    if n_rooms:
+        be_r, cv_r = exchange_room(N=N, rho=rho, solver_options=solver_options)
+        classes.append(FleetClass("room", be_r, _class_inputs(be_r, cv_r, {"T": T0, "d": d}, n_rooms),
+                                  aliases={"mDot_out": "mDot_coupling"}, initial={"mDot_out": 0.02}))
+    if n_supply:
+        be_s, cv_s = exchange_supply(N=N, rho=rho, solver_options=solver_options)
+        classes.append(FleetClass("supply", be_s, _class_inputs(be_s, cv_s, {}, n_supply),
+                                  aliases={"mDot_out": "mDot_coupling"}, initial={"mDot_out": 0.02}))
+    return classes

@@ -75,9 +75,11 @@ STATS_BYTES = ctypes.sizeof(Stats)
 EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
     "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_batch_solve",
-    "mpcx_admm_group_sums", "mpcx_admm_mean_from_sums", "mpcx_admm_consensus_multipliers",
-    "mpcx_admm_exchange_update", "mpcx_admm_residual_partials", "mpcx_admm_shift",
+    "mpcx_admm_moments_size", "mpcx_admm_moments", "mpcx_admm_finalize",
+    "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
+    "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
 ]
+ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -130,12 +132,17 @@ def load_library():
         lib.mpcx_workspace_bytes_per_agent.argtypes = [vp]
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
         lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp]
-        lib.mpcx_admm_group_sums.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp]
-        lib.mpcx_admm_mean_from_sums.argtypes = [i32, i32, vp, vp, vp, vp]
-        lib.mpcx_admm_consensus_multipliers.argtypes = [i32, i32, vp, i32, vp, vp, vp, f64, vp, vp, vp]
-        lib.mpcx_admm_exchange_update.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, f64, vp]
-        lib.mpcx_admm_residual_partials.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, vp, f64, i32, vp, vp]
+        i64 = ctypes.c_int64
+        lib.mpcx_admm_moments_size.argtypes = [i32, i32]
+        lib.mpcx_admm_moments_size.restype = i64
+        lib.mpcx_admm_moments.argtypes = [i32, i32, i32, vp, i32, vp, vp, vp, vp, vp]
+        lib.mpcx_admm_finalize.argtypes = [i32, i32, i32, i32, vp, vp, vp, f64, vp, vp, vp, vp]
+        lib.mpcx_admm_consensus_multipliers.argtypes = [i32, i32, vp, i32, vp, vp, f64, vp, vp, vp]
+        lib.mpcx_admm_exchange_update.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, f64, vp]
         lib.mpcx_admm_shift.argtypes = [i32, i32, i32, vp, vp]
+        lib.mpcx_gather_rows.argtypes = [i32, i32, vp, i64, vp, vp, vp, vp]
+        lib.mpcx_scatter_rows.argtypes = [i32, i32, vp, vp, vp, i64, vp, vp]
+        lib.mpcx_fill_column.argtypes = [i32, vp, i64, i32, f64, vp]
         for name in EXPORTED_SYMBOLS:
             getattr(lib, name)  # raises AttributeError if a symbol is missing
         _lib = lib

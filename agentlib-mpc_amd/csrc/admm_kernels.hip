@@ -1,15 +1,26 @@
-// admm_kernels.hip — agent-batched ADMM arithmetic (consensus and exchange).
+// admm_kernels.hip — agent-batched ADMM arithmetic (consensus and exchange) and the
+// NLP-vector <-> trajectory moves around it.
 //
 // Reference semantics: ConsensusVariable / ExchangeVariable
-// (agentlib_mpc/data_structures/admm_datatypes.py:217-331), ADMM._set_mean_coupling_values
-// and update_lambda (modules/dmpc/admm/admm.py:528-570, 612-655), residual norms of
-// ADMMCoordinator._check_convergence (modules/dmpc/admm/admm_coordinator.py:354-435).
+// (agentlib_mpc/data_structures/admm_datatypes.py:202-331), ADMM._set_mean_coupling_values
+// and update_lambda (modules/dmpc/admm/admm.py:528-655), the residual norms and stopping
+// rule of ADMMCoordinator._check_convergence (modules/dmpc/admm/admm_coordinator.py:354-435).
 //
-// All kernels are HBM-bound streaming passes over [rows][T] fp64 trajectories.
-// Layout: grid.y = coupling group (alias), grid.x = chunks of ROWS_PER_BLOCK
-// participant rows; sums are formed in LDS and added to global with fp64 atomics
-// (one atomic per (block, t)), so a group of 16k participants spreads over 64
-// workgroups instead of serialising on one CU.
+// Layout: local trajectories are rows of X [n_rows][T] (fp64), the participants of one
+// coupling alias ("group") are the contiguous rows gstart[g] .. gstart[g+1]-1.
+// Every kernel is an HBM-bound streaming pass; the only reductions are per (group, t)
+// and use registers -> LDS -> one fp64 atomic per (workgroup, value).
+//
+// One all-reduce per ADMM iteration: mpcx_admm_moments forms, per (group, t), the
+// moments of the locals about the CURRENT mean c (the "old" mean):
+//   S1 = sum (x - c), S2 = sum (x - c)^2, SL = sum lam, SL2 = sum lam^2, SLX = sum lam (x - c)
+// plus the participant count.  Everything the reference computes from the individual
+// rows after the mean is known follows from them exactly (m = c + S1/n):
+//   sum (m - x)^2                 = S2 - S1^2/n                      (primal residual)
+//   sum (lam + rho (x - m))^2     = SL2 + 2 rho (SLX - (m - c) SL) + rho^2 (S2 - S1^2/n)
+//   sum x^2                       = S2 + 2 c S1 + n c^2
+// so groups whose participants live on several GPUs need only their moments summed
+// across ranks (RCCL all-reduce) before mpcx_admm_finalize.
 #include <hip/hip_runtime.h>
 
 #include "mpcx.h"
@@ -18,136 +29,186 @@ namespace {
 
 constexpr int THREADS = 256;
 constexpr int ROWS_PER_BLOCK = 256;
-constexpr int MAX_T = 512;
+constexpr int NMOM = 5;            // S1, S2, SL, SL2, SLX
+constexpr int WAVE = 64;
 
+__device__ __forceinline__ long mom_offset(int g, int g_global, int T) {
+  const long S = (long)NMOM * T + 1;
+  return (long)g * S + (g >= g_global ? MPCX_ADMM_TOTALS : 0);
+}
+
+// --- NLP vector <-> trajectory rows ---------------------------------------------------
+__global__ void k_gather_rows(int n, int T, const double* __restrict__ src, long ld,
+                              const int* __restrict__ cols, double* __restrict__ dst,
+                              const int* __restrict__ dst_rows) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)n * T) return;
+  const int a = (int)(e / T), t = (int)(e % T);
+  dst[(long)dst_rows[a] * T + t] = src[(long)a * ld + cols[t]];
+}
+
+__global__ void k_scatter_rows(int n, int T, const double* __restrict__ src,
+                               const int* __restrict__ src_rows, double* __restrict__ dst, long ld,
+                               const int* __restrict__ cols) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)n * T) return;
+  const int a = (int)(e / T), t = (int)(e % T);
+  const long r = src_rows ? src_rows[a] : a;
+  dst[(long)a * ld + cols[t]] = src[r * T + t];
+}
+
+__global__ void k_fill_column(int n, double* __restrict__ dst, long ld, int col, double v) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a < n) dst[(long)a * ld + col] = v;
+}
+
+// --- moments -----------------------------------------------------------------------------
+// grid (n_groups, row chunks). Thread (r, tc): column t0+tc, rows rb+r, rb+r+R, ...
 __global__ void __launch_bounds__(THREADS)
-k_group_sums(int T, const int* __restrict__ gstart, const double* __restrict__ x,
-             const int* __restrict__ active, double* __restrict__ sums) {
-  __shared__ double acc[MAX_T + 1];
-  const int g = blockIdx.y;
+k_moments(int g_global, int T, const int* __restrict__ gstart, const double* __restrict__ x,
+          const double* __restrict__ lam, const double* __restrict__ center,
+          double* __restrict__ out) {
+  __shared__ double part[THREADS * NMOM];
+  const int g = blockIdx.x;
   const int r0 = gstart[g], r1 = gstart[g + 1];
-  const int rb = r0 + blockIdx.x * ROWS_PER_BLOCK;
+  const int rb = r0 + blockIdx.y * ROWS_PER_BLOCK;
   if (rb >= r1) return;
   const int re = min(rb + ROWS_PER_BLOCK, r1);
-  for (int t = threadIdx.x; t <= T; t += THREADS) acc[t] = 0.0;
-  __syncthreads();
-  const long base = (long)rb * T;
-  const int n = (re - rb) * T;
-  for (int e = threadIdx.x; e < n; e += THREADS) {
-    const int row = rb + e / T;
-    if (active && !active[row]) continue;
-    atomicAdd(&acc[e % T], x[base + e]);
+  double* o = out + mom_offset(g, g_global, T);
+  const int cpp = T < THREADS ? T : THREADS;  // columns per pass
+  const int R = THREADS / cpp;                // row lanes
+  const int r = threadIdx.x / cpp, tc = threadIdx.x % cpp;
+  for (int t0 = 0; t0 < T; t0 += cpp) {
+    const int t = t0 + tc;
+    double s1 = 0.0, s2 = 0.0, sl = 0.0, sl2 = 0.0, slx = 0.0;
+    if (r < R && t < T) {
+      const double c = center[(long)g * T + t];
+      for (int row = rb + r; row < re; row += R) {
+        const double d = x[(long)row * T + t] - c;
+        s1 += d;
+        s2 += d * d;
+        if (lam) {
+          const double l = lam[(long)row * T + t];
+          sl += l;
+          sl2 += l * l;
+          slx += l * d;
+        }
+      }
+    }
+    double* p = part + threadIdx.x * NMOM;
+    p[0] = s1; p[1] = s2; p[2] = sl; p[3] = sl2; p[4] = slx;
+    __syncthreads();
+    if (r == 0 && t < T) {
+      for (int q = 1; q < R; ++q) {
+        const double* pq = part + (q * cpp + tc) * NMOM;
+        s1 += pq[0]; s2 += pq[1]; sl += pq[2]; sl2 += pq[3]; slx += pq[4];
+      }
+      atomicAdd(&o[0 * T + t], s1);
+      atomicAdd(&o[1 * T + t], s2);
+      if (lam) {
+        atomicAdd(&o[2 * T + t], sl);
+        atomicAdd(&o[3 * T + t], sl2);
+        atomicAdd(&o[4 * T + t], slx);
+      }
+    }
+    __syncthreads();
   }
-  for (int row = rb + threadIdx.x; row < re; row += THREADS)
-    if (!active || active[row]) atomicAdd(&acc[T], 1.0);
-  __syncthreads();
-  for (int t = threadIdx.x; t <= T; t += THREADS)
-    if (acc[t] != 0.0) atomicAdd(&sums[(long)g * (T + 1) + t], acc[t]);
+  if (threadIdx.x == 0) atomicAdd(&o[NMOM * T], (double)(re - rb));
 }
 
-__global__ void k_mean_from_sums(int n_groups, int T, const double* __restrict__ sums,
-                                 double* __restrict__ mean, double* __restrict__ dmean) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n_groups * T) return;
-  const int g = e / T, t = e % T;
-  const double cnt = sums[(long)g * (T + 1) + T];
-  if (cnt <= 0.0) return;
-  const double m = sums[(long)g * (T + 1) + t] / cnt;
-  dmean[e] = mean[e] - m;
-  mean[e] = m;
+// --- finalize: one wavefront per group ------------------------------------------------
+__global__ void __launch_bounds__(WAVE)
+k_finalize(int g0, int g1, int g_global, int T, const double* __restrict__ mom,
+           const int* __restrict__ exchange, const double* __restrict__ gmult, double rho,
+           double* __restrict__ mean, double* __restrict__ dmean, double* __restrict__ totals) {
+  const int g = g0 + blockIdx.x;
+  if (g >= g1) return;
+  const double* o = mom + mom_offset(g, g_global, T);
+  const double n = o[NMOM * T];
+  const bool ex = exchange && exchange[g];
+  double prim = 0.0, dual = 0.0, xs = 0.0, ms = 0.0, ls = 0.0;
+  if (n > 0.0) {
+    for (int t = threadIdx.x; t < T; t += WAVE) {
+      const double c = mean[(long)g * T + t];
+      const double s1 = o[t], s2 = o[T + t];
+      const double dm = s1 / n;                 // m - c
+      const double m = c + dm;
+      const double var = fmax(s2 - s1 * dm, 0.0);  // sum (x - m)^2
+      mean[(long)g * T + t] = m;
+      dmean[(long)g * T + t] = c - m;           // delta_mean = old - new
+      const double dd = rho * (c - m);
+      dual += dd * dd;
+      xs += s2 + 2.0 * c * s1 + n * c * c;
+      ms += m * m;
+      if (ex) {
+        prim += m * m;                          // exchange primal residual = mean
+        const double l = gmult[(long)g * T + t] + rho * m;
+        ls += l * l;
+      } else {
+        prim += var;
+        const double sl = o[2 * T + t], sl2 = o[3 * T + t], slx = o[4 * T + t];
+        ls += sl2 + 2.0 * rho * (slx - dm * sl) + rho * rho * var;
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    prim += __shfl_xor(prim, s, WAVE);
+    dual += __shfl_xor(dual, s, WAVE);
+    xs += __shfl_xor(xs, s, WAVE);
+    ms += __shfl_xor(ms, s, WAVE);
+    ls += __shfl_xor(ls, s, WAVE);
+  }
+  if (threadIdx.x == 0 && n > 0.0) {
+    atomicAdd(&totals[0], prim);
+    atomicAdd(&totals[1], dual);
+    atomicAdd(&totals[2], xs);
+    atomicAdd(&totals[3], ms);
+    atomicAdd(&totals[4], ls);
+    atomicAdd(&totals[5], n);                   // trajectories (flat_locals entries)
+    atomicAdd(&totals[6], ex ? (double)T : n);  // flat_multipliers entries (reference quirk)
+    atomicAdd(&totals[7], 1.0);                 // groups with participants
+  }
 }
 
+// --- multiplier / diff updates ---------------------------------------------------------
 __global__ void __launch_bounds__(THREADS)
 k_consensus_mult(int T, const int* __restrict__ gstart, const double* __restrict__ x,
-                 const int* __restrict__ active, const double* __restrict__ mean, double rho,
-                 double* __restrict__ lam, double* __restrict__ res) {
-  const int g = blockIdx.y;
+                 const double* __restrict__ mean, double rho, double* __restrict__ lam,
+                 double* __restrict__ res) {
+  const int g = blockIdx.x;
   const int r0 = gstart[g], r1 = gstart[g + 1];
-  const int rb = r0 + blockIdx.x * ROWS_PER_BLOCK;
+  const int rb = r0 + blockIdx.y * ROWS_PER_BLOCK;
   if (rb >= r1) return;
   const int re = min(rb + ROWS_PER_BLOCK, r1);
   const long base = (long)rb * T;
   const int n = (re - rb) * T;
   for (int e = threadIdx.x; e < n; e += THREADS) {
-    const int row = rb + e / T;
-    if (active && !active[row]) { res[base + e] = 0.0; continue; }
     const double r = mean[(long)g * T + e % T] - x[base + e];
-    res[base + e] = r;
+    if (res) res[base + e] = r;
     lam[base + e] -= rho * r;
   }
 }
 
 __global__ void __launch_bounds__(THREADS)
 k_exchange_diff(int T, const int* __restrict__ gstart, const double* __restrict__ x,
-                const int* __restrict__ active, const double* __restrict__ mean,
-                double* __restrict__ diff) {
-  const int g = blockIdx.y;
+                const double* __restrict__ mean, double* __restrict__ diff) {
+  const int g = blockIdx.x;
   const int r0 = gstart[g], r1 = gstart[g + 1];
-  const int rb = r0 + blockIdx.x * ROWS_PER_BLOCK;
+  const int rb = r0 + blockIdx.y * ROWS_PER_BLOCK;
   if (rb >= r1) return;
   const int re = min(rb + ROWS_PER_BLOCK, r1);
   const long base = (long)rb * T;
   const int n = (re - rb) * T;
-  for (int e = threadIdx.x; e < n; e += THREADS) {
-    const int row = rb + e / T;
-    if (active && !active[row]) continue;
+  for (int e = threadIdx.x; e < n; e += THREADS)
     diff[base + e] = x[base + e] - mean[(long)g * T + e % T];
-  }
 }
 
 __global__ void k_exchange_mult(int n_groups, int T, const double* __restrict__ mean, double rho,
-                                double* __restrict__ lam, double* __restrict__ res) {
+                                double* __restrict__ lam) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_groups * T) return;
-  const double m = mean[e];
-  res[e] = m;
-  lam[e] += rho * m;
-}
-
-__global__ void __launch_bounds__(THREADS)
-k_residual_partials(int T, const int* __restrict__ gstart, const double* __restrict__ res,
-                    const double* __restrict__ dmean, const double* __restrict__ x,
-                    const double* __restrict__ lam, const int* __restrict__ active, double rho,
-                    int exchange, double* __restrict__ out) {
-  __shared__ double acc[4];
-  const int g = blockIdx.y;
-  const int r0 = gstart[g], r1 = gstart[g + 1];
-  const int rb = r0 + blockIdx.x * ROWS_PER_BLOCK;
-  if (rb >= r1) return;
-  const int re = min(rb + ROWS_PER_BLOCK, r1);
-  if (threadIdx.x < 4) acc[threadIdx.x] = 0.0;
-  __syncthreads();
-  double s_r = 0.0, s_x = 0.0, s_l = 0.0, s_d = 0.0;
-  const long base = (long)rb * T;
-  const int n = (re - rb) * T;
-  for (int e = threadIdx.x; e < n; e += THREADS) {
-    const int row = rb + e / T;
-    if (active && !active[row]) continue;
-    const double xv = x[base + e];
-    s_x += xv * xv;
-    if (!exchange) {
-      const double r = res[base + e], l = lam[base + e];
-      s_r += r * r;
-      s_l += l * l;
-    }
-  }
-  if (blockIdx.x == 0) {  // per-group terms counted once
-    for (int t = threadIdx.x; t < T; t += THREADS) {
-      const double d = rho * dmean[(long)g * T + t];
-      s_d += d * d;
-      if (exchange) {
-        const double r = res[(long)g * T + t], l = lam[(long)g * T + t];
-        s_r += r * r;
-        s_l += l * l;
-      }
-    }
-  }
-  atomicAdd(&acc[0], s_r);
-  atomicAdd(&acc[1], s_d);
-  atomicAdd(&acc[2], s_x);
-  atomicAdd(&acc[3], s_l);
-  __syncthreads();
-  if (threadIdx.x < 4) atomicAdd(&out[(long)g * 4 + threadIdx.x], acc[threadIdx.x]);
+  lam[e] += rho * mean[e];
 }
 
 __global__ void k_shift(int n_rows, int T, int shift, double* __restrict__ x) {
@@ -158,10 +219,12 @@ __global__ void k_shift(int n_rows, int T, int shift, double* __restrict__ x) {
   for (int t = 0; t < T - shift; ++t) r[t] = r[t + shift];
 }
 
-inline dim3 group_grid(int n_groups, const int* /*gstart (device)*/, int max_rows) {
+inline dim3 group_grid(int n_groups, int max_rows) {
   const int chunks = (max_rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-  return dim3(chunks > 0 ? chunks : 1, n_groups, 1);
+  return dim3(n_groups, chunks > 0 ? chunks : 1, 1);
 }
+
+inline unsigned blocks_for(long n, int threads) { return (unsigned)((n + threads - 1) / threads); }
 
 }  // namespace
 
@@ -170,83 +233,115 @@ inline dim3 group_grid(int n_groups, const int* /*gstart (device)*/, int max_row
     if (hipGetLastError() != hipSuccess) return MPCX_ERR_HIP; \
   } while (0)
 
-extern "C" int mpcx_admm_group_sums(int32_t n_groups, int32_t T, const int32_t* gstart,
-                                    int32_t max_group_rows,
-                                    const double* locals, const int32_t* active, double* sums,
-                                    void* stream) {
-  if (n_groups <= 0 || T <= 0 || T > MAX_T || !gstart || !locals || !sums) return MPCX_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  const int mr = max_group_rows;
-  hipLaunchKernelGGL(k_group_sums, group_grid(n_groups, gstart, mr), dim3(THREADS), 0, s, T, gstart,
-                     locals, active, sums);
+extern "C" int mpcx_gather_rows(int32_t n_agents, int32_t T, const double* src, int64_t src_ld,
+                                const int32_t* cols, double* dst, const int32_t* dst_rows,
+                                void* stream) {
+  if (n_agents < 0 || T <= 0 || src_ld <= 0 || !src || !cols || !dst || !dst_rows) return MPCX_ERR_ARG;
+  if (n_agents == 0) return MPCX_OK;
+  const long n = (long)n_agents * T;
+  hipLaunchKernelGGL(k_gather_rows, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     n_agents, T, src, (long)src_ld, cols, dst, dst_rows);
   LAUNCH_CHECK();
   return MPCX_OK;
 }
 
-extern "C" int mpcx_admm_mean_from_sums(int32_t n_groups, int32_t T, const double* sums,
-                                        double* mean, double* delta_mean, void* stream) {
-  if (n_groups <= 0 || T <= 0 || !sums || !mean || !delta_mean) return MPCX_ERR_ARG;
-  const int n = n_groups * T;
-  hipLaunchKernelGGL(k_mean_from_sums, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     n_groups, T, sums, mean, delta_mean);
+extern "C" int mpcx_scatter_rows(int32_t n_agents, int32_t T, const double* src,
+                                 const int32_t* src_rows, double* dst, int64_t dst_ld,
+                                 const int32_t* cols, void* stream) {
+  if (n_agents < 0 || T <= 0 || dst_ld <= 0 || !src || !dst || !cols) return MPCX_ERR_ARG;
+  if (n_agents == 0) return MPCX_OK;
+  const long n = (long)n_agents * T;
+  hipLaunchKernelGGL(k_scatter_rows, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     n_agents, T, src, src_rows, dst, (long)dst_ld, cols);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int mpcx_fill_column(int32_t n_agents, double* dst, int64_t dst_ld, int32_t col,
+                                double value, void* stream) {
+  if (n_agents < 0 || dst_ld <= 0 || col < 0 || col >= dst_ld || !dst) return MPCX_ERR_ARG;
+  if (n_agents == 0) return MPCX_OK;
+  hipLaunchKernelGGL(k_fill_column, dim3(blocks_for(n_agents, 256)), dim3(256), 0,
+                     (hipStream_t)stream, n_agents, dst, (long)dst_ld, col, value);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t T) {
+  if (n_groups < 0 || T <= 0) return MPCX_ERR_ARG;
+  return (int64_t)n_groups * (NMOM * (int64_t)T + 1) + MPCX_ADMM_TOTALS;
+}
+
+extern "C" int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t T,
+                                 const int32_t* gstart, int32_t max_group_rows,
+                                 const double* locals, const double* multipliers,
+                                 const double* center, double* out, void* stream) {
+  if (n_groups <= 0 || n_global < 0 || n_global > n_groups || T <= 0 || max_group_rows < 0 ||
+      !gstart || !locals || !center || !out)
+    return MPCX_ERR_ARG;
+  if (max_group_rows == 0) return MPCX_OK;
+  hipLaunchKernelGGL(k_moments, group_grid(n_groups, max_group_rows), dim3(THREADS), 0,
+                     (hipStream_t)stream, n_global, T, gstart, locals, multipliers, center, out);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_global, int32_t T,
+                                  const double* moments, const int32_t* exchange,
+                                  const double* group_multipliers, double rho, double* mean,
+                                  double* delta_mean, double* totals, void* stream) {
+  if (g_begin < 0 || g_end < g_begin || n_global < 0 || T <= 0 || !moments || !mean ||
+      !delta_mean || !totals)
+    return MPCX_ERR_ARG;
+  if (exchange && !group_multipliers) return MPCX_ERR_ARG;
+  if (g_end == g_begin) return MPCX_OK;
+  hipLaunchKernelGGL(k_finalize, dim3(g_end - g_begin), dim3(WAVE), 0, (hipStream_t)stream, g_begin,
+                     g_end, n_global, T, moments, exchange, group_multipliers, rho, mean,
+                     delta_mean, totals);
   LAUNCH_CHECK();
   return MPCX_OK;
 }
 
 extern "C" int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, const int32_t* gstart,
-                                    int32_t max_group_rows,
-                                               const double* locals, const int32_t* active,
+                                               int32_t max_group_rows, const double* locals,
                                                const double* mean, double rho, double* mult,
                                                double* res, void* stream) {
-  if (n_groups <= 0 || T <= 0 || !gstart || !locals || !mean || !mult || !res) return MPCX_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  const int mr = max_group_rows;
-  hipLaunchKernelGGL(k_consensus_mult, group_grid(n_groups, gstart, mr), dim3(THREADS), 0, s, T,
-                     gstart, locals, active, mean, rho, mult, res);
+  if (n_groups <= 0 || T <= 0 || max_group_rows < 0 || !gstart || !locals || !mean || !mult)
+    return MPCX_ERR_ARG;
+  if (max_group_rows == 0) return MPCX_OK;
+  hipLaunchKernelGGL(k_consensus_mult, group_grid(n_groups, max_group_rows), dim3(THREADS), 0,
+                     (hipStream_t)stream, T, gstart, locals, mean, rho, mult, res);
   LAUNCH_CHECK();
   return MPCX_OK;
 }
 
 extern "C" int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* gstart,
-                                    int32_t max_group_rows,
-                                         const double* locals, const int32_t* active,
+                                         int32_t max_group_rows, const double* locals,
                                          const double* mean, double* diff, double* mult,
-                                         double* res, double rho, void* stream) {
-  if (n_groups <= 0 || T <= 0 || !gstart || !locals || !mean || !diff || !mult || !res)
+                                         double rho, void* stream) {
+  if (n_groups <= 0 || T <= 0 || max_group_rows < 0 || !gstart || !locals || !mean || !diff)
     return MPCX_ERR_ARG;
+  if (rho != 0.0 && !mult) return MPCX_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const int mr = max_group_rows;
-  hipLaunchKernelGGL(k_exchange_diff, group_grid(n_groups, gstart, mr), dim3(THREADS), 0, s, T,
-                     gstart, locals, active, mean, diff);
-  LAUNCH_CHECK();
-  const int n = n_groups * T;
-  hipLaunchKernelGGL(k_exchange_mult, dim3((n + 255) / 256), dim3(256), 0, s, n_groups, T, mean,
-                     rho, mult, res);
-  LAUNCH_CHECK();
-  return MPCX_OK;
-}
-
-extern "C" int mpcx_admm_residual_partials(int32_t n_groups, int32_t T, const int32_t* gstart,
-                                    int32_t max_group_rows,
-                                           const double* res, const double* dmean,
-                                           const double* locals, const double* mult,
-                                           const int32_t* active, double rho, int32_t exchange,
-                                           double* out, void* stream) {
-  if (n_groups <= 0 || T <= 0 || !gstart || !res || !dmean || !locals || !mult || !out)
-    return MPCX_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  const int mr = max_group_rows;
-  hipLaunchKernelGGL(k_residual_partials, group_grid(n_groups, gstart, mr), dim3(THREADS), 0, s, T,
-                     gstart, res, dmean, locals, mult, active, rho, exchange, out);
-  LAUNCH_CHECK();
+  if (max_group_rows > 0) {
+    hipLaunchKernelGGL(k_exchange_diff, group_grid(n_groups, max_group_rows), dim3(THREADS), 0, s,
+                       T, gstart, locals, mean, diff);
+    LAUNCH_CHECK();
+  }
+  if (rho != 0.0) {
+    const int n = n_groups * T;
+    hipLaunchKernelGGL(k_exchange_mult, dim3(blocks_for(n, 256)), dim3(256), 0, s, n_groups, T,
+                       mean, rho, mult);
+    LAUNCH_CHECK();
+  }
   return MPCX_OK;
 }
 
 extern "C" int mpcx_admm_shift(int32_t n_rows, int32_t T, int32_t shift, double* x, void* stream) {
   if (n_rows < 0 || T <= 0 || shift < 0 || shift > T || !x) return MPCX_ERR_ARG;
   if (n_rows == 0 || shift == 0) return MPCX_OK;
-  hipLaunchKernelGGL(k_shift, dim3((n_rows + 255) / 256), dim3(256), 0, (hipStream_t)stream, n_rows,
-                     T, shift, x);
+  hipLaunchKernelGGL(k_shift, dim3(blocks_for(n_rows, 256)), dim3(256), 0, (hipStream_t)stream,
+                     n_rows, T, shift, x);
   LAUNCH_CHECK();
   return MPCX_OK;
 }

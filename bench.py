@@ -90,6 +90,53 @@ def cpu_baseline(p, lbw, ubw, w0, tol, repeats=3):
                       f"gcc -O3 -march=native, OpenMP {threads} threads): {dt:.2f} s wall"}
 
 
+def admm_bench(args, world, rank, dev):
+    """C4 (BASELINE.json configs[3]): decentralised exchange ADMM (LocalADMM semantics,
+    examples/exchange_admm: MS-Euler, N=10, ts=120, rho=1e4, 15 iterations) on
+    ``--admm-agents`` agents per GPU (rooms:supply = 4:1) sharing ONE exchange alias
+    across all ranks: one RCCL all-reduce per ADMM iteration."""
+    import torch
+    import torch.distributed as dist
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.admm.fleet import ADMMFleet
+
+    n = args.admm_agents
+    n_sup = n // 5
+    opts = {"ipopt": {"tol": args.tol, "max_iter": 500}}
+    classes = bm.c4_fleet_classes(n_rooms=n - n_sup, n_supply=n_sup, N=10, seed=20261015 + 4 + rank,
+                                  solver_options=opts)
+    fleet = ADMMFleet(classes, device=dev, comm="default" if world > 1 else None)
+    for c in classes:
+        c.native.reserve(c.n)
+    fleet.run_local(1e4, max_iterations=1, record_residuals=False)  # warm-up (code objects, RCCL)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    out = fleet.run_local(1e4, max_iterations=args.admm_iters, record_residuals=False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall, float(out["converged_solves"])], dtype=torch.float64, device=dev)
+    if world > 1:
+        w = t[:1].clone()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t[0] = w[0]
+    wall, ok = float(t[0]), float(t[1])
+    return {
+        "workload": "C4: exchange ADMM (LocalADMM), examples/exchange_admm rooms+supply 4:1, MS-Euler "
+                    "N=10 ts=120 rho=1e4, one exchange alias spanning all GPUs",
+        "agents_per_gpu": n, "agents_total": n * world, "admm_iterations": args.admm_iters,
+        "admm_iters_per_s": args.admm_iters / wall,
+        "agent_solves_per_s": ok / wall,
+        "converged_fraction": ok / (n * world * args.admm_iters),
+        "ms_per_admm_iteration": wall / args.admm_iters * 1e3,
+        "allreduce_per_iteration": 1 if world > 1 else 0,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +145,8 @@ def main():
     ap.add_argument("--agents", type=int, default=4096, help="agents per GPU")
     ap.add_argument("--tol", type=float, default=1e-8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--admm-agents", type=int, default=16384, help="C4 agents per GPU (0: skip)")
+    ap.add_argument("--admm-iters", type=int, default=15)
     args = ap.parse_args()
 
     import torch
@@ -155,6 +204,7 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
+    admm = admm_bench(args, world, rank, dev) if args.admm_agents > 0 else None
     stats = stats_to_dicts(st.cpu().numpy().tobytes())
     n_ok = sum(1 for s in stats if s["success"])
     arr = {"iter": np.array([s["iter_count"] for s in stats]),
@@ -210,6 +260,8 @@ def main():
                         "counts x per-agent iteration/factorisation/trial counters",
             },
         }
+        if admm is not None:
+            out["admm"] = admm
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(p, lbw, ubw, w0, args.tol)

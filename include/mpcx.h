@@ -14,19 +14,23 @@
  *                            ca.nlpsol("mpc", "ipopt", ...)(p, x0, lbx, ubx, lbg, ubg),
  *                            batched over agents; outputs x, lam_g, lam_x and the
  *                            IPOPT-style stats (success, return_status, iter_count, obj).
- *   mpcx_admm_group_sums + mpcx_admm_mean_from_sums
- *                         <- ConsensusVariable.update_mean_trajectory
- *                            (data_structures/admm_datatypes.py:221-236) and
- *                            ADMM._set_mean_coupling_values (modules/dmpc/admm/admm.py:528-548)
+ *   mpcx_admm_moments + mpcx_admm_finalize
+ *                         <- ConsensusVariable.update_mean_trajectory / ExchangeVariable.
+ *                            update_diff_trajectories (data_structures/admm_datatypes.py:221-236,
+ *                            292-309), ADMM._set_mean_coupling_values
+ *                            (modules/dmpc/admm/admm.py:528-570) and the residual norms of
+ *                            ADMMCoordinator._check_convergence
+ *                            (modules/dmpc/admm/admm_coordinator.py:354-435)
  *   mpcx_admm_consensus_multipliers
  *                         <- ConsensusVariable.update_multipliers (admm_datatypes.py:238-267),
  *                            ADMM.update_lambda (admm.py:612-633)
  *   mpcx_admm_exchange_update
  *                         <- ExchangeVariable.update_diff_trajectories / update_multiplier
  *                            (admm_datatypes.py:292-324), admm.py:550-570, 635-655
- *   mpcx_admm_residual_partials
- *                         <- ADMMCoordinator._check_convergence norms
- *                            (modules/dmpc/admm/admm_coordinator.py:354-435)
+ *   mpcx_admm_shift       <- shift_values_by_one (admm_datatypes.py:275-282, 326-331)
+ *   mpcx_gather_rows / mpcx_scatter_rows / mpcx_fill_column
+ *                         <- moving coupling trajectories between Results and the
+ *                            coordinator messages (modules/dmpc/admm/admm_coordinated.py:133-193)
  *
  * Conventions: all array arguments are DEVICE pointers (HBM-resident, fp64),
  * agent-major ([n_agents][len]).  Functions return 0 on success and a
@@ -43,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 3
+#define MPCX_API_VERSION 4
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -138,50 +142,78 @@ int mpcx_batch_solve(mpcx_handle* h, int32_t n_agents, const double* p, const do
                      const double* ubw, const double* lbg, const double* ubg, double* w_io,
                      double* lam_g, double* lam_w, mpcx_stats* stats, void* stream);
 
-/* ---- ADMM kernels (agent-batched, see header comment for reference mapping) ----
- * Local trajectories are rows of `locals` [n_rows][T].  The participants of one
- * coupling alias ("group") are the contiguous rows group_start[g] ..
- * group_start[g+1]-1 (device array); max_group_rows = max over g of the group
- * size (host value, sizes the launch grid).  `active` [n_rows] (0/1, NULL = all) masks participants
- * that did not report this round (coordinator: agents not "ready").
- * Multi-GPU: every rank calls mpcx_admm_group_sums on its rows, the [n_groups][T+1]
- * sums are all-reduced (RCCL), then mpcx_admm_mean_from_sums finalises.
+/* ---- ADMM kernels (agent-batched) --------------------------------------------------
+ * Local trajectories are rows of `locals` [n_rows][T] (fp64, device).  The participants
+ * of one coupling alias ("group") are the contiguous rows gstart[g] .. gstart[g+1]-1
+ * (device int32 array); max_group_rows = max over g of the group size (host value, sizes
+ * the launch grid).  Groups [0, n_global) may have participants on other GPUs: their
+ * moments are all-reduced (RCCL, sum) between mpcx_admm_moments and mpcx_admm_finalize;
+ * groups [n_global, n_groups) are GPU-local.  One ADMM iteration of the reference
+ * coordinator (admm_coordinator.py:288-304) is
+ *   moments -> [all-reduce of the first mpcx_admm_reduce_count() doubles] -> finalize
+ *   -> consensus_multipliers / exchange_update -> scatter into the NLP parameters.
  */
-/* sums[g][t] += sum over active rows of group g of locals[row][t]; sums[g][T] += count.
- * `sums` must be zeroed by the caller. */
-int mpcx_admm_group_sums(int32_t n_groups, int32_t T, const int32_t* group_start,
-                         int32_t max_group_rows,
-                         const double* locals, const int32_t* active, double* sums,
-                         void* stream);
-/* mean[g][:] <- sums[g][:T]/sums[g][T]; delta_mean <- old mean - new mean (groups with
- * count 0 keep mean and delta_mean). */
-int mpcx_admm_mean_from_sums(int32_t n_groups, int32_t T, const double* sums, double* mean,
-                             double* delta_mean, void* stream);
-/* consensus: r = mean[g] - x_i ; lambda_i <- lambda_i - rho * r  (active rows; inactive r = 0) */
-int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, const int32_t* group_start,
-                                    int32_t max_group_rows,
-                                    const double* locals, const int32_t* active,
+#define MPCX_ADMM_TOTALS 8
+/* doubles in a moments buffer (zero it before mpcx_admm_moments); the all-reduce range
+ * is the first n_global*(5T+1) + MPCX_ADMM_TOTALS doubles. */
+int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t T);
+
+/* Per (group, t) moments of the locals about center = the current mean [n_groups][T]:
+ * sum(x-c), sum(x-c)^2 and, if multipliers != NULL (consensus rows), sum lam, sum lam^2,
+ * sum lam*(x-c); plus the participant count.  ADDED into `out`.
+ *   <- ConsensusVariable.update_mean_trajectory (admm_datatypes.py:221-236),
+ *      ExchangeVariable.update_diff_trajectories (:292-309), ADMM._set_mean_coupling_values
+ *      (modules/dmpc/admm/admm.py:528-570) — the participant sums of np.mean(axis=0). */
+int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t T, const int32_t* gstart,
+                      int32_t max_group_rows, const double* locals, const double* multipliers,
+                      const double* center, double* out, void* stream);
+
+/* Groups [g_begin, g_end): mean <- c + S1/n, delta_mean <- c - mean (groups without
+ * participants keep both); ADDS to totals[8]:
+ *   {||r||^2, ||rho*delta_mean||^2, ||X||_F^2, ||mean||^2, ||Lambda_new||^2,
+ *    #trajectories, #flat_multipliers, #groups}
+ * with the reference's conventions: consensus r = mean - x_i and Lambda_new the updated
+ * per-participant multipliers; exchange (exchange[g] != 0) r = mean and Lambda_new =
+ * group_multipliers + rho*mean  <- ADMMCoordinator._check_convergence
+ * (admm_coordinator.py:354-435), CouplingVariable.get_residual (admm_datatypes.py:202-214). */
+int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_global, int32_t T,
+                       const double* moments, const int32_t* exchange,
+                       const double* group_multipliers, double rho, double* mean,
+                       double* delta_mean, double* totals, void* stream);
+
+/* consensus: r = mean[g] - x_i ; lambda_i <- lambda_i - rho * r  (res may be NULL)
+ *   <- ConsensusVariable.update_multipliers (admm_datatypes.py:238-267),
+ *      ADMM.update_lambda (admm.py:612-633) */
+int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, const int32_t* gstart,
+                                    int32_t max_group_rows, const double* locals,
                                     const double* mean, double rho, double* multipliers,
                                     double* primal_residual, void* stream);
-/* exchange: diff_i <- x_i - mean[g] (active rows); lambda[g] <- lambda[g] + rho*mean[g];
- * primal_residual[g] <- mean[g].  rho = 0 updates diffs only. */
-int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* group_start,
-                              int32_t max_group_rows,
-                              const double* locals, const int32_t* active, const double* mean,
-                              double* diff, double* multiplier, double* primal_residual,
-                              double rho, void* stream);
-/* Per-group partial sums of squares, ADDED to out[n_groups][4] (zeroed by caller):
- *   {sum r^2, sum (rho*delta_mean)^2, sum x_local^2 (active rows), sum lambda^2}.
- * consensus: r/lambda are [n_rows][T]; exchange: r/lambda are [n_groups][T]. */
-int mpcx_admm_residual_partials(int32_t n_groups, int32_t T, const int32_t* group_start,
-                                int32_t max_group_rows,
-                                const double* primal_residual, const double* delta_mean,
-                                const double* locals, const double* multipliers,
-                                const int32_t* active, double rho, int32_t exchange,
-                                double* out, void* stream);
-/* Shift rows by one control interval (admm_datatypes.py:275-282, 326-331):
- * x[i][:] <- x[i][shift:] ++ x[i][T-shift:] */
+/* exchange: diff_i <- x_i - mean[g]; if rho != 0: lambda[g] <- lambda[g] + rho*mean[g]
+ *   <- ExchangeVariable.update_diff_trajectories / update_multiplier
+ *      (admm_datatypes.py:292-324), admm.py:550-570, 635-655 */
+int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* gstart,
+                              int32_t max_group_rows, const double* locals, const double* mean,
+                              double* diff, double* multiplier, double rho, void* stream);
+/* Shift rows by one control interval: x[i][:] <- x[i][shift:] ++ x[i][T-shift:]
+ *   <- ConsensusVariable/ExchangeVariable.shift_values_by_one (admm_datatypes.py:275-282,
+ *      326-331), ADMM._shift (admm.py:329-342) */
 int mpcx_admm_shift(int32_t n_rows, int32_t T, int32_t shift, double* x, void* stream);
+
+/* ---- NLP vector <-> trajectory moves (no host round trip) ----------------------------
+ * dst[dst_rows[a]][t] <- src[a*src_ld + cols[t]]: the coupling trajectories out of the
+ * solutions w  <- Results[coupling.name] in CoordinatedADMM.optimize
+ * (modules/dmpc/admm/admm_coordinated.py:170-184) / ADMM.send_coupling_values. */
+int mpcx_gather_rows(int32_t n_agents, int32_t T, const double* src, int64_t src_ld,
+                     const int32_t* cols, double* dst, const int32_t* dst_rows, void* stream);
+/* dst[a*dst_ld + cols[t]] <- src[src_rows[a]][t] (src_rows NULL: row a): means,
+ * diffs and multipliers into the NLP parameters p  <- the MPCVariable updates of
+ * CoordinatedADMM.optimize (admm_coordinated.py:147-163) sampled by
+ * CasADiBackend._get_current_mpc_inputs (core/casadi_backend.py:141-253). */
+int mpcx_scatter_rows(int32_t n_agents, int32_t T, const double* src, const int32_t* src_rows,
+                      double* dst, int64_t dst_ld, const int32_t* cols, void* stream);
+/* dst[a*dst_ld + col] <- value (the penalty factor rho into p). */
+int mpcx_fill_column(int32_t n_agents, double* dst, int64_t dst_ld, int32_t col, double value,
+                     void* stream);
 
 #ifdef __cplusplus
 }

@@ -72,3 +72,197 @@ def residual_norms(primal_residual, delta_mean, rho):
 def shift(x, shift_by):
     x = np.asarray(x, float)
     return np.concatenate([x[:, shift_by:], x[:, x.shape[1] - shift_by:]], axis=1)
+
+
+# ---------------------------------------------------------------------------
+# Loop restatements (per-agent dictionaries, the reference's own formulas)
+# ---------------------------------------------------------------------------
+
+class _Consensus:
+    """`admm_datatypes.py:160-282` (CouplingVariable + ConsensusVariable)."""
+
+    def __init__(self):
+        self.local = {}
+        self.mean = [0]
+        self.delta_mean = np.array([0.0])
+        self.primal_residual = np.array([0.0])
+        self.mult = {}
+
+    def update_mean(self):
+        arr = np.array([self.local[s] for s in self.local])
+        mean = np.mean(arr, axis=0)
+        self.delta_mean = self.mean - mean
+        self.mean = list(mean)
+
+    def update_multipliers(self, rho):
+        srcs = list(self.local)
+        traj = np.array([self.local[s] for s in srcs])
+        mul = np.array([self.mult[s] for s in srcs])
+        self.primal_residual = np.array(self.mean) - traj
+        new = mul - rho * self.primal_residual
+        for i, s in enumerate(srcs):
+            self.mult[s] = list(new[i])
+
+    def shift(self, horizon):
+        k = int(len(self.mean) / horizon)
+        self.mean = self.mean[k:] + self.mean[-k:]
+        for s, m in self.mult.items():
+            self.mult[s] = m[k:] + m[-k:]
+
+
+class _Exchange:
+    """`admm_datatypes.py:285-331` (ExchangeVariable)."""
+
+    def __init__(self):
+        self.local = {}
+        self.mean = [0]
+        self.delta_mean = np.array([0.0])
+        self.primal_residual = np.array([0.0])
+        self.diff = {}
+        self.mult = []
+
+    def update_mean(self):
+        arr = np.array([self.local[s] for s in self.local])
+        mean = np.mean(arr, axis=0)
+        self.delta_mean = self.mean - mean
+        self.mean = list(mean)
+        for s in self.local:
+            self.diff[s] = list(np.asarray(self.local[s]) - mean)
+
+    def update_multipliers(self, rho):
+        self.primal_residual = np.array(self.mean)
+        self.mult = list(self.mult + rho * self.primal_residual)
+
+    def shift(self, horizon):
+        k = int(len(self.mult) / horizon)
+        self.mult = self.mult[k:] + self.mult[-k:]
+        for s, d in self.diff.items():
+            self.diff[s] = d[k:] + d[-k:]
+
+
+def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max, primal_tol=1e-3,
+                      dual_tol=1e-3, use_relative_tolerances=True, abs_tol=1e-3, rel_tol=1e-3,
+                      penalty_change_threshold=-1.0, penalty_change_factor=2.0, T=None, state=None):
+    """One round of ``ADMMCoordinator._fast_process`` (`admm_coordinator.py:259-321`).
+
+    participation: {agent: {alias: "consensus"|"exchange"}}; initial: {agent: {alias: value}}
+    solve(agent, {alias: (mean_or_diff, multiplier)}, rho) -> {alias: local trajectory}
+    Returns (state, history [(primal, dual, rho)], iterations, converged).
+    """
+    if state is None:  # registration (`admm_coordinator.py:528-560`)
+        state = {"vars": {}, "order": []}
+        for ag, coups in participation.items():
+            for al, kind in coups.items():
+                v = state["vars"].setdefault(al, _Consensus() if kind == "consensus" else _Exchange())
+                traj = [float(initial[ag][al])] * T
+                v.local[ag] = traj
+                if kind == "consensus":
+                    v.mult[ag] = [0] * T
+                else:
+                    v.mult = [0] * T
+    vars_ = state["vars"]
+    for v in vars_.values():
+        v.update_mean()
+    for v in vars_.values():
+        v.shift(horizon)
+    hist = []
+    converged = False
+    it = 0
+    for it in range(1, admm_iter_max + 1):
+        for ag, coups in participation.items():
+            inp = {}
+            for al, kind in coups.items():
+                v = vars_[al]
+                inp[al] = (np.array(v.mean), np.array(v.mult[ag])) if kind == "consensus" else \
+                    (np.array(v.diff[ag]), np.array(v.mult))
+            out = solve(ag, inp, rho)
+            for al in coups:
+                vars_[al].local[ag] = list(np.ravel(out[al]))
+        for v in vars_.values():
+            v.update_mean()
+        for v in vars_.values():
+            v.update_multipliers(rho)
+        prim, dual, flat_locals, flat_means, flat_mult = [], [], [], [], []
+        for v in vars_.values():
+            prim.extend(v.primal_residual.flatten())
+            dual.extend((rho * v.delta_mean).flatten())
+            flat_locals.extend(list(v.local.values()))
+            flat_means.extend(v.mean)
+            if isinstance(v, _Consensus):
+                flat_mult.extend(list(v.mult.values()))
+            else:
+                flat_mult.extend(v.mult)
+        pn, dn = float(np.linalg.norm(prim)), float(np.linalg.norm(dual))
+        hist.append((pn, dn, rho))
+        if penalty_change_threshold > 1:
+            if pn > penalty_change_threshold * dn:
+                rho = rho * penalty_change_factor
+            elif dn > penalty_change_threshold * pn:
+                rho = rho / penalty_change_factor
+        if use_relative_tolerances:
+            sp = max(_norm_lists(flat_locals), float(np.linalg.norm(flat_means)))
+            sd = _norm_lists(flat_mult)
+            eps_pri = np.sqrt(len(flat_mult)) * abs_tol + rel_tol * sp
+            eps_dual = np.sqrt(len(flat_locals)) * abs_tol + rel_tol * sd
+            conv = pn < eps_pri and dn < eps_dual
+        else:
+            conv = pn < primal_tol and dn < dual_tol
+        if conv:
+            converged = True
+            break
+    return state, hist, it, converged
+
+
+def _norm_lists(items):
+    return float(np.sqrt(sum(float(np.sum(np.square(np.asarray(x, float)))) for x in items)))
+
+
+def local_round(participation, initial, solve, rho, shift_by, max_iterations, T=None, state=None):
+    """One control step of ``LocalADMM.process`` (`modules/dmpc/admm/admm.py:873-937`) for
+    all agents at once. Returns (state, per-iteration {alias: mean})."""
+    if state is None:
+        state = {"local": {}, "mult": {}}
+        for ag, coups in participation.items():
+            for al in coups:
+                state["local"][(ag, al)] = [float(initial[ag][al])] * T
+                state["mult"][(ag, al)] = [0] * T
+    loc, mult = state["local"], state["mult"]
+
+    def sh(seq):
+        return list(seq[shift_by:]) + list(seq[-shift_by:])
+
+    for k in list(loc):
+        loc[k] = sh(loc[k])
+        mult[k] = sh(mult[k])
+    aliases = sorted({al for coups in participation.values() for al in coups})
+
+    def means():
+        out = {}
+        for al in aliases:
+            out[al] = np.mean(np.array([loc[(ag, al)] for ag, c in participation.items() if al in c]), axis=0)
+        return out
+
+    mean = means()
+    hist = []
+    for _ in range(max_iterations):
+        for ag, coups in participation.items():
+            inp = {}
+            for al, kind in coups.items():
+                own = np.array(loc[(ag, al)])
+                inp[al] = (mean[al], np.array(mult[(ag, al)])) if kind == "consensus" else \
+                    (own - mean[al], np.array(mult[(ag, al)]))
+            out = solve(ag, inp, rho)
+            for al in coups:
+                loc[(ag, al)] = list(np.ravel(out[al]))
+        mean = means()
+        for ag, coups in participation.items():
+            for al, kind in coups.items():
+                own = np.array(loc[(ag, al)])
+                lam = np.array(mult[(ag, al)])
+                if kind == "consensus":
+                    mult[(ag, al)] = list(lam - rho * (mean[al] - own))
+                else:
+                    diff = own - mean[al]
+                    mult[(ag, al)] = list(lam - rho * (diff - own))
+        hist.append({al: mean[al].copy() for al in aliases})
+    return state, hist

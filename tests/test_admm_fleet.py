@@ -1,0 +1,139 @@
+"""Fleet ADMM driver host logic on CPU (test-side device ops, oracle IPM solves)
+against the oracle's loop restatements of the reference
+(`oracle/admm.py`: ``coordinated_round`` = ADMMCoordinator._fast_process,
+``local_round`` = LocalADMM.process), and the partitioned (world_size 2, gloo)
+driver against the single-process one.
+
+Tolerances (north star, fp64): consensus / residual histories rel 1e-5.
+"""
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from agentlib_mpc_amd import benchmarks as bm
+from agentlib_mpc_amd.admm.fleet import ADMMFleet
+from oracle import admm as oadmm
+from oracle import nlps
+from tests.admm_cases import C2Oracle, C4Oracle
+from tests.cpu_admm_ops import CpuADMMOps
+
+RTOL = 1e-5
+
+
+def _c4_ops(N):
+    return CpuADMMOps({"room": nlps.exchange_room(N=N), "supply": nlps.exchange_supply(N=N)})
+
+
+def _c2_ops(N):
+    return CpuADMMOps({"room": nlps.admm_room(N=N), "ahu": nlps.admm_ahu(N=N)})
+
+
+def test_fleet_groups_and_rows():
+    classes = bm.c2_fleet_classes(n_blocks=2, N=2)
+    fl = ADMMFleet(classes, device="cpu", ops=_c2_ops(2))
+    assert fl.G == 8 and fl.R == 16 and fl.max_rows == 2
+    assert list(fl.gstart) == list(range(0, 17, 2))
+    # every alias: one room row then the air handler row
+    for g, al in enumerate(fl.aliases):
+        i, b = int(al[4]) - 1, int(al.split("_b")[1])
+        assert fl.slot_rows[(0, 0)][4 * b + i] == 2 * g
+        assert fl.slot_rows[(1, i)][b] == 2 * g + 1
+
+
+def test_local_exchange_round_matches_oracle():
+    N, iters = 4, 3
+    fl = ADMMFleet(bm.c4_fleet_classes(n_rooms=2, n_supply=1, N=N), device="cpu", ops=_c4_ops(N))
+    out = fl.run_local(penalty_factor=1e4, max_iterations=iters)
+    orc = C4Oracle(N, bm.C4_ROOMS[:2])
+    shift = 1  # first multiple-shooting grid point >= ts
+    state, hist = oadmm.local_round(orc.participation, orc.initial, orc, 1e4, shift, iters, T=N)
+    np.testing.assert_allclose(fl.trajectories()["mDot_coupling"], hist[-1]["mDot_coupling"],
+                               rtol=RTOL, atol=1e-9)
+    np.testing.assert_allclose(fl.locals_of("room", "mDot_out")[1], state["local"][("room1", "mDot_coupling")],
+                               rtol=RTOL, atol=1e-9)
+    np.testing.assert_allclose(fl.multipliers_of("supply", "mDot_out")[0],
+                               state["mult"][("supply0", "mDot_coupling")], rtol=RTOL, atol=1e-6)
+    assert out["converged_solves"] == 3 * iters
+
+
+def test_coordinated_consensus_round_matches_oracle():
+    N, iters = 2, 3
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N), device="cpu", ops=_c2_ops(N))
+    out = fl.run_coordinated(0.4, admm_iter_max=iters, use_relative_tolerances=False, primal_tol=0.002,
+                             dual_tol=0.1)
+    orc = C2Oracle(N, bm.C2_ROOMS)
+    state, hist, it, conv = oadmm.coordinated_round(
+        orc.participation, orc.initial, orc, 0.4, N, iters, primal_tol=0.002, dual_tol=0.1,
+        use_relative_tolerances=False, T=3 * N)
+    assert out["iterations"] == it and out["converged"] == conv
+    got = np.array([[r.primal_residual, r.dual_residual] for r in out["records"]])
+    np.testing.assert_allclose(got, np.array(hist)[:, :2], rtol=RTOL, atol=1e-10)
+    for i in range(4):
+        al = f"mDot{i + 1}_coupling_b0"
+        np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
+
+
+def test_relative_tolerance_totals_match_oracle():
+    """The moment identities behind the single all-reduce reproduce the
+    reference's relative stopping quantities (admm_coordinator.py:405-419)."""
+    N, iters = 2, 2
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N), device="cpu", ops=_c2_ops(N))
+    out = fl.run_coordinated(0.4, admm_iter_max=iters, use_relative_tolerances=True, abs_tol=1e-12,
+                             rel_tol=1e-12, penalty_change_threshold=1.5)
+    orc = C2Oracle(N, bm.C2_ROOMS)
+    _, hist, it, _ = oadmm.coordinated_round(orc.participation, orc.initial, orc, 0.4, N, iters,
+                                             use_relative_tolerances=True, abs_tol=1e-12, rel_tol=1e-12,
+                                             penalty_change_threshold=1.5, T=3 * N)
+    got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["records"]])
+    np.testing.assert_allclose(got, np.array(hist), rtol=RTOL, atol=1e-10)
+
+
+# ---------------------------------------------------------------------------
+# world_size 2 (gloo): agents partitioned across ranks, one all-reduce per iteration
+# ---------------------------------------------------------------------------
+
+def _worker(rank, world, init_file, N, iters, out_file):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        full = bm.c4_fleet_classes(n_rooms=4, n_supply=1, N=N)
+        room, supply = full
+        # rank r keeps rooms [2r, 2r+2); rank 0 also holds the supply unit
+        from agentlib_mpc_amd.admm.fleet import FleetClass
+
+        lo, hi = (2 * rank, 2 * rank + 2) if world == 2 else (0, 4)
+        sl = lambda a: a[lo:hi]  # noqa: E731
+        mine = [FleetClass("room", room.backend, (sl(room.p0), sl(room.lbw), sl(room.ubw), sl(room.w0)),
+                           aliases={"mDot_out": "mDot_coupling"}, initial={"mDot_out": 0.02})]
+        if rank == 0:
+            mine.append(supply)
+        fl = ADMMFleet(mine, device="cpu", ops=_c4_ops(N), comm="default" if world > 1 else None)
+        out = fl.run_local(penalty_factor=1e4, max_iterations=iters)
+        np.savez(f"{out_file}.{rank}.npz", mean=fl.trajectories()["mDot_coupling"],
+                 prim=np.array([r.primal_residual for r in out["records"]]),
+                 locals=fl.locals_of("room", "mDot_out"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, N, iters, tmp):
+    init = os.path.join(tmp, f"init{world}")
+    out = os.path.join(tmp, f"out{world}")
+    mp.spawn(_worker, args=(world, init, N, iters, out), nprocs=world, join=True)
+    return [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
+
+
+def test_partitioned_fleet_world2_matches_world1():
+    N, iters = 3, 2
+    with tempfile.TemporaryDirectory() as tmp:
+        one = _run(1, N, iters, tmp)[0]
+        two = _run(2, N, iters, tmp)
+    for r in two:
+        np.testing.assert_allclose(r["mean"], one["mean"], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(r["prim"], one["prim"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(np.concatenate([two[0]["locals"], two[1]["locals"]]), one["locals"],
+                               rtol=1e-10, atol=1e-12)

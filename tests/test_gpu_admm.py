@@ -1,0 +1,120 @@
+"""GPU parity of the ADMM path: the HIP ADMM kernels (C ABI) against their
+numpy restatement, and the fleet driver on the GPU against the oracle's loop
+restatements of the reference (`oracle/admm.py`) with oracle IPM solves.
+
+Tolerances: kernels 1e-12 (fp64 atomics reorder sums); trajectories and
+residual histories rel 1e-5 (north star).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from agentlib_mpc_amd import benchmarks as bm
+from agentlib_mpc_amd.admm.fleet import ADMMFleet
+from agentlib_mpc_amd.admm.ops import NativeADMMOps
+from oracle import admm as oadmm
+from tests.admm_cases import C2Oracle, C4Oracle
+from tests.cpu_admm_ops import CpuADMMOps
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _pair(a):
+    return torch.as_tensor(a).cuda(), torch.as_tensor(np.array(a, copy=True))
+
+
+@pytest.mark.parametrize("T,sizes,n_global", [(10, [5, 1, 300, 2], 0), (30, [2] * 7, 3), (300, [3, 600], 1)])
+def test_admm_kernels_match_restatement(T, sizes, n_global):
+    rng = np.random.default_rng(T)
+    G = len(sizes)
+    gstart = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    R = int(gstart[-1])
+    X = rng.normal(0.02, 0.01, (R, T))
+    LAM = rng.normal(0.0, 1.0, (R, T))
+    MEAN = rng.normal(0.02, 0.01, (G, T))
+    GM = rng.normal(0.0, 1.0, (G, T))
+    EX = (np.arange(G) % 2).astype(np.int32)
+    gpu, cpu = NativeADMMOps(), CpuADMMOps({})
+    res = []
+    for ops, mk in ((gpu, lambda a: _pair(a)[0]), (cpu, lambda a: _pair(a)[1])):
+        gs, x, lam, mean, gm, ex = map(mk, (gstart, X, LAM, MEAN, GM, EX))
+        dmean = mk(np.zeros((G, T)))
+        diff = mk(np.zeros((R, T)))
+        mom = mk(np.zeros(ops.moments_size(G, T)))
+        ops.moments(G, n_global, T, gs, max(sizes), x, lam, mean, mom)
+        off = n_global * (5 * T + 1)
+        tot = mom[off:off + 8]
+        ops.finalize(n_global, G, n_global, T, mom, ex, gm, 0.7, mean, dmean, tot)
+        ops.finalize(0, n_global, n_global, T, mom, ex, gm, 0.7, mean, dmean, tot)
+        ops.consensus_multipliers(G, T, gs, max(sizes), x, mean, 0.7, lam)
+        ops.exchange_update(G, T, gs, max(sizes), x, mean, diff, gm, 0.7)
+        ops.shift(T, 3, lam)
+        cols = mk(rng.permutation(T + 5)[:T].astype(np.int32))
+        dst = mk(np.zeros((R, T + 5)))
+        ops.scatter_rows(T, x, None, dst, cols)
+        ops.fill_column(dst, 2, 1.5)
+        back = mk(np.zeros((R, T)))
+        ops.gather_rows(T, dst, cols, back, mk(np.arange(R, dtype=np.int32)[::-1].copy()))
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in (mom, mean, dmean, lam, diff, gm, dst, back)])
+    for a, b in zip(*res):
+        np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-13)
+
+
+def test_gpu_local_exchange_fleet_matches_oracle():
+    """examples/exchange_admm: 4 rooms + supply, N=10, ts=120, rho=1e4 (LocalADMM)."""
+    N, iters = 10, 4
+    fl = ADMMFleet(bm.c4_fleet_classes(n_rooms=4, n_supply=1, N=N))
+    out = fl.run_local(penalty_factor=1e4, max_iterations=iters)
+    assert out["converged_solves"] == 5 * iters
+    orc = C4Oracle(N, bm.C4_ROOMS)
+    state, hist = oadmm.local_round(orc.participation, orc.initial, orc, 1e4, 1, iters, T=N)
+    np.testing.assert_allclose(fl.trajectories()["mDot_coupling"], hist[-1]["mDot_coupling"],
+                               rtol=RTOL, atol=1e-9)
+    loc = fl.locals_of("room", "mDot_out")
+    for i in range(4):
+        np.testing.assert_allclose(loc[i], state["local"][(f"room{i}", "mDot_coupling")], rtol=RTOL, atol=1e-9)
+    np.testing.assert_allclose(fl.multipliers_of("room", "mDot_out")[0],
+                               state["mult"][("room0", "mDot_coupling")], rtol=RTOL, atol=1e-6)
+
+
+def test_gpu_coordinated_fleet_matches_oracle():
+    """examples/4_Room_ADMM_Coordinator: rho=0.4, N=10, ts=60, absolute criterion."""
+    N, iters = 10, 3
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N))
+    out = fl.run_coordinated(0.4, admm_iter_max=iters, use_relative_tolerances=False, primal_tol=0.002,
+                             dual_tol=0.1)
+    orc = C2Oracle(N, bm.C2_ROOMS)
+    state, hist, it, conv = oadmm.coordinated_round(
+        orc.participation, orc.initial, orc, 0.4, N, iters, primal_tol=0.002, dual_tol=0.1,
+        use_relative_tolerances=False, T=3 * N)
+    assert out["iterations"] == it and out["converged"] == conv
+    got = np.array([[r.primal_residual, r.dual_residual] for r in out["records"]])
+    np.testing.assert_allclose(got, np.array(hist)[:, :2], rtol=RTOL, atol=1e-10)
+    for i in range(4):
+        al = f"mDot{i + 1}_coupling_b0"
+        np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
+        np.testing.assert_allclose(fl.multipliers_of("ahu", f"mDot_out_{i + 1}")[0],
+                                   state["vars"][al].mult["ahu"], rtol=RTOL, atol=1e-8)
+
+
+def test_gpu_fleet_blocks_are_independent():
+    """A scaled C2 fleet (many 4-room blocks, one launch per class) gives every
+    block the trajectory a single-block run gives it."""
+    N = 10
+    big = ADMMFleet(bm.c2_fleet_classes(n_blocks=64, N=N, seed=5))
+    big.run_coordinated(0.4, admm_iter_max=3, use_relative_tolerances=False, primal_tol=0.0, dual_tol=0.0)
+    one = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N, seed=5, block_offset=37))
+    one.run_coordinated(0.4, admm_iter_max=3, use_relative_tolerances=False, primal_tol=0.0, dual_tol=0.0)
+    tb, to = big.trajectories(), one.trajectories()
+    for i in range(4):
+        al = f"mDot{i + 1}_coupling_b37"
+        np.testing.assert_allclose(tb[al], to[al], rtol=1e-9, atol=1e-12)

@@ -1924,8 +1924,9 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
 #pragma unroll 1
     for (int mu_up = 0; mu_up < 64; ++mu_up) {
       if (e0.err_at(mu) > o.kappa_eps * mu || mu <= o.mu_min) break;
-      mu = fmax(o.tol / 10.0, fmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
-      mu = fmax(mu, o.mu_min);
+      const double new_mu = fmax(fmax(o.tol / 10.0, o.mu_min), fmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
+      if (new_mu == mu) break;  // IPOPT MonotoneMuUpdate: done when mu no longer changes
+      mu = new_mu;
       tau = fmax(o.tau_min, 1.0 - mu);
       nfilt = 0;
     }

@@ -571,8 +571,9 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
     if (it >= o->max_iter) break;
     for (int g = 0; g < 64; ++g) {
       if (opt_error(w, mu, 0, 0, 0) > 10.0 * mu || mu <= 1e-11) break;
-      mu = fmax(o->tol / 10.0, fmin(0.2 * mu, pow(mu, 1.5)));
-      mu = fmax(mu, 1e-11);
+      const double new_mu = fmax(fmax(o->tol / 10.0, 1e-11), fmin(0.2 * mu, pow(mu, 1.5)));
+      if (new_mu == mu) break;  /* IPOPT: done when mu no longer changes */
+      mu = new_mu;
       tau = fmax(0.99, 1.0 - mu);
       nfilt = 0;
     }

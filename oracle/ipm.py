@@ -270,6 +270,7 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
     history = []
     status = "Maximum_Iterations_Exceeded"
     it = 0
+    mu_floor = max(o.tol / 10.0, o.mu_min)
     while True:
         err0, dual, primal, compl = opt_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, 0.0)
         # unscaled checks
@@ -289,8 +290,10 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
             err_mu = opt_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu)[0]
             if err_mu > o.kappa_eps * mu or mu <= o.mu_min:
                 break
-            mu = max(o.tol / 10.0, min(o.kappa_mu * mu, mu ** o.theta_mu))
-            mu = max(mu, o.mu_min)
+            new_mu = max(mu_floor, min(o.kappa_mu * mu, mu ** o.theta_mu))
+            if new_mu == mu:  # IPOPT MonotoneMuUpdate: done when mu no longer changes
+                break
+            mu = new_mu
             tau = max(o.tau_min, 1.0 - mu)
             filt = []
         Hx = H(x, lam)

@@ -42,6 +42,7 @@ def test_admm_kernels_match_restatement(T, sizes, n_global):
     MEAN = rng.normal(0.02, 0.01, (G, T))
     GM = rng.normal(0.0, 1.0, (G, T))
     EX = (np.arange(G) % 2).astype(np.int32)
+    COLS = rng.permutation(T + 5)[:T].astype(np.int32)
     gpu, cpu = NativeADMMOps(), CpuADMMOps({})
     res = []
     for ops, mk in ((gpu, lambda a: _pair(a)[0]), (cpu, lambda a: _pair(a)[1])):
@@ -57,7 +58,7 @@ def test_admm_kernels_match_restatement(T, sizes, n_global):
         ops.consensus_multipliers(G, T, gs, max(sizes), x, mean, 0.7, lam)
         ops.exchange_update(G, T, gs, max(sizes), x, mean, diff, gm, 0.7)
         ops.shift(T, 3, lam)
-        cols = mk(rng.permutation(T + 5)[:T].astype(np.int32))
+        cols = mk(COLS)
         dst = mk(np.zeros((R, T + 5)))
         ops.scatter_rows(T, x, None, dst, cols)
         ops.fill_column(dst, 2, 1.5)

@@ -71,23 +71,45 @@ def flops_model(gen, stats):
     return float(tot.sum())
 
 
-def cpu_baseline(p, lbw, ubw, w0, tol, repeats=3):
+def cpu_baseline(p, lbw, ubw, w0, tol, min_seconds=10.0, max_repeats=200):
     """C restatement of the oracle IPM (oracle/c/ipm_oracle.c), OpenMP over the
-    host cores allotted to this process (OMP_NUM_THREADS), on the rank-0 fleet."""
+    host cores allotted to this process (OMP_NUM_THREADS), on the rank-0 fleet,
+    repeated until at least ``min_seconds`` of wall time (a bounded sample)."""
     from oracle import cbuild
 
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     cbuild.build()
     ok = 0
+    repeats = 0
     t0 = time.perf_counter()
-    for _ in range(repeats):
+    while repeats < max_repeats and (repeats == 0 or time.perf_counter() - t0 < min_seconds):
         _, _, n_ok = cbuild.solve_room_fleet(p, lbw, ubw, w0, tol=tol, threads=threads)
         ok += n_ok
+        repeats += 1
     dt = time.perf_counter() - t0
     return {"value": ok / dt, "unit": "solves/s", "cores": threads, "kind": "port",
             "sample": f"{repeats} x the rank-0 C3 fleet ({p.shape[0]} agents, same inputs, tol={tol}) "
                       f"with oracle/c/ipm_oracle.c (IPOPT restatement, block-tridiagonal LDL^T, "
                       f"gcc -O3 -march=native, OpenMP {threads} threads): {dt:.2f} s wall"}
+
+
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "s4", "pmc_traffic_c3.json")
+
+
+def pmc_traffic(code_object: str, n_agents: int):
+    """HBM bytes per launch of the bench kernel from the committed rocprofv3 PMC
+    passes (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled as the
+    MI355X guide prescribes for gfx950). Only used when the summary was taken on
+    the same code object and fleet size; otherwise None (PMC cannot run inside
+    the timed process)."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("code_object") != code_object or n_agents != 4096:
+        return None, None
+    return float(d["hbm_bytes_per_launch"]), os.path.relpath(PMC_TRAFFIC, ROOT)
 
 
 def admm_bench(args, world, rank, dev):
@@ -222,6 +244,9 @@ def main():
     value = total_ok * args.steps / wall
     if rank == 0:
         achieved = flops / (kernel_ms * 1e-3) / 1e12
+        from agentlib_mpc_amd.runtime.native import code_object_path
+        traffic, traffic_src = pmc_traffic(code_object_path(prob.gen.key).name, n)
+        io_bytes = n * 8 * (prob.nlp.npar + 3 * prob.nlp.nw + prob.nlp.ng_total) + n * STATS_BYTES
         out = {
             "metric": METRIC,
             "value": value,
@@ -252,7 +277,9 @@ def main():
                 "peak": PEAK_FP64_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP64_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_io_bytes": io_bytes,
                 "kernel": "mpcx_ipm_solve",
                 "kernel_ms": kernel_ms,
                 "flops_per_launch": flops,

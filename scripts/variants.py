@@ -1,0 +1,111 @@
+"""Diagnostic: time compile-time variants of mpcx_ipm_solve on the C3 fleet.
+
+``python scripts/variants.py build`` (CPU) compiles every variant below into
+``_build/variants/``; ``python scripts/variants.py run`` (GPU) times them on the
+bench fleet and checks each against the default build's solution.
+A variant = extra -D defines and/or a source transform of mpcx_ipm.hip.
+"""
+import json
+import os
+import pathlib
+import subprocess
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "agentlib-mpc_amd")]
+
+VARIANTS = {
+    "base": ([], None),
+    "w2": (["-DMPCX_MIN_WAVES=2"], None),
+    "w1": (["-DMPCX_MIN_WAVES=1"], None),
+    "inl_w2": (["-DMPCX_MIN_WAVES=2"], ("__noinline__", "__attribute__((always_inline))")),
+    "inl_w4": ([], ("__noinline__", "__attribute__((always_inline))")),
+}
+
+
+def vdir():
+    from agentlib_mpc_amd.runtime import native
+    return native.KERNEL_DIR.parent / "variants"
+
+
+def build(names):
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.runtime import native
+    be, _ = bm.one_room()
+    gen = be.problem.gen
+    d = vdir()
+    d.mkdir(parents=True, exist_ok=True)
+    for name in names:
+        defs, tr = VARIANTS[name]
+        kern = native.CSRC / "mpcx_ipm.hip"
+        src_text = gen.source
+        if tr is not None:
+            ktxt = kern.read_text().replace(*tr)
+            kp = d / f"mpcx_ipm_{name}.hip"
+            kp.write_text(ktxt)
+            src_text = src_text.replace('#include "mpcx_ipm.hip"', f'#include "{kp}"')
+            assert str(kp) in src_text, "kernel include not found in generated source"
+        src = d / f"{name}.hip"
+        src.write_text(src_text)
+        out = d / f"{name}.hsaco"
+        cmd = [native._hipcc(), "--genco", "--offload-arch=gfx950", "-O3", "-std=c++17", *defs,
+               f"-I{native.INCLUDE}", f"-I{native.CSRC}", str(src), "-o", str(out),
+               "-Rpass-analysis=kernel-resource-usage"]
+        r = subprocess.run(cmd, capture_output=True, text=True, check=True)
+        info = [l.split("remark:")[1].strip() for l in r.stderr.splitlines()
+                if "remark:" in l and any(k in l for k in ("VGPRs:", "Scratch", "Occupancy"))][:4]
+        print(name, info)
+
+
+def run(names):
+    import numpy as np
+    import torch
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import NativeProblem, STATS_BYTES, stats_to_dicts
+    import bench
+    be, cv = bm.one_room(solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
+    n = int(os.environ.get("AGENTS", "4096"))
+    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261017))
+    dev = torch.device("cuda")
+    T = lambda a: torch.as_tensor(a, device=dev).contiguous()
+    tp, tl, tu, tw0 = T(p), T(lbw), T(ubw), T(w0)
+    ref = None
+    res = {}
+    for name in names:
+        nat = NativeProblem(be.problem.gen, hsaco=vdir() / f"{name}.hsaco")
+        nat.set_options(tol=1e-8, max_iter=500)
+        nat.reserve(n)
+        tw = tw0.clone()
+        st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=dev)
+        s = torch.cuda.current_stream()
+        for _ in range(2):
+            tw.copy_(tw0)
+            nat.solve(tp, tl, tu, tw, stats=st, stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 5
+        e0.record(s)
+        for _ in range(reps):
+            tw.copy_(tw0)
+            nat.solve(tp, tl, tu, tw, stats=st, stream=s.cuda_stream)
+        e1.record(s)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        w = tw.cpu().numpy()
+        stats = stats_to_dicts(st.cpu().numpy().tobytes())
+        ok = sum(x["success"] for x in stats)
+        if ref is None:
+            ref = w
+        dev_max = float(np.max(np.abs(w - ref) / (1 + np.abs(ref))))
+        res[name] = {"ms": ms, "solves_per_s": ok / ms * 1e3, "ok": ok, "maxdev_vs_first": dev_max}
+        print(name, json.dumps(res[name]), flush=True)
+        del nat
+    return res
+
+
+if __name__ == "__main__":
+    cmd = sys.argv[1]
+    names = sys.argv[2:] or list(VARIANTS)
+    {"build": build, "run": run}[cmd](names)

@@ -5,6 +5,7 @@
 * ``admm_ahu``        C2 air handler — `examples/4_Room_ADMM_Coordinator/configs/rlt_admm.json`
 * ``exchange_room``   C4 room agent — `examples/exchange_admm/configs/room_1_admm.json`
 * ``exchange_supply`` C4 supply agent — `examples/exchange_admm/configs/rlt_admm.json`
+* ``room_nn``         C5 zone agent (NARX ANNs) — `examples/three_zone_datadriven_admm/configs/mpc/Room_1.json`
 
 Each builder returns ``(backend, current_vars)`` with the example's values;
 keyword arguments override the per-agent values used for synthetic fleets.
@@ -143,12 +144,58 @@ def exchange_supply(N=10, rho=1e4, diff=0.0, lam=0.0, penalty=0.1, solver_option
     return be, cv
 
 
+ROOM_NN_COUPLINGS = (("T_v", 294.15, 285.0, 308.0), ("T_ahu", 295.0, 285.0, 308.0),
+                     ("T_CCA_out", 294.15, 285.0, 310.0), ("T_air_out", 294.0, 285.0, 310.0))
+
+
+def room_nn(N=24, T_air=294.0, T_CCA=294.15, load=100.0, T_amb=299.0, Q_rad=50.0, T_set=295.0,
+            T_upper=301.15, T_lower=290.15, q_T=0.0, s_T=1.0, rho=1.0, zbar=None, lam=0.0,
+            past_couplings=None, anns=None, solver_options=TIGHT):
+    """C5 zone agent: ``RoomCCA`` with two NARX ANNs, backend ``casadi_admm_nn``
+    (`examples/three_zone_datadriven_admm/configs/mpc/Room_1.json`: N=24, ts=1800,
+    q_T=0, s_T=1, couplings T_v/T_ahu/T_CCA_out/T_air_out).  ``zbar`` / ``lam``
+    are per coupling (scalar or length-N trajectory); the synthetic ANNs come
+    from :func:`examples.room_cca_anns`."""
+    from agentlib_mpc_amd.models import examples as ex
+
+    be = create_optimization_backend({
+        "type": "casadi_admm_nn",
+        "model": {"type": "agentlib_mpc_amd.models.examples.RoomCCA",
+                  "ml_model_sources": anns if anns is not None else ex.room_cca_anns(), "dt": 1800},
+        "discretization_options": {"method": "multiple_shooting", "prediction_horizon": N, "time_step": 1800},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    coups = [adt.CouplingEntry(c[0]) for c in ROOM_NN_COUPLINGS]
+    be.setup_optimization(adt.VariableReference(
+        states=["T_air", "T_CCA_0"], controls=[],
+        inputs=["mDot", "mDot_ahu", "d", "T_amb", "Q_rad", "T_set", "T_upper", "T_lower"],
+        parameters=["q_T", "s_T"], outputs=[], couplings=coups))
+    n = len(be.coupling_grid)
+    cv = {
+        "T_air": V("T_air", T_air, 280.15, 303.15), "T_CCA_0": V("T_CCA_0", T_CCA, 280.15, 303.15),
+        "mDot": V("mDot", 0.1), "mDot_ahu": V("mDot_ahu", 0.025), "d": V("d", load),
+        "T_amb": V("T_amb", T_amb), "Q_rad": V("Q_rad", Q_rad), "T_set": V("T_set", T_set),
+        "T_upper": V("T_upper", T_upper), "T_lower": V("T_lower", T_lower),
+        "q_T": V("q_T", q_T), "s_T": V("s_T", s_T), "penalty_factor": V("penalty_factor", rho),
+    }
+    for i, (c, (name, init, lb, ub)) in enumerate(zip(coups, ROOM_NN_COUPLINGS)):
+        cv[name] = V(name, init, lb, ub)
+        zb = init if zbar is None else (zbar[i] if np.ndim(zbar) > 0 else zbar)
+        lm = lam[i] if np.ndim(lam) > 0 else lam
+        cv[c.mean] = V(c.mean, _vals(zb, n))
+        cv[c.multiplier] = V(c.multiplier, _vals(lm, n))
+        past = init if past_couplings is None else past_couplings[i]
+        cv[c.lagged] = V(c.lagged, past)
+    return be, cv
+
+
 BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
     "one_room": one_room,
     "admm_room": admm_room,
     "admm_ahu": admm_ahu,
     "exchange_room": exchange_room,
     "exchange_supply": exchange_supply,
+    "room_nn": room_nn,
 }
 
 

@@ -7,11 +7,14 @@ Equations restate the reference examples:
 * ``AirHandler``   — `examples/4_Room_ADMM_Coordinator/models/rlt_model.py` (C2)
 * ``ExchangeRoom`` — `examples/exchange_admm/models/room_model.py` (C4)
 * ``ExchangeSupply`` — `examples/exchange_admm/models/rlt_model.py` (C4)
+* ``RoomCCA``      — `examples/three_zone_datadriven_admm/models/Room_model.py` (C5, NARX)
 """
 
 from __future__ import annotations
 
 from typing import List
+
+import numpy as np
 
 from agentlib_mpc_amd.models.casadi_model import (
     CasadiInput, CasadiModel, CasadiModelConfig, CasadiOutput, CasadiParameter, CasadiState,
@@ -138,3 +141,95 @@ class ExchangeSupply(CasadiModel):
     def setup_system(self):
         self.mDot_out.alg = -self.mDot
         return self.penalty * self.mDot
+
+
+# ---------------------------------------------------------------------------
+# C5: three-zone data-driven ADMM (`examples/three_zone_datadriven_admm`)
+# ---------------------------------------------------------------------------
+
+from agentlib_mpc_amd.models.casadi_ml_model import CasadiMLModel, CasadiMLModelConfig  # noqa: E402
+
+
+class RoomCCAConfig(CasadiMLModelConfig):
+    """`examples/three_zone_datadriven_admm/models/Room_model.py:13-81`."""
+
+    inputs: List[CasadiInput] = [
+        _inp("T_v", 293.15, unit="K"), _inp("T_ahu", 293.15, unit="K"),
+        _inp("mDot", 0.1), _inp("mDot_ahu", 0.025),
+        _inp("d", 0, unit="W"), _inp("T_amb", 299, unit="K"), _inp("Q_rad", 0, unit="W/m²"),
+        _inp("T_set", 298.55, unit="K"), _inp("T_upper", 301.15, unit="K"), _inp("T_lower", 288.15, unit="K"),
+    ]
+    states: List[CasadiState] = [
+        CasadiState(name="T_air", value=290.15, unit="K"),
+        CasadiState(name="T_CCA_0", value=293.15, unit="K"),
+        CasadiState(name="T_slack", value=0, unit="K"),  # no model -> auxiliary
+    ]
+    parameters: List[CasadiParameter] = [_par("q_T", 1), _par("s_T", 1)]
+    outputs: List[CasadiOutput] = [
+        CasadiOutput(name="T_CCA_out", value=293.15, unit="K"),
+        CasadiOutput(name="T_air_out", value=293.15, unit="K"),
+    ]
+
+
+class RoomCCA(CasadiMLModel):
+    """`Room_model.py:84-105`: T_air and T_CCA_0 are predicted by two ANNs."""
+
+    config: RoomCCAConfig
+
+    def setup_system(self):
+        self.T_CCA_out.alg = self.T_CCA_0
+        self.T_air_out.alg = self.T_air
+        self.constraints = [(self.T_lower, self.T_air + self.T_slack, self.T_upper)]
+        return sum([
+            1 * 10 * self.q_T * (self.T_air - self.T_set) ** 2,
+            1 * 10 * self.s_T * self.T_slack ** 2,
+        ])
+
+
+#: ANN feature lags of `examples/three_zone_datadriven_admm/training_direct.py:575-620`
+T_AIR_FEATURES = {"inputs": {"T_CCA_0": 1, "T_ahu": 1, "mDot_ahu": 1, "d": 2, "T_amb": 1, "Q_rad": 2},
+                  "output": ("T_air", 1)}
+T_CCA_FEATURES = {"inputs": {"T_air": 1, "T_v": 3, "d": 1, "mDot": 2},
+                  "output": ("T_CCA_0", 1)}
+#: (typical value, spread) of each feature, used for the BatchNormalization statistics
+_FEATURE_SCALE = {"T_CCA_0": (295.0, 2.0), "T_ahu": (295.0, 3.0), "mDot_ahu": (0.025, 0.01),
+                  "d": (100.0, 60.0), "T_amb": (299.0, 5.0), "Q_rad": (100.0, 80.0),
+                  "T_air": (296.0, 2.0), "T_v": (295.0, 4.0), "mDot": (0.1, 0.04)}
+
+
+def synthetic_ann(features: dict, seed: int, hidden: int = 32, dt: float = 1800.0):
+    """A seeded ANN with the reference trainer's topology
+    (`ml_model_trainer.py:617-626`: BatchNormalization -> Dense(32, sigmoid) ->
+    Dense(1, linear)) on the lagged features of the three-zone example.  The
+    trained networks of the example are produced at run time by keras
+    (`admm_3zone_sim.py:57-65`) and are not part of the reference, so the C5
+    weights are synthetic; the output weights are scaled so one step changes the
+    temperature by at most a few tenths of a kelvin."""
+    from agentlib_mpc_amd.data_structures.ml_model_datatypes import Feature, OutputFeature, column_order
+    from agentlib_mpc_amd.models.serialized_ml_model import SerializedANN
+
+    rng = np.random.default_rng(seed)
+    inputs = {n: Feature(name=n, lag=l) for n, l in features["inputs"].items()}
+    oname, olag = features["output"]
+    outputs = {oname: OutputFeature(name=oname, lag=olag, output_type="difference", recursive=True)}
+    cols = column_order(inputs, outputs)
+    base = [c.rsplit("_", 1)[0] if c not in _FEATURE_SCALE else c for c in cols]
+    mean = np.array([_FEATURE_SCALE[b][0] for b in base])
+    var = np.array([_FEATURE_SCALE[b][1] ** 2 for b in base])
+    n_in = len(cols)
+    W1 = rng.normal(0.0, 1.0 / np.sqrt(n_in), (n_in, hidden))
+    b1 = rng.normal(0.0, 0.1, hidden)
+    W2 = rng.normal(0.0, 0.6 / np.sqrt(hidden), (hidden, 1))
+    b2 = np.array([-0.5 * W2[:, 0].sum()])  # zero-centred output at sigmoid midpoints
+    layers = [
+        {"class_name": "BatchNormalization", "config": {"axis": -1, "epsilon": 0.001},
+         "weights": [np.ones(n_in), np.zeros(n_in), mean, var]},
+        {"class_name": "Dense", "config": {"units": hidden, "activation": "sigmoid"}, "weights": [W1, b1]},
+        {"class_name": "Dense", "config": {"units": 1, "activation": "linear"}, "weights": [W2, b2]},
+    ]
+    return SerializedANN.from_layers(layers, dt=dt, input=inputs, output=outputs)
+
+
+def room_cca_anns(seed: int = 20261015 + 5):
+    """The two shared networks of the C5 zones (T_air and T_CCA_0)."""
+    return [synthetic_ann(T_AIR_FEATURES, seed), synthetic_ann(T_CCA_FEATURES, seed + 1)]

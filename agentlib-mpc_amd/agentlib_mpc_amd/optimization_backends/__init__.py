@@ -28,10 +28,16 @@ backend_types = {
     "mi355x": BackendImport(import_path=_MOD, class_name="MI355XBackend"),
     "mi355x_basic": BackendImport(import_path=_MOD, class_name="MI355XBaseBackend"),
     "mi355x_admm": BackendImport(import_path=_MOD, class_name="MI355XADMMBackend"),
+    "mi355x_ml": BackendImport(import_path=_MOD, class_name="MI355XMLBackend"),
+    "mi355x_admm_ml": BackendImport(import_path=_MOD, class_name="MI355XADMMNNBackend"),
     # drop-in aliases of the reference keys this backend replaces
     "casadi": BackendImport(import_path=_MOD, class_name="MI355XBackend"),
     "casadi_basic": BackendImport(import_path=_MOD, class_name="MI355XBaseBackend"),
     "casadi_admm": BackendImport(import_path=_MOD, class_name="MI355XADMMBackend"),
+    "casadi_ml": BackendImport(import_path=_MOD, class_name="MI355XMLBackend"),
+    "casadi_nn": BackendImport(import_path=_MOD, class_name="MI355XMLBackend"),
+    "casadi_admm_ml": BackendImport(import_path=_MOD, class_name="MI355XADMMNNBackend"),
+    "casadi_admm_nn": BackendImport(import_path=_MOD, class_name="MI355XADMMNNBackend"),
 }
 
 uninstalled_backend_types = {}

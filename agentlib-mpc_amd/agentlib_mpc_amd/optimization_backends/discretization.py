@@ -161,10 +161,25 @@ class StageNLP:
     stage: StageFunction
     tk_values: np.ndarray
     gap_closing: List[bool]
+    #: index maps to the kernel's lifted stage NLP (NARX transcriptions), else None
+    lift: Optional[object] = None
 
     @property
     def nw(self) -> int:
         return len(self.w_syms)
+
+    # sizes of the NLP the kernel solves (== reference sizes unless lifted)
+    @property
+    def kernel_nw(self) -> int:
+        return self.nx + self.N * (self.nv + self.nx)
+
+    @property
+    def kernel_ng(self) -> int:
+        return self.N * self.ng
+
+    @property
+    def kernel_np(self) -> int:
+        return self.npg + self.N * self.nps
 
     @property
     def npar(self) -> int:

@@ -32,6 +32,7 @@ from agentlib_mpc_amd.data_structures.mpc_datamodels import (
 )
 from agentlib_mpc_amd.models.casadi_model import CasadiModel
 from agentlib_mpc_amd.optimization_backends import discretization as disc
+from agentlib_mpc_amd.optimization_backends import narx
 from agentlib_mpc_amd.optimization_backends.backend import (
     ADMMBackend, BackendConfig, OptimizationBackend,
 )
@@ -129,17 +130,19 @@ class MI355XBackend(OptimizationBackend):
         native = self._native()
         dev = torch.device("cuda")
         t0 = time.perf_counter()
-        tp = torch.as_tensor(np.stack(P), dtype=torch.float64, device=dev)
-        tl = torch.as_tensor(np.stack(LB), dtype=torch.float64, device=dev)
-        tu = torch.as_tensor(np.stack(UB), dtype=torch.float64, device=dev)
-        tw = torch.as_tensor(np.stack(W), dtype=torch.float64, device=dev)
+        LB = np.stack(LB)
+        kp, kl, ku, kw = prob.to_kernel(np.stack(P), LB, np.stack(UB), np.stack(W))
+        tp = torch.as_tensor(kp, dtype=torch.float64, device=dev)
+        tl = torch.as_tensor(kl, dtype=torch.float64, device=dev)
+        tu = torch.as_tensor(ku, dtype=torch.float64, device=dev)
+        tw = torch.as_tensor(kw, dtype=torch.float64, device=dev)
         n = len(batch_vars)
         from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
 
-        lam_g = torch.empty((n, prob.nlp.ng_total), dtype=torch.float64, device=dev)
+        lam_g = torch.empty((n, prob.nlp.kernel_ng), dtype=torch.float64, device=dev)
         st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=dev)
         native.solve(tp, tl, tu, tw, lam_g=lam_g, stats=st)
-        w = tw.cpu().numpy()
+        w = prob.from_kernel(tw.cpu().numpy(), LB)
         stats = stats_to_dicts(st.cpu().numpy().tobytes())
         wall = time.perf_counter() - t0
         results = []
@@ -196,4 +199,38 @@ class MI355XADMMBackend(MI355XBackend, ADMMBackend):
     @property
     def coupling_grid(self) -> list:
         """`casadi_/admm.py:360-362`: grid of the multipliers parameter group."""
+        return list(self.problem.nlp.par_groups[self.system.multipliers.name].grid)
+
+
+class MI355XMLBackend(MI355XBackend):
+    """Backend ``"casadi_ml"`` / ``"casadi_nn"`` replacement (``CasADiBBBackend``,
+    `casadi_/casadi_ml.py:347-397`): NARX models, multiple shooting, solved by the
+    kernel on the lifted stage NLP (:mod:`.narx`)."""
+
+    system_type = narx.MLSystem
+    discretization_types = {DiscretizationMethod.multiple_shooting: narx.NarxMultipleShooting}
+
+    def setup_optimization(self, var_ref):
+        method = self.config.discretization_options.method
+        if method not in self.discretization_types:
+            raise ValueError(f"discretization method {method!r} is not available for ML models "
+                             "(the reference supports multiple_shooting only)")
+        super().setup_optimization(var_ref)
+
+    def get_lags_per_variable(self) -> Dict[str, float]:
+        """`casadi_ml.py:387-397`: history length the MPC module has to keep per variable."""
+        ts = self.config.discretization_options.time_step
+        names = set(self.var_ref.all_variables()) if self.var_ref is not None else set()
+        return {name: (lag - 1) * ts for name, lag in self.system.lags_dict.items() if name in names}
+
+
+class MI355XADMMNNBackend(MI355XMLBackend, ADMMBackend):
+    """Backend ``"casadi_admm_ml"`` / ``"casadi_admm_nn"`` replacement
+    (``CasADiADMMBackend_NN``, `casadi_/casadi_admm_ml.py:508-518`)."""
+
+    system_type = narx.ADMMNNSystem
+    discretization_types = {DiscretizationMethod.multiple_shooting: narx.NarxADMMMultipleShooting}
+
+    @property
+    def coupling_grid(self) -> list:
         return list(self.problem.nlp.par_groups[self.system.multipliers.name].grid)

@@ -139,6 +139,38 @@ class CompiledProblem:
             raise ValueError("incomplete NLP inputs (NaN in parameters or bounds)")
         return p, lbw, ubw, np.nan_to_num(w0)
 
+    # -- reference layout <-> kernel layout (identity unless the NLP is lifted) ----
+    def to_kernel(self, p, lbw, ubw, w0):
+        """Map reference-layout NLP inputs ([n, .] or [.]) to the kernel's stage NLP.
+
+        Lag-window copies of a lifted (NARX) NLP are unbounded and start at the
+        guess of the variable they copy (see :mod:`.narx`)."""
+        lift = self.nlp.lift
+        if lift is None:
+            return p, lbw, ubw, w0
+        kp = np.array(p[..., lift.p_src], order="C")
+        klb = np.array(lbw[..., lift.w_src], order="C")
+        kub = np.array(ubw[..., lift.w_src], order="C")
+        klb[..., lift.w_dup] = -np.inf
+        kub[..., lift.w_dup] = np.inf
+        kw = np.array(w0[..., lift.w_src], order="C")
+        return kp, klb, kub, kw
+
+    def from_kernel(self, w_k: np.ndarray, lbw: np.ndarray) -> np.ndarray:
+        """Reference-layout solution from the kernel solution; reference variables
+        the lifted NLP does not use are fixed past values (= their bound)."""
+        lift = self.nlp.lift
+        if lift is None:
+            return w_k
+        w = np.array(lbw, dtype=float, copy=True)
+        used = lift.w_primary >= 0
+        w[..., used] = w_k[..., lift.w_primary[used]]
+        return w
+
+    def lam_g_from_kernel(self, lam_k: np.ndarray) -> np.ndarray:
+        lift = self.nlp.lift
+        return lam_k if lift is None else lam_k[..., lift.g_of_ref]
+
     def outputs(self, w: np.ndarray) -> Dict[str, np.ndarray]:
         """``_nlp_outputs_to_mpc_outputs``: group matrices of the optimum."""
         return {name: np.asarray(w)[lay.index] for name, lay in self.nlp.var_groups.items()}

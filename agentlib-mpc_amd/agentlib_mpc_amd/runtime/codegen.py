@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import dataclasses
 import hashlib
+import re
 from typing import Dict, List
 
 from agentlib_mpc_amd import symbolic as sx
@@ -164,5 +165,15 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         "",
     ]
     src = "\n".join(out)
+    # network weight tables; ids renumbered by first use so the source is deterministic
+    used = []
+    for m in re.finditer(r"ANN(\d+)_", src):
+        if int(m.group(1)) not in used:
+            used.append(int(m.group(1)))
+    if used:
+        local = {nid: i for i, nid in enumerate(used)}
+        tables = sx.network_tables(used)
+        src = src.replace('#include <math.h>\n', '#include <math.h>\n' + "\n".join(tables) + "\n", 1)
+        src = re.sub(r"ANN(\d+)_", lambda m: f"ANN{local[int(m.group(1))]}_", src)
     key = hashlib.sha1(src.encode()).hexdigest()[:16]
     return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz)

@@ -352,6 +352,112 @@ def sum1(items: Iterable) -> Expr:
 
 
 # ---------------------------------------------------------------------------
+# opaque one-hidden-layer networks (the NARX models of the ML backends)
+# ---------------------------------------------------------------------------
+#
+# A network y = b2 + sum_j w2_j act(b1_j + sum_i W1_ij x_i) is one n-ary node
+# ``annv<id>`` instead of its expanded graph.  Its derivatives are nodes too:
+# ``annd<id>_<i>`` = dy/dx_i and ``anndd<id>_<i>_<k>`` (i >= k) = d2y/dx_i dx_k,
+# so gradients and Lagrangian Hessians stay compact, and the code generator
+# evaluates each network once per stage in a loop over the hidden units with
+# the weights in constant memory (only the derivative entries that are used).
+
+_ACTS = ("sigmoid", "tanh", "linear", "softplus", "exponential", "gaussian")
+
+
+class Network:
+    """Dense weights of a single-hidden-layer, single-output network."""
+
+    def __init__(self, W1: np.ndarray, b1: np.ndarray, w2: np.ndarray, b2: float, act: str):
+        if act not in _ACTS:
+            raise ValueError(f"activation {act!r} has no smooth closed-form derivatives")
+        self.W1 = np.ascontiguousarray(W1, dtype=float)   # [n_in, H]
+        self.b1 = np.asarray(b1, dtype=float).reshape(-1)
+        self.w2 = np.asarray(w2, dtype=float).reshape(-1)
+        self.b2 = float(b2)
+        self.act = act
+        self.n_in, self.H = self.W1.shape
+
+    def key(self) -> tuple:
+        return (self.act, self.b2, self.W1.tobytes(), self.b1.tobytes(), self.w2.tobytes())
+
+    def act_derivs(self, a):
+        """act(a), act'(a), act''(a) (numpy)."""
+        if self.act == "sigmoid":
+            s = 1.0 / (1.0 + np.exp(-a))
+            s1 = s * (1.0 - s)
+            return s, s1, s1 * (1.0 - 2.0 * s)
+        if self.act == "tanh":
+            t = np.tanh(a)
+            t1 = 1.0 - t * t
+            return t, t1, -2.0 * t * t1
+        if self.act == "linear":
+            return a, np.ones_like(a), np.zeros_like(a)
+        if self.act == "softplus":
+            s = 1.0 / (1.0 + np.exp(-a))
+            return np.log(1.0 + np.exp(a)), s, s * (1.0 - s)
+        if self.act == "exponential":
+            e = np.exp(a)
+            return e, e, e
+        g = np.exp(-a * a)  # gaussian
+        return g, -2.0 * a * g, (4.0 * a * a - 2.0) * g
+
+    def evaluate(self, x: np.ndarray):
+        """value [...], gradient [..., n_in], Hessian [..., n_in, n_in] on rows x [..., n_in]."""
+        a = x @ self.W1 + self.b1
+        s0, s1, s2 = self.act_derivs(a)
+        v = s0 @ self.w2 + self.b2
+        g = (s1 * self.w2) @ self.W1.T
+        h = np.einsum("...j,ij,kj->...ik", s2 * self.w2, self.W1, self.W1)
+        return v, g, h
+
+
+_NETWORKS: List[Network] = []
+_NETWORK_IDS: Dict[tuple, int] = {}
+
+
+def register_network(net: Network) -> int:
+    """Intern a network; identical weights share one id."""
+    k = net.key()
+    if k not in _NETWORK_IDS:
+        _NETWORK_IDS[k] = len(_NETWORKS)
+        _NETWORKS.append(net)
+    return _NETWORK_IDS[k]
+
+
+def network(net_id: int) -> Network:
+    return _NETWORKS[net_id]
+
+
+def ann_call(net_id: int, inputs: Sequence) -> Expr:
+    """Output of network ``net_id`` at ``inputs`` (one node)."""
+    args = tuple(as_expr(x) for x in inputs)
+    if len(args) != _NETWORKS[net_id].n_in:
+        raise ValueError("network input size mismatch")
+    return Expr(f"annv{net_id}", args)
+
+
+def ann_parse(op: str):
+    """(kind, net id, i, k) of a network op, or None: kind in {'v', 'd', 'dd'}."""
+    if not op.startswith("ann"):
+        return None
+    if op.startswith("annv"):
+        return "v", int(op[4:]), -1, -1
+    if op.startswith("anndd"):
+        nid, i, k = op[5:].split("_")
+        return "dd", int(nid), int(i), int(k)
+    nid, i = op[4:].split("_")
+    return "d", int(nid), int(i), -1
+
+
+def _ann_node(kind: str, nid: int, args, i: int = -1, k: int = -1) -> Expr:
+    if kind == "d":
+        return Expr(f"annd{nid}_{i}", tuple(args))
+    i, k = max(i, k), min(i, k)
+    return Expr(f"anndd{nid}_{i}_{k}", tuple(args))
+
+
+# ---------------------------------------------------------------------------
 # traversal helpers
 # ---------------------------------------------------------------------------
 
@@ -406,6 +512,8 @@ def substitute(outputs: Sequence[Expr], mapping: Dict[Expr, Union[Expr, float]])
 
 
 def _rebuild(op: str, args: List[Expr]) -> Expr:
+    if op.startswith("ann"):
+        return Expr(op, tuple(args))
     if op == "add":
         return add(*args)
     if op == "sub":
@@ -454,6 +562,18 @@ def _diff_node(n: Expr, x: Expr, m: Dict[int, Expr]) -> Expr:
         return ONE if n is x else ZERO
     if op == "const":
         return ZERO
+    if op.startswith("ann"):
+        kind, nid, i, _ = ann_parse(op)
+        if kind == "dd":
+            raise NotImplementedError("third derivatives of networks are not needed by the solver")
+        out = ZERO
+        for j, a in enumerate(n.args):
+            da = m[a.uid]
+            if da.is_const(0.0):
+                continue
+            dn = _ann_node("d", nid, n.args, j) if kind == "v" else _ann_node("dd", nid, n.args, i, j)
+            out = add(out, mul(dn, da))
+        return out
     a = n.args[0]
     da = m[a.uid]
     if op == "neg":
@@ -545,6 +665,12 @@ def evaluate(outputs: Sequence, values: Dict[Expr, Union[float, np.ndarray]]) ->
             if op == "sym":
                 raise KeyError(f"No value for symbol {n.name}")
             a = [vals[x.uid] for x in n.args]
+            if op.startswith("ann"):
+                kind, nid, i, k = ann_parse(op)
+                xs = np.stack(np.broadcast_arrays(*a), axis=-1)
+                v, g, h = _NETWORKS[nid].evaluate(xs)
+                vals[n.uid] = v if kind == "v" else (g[..., i] if kind == "d" else h[..., i, k])
+                continue
             vals[n.uid] = _NUMPY_OPS[op](*a)
     return [np.asarray(vals[o.uid], dtype=float) for o in outs]
 
@@ -590,11 +716,22 @@ def count_ops(outputs: Sequence[Expr]) -> Dict[str, int]:
 
 
 def flop_count(outputs: Sequence[Expr]) -> int:
-    c = count_ops(outputs)
+    nodes = topo_order([as_expr(o) for o in outputs])
+    groups: Dict[tuple, set] = {}
+    for n in nodes:
+        pa = ann_parse(n.op) if n.op.startswith("ann") else None
+        if pa is not None:
+            groups.setdefault((pa[1], tuple(a.uid for a in n.args)), set()).add(pa[0] + str(pa[2]) + str(pa[3]))
+    ann_flops = 0
+    for (nid, _), used in groups.items():
+        net = _NETWORKS[nid]
+        # pre-activation + activation (+ derivatives) + one FMA per used output entry
+        ann_flops += net.H * (2 * net.n_in + 14 + 2 * len(used))
+    c = {k: v for k, v in count_ops(outputs).items() if not k.startswith("ann")}
     # transcendental functions are priced as a handful of flops
     weights = {"exp": 8, "log": 8, "sqrt": 4, "tanh": 10, "sin": 8, "cos": 8,
                "pow": 16, "div": 4}
-    return int(sum(v * weights.get(k, 1) for k, v in c.items()))
+    return int(sum(v * weights.get(k, 1) for k, v in c.items())) + ann_flops
 
 
 # ---------------------------------------------------------------------------
@@ -616,20 +753,31 @@ class CodeGen:
     """Emit straight-line C for a set of outputs.
 
     ``inputs`` maps symbols to C l-value expressions; ``emit`` returns the body
-    lines assigning each output expression to the given C target.
+    lines assigning each output expression to the given C target.  Network
+    nodes (``annv/annd/anndd``) sharing one input tuple are evaluated together
+    by one loop over the hidden units (weights ``ANN<id>_*`` in constant memory,
+    see :func:`network_tables`); ``networks`` collects the ids used.
     """
 
     def __init__(self, inputs: Dict[Expr, str], prefix: str = "t"):
         self.inputs = {k.uid: v for k, v in inputs.items()}
         self.prefix = prefix
+        self.networks = set()
 
     def emit(self, assignments: Sequence[Tuple[str, Expr]], indent: str = "  ") -> List[str]:
         outs = [as_expr(e) for _, e in assignments]
         order = topo_order(outs)
-        # reference counts: inline leaf-ish nodes used once
+        groups: Dict[tuple, Dict[tuple, Expr]] = {}
+        for n in order:
+            pa = ann_parse(n.op) if n.op.startswith("ann") else None
+            if pa is not None:
+                groups.setdefault((pa[1], tuple(a.uid for a in n.args)), {})[pa[0], pa[2], pa[3]] = n
         names: Dict[int, str] = {}
         lines: List[str] = []
+        n_groups = 0
         for n in order:
+            if n.uid in names:
+                continue
             if n.op == "const":
                 names[n.uid] = _c_literal(n.value)
                 continue
@@ -639,13 +787,92 @@ class CodeGen:
                 names[n.uid] = self.inputs[n.uid]
                 continue
             a = [names[x.uid] for x in n.args]
+            if n.op.startswith("ann"):
+                nid = ann_parse(n.op)[1]
+                members = groups[(nid, tuple(x.uid for x in n.args))]
+                gp = f"{self.prefix}n{n_groups}"
+                n_groups += 1
+                lines += _emit_network(nid, a, members, gp, names, indent)
+                self.networks.add(nid)
+                continue
             expr = _c_op(n.op, a)
-            var = f"{self.prefix}{n.uid}"
+            # temporaries are numbered in emission order (not by node uid), so the
+            # generated source -- and the code-object cache key -- is independent of
+            # what else the process has traced before
+            var = f"{self.prefix}{len(lines)}"
             lines.append(f"{indent}const double {var} = {expr};")
             names[n.uid] = var
         for target, e in assignments:
             lines.append(f"{indent}{target} = {names[as_expr(e).uid]};")
         return lines
+
+
+_ACT_C = {
+    "sigmoid": ("const double s0 = 1.0 / (1.0 + exp(-a));", "const double s1 = s0 * (1.0 - s0);",
+                "const double s2 = s1 * (1.0 - 2.0 * s0);"),
+    "tanh": ("const double s0 = tanh(a);", "const double s1 = 1.0 - s0 * s0;",
+             "const double s2 = -2.0 * s0 * s1;"),
+    "linear": ("const double s0 = a;", "const double s1 = 1.0;", "const double s2 = 0.0;"),
+    "softplus": ("const double sg = 1.0 / (1.0 + exp(-a)); const double s0 = log(1.0 + exp(a));",
+                 "const double s1 = sg;", "const double s2 = sg * (1.0 - sg);"),
+    "exponential": ("const double s0 = exp(a);", "const double s1 = s0;", "const double s2 = s0;"),
+    "gaussian": ("const double s0 = exp(-a * a);", "const double s1 = -2.0 * a * s0;",
+                 "const double s2 = (4.0 * a * a - 2.0) * s0;"),
+}
+
+
+def _emit_network(nid: int, x: List[str], members: Dict[tuple, Expr], gp: str,
+                  names: Dict[int, str], indent: str) -> List[str]:
+    """One loop over the hidden units computing the used value/derivative entries."""
+    net = _NETWORKS[nid]
+    T = f"ANN{nid}"
+    nin, H = net.n_in, net.H
+    d1 = sorted(i for (k, i, _) in members if k == "d")
+    d2 = sorted((i, j) for (k, i, j) in members if k == "dd")
+    need_v = ("v", -1, -1) in members
+    L = []
+    if need_v:
+        L.append(f"double {gp}v = {_c_literal(net.b2)};")
+    L += [f"double {gp}g{i} = 0.0;" for i in d1]
+    L += [f"double {gp}h{i}_{j} = 0.0;" for i, j in d2]
+    L.append("#pragma unroll 4")
+    L.append(f"for (int j = 0; j < {H}; ++j) {{")
+    pre = " + ".join([f"{T}_B1[j]"] + [f"({x[i]}) * {T}_W1T[j * {nin} + {i}]" for i in range(nin)
+                                        if np.any(net.W1[i] != 0.0)])
+    L.append(f"  const double a = {pre};")
+    acts = _ACT_C[net.act]
+    L.append("  " + acts[0])
+    L.append(f"  const double w = {T}_W2[j];")
+    if need_v:
+        L.append(f"  {gp}v += w * s0;")
+    if d1:
+        L.append("  " + acts[1])
+        L.append("  const double c1 = w * s1;")
+        L += [f"  {gp}g{i} += c1 * {T}_W1T[j * {nin} + {i}];" for i in d1]
+    if d2:
+        if not d1:
+            L.append("  " + acts[1])
+        L.append("  " + acts[2])
+        L.append("  const double c2 = w * s2;")
+        L += [f"  {gp}h{i}_{j} += c2 * ({T}_W1T[j * {nin} + {i}] * {T}_W1T[j * {nin} + {j}]);" for i, j in d2]
+    L.append("}")
+    for (k, i, j), node in members.items():
+        names[node.uid] = f"{gp}v" if k == "v" else (f"{gp}g{i}" if k == "d" else f"{gp}h{i}_{j}")
+    return [indent + l for l in L]
+
+
+def network_tables(net_ids) -> List[str]:
+    """``__constant__`` weight tables of the networks (W1 transposed: [H][n_in])."""
+    out = []
+    for nid in sorted(net_ids):
+        net = _NETWORKS[nid]
+        w1t = ", ".join(_c_literal(v) for v in net.W1.T.reshape(-1))
+        b1 = ", ".join(_c_literal(v) for v in net.b1)
+        w2 = ", ".join(_c_literal(v) for v in net.w2)
+        out += [f"__constant__ double ANN{nid}_W1T[{net.H * net.n_in}] = {{{w1t}}};",
+                f"__constant__ double ANN{nid}_B1[{net.H}] = {{{b1}}};",
+                f"__constant__ double ANN{nid}_W2[{net.H}] = {{{w2}}};"]
+    return out
 
 
 def _c_op(op: str, a: List[str]) -> str:

@@ -159,6 +159,60 @@ def admm_bench(args, world, rank, dev):
     }
 
 
+def nn_bench(args, world, rank, dev):
+    """C5 (BASELINE.json configs[4]): ``--nn-zones`` three-zone NARX room agents per GPU
+    (two ANNs BN->Dense(32,sigmoid)->Dense(1), backend casadi_admm_nn, N=24, ts=1800),
+    one batched local ADMM solve of the whole fleet per step (first iteration:
+    z-bar = initial coupling values, lambda = 0), cold start."""
+    import torch
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+
+    n = args.nn_zones
+    be, cv = bm.room_nn(solver_options={"ipopt": {"tol": args.tol, "max_iter": 500}})
+    prob = be.problem
+    rng = np.random.default_rng(20261015 + 5 + rank)
+    vals = {"T_air": rng.uniform(292.0, 297.0, n), "d": rng.uniform(50.0, 200.0, n),
+            "T_amb": rng.uniform(295.0, 303.0, n), "Q_rad": rng.uniform(0.0, 200.0, n)}
+    p, lbw, ubw, w0 = prob.to_kernel(*fleet_nlp_inputs(prob, cv, vals))
+    native = be._native()
+    native.reserve(n)
+    T = lambda a: torch.as_tensor(a, device=dev).contiguous()  # noqa: E731
+    tp, tl, tu, tw0 = T(p), T(lbw), T(ubw), T(w0)
+    tw = torch.empty_like(tw0)
+    lam = torch.empty((n, prob.nlp.kernel_ng), dtype=torch.float64, device=dev)
+    st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        tw.copy_(tw0)
+        native.solve(tp, tl, tu, tw, lam_g=lam, stats=st, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    stats = stats_to_dicts(st.cpu().numpy().tobytes())
+    ok = sum(1 for s in stats if s["success"])
+    return {
+        "workload": "C5: three-zone NARX room agents (casadi_admm_nn, 2 ANNs 9/8->32 sigmoid->1, "
+                    "N=24 ts=1800, lifted lag window), one batched local ADMM solve per step",
+        "zones_per_gpu": n, "nlp": prob.nlp.nlp_dims(),
+        "kernel_nlp": {"nw": prob.nlp.kernel_nw, "ng": prob.nlp.kernel_ng, "np": prob.nlp.kernel_np},
+        "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
+        "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
+        "kernel_ms": ev0.elapsed_time(ev1) / args.steps,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,6 +223,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--admm-agents", type=int, default=16384, help="C4 agents per GPU (0: skip)")
     ap.add_argument("--admm-iters", type=int, default=15)
+    ap.add_argument("--nn-zones", type=int, default=1024, help="C5 NARX zones per GPU (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -227,6 +282,7 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
     admm = admm_bench(args, world, rank, dev) if args.admm_agents > 0 else None
+    nn = nn_bench(args, world, rank, dev) if args.nn_zones > 0 else None
     stats = stats_to_dicts(st.cpu().numpy().tobytes())
     n_ok = sum(1 for s in stats if s["success"])
     arr = {"iter": np.array([s["iter_count"] for s in stats]),
@@ -289,6 +345,8 @@ def main():
         }
         if admm is not None:
             out["admm"] = admm
+        if nn is not None:
+            out["narx"] = nn
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(p, lbw, ubw, w0, args.tol)

@@ -13,6 +13,9 @@ independent of the product's tracer and transcriber:
 * ``exchange_room`` / ``exchange_supply`` — backend ``casadi_admm`` multiple
   shooting with Euler (`casadi_/admm.py:198-310`) on
   `examples/exchange_admm/models/{room,rlt}_model.py` (C4).
+* ``room_nn`` — backend ``casadi_admm_nn`` NARX multiple shooting
+  (`casadi_/casadi_admm_ml.py:247-397`) on
+  `examples/three_zone_datadriven_admm/models/Room_model.py` with two ANNs (C5).
 
 Derivatives come from torch fp64 autograd.  Initial guesses follow
 `core/discretization.py:212-245` (cold start).
@@ -449,3 +452,161 @@ def exchange_supply_inputs(prob, N=10, penalty=0.1, rho=1e4, diff=None, lam=None
         lbw[2 * k], ubw[2 * k], w0[2 * k] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
         lbw[2 * k + 1], ubw[2 * k + 1], w0[2 * k + 1] = y_lb, y_ub, 0.5 * (y_lb + y_ub)
     return p, lbw, ubw, w0
+
+
+# ---------------------------------------------------------------------------
+# C5: three-zone NARX room, backend "casadi_admm_nn", multiple shooting
+# ---------------------------------------------------------------------------
+
+def _ann_torch(layers):
+    """Sequential forward of a BatchNormalization -> Dense(sigmoid) -> Dense(linear)
+    network given as [(kind, arrays)] (`models/casadi_predictor.py:306-376`)."""
+    def fwd(x):
+        for kind, arrs in layers:
+            if kind == "bn":
+                gamma, beta, mean, var, eps = arrs
+                x = (x - torch.as_tensor(mean)) / torch.sqrt(torch.as_tensor(var) + eps) * torch.as_tensor(gamma) \
+                    + torch.as_tensor(beta)
+            elif kind == "sigmoid":
+                W, b = arrs
+                x = torch.sigmoid(x @ torch.as_tensor(W) + torch.as_tensor(b))
+            else:
+                W, b = arrs
+                x = x @ torch.as_tensor(W) + torch.as_tensor(b)
+        return x
+    return fwd
+
+
+def room_nn(ann_air, ann_cca, N=24, ts=1800.0) -> OracleProblem:
+    """`casadi_admm_ml.py:247-397` on `three_zone_datadriven_admm/models/Room_model.py`.
+
+    Lags (`training_direct.py:575-620`): max lag L = 3 (T_v), so past states at
+    {-2ts, -ts, 0} and past couplings at {-2ts, -ts} are fixed variables.
+    ``ann_air`` / ``ann_cca``: [(kind, arrays)] layer lists (see ``_ann_torch``)
+    with input columns [T_CCA_0, T_ahu, mDot_ahu, d, d_1, T_amb, Q_rad, Q_rad_1,
+    T_air] and [T_air, T_v, T_v_1, T_v_2, d, mDot, mDot_1, T_CCA_0].
+    w = [x(-2ts), x(-ts), x(0), c(-2ts), c(-ts), {T_slack_k, c_k}_{k<N}, x(ts)..x(N ts)]
+    with x = (T_air, T_CCA_0), c = (T_v, T_ahu, T_CCA_out, T_air_out);
+    p = [q_T, s_T, rho, x0 x3, {d(8), past_c(4)} x2, {d(8), lam(4), zbar(4)} x N],
+    d = (mDot, mDot_ahu, d, T_amb, Q_rad, T_set, T_upper, T_lower).
+    """
+    f_air, f_cca = _ann_torch(ann_air), _ann_torch(ann_cca)
+    n = 6 + 8 + 5 * N + 2 * N
+    m = 5 * N
+    npar = 3 + 6 + 24 + 16 * N
+    names = [f"{v}@{t}" for t in (-2, -1, 0) for v in ("T_air", "T_CCA_0")]
+    names += [f"{v}@{t}" for t in (-2, -1) for v in ("T_v", "T_ahu", "T_CCA_out", "T_air_out")]
+    for k in range(N):
+        names += [f"T_slack@{k}"] + [f"{v}@{k}" for v in ("T_v", "T_ahu", "T_CCA_out", "T_air_out")]
+    for k in range(1, N + 1):
+        names += [f"T_air@{k}", f"T_CCA_0@{k}"]
+
+    def x_at(w, k):  # state at step k (k >= -2)
+        if k <= 0:
+            return w[2 * (k + 2)], w[2 * (k + 2) + 1]
+        i = 14 + 5 * N + 2 * (k - 1)
+        return w[i], w[i + 1]
+
+    def c_at(w, k):  # couplings at step k (k >= -2)
+        if k < 0:
+            i = 6 + 4 * (k + 2)
+        else:
+            i = 14 + 5 * k + 1
+        return w[i:i + 4]
+
+    def d_at(p, k):  # disturbances/settings at step k (k >= -2)
+        i = 9 + 12 * (k + 2) if k < 0 else 33 + 16 * k
+        return p[i:i + 8]
+
+    def stage(w, p, k):
+        q_T, s_T, rho = p[0], p[1], p[2]
+        Ta, Tc = x_at(w, k)
+        Ta1, Tc1 = x_at(w, k + 1)
+        sl = w[14 + 5 * k]
+        c = c_at(w, k)
+        T_v, T_ahu, T_co, T_ao = c[0], c[1], c[2], c[3]
+        dk, dm = d_at(p, k), d_at(p, k - 1)
+        mDot, mDot_ahu, load, T_amb, Q_rad, T_set = dk[0], dk[1], dk[2], dk[3], dk[4], dk[5]
+        T_v1, T_v2 = c_at(w, k - 1)[0], c_at(w, k - 2)[0]
+        base = 33 + 16 * k
+        lam, zbar = p[base + 8:base + 12], p[base + 12:base + 16]
+        xa = torch.stack([Tc, T_ahu, mDot_ahu, load, dm[2], T_amb, Q_rad, dm[4], Ta])
+        xc = torch.stack([Ta, T_v, T_v1, T_v2, load, mDot, dm[0], Tc])
+        na = Ta + f_air(xa[None])[0, 0]
+        ncc = Tc + f_cca(xc[None])[0, 0]
+        cost = 10 * q_T * (Ta - T_set) ** 2 + 10 * s_T * sl ** 2
+        for i in range(4):
+            cost = cost + lam[i] * c[i] + rho / 2 * (zbar[i] - c[i]) ** 2
+        g = torch.stack([Ta + sl, T_co - Tc, T_ao - Ta, na - Ta1, ncc - Tc1])
+        return ts * cost, g
+
+    def f(w, p):
+        return sum(stage(w, p, k)[0] for k in range(N))
+
+    def g(w, p):
+        return torch.cat([stage(w, p, k)[1] for k in range(N)])
+
+    def lbg(p):
+        out = []
+        for k in range(N):
+            out += [p[33 + 16 * k + 7], 0.0, 0.0, 0.0, 0.0]
+        return np.array(out, float)
+
+    def ubg(p):
+        out = []
+        for k in range(N):
+            out += [p[33 + 16 * k + 6], 0.0, 0.0, 0.0, 0.0]
+        return np.array(out, float)
+
+    return OracleProblem("room_nn", n, m, npar, f, g, lbg, ubg, names)
+
+
+def room_nn_inputs(prob, N=24, T_air=294.0, T_CCA=294.15, load=100.0, T_amb=299.0, Q_rad=50.0,
+                   T_set=295.0, T_upper=301.15, T_lower=290.15, q_T=0.0, s_T=1.0, rho=1.0,
+                   mDot=0.1, mDot_ahu=0.025, zbar=None, lam=None, past_couplings=None):
+    """Cold-start inputs (`core/discretization.py:212-245`) for ``room_nn``."""
+    init = np.array([294.15, 295.0, 294.15, 294.0])
+    bounds = [(285.0, 308.0), (285.0, 308.0), (285.0, 310.0), (285.0, 310.0)]
+    zbar = np.tile(init[:, None], N) if zbar is None else np.broadcast_to(np.asarray(zbar, float).reshape(4, -1), (4, N))
+    lam = np.zeros((4, N)) if lam is None else np.broadcast_to(np.asarray(lam, float).reshape(4, -1), (4, N))
+    past = init if past_couplings is None else np.asarray(past_couplings, float)
+    d = [mDot, mDot_ahu, load, T_amb, Q_rad, T_set, T_upper, T_lower]
+    p = [q_T, s_T, rho] + [T_air, T_CCA] * 3
+    for _ in range(2):
+        p += d + list(past)
+    for k in range(N):
+        p += d + list(lam[:, k]) + list(zbar[:, k])
+    p = np.array(p, float)
+    lbw, ubw, w0 = np.zeros(prob.n), np.zeros(prob.n), np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        v, t = name.split("@")
+        t = int(t)
+        if v in ("T_air", "T_CCA_0"):
+            x = T_air if v == "T_air" else T_CCA
+            if t <= 0:
+                lbw[i] = ubw[i] = w0[i] = x
+            else:
+                lbw[i], ubw[i], w0[i] = 280.15, 303.15, x
+        elif v == "T_slack":
+            lbw[i], ubw[i], w0[i] = -np.inf, np.inf, 0.0
+        else:
+            j = ("T_v", "T_ahu", "T_CCA_out", "T_air_out").index(v)
+            if t < 0:
+                lbw[i] = ubw[i] = w0[i] = past[j]
+            else:
+                lbw[i], ubw[i] = bounds[j]
+                w0[i] = 0.5 * (bounds[j][0] + bounds[j][1])
+    return p, lbw, ubw, w0
+
+
+def ann_layers_from_serialized(layer_specs):
+    """[(kind, arrays)] from ``[{"class_name", "config", "weights"}]`` (data only)."""
+    out = []
+    for spec in layer_specs:
+        w = [np.asarray(a, float) for a in spec["weights"]]
+        if spec["class_name"] == "BatchNormalization":
+            out.append(("bn", (w[0], w[1], w[2], w[3], float(spec["config"].get("epsilon", 1e-3)))))
+        elif spec["class_name"] == "Dense":
+            act = spec["config"].get("activation", "linear")
+            out.append(("sigmoid" if act == "sigmoid" else "linear", (w[0], w[1])))
+    return out

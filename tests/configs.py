@@ -74,12 +74,31 @@ def exchange_supply(**kw) -> Case:
     return Case(be, cv, prob, nlps.exchange_supply_inputs(prob, N=N, **o))
 
 
+def room_nn(**kw) -> Case:
+    from agentlib_mpc_amd.models import examples as ex
+
+    anns = ex.room_cca_anns()
+    be, cv = bm.room_nn(anns=anns, **kw)
+    N = kw.get("N", 24)
+    air, cca = (nlps.ann_layers_from_serialized(a.layer_specs()) for a in anns)
+    prob = nlps.room_nn(air, cca, N=N)
+    keys = ("T_air", "T_CCA", "load", "T_amb", "Q_rad", "T_set", "T_upper", "T_lower", "q_T", "s_T",
+            "rho", "zbar", "lam", "past_couplings")
+    o = {k: kw[k] for k in keys if k in kw}
+    if "zbar" in o:
+        o["zbar"] = np.broadcast_to(np.asarray(o["zbar"], float).reshape(4, -1), (4, N))
+    if "lam" in o:
+        o["lam"] = np.broadcast_to(np.asarray(o["lam"], float).reshape(4, -1), (4, N))
+    return Case(be, cv, prob, nlps.room_nn_inputs(prob, N=N, **o))
+
+
 CASES: Dict[str, Callable[..., Case]] = {
     "one_room": one_room,
     "admm_room": admm_room,
     "admm_ahu": admm_ahu,
     "exchange_room": exchange_room,
     "exchange_supply": exchange_supply,
+    "room_nn": room_nn,
 }
 
 

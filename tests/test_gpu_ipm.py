@@ -46,6 +46,9 @@ def _cuda():
     ("exchange_room", {"diff": 0.004, "lam": -5.0, "T0": 303.0}),
     ("exchange_supply", {}),
     ("exchange_supply", {"diff": -0.01, "lam": 20.0}),
+    ("room_nn", {}),
+    ("room_nn", {"T_air": 296.5, "load": 180.0, "Q_rad": 150.0, "q_T": 1.0,
+                 "zbar": [296.0, 293.0, 295.0, 296.0], "lam": [0.5, -0.2, 0.1, 0.0]}),
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)
@@ -55,6 +58,7 @@ def test_gpu_matches_oracle(name, kw):
     nlp = case.backend.problem.nlp
     for r in res:
         assert r.stats["success"], r.stats
+        assert r.stats["iter_count"] > 0
         np.testing.assert_allclose(r.stats["obj"], ref.f, rtol=RTOL_OBJ, atol=1e-9)
         # every variable group on its grid, against the oracle's vector
         for gname, lay in nlp.var_groups.items():

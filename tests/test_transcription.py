@@ -19,6 +19,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "admm_ahu": (160, 150, None),
     "exchange_room": (31, 20, 71),
     "exchange_supply": (20, 10, None),
+    "room_nn": (182, 120, 417),  # n_x≈182, n_g≈120
 }
 
 

@@ -209,7 +209,10 @@ def compile_all(verbose: bool = False):
             if current not in f.name:
                 f.unlink()
     paths = {}
-    for name, fn in BUILDERS.items():
+    # the benchmark structures plus the test-only variants (copy-lifted NARX, N=23)
+    variants = dict(BUILDERS)
+    variants["room_nn_n23"] = lambda: room_nn(N=23)
+    for name, fn in variants.items():
         be, _ = fn()
         paths[name] = be.problem.compile()
         if verbose:

@@ -167,6 +167,7 @@ class LiftMaps:
     p_src: np.ndarray        # [np_kernel] reference parameter index of each kernel parameter
     g_of_ref: np.ndarray     # [ng_ref] kernel constraint index of each reference constraint
     w_primary: np.ndarray    # [nw_ref] kernel index of each reference variable (-1: fixed, unused)
+    steps_per_stage: int = 1  # reference steps per kernel stage
 
     @property
     def nw(self) -> int:
@@ -186,7 +187,163 @@ class NarxMultipleShooting(Discretization):
     def transcribe(self, system: MLSystem) -> StageNLP:
         t = _Transcriber(self.options)
         ref = self._discretize(t, system)
+        S = self._super_stage_length(system, ref["n"], ref["lagged"])
+        if S is not None:
+            return self._lift_super(t, system, ref, S)
         return self._lift(t, system, ref)
+
+    @staticmethod
+    def _super_stage_length(s: MLSystem, N: int, lagged) -> "int | None":
+        """Steps per kernel stage: the smallest S >= (largest lag of a variable) - 1
+        dividing N, so every lagged value a stage reads lies in the stage itself or
+        in the previous one (no copies).  None: no such S (copy-lifting instead)."""
+        var_groups = {q.name for q in s.variables}
+        need = 1
+        for j, per_den in lagged.items():
+            if any(den in var_groups for den in per_den):
+                need = max(need, j)
+        for S in range(need, N + 1):
+            if N % S == 0:
+                return S if S < N or N == need else None
+        return None
+
+    def _lift_super(self, t: _Transcriber, s: MLSystem, ref, S: int) -> StageNLP:
+        """Kernel stages of S steps.  The stage state X_b (boundary b, step bS) holds
+        x(bS) and the window v(bS - j), 1 <= j < lag(v), of every lagged variable, all
+        as primary reference variables (they are the last steps' variables of stage
+        b-1); V holds the remaining variables of the S steps (incl. the internal
+        states).  Same NLP as the reference, only permuted."""
+        mx, lagged, pred, ts, N = ref["mx"], ref["lagged"], ref["pred"], ref["ts"], ref["n"]
+        uid_w = {sym_.uid: i for i, sym_ in enumerate(t.w)}
+        uid_p = {sym_.uid: i for i, sym_ in enumerate(t.p)}
+        nx = s.states.dim
+        NB = N // S
+        var_groups = {q.name for q in s.variables}
+        window: List[Tuple[str, int, int]] = []
+        for j in sorted(lagged):
+            for den, names in lagged[j].items():
+                if den not in var_groups:
+                    continue
+                q = next(q for q in s.quantities if q.name == den)
+                for v_name in names:
+                    window.append((den, q.full_names.index(v_name), j))
+
+        def xbound(b):
+            tm = b * S * ts
+            xs = list(mx[tm][s.states.name])
+            for den, i, j in window:
+                xs.append(mx[tm - j * ts][den][i])
+            return xs
+
+        def vstage(b):
+            xin = {sym_.uid for sym_ in xbound(b) + xbound(b + 1)}
+            out = []
+            for r in range(S):
+                tm = (b * S + r) * ts
+                for den, syms in mx[tm].items():
+                    if den not in var_groups:
+                        continue
+                    out += [sym_ for sym_ in syms if sym_.uid not in xin]
+            out.sort(key=lambda e: uid_w[e.uid])
+            return out
+
+        NXK = nx + len(window)
+        NVK = len(vstage(0))
+        X0 = [sx.sym(f"X0[{i}]") for i in range(NXK)]
+        V = [sx.sym(f"V[{i}]") for i in range(NVK)]
+        X1 = [sx.sym(f"X1[{i}]") for i in range(NXK)]
+        TK = sx.sym("TK")
+        rank = {q.name: r for r, q in enumerate(s.quantities)}
+        glob_idx = list(range(ref["n_global_par"]))
+        PG = [sx.sym(f"PG[{i}]") for i in range(len(glob_idx))]
+        step_g = [[i for i, c in enumerate(t.g) if c[3] == k] for k in range(N)]
+        roles_ref, stage_exprs, PS = None, None, []
+        p_src_stage: List[List[int]] = []
+        g_of_ref = np.empty(len(t.g), dtype=np.int64)
+        ng_stage = None
+        for b in range(NB):
+            vb = vstage(b)
+            if len(vb) != NVK:
+                raise TranscriptionError("NARX stages differ in size")
+            mapping = dict(zip(xbound(b), X0))
+            mapping.update(zip(vb, V))
+            mapping.update(zip(xbound(b + 1), X1))
+            for i, gi in enumerate(glob_idx):
+                mapping[t.p[gi]] = PG[i]
+            for r in range(S):
+                k = b * S + r
+                if k in t.tk_syms:
+                    mapping[t.tk_syms[k]] = sx.add(TK, sx.const(r * ts)) if r else TK
+            gidx = [i for r in range(S) for i in step_g[b * S + r]]
+            ng_stage = len(gidx) if ng_stage is None else ng_stage
+            if len(gidx) != ng_stage:
+                raise TranscriptionError("NARX stages differ in constraint count")
+            gs = [t.g[i] for i in gidx]
+            cost = sx.ZERO
+            for r in range(S):
+                cost = sx.add(cost, t.cost.get(b * S + r, sx.ZERO))
+            exprs = [cost] + [c[0] for c in gs] + [c[1] for c in gs] + [c[2] for c in gs]
+            used_p = sorted({uid_p[fs.uid] for fs in sx.free_symbols(exprs) if fs.uid in uid_p} - set(glob_idx))
+            t0 = b * S * ts
+            roles = [(t.p_labels[pi][0], t.p_labels[pi][1], round((t0 - t.p_labels[pi][2]) / ts)) for pi in used_p]
+            order = sorted(range(len(roles)), key=lambda i: (roles[i][2], rank[roles[i][0]], roles[i][1]))
+            roles = [roles[i] for i in order]
+            used_p = [used_p[i] for i in order]
+            if roles_ref is None:
+                roles_ref = roles
+                PS = [sx.sym(f"PS[{i}]") for i in range(len(roles))]
+            elif roles != roles_ref:
+                raise TranscriptionError(f"stage {b} uses different parameters than stage 0")
+            mapping.update(zip([t.p[pi] for pi in used_p], PS))
+            p_src_stage.append(used_p)
+            sub = sx.substitute(exprs, mapping)
+            allowed = {x.uid for x in X0 + V + X1 + PS + PG + [TK]}
+            for fs in sx.free_symbols(sub):
+                if fs.uid not in allowed:
+                    raise TranscriptionError(f"NARX stage {b} depends on {fs.name}, which is not stage-local")
+            if stage_exprs is None:
+                stage_exprs = sub
+            elif any(a is not c for a, c in zip(stage_exprs, sub)):
+                raise TranscriptionError(f"NARX stage {b} differs structurally from stage 0")
+            for pos, gi in enumerate(gidx):
+                g_of_ref[gi] = b * ng_stage + pos
+        ngs = ng_stage
+        stage = StageFunction(X0=X0, V=V, X1=X1, PS=PS, PG=PG, TK=TK, cost=stage_exprs[0],
+                              g=list(stage_exprs[1:1 + ngs]), g_lb=list(stage_exprs[1 + ngs:1 + 2 * ngs]),
+                              g_ub=list(stage_exprs[1 + 2 * ngs:]))
+        w_src = [uid_w[x.uid] for x in xbound(0)]
+        for b in range(NB):
+            w_src += [uid_w[x.uid] for x in vstage(b)] + [uid_w[x.uid] for x in xbound(b + 1)]
+        w_src = np.asarray(w_src, dtype=np.int64)
+        w_dup = np.zeros(len(w_src), dtype=bool)
+        w_primary = np.full(len(t.w), -1, dtype=np.int64)
+        for ki, ri in enumerate(w_src):
+            if w_primary[ri] != -1:
+                raise TranscriptionError("reference variable mapped twice in the lifted NLP")
+            w_primary[ri] = ki
+        self._check_unused_fixed(t, w_primary)
+        p_src = np.asarray(glob_idx + [pi for st in p_src_stage for pi in st], dtype=np.int64)
+        lift = LiftMaps(w_src=w_src, w_dup=w_dup, p_src=p_src, g_of_ref=g_of_ref, w_primary=w_primary,
+                        steps_per_stage=S)
+        f_total = sx.ZERO
+        for k in range(N):
+            f_total = sx.add(f_total, t.cost.get(k, sx.ZERO))
+        return StageNLP(
+            N=NB, nx=NXK, nv=NVK, ng=ngs, nps=len(PS), npg=len(PG), ts=S * ts,
+            w_syms=list(t.w), p_syms=list(t.p), w_labels=list(t.w_labels), p_labels=list(t.p_labels),
+            g_exprs=[c[0] for c in t.g], g_lb=[c[1] for c in t.g], g_ub=[c[2] for c in t.g],
+            f_expr=f_total, var_groups=t.var_groups, par_groups=t.par_groups, stage=stage,
+            tk_values=np.arange(NB, dtype=float) * S * ts, gap_closing=[c[4] for c in t.g], lift=lift,
+        )
+
+    @staticmethod
+    def _check_unused_fixed(t: _Transcriber, w_primary: np.ndarray):
+        """Reference variables the kernel NLP does not contain must be fixed past values."""
+        for ri in np.nonzero(w_primary < 0)[0]:
+            lay = t.var_groups[t.w_labels[ri][0]]
+            col = [c for c in lay.columns if ri in c][0]
+            if lay.lb_par[lay.columns.index(col)][col.index(ri)] < 0:
+                raise TranscriptionError(f"reference variable {t.w_labels[ri]} is not used by any stage")
 
     # -- reference loops -----------------------------------------------------------
     def _discretize(self, t: _Transcriber, s: MLSystem):

@@ -128,6 +128,12 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
             lp_h.append((f"lp[{pk(lidx(i), lidx(j))}]", e))
     cg = sx.CodeGen(hb, prefix="h")
     h_lines = cg.emit(h_assign + lp_h)
+    # the strided full Hessian is stored only when requested (block-chain fallback)
+    nh = len(h_assign)
+    h_store = h_lines[len(h_lines) - len(h_assign) - len(lp_h):len(h_lines) - len(lp_h)]
+    assert all(l.lstrip().startswith("hess[") for l in h_store)
+    h_lines = (h_lines[:len(h_lines) - nh - len(lp_h)] + (["  if (full) {"] + h_store + ["  }"] if nh else [])
+               + h_lines[len(h_lines) - len(lp_h):])
 
     dims = dict(N=nlp.N, NX=nlp.nx, NV=nlp.nv, NG=ng, NPS=nlp.nps, NPG=nlp.npg)
     ts = nlp.ts if ts is None else ts
@@ -138,6 +144,18 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     }
     nnz = {"jac": sum(1 for a, _ in gj_assign if a.startswith("jac")),
            "hess": sum(1 for a, _ in h_assign)}
+
+    # LDS budget per one-wave workgroup: 9.6 KB keeps 16 agents per CU; a problem
+    # where not even two stage systems fit gets up to 40 KB (4 agents per CU) so
+    # its stages are factorised in one or two rounds (mirrors SLOT_BYTES /
+    # OTHER_BYTES in csrc/mpcx_ipm.hip)
+    N_, NX_, NI_ = nlp.N, nlp.nx, nv + ng
+    nxp = max(NX_, 1)
+    pks = ((NI_ + 2 * NX_ + 1) * (NI_ + 2 * NX_ + 2) // 2) | 1
+    slot = 8 * pks + 8 * NI_
+    other = 8 * (N_ * 4 * nxp * nxp + 3 * N_ * nxp + 3 * nxp * nxp + 64 + nlp.npg + N_ * nlp.nps + N_) + 8 * nxp + 64
+    need = other + N_ * slot
+    lds_target = 9600 if other + 2 * slot <= 9600 else min(need, 40960)
 
     sig = "const double* __restrict__ L, const double* __restrict__ PS, const double* __restrict__ PG, const double TK"
     out: List[str] = [
@@ -150,6 +168,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         f"#define MPCX_NPG {nlp.npg}",
         f"#define MPCX_TS {float(ts)!r}",
         f"#define MPCX_ABI {KERNEL_ABI_VERSION}",
+        f"#define MPCX_LDS_TARGET {lds_target}",
         "#include <hip/hip_runtime.h>",
         "#include <math.h>",
         "",
@@ -159,7 +178,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         *bd_lines, "}", "",
         f"__device__ __forceinline__ void gen_stage_gj({sig}, double* __restrict__ grad, double* __restrict__ jac, const int S, const double* __restrict__ G, double* __restrict__ lp) {{",
         *gj_lines, "}", "",
-        f"__device__ __forceinline__ void gen_stage_hess({sig}, const double sigma, const double* __restrict__ lam, double* __restrict__ hess, const int S, double* __restrict__ lp) {{",
+        f"__device__ __forceinline__ void gen_stage_hess({sig}, const double sigma, const double* __restrict__ lam, double* __restrict__ hess, const int S, double* __restrict__ lp, const int full) {{",
         *h_lines, "}", "",
         '#include "mpcx_ipm.hip"',
         "",

@@ -68,7 +68,8 @@ class Options(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")] + \
                [(n, ctypes.c_int32) for n in ("iter_count", "status", "n_inertia_corrections",
-                                              "n_linesearch_fallbacks", "n_factorizations", "n_trials")]
+                                              "n_linesearch_fallbacks", "n_factorizations", "n_trials",
+                                              "n_block_chain", "reserved")]
 
 
 STATS_BYTES = ctypes.sizeof(Stats)
@@ -275,5 +276,6 @@ def stats_to_dicts(raw_bytes) -> list:
             "n_linesearch_fallbacks": s.n_linesearch_fallbacks,
             "n_factorizations": s.n_factorizations,
             "n_trials": s.n_trials,
+            "n_block_chain": s.n_block_chain,
         })
     return out

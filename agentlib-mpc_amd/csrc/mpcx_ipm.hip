@@ -246,6 +246,9 @@ struct Lds {
   int cperm[NXP];
   int cpiv[NXP];
   int seq;                 // 1: last factorisation used the block chain
+  int want_sdh;            // 1: keep the strided stage Hessians (block chain in use)
+  int sdh_ok;              // 1: the workspace Hessians match the last eval_hess
+  double hsig;             // sigma of the last eval_hess
   double fth[MAXF];
   double fph[MAXF];
 #ifdef MPCX_PROFILE
@@ -352,16 +355,20 @@ __device__ __noinline__ void eval_gj_lds(const Agent a) {
                  (double*)a.lp(k));
 }
 
-// Hessian of sigma*f + sum lam_i * gs_i * g_i (scaled Lagrangian)
-__device__ __noinline__ void eval_hess(const Agent a, double sigma) {
+// Hessian of sigma*f + sum lam_i * gs_i * g_i (scaled Lagrangian) into the packed
+// stage systems; the strided full Hessians (read only by the block-chain fallback)
+// are written when that path is in use, or on demand (eval_hess_full)
+__device__ __noinline__ void eval_hess_impl(const Agent a, double sigma, int full) {
   for (int k = a.lane; k < N; k += WAVE) {
     double lk[NG > 0 ? NG : 1];
 #pragma unroll
     for (int r = 0; r < NG; ++r) lk[r] = a.lam()[k * NG + r] * a.gs()[k * NG + r];
     gen_stage_hess((const double*)(a.x() + k * NP), par_stage(k), par_global(), k * TS, sigma, lk,
-                   (double*)(a.sdh() + k), N, (double*)a.lp(k));
+                   (double*)(a.sdh() + k), N, (double*)a.lp(k), full);
   }
+  if (a.lane == 0) { gL.hsig = sigma; gL.sdh_ok = full; }
 }
+__device__ __forceinline__ void eval_hess(const Agent a, double sigma) { eval_hess_impl(a, sigma, gL.want_sdh); }
 
 // gradient of the (unscaled) objective w.r.t. w[i], i >= NX (stage derivatives of
 // stage b and, for a state, the X0 part of stage b+1)
@@ -1244,7 +1251,12 @@ __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     SPROF(1);
     if constexpr (NX > 0) {
       if (wsumi(g == 0 ? bad : 0) > 0) {  // singular stage interior: block chain instead
-        if (lane == 0) L.seq = 1;
+        sync();
+        if (!L.sdh_ok && kd.mode != LSQ) {  // the chain reads the strided Hessians
+          eval_hess_impl(a, L.hsig, 1);
+          sync();
+        }
+        if (lane == 0) { L.seq = 1; L.want_sdh = 1; }
         sync();
         return seq_factor(a, kd);
       }
@@ -1888,11 +1900,12 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   if (lane < 6) gL.sprof[lane] = 0.0;
   sync();
 #endif
+  if (lane == 0) { gL.want_sdh = 0; gL.sdh_ok = 0; gL.hsig = 1.0; gL.seq = 0; }
   const Scal sc = init_agent(a, args, agent);
   PROF(0);
   const double obj_scale = sc.obj_scale;
   double fx = sc.fx;
-  int n_fact = 0, n_ic = 0, n_fallback = 0, n_trials = 0;
+  int n_fact = 0, n_ic = 0, n_fallback = 0, n_trials = 0, n_chain = 0;
   if (M > 0 && o.constr_mult_init_max > 0.0) {
     ls_multipliers(a, o.constr_mult_init_max, obj_scale);
     n_fact++;
@@ -1944,6 +1957,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
       KKTDiag kd{dw, dc, NEWTON};
       const Inertia in = factor(a, kd);
       n_fact++;
+      n_chain += gL.seq;
       if (in.pos == N * NP && in.neg == M && in.zero == 0) {
         if (attempt > 0) dw_last = dw;
         ok = true;
@@ -2023,6 +2037,8 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     st.n_linesearch_fallbacks = n_fallback;
     st.n_factorizations = n_fact;
     st.n_trials = n_trials;
+    st.n_block_chain = n_chain;
+    st.reserved = 0;
     args.stats[agent] = st;
   }
 }

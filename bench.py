@@ -209,6 +209,9 @@ def nn_bench(args, world, rank, dev):
         "kernel_nlp": {"nw": prob.nlp.kernel_nw, "ng": prob.nlp.kernel_ng, "np": prob.nlp.kernel_np},
         "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
         "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
+        "mean_factorizations": float(np.mean([s["n_factorizations"] for s in stats])),
+        "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
+                                      max(1, np.sum([s["n_factorizations"] for s in stats]))),
         "kernel_ms": ev0.elapsed_time(ev1) / args.steps,
     }
 

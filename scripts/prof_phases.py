@@ -19,22 +19,47 @@ def main():
     from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
     from agentlib_mpc_amd.runtime.native import NativeProblem
     import bench
-    be, cv = bm.one_room(solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
+    model = os.environ.get("MODEL", "one_room")
+    be, cv = bm.BUILDERS[model](solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
     path = build_profile_hsaco(be.problem.gen)
     if len(sys.argv) > 1 and sys.argv[1] == "build":
         print(path); return
     import torch
     n = int(os.environ.get("AGENTS", "4096"))
-    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261017))
+    if model == "one_room":
+        vals = bench.fleet_values(n, 20261017)
+    else:
+        first = next(k for q in be.problem.system.parameters for k in q.ref_names if k in cv)
+        vals = {first: np.full(n, cv[first].value, float)}
+    p, lbw, ubw, w0 = be.problem.to_kernel(*fleet_nlp_inputs(be.problem, cv, vals))
     nat = NativeProblem(be.problem.gen, hsaco=path)
     nat.set_options(tol=1e-8, max_iter=500)
+    nat.reserve(n)
     d = torch.device("cuda")
     T = lambda a: torch.as_tensor(a, device=d).contiguous()
     tp, tl, tu, tw = T(p), T(lbw), T(ubw), T(w0)
     lw = torch.zeros_like(tw)
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts, NativeProblem as NP
+    st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=d)
+    tw0 = T(w0)
     for _ in range(2):
-        tw.copy_(T(w0)); nat.solve(tp, tl, tu, tw, lam_w=lw)
+        tw.copy_(tw0); nat.solve(tp, tl, tu, tw, lam_w=lw, stats=st)
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(); tw.copy_(tw0); nat.solve(tp, tl, tu, tw, lam_w=lw, stats=st); e1.record()
+    torch.cuda.synchronize()
+    stats = stats_to_dicts(st.cpu().numpy().tobytes())
+    print("profile build: kernel ms", e0.elapsed_time(e1), "mean iters", np.mean([x["iter_count"] for x in stats]),
+          "mean fact", np.mean([x["n_factorizations"] for x in stats]))
+    plain = NP(be.problem.gen)
+    plain.set_options(tol=1e-8, max_iter=500)
+    plain.reserve(n)
+    for _ in range(2):
+        tw.copy_(tw0); plain.solve(tp, tl, tu, tw, stats=st)
+    torch.cuda.synchronize()
+    e0.record(); tw.copy_(tw0); plain.solve(tp, tl, tu, tw, stats=st); e1.record()
+    torch.cuda.synchronize()
+    print("plain build: kernel ms", e0.elapsed_time(e1))
     prof = lw[:, :16].cpu().numpy()
     names = ["init", "ls_mult", "opt_err+mu", "hess", "rhs_x", "factor", "solve", "recover", "linesearch", "accept+gj",
              "f:assemble", "f:interior_bk", "f:schur+store", "f:chain", "s:forward", "s:chain+back"]

@@ -49,6 +49,9 @@ def _cuda():
     ("room_nn", {}),
     ("room_nn", {"T_air": 296.5, "load": 180.0, "Q_rad": 150.0, "q_T": 1.0,
                  "zbar": [296.0, 293.0, 295.0, 296.0], "lam": [0.5, -0.2, 0.1, 0.0]}),
+    # N=23 has no super-stage length dividing it: copy-lifted stages whose interiors
+    # are singular, i.e. the sequential block-chain fallback of the kernel
+    ("room_nn", {"N": 23}),
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)
@@ -67,6 +70,13 @@ def test_gpu_matches_oracle(name, kw):
             got = case.backend.problem.outputs(_w_of(case, r))[gname]
             want = ref.x[lay.index]
             np.testing.assert_allclose(got, want, rtol=RTOL_TRAJ, atol=1e-7 * max(1.0, np.abs(want).max()))
+
+
+def test_copy_lifted_narx_uses_block_chain():
+    case = configs.room_nn(N=23)
+    assert case.backend.problem.nlp.lift.w_dup.any()
+    r = case.backend.solve(0.0, case.current_vars)
+    assert r.stats["success"] and r.stats["n_block_chain"] > 0, r.stats
 
 
 def _w_of(case, results):

@@ -32,9 +32,9 @@ def test_library_builds_loads_and_exports_all_symbols():
 
 
 def test_struct_sizes_match_header():
-    # mpcx_options: 36 doubles + 4 int32; mpcx_stats: 6 doubles + 6 int32
+    # mpcx_options: 36 doubles + 4 int32; mpcx_stats: 6 doubles + 8 int32
     assert ctypes.sizeof(native.Options) == 36 * 8 + 4 * 4
-    assert ctypes.sizeof(native.Stats) == 6 * 8 + 6 * 4
+    assert ctypes.sizeof(native.Stats) == 6 * 8 + 8 * 4
     assert ctypes.sizeof(native.ProblemDesc) == 8 * 4
 
 

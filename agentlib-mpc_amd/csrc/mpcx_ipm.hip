@@ -196,6 +196,10 @@ constexpr int OTHER_BYTES = 8 * (N * 3 * NXX + N * NXX + 3 * N * NXP + 3 * NXX +
 #ifndef MPCX_LDS_TARGET
 #define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
 #endif
+#ifdef MPCX_LDS_TARGET_OVERRIDE  // diagnostics (scripts/variants.py)
+#undef MPCX_LDS_TARGET
+#define MPCX_LDS_TARGET MPCX_LDS_TARGET_OVERRIDE
+#endif
 constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / SLOT_BYTES));
 constexpr int ROUNDS = (N + SR0 - 1) / SR0;
 constexpr int SR = (N + ROUNDS - 1) / ROUNDS;   // stages per round (balanced)

@@ -209,6 +209,8 @@ def nn_bench(args, world, rank, dev):
         "kernel_nlp": {"nw": prob.nlp.kernel_nw, "ng": prob.nlp.kernel_ng, "np": prob.nlp.kernel_np},
         "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
         "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
+        "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
+        "statuses": sorted({int(s["status"]) for s in stats}),
         "mean_factorizations": float(np.mean([s["n_factorizations"] for s in stats])),
         "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
                                       max(1, np.sum([s["n_factorizations"] for s in stats]))),
@@ -328,6 +330,7 @@ def main():
                 "tol": args.tol,
                 "converged_fraction_rank0": n_ok / n,
                 "mean_ipm_iterations": float(arr["iter"].mean()),
+                "ipm_iterations_p50_p99_max": [float(np.percentile(arr["iter"], q)) for q in (50, 99, 100)],
                 "parallelism": f"agent-partitioned dp{world}",
             },
             "roofline": {

@@ -17,6 +17,8 @@ sys.path[:0] = [str(ROOT), str(ROOT / "agentlib-mpc_amd")]
 
 VARIANTS = {
     "base": ([], None),
+    "lds20k": (["-DMPCX_LDS_TARGET_OVERRIDE=20000"], None),
+    "lds14k": (["-DMPCX_LDS_TARGET_OVERRIDE=14000"], None),
     "w2": (["-DMPCX_MIN_WAVES=2"], None),
     "w1": (["-DMPCX_MIN_WAVES=1"], None),
     "inl_w2": (["-DMPCX_MIN_WAVES=2"], ("__noinline__", "__attribute__((always_inline))")),
@@ -32,7 +34,7 @@ def vdir():
 def build(names):
     from agentlib_mpc_amd import benchmarks as bm
     from agentlib_mpc_amd.runtime import native
-    be, _ = bm.one_room()
+    be, _ = bm.BUILDERS[os.environ.get("MODEL", "one_room")]()
     gen = be.problem.gen
     d = vdir()
     d.mkdir(parents=True, exist_ok=True)
@@ -65,9 +67,15 @@ def run(names):
     from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
     from agentlib_mpc_amd.runtime.native import NativeProblem, STATS_BYTES, stats_to_dicts
     import bench
-    be, cv = bm.one_room(solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
+    model = os.environ.get("MODEL", "one_room")
+    be, cv = bm.BUILDERS[model](solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
     n = int(os.environ.get("AGENTS", "4096"))
-    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261017))
+    if model == "one_room":
+        vals = bench.fleet_values(n, 20261017)
+    else:
+        first = next(k for q in be.problem.system.parameters for k in q.ref_names if k in cv)
+        vals = {first: np.full(n, cv[first].value, float)}
+    p, lbw, ubw, w0 = be.problem.to_kernel(*fleet_nlp_inputs(be.problem, cv, vals))
     dev = torch.device("cuda")
     T = lambda a: torch.as_tensor(a, device=dev).contiguous()
     tp, tl, tu, tw0 = T(p), T(lbw), T(ubw), T(w0)

@@ -83,11 +83,14 @@ class FleetClass:
                  initial: Optional[Dict[str, Union[float, Sequence[float]]]] = None):
         self.name = name
         self.backend = backend
-        p, lbw, ubw, w0 = (np.ascontiguousarray(a, dtype=np.float64) for a in inputs)
-        self.p0, self.lbw, self.ubw, self.w0 = p, lbw, ubw, w0
-        self.n = p.shape[0]
         prob = backend.problem
         nlp = prob.nlp
+        self.lift = nlp.lift
+        self.lbw_ref = np.ascontiguousarray(inputs[1], dtype=np.float64)
+        # device arrays are in the kernel's stage order (== reference order unless lifted)
+        p, lbw, ubw, w0 = (np.ascontiguousarray(a, dtype=np.float64) for a in prob.to_kernel(*inputs))
+        self.p0, self.lbw, self.ubw, self.w0 = p, lbw, ubw, w0
+        self.n = p.shape[0]
         sysm = backend.system
         aliases = aliases or {}
         initial = initial or {}
@@ -107,6 +110,10 @@ class FleetClass:
             if not (len(w_cols) == len(mean_cols) == len(mult_cols)):
                 raise ValueError(f"{name}: trajectory lengths differ (local {len(w_cols)}, mean "
                                  f"{len(mean_cols)}, multiplier {len(mult_cols)})")
+            if self.lift is not None:
+                w_cols = self.lift.w_primary[np.asarray(w_cols)]
+                mean_cols = [self._kernel_par(c) for c in mean_cols]
+                mult_cols = [self._kernel_par(c) for c in mult_cols]
             al = aliases.get(name, name)
             al = [al] * self.n if isinstance(al, str) else list(al)
             if len(al) != self.n:
@@ -117,11 +124,30 @@ class FleetClass:
         if not self.slots:
             raise ValueError(f"class {name}: backend has no couplings or exchange variables")
         self.rho_col = int(nlp.par_groups[sysm.penalty_factor.name].columns[0][0])
+        if self.lift is not None:
+            self.rho_col = self._kernel_par(self.rho_col)
         self.T = len(self.slots[0].w_cols)
         opts = backend.config.discretization_options
         self.horizon = int(opts.prediction_horizon)
         self.time_step = float(opts.time_step)
         self.coupling_grid = list(backend.coupling_grid)
+
+    def _kernel_par(self, ref_col: int) -> int:
+        """Kernel parameter column of a reference parameter that the stages read once."""
+        hits = np.flatnonzero(self.lift.p_src == ref_col)
+        if len(hits) != 1:
+            raise ValueError(f"parameter {ref_col} appears {len(hits)} times in the kernel NLP")
+        return int(hits[0])
+
+    def to_kernel(self, p=None, lbw=None, ubw=None):
+        """Reference-layout class inputs -> kernel layout (None passes through)."""
+        if self.lift is None:
+            return p, lbw, ubw
+        l = self.lift
+        kp = None if p is None else np.ascontiguousarray(np.asarray(p)[..., l.p_src])
+        klb = None if lbw is None else np.where(l.w_dup, -np.inf, np.asarray(lbw)[..., l.w_src])
+        kub = None if ubw is None else np.where(l.w_dup, np.inf, np.asarray(ubw)[..., l.w_src])
+        return kp, klb, kub
 
     @property
     def native(self):
@@ -246,7 +272,7 @@ class ADMMFleet:
             c.LB = t.as_tensor(c.lbw, device=dev).contiguous()
             c.UB = t.as_tensor(c.ubw, device=dev).contiguous()
             c.W = t.as_tensor(c.w0, device=dev).contiguous()
-            c.LAMG = t.zeros((c.n, c.backend.problem.nlp.ng_total), dtype=f64, device=dev)
+            c.LAMG = t.zeros((c.n, c.backend.problem.nlp.kernel_ng), dtype=f64, device=dev)
             c.ST = t.zeros(c.n * STATS_BYTES, dtype=t.uint8, device=dev)
             c.dev_slots = []
             for si, s in enumerate(c.slots):
@@ -268,8 +294,10 @@ class ADMMFleet:
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
-        """New measurements/forecasts for the next control step (host -> HBM)."""
+        """New measurements/forecasts for the next control step (host -> HBM);
+        reference-layout arrays."""
         c = next(c for c in self.classes if c.name == class_name)
+        p, lbw, ubw = c.to_kernel(p, lbw, ubw)
         c.P.copy_(self.torch.as_tensor(p))
         if lbw is not None:
             c.LB.copy_(self.torch.as_tensor(lbw))
@@ -405,8 +433,9 @@ class ADMMFleet:
 
     # ------------------------------------------------------------------ outputs
     def solutions(self, class_name: str) -> np.ndarray:
+        """Reference-layout NLP solution vectors [n, nw] of one class."""
         c = next(c for c in self.classes if c.name == class_name)
-        return c.W.cpu().numpy()
+        return c.backend.problem.from_kernel(c.W.cpu().numpy(), c.lbw_ref)
 
     def stats(self, class_name: str) -> list:
         from agentlib_mpc_amd.runtime.native import stats_to_dicts

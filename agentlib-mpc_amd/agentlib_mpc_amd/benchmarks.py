@@ -189,6 +189,65 @@ def room_nn(N=24, T_air=294.0, T_CCA=294.15, load=100.0, T_amb=299.0, Q_rad=50.0
     return be, cv
 
 
+TZ_AHU_COUPLINGS = ("T_ahu_out1", "T_room1", "T_ahu_out2", "T_room2", "T_ahu_out3", "T_room3")
+TZ_CCA_COUPLINGS = ("T_v_out", "T_r1", "T_v_out2", "T_r2", "T_v_out3", "T_r3")
+
+
+def tz_ahu(N=24, rho=1.0, zbar=295.0, lam=0.0, mDot_0=0.025, T_amb=299.0, r_T_v=1.0,
+           solver_options=TIGHT):
+    """C5 air handling unit: `three_zone_datadriven_admm/configs/mpc/ahu_controller.json`
+    (casadi_admm, multiple shooting, N=24, ts=1800; controls T_ahu1..3 in [285, 308],
+    outputs W1..3 in [-500, 500]).  ``zbar``/``lam``: scalar or [6][N] per coupling."""
+    be = create_optimization_backend({
+        "type": "mi355x_admm",
+        "model": {"type": "agentlib_mpc_amd.models.examples.ThreeZoneAHU"},
+        "discretization_options": {"method": "multiple_shooting", "prediction_horizon": N, "time_step": 1800},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    coups = [adt.CouplingEntry(n) for n in TZ_AHU_COUPLINGS]
+    be.setup_optimization(adt.VariableReference(
+        states=[], controls=["T_ahu1", "T_ahu2", "T_ahu3"], inputs=["mDot_0", "T_amb"],
+        parameters=["r_T_v"], outputs=["W1", "W2", "W3"], couplings=coups))
+    n = len(be.coupling_grid)
+    cv = {f"T_ahu{i}": V(f"T_ahu{i}", 295.0, 285.0, 308.0) for i in (1, 2, 3)}
+    cv.update({f"W{i}": V(f"W{i}", 0.0, -500.0, 500.0) for i in (1, 2, 3)})
+    cv.update({"mDot_0": V("mDot_0", mDot_0), "T_amb": V("T_amb", T_amb), "r_T_v": V("r_T_v", r_T_v),
+               "penalty_factor": V("penalty_factor", rho)})
+    zb = np.broadcast_to(np.asarray(zbar, float).reshape(-1, 1) if np.ndim(zbar) == 1 else zbar, (6, n))
+    lm = np.broadcast_to(np.asarray(lam, float).reshape(-1, 1) if np.ndim(lam) == 1 else lam, (6, n))
+    for i, c in enumerate(coups):
+        cv[c.name] = V(c.name, 295.0)
+        cv[c.mean] = V(c.mean, list(zb[i]))
+        cv[c.multiplier] = V(c.multiplier, list(lm[i]))
+    return be, cv
+
+
+def tz_cca(N=24, rho=1.0, zbar=294.15, lam=0.0, mDot_0=0.1, r_T_v=1.0, solver_options=TIGHT):
+    """C5 concrete-core supply: `three_zone_datadriven_admm/configs/mpc/cca_controller.json`
+    (control T_v in [285, 308], outputs W1..3 in [-1e5, 1e5])."""
+    be = create_optimization_backend({
+        "type": "mi355x_admm",
+        "model": {"type": "agentlib_mpc_amd.models.examples.TempController"},
+        "discretization_options": {"method": "multiple_shooting", "prediction_horizon": N, "time_step": 1800},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    coups = [adt.CouplingEntry(n) for n in TZ_CCA_COUPLINGS]
+    be.setup_optimization(adt.VariableReference(
+        states=[], controls=["T_v"], inputs=["mDot_0"], parameters=["r_T_v"],
+        outputs=["W1", "W2", "W3"], couplings=coups))
+    n = len(be.coupling_grid)
+    cv = {"T_v": V("T_v", 294.15, 285.0, 308.0), "mDot_0": V("mDot_0", mDot_0), "r_T_v": V("r_T_v", r_T_v),
+          "penalty_factor": V("penalty_factor", rho)}
+    cv.update({f"W{i}": V(f"W{i}", 0.0, -1e5, 1e5) for i in (1, 2, 3)})
+    zb = np.broadcast_to(np.asarray(zbar, float).reshape(-1, 1) if np.ndim(zbar) == 1 else zbar, (6, n))
+    lm = np.broadcast_to(np.asarray(lam, float).reshape(-1, 1) if np.ndim(lam) == 1 else lam, (6, n))
+    for i, c in enumerate(coups):
+        cv[c.name] = V(c.name, 294.15)
+        cv[c.mean] = V(c.mean, list(zb[i]))
+        cv[c.multiplier] = V(c.multiplier, list(lm[i]))
+    return be, cv
+
+
 BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -196,6 +255,8 @@ BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
     "exchange_room": exchange_room,
     "exchange_supply": exchange_supply,
     "room_nn": room_nn,
+    "tz_ahu": tz_ahu,
+    "tz_cca": tz_cca,
 }
 
 
@@ -212,6 +273,9 @@ def compile_all(verbose: bool = False):
     # the benchmark structures plus the test-only variants (copy-lifted NARX, N=23)
     variants = dict(BUILDERS)
     variants["room_nn_n23"] = lambda: room_nn(N=23)
+    variants["room_nn_n8"] = lambda: room_nn(N=8)      # C5 ADMM fixture (tests/golden/c5_admm_N8.json)
+    variants["tz_ahu_n8"] = lambda: tz_ahu(N=8)
+    variants["tz_cca_n8"] = lambda: tz_cca(N=8)
     for name, fn in variants.items():
         be, _ = fn()
         paths[name] = be.problem.compile()
@@ -288,3 +352,49 @@ def c4_fleet_classes(n_rooms=4, n_supply=1, N=10, rho=1e4, seed=None, solver_opt
         classes.append(FleetClass("supply", be_s, _class_inputs(be_s, cv_s, {}, n_supply),
                                   aliases={"mDot_out": "mDot_coupling"}, initial={"mDot_out": 0.02}))
     return classes
+
+
+def c5_fleet_classes(n_blocks=1, N=24, rho=1.0, seed=None, block_offset=0, solver_options=TIGHT):
+    """Coordinated consensus fleet of `examples/three_zone_datadriven_admm`:
+    ``n_blocks`` x (3 NARX zones + 1 AHU + 1 CCA supply).  Couplings per zone i
+    of block b (`configs/mpc/Room_{i}.json`, `ahu_controller.json`,
+    `cca_controller.json`): T_v <-> CCA T_v_out{i} (alias T_coupling{i}), T_ahu <->
+    AHU T_ahu_out{i} (T_coupling_ahu{i}), T_CCA_out <-> CCA T_r{i} (T_rucklauf{i}),
+    T_air_out <-> AHU T_room{i} (T_airin{i}).  Block 0 = the example's values;
+    further blocks draw T_air~U(292,297), d~U(50,200), T_amb~U(295,303),
+    Q_rad~U(0,200) from ``default_rng([seed, block])``."""
+    from agentlib_mpc_amd.admm.fleet import FleetClass
+
+    blocks = list(range(block_offset, block_offset + n_blocks))
+    vals = {"T_air": [], "d": [], "T_amb": [], "Q_rad": []}
+    for b in blocks:
+        rng = np.random.default_rng([seed, b]) if seed is not None else None
+        for _ in range(3):
+            if b == 0 or rng is None:
+                vals["T_air"].append(294.0); vals["d"].append(100.0)
+                vals["T_amb"].append(299.0); vals["Q_rad"].append(50.0)
+            else:
+                vals["T_air"].append(rng.uniform(292.0, 297.0)); vals["d"].append(rng.uniform(50.0, 200.0))
+                vals["T_amb"].append(rng.uniform(295.0, 303.0)); vals["Q_rad"].append(rng.uniform(0.0, 200.0))
+    be_r, cv_r = room_nn(N=N, rho=rho, solver_options=solver_options)
+    nz = 3 * n_blocks
+    zone_alias = lambda pre: [f"{pre}{i + 1}_b{b}" for b in blocks for i in range(3)]  # noqa: E731
+    rooms = FleetClass("zone", be_r, _class_inputs(be_r, cv_r, vals, nz),
+                       aliases={"T_v": zone_alias("T_coupling"), "T_ahu": zone_alias("T_coupling_ahu"),
+                                "T_CCA_out": zone_alias("T_rucklauf"), "T_air_out": zone_alias("T_airin")},
+                       initial={"T_v": 294.15, "T_ahu": 295.0, "T_CCA_out": 294.15, "T_air_out": 294.0})
+    be_a, cv_a = tz_ahu(N=N, rho=rho, solver_options=solver_options)
+    ahu_al = {}
+    for i in range(3):
+        ahu_al[f"T_ahu_out{i + 1}"] = [f"T_coupling_ahu{i + 1}_b{b}" for b in blocks]
+        ahu_al[f"T_room{i + 1}"] = [f"T_airin{i + 1}_b{b}" for b in blocks]
+    ahu = FleetClass("ahu", be_a, _class_inputs(be_a, cv_a, {}, n_blocks), aliases=ahu_al,
+                     initial={k: 295.0 for k in ahu_al})
+    be_c, cv_c = tz_cca(N=N, rho=rho, solver_options=solver_options)
+    cca_al = {}
+    for i, (vo, tr) in enumerate((("T_v_out", "T_r1"), ("T_v_out2", "T_r2"), ("T_v_out3", "T_r3"))):
+        cca_al[vo] = [f"T_coupling{i + 1}_b{b}" for b in blocks]
+        cca_al[tr] = [f"T_rucklauf{i + 1}_b{b}" for b in blocks]
+    cca = FleetClass("cca", be_c, _class_inputs(be_c, cv_c, {}, n_blocks), aliases=cca_al,
+                     initial={k: 294.15 for k in cca_al})
+    return [rooms, ahu, cca]

@@ -233,3 +233,72 @@ def synthetic_ann(features: dict, seed: int, hidden: int = 32, dt: float = 1800.
 def room_cca_anns(seed: int = 20261015 + 5):
     """The two shared networks of the C5 zones (T_air and T_CCA_0)."""
     return [synthetic_ann(T_AIR_FEATURES, seed), synthetic_ann(T_CCA_FEATURES, seed + 1)]
+
+
+class ThreeZoneAHUConfig(CasadiModelConfig):
+    """`examples/three_zone_datadriven_admm/models/AHU.py:4-75` (air handling unit of 3 zones)."""
+
+    inputs: List[CasadiInput] = [
+        _inp("mDot_0", 0.025), _inp("T_amb", 295, unit="K"),
+        _inp("T_ahu1", 294, unit="K"), _inp("T_ahu2", 294, unit="K"), _inp("T_ahu3", 294, unit="K"),
+        _inp("T_room1", 299, unit="K"), _inp("T_room2", 299, unit="K"), _inp("T_room3", 299, unit="K"),
+    ]
+    states: List[CasadiState] = []
+    parameters: List[CasadiParameter] = [_par("r_T_v", 1), _par("cl", 1000, unit="J/kg*K")]
+    outputs: List[CasadiOutput] = [
+        CasadiOutput(name="T_ahu_out1", value=293), CasadiOutput(name="T_ahu_out2", value=293),
+        CasadiOutput(name="T_ahu_out3", value=293),
+        CasadiOutput(name="W1", value=200), CasadiOutput(name="W2", value=200), CasadiOutput(name="W3", value=200),
+    ]
+
+
+class ThreeZoneAHU(CasadiModel):
+    """`AHU.py:78-130`: supply temperatures of three zones, smoothed |power| cost."""
+
+    config: ThreeZoneAHUConfig
+
+    def setup_system(self):
+        zones = ((self.T_ahu1, self.T_room1, self.T_ahu_out1, self.W1),
+                 (self.T_ahu2, self.T_room2, self.T_ahu_out2, self.W2),
+                 (self.T_ahu3, self.T_room3, self.T_ahu_out3, self.W3))
+        terms = []
+        for t_ahu, t_room, out, w in zones:
+            out.alg = 1 * t_ahu
+            w.alg = self.cl * self.mDot_0 * (t_ahu - (t_room + self.T_amb) / 2)
+            terms.append(0.1 * 0.001 * self.r_T_v
+                         * ((self.cl * self.mDot_0 * (t_ahu - (t_room + self.T_amb) / 2)) ** 2 + 0.02) ** 0.5)
+        self.constraints = []
+        return sum(terms)
+
+
+class TempControllerConfig(CasadiModelConfig):
+    """`examples/three_zone_datadriven_admm/models/CCA.py:4-50` (concrete core activation supply)."""
+
+    inputs: List[CasadiInput] = [
+        _inp("mDot_0", 0.1), _inp("T_v", 294, unit="K"),
+        _inp("T_r1", 296), _inp("T_r2", 296), _inp("T_r3", 296),
+    ]
+    states: List[CasadiState] = []
+    parameters: List[CasadiParameter] = [_par("r_T_v", 1), _par("cp", 4200, unit="J/kg*K")]
+    outputs: List[CasadiOutput] = [
+        CasadiOutput(name="T_v_out", value=293), CasadiOutput(name="T_v_out2", value=293),
+        CasadiOutput(name="T_v_out3", value=293),
+        CasadiOutput(name="W1", value=200), CasadiOutput(name="W2", value=200), CasadiOutput(name="W3", value=200),
+    ]
+
+
+class TempController(CasadiModel):
+    """`CCA.py:53-88`: one supply temperature for three zones."""
+
+    config: TempControllerConfig
+
+    def setup_system(self):
+        self.T_v_out.alg = 1 * self.T_v
+        self.T_v_out2.alg = 1 * self.T_v
+        self.T_v_out3.alg = 1 * self.T_v
+        self.W1.alg = self.cp * self.mDot_0 * (self.T_v - self.T_r1)
+        self.W2.alg = self.cp * self.mDot_0 * (self.T_v - self.T_r2)
+        self.W3.alg = self.cp * self.mDot_0 * (self.T_v - self.T_r3)
+        self.constraints = []
+        return sum(0.1 * 0.001 * self.r_T_v * ((self.cp * self.mDot_0 * (self.T_v - t_r)) ** 2 + 0.02) ** 0.5
+                   for t_r in (self.T_r1, self.T_r2, self.T_r3))

@@ -533,13 +533,18 @@ def _euler(ode: List[sx.Expr], x: List[sx.Expr], ts: float) -> List[sx.Expr]:
 class BasicMultipleShooting(Discretization):
     """`casadi_/basic.py:395-448` (backend ``casadi_basic``, multiple shooting)."""
 
-    def _check_integrator(self):
+    def _check_integrator(self, system=None):
+        """Only Euler is implemented; without differential states (e.g. the
+        three-zone AHU/CCA controllers, which keep the cvodes default) the
+        integrator is never used."""
+        if system is not None and system.states.dim == 0:
+            return
         if self.options.integrator != Integrators.euler:
             raise TranscriptionError(
                 f"integrator '{self.options.integrator.value}' is not supported on MI355X yet; use 'euler'")
 
     def _discretize(self, t, s):
-        self._check_integrator()
+        self._check_integrator(s)
         n, ts = self.options.prediction_horizon, self.options.time_step
         x0 = t.add_opt_par(s.initial_state)
         xk = t.add_opt_var(s.states, lb=x0, ub=x0, guess=x0)
@@ -568,7 +573,7 @@ class FullMultipleShooting(BasicMultipleShooting):
     system_type = FullSystem
 
     def _discretize(self, t, s):
-        self._check_integrator()
+        self._check_integrator(s)
         n, ts = self.options.prediction_horizon, self.options.time_step
         x0 = t.add_opt_par(s.initial_state)
         xk = t.add_opt_var(s.states, lb=x0, ub=x0, guess=x0)
@@ -605,7 +610,7 @@ class ADMMMultipleShooting(BasicMultipleShooting):
     system_type = ADMMSystem
 
     def _discretize(self, t, s):
-        self._check_integrator()
+        self._check_integrator(s)
         n, ts = self.options.prediction_horizon, self.options.time_step
         x0 = t.add_opt_par(s.initial_state)
         xk = t.add_opt_var(s.states, lb=x0, ub=x0, guess=x0)

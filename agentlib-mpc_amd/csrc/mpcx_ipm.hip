@@ -1990,6 +1990,9 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
                                     theta_max, nfilt);
     n_trials += ls.trials;
     bool ftype = ls.ftype;
+    // no acceptable trial and the last one is not even finite: IPOPT would enter its
+    // restoration phase; stop with Restoration_Failed at the current (finite) iterate
+    if (!ls.accepted && !(isfin(ls.tr.theta) && isfin(ls.tr.phi))) { status = MPCX_RESTORATION_FAILED; break; }
     if (!ls.accepted) { nfilt = 0; ftype = true; n_fallback++; }
     if (!ftype) {
       if (nfilt == MAXF) {

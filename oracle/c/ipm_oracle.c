@@ -676,7 +676,7 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
     else if (gphid < 0) amin = 0.05 * fmin(1e-5, 1e-8 * theta / -gphid);
     else amin = 0.05 * 1e-5;
     if (!(amin > 0)) amin = 0.05 * 1e-5;
-    double alpha = amax, ft = 0.0;
+    double alpha = amax, ft = 0.0, last_th = 0.0, last_ph = 0.0;
     int accepted = 0, ftype = 0;
     for (int ls = 0; ls < 64; ++ls) {
       for (int i = 0; i < NW; ++i) w->xt[i] = w->x[i] + alpha * w->dx[i];
@@ -685,6 +685,7 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
       n_trials++;
       for (int c = 0; c < M; ++c) w->gt[c] *= w->gs[c];
       const double tht = theta_of(w, w->gt, w->st), pht = ft - mu * barrier_of(w, w->xt, w->st);
+      last_th = tht; last_ph = pht;
       int okt = tht <= theta_max && pht == pht;
       for (int j = 0; j < nfilt && okt; ++j) if (tht >= fth[j] && pht >= fph[j]) okt = 0;
       if (okt) {
@@ -696,6 +697,9 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
       alpha *= 0.5;
       if (alpha < amin) break;
     }
+    /* no acceptable trial and the last one is not even finite: IPOPT would enter
+       restoration; stop with Restoration_Failed at the current (finite) iterate */
+    if (!accepted && !(isfin(last_th) && isfin(last_ph))) { status = -2; break; }
     if (!accepted) { nfilt = 0; ftype = 1; }
     if (!ftype) {
       if (nfilt == 32) { for (int j = 1; j < 32; ++j) { fth[j - 1] = fth[j]; fph[j - 1] = fph[j]; } nfilt--; }

@@ -402,6 +402,11 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
             alpha *= 0.5
             if alpha < a_min:
                 break
+        if not accepted and not (np.isfinite(th_t) and np.isfinite(ph_t)):
+            # no acceptable trial and the last one is not even finite: IPOPT would enter
+            # its restoration phase; stop with Restoration_Failed at the current iterate
+            status = "Restoration_Failed"
+            break
         if not accepted:
             # fallback instead of IPOPT's restoration phase: take the last trial
             filt = []

@@ -610,3 +610,97 @@ def ann_layers_from_serialized(layer_specs):
             act = spec["config"].get("activation", "linear")
             out.append(("sigmoid" if act == "sigmoid" else "linear", (w[0], w[1])))
     return out
+
+
+# ---------------------------------------------------------------------------
+# C5: three-zone AHU and CCA supply controllers, backend "casadi_admm",
+# multiple shooting without states (`casadi_/admm.py:198-310`)
+# ---------------------------------------------------------------------------
+
+def _tz_supply(kind: str, N=24, ts=1800.0) -> OracleProblem:
+    """``kind`` "ahu" (`models/AHU.py`): u = T_ahu1..3, couplings (T_ahu_out_i, T_room_i);
+    "cca" (`models/CCA.py`): u = T_v, couplings (T_v_out(i), T_r_i).
+    Per step w = [u, W1..3, c1..c6]; g = [outputs' equations (3 supply temperatures, W1..3)];
+    p = [u_prev, (r_T_v, c) x 2, rho, {d, zbar(6), lam(6)} x N] with c = cl (AHU) / cp (CCA),
+    d = (mDot_0, T_amb) (AHU) / (mDot_0) (CCA)."""
+    nu = 3 if kind == "ahu" else 1
+    nd = 2 if kind == "ahu" else 1
+    nb = nu + 3 + 6
+    n, m = N * nb, N * 6
+    npg = nu + 4 + 1
+    nps = nd + 12
+    npar = npg + N * nps
+    cn = ("T_ahu_out1", "T_room1", "T_ahu_out2", "T_room2", "T_ahu_out3", "T_room3") if kind == "ahu" else \
+        ("T_v_out", "T_r1", "T_v_out2", "T_r2", "T_v_out3", "T_r3")
+    un = ["T_ahu1", "T_ahu2", "T_ahu3"] if kind == "ahu" else ["T_v"]
+    names = []
+    for k in range(N):
+        names += [f"{u}@{k}" for u in un] + [f"W{i}@{k}" for i in (1, 2, 3)] + [f"{c}@{k}" for c in cn]
+
+    def stage(w, p, k):
+        r_T_v, c, rho = p[nu + 2], p[nu + 3], p[nu + 4]
+        o = k * nb
+        u, W, cp_ = w[o:o + nu], w[o + nu:o + nu + 3], w[o + nu + 3:o + nb]
+        b = npg + k * nps
+        d = p[b:b + nd]
+        zbar, lam = p[b + nd:b + nd + 6], p[b + nd + 6:b + nd + 12]
+        mDot = d[0]
+        cost = 0.0
+        sup, alg = [], []
+        for i in range(3):
+            if kind == "ahu":
+                t_sup, t_room = u[i], cp_[2 * i + 1]
+                pw = c * mDot * (t_sup - (t_room + d[1]) / 2)
+            else:
+                t_sup, t_r = u[0], cp_[2 * i + 1]
+                pw = c * mDot * (t_sup - t_r)
+            cost = cost + 0.1 * 0.001 * r_T_v * (pw ** 2 + 0.02) ** 0.5
+            sup.append(cp_[2 * i] - 1 * t_sup)
+            alg.append(W[i] - pw)
+        for i in range(6):
+            cost = cost + lam[i] * cp_[i] + rho / 2 * (zbar[i] - cp_[i]) ** 2
+        return ts * cost, torch.stack(sup + alg)
+
+    def f(w, p):
+        return sum(stage(w, p, k)[0] for k in range(N))
+
+    def g(w, p):
+        return torch.cat([stage(w, p, k)[1] for k in range(N)])
+
+    return OracleProblem(f"tz_{kind}", n, m, npar, f, g, lambda p: np.zeros(m), lambda p: np.zeros(m), names)
+
+
+def tz_ahu(N=24) -> OracleProblem:
+    return _tz_supply("ahu", N)
+
+
+def tz_cca(N=24) -> OracleProblem:
+    return _tz_supply("cca", N)
+
+
+def tz_supply_inputs(prob, N=24, rho=1.0, zbar=None, lam=None, mDot_0=None, T_amb=299.0, r_T_v=1.0):
+    """Cold-start inputs (`core/discretization.py:212-245`) of ``tz_ahu`` / ``tz_cca``."""
+    ahu = prob.name == "tz_ahu"
+    nu = 3 if ahu else 1
+    mDot_0 = (0.025 if ahu else 0.1) if mDot_0 is None else mDot_0
+    c = 1000.0 if ahu else 4200.0
+    init = 295.0 if ahu else 294.15
+    zbar = np.full((6, N), init) if zbar is None else np.broadcast_to(np.asarray(zbar, float).reshape(6, -1), (6, N))
+    lam = np.zeros((6, N)) if lam is None else np.broadcast_to(np.asarray(lam, float).reshape(6, -1), (6, N))
+    u0 = 295.0 if ahu else 294.15
+    p = [u0] * nu + [r_T_v, c, r_T_v, c, rho]
+    d = [mDot_0, T_amb] if ahu else [mDot_0]
+    for k in range(N):
+        p += d + list(zbar[:, k]) + list(lam[:, k])
+    p = np.array(p, float)
+    wlim = 500.0 if ahu else 1e5
+    lbw, ubw, w0 = np.zeros(prob.n), np.zeros(prob.n), np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        v = name.split("@")[0]
+        if v.startswith("T_ahu") and not v.startswith("T_ahu_out") or v == "T_v":
+            lbw[i], ubw[i], w0[i] = 285.0, 308.0, 296.5
+        elif v.startswith("W"):
+            lbw[i], ubw[i], w0[i] = -wlim, wlim, 0.0
+        else:
+            lbw[i], ubw[i], w0[i] = -np.inf, np.inf, 0.0
+    return p, lbw, ubw, w0

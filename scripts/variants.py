@@ -19,6 +19,9 @@ VARIANTS = {
     "base": ([], None),
     "lds20k": (["-DMPCX_LDS_TARGET_OVERRIDE=20000"], None),
     "lds14k": (["-DMPCX_LDS_TARGET_OVERRIDE=14000"], None),
+    "lds24k_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=24000", "-DMPCX_MIN_WAVES=2"], None),
+    "lds14k_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=14000", "-DMPCX_MIN_WAVES=2"], None),
+    "lds24k": (["-DMPCX_LDS_TARGET_OVERRIDE=24000"], None),
     "w2": (["-DMPCX_MIN_WAVES=2"], None),
     "w1": (["-DMPCX_MIN_WAVES=1"], None),
     "inl_w2": (["-DMPCX_MIN_WAVES=2"], ("__noinline__", "__attribute__((always_inline))")),

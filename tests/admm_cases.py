@@ -15,6 +15,8 @@ from oracle import ipm, nlps
 
 
 class _Solver:
+    tol = 1e-10
+
     def __init__(self):
         self.last = {}
 
@@ -25,7 +27,7 @@ class _Solver:
             fixed = lbw == ubw
             w0[fixed] = lbw[fixed]
         r = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p),
-                      ipm.IPMOptions(tol=1e-10, max_iter=500))
+                      ipm.IPMOptions(tol=self.tol, max_iter=500))
         assert r.success, (key, r.status)
         self.last[key] = r.x
         return r.x
@@ -91,3 +93,58 @@ class C2Oracle(_Solver):
         p, lbw, ubw, w0 = nlps.admm_ahu_inputs(self.ahu, N=self.N, rho=rho, zbar=zbar, lam=lam)
         x = self._run(ag, self.ahu, p, lbw, ubw, w0)
         return {a: _pick(self.ahu, x, f"mDot_out_{i + 1}") for i, a in enumerate(als)}
+
+
+class C5Oracle(_Solver):
+    """examples/three_zone_datadriven_admm: 3 NARX zones + AHU + CCA supply, one block.
+
+    tol 1e-8: the supply controllers' objectives reach ~5e6 (ts = 1800 s) and their
+    smoothed |power| terms are nearly non-smooth, so tol 1e-10 is below fp64 reach."""
+
+    tol = 1e-8
+
+    ZONE_COUPLINGS = (("T_v", "T_coupling"), ("T_ahu", "T_coupling_ahu"), ("T_CCA_out", "T_rucklauf"),
+                      ("T_air_out", "T_airin"))
+
+    def __init__(self, N, anns):
+        super().__init__()
+        self.N = N
+        air, cca = (nlps.ann_layers_from_serialized(a.layer_specs()) for a in anns)
+        self.zone = nlps.room_nn(air, cca, N=N)
+        self.ahu = nlps.tz_ahu(N=N)
+        self.cca = nlps.tz_cca(N=N)
+        self.participation, self.initial = {}, {}
+        init = {"T_v": 294.15, "T_ahu": 295.0, "T_CCA_out": 294.15, "T_air_out": 294.0}
+        for i in range(3):
+            ag = f"zone{i}"
+            self.participation[ag] = {f"{pre}{i + 1}_b0": "consensus" for _, pre in self.ZONE_COUPLINGS}
+            self.initial[ag] = {f"{pre}{i + 1}_b0": init[v] for v, pre in self.ZONE_COUPLINGS}
+        self.ahu_al = [a for i in range(3) for a in (f"T_coupling_ahu{i + 1}_b0", f"T_airin{i + 1}_b0")]
+        self.cca_al = [a for i in range(3) for a in (f"T_coupling{i + 1}_b0", f"T_rucklauf{i + 1}_b0")]
+        self.participation["ahu"] = {a: "consensus" for a in self.ahu_al}
+        self.participation["cca"] = {a: "consensus" for a in self.cca_al}
+        self.initial["ahu"] = {a: 295.0 for a in self.ahu_al}
+        self.initial["cca"] = {a: 294.15 for a in self.cca_al}
+
+    def __call__(self, ag, inp, rho):
+        if ag.startswith("zone"):
+            i = int(ag[4:])
+            als = [f"{pre}{i + 1}_b0" for _, pre in self.ZONE_COUPLINGS]
+            zbar = np.stack([inp[a][0] for a in als])
+            lam = np.stack([inp[a][1] for a in als])
+            p, lbw, ubw, w0 = nlps.room_nn_inputs(self.zone, N=self.N, rho=rho, zbar=zbar, lam=lam)
+            x = self._run(ag, self.zone, p, lbw, ubw, w0)
+            return {a: _pick_times(self.zone, x, v) for a, (v, _) in zip(als, self.ZONE_COUPLINGS)}
+        prob, als = (self.ahu, self.ahu_al) if ag == "ahu" else (self.cca, self.cca_al)
+        zbar = np.stack([inp[a][0] for a in als])
+        lam = np.stack([inp[a][1] for a in als])
+        p, lbw, ubw, w0 = nlps.tz_supply_inputs(prob, N=self.N, rho=rho, zbar=zbar, lam=lam)
+        x = self._run(ag, prob, p, lbw, ubw, w0)
+        cn = [n.split("@")[0] for n in prob.w_names[:len(prob.w_names) // self.N]][-6:]
+        return {a: _pick(prob, x, c) for a, c in zip(als, cn)}
+
+
+def _pick_times(prob, x, prefix):
+    """Trajectory of ``prefix`` on its grid times >= 0 (``Results[name]``)."""
+    idx = [i for i, n in enumerate(prob.w_names) if n.split("@")[0] == prefix and int(n.split("@")[1]) >= 0]
+    return np.asarray(x)[idx]

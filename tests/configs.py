@@ -92,6 +92,24 @@ def room_nn(**kw) -> Case:
     return Case(be, cv, prob, nlps.room_nn_inputs(prob, N=N, **o))
 
 
+def _tz(kind, **kw) -> Case:
+    be, cv = (bm.tz_ahu if kind == "ahu" else bm.tz_cca)(**kw)
+    N = kw.get("N", 24)
+    prob = nlps.tz_ahu(N=N) if kind == "ahu" else nlps.tz_cca(N=N)
+    o = {k: kw[k] for k in ("rho", "zbar", "lam", "mDot_0", "r_T_v") if k in kw}
+    if kind == "ahu" and "T_amb" in kw:
+        o["T_amb"] = kw["T_amb"]
+    return Case(be, cv, prob, nlps.tz_supply_inputs(prob, N=N, **o))
+
+
+def tz_ahu(**kw) -> Case:
+    return _tz("ahu", **kw)
+
+
+def tz_cca(**kw) -> Case:
+    return _tz("cca", **kw)
+
+
 CASES: Dict[str, Callable[..., Case]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -99,6 +117,8 @@ CASES: Dict[str, Callable[..., Case]] = {
     "exchange_room": exchange_room,
     "exchange_supply": exchange_supply,
     "room_nn": room_nn,
+    "tz_ahu": tz_ahu,
+    "tz_cca": tz_cca,
 }
 
 

@@ -6,6 +6,9 @@ Tolerances: kernels 1e-12 (fp64 atomics reorder sums); trajectories and
 residual histories rel 1e-5 (north star).
 """
 
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -105,6 +108,23 @@ def test_gpu_coordinated_fleet_matches_oracle():
         np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
         np.testing.assert_allclose(fl.multipliers_of("ahu", f"mDot_out_{i + 1}")[0],
                                    state["vars"][al].mult["ahu"], rtol=RTOL, atol=1e-8)
+
+
+def test_gpu_three_zone_narx_fleet_matches_oracle_fixture():
+    """examples/three_zone_datadriven_admm: 3 NARX zones + AHU + CCA, coordinated ADMM,
+    rho=1, absolute criterion 0.04/0.04, N=8, 3 iterations, against the oracle's round
+    (`tests/golden/c5_admm_N8.json`, `tests/golden/make_c5_admm_golden.py`; both at tol 1e-8)."""
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c5_admm_N8.json")))
+    opts = {"ipopt": {"tol": 1e-8, "max_iter": 500}}
+    fl = ADMMFleet(bm.c5_fleet_classes(n_blocks=1, N=gold["N"], solver_options=opts))
+    out = fl.run_coordinated(gold["rho"], admm_iter_max=3, use_relative_tolerances=False, primal_tol=0.04,
+                             dual_tol=0.04)
+    assert out["iterations"] == gold["iterations"] and out["converged"] == gold["converged"]
+    got = np.array([[r.primal_residual, r.dual_residual] for r in out["records"]])
+    np.testing.assert_allclose(got, np.array(gold["history"]), rtol=RTOL, atol=1e-8)
+    traj = fl.trajectories()
+    for al, mean in gold["means"].items():
+        np.testing.assert_allclose(traj[al], mean, rtol=RTOL, atol=1e-6)
 
 
 def test_gpu_fleet_blocks_are_independent():

@@ -20,6 +20,8 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "exchange_room": (31, 20, 71),
     "exchange_supply": (20, 10, None),
     "room_nn": (182, 120, 417),  # n_x≈182, n_g≈120
+    "tz_ahu": (288, 144, 344),     # 24 x (3 u + 3 W + 6 couplings), 24 x 6 output equations
+    "tz_cca": (240, 144, 318),
 }
 
 

@@ -93,23 +93,25 @@ def cpu_baseline(p, lbw, ubw, w0, tol, min_seconds=10.0, max_repeats=200):
                       f"gcc -O3 -march=native, OpenMP {threads} threads): {dt:.2f} s wall"}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "s4", "pmc_traffic_c3.json")
-
-
 def pmc_traffic(code_object: str, n_agents: int):
     """HBM bytes per launch of the bench kernel from the committed rocprofv3 PMC
-    passes (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH_SIZE doubled as the
-    MI355X guide prescribes for gfx950). Only used when the summary was taken on
-    the same code object and fleet size; otherwise None (PMC cannot run inside
-    the timed process)."""
-    try:
-        with open(PMC_TRAFFIC) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
+    passes (``profiles/*/*/pmc_traffic_c3.json``: FETCH_SIZE and WRITE_SIZE in
+    separate runs, FETCH_SIZE doubled as the MI355X guide prescribes for gfx950).
+    Only a summary taken on the same code object and fleet size is used;
+    otherwise None (PMC counters cannot be read inside the timed process)."""
+    import glob
+
+    if n_agents != 4096:
         return None, None
-    if d.get("code_object") != code_object or n_agents != 4096:
-        return None, None
-    return float(d["hbm_bytes_per_launch"]), os.path.relpath(PMC_TRAFFIC, ROOT)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*", "pmc_traffic_c3.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("code_object") == code_object:
+            return float(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def admm_bench(args, world, rank, dev):

@@ -160,6 +160,7 @@ class IterationRecord:
     dual_residual: float
     penalty: float
     converged_solves: Optional[int] = None
+    wall_time: Optional[float] = None  # seconds of this ADMM iteration (coordinated runs)
 
 
 class ADMMFleet:
@@ -374,11 +375,14 @@ class ADMMFleet:
         records = []
         t0 = time.perf_counter()
         self._ok_count.zero_()
+        t_it = t0
         for it in range(1, admm_iter_max + 1):
             self._solve_all(rho)
             tot = self._update_means(rho, apply_multipliers=True).cpu().numpy()
             prim, dual = math.sqrt(max(tot[0], 0.0)), math.sqrt(max(tot[1], 0.0))
-            records.append(IterationRecord(prim, dual, rho))
+            now_t = time.perf_counter()
+            records.append(IterationRecord(prim, dual, rho, wall_time=now_t - t_it))
+            t_it = now_t
             if use_relative_tolerances:
                 scale_p = max(math.sqrt(max(tot[2], 0.0)), math.sqrt(max(tot[3], 0.0)))
                 eps_pri = math.sqrt(tot[6]) * abs_tol + rel_tol * scale_p
@@ -402,6 +406,24 @@ class ADMMFleet:
         self.rounds += 1
         return {"iterations": it, "converged": converged, "records": records, "wall_s": wall,
                 "converged_solves": int(self._ok_count.item())}
+
+    def save_stats(self, path, start_time: float, records: Sequence[IterationRecord], first_iteration: int = 0):
+        """Append one round's residual history to the coordinator's ``solve_stats_file``
+        (``ADMMCoordinator._save_stats``, `admm_coordinator.py:437-465`): index
+        ``(start_time, iteration)``, columns primal_residual, dual_residual,
+        penalty_parameter, wall_time."""
+        import pandas as pd
+        from pathlib import Path
+
+        path = Path(path)
+        header = not path.is_file()
+        df = pd.DataFrame({"primal_residual": [r.primal_residual for r in records],
+                           "dual_residual": [r.dual_residual for r in records],
+                           "penalty_parameter": [r.penalty for r in records],
+                           "wall_time": [r.wall_time for r in records]},
+                          index=[(start_time, first_iteration + i) for i in range(len(records))])
+        path.parent.mkdir(exist_ok=True, parents=True)
+        df.to_csv(path_or_buf=path, header=header, mode="a")
 
     def run_local(self, penalty_factor: float, max_iterations: int, record_residuals: bool = True) -> dict:
         """One control step of decentralised ADMM (``LocalADMM.process``, `admm.py:873-937`)."""

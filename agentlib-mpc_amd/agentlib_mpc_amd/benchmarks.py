@@ -29,11 +29,11 @@ def V(name, value=None, lb=-np.inf, ub=np.inf):
 
 
 def one_room(N=15, T0=298.16, load=150.0, T_in=290.15, T_upper=295.15, u_prev=0.02,
-             s_T=0.001, r_mDot=0.01, d=2, solver_options=TIGHT):
+             s_T=0.001, r_mDot=0.01, d=2, solver_options=TIGHT, method="legendre"):
     be = create_optimization_backend({
         "type": "mi355x",
         "model": {"type": "agentlib_mpc_amd.models.examples.OneRoom"},
-        "discretization_options": {"collocation_order": d, "collocation_method": "legendre",
+        "discretization_options": {"collocation_order": d, "collocation_method": method,
                                    "prediction_horizon": N, "time_step": 300},
         "solver": {"name": "ipopt", "options": solver_options},
     })
@@ -99,11 +99,11 @@ def admm_ahu(N=10, rho=0.4, zbar=0.01, lam=0.0, solver_options=TIGHT):
 
 
 def exchange_room(N=10, T0=296.0, dist=150.0, rho=1e4, diff=0.0, lam=0.0, T_set=296.0,
-                  solver_options=TIGHT):
+                  solver_options=TIGHT, integrator="euler"):
     be = create_optimization_backend({
         "type": "mi355x_admm",
         "model": {"type": "agentlib_mpc_amd.models.examples.ExchangeRoom"},
-        "discretization_options": {"method": "multiple_shooting", "integrator": "euler",
+        "discretization_options": {"method": "multiple_shooting", "integrator": integrator,
                                    "prediction_horizon": N, "time_step": 120},
         "solver": {"name": "ipopt", "options": solver_options},
     })
@@ -273,6 +273,8 @@ def compile_all(verbose: bool = False):
     # the benchmark structures plus the test-only variants (copy-lifted NARX, N=23)
     variants = dict(BUILDERS)
     variants["room_nn_n23"] = lambda: room_nn(N=23)
+    variants["exchange_room_rk"] = lambda: exchange_room(integrator="rk")
+    variants["one_room_radau3"] = lambda: one_room(d=3, method="radau")
     variants["room_nn_n8"] = lambda: room_nn(N=8)      # C5 ADMM fixture (tests/golden/c5_admm_N8.json)
     variants["tz_ahu_n8"] = lambda: tz_ahu(N=8)
     variants["tz_cca_n8"] = lambda: tz_cca(N=8)

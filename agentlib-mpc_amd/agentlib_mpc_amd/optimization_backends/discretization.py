@@ -530,18 +530,50 @@ def _euler(ode: List[sx.Expr], x: List[sx.Expr], ts: float) -> List[sx.Expr]:
     return [sx.add(xi, sx.mul(oi, ts)) for xi, oi in zip(x, ode)]
 
 
+#: CasADi's "rk" integrator plugin: fixed-step classical RK4 over
+#: ``number_of_finite_elements`` (default 20) steps of the interval
+RK_FINITE_ELEMENTS = 20
+
+
+def _rk4(f, x: List[sx.Expr], ts: float, steps: int = RK_FINITE_ELEMENTS) -> List[sx.Expr]:
+    """``ca.integrator("system", "rk", ...)`` (`casadi_/basic.py:450-476`): the model
+    inputs, parameters, algebraics and outputs are constant over the interval."""
+    h = ts / steps
+    for _ in range(steps):
+        k1 = f(x)
+        k2 = f([sx.add(a, sx.mul(h / 2, b)) for a, b in zip(x, k1)])
+        k3 = f([sx.add(a, sx.mul(h / 2, b)) for a, b in zip(x, k2)])
+        k4 = f([sx.add(a, sx.mul(h, b)) for a, b in zip(x, k3)])
+        x = [sx.add(a, sx.mul(h / 6, sx.add(sx.add(b1, sx.mul(2.0, b2)), sx.add(sx.mul(2.0, b3), b4))))
+             for a, b1, b2, b3, b4 in zip(x, k1, k2, k3, k4)]
+    return x
+
+
 class BasicMultipleShooting(Discretization):
     """`casadi_/basic.py:395-448` (backend ``casadi_basic``, multiple shooting)."""
 
     def _check_integrator(self, system=None):
-        """Only Euler is implemented; without differential states (e.g. the
-        three-zone AHU/CCA controllers, which keep the cvodes default) the
-        integrator is never used."""
+        """Euler and the fixed-step "rk" plugin are restated; cvodes (adaptive) is
+        not.  Without differential states (e.g. the three-zone AHU/CCA controllers,
+        which keep the cvodes default) the integrator is never used."""
         if system is not None and system.states.dim == 0:
             return
-        if self.options.integrator != Integrators.euler:
+        if self.options.integrator not in (Integrators.euler, Integrators.rk):
             raise TranscriptionError(
-                f"integrator '{self.options.integrator.value}' is not supported on MI355X yet; use 'euler'")
+                f"integrator '{self.options.integrator.value}' is not supported on MI355X yet; "
+                "use 'euler' or 'rk'")
+
+    def _integrate(self, t, s, vals, xk, ode, time):
+        """End state of the interval (`casadi_/basic.py:450-476` ``_create_ode``)."""
+        ts = self.options.time_step
+        if s.states.dim == 0 or self.options.integrator == Integrators.euler:
+            return _euler(ode, xk, ts)
+        name = s.states.name
+
+        def f(x):
+            return t.stage_call(s, {**vals, name: x}, time)[0]
+
+        return _rk4(f, xk, ts)
 
     def _discretize(self, t, s):
         self._check_integrator(s)
@@ -558,9 +590,10 @@ class BasicMultipleShooting(Discretization):
             vals = {s.states.name: xk, s.algebraics.name: zk, s.outputs.name: yk,
                     s.controls.name: uk, s.non_controlled_inputs.name: dk,
                     s.model_parameters.name: const_par}
-            ode, cost, g, lb, ub = t.stage_call(s, vals, t.time_expr())
+            tk = t.time_expr()
+            ode, cost, g, lb, ub = t.stage_call(s, vals, tk)
             t.add_constraint(g, lb, ub)
-            x_end = _euler(ode, xk, ts)
+            x_end = self._integrate(t, s, vals, xk, ode, tk)
             t.pred_time = ts * (k + 1)
             xk = t.add_opt_var(s.states)
             t.add_constraint([sx.sub(a, b) for a, b in zip(x_end, xk)], gap_closing=True)
@@ -590,8 +623,9 @@ class FullMultipleShooting(BasicMultipleShooting):
             vals = {s.states.name: xk, s.algebraics.name: zk, s.outputs.name: yk,
                     s.controls.name: uk, s.non_controlled_inputs.name: dk,
                     s.model_parameters.name: const_par}
-            ode, cost, g, lb, ub = t.stage_call(s, vals, t.time_expr())
-            x_end = _euler(ode, xk, ts)
+            tk = t.time_expr()
+            ode, cost, g, lb, ub = t.stage_call(s, vals, tk)
+            x_end = self._integrate(t, s, vals, xk, ode, tk)
             t.pred_time = ts * (k + 1)
             xk = t.add_opt_var(s.states)
             t.add_constraint([sx.sub(a, b) for a, b in zip(xk, x_end)], gap_closing=True)
@@ -639,7 +673,7 @@ class ADMMMultipleShooting(BasicMultipleShooting):
                     s.penalty_factor.name: rho, s.exchange_diff.name: ed,
                     s.exchange_multipliers.name: em}
             ode, cost, g, lb, ub = t.stage_call(s, vals, sx.ZERO)
-            x_end = _euler(ode, xk, ts)
+            x_end = self._integrate(t, s, vals, xk, ode, sx.ZERO)
             t.pred_time = ts * (k + 1)
             xk = t.add_opt_var(s.states)
             t.add_constraint([sx.sub(a, b) for a, b in zip(xk, x_end)], gap_closing=True)

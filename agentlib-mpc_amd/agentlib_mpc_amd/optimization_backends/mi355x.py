@@ -201,6 +201,38 @@ class MI355XADMMBackend(MI355XBackend, ADMMBackend):
         """`casadi_/admm.py:360-362`: grid of the multipliers parameter group."""
         return list(self.problem.nlp.par_groups[self.system.multipliers.name].grid)
 
+    def save_result_df(self, results: Results, now: float = 0):
+        """`casadi_/admm.py:364-424`: results of every ADMM iteration, indexed
+        ``(now, iteration, t)``, buffered and flushed at the start of a new time
+        step or every 1000 iterations."""
+        if not self.config.save_results:
+            return
+        res_file = self.config.results_file
+        if not hasattr(self, "_admm_buffer"):
+            self._admm_buffer, self._admm_stats, self.it, self.now = [], [], 0, now
+        if self.results_folder_exists():
+            self.it += 1
+            if now != self.now:
+                self.it = 0
+                self.now = now
+        else:
+            self.it = 0
+            self.now = now
+            results.write_columns(res_file)
+            results.write_stats_columns(stats_path(res_file))
+        df = results.df
+        df.index = [str((now, self.it, x)) for x in df.index]
+        self._admm_buffer.append(df)
+        self._admm_stats.append(results.stats_line(str((now, self.it))))
+        if not (self.it == 0 or self.it % 1000 == 0):
+            return
+        with open(res_file, "a", newline="") as f:
+            for it_result in self._admm_buffer:
+                it_result.to_csv(f, mode="a", header=False)
+        with open(stats_path(res_file), "a") as f:
+            f.writelines(self._admm_stats)
+        self._admm_buffer, self._admm_stats = [], []
+
 
 class MI355XMLBackend(MI355XBackend):
     """Backend ``"casadi_ml"`` / ``"casadi_nn"`` replacement (``CasADiBBBackend``,
@@ -234,3 +266,7 @@ class MI355XADMMNNBackend(MI355XMLBackend, ADMMBackend):
     @property
     def coupling_grid(self) -> list:
         return list(self.problem.nlp.par_groups[self.system.multipliers.name].grid)
+
+
+# the NN-ADMM backend saves like the ADMM backend (`casadi_admm_ml.py:508` inherits it)
+MI355XADMMNNBackend.save_result_df = MI355XADMMBackend.save_result_df

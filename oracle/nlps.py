@@ -343,7 +343,20 @@ def admm_ahu_inputs(prob, N=10, d=3, rooms=4, mDot_max=0.1, rho=0.4, zbar=None, 
 # C4: exchange ADMM, backend "casadi_admm", multiple shooting + Euler
 # ---------------------------------------------------------------------------
 
-def exchange_room(N=10, ts=120.0) -> OracleProblem:
+def _rk4_step(fun, x, ts, steps=20):
+    """Fixed-step RK4 over ``steps`` sub-intervals (CasADi "rk" integrator plugin,
+    default ``number_of_finite_elements`` = 20; `casadi_/basic.py:450-476`)."""
+    h = ts / steps
+    for _ in range(steps):
+        k1 = fun(x)
+        k2 = fun(x + h / 2 * k1)
+        k3 = fun(x + h / 2 * k2)
+        k4 = fun(x + h * k3)
+        x = x + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+    return x
+
+
+def exchange_room(N=10, ts=120.0, integrator="euler") -> OracleProblem:
     nb = 3                       # mDot, mDot_out, T_end
     n = 1 + N * nb
     m = N * 2                    # cont, output eq
@@ -378,8 +391,9 @@ def exchange_room(N=10, ts=120.0) -> OracleProblem:
             u, y, T1 = w[o], w[o + 1], w[o + 2]
             ps = npg + k * nps
             dist, T_in = p[ps], p[ps + 3]
-            ode = cp * u / cZ * (T_in - T) + dist / cZ
-            out.append(T1 - (T + ode * ts))
+            fun = lambda x: cp * u / cZ * (T_in - x) + dist / cZ  # noqa: E731
+            x_end = T + fun(T) * ts if integrator == "euler" else _rk4_step(fun, T, ts)
+            out.append(T1 - x_end)
             out.append(y - u)
         return torch.stack(out)
 

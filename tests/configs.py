@@ -26,7 +26,7 @@ class Case:
 def one_room(**kw) -> Case:
     be, cv = bm.one_room(**kw)
     N, d = kw.get("N", 15), kw.get("d", 2)
-    prob = nlps.one_room(N=N, d=d)
+    prob = nlps.one_room(N=N, d=d, method=kw.get("method", "legendre"))
     keys = ("T0", "load", "T_in", "T_upper", "s_T", "r_mDot", "u_prev")
     return Case(be, cv, prob, nlps.one_room_inputs(prob, N=N, d=d, **{k: kw[k] for k in keys if k in kw}))
 
@@ -56,7 +56,7 @@ def exchange_room(**kw) -> Case:
     be, cv = bm.exchange_room(**kw)
     N = kw.get("N", 10)
     n = len(be.coupling_grid)
-    prob = nlps.exchange_room(N=N)
+    prob = nlps.exchange_room(N=N, integrator=kw.get("integrator", "euler"))
     o = {k: kw[k] for k in ("T0", "dist", "rho", "T_set") if k in kw}
     o["diff"] = np.asarray(bm._vals(kw.get("diff", 0.0), n))
     o["lam"] = np.asarray(bm._vals(kw.get("lam", 0.0), n))
@@ -110,6 +110,14 @@ def tz_cca(**kw) -> Case:
     return _tz("cca", **kw)
 
 
+def one_room_radau(**kw) -> Case:
+    return one_room(d=3, method="radau", **kw)
+
+
+def exchange_room_rk(**kw) -> Case:
+    return exchange_room(integrator="rk", **kw)
+
+
 CASES: Dict[str, Callable[..., Case]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -119,6 +127,8 @@ CASES: Dict[str, Callable[..., Case]] = {
     "room_nn": room_nn,
     "tz_ahu": tz_ahu,
     "tz_cca": tz_cca,
+    "exchange_room_rk": exchange_room_rk,
+    "one_room_radau": one_room_radau,
 }
 
 

@@ -52,6 +52,8 @@ def _cuda():
     # N=23 has no super-stage length dividing it: copy-lifted stages whose interiors
     # are singular, i.e. the sequential block-chain fallback of the kernel
     ("room_nn", {"N": 23}),
+    ("exchange_room_rk", {}),          # multiple shooting with the "rk" integrator
+    ("one_room_radau", {}),            # Radau IIA collocation, d=3
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)

@@ -22,6 +22,8 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "room_nn": (182, 120, 417),  # n_x≈182, n_g≈120
     "tz_ahu": (288, 144, 344),     # 24 x (3 u + 3 W + 6 couplings), 24 x 6 output equations
     "tz_cca": (240, 144, 318),
+    "exchange_room_rk": (31, 20, 71),  # C4 room with the "rk" integrator (20 RK4 steps)
+    "one_room_radau": (1 + 15 * (1 + 3 * 3 + 1), 15 * (1 + 3 * 3), None),  # Radau IIA, d=3
 }
 
 

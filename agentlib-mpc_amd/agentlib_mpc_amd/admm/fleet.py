@@ -143,10 +143,10 @@ class FleetClass:
         """Reference-layout class inputs -> kernel layout (None passes through)."""
         if self.lift is None:
             return p, lbw, ubw
-        l = self.lift
-        kp = None if p is None else np.ascontiguousarray(np.asarray(p)[..., l.p_src])
-        klb = None if lbw is None else np.where(l.w_dup, -np.inf, np.asarray(lbw)[..., l.w_src])
-        kub = None if ubw is None else np.where(l.w_dup, np.inf, np.asarray(ubw)[..., l.w_src])
+        if p is None or lbw is None or ubw is None:
+            raise ValueError("lifted classes need p, lbw and ubw together")
+        kp, klb, kub, _ = self.backend.problem.to_kernel(np.asarray(p), np.asarray(lbw), np.asarray(ubw),
+                                                         np.asarray(lbw))
         return kp, klb, kub
 
     @property
@@ -296,7 +296,7 @@ class ADMMFleet:
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
         """New measurements/forecasts for the next control step (host -> HBM);
-        reference-layout arrays."""
+        reference-layout arrays (lifted classes need all three)."""
         c = next(c for c in self.classes if c.name == class_name)
         p, lbw, ubw = c.to_kernel(p, lbw, ubw)
         c.P.copy_(self.torch.as_tensor(p))

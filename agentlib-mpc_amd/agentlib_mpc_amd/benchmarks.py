@@ -29,22 +29,27 @@ def V(name, value=None, lb=-np.inf, ub=np.inf):
 
 
 def one_room(N=15, T0=298.16, load=150.0, T_in=290.15, T_upper=295.15, u_prev=0.02,
-             s_T=0.001, r_mDot=0.01, d=2, solver_options=TIGHT, method="legendre"):
+             s_T=0.001, r_mDot=0.01, d=2, solver_options=TIGHT, method="legendre", r_delta_mDot=None):
+    """``r_delta_mDot``: use the change-penalty model (`with_change_control_penalty.py`)."""
     be = create_optimization_backend({
         "type": "mi355x",
-        "model": {"type": "agentlib_mpc_amd.models.examples.OneRoom"},
+        "model": {"type": "agentlib_mpc_amd.models.examples."
+                          + ("OneRoom" if r_delta_mDot is None else "OneRoomDU")},
         "discretization_options": {"collocation_order": d, "collocation_method": method,
                                    "prediction_horizon": N, "time_step": 300},
         "solver": {"name": "ipopt", "options": solver_options},
     })
+    pars = ["s_T", "r_mDot"] + ([] if r_delta_mDot is None else ["r_delta_mDot"])
     be.setup_optimization(VariableReference(
         states=["T"], controls=["mDot"], inputs=["T_in", "load", "T_upper"],
-        parameters=["s_T", "r_mDot"], outputs=["T_out"]))
+        parameters=pars, outputs=["T_out"]))
     cv = {
         "T": V("T", T0, 288.15, 303.15), "mDot": V("mDot", u_prev, 0.0, 0.05),
         "T_in": V("T_in", T_in), "load": V("load", load), "T_upper": V("T_upper", T_upper),
         "s_T": V("s_T", s_T), "r_mDot": V("r_mDot", r_mDot), "T_out": V("T_out"),
     }
+    if r_delta_mDot is not None:
+        cv["r_delta_mDot"] = V("r_delta_mDot", r_delta_mDot)
     return be, cv
 
 
@@ -275,6 +280,7 @@ def compile_all(verbose: bool = False):
     variants["room_nn_n23"] = lambda: room_nn(N=23)
     variants["exchange_room_rk"] = lambda: exchange_room(integrator="rk")
     variants["one_room_radau3"] = lambda: one_room(d=3, method="radau")
+    variants["one_room_du"] = lambda: one_room(r_delta_mDot=0.1)
     variants["room_nn_n8"] = lambda: room_nn(N=8)      # C5 ADMM fixture (tests/golden/c5_admm_N8.json)
     variants["tz_ahu_n8"] = lambda: tz_ahu(N=8)
     variants["tz_cca_n8"] = lambda: tz_cca(N=8)

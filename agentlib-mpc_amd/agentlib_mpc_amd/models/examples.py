@@ -58,6 +58,28 @@ class OneRoom(CasadiModel):
         return self.create_combined_objective(ctrl, slack, normalization=1)
 
 
+class OneRoomDUConfig(OneRoomConfig):
+    parameters: List[CasadiParameter] = [
+        _par("cp", 1000), _par("C", 100000), _par("s_T", 1), _par("r_mDot", 1), _par("r_delta_mDot", 1),
+    ]
+
+
+class OneRoomDU(CasadiModel):
+    """`examples/one_room_mpc/physical/with_change_control_penalty.py:98-133`:
+    the one-room model with a change penalty on the supply mass flow."""
+
+    config: OneRoomDUConfig
+
+    def setup_system(self):
+        self.T.ode = self.cp * self.mDot / self.C * (self.T_in - self.T) + self.load / self.C
+        self.T_out.alg = self.T
+        self.constraints = [(0, self.T + self.T_slack, self.T_upper)]
+        obj1 = self.create_sub_objective(expressions=self.mDot, weight=self.r_mDot, name="control_costs")
+        obj2 = self.create_sub_objective(expressions=self.T_slack ** 2, weight=self.s_T, name="temp_slack")
+        obj3 = self.create_change_penalty(expressions=self.mDot, name="delta_control_penalty")
+        return self.create_combined_objective(obj1, obj2, obj3 * self.r_delta_mDot, normalization=1)
+
+
 class CooledRoomConfig(CasadiModelConfig):
     inputs: List[CasadiInput] = [
         _inp("mDot", 0.0225), _inp("d", 150), _inp("T_in", 290.15),

@@ -216,6 +216,9 @@ class _Transcriber:
         self.var_groups: Dict[str, GroupLayout] = {}
         self.par_groups: Dict[str, GroupLayout] = {}
         self.tk_syms: Dict[int, sx.Expr] = {}
+        #: change penalties: the previous controls carried in the kernel's stage state
+        #: ({"v_pos": positions of u in V, "init": u_prev parameter symbols})
+        self.carry: Optional[dict] = None
 
     # time as "stage start symbol + offset" keeps all stages structurally equal
     def time_expr(self) -> sx.Expr:
@@ -341,9 +344,14 @@ class _Transcriber:
         if [i for s in stage_p for i in s] != list(range(npg, len(self.p))):
             raise TranscriptionError("stage parameters are not contiguous")
 
-        X0 = [sx.sym(f"X0[{i}]") for i in range(nx)]
+        # change penalties read u_{k-1}: the kernel stage state carries a copy of it
+        # (X_k = [x_k, u_{k-1}], shift constraint X_{k+1}[u] = u_k; X_0[u] is fixed
+        # to u_prev), every reference variable keeps its primary position
+        carry = self.carry
+        nc = len(carry["v_pos"]) if carry else 0
+        X0 = [sx.sym(f"X0[{i}]") for i in range(nx + nc)]
         V = [sx.sym(f"V[{i}]") for i in range(nv)]
-        X1 = [sx.sym(f"X1[{i}]") for i in range(nx)]
+        X1 = [sx.sym(f"X1[{i}]") for i in range(nx + nc)]
         PS = [sx.sym(f"PS[{i}]") for i in range(nps)]
         PG = [sx.sym(f"PG[{i}]") for i in range(npg)]
         TK = sx.sym("TK")
@@ -362,6 +370,10 @@ class _Transcriber:
                 mapping[s] = ph
             for s, ph in zip(self.p[:npg], PG):
                 mapping[s] = ph
+            if carry:
+                src = carry["init"] if k == 0 else [self.w[stage_w[k - 1][q]] for q in carry["v_pos"]]
+                for s, ph in zip(src, X0[nx:]):
+                    mapping[s] = ph
             if k in self.tk_syms:
                 mapping[self.tk_syms[k]] = TK
             gs = [self.g[i] for i in stage_g[k]]
@@ -378,13 +390,21 @@ class _Transcriber:
                 ref = sub
             elif any(a is not b for a, b in zip(ref, sub)):
                 raise TranscriptionError(f"stage {k} differs structurally from stage 0")
-        stage = StageFunction(X0=X0, V=V, X1=X1, PS=PS, PG=PG, TK=TK, cost=ref[0],
-                              g=ref[1:1 + ng], g_lb=ref[1 + ng:1 + 2 * ng], g_ub=ref[1 + 2 * ng:])
+        g, g_lb, g_ub = list(ref[1:1 + ng]), list(ref[1 + ng:1 + 2 * ng]), list(ref[1 + 2 * ng:])
+        lift = None
+        if carry:
+            for i, q in enumerate(carry["v_pos"]):
+                g.append(sx.sub(X1[nx + i], V[q]))
+                g_lb.append(sx.ZERO)
+                g_ub.append(sx.ZERO)
+            lift = self._carry_maps(N, nx, nv, ng, nc, stage_w, carry)
+        stage = StageFunction(X0=X0, V=V, X1=X1, PS=PS, PG=PG, TK=TK, cost=ref[0], g=g, g_lb=g_lb, g_ub=g_ub)
         f_total = sx.ZERO
         for k in range(N):
             f_total = sx.add(f_total, self.cost.get(k, sx.ZERO))
         return StageNLP(
-            N=N, nx=nx, nv=nv, ng=ng, nps=nps, npg=npg, ts=float(opts.time_step),
+            lift=lift,
+            N=N, nx=nx + nc, nv=nv, ng=ng + nc, nps=nps, npg=npg, ts=float(opts.time_step),
             w_syms=list(self.w), p_syms=list(self.p), w_labels=list(self.w_labels),
             p_labels=list(self.p_labels), g_exprs=[c[0] for c in self.g],
             g_lb=[c[1] for c in self.g], g_ub=[c[2] for c in self.g], f_expr=f_total,
@@ -392,6 +412,31 @@ class _Transcriber:
             tk_values=np.arange(N, dtype=float) * float(opts.time_step),
             gap_closing=[c[4] for c in self.g],
         )
+
+
+    def _carry_maps(self, N, nx, nv, ng, nc, stage_w, carry):
+        from agentlib_mpc_amd.optimization_backends.narx import LiftMaps
+
+        pos = {s.uid: i for i, s in enumerate(self.p)}
+        w_src, w_dup, w_fix = list(range(nx)), [False] * nx, [-1] * nx
+        w_src += [0] * nc
+        w_dup += [False] * nc
+        w_fix += [pos[s.uid] for s in carry["init"]]           # X_0[u] = u_prev (fixed)
+        for k in range(N):
+            loc = stage_w[k]
+            w_src += loc[:nv] + loc[nv:] + [loc[q] for q in carry["v_pos"]]
+            w_dup += [False] * (nv + nx) + [True] * nc         # X_{k+1}[u]: copy of u_k
+            w_fix += [-1] * (nv + nx + nc)
+        w_src = np.asarray(w_src, dtype=np.int64)
+        w_dup = np.asarray(w_dup, dtype=bool)
+        w_fix = np.asarray(w_fix, dtype=np.int64)
+        w_primary = np.full(len(self.w), -1, dtype=np.int64)
+        for ki in np.nonzero(~w_dup & (w_fix < 0))[0]:
+            w_primary[w_src[ki]] = ki
+        ngk = ng + nc
+        g_of_ref = np.asarray([k * ngk + r for k in range(N) for r in range(ng)], dtype=np.int64)
+        return LiftMaps(w_src=w_src, w_dup=w_dup, p_src=np.arange(len(self.p), dtype=np.int64),
+                        g_of_ref=g_of_ref, w_primary=w_primary, w_fix_par=w_fix)
 
 
 # ---------------------------------------------------------------------------
@@ -415,6 +460,29 @@ class Discretization:
 
     def _discretize(self, t: _Transcriber, sys_: BaseSystem):
         raise NotImplementedError
+
+    @staticmethod
+    def _delta_u(t: _Transcriber, s, u_prev, uk, const_par, u_prev_par):
+        """Change penalties ``w**2 * (u_k - u_{k-1})**2`` (`core/delta_u.py:13-26`;
+        not multiplied by ts) added to the cost of the current stage; registers the
+        carried previous control for the kernel's stage form."""
+        dus = s.objective.get_delta_u_objectives()
+        if not dus:
+            return
+        from agentlib_mpc_amd.data_structures.objective import _weight_sym
+
+        if t.carry is None:
+            t.carry = {"v_pos": list(range(s.controls.dim)), "init": list(u_prev_par)}
+        sub = dict(zip(s.model_parameters.full_symbolic, const_par))
+        total = sx.ZERO
+        for obj in dus:
+            names = list(s.controls.ref_names)
+            if obj.control.name not in names:
+                continue  # the reference logs an error and adds 0 (`delta_u.py:24-26`)
+            idx = names.index(obj.control.name)
+            w = sx.substitute([sx.as_expr(_weight_sym(obj.weight))], sub)[0]
+            total = sx.add(total, sx.mul(sx.power(w, 2), sx.power(sx.sub(uk[idx], u_prev[idx]), 2)))
+        t.add_cost(total)
 
     # shared collocation inner loop (`casadi_/basic.py:251-342`)
     def _collocation_inner_loop(self, t: _Transcriber, sys_: BaseSystem, cm: CollocationMatrices,
@@ -478,13 +546,12 @@ class FullCollocation(Discretization):
         n, ts = self.options.prediction_horizon, self.options.time_step
         x0 = t.add_opt_par(s.initial_state)
         xk = t.add_opt_var(s.states, lb=x0, ub=x0, guess=x0)
-        t.add_opt_par(s.last_control)
+        u_prev_par = uk = t.add_opt_par(s.last_control)
         const_par = t.add_opt_par(s.model_parameters)
-        if s.objective.get_delta_u_objectives():
-            raise TranscriptionError("change penalties (delta-u) are not supported yet")
         for k in range(n):
             t.block = k
-            uk = t.add_opt_var(s.controls)
+            u_prev, uk = uk, t.add_opt_var(s.controls)
+            self._delta_u(t, s, u_prev, uk, const_par, u_prev_par)
             const = {s.controls.name: uk, s.model_parameters.name: const_par}
             x_end, cons = self._collocation_inner_loop(
                 t, s, cm, xk, [s.algebraics, s.outputs], [s.non_controlled_inputs], const)
@@ -505,14 +572,13 @@ class ADMMCollocation(Discretization):
         n, ts = self.options.prediction_horizon, self.options.time_step
         x0 = t.add_opt_par(s.initial_state)
         xk = t.add_opt_var(s.states, lb=x0, ub=x0, guess=x0)
-        t.add_opt_par(s.last_control)
+        u_prev_par = uk = t.add_opt_par(s.last_control)
         const_par = t.add_opt_par(s.model_parameters)
         rho = t.add_opt_par(s.penalty_factor)
-        if s.objective.get_delta_u_objectives():
-            raise TranscriptionError("change penalties (delta-u) are not supported yet")
         for k in range(n):
             t.block = k
-            uk = t.add_opt_var(s.controls)
+            u_prev, uk = uk, t.add_opt_var(s.controls)
+            self._delta_u(t, s, u_prev, uk, const_par, u_prev_par)
             inner_vars = [s.algebraics, s.outputs, s.local_couplings, s.local_exchange]
             inner_pars = [s.global_couplings, s.multipliers, s.exchange_multipliers,
                           s.exchange_diff, s.non_controlled_inputs]
@@ -610,13 +676,12 @@ class FullMultipleShooting(BasicMultipleShooting):
         n, ts = self.options.prediction_horizon, self.options.time_step
         x0 = t.add_opt_par(s.initial_state)
         xk = t.add_opt_var(s.states, lb=x0, ub=x0, guess=x0)
-        t.add_opt_par(s.last_control)
+        u_prev_par = uk = t.add_opt_par(s.last_control)
         const_par = t.add_opt_par(s.model_parameters)
-        if s.objective.get_delta_u_objectives():
-            raise TranscriptionError("change penalties (delta-u) are not supported yet")
         for k in range(n):
             t.block = k
-            uk = t.add_opt_var(s.controls)
+            u_prev, uk = uk, t.add_opt_var(s.controls)
+            self._delta_u(t, s, u_prev, uk, const_par, u_prev_par)
             dk = t.add_opt_par(s.non_controlled_inputs)
             zk = t.add_opt_var(s.algebraics)
             yk = t.add_opt_var(s.outputs)
@@ -648,15 +713,14 @@ class ADMMMultipleShooting(BasicMultipleShooting):
         n, ts = self.options.prediction_horizon, self.options.time_step
         x0 = t.add_opt_par(s.initial_state)
         xk = t.add_opt_var(s.states, lb=x0, ub=x0, guess=x0)
-        t.add_opt_par(s.last_control)
-        t.add_opt_par(s.model_parameters)
+        u_prev_par = uk = t.add_opt_par(s.last_control)
+        const_par = t.add_opt_par(s.model_parameters)   # first copy weights the change penalties
         model_pars = t.add_opt_par(s.model_parameters)
         rho = t.add_opt_par(s.penalty_factor)
-        if s.objective.get_delta_u_objectives():
-            raise TranscriptionError("change penalties (delta-u) are not supported yet")
         for k in range(n):
             t.block = k
-            uk = t.add_opt_var(s.controls)
+            u_prev, uk = uk, t.add_opt_var(s.controls)
+            self._delta_u(t, s, u_prev, uk, const_par, u_prev_par)
             dk = t.add_opt_par(s.non_controlled_inputs)
             zk = t.add_opt_var(s.algebraics)
             yk = t.add_opt_var(s.outputs)

@@ -168,6 +168,7 @@ class LiftMaps:
     g_of_ref: np.ndarray     # [ng_ref] kernel constraint index of each reference constraint
     w_primary: np.ndarray    # [nw_ref] kernel index of each reference variable (-1: fixed, unused)
     steps_per_stage: int = 1  # reference steps per kernel stage
+    w_fix_par: "np.ndarray | None" = None  # [nw_kernel] parameter fixing the variable (-1: none)
 
     @property
     def nw(self) -> int:

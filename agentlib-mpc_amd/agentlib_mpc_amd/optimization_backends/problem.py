@@ -154,6 +154,12 @@ class CompiledProblem:
         klb[..., lift.w_dup] = -np.inf
         kub[..., lift.w_dup] = np.inf
         kw = np.array(w0[..., lift.w_src], order="C")
+        if lift.w_fix_par is not None:  # kernel-only variables fixed to a parameter
+            fx = np.flatnonzero(lift.w_fix_par >= 0)
+            val = p[..., lift.w_fix_par[fx]]
+            klb[..., fx] = val
+            kub[..., fx] = val
+            kw[..., fx] = val
         return kp, klb, kub, kw
 
     def from_kernel(self, w_k: np.ndarray, lbw: np.ndarray) -> np.ndarray:

@@ -101,12 +101,16 @@ class OracleProblem:
 # C1 / C3: one room, backend "casadi", collocation
 # ---------------------------------------------------------------------------
 
-def one_room(N=15, ts=300.0, d=2, method="legendre") -> OracleProblem:
+def one_room(N=15, ts=300.0, d=2, method="legendre", delta_u=False) -> OracleProblem:
+    """``delta_u``: the change-penalty variant of
+    `examples/one_room_mpc/physical/with_change_control_penalty.py` (extra model
+    parameter r_delta_mDot; cost += r_delta_mDot**2 (u_k - u_{k-1})**2 with
+    u_{-1} = u_prev, `casadi_/full.py:58-70`, `core/delta_u.py:13-26`)."""
     tau, B, C, D = collocation(d, method)
     nb = 1 + 3 * d + 1          # u, (T, T_slack, T_out) per point, T_end
     n = 1 + N * nb
     m = N * (1 + 3 * d)         # cont, (col, path, out) per point
-    npg = 1 + 1 + 4             # T0, u_prev, (cp, C, s_T, r_mDot)
+    npg = 1 + 1 + 4 + int(delta_u)  # T0, u_prev, (cp, C, s_T, r_mDot[, r_delta_mDot])
     nps = 3 * d                 # (T_in, load, T_upper) per point
     names = ["T@0"]
     for k in range(N):
@@ -125,6 +129,9 @@ def one_room(N=15, ts=300.0, d=2, method="legendre") -> OracleProblem:
         for k in range(N):
             o = 1 + k * nb
             u = w[o]
+            if delta_u:
+                u_prev = p[1] if k == 0 else w[o - nb]
+                tot = tot + p[6] ** 2 * (u - u_prev) ** 2
             for j in range(d):
                 zs = w[o + 1 + 3 * j + 1]
                 tot = tot + B[j + 1] * (r * u + s_T * zs ** 2) * ts
@@ -166,8 +173,8 @@ def one_room(N=15, ts=300.0, d=2, method="legendre") -> OracleProblem:
 
 def one_room_inputs(prob: OracleProblem, N=15, d=2, T0=298.16, load=150.0, T_in=290.15,
                     T_upper=295.15, s_T=0.001, r_mDot=0.01, u_prev=0.02, cp=1000.0, C=100000.0,
-                    T_lb=288.15, T_ub=303.15, u_lb=0.0, u_ub=0.05):
-    p = [T0, u_prev, cp, C, s_T, r_mDot]
+                    T_lb=288.15, T_ub=303.15, u_lb=0.0, u_ub=0.05, r_delta_mDot=None):
+    p = [T0, u_prev, cp, C, s_T, r_mDot] + ([] if r_delta_mDot is None else [r_delta_mDot])
     for k in range(N):
         for j in range(d):
             p += [T_in, load, T_upper]

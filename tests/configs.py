@@ -26,8 +26,8 @@ class Case:
 def one_room(**kw) -> Case:
     be, cv = bm.one_room(**kw)
     N, d = kw.get("N", 15), kw.get("d", 2)
-    prob = nlps.one_room(N=N, d=d, method=kw.get("method", "legendre"))
-    keys = ("T0", "load", "T_in", "T_upper", "s_T", "r_mDot", "u_prev")
+    prob = nlps.one_room(N=N, d=d, method=kw.get("method", "legendre"), delta_u="r_delta_mDot" in kw)
+    keys = ("T0", "load", "T_in", "T_upper", "s_T", "r_mDot", "u_prev", "r_delta_mDot")
     return Case(be, cv, prob, nlps.one_room_inputs(prob, N=N, d=d, **{k: kw[k] for k in keys if k in kw}))
 
 
@@ -114,6 +114,11 @@ def one_room_radau(**kw) -> Case:
     return one_room(d=3, method="radau", **kw)
 
 
+def one_room_du(**kw) -> Case:
+    kw.setdefault("r_delta_mDot", 0.1)
+    return one_room(**kw)
+
+
 def exchange_room_rk(**kw) -> Case:
     return exchange_room(integrator="rk", **kw)
 
@@ -129,6 +134,7 @@ CASES: Dict[str, Callable[..., Case]] = {
     "tz_cca": tz_cca,
     "exchange_room_rk": exchange_room_rk,
     "one_room_radau": one_room_radau,
+    "one_room_du": one_room_du,
 }
 
 

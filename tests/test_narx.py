@@ -74,9 +74,12 @@ def test_network_node_derivatives_match_expanded_graph():
     np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-12)
 
 
-def test_lifted_stage_nlp_reproduces_reference_nlp():
-    """Kernel stage form (lag-window copies + shift constraints) == reference NLP."""
-    case = configs.room_nn()
+@pytest.mark.parametrize("name,kw", [("room_nn", {}), ("room_nn", {"N": 23}), ("one_room_du", {})])
+def test_lifted_stage_nlp_reproduces_reference_nlp(name, kw):
+    """Kernel stage form == reference NLP: NARX super-stages (N=24), NARX copy-lifting
+    (N=23, lag-window copies + shift constraints) and carried previous controls of
+    change penalties (copy of u_{k-1} in the stage state, X_0[u] = u_prev)."""
+    case = configs.CASES[name](**kw)
     prob = case.backend.problem
     nlp, lift, st = prob.nlp, prob.nlp.lift, prob.nlp.stage
     (p, lbw, ubw, w0), _ = configs.product_nlp_inputs(case)

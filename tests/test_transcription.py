@@ -24,6 +24,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "tz_cca": (240, 144, 318),
     "exchange_room_rk": (31, 20, 71),  # C4 room with the "rk" integrator (20 RK4 steps)
     "one_room_radau": (1 + 15 * (1 + 3 * 3 + 1), 15 * (1 + 3 * 3), None),  # Radau IIA, d=3
+    "one_room_du": (121, 105, 97),  # C1 + change penalty (one more model parameter)
 }
 
 

@@ -285,9 +285,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        # BENCH_DIST_BACKEND=gloo + ranks sharing a device: rehearsal of the N>1 path on
+        # a one-GPU box (the driver's multi-GPU runs use nccl = RCCL, one GPU per rank)
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        gpu = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
 
     from agentlib_mpc_amd import benchmarks as bm
     from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs

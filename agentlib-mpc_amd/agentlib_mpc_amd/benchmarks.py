@@ -149,6 +149,30 @@ def exchange_supply(N=10, rho=1e4, diff=0.0, lam=0.0, penalty=0.1, solver_option
     return be, cv
 
 
+def one_room_switch(N=15, T0=298.16, load=150.0, T_in=290.15, T_upper=295.15, u_prev=0.02, s_T=3.0,
+                    r_mDot=1.0, r_mDot2=5.0, switch=600.0, integrator="euler", solver_options=TIGHT):
+    """`examples/one_room_mpc/physical/simple_mpc_time_dependent_obj.py` (conditional
+    objective switching at ``switch`` seconds), backend "casadi", multiple shooting
+    (the example keeps the cvodes default; Euler / "rk" here)."""
+    be = create_optimization_backend({
+        "type": "mi355x",
+        "model": {"type": "agentlib_mpc_amd.models.examples.SwitchRoom"},
+        "discretization_options": {"method": "multiple_shooting", "integrator": integrator,
+                                   "prediction_horizon": N, "time_step": 300},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    be.setup_optimization(VariableReference(
+        states=["T"], controls=["mDot"], inputs=["T_in", "load", "T_upper"],
+        parameters=["s_T", "r_mDot", "r_mDot2", "switch"], outputs=["T_out", "switch_test"]))
+    cv = {
+        "T": V("T", T0, 288.15, 303.15), "mDot": V("mDot", u_prev, 0.0, 0.05),
+        "T_in": V("T_in", T_in), "load": V("load", load), "T_upper": V("T_upper", T_upper),
+        "s_T": V("s_T", s_T), "r_mDot": V("r_mDot", r_mDot), "r_mDot2": V("r_mDot2", r_mDot2),
+        "switch": V("switch", switch), "T_out": V("T_out"), "switch_test": V("switch_test"),
+    }
+    return be, cv
+
+
 ROOM_NN_COUPLINGS = (("T_v", 294.15, 285.0, 308.0), ("T_ahu", 295.0, 285.0, 308.0),
                      ("T_CCA_out", 294.15, 285.0, 310.0), ("T_air_out", 294.0, 285.0, 310.0))
 
@@ -281,6 +305,7 @@ def compile_all(verbose: bool = False):
     variants["exchange_room_rk"] = lambda: exchange_room(integrator="rk")
     variants["one_room_radau3"] = lambda: one_room(d=3, method="radau")
     variants["one_room_du"] = lambda: one_room(r_delta_mDot=0.1)
+    variants["one_room_switch"] = lambda: one_room_switch()
     variants["room_nn_n8"] = lambda: room_nn(N=8)      # C5 ADMM fixture (tests/golden/c5_admm_N8.json)
     variants["tz_ahu_n8"] = lambda: tz_ahu(N=8)
     variants["tz_cca_n8"] = lambda: tz_cca(N=8)

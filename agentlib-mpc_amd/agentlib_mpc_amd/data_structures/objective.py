@@ -140,3 +140,44 @@ class CombinedObjective:
         for obj in self.objectives:
             total = sx.add(total, obj.get_weighted_expression())
         return sx.div(total, self.normalization)
+
+
+class ConditionalObjective:
+    """Switches between objectives by conditions (`objective.py:456-499`):
+    ``if_else(c_1, o_1, if_else(c_2, o_2, ... default))``; the conditions are
+    expressions of the model variables (non-differentiable switches, as in CasADi)."""
+
+    def __init__(self, *condition_objective_pairs, default_objective=None):
+        self.condition_objective_pairs = condition_objective_pairs
+        self.default_objective = default_objective or CombinedObjective()
+        self.all_objectives = [self.default_objective]
+        for _, objective in condition_objective_pairs:
+            if objective not in self.all_objectives:
+                self.all_objectives.append(objective)
+        self._flattened_objectives = []
+        for obj in self.all_objectives:
+            if hasattr(obj, "objectives"):
+                self._flattened_objectives.extend(obj.objectives)
+
+    @property
+    def objectives(self):
+        return self._flattened_objectives
+
+    @property
+    def normalization(self):
+        return 1.0
+
+    def get_casadi_expression(self):
+        result = self.default_objective.get_casadi_expression()
+        for condition, objective in reversed(self.condition_objective_pairs):
+            cond = condition.sym if hasattr(condition, "sym") else condition
+            result = sx.if_else(sx.as_expr(cond), objective.get_casadi_expression(), result)
+        return result
+
+    def get_delta_u_objectives(self):
+        out = []
+        for objective in self.all_objectives:
+            for d in objective.get_delta_u_objectives():
+                if d not in out:
+                    out.append(d)
+        return out

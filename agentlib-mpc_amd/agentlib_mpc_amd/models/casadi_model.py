@@ -445,3 +445,9 @@ class CasadiModel:
         from agentlib_mpc_amd.data_structures.objective import CombinedObjective
 
         return CombinedObjective(*objectives, normalization=normalization)
+
+    def create_conditional_objective(self, *condition_objective_pairs, default_objective=None):
+        """`casadi_model.py:549-557`."""
+        from agentlib_mpc_amd.data_structures.objective import ConditionalObjective
+
+        return ConditionalObjective(*condition_objective_pairs, default_objective=default_objective)

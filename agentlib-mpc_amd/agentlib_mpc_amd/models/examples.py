@@ -80,6 +80,39 @@ class OneRoomDU(CasadiModel):
         return self.create_combined_objective(obj1, obj2, obj3 * self.r_delta_mDot, normalization=1)
 
 
+class SwitchRoomConfig(OneRoomConfig):
+    parameters: List[CasadiParameter] = [
+        _par("cp", 1000), _par("C", 100000), _par("s_T", 1), _par("r_mDot", 1), _par("r_mDot2", 1),
+        _par("switch", 600, unit="s"),
+    ]
+    outputs: List[CasadiOutput] = [CasadiOutput(name="T_out", unit="K"), CasadiOutput(name="switch_test", unit="-")]
+
+
+class SwitchRoom(CasadiModel):
+    """`examples/one_room_mpc/physical/simple_mpc_time_dependent_obj.py:108-165`:
+    the one-room model with a time-dependent (conditional) objective."""
+
+    config: SwitchRoomConfig
+
+    def setup_system(self):
+        from agentlib_mpc_amd.models.casadi_model import ca
+
+        self.T.ode = self.cp * self.mDot / self.C * (self.T_in - self.T) + self.load / self.C
+        self.T_out.alg = self.T
+        self.constraints = [(0, self.T + self.T_slack, self.T_upper)]
+        obj1_mDot = self.create_sub_objective(expressions=self.mDot, weight=self.r_mDot, name="mDot_cost_normal")
+        obj1_slack = self.create_sub_objective(expressions=self.T_slack ** 2, weight=self.s_T,
+                                               name="temperature_slack")
+        objective1 = self.create_combined_objective(obj1_mDot, obj1_slack, normalization=10)
+        obj2_mDot = self.create_sub_objective(expressions=self.mDot, weight=self.r_mDot2, name="mDot_cost_doubled")
+        obj2_slack = self.create_sub_objective(expressions=self.T_slack ** 2, name="temperature_slack_2")
+        objective2 = self.create_combined_objective(obj2_mDot) + self.create_combined_objective(obj2_slack) * self.s_T
+        condition = self.time < self.switch.sym
+        objective = self.create_conditional_objective((condition, objective1), default_objective=objective2)
+        self.switch_test.alg = ca.if_else(self.time < self.switch.sym, 1, 2)
+        return objective
+
+
 class CooledRoomConfig(CasadiModelConfig):
     inputs: List[CasadiInput] = [
         _inp("mDot", 0.0225), _inp("d", 150), _inp("T_in", 290.15),

@@ -163,6 +163,8 @@ class StageNLP:
     gap_closing: List[bool]
     #: index maps to the kernel's lifted stage NLP (NARX transcriptions), else None
     lift: Optional[object] = None
+    #: symbols of the stage start times in the reference expressions (value tk_values[k])
+    tk_syms: Optional[Dict[int, sx.Expr]] = None
 
     @property
     def nw(self) -> int:
@@ -403,7 +405,7 @@ class _Transcriber:
         for k in range(N):
             f_total = sx.add(f_total, self.cost.get(k, sx.ZERO))
         return StageNLP(
-            lift=lift,
+            lift=lift, tk_syms=dict(self.tk_syms),
             N=N, nx=nx + nc, nv=nv, ng=ng + nc, nps=nps, npg=npg, ts=float(opts.time_step),
             w_syms=list(self.w), p_syms=list(self.p), w_labels=list(self.w_labels),
             p_labels=list(self.p_labels), g_exprs=[c[0] for c in self.g],

@@ -207,6 +207,12 @@ class ADMMSystem(FullSystem):
             lam = self.exchange_multipliers.full_symbolic[i]
             terms.append(lam * x_loc)
             terms.append(rho / 2 * (diff - x_loc) ** 2)
+        from agentlib_mpc_amd.data_structures.objective import ConditionalObjective
+
+        if isinstance(self.objective, ConditionalObjective):
+            # the reference's in-place append (`admm.py:90-116`) fails on the read-only
+            # ``objectives`` property of a ConditionalObjective as well
+            raise NotImplementedError("ADMM terms cannot be added to a ConditionalObjective")
         # the reference appends to the model's objective list in place
         self.objective = CombinedObjective(
             *self.objective.objectives,

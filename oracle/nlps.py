@@ -725,3 +725,69 @@ def tz_supply_inputs(prob, N=24, rho=1.0, zbar=None, lam=None, mDot_0=None, T_am
         else:
             lbw[i], ubw[i], w0[i] = -np.inf, np.inf, 0.0
     return p, lbw, ubw, w0
+
+
+# ---------------------------------------------------------------------------
+# one room with a time-dependent (conditional) objective, backend "casadi",
+# multiple shooting with Euler (`simple_mpc_time_dependent_obj.py:108-165`,
+# `casadi_/full.py:101-166`, `objective.py:456-492`)
+# ---------------------------------------------------------------------------
+
+def one_room_switch(N=15, ts=300.0) -> OracleProblem:
+    """w = [T0, {mDot_k, T_slack_k, T_out_k, switch_test_k, T_{k+1}}];
+    g_k = [continuity, T + T_slack (<= T_upper), T_out - T, switch_test - (t_k < switch ? 1 : 2)];
+    p = [T0, u_prev, cp, C, s_T, r_mDot, r_mDot2, switch, {T_in, load, T_upper}_k];
+    stage cost (x ts): t_k < switch ? (r_mDot u + s_T slack^2) / 10 : r_mDot2 u + s_T slack^2."""
+    nb = 5
+    n = 1 + N * nb
+    m = 4 * N
+    npg, nps = 8, 3
+    names = ["T@0"]
+    for k in range(N):
+        names += [f"mDot@{k}", f"T_slack@{k}", f"T_out@{k}", f"switch_test@{k}", f"T@{k + 1}"]
+
+    def f(w, p):
+        s_T, r1, r2, sw = p[4], p[5], p[6], p[7]
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = 1 + k * nb
+            u, sl = w[o], w[o + 1]
+            c = (r1 * u + s_T * sl ** 2) / 10 if k * ts < float(sw) else r2 * u + s_T * sl ** 2
+            tot = tot + c * ts
+        return tot
+
+    def g(w, p):
+        cp, Cz, sw = p[2], p[3], p[7]
+        out = []
+        for k in range(N):
+            o = 1 + k * nb
+            T = w[o - 1]
+            u, sl, To, st, T1 = w[o], w[o + 1], w[o + 2], w[o + 3], w[o + 4]
+            ps = npg + k * nps
+            T_in, load = p[ps], p[ps + 1]
+            ode = cp * u / Cz * (T_in - T) + load / Cz
+            out += [T1 - (T + ode * ts), T + sl, To - T, st - (1.0 if k * ts < float(sw) else 2.0)]
+        return torch.stack([torch.as_tensor(v) for v in out])
+
+    def ubg(p):
+        u = np.zeros(m)
+        for k in range(N):
+            u[4 * k + 1] = p[npg + k * nps + 2]
+        return u
+
+    return OracleProblem("one_room_switch", n, m, npg + N * nps, f, g, lambda p: np.zeros(m), ubg, names)
+
+
+def one_room_switch_inputs(prob, N=15, T0=298.16, load=150.0, T_in=290.15, T_upper=295.15, u_prev=0.02,
+                           s_T=3.0, r_mDot=1.0, r_mDot2=5.0, switch=600.0):
+    p = [T0, u_prev, 1000.0, 100000.0, s_T, r_mDot, r_mDot2, switch] + [T_in, load, T_upper] * N
+    p = np.array(p, float)
+    lbw, ubw, w0 = np.full(prob.n, -np.inf), np.full(prob.n, np.inf), np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        v = name.split("@")[0]
+        if v == "T":
+            lbw[i], ubw[i], w0[i] = 288.15, 303.15, T0
+        elif v == "mDot":
+            lbw[i], ubw[i], w0[i] = 0.0, 0.05, 0.025
+    lbw[0] = ubw[0] = w0[0] = T0
+    return p, lbw, ubw, w0

@@ -123,6 +123,14 @@ def exchange_room_rk(**kw) -> Case:
     return exchange_room(integrator="rk", **kw)
 
 
+def one_room_switch(**kw) -> Case:
+    be, cv = bm.one_room_switch(**kw)
+    N = kw.get("N", 15)
+    prob = nlps.one_room_switch(N=N)
+    keys = ("T0", "load", "T_in", "T_upper", "u_prev", "s_T", "r_mDot", "r_mDot2", "switch")
+    return Case(be, cv, prob, nlps.one_room_switch_inputs(prob, N=N, **{k: kw[k] for k in keys if k in kw}))
+
+
 CASES: Dict[str, Callable[..., Case]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -135,6 +143,7 @@ CASES: Dict[str, Callable[..., Case]] = {
     "exchange_room_rk": exchange_room_rk,
     "one_room_radau": one_room_radau,
     "one_room_du": one_room_du,
+    "one_room_switch": one_room_switch,
 }
 
 

@@ -56,6 +56,8 @@ def _cuda():
     ("one_room_radau", {}),            # Radau IIA collocation, d=3
     ("one_room_du", {}),               # change penalty (carried u_{k-1})
     ("one_room_du", {"r_delta_mDot": 1.0, "T0": 292.0, "load": 250.0}),
+    ("one_room_switch", {}),           # conditional (time-dependent) objective
+    ("one_room_switch", {"switch": 1800.0, "r_mDot2": 20.0}),
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)

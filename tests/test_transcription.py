@@ -25,6 +25,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "exchange_room_rk": (31, 20, 71),  # C4 room with the "rk" integrator (20 RK4 steps)
     "one_room_radau": (1 + 15 * (1 + 3 * 3 + 1), 15 * (1 + 3 * 3), None),  # Radau IIA, d=3
     "one_room_du": (121, 105, 97),  # C1 + change penalty (one more model parameter)
+    "one_room_switch": (76, 60, 53),  # time-dependent conditional objective, MS Euler
 }
 
 
@@ -56,6 +57,7 @@ def test_functions_match_oracle(name):
         pp = p * (1 + 0.1 * rng.normal(size=p.shape))
         vals = {s: v for s, v in zip(nlp.w_syms, w)}
         vals.update({s: v for s, v in zip(nlp.p_syms, pp)})
+        vals.update({s: nlp.tk_values[k] for k, s in (nlp.tk_syms or {}).items()})
         f, *g = sx.evaluate([nlp.f_expr] + nlp.g_exprs, vals)
         lb = sx.evaluate(nlp.g_lb, vals) if nlp.g_lb else []
         ub = sx.evaluate(nlp.g_ub, vals) if nlp.g_ub else []

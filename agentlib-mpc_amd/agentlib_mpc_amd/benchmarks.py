@@ -6,6 +6,7 @@
 * ``exchange_room``   C4 room agent — `examples/exchange_admm/configs/room_1_admm.json`
 * ``exchange_supply`` C4 supply agent — `examples/exchange_admm/configs/rlt_admm.json`
 * ``room_nn``         C5 zone agent (NARX ANNs) — `examples/three_zone_datadriven_admm/configs/mpc/Room_1.json`
+* ``mhe_room``        moving horizon estimator — `examples/Estimators/mhe_example.py:188-228`
 
 Each builder returns ``(backend, current_vars)`` with the example's values;
 keyword arguments override the per-agent values used for synthetic fleets.
@@ -173,6 +174,83 @@ def one_room_switch(N=15, T0=298.16, load=150.0, T_in=290.15, T_upper=295.15, u_
     return be, cv
 
 
+MHE_KNOWN_INPUTS = {"mDot": 0.22, "load": 0.0, "T_in": 17.0, "T_ambient": 28.0, "T_upper": 22.0}
+
+
+def mhe_measurements(N=15, ts=200.0, d=2, theta=5.5, T0=25.0, T_wall0=27.0, noise=0.0, seed=0,
+                     inputs=None):
+    """Synthetic measurements of the estimator example: the RNGRoom model
+    (`examples/Estimators/mhe_example.py:142-170`) simulated with the true
+    capacity factor ``theta`` (RK4, 50 steps per interval), sampled at the
+    collocation times of the past horizon ``[-N ts, 0]``.  Returns
+    ``(measured T, measured T_wall)`` on the collocation grid (N*d points)."""
+    from agentlib_mpc_amd.optimization_backends.discretization import collocation_polynomial
+
+    u = dict(MHE_KNOWN_INPUTS, **(inputs or {}))
+    cp, rho, Cw, Rzw, Rha, Vz = 1005.0, 1.2, 4_569_348.0, 0.0129, 0.1128, 59.0
+
+    def f(x):
+        T, Tw = x
+        pw = (Tw - T) / Rzw
+        dT = (u["load"] + cp * u["mDot"] * (u["T_in"] - T) + pw) / (rho * cp * Vz * theta)
+        return np.array([dT, -((Tw - u["T_ambient"]) / Rha + pw) / Cw])
+
+    def advance(x, dt, steps=50):
+        h = dt / steps
+        for _ in range(steps):
+            k1 = f(x); k2 = f(x + h / 2 * k1); k3 = f(x + h / 2 * k2); k4 = f(x + h * k3)
+            x = x + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+        return x
+
+    roots = collocation_polynomial(d, "legendre").root[1:]
+    x = np.array([T0, T_wall0], float)
+    out = []
+    for k in range(N):
+        for r in roots:
+            out.append(advance(x, r * ts))
+        x = advance(x, ts)
+    meas = np.array(out).T
+    if noise:
+        meas = meas + np.random.default_rng(seed).normal(scale=noise, size=meas.shape)
+    return meas[0], meas[1]
+
+
+def mhe_room(N=15, ts=200.0, d=2, theta_lb=5.0, theta_ub=6.0, theta_guess=None, w_T=1.0, w_T_wall=0.0,
+             measured=None, inputs=None, model="RNGRoomMHE", solver_options=TIGHT):
+    """`examples/Estimators/mhe_example.py:188-228`: backend ``casadi_mhe`` on the
+    RNGRoom model, estimating ``full_capacity_from_volume_factor`` (bounds 5..6)
+    from zone temperature measurements (state weights T: 1, T_wall: 0).  The
+    default model bounds the (cost-free) slack, see :class:`examples.RNGRoomMHE`."""
+    from agentlib_mpc_amd.data_structures.mpc_datamodels import MHEVariableReference
+
+    be = create_optimization_backend({
+        "type": "casadi_mhe",
+        "model": {"type": f"agentlib_mpc_amd.models.examples.{model}"},
+        "discretization_options": {"collocation_order": d, "collocation_method": "legendre",
+                                   "prediction_horizon": N, "time_step": ts},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    known = list(MHE_KNOWN_INPUTS)
+    be.setup_optimization(MHEVariableReference(
+        states=["T", "T_wall"], measured_states=["measured_T", "measured_T_wall"],
+        weights_states=["weight_T", "weight_T_wall"], estimated_inputs=[],
+        estimated_parameters=["full_capacity_from_volume_factor"], known_inputs=known,
+        known_parameters=[], outputs=[]))
+    if measured is None:
+        measured = mhe_measurements(N=N, ts=ts, d=d)
+    u = dict(MHE_KNOWN_INPUTS, **(inputs or {}))
+    th = 0.5 * (theta_lb + theta_ub) if theta_guess is None else theta_guess
+    cv = {
+        "T": V("T", 25.0), "T_wall": V("T_wall", 27.0),
+        "full_capacity_from_volume_factor": V("full_capacity_from_volume_factor", th, theta_lb, theta_ub),
+        "measured_T": V("measured_T", [float(v) for v in measured[0]]),
+        "measured_T_wall": V("measured_T_wall", [float(v) for v in measured[1]]),
+        "weight_T": V("weight_T", w_T), "weight_T_wall": V("weight_T_wall", w_T_wall),
+    }
+    cv.update({n: V(n, u[n]) for n in known})
+    return be, cv
+
+
 ROOM_NN_COUPLINGS = (("T_v", 294.15, 285.0, 308.0), ("T_ahu", 295.0, 285.0, 308.0),
                      ("T_CCA_out", 294.15, 285.0, 310.0), ("T_air_out", 294.0, 285.0, 310.0))
 
@@ -309,6 +387,7 @@ def compile_all(verbose: bool = False):
     variants["room_nn_n8"] = lambda: room_nn(N=8)      # C5 ADMM fixture (tests/golden/c5_admm_N8.json)
     variants["tz_ahu_n8"] = lambda: tz_ahu(N=8)
     variants["tz_cca_n8"] = lambda: tz_cca(N=8)
+    variants["mhe_room"] = lambda: mhe_room()
     for name, fn in variants.items():
         be, _ = fn()
         paths[name] = be.problem.compile()

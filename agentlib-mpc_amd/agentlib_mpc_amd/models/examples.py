@@ -8,6 +8,7 @@ Equations restate the reference examples:
 * ``ExchangeRoom`` — `examples/exchange_admm/models/room_model.py` (C4)
 * ``ExchangeSupply`` — `examples/exchange_admm/models/rlt_model.py` (C4)
 * ``RoomCCA``      — `examples/three_zone_datadriven_admm/models/Room_model.py` (C5, NARX)
+* ``RNGRoom``      — `examples/Estimators/mhe_example.py:21-170` (moving horizon estimation)
 """
 
 from __future__ import annotations
@@ -357,3 +358,61 @@ class TempController(CasadiModel):
         self.constraints = []
         return sum(0.1 * 0.001 * self.r_T_v * ((self.cp * self.mDot_0 * (self.T_v - t_r)) ** 2 + 0.02) ** 0.5
                    for t_r in (self.T_r1, self.T_r2, self.T_r3))
+
+
+class RNGRoomConfig(CasadiModelConfig):
+    inputs: List[CasadiInput] = [
+        _inp("mDot", 0.22, unit="kg/s"), _inp("load", 150, unit="W"), _inp("T_in", 290.15, unit="K"),
+        _inp("T_ambient", 28, unit="K"), _inp("T_upper", 22, unit="K"),
+    ]
+    states: List[CasadiState] = [
+        CasadiState(name="T", value=22, unit="K"),
+        CasadiState(name="T_wall", value=23, unit="K"),
+        CasadiState(name="T_slack", value=0, unit="K"),  # no ode -> auxiliary
+    ]
+    parameters: List[CasadiParameter] = [
+        _par("cp", 1005), _par("rho", 1.2), _par("full_capacity_from_volume_factor", 5.5),
+        _par("C_Wall", 4_569_348), _par("RZone_Wall", 0.0129), _par("R_hull_amb", 0.1128),
+        _par("V", 59), _par("s_T", 1), _par("r_mDot", 1),
+    ]
+    outputs: List[CasadiOutput] = [
+        CasadiOutput(name="T_out", unit="K"), CasadiOutput(name="cooling"), CasadiOutput(name="power_wall2zone"),
+    ]
+
+
+class RNGRoom(CasadiModel):
+    """`examples/Estimators/mhe_example.py:21-170`: zone + wall model whose
+    capacity factor the moving horizon estimator identifies."""
+
+    config: RNGRoomConfig
+
+    def setup_system(self):
+        power_wall2zone = (self.T_wall - self.T) / self.RZone_Wall
+        air_cooling = self.cp * self.mDot * (self.T_in - self.T)
+        C_zone = self.rho * self.cp * self.V * self.full_capacity_from_volume_factor
+        self.T.ode = (self.load + air_cooling + power_wall2zone) / C_zone
+        power_wall2amb = (self.T_wall - self.T_ambient) / self.R_hull_amb
+        self.T_wall.ode = -(power_wall2amb + power_wall2zone) / self.C_Wall
+        self.T_out.alg = self.T
+        self.cooling.alg = air_cooling
+        self.power_wall2zone.alg = power_wall2zone
+        self.constraints = [(0, self.T + self.T_slack, self.T_upper)]
+        return sum([self.r_mDot * self.mDot, self.s_T * self.T_slack ** 2])
+
+
+class RNGRoomMHEConfig(RNGRoomConfig):
+    states: List[CasadiState] = [
+        CasadiState(name="T", value=22, unit="K"),
+        CasadiState(name="T_wall", value=23, unit="K"),
+        CasadiState(name="T_slack", value=0, unit="K", lb=-50),
+    ]
+
+
+class RNGRoomMHE(RNGRoom):
+    """``RNGRoom`` with the soft-constraint slack bounded below.  In the estimator
+    the slack has no cost, so with the example's unbounded slack every value below
+    ``T_upper - T`` is optimal and the solver returns an arbitrary point of that
+    ray; with a finite lower bound the barrier problems have a unique solution
+    (the middle of the feasible interval) that two interior-point solvers agree on."""
+
+    config: RNGRoomMHEConfig

@@ -23,6 +23,7 @@ class BackendImport(BaseModel):
 
 
 _MOD = "agentlib_mpc_amd.optimization_backends.mi355x"
+_MHE = "agentlib_mpc_amd.optimization_backends.mhe"
 
 backend_types = {
     "mi355x": BackendImport(import_path=_MOD, class_name="MI355XBackend"),
@@ -30,6 +31,7 @@ backend_types = {
     "mi355x_admm": BackendImport(import_path=_MOD, class_name="MI355XADMMBackend"),
     "mi355x_ml": BackendImport(import_path=_MOD, class_name="MI355XMLBackend"),
     "mi355x_admm_ml": BackendImport(import_path=_MOD, class_name="MI355XADMMNNBackend"),
+    "mi355x_mhe": BackendImport(import_path=_MHE, class_name="MHEBackend"),
     # drop-in aliases of the reference keys this backend replaces
     "casadi": BackendImport(import_path=_MOD, class_name="MI355XBackend"),
     "casadi_basic": BackendImport(import_path=_MOD, class_name="MI355XBaseBackend"),
@@ -38,6 +40,7 @@ backend_types = {
     "casadi_nn": BackendImport(import_path=_MOD, class_name="MI355XMLBackend"),
     "casadi_admm_ml": BackendImport(import_path=_MOD, class_name="MI355XADMMNNBackend"),
     "casadi_admm_nn": BackendImport(import_path=_MOD, class_name="MI355XADMMNNBackend"),
+    "casadi_mhe": BackendImport(import_path=_MHE, class_name="MHEBackend"),
 }
 
 uninstalled_backend_types = {}

@@ -205,6 +205,8 @@ class _Transcriber:
     def __init__(self, options: CasadiDiscretizationOptions):
         self.options = options
         self.pred_time = 0.0
+        #: time of stage 0's start (0 for MPC; -N*ts for the MHE's past horizon)
+        self.t_start = 0.0
         self.k = 0
         self.block = -1
         self.w: List[sx.Expr] = []
@@ -227,7 +229,7 @@ class _Transcriber:
         if self.block < 0:
             return sx.const(self.pred_time)
         tk = self.tk_syms.setdefault(self.block, sx.sym(f"__tk_{self.block}"))
-        return sx.add(tk, sx.const(self.pred_time - self.block * self.options.time_step))
+        return sx.add(tk, sx.const(self.pred_time - self.t_start - self.block * self.options.time_step))
 
     def add_opt_var(self, q: OptimizationVariable, lb=None, ub=None, guess=None) -> List[sx.Expr]:
         lay = self.var_groups.setdefault(q.name, GroupLayout(q.name, True, q.dim))

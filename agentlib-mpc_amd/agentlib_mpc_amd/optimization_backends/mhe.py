@@ -1,0 +1,285 @@
+"""Moving horizon estimation backend (``casadi_mhe`` replacement).
+
+Restates `optimization_backends/casadi_/mhe.py`:
+
+* ``MHESystem`` (:34-124) — variable groups ``states`` (x), ``estimated_inputs``,
+  ``estimated_parameters`` (one value over the whole horizon), ``algebraics``
+  (z), ``outputs`` (y); parameter groups ``known_inputs``, ``known_parameters``,
+  ``measured_states``, ``weight_states``; objective
+  ``Σ_i weight_i · (x_i − x_meas_i)²`` (the model's own objective is not used).
+* ``DirectCollocation._discretize`` (:138-196) / ``_collocation_inner_loop``
+  (:272-361) — the horizon runs over the PAST, ``t ∈ [−N·ts, 0]``; ``x_0`` and the
+  estimated parameters are free variables; per interval ``[u_est_k, {x_kj, y_kj,
+  z_kj}_j, x_{k+1}]``; constraints ``{ts·ode_kj − Σ_r C[r,j]·x_kr, path_kj}_j``
+  then the continuity ``x_end − x_{k+1}`` (added LAST, with this sign).
+* ``only_positive_times_in_results = False`` (:136): result columns hold the past.
+
+The reference layout is kept bit for bit (``w``/``p``/``g`` order, result matrix).
+For the kernel, whose stage form fixes ``X_0`` and has no horizon-global
+variables, the NLP is lifted (maps in :class:`~.narx.LiftMaps`):
+
+* kernel stage state ``X_k = [x_k, θ_k]`` (θ = estimated parameters), with
+  ``X_0`` a dummy fixed to 0;
+* kernel stage variables ``V_k = [ξ_k, ϑ_k, reference stage variables]``: the
+  interval start state and parameter copy read by the stage;
+* link constraints ``ξ_k − x_k``, ``ϑ_k − θ_k`` whose bounds are ``0`` for
+  ``k ≥ 1`` and ``[−1e8, 1e8]`` for ``k = 0`` (an open row: ``ξ_0`` IS the free
+  reference ``x_0``, ``ϑ_0`` the reference θ; with ``X_0 = 0`` the row only
+  bounds ``|x_0|, |θ| ≤ 1e8``, never active for physical values), and the shift
+  ``θ_{k+1} − ϑ_k = 0``.
+
+At any feasible point the lifted and the reference NLP have the same objective
+and the same reference-variable values; ``ξ_k, ϑ_k (k ≥ 1)`` and ``θ_k`` are copies.
+(Rows with two infinite bounds instead of ±1e8 stall the iteration — in the
+kernel and in the oracle IPM alike — so the open rows use finite bounds.)
+
+``MHEBackend.sample`` (:426-542) is not restated: the reference backend samples
+through ``utils.sampling.sample`` (`core/casadi_backend.py:177-240`), so that
+override is never called.  Known-parameter order: the reference builds it from a
+``set`` difference (`mhe.py:86-94`), i.e. in hash order; here it is the model's
+declaration order.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+
+from agentlib_mpc_amd import symbolic as sx
+from agentlib_mpc_amd.data_structures.mpc_datamodels import (
+    DiscretizationMethod, MHEVariableReference,
+)
+from agentlib_mpc_amd.data_structures.objective import CombinedObjective, SubObjective
+from agentlib_mpc_amd.models.casadi_model import CasadiInput, CasadiModel
+from agentlib_mpc_amd.optimization_backends import discretization as disc
+from agentlib_mpc_amd.optimization_backends.discretization import (
+    StageFunction, StageNLP, TranscriptionError, _Transcriber, collocation_polynomial,
+)
+from agentlib_mpc_amd.optimization_backends.system import (
+    OptimizationParameter, OptimizationVariable, System,
+)
+
+#: bounds of the stage-0 link rows: finite and far outside any physical state or
+#: parameter value, so they never become active (rows with two infinite bounds
+#: stall the IPOPT-style iteration: the free slack's dual block degenerates)
+_OPEN = 1e8
+
+
+class MHESystem(System):
+    """`casadi_/mhe.py:34-124`."""
+
+    def initialize(self, model: CasadiModel, var_ref: MHEVariableReference):
+        self.states = OptimizationVariable.declare(
+            "states", model.get_states(var_ref.states), var_ref.states, assert_complete=True)
+        self.estimated_inputs = OptimizationVariable.declare(
+            "estimated_inputs", model.get_inputs(var_ref.estimated_inputs), var_ref.estimated_inputs,
+            assert_complete=True)
+        self.estimated_parameters = OptimizationVariable.declare(
+            "estimated_parameters", model.get_parameters(var_ref.estimated_parameters),
+            var_ref.estimated_parameters)
+        self.algebraics = OptimizationVariable.declare("algebraics", model.auxiliaries, [])
+        self.outputs = OptimizationVariable.declare("outputs", model.outputs, var_ref.outputs)
+        self.known_inputs = OptimizationParameter.declare(
+            "known_inputs", model.get_inputs(var_ref.known_inputs), var_ref.known_inputs,
+            assert_complete=True)
+        known = [p for p in model.parameters if p.name not in set(var_ref.estimated_parameters)]
+        self.known_parameters = OptimizationParameter.declare(
+            "known_parameters", known, var_ref.known_parameters)
+        self.measured_states = OptimizationParameter.declare(
+            "measured_states", [CasadiInput(name=n) for n in var_ref.measured_states],
+            var_ref.measured_states)
+        self.weights_states = OptimizationParameter.declare(
+            "weight_states", [CasadiInput(name=n) for n in var_ref.weights_states],
+            var_ref.weights_states)
+
+        objective = sx.ZERO
+        for i in range(len(var_ref.states)):
+            x = self.states.full_symbolic[i]
+            meas = self.measured_states.full_symbolic[i]
+            w = self.weights_states.full_symbolic[i]
+            objective = sx.add(objective, sx.mul(w, sx.power(sx.sub(x, meas), 2)))
+        states = model.get_states(var_ref.states)
+        missing_ode = [s.name for s in states if s.ode is None]
+        if missing_ode:
+            raise ValueError(f"States {missing_ode} are declared as MHE states but have no ode.")
+        self.ode = [s.ode for s in states]
+        self.objective = CombinedObjective(SubObjective(objective, name="mhe_state_deviation"),
+                                           normalization=1)
+        self.model_constraints = model.get_constraints()
+        self.time = model.time
+
+
+class MHECollocation(disc.Discretization):
+    """`casadi_/mhe.py:135-196` (direct collocation over the past horizon)."""
+
+    system_type = MHESystem
+
+    def transcribe(self, system: MHESystem) -> StageNLP:
+        t = _Transcriber(self.options)
+        n, ts = int(self.options.prediction_horizon), float(self.options.time_step)
+        t.t_start = -n * ts
+        self._discretize(t, system)
+        return _lift_mhe(t, system)
+
+    def _discretize(self, t: _Transcriber, s: MHESystem):
+        cm = collocation_polynomial(self.options.collocation_order, self.options.collocation_method)
+        n, ts = int(self.options.prediction_horizon), float(self.options.time_step)
+        start = -n * ts
+        t.pred_time = start
+        xk = t.add_opt_var(s.states)
+        known_pars = t.add_opt_par(s.known_parameters)
+        est_pars = t.add_opt_var(s.estimated_parameters)
+        weights = t.add_opt_par(s.weights_states)
+        for k in range(n):
+            t.block = k
+            inp_known = t.add_opt_par(s.known_inputs)
+            inp_est = t.add_opt_var(s.estimated_inputs)
+            const = {s.known_inputs.name: inp_known, s.estimated_inputs.name: inp_est,
+                     s.estimated_parameters.name: est_pars, s.known_parameters.name: known_pars,
+                     s.weights_states.name: weights}
+            x_end, cons = self._collocation_inner_loop(
+                t, s, cm, xk, [s.outputs, s.algebraics], [s.measured_states], const)
+            for c in cons:
+                t.add_constraint(*c)
+            t.pred_time = start + ts * (k + 1)
+            xk = t.add_opt_var(s.states)
+            t.add_constraint([sx.sub(a, b) for a, b in zip(x_end, xk)])
+
+
+def _lift_mhe(t: _Transcriber, system: MHESystem) -> StageNLP:
+    """Reference-layout MHE transcription -> kernel stage NLP (module docstring)."""
+    from agentlib_mpc_amd.optimization_backends.narx import LiftMaps
+
+    opts = t.options
+    N, ts = int(opts.prediction_horizon), float(opts.time_step)
+    nx, nth = system.states.dim, system.estimated_parameters.dim
+    blocks: Dict[int, List[int]] = {}
+    for i, b in enumerate(t.w_block):
+        blocks.setdefault(b, []).append(i)
+    init = blocks.get(-1, [])
+    if len(init) != nx + nth:
+        raise TranscriptionError("MHE initial block must hold the initial state and the estimated parameters")
+    x0_ref, th_ref = init[:nx], init[nx:]
+    npg = sum(1 for b in t.p_block if b == -1)
+    if any(b == -1 for b in t.p_block[npg:]):
+        raise TranscriptionError("global parameters must precede stage parameters")
+    stage_w = [blocks.get(k, []) for k in range(N)]
+    if len({len(s) for s in stage_w}) != 1:
+        raise TranscriptionError("stages have different numbers of variables")
+    nvr = len(stage_w[0]) - nx
+    stage_p = [[i for i, b in enumerate(t.p_block) if b == k] for k in range(N)]
+    nps = len(stage_p[0])
+    stage_g = [[i for i, c in enumerate(t.g) if c[3] == k] for k in range(N)]
+    ngr = len(stage_g[0])
+    if any(len(s) != nps for s in stage_p) or any(len(s) != ngr for s in stage_g):
+        raise TranscriptionError("stages have different numbers of parameters or constraints")
+    if -1 in t.cost or any(c[3] == -1 for c in t.g):
+        raise TranscriptionError("MHE terms outside the stage loop are not supported")
+
+    nX, nV = nx + nth, nx + nth + nvr
+    X0 = [sx.sym(f"X0[{i}]") for i in range(nX)]
+    V = [sx.sym(f"V[{i}]") for i in range(nV)]
+    X1 = [sx.sym(f"X1[{i}]") for i in range(nX)]
+    PS = [sx.sym(f"PS[{i}]") for i in range(nps)]
+    PG = [sx.sym(f"PG[{i}]") for i in range(npg)]
+    TK = sx.sym("TK")  # kernel stage start time k*ts; the model's time is TK + t_start
+    allowed = {s.uid for s in X0 + V + X1 + PS + PG + [TK]}
+    ref = None
+    for k in range(N):
+        start_state = x0_ref if k == 0 else stage_w[k - 1][-nx:]
+        mapping = {}
+        for i, ph in zip(start_state, V[:nx]):
+            mapping[t.w[i]] = ph
+        for i, ph in zip(th_ref, V[nx:nX]):
+            mapping[t.w[i]] = ph
+        for i, ph in zip(stage_w[k][:nvr], V[nX:]):
+            mapping[t.w[i]] = ph
+        for i, ph in zip(stage_w[k][nvr:], X1[:nx]):
+            mapping[t.w[i]] = ph
+        for i, ph in zip(stage_p[k], PS):
+            mapping[t.p[i]] = ph
+        for i, ph in zip(range(npg), PG):
+            mapping[t.p[i]] = ph
+        if k in t.tk_syms:
+            mapping[t.tk_syms[k]] = sx.add(TK, sx.const(t.t_start))
+        gs = [t.g[i] for i in stage_g[k]]
+        exprs = [t.cost.get(k, sx.ZERO)] + [c[0] for c in gs] + [c[1] for c in gs] + [c[2] for c in gs]
+        sub = sx.substitute(exprs, mapping)
+        for fs in sx.free_symbols(sub):
+            if fs.uid not in allowed:
+                raise TranscriptionError(f"MHE stage {k} depends on {fs.name}, which is not stage-local")
+        if ref is None:
+            ref = sub
+        elif any(a is not b for a, b in zip(ref, sub)):
+            raise TranscriptionError(f"MHE stage {k} differs structurally from stage 0")
+    g = list(ref[1:1 + ngr])
+    g_lb = list(ref[1 + ngr:1 + 2 * ngr])
+    g_ub = list(ref[1 + 2 * ngr:])
+    first = TK < 0.5 * ts
+    link_lb = sx.if_else(first, sx.const(-_OPEN), sx.ZERO)
+    link_ub = sx.if_else(first, sx.const(_OPEN), sx.ZERO)
+    for i in range(nX):  # xi_k - x_k, vartheta_k - theta_k: open at k = 0
+        g.append(sx.sub(V[i], X0[i]))
+        g_lb.append(link_lb)
+        g_ub.append(link_ub)
+    for i in range(nth):  # theta_{k+1} = vartheta_k
+        g.append(sx.sub(X1[nx + i], V[nx + i]))
+        g_lb.append(sx.ZERO)
+        g_ub.append(sx.ZERO)
+    stage = StageFunction(X0=X0, V=V, X1=X1, PS=PS, PG=PG, TK=TK, cost=ref[0], g=g, g_lb=g_lb, g_ub=g_ub)
+
+    # index maps (kernel w = [X_0, {V_k, X_{k+1}}])
+    w_src, w_dup, w_zero = [0] * nX, [False] * nX, [True] * nX
+    for k in range(N):
+        start_state = x0_ref if k == 0 else stage_w[k - 1][-nx:]
+        w_src += list(start_state) + list(th_ref) + stage_w[k][:nvr]
+        w_dup += [k > 0] * nX + [False] * nvr
+        w_src += stage_w[k][nvr:] + list(th_ref)
+        w_dup += [False] * nx + [True] * nth
+        w_zero += [False] * (nV + nX)
+    w_src = np.asarray(w_src, dtype=np.int64)
+    w_dup = np.asarray(w_dup, dtype=bool)
+    w_zero = np.asarray(w_zero, dtype=bool)
+    w_primary = np.full(len(t.w), -1, dtype=np.int64)
+    for ki in np.nonzero(~w_dup & ~w_zero)[0]:
+        w_primary[w_src[ki]] = ki
+    ngk = ngr + nX + nth
+    g_of_ref = np.asarray([k * ngk + r for k in range(N) for r in range(ngr)], dtype=np.int64)
+    lift = LiftMaps(w_src=w_src, w_dup=w_dup, p_src=np.arange(len(t.p), dtype=np.int64),
+                    g_of_ref=g_of_ref, w_primary=w_primary, w_zero=w_zero)
+
+    f_total = sx.ZERO
+    for k in range(N):
+        f_total = sx.add(f_total, t.cost.get(k, sx.ZERO))
+    return StageNLP(
+        lift=lift, tk_syms=dict(t.tk_syms),
+        N=N, nx=nX, nv=nV, ng=ngk, nps=nps, npg=npg, ts=ts,
+        w_syms=list(t.w), p_syms=list(t.p), w_labels=list(t.w_labels), p_labels=list(t.p_labels),
+        g_exprs=[c[0] for c in t.g], g_lb=[c[1] for c in t.g], g_ub=[c[2] for c in t.g], f_expr=f_total,
+        var_groups=t.var_groups, par_groups=t.par_groups, stage=stage,
+        tk_values=t.t_start + np.arange(N, dtype=float) * ts,
+        gap_closing=[c[4] for c in t.g],
+    )
+
+
+def _backend_base():
+    from agentlib_mpc_amd.optimization_backends.mi355x import MI355XBackend
+
+    return MI355XBackend
+
+
+class MHEBackend(_backend_base()):
+    """``casadi_mhe`` replacement (`casadi_/mhe.py:414-424`): collocation only."""
+
+    system_type = MHESystem
+    discretization_types = {DiscretizationMethod.collocation: MHECollocation}
+    #: `casadi_/mhe.py:136`: results keep the past horizon (t < 0)
+    only_positive_times_in_results = False
+
+    def setup_optimization(self, var_ref):
+        method = self.config.discretization_options.method
+        if method not in self.discretization_types:
+            raise ValueError(f"discretization method {method!r} is not available for the MHE "
+                             "(the reference supports collocation only)")
+        super().setup_optimization(var_ref)

@@ -84,6 +84,8 @@ class MI355XBackend(OptimizationBackend):
     }
     _supported_models = {"CasadiModel": CasadiModel}
     config_type = MI355XBackendConfig
+    #: `core/discretization.py:126`: ``Results[name]`` keeps only t >= 0
+    only_positive_times_in_results = True
 
     def __init__(self, config: dict):
         super().__init__(config)
@@ -100,7 +102,8 @@ class MI355XBackend(OptimizationBackend):
         opts = self.config.discretization_options
         discretization = self.discretization_types[opts.method](options=opts)
         nlp = discretization.transcribe(self.system)
-        self.problem = CompiledProblem(nlp, self.system)
+        self.problem = CompiledProblem(nlp, self.system,
+                                       only_positive_times=self.only_positive_times_in_results)
         self._remembered = None
 
     def _native(self):

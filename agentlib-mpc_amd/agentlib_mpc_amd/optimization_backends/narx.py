@@ -169,6 +169,7 @@ class LiftMaps:
     w_primary: np.ndarray    # [nw_ref] kernel index of each reference variable (-1: fixed, unused)
     steps_per_stage: int = 1  # reference steps per kernel stage
     w_fix_par: "np.ndarray | None" = None  # [nw_kernel] parameter fixing the variable (-1: none)
+    w_zero: "np.ndarray | None" = None     # [nw_kernel] kernel-only dummies fixed to 0 (MHE X_0)
 
     @property
     def nw(self) -> int:

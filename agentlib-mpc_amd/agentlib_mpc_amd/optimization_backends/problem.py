@@ -31,8 +31,9 @@ GUESS_PREFIX = "guess_"
 
 
 class CompiledProblem:
-    def __init__(self, nlp: StageNLP, system: System):
+    def __init__(self, nlp: StageNLP, system: System, only_positive_times: bool = True):
         self.nlp = nlp
+        self.only_positive_times = only_positive_times
         self.system = system
         self.gen = codegen.generate(nlp)
         self._native = None
@@ -160,6 +161,10 @@ class CompiledProblem:
             klb[..., fx] = val
             kub[..., fx] = val
             kw[..., fx] = val
+        if lift.w_zero is not None:  # kernel-only dummies (MHE: the fixed X_0)
+            klb[..., lift.w_zero] = 0.0
+            kub[..., lift.w_zero] = 0.0
+            kw[..., lift.w_zero] = 0.0
         return kp, klb, kub, kw
 
     def from_kernel(self, w_k: np.ndarray, lbw: np.ndarray) -> np.ndarray:
@@ -204,7 +209,7 @@ class CompiledProblem:
             for key, header in (("var", "variable"), ("ub", "upper"), ("lb", "lower")):
                 columns += [(header, n) for n in var.full_names]
                 blocks.append((key, var.name, var.dim, rc))
-            rows = [r for r, _ in rc if full_grid[r] >= 0]
+            rows = [r for r, _ in rc if full_grid[r] >= 0 or not self.only_positive_times]
             for n in var.full_names:
                 var_rows[n] = rows
         return ResultLayout(full_grid=full_grid, columns=pd.MultiIndex.from_tuples(columns),

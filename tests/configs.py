@@ -131,6 +131,21 @@ def one_room_switch(**kw) -> Case:
     return Case(be, cv, prob, nlps.one_room_switch_inputs(prob, N=N, **{k: kw[k] for k in keys if k in kw}))
 
 
+def mhe_room(**kw) -> Case:
+    N, d = kw.get("N", 15), kw.get("d", 2)
+    meas = kw.pop("measured", None)
+    if meas is None:
+        meas = bm.mhe_measurements(N=N, d=d, **{k: kw.pop(k) for k in ("theta", "noise", "seed") if k in kw})
+    be, cv = bm.mhe_room(measured=meas, **kw)
+    prob = nlps.mhe_room(N=N, d=d)
+    o = {"w_T": kw.get("w_T", 1.0), "w_Tw": kw.get("w_T_wall", 0.0)}
+    if "theta_lb" in kw:
+        o["theta_lb"] = kw["theta_lb"]
+    if "theta_ub" in kw:
+        o["theta_ub"] = kw["theta_ub"]
+    return Case(be, cv, prob, nlps.mhe_room_inputs(prob, meas[0], meas[1], N=N, d=d, **o))
+
+
 CASES: Dict[str, Callable[..., Case]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -144,6 +159,7 @@ CASES: Dict[str, Callable[..., Case]] = {
     "one_room_radau": one_room_radau,
     "one_room_du": one_room_du,
     "one_room_switch": one_room_switch,
+    "mhe_room": mhe_room,
 }
 
 

@@ -16,6 +16,11 @@ pytestmark = pytest.mark.gpu
 
 RTOL_OBJ = 1e-6
 RTOL_TRAJ = 1e-5
+#: groups the NLP leaves numerically undetermined: the estimator's soft-constraint
+#: slack has no cost and one active-free inequality, so only the barrier curvature
+#: (mu / distance^2, ~1e-14 at convergence) pins it and any point of its interval
+#: meets the termination test (see models/examples.py RNGRoomMHE)
+UNDETERMINED = {"mhe_room": {"algebraics"}}
 
 
 def _oracle(case):
@@ -58,6 +63,10 @@ def _cuda():
     ("one_room_du", {"r_delta_mDot": 1.0, "T0": 292.0, "load": 250.0}),
     ("one_room_switch", {}),           # conditional (time-dependent) objective
     ("one_room_switch", {"switch": 1800.0, "r_mDot2": 20.0}),
+    # moving horizon estimation: free x_0 / estimated parameter (lifted, free link rows)
+    ("mhe_room", {}),
+    ("mhe_room", {"theta": 5.8, "noise": 0.05, "seed": 3, "w_T_wall": 0.5}),
+    ("mhe_room", {"theta": 7.0}),      # true value outside the bounds: estimate at ub
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)
@@ -71,7 +80,7 @@ def test_gpu_matches_oracle(name, kw):
         np.testing.assert_allclose(r.stats["obj"], ref.f, rtol=RTOL_OBJ, atol=1e-9)
         # every variable group on its grid, against the oracle's vector
         for gname, lay in nlp.var_groups.items():
-            if not lay.dim:
+            if not lay.dim or gname in UNDETERMINED.get(name, ()):
                 continue
             got = case.backend.problem.outputs(_w_of(case, r))[gname]
             want = ref.x[lay.index]

@@ -1,0 +1,108 @@
+"""Moving horizon estimation backend (CPU): layout, lifting and the oracle solve.
+
+Reference: `optimization_backends/casadi_/mhe.py` (system :34-124, past-horizon
+collocation :135-361, results keep t < 0 :136), `examples/Estimators/mhe_example.py`.
+The transcription itself is checked against the oracle restatement in
+`tests/test_transcription.py` (case ``mhe_room``); GPU parity in `tests/test_gpu_ipm.py`.
+"""
+
+import numpy as np
+import pytest
+
+from agentlib_mpc_amd import symbolic as sx
+from agentlib_mpc_amd.data_structures.mpc_datamodels import MHEVariableReference
+from oracle import ipm
+from tests import configs
+
+
+def _stage_eval(nlp, kp, kw):
+    st = nlp.stage
+    npb = nlp.nv + nlp.nx
+    ftot, g, lb, ub = 0.0, [], [], []
+    for k in range(nlp.N):
+        sv = dict(zip(st.local, kw[k * npb: k * npb + len(st.local)]))
+        sv.update(zip(st.PS, kp[nlp.npg + k * nlp.nps: nlp.npg + (k + 1) * nlp.nps]))
+        sv.update(zip(st.PG, kp[:nlp.npg]))
+        sv[st.TK] = k * nlp.ts  # the kernel's stage start time
+        out = sx.evaluate([st.cost] + st.g + st.g_lb + st.g_ub, sv)
+        ng = len(st.g)
+        ftot += float(out[0])
+        g += [float(v) for v in out[1:1 + ng]]
+        lb += [float(v) for v in out[1 + ng:1 + 2 * ng]]
+        ub += [float(v) for v in out[1 + 2 * ng:]]
+    return ftot, np.array(g), np.array(lb), np.array(ub)
+
+
+def test_lifted_mhe_reproduces_reference_nlp():
+    """Kernel stage form (X_0 dummy, free link rows at k = 0, carried theta) ==
+    the reference MHE NLP at mapped points."""
+    case = configs.mhe_room()
+    prob = case.backend.problem
+    nlp, lift = prob.nlp, prob.nlp.lift
+    (p, lbw, ubw, w0), mi = configs.product_nlp_inputs(case)
+    rng = np.random.default_rng(11)
+    w = w0 + rng.normal(scale=0.5, size=w0.shape)
+    w[2] = 5.3
+    vals = {s: v for s, v in zip(nlp.w_syms, w)}
+    vals.update({s: v for s, v in zip(nlp.p_syms, p)})
+    ref = np.array(sx.evaluate([nlp.f_expr] + nlp.g_exprs, vals), float)
+    kp, kl, ku, kw = prob.to_kernel(p, lbw, ubw, w)
+    assert len(kw) == nlp.kernel_nw and len(kp) == nlp.kernel_np
+    np.testing.assert_array_equal(kl[:nlp.nx], 0.0)  # X_0 dummy fixed to 0
+    np.testing.assert_array_equal(ku[:nlp.nx], 0.0)
+    f, g, lb, ub = _stage_eval(nlp, kp, kw)
+    np.testing.assert_allclose(f, ref[0], rtol=1e-13)
+    np.testing.assert_allclose(g[lift.g_of_ref], ref[1:], rtol=1e-12, atol=1e-9)
+    extra = np.setdiff1d(np.arange(len(g)), lift.g_of_ref)
+    ngk = nlp.ng
+    first = extra[extra < ngk]          # stage 0: link rows are open (never active)
+    rest = extra[extra >= ngk]
+    nlink = nlp.nx                      # xi - x, vartheta - theta
+    np.testing.assert_array_equal(lb[first[:nlink]], -1e8)
+    np.testing.assert_array_equal(ub[first[:nlink]], 1e8)
+    np.testing.assert_array_equal(g[first[nlink:]], 0.0)  # theta_1 = vartheta_0
+    np.testing.assert_array_equal(g[rest], 0.0)           # copies consistent
+    np.testing.assert_array_equal(lb[rest], 0.0)
+    np.testing.assert_array_equal(ub[rest], 0.0)
+    np.testing.assert_array_equal(prob.from_kernel(kw, lbw), w)
+
+
+def test_oracle_mhe_recovers_true_parameter():
+    """Noise-free measurements of the true model: the estimate recovers theta = 5.5
+    and the unmeasured wall temperature (collocation error only)."""
+    case = configs.mhe_room()
+    p, lbw, ubw, w0 = case.oracle_inputs
+    fn = case.oracle.functions(p)
+    res = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), ipm.IPMOptions(tol=1e-10))
+    assert res.success, res.status
+    assert abs(res.x[2] - 5.5) < 1e-3
+    assert abs(res.x[1] - 27.0) < 0.05 and abs(res.x[0] - 25.0) < 0.05
+
+
+def test_mhe_results_keep_past_horizon():
+    case = configs.mhe_room()
+    lay = case.backend.problem.layout
+    assert min(lay.full_grid) == -15 * 200.0 and max(lay.full_grid) == 0.0
+    assert len(lay.variable_grid_indices["T"]) == 46  # (d+1)N+1 points, all t <= 0
+    assert len(lay.variable_grid_indices["full_capacity_from_volume_factor"]) == 1
+    cols = [c for c in lay.columns if c[0] == "parameter"]
+    assert cols[:5] == [("parameter", n) for n in ("mDot", "load", "T_in", "T_ambient", "T_upper")]
+    assert ("parameter", "measured_T") in cols and ("parameter", "weight_T_wall") in cols
+
+
+def test_mhe_var_ref_and_registration():
+    vr = MHEVariableReference(states=["T"], measured_states=["measured_T"], weights_states=["weight_T"],
+                              known_inputs=["mDot"])
+    assert sorted(vr.all_variables()) == ["T", "mDot"]
+    from agentlib_mpc_amd.optimization_backends import backend_types
+    assert "casadi_mhe" in backend_types and "mi355x_mhe" in backend_types
+
+
+def test_mhe_rejects_multiple_shooting():
+    from agentlib_mpc_amd.optimization_backends import create_optimization_backend
+
+    be = create_optimization_backend({
+        "type": "casadi_mhe", "model": {"type": "agentlib_mpc_amd.models.examples.RNGRoom"},
+        "discretization_options": {"method": "multiple_shooting"}})
+    with pytest.raises(ValueError, match="collocation"):
+        be.setup_optimization(MHEVariableReference(states=["T", "T_wall"]))

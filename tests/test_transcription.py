@@ -26,6 +26,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "one_room_radau": (1 + 15 * (1 + 3 * 3 + 1), 15 * (1 + 3 * 3), None),  # Radau IIA, d=3
     "one_room_du": (121, 105, 97),  # C1 + change penalty (one more model parameter)
     "one_room_switch": (76, 60, 53),  # time-dependent conditional objective, MS Euler
+    "mhe_room": (3 + 15 * 14, 15 * 14, 10 + 15 * 9),  # MHE: x_0, theta free; 6 vars per point
 }
 
 

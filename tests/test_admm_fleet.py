@@ -78,6 +78,61 @@ def test_coordinated_consensus_round_matches_oracle():
         np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
 
 
+def test_coordinated_closed_loop_rounds_match_oracle():
+    """Three control steps of the coordinator with new room measurements between
+    them: mean update from the last round's locals, shift of means
+    and multipliers by one interval (`admm_coordinator.py:278-279`,
+    `admm_datatypes.py:275-331`), warm-started local solves, varying penalty
+    (`admm_coordinator.py:467-479`) — residual histories and means per round."""
+    N, iters = 2, 3
+    classes = bm.c2_fleet_classes(n_blocks=1, N=N)
+    fl = ADMMFleet(classes, device="cpu", ops=_c2_ops(N))
+    orc = C2Oracle(N, bm.C2_ROOMS)
+    kw = dict(admm_iter_max=iters, use_relative_tolerances=False, primal_tol=1e-9, dual_tol=1e-9,
+              penalty_change_threshold=1.5, penalty_change_factor=1.3)
+    be_r, cv_r = bm.admm_room(N=N)
+    state = None
+    for step in range(3):
+        rooms = [(d, T0 - 0.7 * step) for d, T0 in bm.C2_ROOMS]
+        if step:
+            p, lbw, ubw, _ = bm._class_inputs(be_r, cv_r, {"T": [r[1] for r in rooms],
+                                                           "d": [r[0] for r in rooms]}, 4)
+            fl.set_inputs("room", p, lbw, ubw)
+            orc.rooms = rooms
+        out = fl.run_coordinated(0.4, **kw)
+        state, hist, it, conv = oadmm.coordinated_round(orc.participation, orc.initial, orc, 0.4, N,
+                                                        T=3 * N, state=state, **kw)
+        assert out["iterations"] == it
+        got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["records"]])
+        np.testing.assert_allclose(got, np.array(hist), rtol=RTOL, atol=1e-10)
+        for i in range(4):
+            al = f"mDot{i + 1}_coupling_b0"
+            np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
+
+
+def test_local_exchange_closed_loop_rounds_match_oracle():
+    """Three LocalADMM control steps (shift of own trajectory and multipliers,
+    `admm.py:873-937`) with new room measurements between them."""
+    N, iters = 4, 2
+    fl = ADMMFleet(bm.c4_fleet_classes(n_rooms=2, n_supply=1, N=N), device="cpu", ops=_c4_ops(N))
+    orc = C4Oracle(N, bm.C4_ROOMS[:2])
+    be_r, cv_r = bm.exchange_room(N=N)
+    state = None
+    for step in range(3):
+        rooms = [(d, T0 + 0.5 * step) for d, T0 in bm.C4_ROOMS[:2]]
+        if step:
+            p, lbw, ubw, _ = bm._class_inputs(be_r, cv_r, {"T": [r[1] for r in rooms],
+                                                           "d": [r[0] for r in rooms]}, 2)
+            fl.set_inputs("room", p, lbw, ubw)
+            orc.rooms = rooms
+        fl.run_local(penalty_factor=1e4, max_iterations=iters)
+        state, hist = oadmm.local_round(orc.participation, orc.initial, orc, 1e4, 1, iters, T=N, state=state)
+        np.testing.assert_allclose(fl.trajectories()["mDot_coupling"], hist[-1]["mDot_coupling"],
+                                   rtol=RTOL, atol=1e-9)
+        np.testing.assert_allclose(fl.multipliers_of("supply", "mDot_out")[0],
+                                   state["mult"][("supply0", "mDot_coupling")], rtol=RTOL, atol=1e-6)
+
+
 def test_relative_tolerance_totals_match_oracle():
     """The moment identities behind the single all-reduce reproduce the
     reference's relative stopping quantities (admm_coordinator.py:405-419)."""

@@ -110,6 +110,35 @@ def test_gpu_coordinated_fleet_matches_oracle():
                                    state["vars"][al].mult["ahu"], rtol=RTOL, atol=1e-8)
 
 
+def test_gpu_coordinated_closed_loop_matches_oracle():
+    """Two coordinator control steps on the GPU fleet with new room measurements
+    between them: device-side mean update, shift of means/multipliers, warm-started
+    batched solves and a varying penalty, against the oracle's round restatement."""
+    N, iters = 10, 3
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N))
+    orc = C2Oracle(N, bm.C2_ROOMS)
+    kw = dict(admm_iter_max=iters, use_relative_tolerances=False, primal_tol=1e-9, dual_tol=1e-9,
+              penalty_change_threshold=1.5, penalty_change_factor=1.3)
+    be_r, cv_r = bm.admm_room(N=N)
+    state = None
+    for step in range(2):
+        rooms = [(d, T0 - 0.7 * step) for d, T0 in bm.C2_ROOMS]
+        if step:
+            p, lbw, ubw, _ = bm._class_inputs(be_r, cv_r, {"T": [r[1] for r in rooms],
+                                                           "d": [r[0] for r in rooms]}, 4)
+            fl.set_inputs("room", p, lbw, ubw)
+            orc.rooms = rooms
+        out = fl.run_coordinated(0.4, **kw)
+        state, hist, it, _ = oadmm.coordinated_round(orc.participation, orc.initial, orc, 0.4, N,
+                                                     T=3 * N, state=state, **kw)
+        assert out["iterations"] == it
+        got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["records"]])
+        np.testing.assert_allclose(got, np.array(hist), rtol=RTOL, atol=1e-10)
+        for i in range(4):
+            al = f"mDot{i + 1}_coupling_b0"
+            np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
+
+
 def test_gpu_three_zone_narx_fleet_matches_oracle_fixture():
     """examples/three_zone_datadriven_admm: 3 NARX zones + AHU + CCA, coordinated ADMM,
     rho=1, absolute criterion 0.04/0.04, N=8, 3 iterations, against the oracle's round

@@ -99,6 +99,10 @@ constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [N][PKS] packed local syst
 constexpr long WS_DOUBLES = O_LP + (long)N * PKS;
 
 using Args = mpcx_kernel_args;
+// kernel arguments read in place from the kernarg segment (address space 4: scalar
+// loads); passing the by-value kernel parameter by reference would make the
+// compiler copy all of it (~400 B) into every lane's scratch
+using KArgs = const __attribute__((address_space(4))) Args;
 
 // ---------------------------------------------------------------------------
 // wave and lane-group helpers
@@ -1417,7 +1421,8 @@ struct Scal {
   double obj_scale, fx;
 };
 
-__device__ __noinline__ Scal init_agent(const Agent a, const Args& args, int agent) {
+__device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
+  KArgs& args = *argp;
   const mpcx_options& o = args.opt;
   const int lane = a.lane;
   const gdbl* lbw = (const gdbl*)args.lbw + (long)agent * NW;
@@ -1719,9 +1724,13 @@ struct LSResult {
 };
 
 // filter line search; trial points live in LDS (xt, scaled gt)
-__device__ __noinline__ LSResult line_search(const Agent a, const LSOpt o, double mu, double obj_scale,
+__device__ __noinline__ LSResult line_search(const Agent a, KArgs* argp, double mu, double obj_scale,
                                              double alpha0, double gphid, double theta, double phi,
                                              double theta_min, double theta_max, int nfilt) {
+  // options from the kernarg segment (scalar loads); a by-value LSOpt exceeds the
+  // argument registers and would be passed through scratch
+  KArgs& ka = *argp;
+#define o (ka.opt)
   const int lane = a.lane;
   double xr[VS], dxr[VS], lor[VS], hir[VS];
 #pragma unroll
@@ -1815,6 +1824,7 @@ __device__ __noinline__ LSResult line_search(const Agent a, const LSOpt o, doubl
   }
   res.tr = tr;
   return res;
+#undef o
 }
 
 // take the last trial point (xt, gt in LDS) and the multiplier steps
@@ -1905,7 +1915,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   sync();
 #endif
   if (lane == 0) { gL.want_sdh = 0; gL.sdh_ok = 0; gL.hsig = 1.0; gL.seq = 0; }
-  const Scal sc = init_agent(a, args, agent);
+  const Scal sc = init_agent(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr(), agent);
   PROF(0);
   const double obj_scale = sc.obj_scale;
   double fx = sc.fx;
@@ -1985,8 +1995,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     // filter line search
     const double theta = st.theta;
     const double phi = fx - mu * st.barrier;
-    const LSOpt lso{o.alpha_min_frac, o.gamma_theta, o.gamma_phi, o.delta, o.s_theta, o.s_phi, o.eta_phi};
-    const LSResult ls = line_search(a, lso, mu, obj_scale, st.amax, st.gphid, theta, phi, theta_min,
+    const LSResult ls = line_search(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr(), mu, obj_scale, st.amax, st.gphid, theta, phi, theta_min,
                                     theta_max, nfilt);
     n_trials += ls.trials;
     bool ftype = ls.ftype;

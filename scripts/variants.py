@@ -26,6 +26,13 @@ VARIANTS = {
     "w1": (["-DMPCX_MIN_WAVES=1"], None),
     "inl_w2": (["-DMPCX_MIN_WAVES=2"], ("__noinline__", "__attribute__((always_inline))")),
     "inl_w4": ([], ("__noinline__", "__attribute__((always_inline))")),
+    # interprocedural register allocation: callers only save what callees clobber
+    "ipra": (["-mllvm", "-enable-ipra"], None),
+    "nounroll": (["-fno-unroll-loops"], None),
+    "ipra_nounroll": (["-mllvm", "-enable-ipra", "-fno-unroll-loops"], None),
+    "o2": (["-O2"], None),
+    # the kernel source of the last commit (A/B against the working tree)
+    "head": ([], "HEAD"),
 }
 
 
@@ -46,7 +53,11 @@ def build(names):
         kern = native.CSRC / "mpcx_ipm.hip"
         src_text = gen.source
         if tr is not None:
-            ktxt = kern.read_text().replace(*tr)
+            if tr == "HEAD":
+                ktxt = subprocess.run(["git", "-C", str(ROOT), "show", "HEAD:agentlib-mpc_amd/csrc/mpcx_ipm.hip"],
+                                      capture_output=True, text=True, check=True).stdout
+            else:
+                ktxt = kern.read_text().replace(*tr)
             kp = d / f"mpcx_ipm_{name}.hip"
             kp.write_text(ktxt)
             src_text = src_text.replace('#include "mpcx_ipm.hip"', f'#include "{kp}"')

@@ -216,11 +216,14 @@ def mhe_measurements(N=15, ts=200.0, d=2, theta=5.5, T0=25.0, T_wall0=27.0, nois
 
 
 def mhe_room(N=15, ts=200.0, d=2, theta_lb=5.0, theta_ub=6.0, theta_guess=None, w_T=1.0, w_T_wall=0.0,
-             measured=None, inputs=None, model="RNGRoomMHE", solver_options=TIGHT):
+             measured=None, inputs=None, model="RNGRoomMHE", estimate="theta", mDot_lb=0.0, mDot_ub=1.0,
+             solver_options=TIGHT):
     """`examples/Estimators/mhe_example.py:188-228`: backend ``casadi_mhe`` on the
     RNGRoom model, estimating ``full_capacity_from_volume_factor`` (bounds 5..6)
     from zone temperature measurements (state weights T: 1, T_wall: 0).  The
-    default model bounds the (cost-free) slack, see :class:`examples.RNGRoomMHE`."""
+    default model bounds the (cost-free) slack, see :class:`examples.RNGRoomMHE`.
+    ``estimate="mDot"`` estimates the supply mass flow per interval instead
+    (``estimated_inputs``, `mhe.py:163`) with the capacity factor known."""
     from agentlib_mpc_amd.data_structures.mpc_datamodels import MHEVariableReference
 
     be = create_optimization_backend({
@@ -230,11 +233,12 @@ def mhe_room(N=15, ts=200.0, d=2, theta_lb=5.0, theta_ub=6.0, theta_guess=None, 
                                    "prediction_horizon": N, "time_step": ts},
         "solver": {"name": "ipopt", "options": solver_options},
     })
-    known = list(MHE_KNOWN_INPUTS)
+    est_u = estimate == "mDot"
+    known = [n for n in MHE_KNOWN_INPUTS if not (est_u and n == "mDot")]
     be.setup_optimization(MHEVariableReference(
         states=["T", "T_wall"], measured_states=["measured_T", "measured_T_wall"],
-        weights_states=["weight_T", "weight_T_wall"], estimated_inputs=[],
-        estimated_parameters=["full_capacity_from_volume_factor"], known_inputs=known,
+        weights_states=["weight_T", "weight_T_wall"], estimated_inputs=["mDot"] if est_u else [],
+        estimated_parameters=[] if est_u else ["full_capacity_from_volume_factor"], known_inputs=known,
         known_parameters=[], outputs=[]))
     if measured is None:
         measured = mhe_measurements(N=N, ts=ts, d=d)
@@ -243,11 +247,14 @@ def mhe_room(N=15, ts=200.0, d=2, theta_lb=5.0, theta_ub=6.0, theta_guess=None, 
     cv = {
         "T": V("T", 25.0), "T_wall": V("T_wall", 27.0),
         "full_capacity_from_volume_factor": V("full_capacity_from_volume_factor", th, theta_lb, theta_ub),
+        "mDot": V("mDot", u["mDot"], mDot_lb, mDot_ub),
         "measured_T": V("measured_T", [float(v) for v in measured[0]]),
         "measured_T_wall": V("measured_T_wall", [float(v) for v in measured[1]]),
         "weight_T": V("weight_T", w_T), "weight_T_wall": V("weight_T_wall", w_T_wall),
     }
     cv.update({n: V(n, u[n]) for n in known})
+    if est_u:
+        del cv["full_capacity_from_volume_factor"]
     return be, cv
 
 
@@ -388,6 +395,7 @@ def compile_all(verbose: bool = False):
     variants["tz_ahu_n8"] = lambda: tz_ahu(N=8)
     variants["tz_cca_n8"] = lambda: tz_cca(N=8)
     variants["mhe_room"] = lambda: mhe_room()
+    variants["mhe_room_u"] = lambda: mhe_room(estimate="mDot")
     for name, fn in variants.items():
         be, _ = fn()
         paths[name] = be.problem.compile()

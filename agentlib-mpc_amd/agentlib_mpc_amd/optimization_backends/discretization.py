@@ -165,6 +165,8 @@ class StageNLP:
     lift: Optional[object] = None
     #: symbols of the stage start times in the reference expressions (value tk_values[k])
     tk_syms: Optional[Dict[int, sx.Expr]] = None
+    #: factor every KKT system with the sequential block chain (MHE lifts, see mhe.py)
+    force_block_chain: bool = False
 
     @property
     def nw(self) -> int:

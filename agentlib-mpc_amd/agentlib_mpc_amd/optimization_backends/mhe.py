@@ -33,6 +33,12 @@ and the same reference-variable values; ``ξ_k, ϑ_k (k ≥ 1)`` and ``θ_k`` ar
 (Rows with two infinite bounds instead of ±1e8 stall the iteration — in the
 kernel and in the oracle IPM alike — so the open rows use finite bounds.)
 
+The lifted MHE runs on the kernel's sequential block-chain factorisation: the
+stage-parallel interior elimination does not converge on it (measured with
+``scripts/mhe_diag.py``: 500 iterations at mu = 0.1 vs 12 iterations on the
+block chain, which matches the oracle), so the code object is built with
+``MPCX_FORCE_BLOCK_CHAIN``.
+
 ``MHEBackend.sample`` (:426-542) is not restated: the reference backend samples
 through ``utils.sampling.sample`` (`core/casadi_backend.py:177-240`), so that
 override is never called.  Known-parameter order: the reference builds it from a
@@ -260,6 +266,7 @@ def _lift_mhe(t: _Transcriber, system: MHESystem) -> StageNLP:
         var_groups=t.var_groups, par_groups=t.par_groups, stage=stage,
         tk_values=t.t_start + np.arange(N, dtype=float) * ts,
         gap_closing=[c[4] for c in t.g],
+        force_block_chain=True,
     )
 
 

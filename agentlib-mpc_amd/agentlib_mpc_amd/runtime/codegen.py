@@ -169,6 +169,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         f"#define MPCX_TS {float(ts)!r}",
         f"#define MPCX_ABI {KERNEL_ABI_VERSION}",
         f"#define MPCX_LDS_TARGET {lds_target}",
+        *(["#define MPCX_FORCE_BLOCK_CHAIN 1"] if nlp.force_block_chain else []),
         "#include <hip/hip_runtime.h>",
         "#include <math.h>",
         "",

@@ -1257,6 +1257,9 @@ __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     }
     wsync();
     SPROF(1);
+#ifdef MPCX_FORCE_BLOCK_CHAIN  // always take the sequential block chain (MHE lifts; diagnostics)
+    bad = 1;
+#endif
     if constexpr (NX > 0) {
       if (wsumi(g == 0 ? bad : 0) > 0) {  // singular stage interior: block chain instead
         sync();

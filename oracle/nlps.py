@@ -797,22 +797,34 @@ def one_room_switch_inputs(prob, N=15, T0=298.16, load=150.0, T_in=290.15, T_upp
 # moving horizon estimation, backend "casadi_mhe", collocation over the past
 # ---------------------------------------------------------------------------
 
-def mhe_room(N=15, ts=200.0, d=2) -> OracleProblem:
-    """`casadi_/mhe.py:34-196` on `examples/Estimators/mhe_example.py:142-170` (RNGRoom),
-    estimating theta = full_capacity_from_volume_factor.
-    w = [T_0, Tw_0, theta, {for j: (T, Tw, T_out, cooling, pw2z, T_slack)_kj; T_{k+1}, Tw_{k+1}}];
+def mhe_room(N=15, ts=200.0, d=2, estimate="theta") -> OracleProblem:
+    """`casadi_/mhe.py:34-196` on `examples/Estimators/mhe_example.py:142-170` (RNGRoom).
+
+    estimate="theta": estimated parameter theta = full_capacity_from_volume_factor,
+      w = [T_0, Tw_0, theta, {for j: (T, Tw, T_out, cooling, pw2z, T_slack)_kj; T_{k+1}, Tw_{k+1}}],
+      p = [cp, rho, C_Wall, RZone_Wall, R_hull_amb, V, s_T, r_mDot, weight_T, weight_Tw,
+           {mDot, load, T_in, T_ambient, T_upper, {meas_T, meas_Tw}_j}_k];
+    estimate="mDot": estimated input mDot (one per interval, `mhe.py:163`), theta known,
+      w = [T_0, Tw_0, {mDot_k, for j: (...)_kj; T_{k+1}, Tw_{k+1}}],
+      p = [cp, rho, theta, C_Wall, RZone_Wall, R_hull_amb, V, s_T, r_mDot, weight_T, weight_Tw,
+           {load, T_in, T_ambient, T_upper, {meas_T, meas_Tw}_j}_k].
     g_k = [{ts*ode_j - xp_j (T, Tw), T + T_slack, T_out - T, cooling - cp mDot (T_in - T),
             pw2z - (Tw - T)/RZ}_j, x_end - x_{k+1} (T, Tw)];
-    p = [cp, rho, C_Wall, RZone_Wall, R_hull_amb, V, s_T, r_mDot, weight_T, weight_Tw,
-         {mDot, load, T_in, T_ambient, T_upper, {meas_T, meas_Tw}_j}_k];
     f = sum_kj B_j ts (w_T (T - mT)^2 + w_Tw (Tw - mTw)^2)."""
     tau, B, C, D = collocation(d, "legendre")
-    nb = 6 * d + 2
-    n = 3 + N * nb
+    est_u = estimate == "mDot"
+    nu = int(est_u)
+    nb = nu + 6 * d + 2
+    head = 2 if est_u else 3
+    n = head + N * nb
     m = N * (6 * d + 2)
-    npg, nps = 10, 5 + 2 * d
-    names = ["T@0", "T_wall@0", "theta"]
+    npg = 11 if est_u else 10
+    nin = 4 if est_u else 5
+    nps = nin + 2 * d
+    iw = npg - 2  # weight_T, weight_Tw
+    names = ["T@0", "T_wall@0"] + ([] if est_u else ["theta"])
     for k in range(N):
+        names += [f"mDot@{k}"] * nu
         for j in range(d):
             names += [f"{v}@{k},{j}" for v in ("T", "T_wall", "T_out", "cooling", "pw2z", "T_slack")]
         names += [f"T@{k + 1}", f"T_wall@{k + 1}"]
@@ -820,22 +832,29 @@ def mhe_room(N=15, ts=200.0, d=2) -> OracleProblem:
     def f(w, p):
         tot = w.new_zeros(())
         for k in range(N):
-            o = 3 + k * nb
+            o = head + k * nb + nu
             for j in range(d):
                 q = o + 6 * j
-                ps = npg + k * nps + 5 + 2 * j
-                tot = tot + B[j + 1] * ts * (p[8] * (w[q] - p[ps]) ** 2 + p[9] * (w[q + 1] - p[ps + 1]) ** 2)
+                ps = npg + k * nps + nin + 2 * j
+                tot = tot + B[j + 1] * ts * (p[iw] * (w[q] - p[ps]) ** 2 + p[iw + 1] * (w[q + 1] - p[ps + 1]) ** 2)
         return tot
 
     def g(w, p):
-        cp, rho, Cw, Rzw, Rha, Vz = p[0], p[1], p[2], p[3], p[4], p[5]
-        th = w[2]
+        if est_u:
+            cp, rho, th, Cw, Rzw, Rha, Vz = p[0], p[1], p[2], p[3], p[4], p[5], p[6]
+        else:
+            cp, rho, Cw, Rzw, Rha, Vz = p[0], p[1], p[2], p[3], p[4], p[5]
+            th = w[2]
         out = []
         xk = [w[0], w[1]]
         for k in range(N):
-            o = 3 + k * nb
+            o = head + k * nb + nu
             ps = npg + k * nps
-            mDot, load, T_in, T_amb = p[ps], p[ps + 1], p[ps + 2], p[ps + 3]
+            if est_u:
+                mDot = w[o - 1]
+                load, T_in, T_amb = p[ps], p[ps + 1], p[ps + 2]
+            else:
+                mDot, load, T_in, T_amb = p[ps], p[ps + 1], p[ps + 2], p[ps + 3]
             X = [[w[o + 6 * j], w[o + 6 * j + 1]] for j in range(d)]
             for j in range(d):
                 q = o + 6 * j
@@ -843,14 +862,14 @@ def mhe_room(N=15, ts=200.0, d=2) -> OracleProblem:
                 pw = (Tw - T) / Rzw
                 cool = cp * mDot * (T_in - T)
                 ode = [(load + cool + pw) / (rho * cp * Vz * th), -((Tw - T_amb) / Rha + pw) / Cw]
-                for s in range(2):
-                    xp = C[0, j + 1] * xk[s] + sum(C[r + 1, j + 1] * X[r][s] for r in range(d))
-                    out.append(ts * ode[s] - xp)
+                for s_ in range(2):
+                    xp = C[0, j + 1] * xk[s_] + sum(C[r + 1, j + 1] * X[r][s_] for r in range(d))
+                    out.append(ts * ode[s_] - xp)
                 out += [T + w[q + 5], w[q + 2] - T, w[q + 3] - cool, w[q + 4] - pw]
-            x1 = [w[o + nb - 2], w[o + nb - 1]]
-            for s in range(2):
-                x_end = D[0] * xk[s] + sum(D[j + 1] * X[j][s] for j in range(d))
-                out.append(x_end - x1[s])
+            x1 = [w[o + 6 * d], w[o + 6 * d + 1]]
+            for s_ in range(2):
+                x_end = D[0] * xk[s_] + sum(D[j + 1] * X[j][s_] for j in range(d))
+                out.append(x_end - x1[s_])
             xk = x1
         return torch.stack(out)
 
@@ -858,7 +877,7 @@ def mhe_room(N=15, ts=200.0, d=2) -> OracleProblem:
         u = np.zeros(m)
         for k in range(N):
             for j in range(d):
-                u[k * (6 * d + 2) + 6 * j + 2] = p[npg + k * nps + 4]
+                u[k * (6 * d + 2) + 6 * j + 2] = p[npg + k * nps + nin - 1]
         return u
 
     def lbg(p):
@@ -868,18 +887,23 @@ def mhe_room(N=15, ts=200.0, d=2) -> OracleProblem:
 
 
 def mhe_room_inputs(prob, meas_T, meas_Tw, N=15, d=2, w_T=1.0, w_Tw=0.0, theta_lb=5.0, theta_ub=6.0,
-                    mDot=0.22, load=0.0, T_in=17.0, T_amb=28.0, T_upper=22.0, slack_lb=-50.0):
+                    mDot=0.22, load=0.0, T_in=17.0, T_amb=28.0, T_upper=22.0, slack_lb=-50.0,
+                    estimate="theta", theta=5.5, mDot_lb=0.0, mDot_ub=1.0):
     """Cold start (`core/discretization.py:212-245`): unbounded states/outputs guess 0,
-    theta guesses the middle of its bounds."""
-    p = [1005.0, 1.2, 4_569_348.0, 0.0129, 0.1128, 59.0, 1.0, 1.0, w_T, w_Tw]
+    the estimated parameter / inputs guess the middle of their bounds."""
+    est_u = estimate == "mDot"
+    p = [1005.0, 1.2] + ([theta] if est_u else []) + [4_569_348.0, 0.0129, 0.1128, 59.0, 1.0, 1.0, w_T, w_Tw]
     for k in range(N):
-        p += [mDot, load, T_in, T_amb, T_upper]
+        p += ([] if est_u else [mDot]) + [load, T_in, T_amb, T_upper]
         for j in range(d):
             p += [meas_T[k * d + j], meas_Tw[k * d + j]]
     p = np.array(p, float)
     lbw, ubw, w0 = np.full(prob.n, -np.inf), np.full(prob.n, np.inf), np.zeros(prob.n)
-    lbw[2], ubw[2], w0[2] = theta_lb, theta_ub, 0.5 * (theta_lb + theta_ub)
-    for i, name in enumerate(prob.w_names):  # RNGRoomMHE: slack bounded below
-        if name.startswith("T_slack@"):
+    for i, name in enumerate(prob.w_names):
+        if name == "theta":
+            lbw[i], ubw[i], w0[i] = theta_lb, theta_ub, 0.5 * (theta_lb + theta_ub)
+        elif name.startswith("mDot@"):
+            lbw[i], ubw[i], w0[i] = mDot_lb, mDot_ub, 0.5 * (mDot_lb + mDot_ub)
+        elif name.startswith("T_slack@"):  # RNGRoomMHE: slack bounded below
             lbw[i] = slack_lb  # guess 0.5 (lb + inf) = inf -> 0 (nan_to_num, posinf=0)
     return p, lbw, ubw, w0

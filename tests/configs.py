@@ -137,8 +137,9 @@ def mhe_room(**kw) -> Case:
     if meas is None:
         meas = bm.mhe_measurements(N=N, d=d, **{k: kw.pop(k) for k in ("theta", "noise", "seed") if k in kw})
     be, cv = bm.mhe_room(measured=meas, **kw)
-    prob = nlps.mhe_room(N=N, d=d)
-    o = {"w_T": kw.get("w_T", 1.0), "w_Tw": kw.get("w_T_wall", 0.0)}
+    est = kw.get("estimate", "theta")
+    prob = nlps.mhe_room(N=N, d=d, estimate=est)
+    o = {"w_T": kw.get("w_T", 1.0), "w_Tw": kw.get("w_T_wall", 0.0), "estimate": est}
     if "theta_lb" in kw:
         o["theta_lb"] = kw["theta_lb"]
     if "theta_ub" in kw:
@@ -160,6 +161,9 @@ CASES: Dict[str, Callable[..., Case]] = {
     "one_room_du": one_room_du,
     "one_room_switch": one_room_switch,
     "mhe_room": mhe_room,
+    # estimating mDot per interval needs the wall temperature measured too (else mDot
+    # and the unmeasured wall state trade off and the minimiser is not unique)
+    "mhe_room_u": lambda **kw: mhe_room(estimate="mDot", **{"w_T_wall": 1.0, **kw}),
 }
 
 

@@ -20,7 +20,7 @@ RTOL_TRAJ = 1e-5
 #: slack has no cost and one active-free inequality, so only the barrier curvature
 #: (mu / distance^2, ~1e-14 at convergence) pins it and any point of its interval
 #: meets the termination test (see models/examples.py RNGRoomMHE)
-UNDETERMINED = {"mhe_room": {"algebraics"}}
+UNDETERMINED = {"mhe_room": {"algebraics"}, "mhe_room_u": {"algebraics"}}
 
 
 def _oracle(case):
@@ -67,6 +67,8 @@ def _cuda():
     ("mhe_room", {}),
     ("mhe_room", {"theta": 5.8, "noise": 0.05, "seed": 3, "w_T_wall": 0.5}),
     ("mhe_room", {"theta": 7.0}),      # true value outside the bounds: estimate at ub
+    ("mhe_room_u", {}),                # estimated input per interval, no global parameter
+    ("mhe_room_u", {"noise": 0.05, "seed": 4}),
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)

@@ -27,6 +27,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "one_room_du": (121, 105, 97),  # C1 + change penalty (one more model parameter)
     "one_room_switch": (76, 60, 53),  # time-dependent conditional objective, MS Euler
     "mhe_room": (3 + 15 * 14, 15 * 14, 10 + 15 * 9),  # MHE: x_0, theta free; 6 vars per point
+    "mhe_room_u": (2 + 15 * 15, 15 * 14, 11 + 15 * 8),  # MHE estimating mDot per interval
 }
 
 

@@ -16,10 +16,11 @@ def build(case_name):
     gen = case.backend.problem.gen
     d = native.KERNEL_DIR.parent / "diag"
     d.mkdir(parents=True, exist_ok=True)
-    src = d / f"{case_name}.hip"
-    src.write_text(gen.source)
+    prefix = os.environ.get("DIAG_PREFIX", "")
+    src = d / f"{prefix}{case_name}.hip"
+    src.write_text(gen.source.replace("#define MPCX_FORCE_BLOCK_CHAIN 1", ""))
     for tag, defs in (("default", []), ("chain", ["-DMPCX_FORCE_BLOCK_CHAIN"])):
-        out = d / f"{case_name}_{tag}.hsaco"
+        out = d / f"{prefix}{case_name}_{tag}.hsaco"
         subprocess.run([native._hipcc(), "--genco", "--offload-arch=gfx950", "-O3", "-std=c++17", *defs,
                         f"-I{native.INCLUDE}", f"-I{native.CSRC}", str(src), "-o", str(out)], check=True)
         print("built", out)
@@ -37,8 +38,10 @@ def run(case_name):
     kp, kl, ku, kw = prob.to_kernel(p[None], lbw[None], ubw[None], w0[None])
     dev = torch.device("cuda")
     T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)
-    for tag in ("default", "chain"):
-        nat = NativeProblem(prob.gen, hsaco=native.KERNEL_DIR.parent / "diag" / f"{case_name}_{tag}.hsaco")
+    d = native.KERNEL_DIR.parent / "diag"
+    for hs in sorted(d.glob(f"*{case_name}_*.hsaco")):
+        tag = hs.stem
+        nat = NativeProblem(prob.gen, hsaco=hs)
         nat.set_options(tol=1e-10, max_iter=500)
         tw = T(kw)
         st = torch.zeros(STATS_BYTES, dtype=torch.uint8, device=dev)

@@ -43,6 +43,8 @@ class GeneratedModel:
     dims: Dict[str, int]
     flops: Dict[str, int]
     nnz: Dict[str, int]
+    #: built with MPCX_FORCE_BLOCK_CHAIN (rank-deficient stage interiors, MHE lifts)
+    block_chain_only: bool = False
 
 
 def _bindings(nlp: StageNLP) -> Dict[sx.Expr, str]:
@@ -58,8 +60,52 @@ def _bindings(nlp: StageNLP) -> Dict[sx.Expr, str]:
     return b
 
 
+def _structural_rank(rows: List[set], n_cols: int) -> int:
+    """Maximum bipartite matching of equality rows to the stage variables they touch."""
+    match_col = [-1] * n_cols
+
+    def augment(r, seen):
+        for c in rows[r]:
+            if c in seen:
+                continue
+            seen.add(c)
+            if match_col[c] < 0 or augment(match_col[c], seen):
+                match_col[c] = r
+                return True
+        return False
+
+    return sum(1 for r in range(len(rows)) if augment(r, set()))
+
+
+def interior_rank_deficient(nlp: StageNLP) -> bool:
+    """True when the equality rows of a stage cannot all be matched to the stage's
+    own variables V (structural rank of their V-Jacobian below the row count), e.g.
+    more states than free inputs per interval (continuity rows), a carried
+    previous control, or an MHE link row.  The kernel's stage-parallel elimination
+    needs nonsingular stage interiors; near-singular ones are not always caught by
+    its zero-pivot test and give inaccurate Newton steps, so such structures are
+    factored by the sequential block chain from the start.  Equality rows are
+    those whose bound expressions coincide at a random parameter point."""
+    import numpy as np
+
+    st = nlp.stage
+    if not st.g or not st.V:
+        return False
+    rng = np.random.default_rng(0)
+    vals = {s: float(rng.uniform(0.5, 1.5)) for s in list(st.PS) + list(st.PG)}
+    vals[st.TK] = nlp.ts * min(1, nlp.N - 1)  # an inner stage (k >= 1)
+    lb = np.array(sx.evaluate(st.g_lb, vals), float)
+    ub = np.array(sx.evaluate(st.g_ub, vals), float)
+    col = {v.uid: i for i, v in enumerate(st.V)}
+    rows = []
+    for i in np.flatnonzero(lb == ub):
+        rows.append({col[f.uid] for f in sx.free_symbols([st.g[i]]) if f.uid in col})
+    return _structural_rank(rows, len(st.V)) < len(rows)
+
+
 def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     st = nlp.stage
+    force_chain = nlp.force_block_chain or interior_rank_deficient(nlp)
     loc = st.local
     nl = len(loc)
     ng = nlp.ng
@@ -169,7 +215,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         f"#define MPCX_TS {float(ts)!r}",
         f"#define MPCX_ABI {KERNEL_ABI_VERSION}",
         f"#define MPCX_LDS_TARGET {lds_target}",
-        *(["#define MPCX_FORCE_BLOCK_CHAIN 1"] if nlp.force_block_chain else []),
+        *(["#define MPCX_FORCE_BLOCK_CHAIN 1"] if force_chain else []),
         "#include <hip/hip_runtime.h>",
         "#include <math.h>",
         "",
@@ -196,4 +242,4 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         src = src.replace('#include <math.h>\n', '#include <math.h>\n' + "\n".join(tables) + "\n", 1)
         src = re.sub(r"ANN(\d+)_", lambda m: f"ANN{local[int(m.group(1))]}_", src)
     key = hashlib.sha1(src.encode()).hexdigest()[:16]
-    return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz)
+    return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz, block_chain_only=force_chain)

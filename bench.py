@@ -166,10 +166,8 @@ def nn_bench(args, world, rank, dev):
     (two ANNs BN->Dense(32,sigmoid)->Dense(1), backend casadi_admm_nn, N=24, ts=1800),
     one batched local ADMM solve of the whole fleet per step (first iteration:
     z-bar = initial coupling values, lambda = 0), cold start."""
-    import torch
     from agentlib_mpc_amd import benchmarks as bm
     from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
-    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
 
     n = args.nn_zones
     be, cv = bm.room_nn(solver_options={"ipopt": {"tol": args.tol, "max_iter": 500}})
@@ -178,6 +176,30 @@ def nn_bench(args, world, rank, dev):
     vals = {"T_air": rng.uniform(292.0, 297.0, n), "d": rng.uniform(50.0, 200.0, n),
             "T_amb": rng.uniform(295.0, 303.0, n), "Q_rad": rng.uniform(0.0, 200.0, n)}
     p, lbw, ubw, w0 = prob.to_kernel(*fleet_nlp_inputs(prob, cv, vals))
+    stats, wall, kernel_ms = _timed_batch(be, prob, p, lbw, ubw, w0, n, args, dev)
+    ok = sum(1 for s in stats if s["success"])
+    return {
+        "workload": "C5: three-zone NARX room agents (casadi_admm_nn, 2 ANNs 9/8->32 sigmoid->1, "
+                    "N=24 ts=1800, lifted lag window), one batched local ADMM solve per step",
+        "zones_per_gpu": n, "nlp": prob.nlp.nlp_dims(),
+        "kernel_nlp": {"nw": prob.nlp.kernel_nw, "ng": prob.nlp.kernel_ng, "np": prob.nlp.kernel_np},
+        "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
+        "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
+        "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
+        "statuses": sorted({int(s["status"]) for s in stats}),
+        "mean_factorizations": float(np.mean([s["n_factorizations"] for s in stats])),
+        "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
+                                      max(1, np.sum([s["n_factorizations"] for s in stats]))),
+        "kernel_ms": kernel_ms,
+    }
+
+
+def _timed_batch(be, prob, p, lbw, ubw, w0, n, args, dev):
+    """W untimed + K timed batched solves of one fleet (cold start each step);
+    returns (per-agent stats of the last step, wall seconds, kernel ms per step)."""
+    import torch
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+
     native = be._native()
     native.reserve(n)
     T = lambda a: torch.as_tensor(a, device=dev).contiguous()  # noqa: E731
@@ -202,21 +224,38 @@ def nn_bench(args, world, rank, dev):
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    stats = stats_to_dicts(st.cpu().numpy().tobytes())
+    return stats_to_dicts(st.cpu().numpy().tobytes()), wall, ev0.elapsed_time(ev1) / args.steps
+
+
+def mhe_bench(args, world, rank, dev):
+    """Moving horizon estimation fleet (backend casadi_mhe, `examples/Estimators/
+    mhe_example.py`: RNGRoom, N=15, ts=200, Legendre d=2, estimating the capacity
+    factor in [5, 6]): ``--mhe-agents`` estimators per GPU, each with its own
+    noisy zone-temperature history (true factor 5.5, noise sigma 0.05 K), one
+    batched solve per step, cold start."""
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+
+    n = args.mhe_agents
+    be, cv = bm.mhe_room(solver_options={"ipopt": {"tol": args.tol, "max_iter": 500}})
+    prob = be.problem
+    p, lbw, ubw, w0 = fleet_nlp_inputs(prob, cv, {"weight_T": np.ones(n)})
+    rng = np.random.default_rng(20261015 + 6 + rank)
+    meas = prob.nlp.par_groups["measured_states"].index  # [2, N*d] positions in p
+    p[:, meas[0]] += rng.normal(scale=0.05, size=(n, meas.shape[1]))
+    p, lbw, ubw, w0 = prob.to_kernel(p, lbw, ubw, w0)
+    stats, wall, kernel_ms = _timed_batch(be, prob, p, lbw, ubw, w0, n, args, dev)
     ok = sum(1 for s in stats if s["success"])
     return {
-        "workload": "C5: three-zone NARX room agents (casadi_admm_nn, 2 ANNs 9/8->32 sigmoid->1, "
-                    "N=24 ts=1800, lifted lag window), one batched local ADMM solve per step",
-        "zones_per_gpu": n, "nlp": prob.nlp.nlp_dims(),
+        "workload": "MHE: RNGRoom estimator fleet (casadi_mhe, collocation Legendre d=2, N=15, ts=200, "
+                    "theta in [5,6], noisy T history), one batched solve per step",
+        "agents_per_gpu": n, "nlp": prob.nlp.nlp_dims(),
         "kernel_nlp": {"nw": prob.nlp.kernel_nw, "ng": prob.nlp.kernel_ng, "np": prob.nlp.kernel_np},
         "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
         "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
         "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
-        "statuses": sorted({int(s["status"]) for s in stats}),
-        "mean_factorizations": float(np.mean([s["n_factorizations"] for s in stats])),
-        "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
-                                      max(1, np.sum([s["n_factorizations"] for s in stats]))),
-        "kernel_ms": ev0.elapsed_time(ev1) / args.steps,
+        "factorisation": "sequential block chain (forced, DESIGN 6a)",
+        "kernel_ms": kernel_ms,
     }
 
 
@@ -276,6 +315,7 @@ def main():
     ap.add_argument("--nn-zones", type=int, default=1024, help="C5 NARX zones per GPU (0: skip)")
     ap.add_argument("--c5-blocks", type=int, default=342, help="C5 ADMM blocks (3 zones+AHU+CCA) per GPU (0: skip)")
     ap.add_argument("--c5-iters", type=int, default=50)
+    ap.add_argument("--mhe-agents", type=int, default=4096, help="MHE estimators per GPU (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -343,6 +383,7 @@ def main():
     admm = admm_bench(args, world, rank, dev) if args.admm_agents > 0 else None
     nn = nn_bench(args, world, rank, dev) if args.nn_zones > 0 else None
     c5 = c5_admm_bench(args, world, rank, dev) if args.c5_blocks > 0 else None
+    mhe = mhe_bench(args, world, rank, dev) if args.mhe_agents > 0 else None
     stats = stats_to_dicts(st.cpu().numpy().tobytes())
     n_ok = sum(1 for s in stats if s["success"])
     arr = {"iter": np.array([s["iter_count"] for s in stats]),
@@ -410,6 +451,8 @@ def main():
             out["narx"] = nn
         if c5 is not None:
             out["narx_admm"] = c5
+        if mhe is not None:
+            out["mhe"] = mhe
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(p, lbw, ubw, w0, args.tol)

@@ -107,3 +107,16 @@ def test_result_layout_matches_reference_shape():
         ("parameter", "T_in"), ("parameter", "load"), ("parameter", "T_upper")]
     assert len(lay.variable_grid_indices["mDot"]) == 15
     assert len(lay.variable_grid_indices["T"]) == 46  # (d+1)N+1 (test_casadi_backend.py:127-132)
+
+
+def test_rank_deficient_stage_interiors_use_the_block_chain():
+    """Stage interiors whose equality rows V cannot satisfy (more coupled rows than
+    stage variables can absorb) are compiled for the sequential block chain; the
+    benchmark structures keep the stage-parallel elimination."""
+    want = {"one_room": False, "admm_room": False, "exchange_room": False, "room_nn": False,
+            "one_room_radau": False, "one_room_du": True, "exchange_room_rk": False,
+            "mhe_room": True, "mhe_room_u": True}
+    for name, chain in want.items():
+        gen = configs.CASES[name]().backend.problem.gen
+        assert gen.block_chain_only == chain, name
+        assert ("#define MPCX_FORCE_BLOCK_CHAIN 1" in gen.source) == chain, name

@@ -53,18 +53,30 @@ class MI355XBackendConfig(BackendConfig):
     save_only_stats: bool = False
 
 
-def ipopt_options_to_kernel(options: dict) -> dict:
-    """Map IPOPT-style options (nested or dotted) onto kernel option names."""
+#: solvers the kernel stands in for: both are primal-dual interior-point methods on
+#: the same NLP (fatrop exploits the stage structure like the kernel does;
+#: `casadi_utils.py:163-217`); the others (SQP, QP, MINLP) are not on this path
+KERNEL_SOLVERS = ("ipopt", "fatrop")
+
+
+def ipopt_options_to_kernel(options: dict, solver: str = "ipopt") -> dict:
+    """Map IPOPT-style options (nested or dotted) onto kernel option names.
+
+    ``solver="fatrop"`` reads the nested ``"fatrop"`` dict instead (the reference
+    merges it into fatrop's own options, `casadi_utils.py:163-189`; its defaults
+    max_iter=100, tol=1e-4 equal the IPOPT ones); fatrop's ``structure_detection``
+    and ``equality`` flags describe what the kernel derives itself."""
     opts = dict(REFERENCE_IPOPT_DEFAULTS)
-    nested = dict(options.get("ipopt", {}))
+    nested = dict(options.get(solver, {}))
     for k, v in options.items():
-        if k.startswith("ipopt."):
-            nested[k[len("ipopt."):]] = v
+        if k.startswith(f"{solver}."):
+            nested[k[len(solver) + 1:]] = v
     aliases = {"mu_linear_decrease_factor": "kappa_mu", "mu_superlinear_decrease_power": "theta_mu",
                "barrier_tol_factor": "kappa_eps", "bound_mult_init_val": "bound_mult_init_val",
                "constr_mult_init_max": "constr_mult_init_max",
                "alpha_min_frac": "alpha_min_frac"}
     ignored = {"print_level", "sb", "print_time", "linear_solver", "hessian_approximation",
+               "structure_detection", "equality", "verbose", "record_time", "expand",
                "acceptable_obj_change_tol", "acceptable_dual_inf_tol", "acceptable_constr_viol_tol",
                "acceptable_compl_inf_tol"}
     for k, v in nested.items():
@@ -92,7 +104,11 @@ class MI355XBackend(OptimizationBackend):
         self.problem: Optional[CompiledProblem] = None
         self.system = None
         self._remembered: Optional[Dict[str, np.ndarray]] = None
-        self.solver_options = ipopt_options_to_kernel(self.config.solver.options)
+        name = getattr(self.config.solver.name, "value", self.config.solver.name)
+        if name not in KERNEL_SOLVERS:
+            raise ValueError(f"solver {name!r} is not available on the MI355X backend "
+                             f"(interior-point solvers {KERNEL_SOLVERS} run on the batched kernel)")
+        self.solver_options = ipopt_options_to_kernel(self.config.solver.options, name)
 
     # -- setup (`core/casadi_backend.py:108-131`) --------------------------------
     def setup_optimization(self, var_ref):

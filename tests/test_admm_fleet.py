@@ -79,7 +79,7 @@ def test_coordinated_consensus_round_matches_oracle():
 
 
 def test_coordinated_closed_loop_rounds_match_oracle():
-    """Three control steps of the coordinator with new room measurements between
+    """Two control steps of the coordinator with new room measurements between
     them: mean update from the last round's locals, shift of means
     and multipliers by one interval (`admm_coordinator.py:278-279`,
     `admm_datatypes.py:275-331`), warm-started local solves, varying penalty
@@ -92,7 +92,7 @@ def test_coordinated_closed_loop_rounds_match_oracle():
               penalty_change_threshold=1.5, penalty_change_factor=1.3)
     be_r, cv_r = bm.admm_room(N=N)
     state = None
-    for step in range(3):
+    for step in range(2):
         rooms = [(d, T0 - 0.7 * step) for d, T0 in bm.C2_ROOMS]
         if step:
             p, lbw, ubw, _ = bm._class_inputs(be_r, cv_r, {"T": [r[1] for r in rooms],

@@ -259,6 +259,47 @@ def mhe_bench(args, world, rank, dev):
     }
 
 
+def c2_admm_bench(args, world, rank, dev):
+    """C2 scaled (BASELINE.json configs[1]): ``--c2-blocks`` blocks per GPU of
+    (4 rooms + air handler) of `examples/4_Room_ADMM_Coordinator`, coordinated
+    consensus ADMM run to consensus with the example's coordinator settings
+    (`configs/coordinator.json`: rho=0.4, admm_iter_max=40, absolute criterion
+    primal_tol=0.002, dual_tol=0.1), reference IPOPT defaults for the local solves;
+    the consensus groups are block-local, so ranks need no data-path collective
+    beyond the residual totals."""
+    import torch
+    import torch.distributed as dist
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.admm.fleet import ADMMFleet
+
+    nb = args.c2_blocks
+    classes = bm.c2_fleet_classes(n_blocks=nb, N=10, seed=20261015 + 1, block_offset=rank * nb,
+                                  solver_options={"ipopt": {}})
+    fleet = ADMMFleet(classes, device=dev, comm="default" if world > 1 else None)
+    for c in classes:
+        c.native.reserve(c.n)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    out = fleet.run_coordinated(0.4, admm_iter_max=40, use_relative_tolerances=False,
+                                primal_tol=0.002, dual_tol=0.1)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    return {
+        "workload": "C2 scaled: 4-room + air-handler blocks (casadi_admm collocation d=3, N=10, ts=60), "
+                    "coordinated consensus, rho=0.4, abs tol 0.002/0.1, iter max 40",
+        "blocks_per_gpu": nb, "agents_per_gpu": 5 * nb,
+        "admm_iterations": out["iterations"], "converged": out["converged"],
+        "admm_iters_per_s": out["iterations"] / wall, "wall_s": wall,
+        "agent_solves_per_s": out["converged_solves"] / wall,
+        "converged_solve_fraction": out["converged_solves"] / (5 * nb * out["iterations"]),
+        "final_residuals": [out["records"][-1].primal_residual, out["records"][-1].dual_residual],
+    }
+
+
 def c5_admm_bench(args, world, rank, dev):
     """C5 as the example runs it: coordinated consensus ADMM over ``--c5-blocks``
     blocks per GPU of (3 NARX zones + AHU + CCA supply)
@@ -316,6 +357,7 @@ def main():
     ap.add_argument("--c5-blocks", type=int, default=342, help="C5 ADMM blocks (3 zones+AHU+CCA) per GPU (0: skip)")
     ap.add_argument("--c5-iters", type=int, default=50)
     ap.add_argument("--mhe-agents", type=int, default=4096, help="MHE estimators per GPU (0: skip)")
+    ap.add_argument("--c2-blocks", type=int, default=1024, help="C2 4-room+AHU blocks per GPU (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -383,6 +425,7 @@ def main():
     admm = admm_bench(args, world, rank, dev) if args.admm_agents > 0 else None
     nn = nn_bench(args, world, rank, dev) if args.nn_zones > 0 else None
     c5 = c5_admm_bench(args, world, rank, dev) if args.c5_blocks > 0 else None
+    c2 = c2_admm_bench(args, world, rank, dev) if args.c2_blocks > 0 else None
     mhe = mhe_bench(args, world, rank, dev) if args.mhe_agents > 0 else None
     stats = stats_to_dicts(st.cpu().numpy().tobytes())
     n_ok = sum(1 for s in stats if s["success"])
@@ -451,6 +494,8 @@ def main():
             out["narx"] = nn
         if c5 is not None:
             out["narx_admm"] = c5
+        if c2 is not None:
+            out["c2_admm"] = c2
         if mhe is not None:
             out["mhe"] = mhe
         if world == 1 and not args.no_cpu_baseline:

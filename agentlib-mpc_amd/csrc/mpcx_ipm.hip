@@ -1733,7 +1733,6 @@ __device__ __noinline__ LSResult line_search(const Agent a, KArgs* argp, double 
   // options from the kernarg segment (scalar loads); a by-value LSOpt exceeds the
   // argument registers and would be passed through scratch
   KArgs& ka = *argp;
-#define o (ka.opt)
   const int lane = a.lane;
   double xr[VS], dxr[VS], lor[VS], hir[VS];
 #pragma unroll
@@ -1754,13 +1753,13 @@ __device__ __noinline__ LSResult line_search(const Agent a, KArgs* argp, double 
   }
   double amin;
   if (gphid < 0 && theta <= theta_min)
-    amin = o.alpha_min_frac * fmin(fmin(o.gamma_theta, o.gamma_phi * theta / (-gphid)),
-                                   o.delta * pow(theta, o.s_theta) / pow(-gphid, o.s_phi));
+    amin = ka.opt.alpha_min_frac * fmin(fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid)),
+                                   ka.opt.delta * pow(theta, ka.opt.s_theta) / pow(-gphid, ka.opt.s_phi));
   else if (gphid < 0)
-    amin = o.alpha_min_frac * fmin(o.gamma_theta, o.gamma_phi * theta / (-gphid));
+    amin = ka.opt.alpha_min_frac * fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid));
   else
-    amin = o.alpha_min_frac * o.gamma_theta;
-  if (!(amin > 0.0)) amin = o.alpha_min_frac * o.gamma_theta;  // NaN guard
+    amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;
+  if (!(amin > 0.0)) amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;  // NaN guard
   LSResult res;
   res.alpha = alpha0;
   res.accepted = 0;
@@ -1810,12 +1809,12 @@ __device__ __noinline__ LSResult line_search(const Agent a, KArgs* argp, double 
       if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
     bool ftype = false;
     if (okt) {
-      const bool switching = gphid < 0 && alpha * pow(-gphid, o.s_phi) > o.delta * pow(theta, o.s_theta);
+      const bool switching = gphid < 0 && alpha * pow(-gphid, ka.opt.s_phi) > ka.opt.delta * pow(theta, ka.opt.s_theta);
       if (theta <= theta_min && switching) {
-        okt = tr.phi <= phi + o.eta_phi * alpha * gphid;
+        okt = tr.phi <= phi + ka.opt.eta_phi * alpha * gphid;
         ftype = true;
       } else {
-        okt = tr.theta <= (1.0 - o.gamma_theta) * theta || tr.phi <= phi - o.gamma_phi * theta;
+        okt = tr.theta <= (1.0 - ka.opt.gamma_theta) * theta || tr.phi <= phi - ka.opt.gamma_phi * theta;
         ftype = false;
       }
     }
@@ -1827,7 +1826,6 @@ __device__ __noinline__ LSResult line_search(const Agent a, KArgs* argp, double 
   }
   res.tr = tr;
   return res;
-#undef o
 }
 
 // take the last trial point (xt, gt in LDS) and the multiplier steps

@@ -128,3 +128,35 @@ def test_batch_of_distinct_agents_matches_individual_solves():
         single = c.backend.solve(0.0, c.current_vars)
         np.testing.assert_allclose(r["T"], single["T"], rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(r.stats["obj"], single.stats["obj"], rtol=1e-12)
+
+
+def test_gpu_c3_fleet_matches_c_oracle():
+    """Bench-shaped parity: 512 agents of the C3 fleet (bench.py inputs, tol 1e-8)
+    solved by the kernel and by the C restatement of the oracle IPM
+    (`oracle/c/ipm_oracle.c`): same return status per agent; objectives rel 1e-6
+    and solutions rel 1e-5 where both converge."""
+    import bench
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+    from oracle import cbuild
+
+    n = 512
+    be, cv = bm.one_room(solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
+    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261015 + 2))
+    native = be._native()
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    tw = T(w0)
+    st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device="cuda")
+    native.solve(T(p), T(lbw), T(ubw), tw, stats=st)
+    torch.cuda.synchronize()
+    gw = tw.cpu().numpy()
+    gs = stats_to_dicts(st.cpu().numpy().tobytes())
+    cbuild.build()
+    cw, cs, _ = cbuild.solve_room_fleet(p, lbw, ubw, w0, tol=1e-8, threads=8)
+    assert [s["status"] for s in gs] == [s["status"] for s in cs]
+    ok = np.array([s["status"] == 0 for s in gs])
+    assert ok.mean() > 0.99
+    np.testing.assert_allclose([s["obj"] for s, o in zip(gs, ok) if o], [s["obj"] for s, o in zip(cs, ok) if o],
+                               rtol=RTOL_OBJ)
+    np.testing.assert_allclose(gw[ok], cw[ok], rtol=RTOL_TRAJ, atol=1e-7 * 300.0)

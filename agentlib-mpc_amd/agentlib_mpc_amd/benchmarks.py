@@ -258,6 +258,29 @@ def mhe_room(N=15, ts=200.0, d=2, theta_lb=5.0, theta_ub=6.0, theta_guess=None, 
     return be, cv
 
 
+def rng_room_mpc(N=15, T0=25.0, T_wall0=27.0, u_prev=0.02, T_upper=23.0, load=0.0, solver_options=TIGHT):
+    """The MPC module of `examples/Estimators/mhe_example.py:230-268`: backend
+    ``casadi`` on the two-state RNGRoom (zone + wall, one control: nx > nu, so
+    the kernel factors it with the block chain), N=15, ts=200, Legendre d=2."""
+    be = create_optimization_backend({
+        "type": "casadi",
+        "model": {"type": "agentlib_mpc_amd.models.examples.RNGRoom"},
+        "discretization_options": {"collocation_order": 2, "collocation_method": "legendre",
+                                   "prediction_horizon": N, "time_step": 200},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    be.setup_optimization(VariableReference(
+        states=["T", "T_wall"], controls=["mDot"], inputs=["load", "T_in", "T_ambient", "T_upper"],
+        parameters=["full_capacity_from_volume_factor"], outputs=[]))
+    cv = {
+        "T": V("T", T0, 15.0, 30.0), "T_wall": V("T_wall", T_wall0), "mDot": V("mDot", u_prev, 0.0, 0.1),
+        "load": V("load", load), "T_in": V("T_in", 17.0), "T_ambient": V("T_ambient", 28.0),
+        "T_upper": V("T_upper", T_upper),
+        "full_capacity_from_volume_factor": V("full_capacity_from_volume_factor", 5.5, 1.0, 50.0),
+    }
+    return be, cv
+
+
 ROOM_NN_COUPLINGS = (("T_v", 294.15, 285.0, 308.0), ("T_ahu", 295.0, 285.0, 308.0),
                      ("T_CCA_out", 294.15, 285.0, 310.0), ("T_air_out", 294.0, 285.0, 310.0))
 
@@ -396,6 +419,7 @@ def compile_all(verbose: bool = False):
     variants["tz_cca_n8"] = lambda: tz_cca(N=8)
     variants["mhe_room"] = lambda: mhe_room()
     variants["mhe_room_u"] = lambda: mhe_room(estimate="mDot")
+    variants["rng_room_mpc"] = lambda: rng_room_mpc()
     for name, fn in variants.items():
         be, _ = fn()
         paths[name] = be.problem.compile()

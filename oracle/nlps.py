@@ -907,3 +907,93 @@ def mhe_room_inputs(prob, meas_T, meas_Tw, N=15, d=2, w_T=1.0, w_Tw=0.0, theta_l
         elif name.startswith("T_slack@"):  # RNGRoomMHE: slack bounded below
             lbw[i] = slack_lb  # guess 0.5 (lb + inf) = inf -> 0 (nan_to_num, posinf=0)
     return p, lbw, ubw, w0
+
+
+# ---------------------------------------------------------------------------
+# two-state zone + wall MPC (nx = 2 > nu = 1): backend "casadi", collocation
+# ---------------------------------------------------------------------------
+
+def rng_room_mpc(N=15, ts=200.0, d=2) -> OracleProblem:
+    """`casadi_/full.py:36-98` on the MPC module of `examples/Estimators/mhe_example.py:230-268`
+    (RNGRoom: states T, T_wall; control mDot; T_slack auxiliary; 3 outputs).
+    w = [T_0, Tw_0, {mDot_k, for j: (T, Tw, T_slack, T_out, cooling, pw2z)_kj, T_{k+1}, Tw_{k+1}}];
+    g_k = [x_{k+1} - x_end (T, Tw), {ts*ode_j - xp_j (T, Tw), T + T_slack, T_out - T,
+           cooling - cp mDot (T_in - T), pw2z - (Tw - T)/RZ}_j];
+    p = [T0, Tw0, u_prev, cp, rho, theta, C_Wall, RZone_Wall, R_hull_amb, V, s_T, r_mDot,
+         {load, T_in, T_ambient, T_upper}_kj];
+    f = sum_kj B_j ts (r_mDot mDot + s_T T_slack^2)."""
+    tau, B, C, D = collocation(d, "legendre")
+    nb = 1 + 6 * d + 2
+    n = 2 + N * nb
+    m = N * (2 + 6 * d)
+    npg, nps = 12, 4 * d
+    names = ["T@0", "T_wall@0"]
+    for k in range(N):
+        names.append(f"mDot@{k}")
+        for j in range(d):
+            names += [f"{v}@{k},{j}" for v in ("T", "T_wall", "T_slack", "T_out", "cooling", "pw2z")]
+        names += [f"T@{k + 1}", f"T_wall@{k + 1}"]
+
+    def f(w, p):
+        s_T, r = p[10], p[11]
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = 2 + k * nb
+            u = w[o]
+            for j in range(d):
+                tot = tot + B[j + 1] * ts * (r * u + s_T * w[o + 1 + 6 * j + 2] ** 2)
+        return tot
+
+    def g(w, p):
+        cp, rho, th, Cw, Rzw, Rha, Vz = p[3], p[4], p[5], p[6], p[7], p[8], p[9]
+        out = []
+        xk = [w[0], w[1]]
+        for k in range(N):
+            o = 2 + k * nb
+            u = w[o]
+            X = [[w[o + 1 + 6 * j], w[o + 2 + 6 * j]] for j in range(d)]
+            x1 = [w[o + nb - 2], w[o + nb - 1]]
+            for s_ in range(2):
+                out.append(x1[s_] - (D[0] * xk[s_] + sum(D[j + 1] * X[j][s_] for j in range(d))))
+            for j in range(d):
+                q = o + 1 + 6 * j
+                ps = npg + k * nps + 4 * j
+                load, T_in, T_amb = p[ps], p[ps + 1], p[ps + 2]
+                T, Tw = X[j]
+                pw = (Tw - T) / Rzw
+                cool = cp * u * (T_in - T)
+                ode = [(load + cool + pw) / (rho * cp * Vz * th), -((Tw - T_amb) / Rha + pw) / Cw]
+                for s_ in range(2):
+                    xp = C[0, j + 1] * xk[s_] + sum(C[r_ + 1, j + 1] * X[r_][s_] for r_ in range(d))
+                    out.append(ts * ode[s_] - xp)
+                out += [T + w[q + 2], w[q + 3] - T, w[q + 4] - cool, w[q + 5] - pw]
+            xk = x1
+        return torch.stack(out)
+
+    def ubg(p):
+        u = np.zeros(m)
+        for k in range(N):
+            for j in range(d):
+                u[k * (2 + 6 * d) + 2 + 6 * j + 2] = p[npg + k * nps + 4 * j + 3]
+        return u
+
+    return OracleProblem("rng_room_mpc", n, m, npg + N * nps, f, g, lambda p: np.zeros(m), ubg, names)
+
+
+def rng_room_mpc_inputs(prob, N=15, d=2, T0=25.0, Tw0=27.0, u_prev=0.02, theta=5.5, load=0.0, T_in=17.0,
+                        T_amb=28.0, T_upper=23.0, T_lb=15.0, T_ub=30.0, u_lb=0.0, u_ub=0.1):
+    p = [T0, Tw0, u_prev, 1005.0, 1.2, theta, 4_569_348.0, 0.0129, 0.1128, 59.0, 1.0, 1.0]
+    p += [load, T_in, T_amb, T_upper] * (N * d)
+    p = np.array(p, float)
+    lbw, ubw, w0 = np.full(prob.n, -np.inf), np.full(prob.n, np.inf), np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        v = name.split("@")[0]
+        if v == "T":
+            lbw[i], ubw[i], w0[i] = T_lb, T_ub, T0
+        elif v == "T_wall":
+            w0[i] = Tw0
+        elif v == "mDot":
+            lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
+    lbw[0] = ubw[0] = w0[0] = T0
+    lbw[1] = ubw[1] = w0[1] = Tw0
+    return p, lbw, ubw, w0

@@ -147,6 +147,15 @@ def mhe_room(**kw) -> Case:
     return Case(be, cv, prob, nlps.mhe_room_inputs(prob, meas[0], meas[1], N=N, d=d, **o))
 
 
+def rng_room_mpc(**kw) -> Case:
+    be, cv = bm.rng_room_mpc(**kw)
+    prob = nlps.rng_room_mpc(N=kw.get("N", 15))
+    o = {k: kw[k] for k in ("T0", "u_prev", "T_upper", "load") if k in kw}
+    if "T_wall0" in kw:
+        o["Tw0"] = kw["T_wall0"]
+    return Case(be, cv, prob, nlps.rng_room_mpc_inputs(prob, N=kw.get("N", 15), **o))
+
+
 CASES: Dict[str, Callable[..., Case]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -161,6 +170,7 @@ CASES: Dict[str, Callable[..., Case]] = {
     "one_room_du": one_room_du,
     "one_room_switch": one_room_switch,
     "mhe_room": mhe_room,
+    "rng_room_mpc": rng_room_mpc,
     # estimating mDot per interval needs the wall temperature measured too (else mDot
     # and the unmeasured wall state trade off and the minimiser is not unique)
     "mhe_room_u": lambda **kw: mhe_room(estimate="mDot", **{"w_T_wall": 1.0, **kw}),

@@ -69,6 +69,10 @@ def _cuda():
     ("mhe_room", {"theta": 7.0}),      # true value outside the bounds: estimate at ub
     ("mhe_room_u", {}),                # estimated input per interval, no global parameter
     ("mhe_room_u", {"noise": 0.05, "seed": 4}),
+    # two states, one control (nx > nu): block-chain factorisation
+    ("rng_room_mpc", {}),
+    ("rng_room_mpc", {"T0": 27.0, "T_upper": 22.0, "load": 300.0}),
+    ("rng_room_mpc", {"T0": 23.5, "T_upper": 24.5, "load": 50.0, "u_prev": 0.0}),
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)

@@ -28,6 +28,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "one_room_switch": (76, 60, 53),  # time-dependent conditional objective, MS Euler
     "mhe_room": (3 + 15 * 14, 15 * 14, 10 + 15 * 9),  # MHE: x_0, theta free; 6 vars per point
     "mhe_room_u": (2 + 15 * 15, 15 * 14, 11 + 15 * 8),  # MHE estimating mDot per interval
+    "rng_room_mpc": (2 + 15 * 15, 15 * 14, 12 + 15 * 8),  # two-state zone + wall MPC (nx > nu)
 }
 
 
@@ -115,7 +116,7 @@ def test_rank_deficient_stage_interiors_use_the_block_chain():
     benchmark structures keep the stage-parallel elimination."""
     want = {"one_room": False, "admm_room": False, "exchange_room": False, "room_nn": False,
             "one_room_radau": False, "one_room_du": True, "exchange_room_rk": False,
-            "mhe_room": True, "mhe_room_u": True}
+            "mhe_room": True, "mhe_room_u": True, "rng_room_mpc": True}
     for name, chain in want.items():
         gen = configs.CASES[name]().backend.problem.gen
         assert gen.block_chain_only == chain, name

@@ -65,3 +65,48 @@ def test_coordinator_residual_file(tmp_path):
     assert list(df.columns) == ["primal_residual", "dual_residual", "penalty_parameter", "wall_time"]
     assert [ast.literal_eval(i) for i in df.index] == [(0.0, 0), (0.0, 1), (60.0, 0)]
     np.testing.assert_allclose(df["dual_residual"], [2.0, 0.25, 2.0])
+
+
+def test_analysis_readers_on_backend_files(tmp_path):
+    """`utils/analysis.py` readers on the files the backends write (`analysis.py:17-290`)."""
+    from agentlib_mpc_amd.utils import analysis
+
+    be, cv = bm.one_room(N=4)
+    f = tmp_path / "room.csv"
+    be.config.results_file, be.config.save_results = f, True
+    for now in (100.0, 400.0):
+        be.save_result_df(_results(be, cv, now), now)
+    df = analysis.load_mpc(f)
+    assert isinstance(df.index, pd.MultiIndex) and analysis.get_time_steps(df) == [100.0, 400.0]
+    st = analysis.load_mpc_stats(f)
+    assert st is not None and st["iter_count"].tolist() == [7, 7]
+    assert analysis.load_mpc_stats(tmp_path / "missing.csv") is None
+    # prediction made at the step closest to t=290 (offset "auto": steps at 0 and 300)
+    T = analysis.mpc_at_time_step(df, 290.0, variable="T")
+    grid = df["variable"]["T"].loc[400.0]
+    np.testing.assert_allclose(T.values, grid.values)
+    np.testing.assert_allclose(T.index.values, grid.index.values + 300.0)
+    first = analysis.first_vals_at_trajectory_index(df["variable"]["T"])
+    np.testing.assert_allclose(first.values, [grid.iloc[0]] * 2)
+    last = analysis.last_vals_at_trajectory_index(df["variable"]["T"].dropna())
+    assert list(last.index) == [100.0, 400.0]
+    hrs = analysis.convert_multi_index(df, "hours")
+    np.testing.assert_allclose(sorted(set(hrs.index.get_level_values(0))), [100 / 3600, 400 / 3600])
+
+
+def test_analysis_readers_on_admm_files(tmp_path):
+    from agentlib_mpc_amd.utils import analysis
+
+    be, cv = bm.exchange_room(N=4)
+    f = tmp_path / "admm.csv"
+    be.config.results_file, be.config.save_results = f, True
+    r = _results(be, cv)
+    for now, n_it in ((0.0, 3), (120.0, 2), (240.0, 1)):
+        for _ in range(n_it):
+            be.save_result_df(r, now)
+    df = analysis.load_admm(f)
+    assert analysis.get_number_of_iterations(df) == {0.0: 3, 120.0: 2, 240.0: 1}
+    last_it = analysis.admm_at_time_step(df, time_step=0.0, iteration=-1)
+    first_it = analysis.admm_at_time_step(df, time_step=0.0, iteration=0)
+    pd.testing.assert_frame_equal(last_it, first_it)
+    assert last_it.index[0] == df.loc[(0.0, 2)].index[0]

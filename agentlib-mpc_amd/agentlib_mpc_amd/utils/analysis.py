@@ -20,9 +20,7 @@ from pandas.api.types import is_float_dtype
 
 from agentlib_mpc_amd.data_structures.mpc_datamodels import stats_path
 
-# `agentlib_mpc/utils/__init__.py:7-13`
-TimeConversionTypes = Literal["seconds", "minutes", "hours", "days"]
-TIME_CONVERSION: Dict[str, int] = {"seconds": 1, "minutes": 60, "hours": 3600, "days": 86400}
+from agentlib_mpc_amd.utils import TIME_CONVERSION, TimeConversionTypes
 
 SimulationTime = NewType("SimulationTime", float)
 

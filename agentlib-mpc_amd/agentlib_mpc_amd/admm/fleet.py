@@ -18,6 +18,13 @@ follow, step for step:
   shift and send locals and multipliers (:329-375), mean / mean-diff from the
   shifted locals, then ``max_iterations`` × (solve → mean → multiplier update).
 
+Blocks: the participation graph (agents — aliases) splits into connected
+components, each the counterpart of ONE reference coordinator (e.g. the
+4-room + air-handler blocks of a scaled C2 fleet).  Coordinated runs keep a
+stopping test, a penalty parameter and an iteration count per block and freeze
+a block (no solves, no updates) once it has converged, exactly as that block's
+own ``ADMMCoordinator`` would stop (`admm_coordinator.py:284-309`).
+
 Multi-GPU: one process per GPU, each holding a contiguous slice of every
 class's agents.  Aliases whose participants live on several ranks are "global
 groups"; their per-(group, t) moments (and the residual partial sums of the
@@ -158,9 +165,9 @@ class FleetClass:
 class IterationRecord:
     primal_residual: float
     dual_residual: float
-    penalty: float
+    penalty: float                     # after the penalty variation (admm_coordinator.py:396-397)
     converged_solves: Optional[int] = None
-    wall_time: Optional[float] = None  # seconds of this ADMM iteration (coordinated runs)
+    wall_time: Optional[float] = None  # seconds since the start of the round (:270, :400-402)
 
 
 class ADMMFleet:
@@ -199,6 +206,7 @@ class ADMMFleet:
         self._allocate()
         self.history: List[IterationRecord] = []
         self.rounds = 0
+        self._masked = False
 
     # ------------------------------------------------------------------ setup
     def _build_groups(self):
@@ -242,6 +250,7 @@ class ADMMFleet:
         for r, (al, ci, si, a) in enumerate(parts):
             counts[gid[al]] += 1
             rows[(ci, si, a)] = r
+        self._build_blocks(parts, order, gid)
         self.R = len(parts)
         self.gstart = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
         self.max_rows = int(counts.max()) if G else 0
@@ -251,6 +260,64 @@ class ADMMFleet:
             for si, s in enumerate(c.slots):
                 self.slot_rows[(ci, si)] = np.array([rows[(ci, si, a)] for a in range(c.n)], np.int32)
                 self.slot_groups[(ci, si)] = np.array([gid[al] for al in s.aliases], np.int32)
+
+    def _build_blocks(self, parts, order, gid):
+        """Connected components of the agent-alias participation graph (over all ranks):
+        one block per reference coordinator."""
+        parent = {al: al for al in order}
+
+        def find(a):
+            while parent[a] != a:
+                parent[a] = parent[parent[a]]
+                a = parent[a]
+            return a
+
+        def union(a, b):
+            ra, rb = find(a), find(b)
+            if ra != rb:
+                parent[max(ra, rb)] = min(ra, rb)
+
+        by_agent: Dict[tuple, List[str]] = {}
+        for al, ci, si, a in sorted(parts, key=lambda x: (x[1], x[3], x[2])):  # class, agent, slot
+            by_agent.setdefault((ci, a), []).append(al)
+        seen: List[str] = []  # aliases in order of first appearance (class, agent)
+        for als in by_agent.values():
+            seen.extend(als)
+            for al in als[1:]:
+                union(als[0], al)
+        if self.world > 1:
+            comps: Dict[str, List[str]] = {}
+            for al in seen:
+                comps.setdefault(find(al), []).append(al)
+            gathered = [None] * self.world
+            self.dist.all_gather_object(gathered, list(comps.values()), group=self.group)
+            seen = []
+            for lst in gathered:  # rank order: the same block numbering on every rank
+                for comp in lst:
+                    seen.extend(comp)
+                    for al in comp:
+                        parent.setdefault(al, al)
+                    for al in comp[1:]:
+                        union(comp[0], al)
+        roots = list(dict.fromkeys(find(al) for al in seen + list(order)))
+        bid = {r: i for i, r in enumerate(roots)}
+        self._block_id = {al: bid[find(al)] for al in parent}
+        self.n_blocks = max(len(roots), 1)
+        self.block_of_group = np.array([bid[find(al)] for al in order], np.int32)
+        self.block_aliases = [[] for _ in range(self.n_blocks)]
+        for al in sorted(parent):
+            self.block_aliases[bid[find(al)]].append(al)
+        self.agent_blocks = {}
+        for ci, c in enumerate(self.classes):
+            blk = np.zeros(c.n, np.int32)
+            for (cj, a), als in by_agent.items():
+                if cj == ci:
+                    blk[a] = bid[find(als[0])]
+            self.agent_blocks[ci] = blk
+
+    def block_index(self, alias: str) -> int:
+        """Block (coordinator) of an alias."""
+        return self._block_id[alias]
 
     def _allocate(self):
         t = self.torch
@@ -265,9 +332,16 @@ class ADMMFleet:
         self.EXCH = t.as_tensor(self.exchange_flags if G else np.zeros(1, np.int32), dtype=i32, device=dev)
         self.GSTART = t.as_tensor(self.gstart, dtype=i32, device=dev)
         self.S = NMOM * T + 1
-        self.MOM = t.zeros(self.ops.moments_size(max(G, 1), T), dtype=f64, device=dev)
+        nb = self.n_blocks
+        self.MOM = t.zeros(self.ops.moments_size(max(G, 1), nb, T), dtype=f64, device=dev)
         self.totals_off = self.n_global * self.S
-        self.reduce_len = self.n_global * self.S + ADMM_TOTALS
+        self.reduce_len = self.n_global * self.S + ADMM_TOTALS * nb
+        # per-block coordinator state on the device: penalty, group freeze mask
+        self.BLOCK_G = t.as_tensor(self.block_of_group if G else np.zeros(1, np.int32), dtype=i32, device=dev)
+        self.RHO_B = t.zeros((nb, 1), dtype=f64, device=dev)
+        self.RHO_G = t.zeros(max(G, 1), dtype=f64, device=dev)
+        self.ACTIVE_G = t.ones(max(G, 1), dtype=i32, device=dev)
+        self._rho_col = t.zeros(1, dtype=i32, device=dev)
         for ci, c in enumerate(self.classes):
             c.P = t.as_tensor(c.p0, device=dev).contiguous()
             c.LB = t.as_tensor(c.lbw, device=dev).contiguous()
@@ -275,6 +349,9 @@ class ADMMFleet:
             c.W = t.as_tensor(c.w0, device=dev).contiguous()
             c.LAMG = t.zeros((c.n, c.backend.problem.nlp.kernel_ng), dtype=f64, device=dev)
             c.ST = t.zeros(c.n * STATS_BYTES, dtype=t.uint8, device=dev)
+            c.BLOCK = t.as_tensor(self.agent_blocks[ci], dtype=i32, device=dev)
+            c.ACTIVE = t.ones(c.n, dtype=i32, device=dev)
+            c.RHO_COL = t.as_tensor(np.array([c.rho_col], np.int32), device=dev)
             c.dev_slots = []
             for si, s in enumerate(c.slots):
                 c.dev_slots.append({
@@ -310,8 +387,22 @@ class ADMMFleet:
             self.torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ steps
+    def _set_blocks(self, rho_b: np.ndarray, active_b: Optional[np.ndarray]):
+        """Upload the per-block penalties and (coordinated runs) the freeze masks."""
+        t = self.torch
+        self.RHO_B.copy_(t.as_tensor(np.asarray(rho_b, float).reshape(-1, 1)))
+        if self.G:
+            self.RHO_G.copy_(t.as_tensor(np.asarray(rho_b, float)[self.block_of_group]))
+        act = np.ones(self.n_blocks, bool) if active_b is None else np.asarray(active_b, bool)
+        if self.G:
+            self.ACTIVE_G.copy_(t.as_tensor(act[self.block_of_group].astype(np.int32)))
+        for ci, c in enumerate(self.classes):
+            c.ACTIVE.copy_(t.as_tensor(act[self.agent_blocks[ci]].astype(np.int32)))
+        self._masked = active_b is not None and not act.all()
+
     def _solve_all(self, rho: float):
-        """Inject mean/diff, multipliers and rho into every agent's p; solve; gather locals."""
+        """Inject mean/diff, multipliers and the block's rho into every agent's p; solve
+        (agents of frozen blocks are skipped); gather locals."""
         ops, T = self.ops, self.T
         for ci, c in enumerate(self.classes):
             for si, s in enumerate(c.slots):
@@ -322,39 +413,57 @@ class ADMMFleet:
                 else:
                     ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
                     ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
-            ops.fill_column(c.P, c.rho_col, rho)
-            ops.solve(c)
+            ops.scatter_rows(1, self.RHO_B, c.BLOCK, c.P, c.RHO_COL)  # the block's penalty
+            ops.solve(c, c.ACTIVE if self._masked else None)
             for si, s in enumerate(c.slots):
                 d = c.dev_slots[si]
                 ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows"])
             st = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)[:, _STATUS_WORD]
-            self._ok_count += ((st == 0) | (st == 1)).sum()
+            ok = (st == 0) | (st == 1)
+            if self._masked:
+                ok &= c.ACTIVE != 0
+            self._ok_count += ok.sum()
 
-    def _update_means(self, rho: float, apply_multipliers: bool) -> Optional[np.ndarray]:
+    def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False):
         """Mean (+ exchange diffs) from the current locals; with ``apply_multipliers``
-        also the multiplier update. Returns the residual totals when requested."""
-        ops, T, G = self.ops, self.T, self.G
+        also the multiplier update.  Returns the residual totals [n_blocks][8] (device).
+        ``per_block``: per-group penalties and freeze masks of the coordinated run."""
+        ops, T, G, nb = self.ops, self.T, self.G, self.n_blocks
         if G == 0:
             return None
+        rho_g = self.RHO_G if per_block else None
+        act_g = self.ACTIVE_G if per_block and self._masked else None
+        blk = self.BLOCK_G if nb > 1 else None
         self.MOM.zero_()
-        ops.moments(G, self.n_global, T, self.GSTART, self.max_rows, self.X, self.LAMR, self.MEAN, self.MOM)
-        totals = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS]
+        ops.moments(G, self.n_global, nb, T, self.GSTART, self.max_rows, self.X, self.LAMR, self.MEAN, self.MOM)
+        totals = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
         exch = self.EXCH if self.exchange_flags.any() else None
         gm = self.GMULT if exch is not None else None
-        ops.finalize(self.n_global, G, self.n_global, T, self.MOM, exch, gm, rho, self.MEAN, self.DMEAN, totals)
+        ops.finalize(self.n_global, G, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
+                     self.MEAN, self.DMEAN, totals)
         if self.world > 1:
             self.dist.all_reduce(self.MOM[:self.reduce_len], group=self.group)
-        ops.finalize(0, self.n_global, self.n_global, T, self.MOM, exch, gm, rho, self.MEAN, self.DMEAN, totals)
+        ops.finalize(0, self.n_global, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
+                     self.MEAN, self.DMEAN, totals)
         if apply_multipliers:
-            ops.consensus_multipliers(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, rho, self.LAMR)
-            # consensus rows of exchange groups are never read; exchange rows of consensus groups neither
-            ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT, rho)
-        else:
-            ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT, 0.0)
-        return totals
+            ops.consensus_multipliers(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, rho, rho_g, act_g,
+                                      self.LAMR)
+        # consensus rows of exchange groups are never read; exchange rows of consensus groups neither
+        ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT,
+                            apply_multipliers, rho, rho_g, act_g)
+        return totals.view(nb, ADMM_TOTALS)
 
     def _shift_all(self, shift: int):
+        """``shift_values_by_one`` of every variable (`admm_datatypes.py:275-282`, `326-331`):
+        consensus means and multipliers; exchange multipliers and diffs — the mean of an
+        exchange alias is NOT shifted."""
         ops, T = self.ops, self.T
+        if self.G:
+            ex = self.torch.as_tensor(self.exchange_flags, device=self.device) != 0
+            keep = self.MEAN[:self.G][ex].clone() if bool(ex.any()) else None
+            ops.shift(T, shift, self.MEAN)
+            if keep is not None:
+                self.MEAN[:self.G][ex] = keep
         ops.shift(T, shift, self.LAMR)
         ops.shift(T, shift, self.DIFF)
         ops.shift(T, shift, self.GMULT)
@@ -364,48 +473,72 @@ class ADMMFleet:
                         dual_tol: float = 1e-3, use_relative_tolerances: bool = True, abs_tol: float = 1e-3,
                         rel_tol: float = 1e-3, penalty_change_threshold: float = -1.0,
                         penalty_change_factor: float = 2.0) -> dict:
-        """One control step of the coordinator (`admm_coordinator.py:259-321`)."""
-        rho = float(penalty_factor)
-        self._update_means(rho, apply_multipliers=False)
+        """One control step of the coordinator (`admm_coordinator.py:259-321`), run by every
+        block independently: its own residual test, penalty variation and iteration count;
+        a converged block is frozen (no solves, no updates) while the others go on.
+
+        Returns ``iterations`` (the last iteration any block ran), ``converged`` (all blocks),
+        ``block_iterations`` / ``block_converged`` / ``block_records`` per block and
+        ``records`` (block 0's history when there is one block, else the per-iteration
+        norms over the blocks still running)."""
+        nb = self.n_blocks
+        t0 = time.perf_counter()  # _performance_counter, set at the start of the round (:270)
+        rho_b = np.full(nb, float(penalty_factor))
+        active = np.ones(nb, bool)
+        self._set_blocks(rho_b, None)
+        self._update_means(float(penalty_factor), apply_multipliers=False, per_block=True)
         shift = int(len(self.classes[0].coupling_grid) / self.classes[0].horizon)
-        self.ops.shift(self.T, shift, self.MEAN)
         self._shift_all(shift)
-        converged = False
-        it = 0
+        iters = np.full(nb, admm_iter_max, np.int64)
+        conv_b = np.zeros(nb, bool)
+        block_records: List[List[IterationRecord]] = [[] for _ in range(nb)]
         records = []
-        t0 = time.perf_counter()
         self._ok_count.zero_()
-        t_it = t0
+        it = 0
         for it in range(1, admm_iter_max + 1):
-            self._solve_all(rho)
-            tot = self._update_means(rho, apply_multipliers=True).cpu().numpy()
-            prim, dual = math.sqrt(max(tot[0], 0.0)), math.sqrt(max(tot[1], 0.0))
-            now_t = time.perf_counter()
-            records.append(IterationRecord(prim, dual, rho, wall_time=now_t - t_it))
-            t_it = now_t
+            self._solve_all(float(penalty_factor))
+            tot = self._update_means(float(penalty_factor), apply_multipliers=True, per_block=True).cpu().numpy()
+            now_t = time.perf_counter() - t0
+            prim = np.sqrt(np.maximum(tot[:, 0], 0.0))
+            dual = np.sqrt(np.maximum(tot[:, 1], 0.0))
             if use_relative_tolerances:
-                scale_p = max(math.sqrt(max(tot[2], 0.0)), math.sqrt(max(tot[3], 0.0)))
-                eps_pri = math.sqrt(tot[6]) * abs_tol + rel_tol * scale_p
-                eps_dual = math.sqrt(tot[5]) * abs_tol + rel_tol * math.sqrt(max(tot[4], 0.0))
-                conv = prim < eps_pri and dual < eps_dual
+                scale_p = np.maximum(np.sqrt(np.maximum(tot[:, 2], 0.0)), np.sqrt(np.maximum(tot[:, 3], 0.0)))
+                eps_pri = np.sqrt(tot[:, 6]) * abs_tol + rel_tol * scale_p
+                eps_dual = np.sqrt(tot[:, 5]) * abs_tol + rel_tol * np.sqrt(np.maximum(tot[:, 4], 0.0))
+                conv = (prim < eps_pri) & (dual < eps_dual)
             else:
-                conv = prim < primal_tol and dual < dual_tol
-            # varying penalty (`admm_coordinator.py:467-479`) before the stopping test,
-            # as _check_convergence does
+                conv = (prim < primal_tol) & (dual < dual_tol)
+            # _check_convergence: vary the penalty, THEN record it (admm_coordinator.py:396-402)
             if penalty_change_threshold > 1:
-                if prim > penalty_change_threshold * dual:
-                    rho *= penalty_change_factor
-                elif dual > penalty_change_threshold * prim:
-                    rho /= penalty_change_factor
-            if conv:
-                converged = True
+                up = active & (prim > penalty_change_threshold * dual)
+                down = active & ~up & (dual > penalty_change_threshold * prim)
+                rho_b = np.where(up, rho_b * penalty_change_factor, np.where(down, rho_b / penalty_change_factor, rho_b))
+            for b in np.flatnonzero(active):
+                block_records[b].append(IterationRecord(float(prim[b]), float(dual[b]), float(rho_b[b]),
+                                                        wall_time=now_t))
+            a = active
+            records.append(IterationRecord(float(np.sqrt(tot[a, 0].clip(0).sum())),
+                                           float(np.sqrt(tot[a, 1].clip(0).sum())),
+                                           float(rho_b[a][0]) if nb == 1 else float(np.mean(rho_b[a])),
+                                           wall_time=now_t))
+            done = active & conv
+            if done.any():
+                iters[done] = it
+                conv_b |= done
+                active = active & ~done
+            if not active.any():
                 break
+            self._set_blocks(rho_b, active)
         self._sync()
+        self._masked = False
         wall = time.perf_counter() - t0
+        if nb == 1:
+            records = block_records[0]
         self.history.extend(records)
         self.rounds += 1
-        return {"iterations": it, "converged": converged, "records": records, "wall_s": wall,
-                "converged_solves": int(self._ok_count.item())}
+        return {"iterations": it, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
+                "converged_solves": int(self._ok_count.item()), "block_iterations": iters,
+                "block_converged": conv_b, "block_records": block_records}
 
     def save_stats(self, path, start_time: float, records: Sequence[IterationRecord], first_iteration: int = 0):
         """Append one round's residual history to the coordinator's ``solve_stats_file``
@@ -434,6 +567,7 @@ class ADMMFleet:
         self.ops.shift(self.T, shift, self.X)   # _shift_and_send_coupling_outputs
         self.ops.shift(self.T, shift, self.LAMR)  # _shift_multipliers
         self.ops.shift(self.T, shift, self.GMULT)
+        self._set_blocks(np.full(self.n_blocks, rho), None)
         self._update_means(rho, apply_multipliers=False)  # _set_mean_coupling_values
         hist = self.torch.zeros((max(max_iterations, 1), ADMM_TOTALS), dtype=self.torch.float64,
                                 device=self.device)
@@ -443,7 +577,7 @@ class ADMMFleet:
             self._solve_all(rho)
             tot = self._update_means(rho, apply_multipliers=True)
             if record_residuals and tot is not None:
-                hist[it].copy_(tot)
+                hist[it].copy_(tot.sum(0))
         h = hist.cpu().numpy()
         wall = time.perf_counter() - t0
         records = [IterationRecord(math.sqrt(max(r[0], 0.0)), math.sqrt(max(r[1], 0.0)), rho)

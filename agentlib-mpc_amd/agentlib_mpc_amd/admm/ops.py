@@ -39,8 +39,10 @@ class NativeADMMOps:
             raise native.NativeError(f"{name} failed ({rc})")
 
     # -- NLP solves ---------------------------------------------------------------------
-    def solve(self, cls) -> None:
-        cls.native.solve(cls.P, cls.LB, cls.UB, cls.W, lam_g=cls.LAMG, stats=cls.ST,
+    def solve(self, cls, active=None) -> None:
+        """Batched solve of one class; ``active`` (int32 [n] device tensor or None) skips the
+        agents of converged blocks."""
+        cls.native.solve(cls.P, cls.LB, cls.UB, cls.W, lam_g=cls.LAMG, stats=cls.ST, active=active,
                          stream=self.stream.value)
 
     # -- moves ---------------------------------------------------------------------------
@@ -57,27 +59,33 @@ class NativeADMMOps:
                                             self.stream), "mpcx_fill_column")
 
     # -- ADMM arithmetic -------------------------------------------------------------------
-    def moments_size(self, n_groups, T) -> int:
-        return int(self.lib.mpcx_admm_moments_size(n_groups, T))
+    # rho_g / active_g / block_g: per-group penalty, freeze mask and block index (device
+    # tensors, or None for one block with the scalar rho), see include/mpcx.h
+    def moments_size(self, n_groups, n_blocks, T) -> int:
+        return int(self.lib.mpcx_admm_moments_size(n_groups, n_blocks, T))
 
-    def moments(self, n_groups, n_global, T, gstart, max_rows, X, LAM, center, out):
-        self._chk(self.lib.mpcx_admm_moments(n_groups, n_global, T, _p(gstart), max_rows, _p(X), _p(LAM),
-                                             _p(center), _p(out), self.stream), "mpcx_admm_moments")
+    def moments(self, n_groups, n_global, n_blocks, T, gstart, max_rows, X, LAM, center, out):
+        self._chk(self.lib.mpcx_admm_moments(n_groups, n_global, n_blocks, T, _p(gstart), max_rows, _p(X),
+                                             _p(LAM), _p(center), _p(out), self.stream), "mpcx_admm_moments")
 
-    def finalize(self, g0, g1, n_global, T, mom, exchange, gmult, rho, mean, dmean, totals):
-        self._chk(self.lib.mpcx_admm_finalize(g0, g1, n_global, T, _p(mom), _p(exchange), _p(gmult),
-                                              float(rho), _p(mean), _p(dmean), _p(totals), self.stream),
+    def finalize(self, g0, g1, n_global, n_blocks, T, mom, exchange, gmult, rho, rho_g, active_g, block_g,
+                 mean, dmean, totals):
+        self._chk(self.lib.mpcx_admm_finalize(g0, g1, n_global, n_blocks, T, _p(mom), _p(exchange), _p(gmult),
+                                              float(rho), _p(rho_g), _p(active_g), _p(block_g), _p(mean),
+                                              _p(dmean), _p(totals), self.stream),
                   "mpcx_admm_finalize")
 
-    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho, LAM):
+    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho, rho_g, active_g, LAM):
         self._chk(self.lib.mpcx_admm_consensus_multipliers(n_groups, T, _p(gstart), max_rows, _p(X),
-                                                           _p(mean), float(rho), _p(LAM), None,
-                                                           self.stream),
+                                                           _p(mean), float(rho), _p(rho_g), _p(active_g),
+                                                           _p(LAM), None, self.stream),
                   "mpcx_admm_consensus_multipliers")
 
-    def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, rho):
+    def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, update, rho, rho_g,
+                        active_g):
         self._chk(self.lib.mpcx_admm_exchange_update(n_groups, T, _p(gstart), max_rows, _p(X), _p(mean),
-                                                     _p(diff), _p(gmult), float(rho), self.stream),
+                                                     _p(diff), _p(gmult), int(bool(update)), float(rho),
+                                                     _p(rho_g), _p(active_g), self.stream),
                   "mpcx_admm_exchange_update")
 
     def shift(self, T, shift, x):

@@ -22,7 +22,11 @@ from agentlib_mpc_amd.data_structures import admm_datatypes as adt
 from agentlib_mpc_amd.data_structures.mpc_datamodels import MPCVariable, VariableReference
 from agentlib_mpc_amd.optimization_backends import create_optimization_backend
 
-TIGHT = {"ipopt": {"tol": 1e-10, "max_iter": 500}}
+#: parity settings: a tight tolerance and no acceptable-level stop, so that two solvers are
+#: compared at (nearly) exact solutions of the same NLP
+TIGHT = {"ipopt": {"tol": 1e-10, "max_iter": 500, "acceptable_iter": 0}}
+#: the reference's solver settings (`casadi_utils.py:197-206`; the backend applies them)
+REFERENCE = {"ipopt": {}}
 
 
 def V(name, value=None, lb=-np.inf, ub=np.inf):

@@ -10,8 +10,11 @@ contract (`core/casadi_backend.py:108-139`), same variable/parameter layout and
 ``Results`` format.  The NLP is solved by the generated HIP interior-point
 kernel.  IPOPT options given in ``solver.options`` (``{"ipopt": {...}}`` or
 ``"ipopt.<key>"``) are mapped onto the kernel options; the reference's
-defaults (`data_structures/casadi_utils.py:191-217`: ``max_iter=100``,
-``tol=1e-4``, acceptable tolerances) are applied unless overridden.
+defaults (`data_structures/casadi_utils.py:197-206`: ``max_iter=100``,
+``tol=1e-4``, ``acceptable_tol=0.1``, ``acceptable_iter=5``,
+``acceptable_constr_viol_tol=1``, ``acceptable_compl_inf_tol=1``) are applied
+unless overridden, and the kernel terminates with IPOPT's semantics
+(``Solve_Succeeded`` / ``Solved_To_Acceptable_Level``, both ``success``).
 
 Besides the per-agent ``solve``, ``solve_batch`` solves many agents of the
 same structure in one launch (the fleet path used by the ADMM drivers).
@@ -40,8 +43,14 @@ from agentlib_mpc_amd.optimization_backends.problem import CompiledProblem
 from agentlib_mpc_amd.optimization_backends.results import Results
 from agentlib_mpc_amd.optimization_backends.system import ADMMSystem, BaseSystem, FullSystem
 
-#: reference IPOPT defaults (`casadi_utils.py:197-206`)
-REFERENCE_IPOPT_DEFAULTS = {"max_iter": 100, "tol": 1e-4}
+#: reference IPOPT defaults (`casadi_utils.py:197-206`); options not named here keep
+#: IPOPT's own defaults (``mpcx_default_options``)
+REFERENCE_IPOPT_DEFAULTS = {"max_iter": 100, "tol": 1e-4, "acceptable_tol": 0.1,
+                            "acceptable_constr_viol_tol": 1.0, "acceptable_iter": 5,
+                            "acceptable_compl_inf_tol": 1.0}
+#: reference fatrop defaults (`casadi_utils.py:173-178`): the acceptable tolerances stay at
+#: the solver library's own defaults
+REFERENCE_FATROP_DEFAULTS = {"max_iter": 100, "tol": 1e-4}
 
 
 class MI355XBackendConfig(BackendConfig):
@@ -66,7 +75,7 @@ def ipopt_options_to_kernel(options: dict, solver: str = "ipopt") -> dict:
     merges it into fatrop's own options, `casadi_utils.py:163-189`; its defaults
     max_iter=100, tol=1e-4 equal the IPOPT ones); fatrop's ``structure_detection``
     and ``equality`` flags describe what the kernel derives itself."""
-    opts = dict(REFERENCE_IPOPT_DEFAULTS)
+    opts = dict(REFERENCE_IPOPT_DEFAULTS if solver == "ipopt" else REFERENCE_FATROP_DEFAULTS)
     nested = dict(options.get(solver, {}))
     for k, v in options.items():
         if k.startswith(f"{solver}."):
@@ -76,9 +85,7 @@ def ipopt_options_to_kernel(options: dict, solver: str = "ipopt") -> dict:
                "constr_mult_init_max": "constr_mult_init_max",
                "alpha_min_frac": "alpha_min_frac"}
     ignored = {"print_level", "sb", "print_time", "linear_solver", "hessian_approximation",
-               "structure_detection", "equality", "verbose", "record_time", "expand",
-               "acceptable_obj_change_tol", "acceptable_dual_inf_tol", "acceptable_constr_viol_tol",
-               "acceptable_compl_inf_tol"}
+               "structure_detection", "equality", "verbose", "record_time", "expand"}
     for k, v in nested.items():
         if k in ignored:
             continue

@@ -33,7 +33,7 @@ from typing import Dict, List
 from agentlib_mpc_amd import symbolic as sx
 from agentlib_mpc_amd.optimization_backends.discretization import StageNLP
 
-KERNEL_ABI_VERSION = 4
+KERNEL_ABI_VERSION = 5
 
 
 @dataclasses.dataclass

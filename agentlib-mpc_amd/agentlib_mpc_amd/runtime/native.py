@@ -51,6 +51,8 @@ class ProblemDesc(ctypes.Structure):
 
 _OPT_DOUBLES = [
     "tol", "dual_inf_tol", "constr_viol_tol", "compl_inf_tol", "acceptable_tol",
+    "acceptable_dual_inf_tol", "acceptable_constr_viol_tol", "acceptable_compl_inf_tol",
+    "acceptable_obj_change_tol",
     "mu_init", "mu_min", "kappa_eps", "kappa_mu", "theta_mu", "tau_min",
     "bound_push", "bound_frac", "bound_relax_factor", "bound_mult_init_val",
     "constr_mult_init_max", "kappa_sigma", "nlp_scaling_max_gradient", "nlp_scaling_min_value",
@@ -81,6 +83,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
 ]
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
+KERNEL_ABI = 5  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -132,14 +135,15 @@ def load_library():
         lib.mpcx_reserve.argtypes = [vp, i32]
         lib.mpcx_workspace_bytes_per_agent.argtypes = [vp]
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
-        lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp]
+        lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp, vp]
         i64 = ctypes.c_int64
-        lib.mpcx_admm_moments_size.argtypes = [i32, i32]
+        lib.mpcx_admm_moments_size.argtypes = [i32, i32, i32]
         lib.mpcx_admm_moments_size.restype = i64
-        lib.mpcx_admm_moments.argtypes = [i32, i32, i32, vp, i32, vp, vp, vp, vp, vp]
-        lib.mpcx_admm_finalize.argtypes = [i32, i32, i32, i32, vp, vp, vp, f64, vp, vp, vp, vp]
-        lib.mpcx_admm_consensus_multipliers.argtypes = [i32, i32, vp, i32, vp, vp, f64, vp, vp, vp]
-        lib.mpcx_admm_exchange_update.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, f64, vp]
+        lib.mpcx_admm_moments.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp]
+        lib.mpcx_admm_finalize.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp,
+                                           vp]
+        lib.mpcx_admm_consensus_multipliers.argtypes = [i32, i32, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp]
+        lib.mpcx_admm_exchange_update.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, i32, f64, vp, vp, vp]
         lib.mpcx_admm_shift.argtypes = [i32, i32, i32, vp, vp]
         lib.mpcx_gather_rows.argtypes = [i32, i32, vp, i64, vp, vp, vp, vp]
         lib.mpcx_scatter_rows.argtypes = [i32, i32, vp, vp, vp, i64, vp, vp]
@@ -198,7 +202,7 @@ class NativeProblem:
         self.gen = gen
         d = gen.dims
         self.desc = ProblemDesc(n_stages=d["N"], nx=d["NX"], nv=d["NV"], ng=d["NG"],
-                                nps=d["NPS"], npg=d["NPG"], abi=4, reserved=0)
+                                nps=d["NPS"], npg=d["NPG"], abi=KERNEL_ABI, reserved=0)
         path = hsaco or code_object_path(gen.key)
         if not pathlib.Path(path).exists():
             path = compile_model(gen)
@@ -239,22 +243,40 @@ class NativeProblem:
             raise NativeError(f"mpcx_reserve failed ({rc})")
 
     def solve(self, p, lbw, ubw, w, lbg=None, ubg=None, lam_g=None, lam_w=None, stats=None,
-              stream=None):
-        """Launch the batched solve on device tensors (stream-ordered, async)."""
+              active=None, stream=None):
+        """Launch the batched solve on device tensors (stream-ordered, async).
+
+        Every buffer the kernel reads or writes is checked here (dtype, device, contiguity,
+        size): an undersized or host buffer would otherwise become an out-of-bounds device
+        access instead of a Python error."""
         import torch
 
         n = int(p.shape[0])
+
+        def check(name, t, shape, dtype=torch.float64):
+            if t.dtype != dtype or not t.is_cuda or not t.is_contiguous() or tuple(t.shape) != shape:
+                raise ValueError(f"{name} must be a contiguous {dtype} device tensor of shape {shape}, "
+                                 f"got {tuple(t.shape)} {t.dtype} on {t.device}")
+
         for name, t, cols in (("p", p, self.npar), ("lbw", lbw, self.nw), ("ubw", ubw, self.nw),
                               ("w", w, self.nw)):
-            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or tuple(t.shape) != (n, cols):
-                raise ValueError(f"{name} must be a contiguous float64 device tensor of shape {(n, cols)}")
+            check(name, t, (n, cols))
         if (lbg is None) != (ubg is None):
             raise ValueError("lbg and ubg must be given together")
+        for name, t, cols in (("lbg", lbg, self.ng_total), ("ubg", ubg, self.ng_total),
+                              ("lam_g", lam_g, self.ng_total), ("lam_w", lam_w, self.nw)):
+            if t is not None:
+                check(name, t, (n, cols))
+        if stats is not None:
+            check("stats", stats, (n * STATS_BYTES,), torch.uint8)
+        if active is not None:
+            check("active", active, (n,), torch.int32)
         if stream is None:
             stream = torch.cuda.current_stream().cuda_stream
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         rc = self.lib.mpcx_batch_solve(self.handle, n, ptr(p), ptr(lbw), ptr(ubw), ptr(lbg), ptr(ubg),
-                                       ptr(w), ptr(lam_g), ptr(lam_w), ptr(stats), ctypes.c_void_p(stream))
+                                       ptr(w), ptr(lam_g), ptr(lam_w), ptr(stats), ptr(active),
+                                       ctypes.c_void_p(stream))
         if rc != 0:
             raise NativeError(f"mpcx_batch_solve failed ({rc})")
 

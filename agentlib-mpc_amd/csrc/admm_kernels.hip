@@ -21,6 +21,12 @@
 //   sum x^2                       = S2 + 2 c S1 + n c^2
 // so groups whose participants live on several GPUs need only their moments summed
 // across ranks (RCCL all-reduce) before mpcx_admm_finalize.
+//
+// Blocks: the groups are partitioned into independent consensus blocks (one reference
+// ADMMCoordinator each, e.g. the 4-room + air-handler blocks of a scaled C2 fleet).  The
+// residual totals are kept per block ([n_blocks][MPCX_ADMM_TOTALS]), every group may carry
+// its own penalty rho_g (penalty variation per coordinator), and groups whose block has
+// converged (active_g == 0) are frozen: no mean, multiplier or diff update.
 #include <hip/hip_runtime.h>
 
 #include "mpcx.h"
@@ -32,10 +38,13 @@ constexpr int ROWS_PER_BLOCK = 256;
 constexpr int NMOM = 5;            // S1, S2, SL, SL2, SLX
 constexpr int WAVE = 64;
 
-__device__ __forceinline__ long mom_offset(int g, int g_global, int T) {
+// moments buffer: [global groups][totals: n_blocks x MPCX_ADMM_TOTALS][local groups]
+__device__ __forceinline__ long mom_offset(int g, int g_global, int T, int n_tot) {
   const long S = (long)NMOM * T + 1;
-  return (long)g * S + (g >= g_global ? MPCX_ADMM_TOTALS : 0);
+  return (long)g * S + (g >= g_global ? n_tot : 0);
 }
+__device__ __forceinline__ bool g_active(const int* active_g, int g) { return active_g == nullptr || active_g[g] != 0; }
+__device__ __forceinline__ double g_rho(const double* rho_g, double rho, int g) { return rho_g ? rho_g[g] : rho; }
 
 // --- NLP vector <-> trajectory rows ---------------------------------------------------
 __global__ void k_gather_rows(int n, int T, const double* __restrict__ src, long ld,
@@ -65,7 +74,7 @@ __global__ void k_fill_column(int n, double* __restrict__ dst, long ld, int col,
 // --- moments -----------------------------------------------------------------------------
 // grid (n_groups, row chunks). Thread (r, tc): column t0+tc, rows rb+r, rb+r+R, ...
 __global__ void __launch_bounds__(THREADS)
-k_moments(int g_global, int T, const int* __restrict__ gstart, const double* __restrict__ x,
+k_moments(int g_global, int n_tot, int T, const int* __restrict__ gstart, const double* __restrict__ x,
           const double* __restrict__ lam, const double* __restrict__ center,
           double* __restrict__ out) {
   __shared__ double part[THREADS * NMOM];
@@ -74,7 +83,7 @@ k_moments(int g_global, int T, const int* __restrict__ gstart, const double* __r
   const int rb = r0 + blockIdx.y * ROWS_PER_BLOCK;
   if (rb >= r1) return;
   const int re = min(rb + ROWS_PER_BLOCK, r1);
-  double* o = out + mom_offset(g, g_global, T);
+  double* o = out + mom_offset(g, g_global, T, n_tot);
   const int cpp = T < THREADS ? T : THREADS;  // columns per pass
   const int R = THREADS / cpp;                // row lanes
   const int r = threadIdx.x / cpp, tc = threadIdx.x % cpp;
@@ -118,12 +127,16 @@ k_moments(int g_global, int T, const int* __restrict__ gstart, const double* __r
 
 // --- finalize: one wavefront per group ------------------------------------------------
 __global__ void __launch_bounds__(WAVE)
-k_finalize(int g0, int g1, int g_global, int T, const double* __restrict__ mom,
-           const int* __restrict__ exchange, const double* __restrict__ gmult, double rho,
-           double* __restrict__ mean, double* __restrict__ dmean, double* __restrict__ totals) {
+k_finalize(int g0, int g1, int g_global, int n_tot, int T, const double* __restrict__ mom,
+           const int* __restrict__ exchange, const double* __restrict__ gmult, double rho_s,
+           const double* __restrict__ rho_g, const int* __restrict__ active_g,
+           const int* __restrict__ block_g, double* __restrict__ mean, double* __restrict__ dmean,
+           double* __restrict__ totals_all) {
   const int g = g0 + blockIdx.x;
-  if (g >= g1) return;
-  const double* o = mom + mom_offset(g, g_global, T);
+  if (g >= g1 || !g_active(active_g, g)) return;
+  const double rho = g_rho(rho_g, rho_s, g);
+  double* totals = totals_all + (block_g ? (long)block_g[g] * MPCX_ADMM_TOTALS : 0);
+  const double* o = mom + mom_offset(g, g_global, T, n_tot);
   const double n = o[NMOM * T];
   const bool ex = exchange && exchange[g];
   double prim = 0.0, dual = 0.0, xs = 0.0, ms = 0.0, ls = 0.0;
@@ -174,9 +187,11 @@ k_finalize(int g0, int g1, int g_global, int T, const double* __restrict__ mom,
 // --- multiplier / diff updates ---------------------------------------------------------
 __global__ void __launch_bounds__(THREADS)
 k_consensus_mult(int T, const int* __restrict__ gstart, const double* __restrict__ x,
-                 const double* __restrict__ mean, double rho, double* __restrict__ lam,
-                 double* __restrict__ res) {
+                 const double* __restrict__ mean, double rho_s, const double* __restrict__ rho_g,
+                 const int* __restrict__ active_g, double* __restrict__ lam, double* __restrict__ res) {
   const int g = blockIdx.x;
+  if (!g_active(active_g, g)) return;
+  const double rho = g_rho(rho_g, rho_s, g);
   const int r0 = gstart[g], r1 = gstart[g + 1];
   const int rb = r0 + blockIdx.y * ROWS_PER_BLOCK;
   if (rb >= r1) return;
@@ -192,8 +207,10 @@ k_consensus_mult(int T, const int* __restrict__ gstart, const double* __restrict
 
 __global__ void __launch_bounds__(THREADS)
 k_exchange_diff(int T, const int* __restrict__ gstart, const double* __restrict__ x,
-                const double* __restrict__ mean, double* __restrict__ diff) {
+                const double* __restrict__ mean, const int* __restrict__ active_g,
+                double* __restrict__ diff) {
   const int g = blockIdx.x;
+  if (!g_active(active_g, g)) return;
   const int r0 = gstart[g], r1 = gstart[g + 1];
   const int rb = r0 + blockIdx.y * ROWS_PER_BLOCK;
   if (rb >= r1) return;
@@ -204,11 +221,14 @@ k_exchange_diff(int T, const int* __restrict__ gstart, const double* __restrict_
     diff[base + e] = x[base + e] - mean[(long)g * T + e % T];
 }
 
-__global__ void k_exchange_mult(int n_groups, int T, const double* __restrict__ mean, double rho,
+__global__ void k_exchange_mult(int n_groups, int T, const double* __restrict__ mean, double rho_s,
+                                const double* __restrict__ rho_g, const int* __restrict__ active_g,
                                 double* __restrict__ lam) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_groups * T) return;
-  lam[e] += rho * mean[e];
+  const int g = e / T;
+  if (!g_active(active_g, g)) return;
+  lam[e] += g_rho(rho_g, rho_s, g) * mean[e];
 }
 
 __global__ void k_shift(int n_rows, int T, int shift, double* __restrict__ x) {
@@ -267,50 +287,54 @@ extern "C" int mpcx_fill_column(int32_t n_agents, double* dst, int64_t dst_ld, i
   return MPCX_OK;
 }
 
-extern "C" int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t T) {
-  if (n_groups < 0 || T <= 0) return MPCX_ERR_ARG;
-  return (int64_t)n_groups * (NMOM * (int64_t)T + 1) + MPCX_ADMM_TOTALS;
+extern "C" int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t n_blocks, int32_t T) {
+  if (n_groups < 0 || n_blocks < 1 || T <= 0) return MPCX_ERR_ARG;
+  return (int64_t)n_groups * (NMOM * (int64_t)T + 1) + (int64_t)MPCX_ADMM_TOTALS * n_blocks;
 }
 
-extern "C" int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t T,
+extern "C" int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
                                  const int32_t* gstart, int32_t max_group_rows,
                                  const double* locals, const double* multipliers,
                                  const double* center, double* out, void* stream) {
-  if (n_groups <= 0 || n_global < 0 || n_global > n_groups || T <= 0 || max_group_rows < 0 ||
-      !gstart || !locals || !center || !out)
+  if (n_groups <= 0 || n_global < 0 || n_global > n_groups || n_blocks < 1 || T <= 0 ||
+      max_group_rows < 0 || !gstart || !locals || !center || !out)
     return MPCX_ERR_ARG;
   if (max_group_rows == 0) return MPCX_OK;
   hipLaunchKernelGGL(k_moments, group_grid(n_groups, max_group_rows), dim3(THREADS), 0,
-                     (hipStream_t)stream, n_global, T, gstart, locals, multipliers, center, out);
+                     (hipStream_t)stream, n_global, MPCX_ADMM_TOTALS * n_blocks, T, gstart, locals,
+                     multipliers, center, out);
   LAUNCH_CHECK();
   return MPCX_OK;
 }
 
-extern "C" int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_global, int32_t T,
-                                  const double* moments, const int32_t* exchange,
-                                  const double* group_multipliers, double rho, double* mean,
+extern "C" int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_global, int32_t n_blocks,
+                                  int32_t T, const double* moments, const int32_t* exchange,
+                                  const double* group_multipliers, double rho, const double* rho_g,
+                                  const int32_t* active_g, const int32_t* block_g, double* mean,
                                   double* delta_mean, double* totals, void* stream) {
-  if (g_begin < 0 || g_end < g_begin || n_global < 0 || T <= 0 || !moments || !mean ||
-      !delta_mean || !totals)
+  if (g_begin < 0 || g_end < g_begin || n_global < 0 || n_blocks < 1 || T <= 0 || !moments ||
+      !mean || !delta_mean || !totals)
     return MPCX_ERR_ARG;
   if (exchange && !group_multipliers) return MPCX_ERR_ARG;
+  if (n_blocks > 1 && !block_g) return MPCX_ERR_ARG;
   if (g_end == g_begin) return MPCX_OK;
   hipLaunchKernelGGL(k_finalize, dim3(g_end - g_begin), dim3(WAVE), 0, (hipStream_t)stream, g_begin,
-                     g_end, n_global, T, moments, exchange, group_multipliers, rho, mean,
-                     delta_mean, totals);
+                     g_end, n_global, MPCX_ADMM_TOTALS * n_blocks, T, moments, exchange,
+                     group_multipliers, rho, rho_g, active_g, block_g, mean, delta_mean, totals);
   LAUNCH_CHECK();
   return MPCX_OK;
 }
 
 extern "C" int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, const int32_t* gstart,
                                                int32_t max_group_rows, const double* locals,
-                                               const double* mean, double rho, double* mult,
-                                               double* res, void* stream) {
+                                               const double* mean, double rho, const double* rho_g,
+                                               const int32_t* active_g, double* mult, double* res,
+                                               void* stream) {
   if (n_groups <= 0 || T <= 0 || max_group_rows < 0 || !gstart || !locals || !mean || !mult)
     return MPCX_ERR_ARG;
   if (max_group_rows == 0) return MPCX_OK;
   hipLaunchKernelGGL(k_consensus_mult, group_grid(n_groups, max_group_rows), dim3(THREADS), 0,
-                     (hipStream_t)stream, T, gstart, locals, mean, rho, mult, res);
+                     (hipStream_t)stream, T, gstart, locals, mean, rho, rho_g, active_g, mult, res);
   LAUNCH_CHECK();
   return MPCX_OK;
 }
@@ -318,20 +342,21 @@ extern "C" int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, cons
 extern "C" int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* gstart,
                                          int32_t max_group_rows, const double* locals,
                                          const double* mean, double* diff, double* mult,
-                                         double rho, void* stream) {
+                                         int32_t update_multiplier, double rho, const double* rho_g,
+                                         const int32_t* active_g, void* stream) {
   if (n_groups <= 0 || T <= 0 || max_group_rows < 0 || !gstart || !locals || !mean || !diff)
     return MPCX_ERR_ARG;
-  if (rho != 0.0 && !mult) return MPCX_ERR_ARG;
+  if (update_multiplier && !mult) return MPCX_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (max_group_rows > 0) {
     hipLaunchKernelGGL(k_exchange_diff, group_grid(n_groups, max_group_rows), dim3(THREADS), 0, s,
-                       T, gstart, locals, mean, diff);
+                       T, gstart, locals, mean, active_g, diff);
     LAUNCH_CHECK();
   }
-  if (rho != 0.0) {
+  if (update_multiplier) {
     const int n = n_groups * T;
     hipLaunchKernelGGL(k_exchange_mult, dim3(blocks_for(n, 256)), dim3(256), 0, s, n_groups, T,
-                       mean, rho, mult);
+                       mean, rho, rho_g, active_g, mult);
     LAUNCH_CHECK();
   }
   return MPCX_OK;

@@ -5,7 +5,7 @@
 
 #include "mpcx.h"
 
-#define MPCX_KERNEL_ABI 4
+#define MPCX_KERNEL_ABI 5
 
 typedef struct mpcx_kernel_args {
   const double* p;
@@ -17,6 +17,7 @@ typedef struct mpcx_kernel_args {
   double* lam_g;
   double* lam_w;
   mpcx_stats* stats;
+  const int* active;
   double* ws;
   long ws_stride;
   int n_agents;

@@ -1339,8 +1339,11 @@ __device__ __noinline__ void solve(const Agent a) {
 // ---------------------------------------------------------------------------
 // optimality error parts; complementarity kept as (max, min) of the products so
 // that E_mu for any mu is max(pmx - mu, mu - pmn) without another pass
+// dual_u / viol_u: IPOPT's unscaled_curr_dual_infeasibility (grad_lag_x and the slack part
+// grad_lag_s*d_scale, / obj_scale) and unscaled_curr_nlp_constraint_violation (|c| and the
+// violation of the (relaxed) bounds of d, not d - s)
 struct OptErr {
-  double dual, dual_u, primal, primal_u, pmx, pmn, s_d, s_c;
+  double dual, dual_u, primal, viol_u, pmx, pmn, s_d, s_c;
   int ncompl;
   __device__ double compl_at(double mu) const { return ncompl > 0 ? fmax(pmx - mu, mu - pmn) : 0.0; }
   __device__ double err_at(double mu) const { return fmax(fmax(dual / s_d, primal), compl_at(mu) / s_c); }
@@ -1349,7 +1352,7 @@ struct OptErr {
 // scaled optimality error E_mu (IPOPT eq. 5) + unscaled parts
 __device__ __noinline__ OptErr opt_error(const Agent a, double obj_scale) {
   const int lane = a.lane;
-  double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, pmax_u = 0.0, pmx = -INFINITY, pmn = INFINITY;
+  double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, vmax_u = 0.0, pmx = -INFINITY, pmn = INFINITY;
   double lsum = 0.0, zsum = 0.0;
   int nz = 0;
 #pragma unroll
@@ -1377,25 +1380,28 @@ __device__ __noinline__ OptErr opt_error(const Agent a, double obj_scale) {
     const double vl = a.vL()[cc], vu = a.vU()[cc];
     if (on) {
       const int cl = cls_of(lbv, ubv, slo, sup);
-      double cv;
+      double cv, vv = 0.0;
       if (cl == 0) {
         cv = gvv - gsc * lbv;
+        vv = fabs(cv);
       } else {
         cv = gvv - sv;
         if (cl == 1) {
           const double rs = -lm - vl + vu;
           dmax = fmax(dmax, fabs(rs));
+          dmax_u = fmax(dmax_u, fabs(rs) * gsc / obj_scale);
+          vv = fmax(0.0, fmax(slo - gvv, gvv - sup));
           if (isfin(slo)) { const double pr = (sv - slo) * vl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vl); nz++; }
           if (isfin(sup)) { const double pr = (sup - sv) * vu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vu); nz++; }
         }
       }
       pmax = fmax(pmax, fabs(cv));
-      pmax_u = fmax(pmax_u, fabs(cv) / gsc);
+      vmax_u = fmax(vmax_u, vv / gsc);
       lsum += fabs(lm);
     }
   }
   OptErr e;
-  e.dual = wmax(dmax); e.dual_u = wmax(dmax_u); e.primal = wmax(pmax); e.primal_u = wmax(pmax_u);
+  e.dual = wmax(dmax); e.dual_u = wmax(dmax_u); e.primal = wmax(pmax); e.viol_u = wmax(vmax_u);
   e.pmx = wmax(pmx); e.pmn = wmin(pmn);
   lsum = wsum(lsum); zsum = wsum(zsum); nz = wsumi(nz);
   e.ncompl = nz;
@@ -1422,6 +1428,7 @@ __device__ __forceinline__ double relax_hi(double b, double f) { return b + f * 
 
 struct Scal {
   double obj_scale, fx;
+  int square;  // IPOPT IsSquareProblem: free variables == equality constraints
 };
 
 __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
@@ -1510,6 +1517,12 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
     gL.fixm[k] = m;
   }
   sc.fx = sc.obj_scale * eval_fg_ws(a, a.x(), a.gv());
+  {
+    int nfree = 0, neq = 0;
+    for (int i = NX + lane; i < NW; i += WAVE) nfree += (a.xL()[i] != a.xU()[i]) ? 1 : 0;
+    for (int c = lane; c < M; c += WAVE) neq += (a.lb()[c] == a.ub()[c]) ? 1 : 0;
+    sc.square = wsumi(nfree) == wsumi(neq);
+  }
   sync();
   for (int c = lane; c < M; c += WAVE) {
     const double gsc = a.gs()[c];
@@ -1884,6 +1897,23 @@ __device__ __noinline__ void accept_step(const Agent a, const double kappa_sigma
   }
 }
 
+// IPOPT OptimalityErrorConvergenceCheck::CurrentIsAcceptable: the objective-change test
+// compares the (scaled) objective of the last two iterations at which it was called
+// (initially -1e50, so the first call never passes a finite acceptable_obj_change_tol)
+struct Acceptable {
+  double curr_f, last_f;
+  int last_it, count;
+};
+__device__ __forceinline__ bool current_is_acceptable(Acceptable& ac, const OptErr& e, double err0, double fx,
+                                                      int it, double obj_scale, int square,
+                                                      const mpcx_options& o) {
+  if (it != ac.last_it) { ac.last_f = ac.curr_f; ac.curr_f = fx; ac.last_it = it; }
+  if (square) return err0 <= o.acceptable_tol && e.viol_u <= o.acceptable_constr_viol_tol;
+  return err0 <= o.acceptable_tol && e.dual_u <= o.acceptable_dual_inf_tol &&
+         e.viol_u <= o.acceptable_constr_viol_tol && e.compl_at(0.0) / obj_scale <= o.acceptable_compl_inf_tol &&
+         fabs(ac.curr_f - ac.last_f) / fmax(1.0, fabs(ac.curr_f)) <= o.acceptable_obj_change_tol;
+}
+
 }  // namespace mpcx_kernel
 
 using namespace mpcx_kernel;
@@ -1904,6 +1934,7 @@ using namespace mpcx_kernel;
 extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(Args args) {
   const int agent = blockIdx.x;
   if (agent >= args.n_agents) return;
+  if (args.active != nullptr && args.active[agent] == 0) return;  // frozen (converged ADMM block)
   const mpcx_options& o = args.opt;
   Agent a;
   a.ws = (gdbl*)args.ws + (long)agent * args.ws_stride;
@@ -1937,22 +1968,32 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   int status = MPCX_MAX_ITER_EXCEEDED;
   int it = 0;
   OptErr e0;
+  Acceptable acc{-1e50, -1e50, -1, 0};
 #pragma unroll 1
   for (;;) {
     e0 = opt_error(a, obj_scale);
     const double err0 = e0.err_at(0.0);
     if (!(err0 == err0) || !(fx == fx)) { status = MPCX_INVALID_NUMBER; break; }
-    if (err0 <= o.tol && e0.dual_u <= o.dual_inf_tol && e0.primal_u <= o.constr_viol_tol &&
-        e0.compl_at(0.0) <= o.compl_inf_tol) {
+    // IPOPT OptimalityErrorConvergenceCheck::CheckConvergence (square problems: the dual
+    // infeasibility and complementarity tolerances are lifted)
+    if (err0 <= o.tol && e0.viol_u <= o.constr_viol_tol &&
+        (sc.square || (e0.dual_u <= o.dual_inf_tol && e0.compl_at(0.0) / obj_scale <= o.compl_inf_tol))) {
       status = MPCX_SOLVE_SUCCEEDED;
       break;
+    }
+    if (o.acceptable_iter > 0 && current_is_acceptable(acc, e0, err0, fx, it, obj_scale, sc.square, o)) {
+      if (++acc.count >= o.acceptable_iter) { status = MPCX_SOLVED_TO_ACCEPTABLE; break; }
+    } else {
+      acc.count = 0;
     }
     if (it >= o.max_iter) break;
     // barrier parameter update (monotone Fiacco-McCormick)
 #pragma unroll 1
     for (int mu_up = 0; mu_up < 64; ++mu_up) {
       if (e0.err_at(mu) > o.kappa_eps * mu || mu <= o.mu_min) break;
-      const double new_mu = fmax(fmax(o.tol / 10.0, o.mu_min), fmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
+      // IPOPT MonotoneMuUpdate::CalcNewMuAndTau: floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
+      const double new_mu = fmax(fmax(fmin(o.tol, o.compl_inf_tol) / (o.kappa_eps + 1.0), o.mu_min),
+                                 fmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
       if (new_mu == mu) break;  // IPOPT MonotoneMuUpdate: done when mu no longer changes
       mu = new_mu;
       tau = fmax(o.tau_min, 1.0 - mu);
@@ -2000,6 +2041,12 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
                                     theta_max, nfilt);
     n_trials += ls.trials;
     bool ftype = ls.ftype;
+    // IPOPT BacktrackingLineSearch: before entering the restoration phase, stop if the
+    // current iterate is acceptable ("Restoration phase called at acceptable point")
+    if (!ls.accepted && current_is_acceptable(acc, e0, e0.err_at(0.0), fx, it, obj_scale, sc.square, o)) {
+      status = MPCX_SOLVED_TO_ACCEPTABLE;
+      break;
+    }
     // no acceptable trial and the last one is not even finite: IPOPT would enter its
     // restoration phase; stop with Restoration_Failed at the current (finite) iterate
     if (!ls.accepted && !(isfin(ls.tr.theta) && isfin(ls.tr.phi))) { status = MPCX_RESTORATION_FAILED; break; }
@@ -2043,9 +2090,9 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   if (args.stats != nullptr && lane == 0) {
     mpcx_stats st;
     st.obj = fx / obj_scale;
-    st.primal_inf = e0.primal_u;
+    st.primal_inf = e0.viol_u;
     st.dual_inf = e0.dual_u;
-    st.compl_inf = e0.compl_at(0.0);
+    st.compl_inf = e0.compl_at(0.0) / obj_scale;
     st.mu = mu;
     st.obj_scale = obj_scale;
     st.iter_count = it;

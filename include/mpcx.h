@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 4
+#define MPCX_API_VERSION 5
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -80,10 +80,19 @@ typedef struct mpcx_problem_desc {
   int32_t reserved;
 } mpcx_problem_desc;
 
-/* IPOPT-named options (defaults: mpcx_default_options). */
+/* IPOPT-named options (defaults: mpcx_default_options = IPOPT's own defaults).
+ * Termination follows IPOPT's OptimalityErrorConvergenceCheck: "Solve_Succeeded" when the
+ * scaled optimality error <= tol and the unscaled dual infeasibility, constraint violation
+ * and complementarity are below dual_inf_tol / constr_viol_tol / compl_inf_tol;
+ * "Solved_To_Acceptable_Level" after acceptable_iter consecutive iterates that meet the
+ * acceptable_* tolerances (acceptable_iter = 0 disables the counter), or when the line search
+ * fails at such an iterate.  The reference sets acceptable_tol 0.1, acceptable_iter 5,
+ * acceptable_constr_viol_tol 1, acceptable_compl_inf_tol 1
+ * (agentlib_mpc/data_structures/casadi_utils.py:197-206). */
 typedef struct mpcx_options {
   double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol;
-  double acceptable_tol;
+  double acceptable_tol, acceptable_dual_inf_tol, acceptable_constr_viol_tol;
+  double acceptable_compl_inf_tol, acceptable_obj_change_tol;
   double mu_init, mu_min, kappa_eps, kappa_mu, theta_mu, tau_min;
   double bound_push, bound_frac, bound_relax_factor, bound_mult_init_val;
   double constr_mult_init_max, kappa_sigma;
@@ -131,6 +140,8 @@ int mpcx_reserve(mpcx_handle* h, int32_t n_agents);
 int64_t mpcx_workspace_bytes_per_agent(const mpcx_handle* h);
 
 /* Batched solve.  Shapes (agent-major, fp64, device):
+ *   active [n_agents] int32 or NULL  agents with active[a] == 0 are skipped (their outputs
+ *                                     are left untouched): converged ADMM blocks
  *   p      [n_agents][np]            np = npg + n_stages*nps   (reference p order)
  *   lbw/ubw[n_agents][nw]            nw = nx + n_stages*(nv+nx) (reference x order)
  *   lbg/ubg[n_agents][ng_total] or NULL (then computed from the generated bound
@@ -142,7 +153,8 @@ int64_t mpcx_workspace_bytes_per_agent(const mpcx_handle* h);
  */
 int mpcx_batch_solve(mpcx_handle* h, int32_t n_agents, const double* p, const double* lbw,
                      const double* ubw, const double* lbg, const double* ubg, double* w_io,
-                     double* lam_g, double* lam_w, mpcx_stats* stats, void* stream);
+                     double* lam_g, double* lam_w, mpcx_stats* stats, const int32_t* active,
+                     void* stream);
 
 /* ---- ADMM kernels (agent-batched) --------------------------------------------------
  * Local trajectories are rows of `locals` [n_rows][T] (fp64, device).  The participants
@@ -150,15 +162,22 @@ int mpcx_batch_solve(mpcx_handle* h, int32_t n_agents, const double* p, const do
  * (device int32 array); max_group_rows = max over g of the group size (host value, sizes
  * the launch grid).  Groups [0, n_global) may have participants on other GPUs: their
  * moments are all-reduced (RCCL, sum) between mpcx_admm_moments and mpcx_admm_finalize;
- * groups [n_global, n_groups) are GPU-local.  One ADMM iteration of the reference
- * coordinator (admm_coordinator.py:288-304) is
- *   moments -> [all-reduce of the first mpcx_admm_reduce_count() doubles] -> finalize
+ * groups [n_global, n_groups) are GPU-local.
+ *
+ * Blocks: the groups form n_blocks independent consensus problems, each the counterpart of
+ * one reference ADMMCoordinator (block_g[g] = block of group g; NULL when n_blocks == 1).
+ * Residual totals are kept per block, each group may carry its own penalty rho_g[g]
+ * (NULL: the scalar rho for all) and groups with active_g[g] == 0 (NULL: all active) are
+ * frozen — the blocks that already met their stopping rule.  One ADMM iteration of the
+ * reference coordinator (admm_coordinator.py:288-304) is
+ *   moments -> [all-reduce of the first mpcx_admm_reduce_count doubles] -> finalize
  *   -> consensus_multipliers / exchange_update -> scatter into the NLP parameters.
  */
 #define MPCX_ADMM_TOTALS 8
-/* doubles in a moments buffer (zero it before mpcx_admm_moments); the all-reduce range
- * is the first n_global*(5T+1) + MPCX_ADMM_TOTALS doubles. */
-int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t T);
+/* doubles in a moments buffer (zero it before mpcx_admm_moments):
+ *   [n_global x (5T+1) global-group moments][n_blocks x MPCX_ADMM_TOTALS totals][local groups];
+ * the all-reduce range is the first n_global*(5T+1) + n_blocks*MPCX_ADMM_TOTALS doubles. */
+int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t n_blocks, int32_t T);
 
 /* Per (group, t) moments of the locals about center = the current mean [n_groups][T]:
  * sum(x-c), sum(x-c)^2 and, if multipliers != NULL (consensus rows), sum lam, sum lam^2,
@@ -166,36 +185,40 @@ int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t T);
  *   <- ConsensusVariable.update_mean_trajectory (admm_datatypes.py:221-236),
  *      ExchangeVariable.update_diff_trajectories (:292-309), ADMM._set_mean_coupling_values
  *      (modules/dmpc/admm/admm.py:528-570) — the participant sums of np.mean(axis=0). */
-int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t T, const int32_t* gstart,
-                      int32_t max_group_rows, const double* locals, const double* multipliers,
-                      const double* center, double* out, void* stream);
+int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
+                      const int32_t* gstart, int32_t max_group_rows, const double* locals,
+                      const double* multipliers, const double* center, double* out, void* stream);
 
-/* Groups [g_begin, g_end): mean <- c + S1/n, delta_mean <- c - mean (groups without
- * participants keep both); ADDS to totals[8]:
+/* Active groups [g_begin, g_end): mean <- c + S1/n, delta_mean <- c - mean (groups without
+ * participants keep both); ADDS to totals[block_g[g]][0..7]:
  *   {||r||^2, ||rho*delta_mean||^2, ||X||_F^2, ||mean||^2, ||Lambda_new||^2,
  *    #trajectories, #flat_multipliers, #groups}
  * with the reference's conventions: consensus r = mean - x_i and Lambda_new the updated
  * per-participant multipliers; exchange (exchange[g] != 0) r = mean and Lambda_new =
  * group_multipliers + rho*mean  <- ADMMCoordinator._check_convergence
  * (admm_coordinator.py:354-435), CouplingVariable.get_residual (admm_datatypes.py:202-214). */
-int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_global, int32_t T,
+int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_global, int32_t n_blocks, int32_t T,
                        const double* moments, const int32_t* exchange,
-                       const double* group_multipliers, double rho, double* mean,
+                       const double* group_multipliers, double rho, const double* rho_g,
+                       const int32_t* active_g, const int32_t* block_g, double* mean,
                        double* delta_mean, double* totals, void* stream);
 
-/* consensus: r = mean[g] - x_i ; lambda_i <- lambda_i - rho * r  (res may be NULL)
+/* consensus: r = mean[g] - x_i ; lambda_i <- lambda_i - rho_g * r  (res may be NULL)
  *   <- ConsensusVariable.update_multipliers (admm_datatypes.py:238-267),
  *      ADMM.update_lambda (admm.py:612-633) */
 int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, const int32_t* gstart,
                                     int32_t max_group_rows, const double* locals,
-                                    const double* mean, double rho, double* multipliers,
+                                    const double* mean, double rho, const double* rho_g,
+                                    const int32_t* active_g, double* multipliers,
                                     double* primal_residual, void* stream);
-/* exchange: diff_i <- x_i - mean[g]; if rho != 0: lambda[g] <- lambda[g] + rho*mean[g]
+/* exchange: diff_i <- x_i - mean[g]; if update_multiplier: lambda[g] <- lambda[g] + rho_g*mean[g]
  *   <- ExchangeVariable.update_diff_trajectories / update_multiplier
  *      (admm_datatypes.py:292-324), admm.py:550-570, 635-655 */
 int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* gstart,
                               int32_t max_group_rows, const double* locals, const double* mean,
-                              double* diff, double* multiplier, double rho, void* stream);
+                              double* diff, double* multiplier, int32_t update_multiplier,
+                              double rho, const double* rho_g, const int32_t* active_g,
+                              void* stream);
 /* Shift rows by one control interval: x[i][:] <- x[i][shift:] ++ x[i][T-shift:]
  *   <- ConsensusVariable/ExchangeVariable.shift_values_by_one (admm_datatypes.py:275-282,
  *      326-331), ADMM._shift (admm.py:329-342) */

@@ -142,12 +142,15 @@ class _Exchange:
 
 def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max, primal_tol=1e-3,
                       dual_tol=1e-3, use_relative_tolerances=True, abs_tol=1e-3, rel_tol=1e-3,
-                      penalty_change_threshold=-1.0, penalty_change_factor=2.0, T=None, state=None):
+                      penalty_change_threshold=-1.0, penalty_change_factor=2.0, T=None, state=None,
+                      solve_batch=None):
     """One round of ``ADMMCoordinator._fast_process`` (`admm_coordinator.py:259-321`).
 
     participation: {agent: {alias: "consensus"|"exchange"}}; initial: {agent: {alias: value}}
     solve(agent, {alias: (mean_or_diff, multiplier)}, rho) -> {alias: local trajectory}
-    Returns (state, history [(primal, dual, rho)], iterations, converged).
+    solve_batch (optional): [(agent, inputs)], rho -> [outputs] — the same solves of one
+    iteration at once (they are independent; the fixture generators run them in parallel).
+    Returns (state, history [(primal, dual, rho after the variation)], iterations, converged).
     """
     if state is None:  # registration (`admm_coordinator.py:528-560`)
         state = {"vars": {}, "order": []}
@@ -169,14 +172,17 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
     converged = False
     it = 0
     for it in range(1, admm_iter_max + 1):
+        reqs = []
         for ag, coups in participation.items():
             inp = {}
             for al, kind in coups.items():
                 v = vars_[al]
                 inp[al] = (np.array(v.mean), np.array(v.mult[ag])) if kind == "consensus" else \
                     (np.array(v.diff[ag]), np.array(v.mult))
-            out = solve(ag, inp, rho)
-            for al in coups:
+            reqs.append((ag, inp))
+        outs = solve_batch(reqs, rho) if solve_batch is not None else [solve(ag, inp, rho) for ag, inp in reqs]
+        for (ag, _), out in zip(reqs, outs):
+            for al in participation[ag]:
                 vars_[al].local[ag] = list(np.ravel(out[al]))
         for v in vars_.values():
             v.update_mean()
@@ -193,12 +199,14 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
             else:
                 flat_mult.extend(v.mult)
         pn, dn = float(np.linalg.norm(prim)), float(np.linalg.norm(dual))
-        hist.append((pn, dn, rho))
+        # _check_convergence varies the penalty first and records it afterwards
+        # (`admm_coordinator.py:396-397`)
         if penalty_change_threshold > 1:
             if pn > penalty_change_threshold * dn:
                 rho = rho * penalty_change_factor
             elif dn > penalty_change_threshold * pn:
                 rho = rho / penalty_change_factor
+        hist.append((pn, dn, rho))
         if use_relative_tolerances:
             sp = max(_norm_lists(flat_locals), float(np.linalg.norm(flat_means)))
             sd = _norm_lists(flat_mult)

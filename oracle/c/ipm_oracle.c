@@ -126,9 +126,14 @@ void oracle_room_init(room_t* m, int N, int d, double ts, const double* B, const
 /* --------------------------------------------------------------------------
  * IPM
  * -------------------------------------------------------------------------- */
+/* IPOPT termination options (OptimalityErrorConvergenceCheck); the reference sets
+   tol 1e-4, max_iter 100, acceptable_tol 0.1, acceptable_iter 5,
+   acceptable_constr_viol_tol 1, acceptable_compl_inf_tol 1 (casadi_utils.py:197-206) */
 typedef struct {
   double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol;
-  int max_iter;
+  double acceptable_tol, acceptable_dual_inf_tol, acceptable_constr_viol_tol;
+  double acceptable_compl_inf_tol, acceptable_obj_change_tol;
+  int max_iter, acceptable_iter;
 } opts_t;
 
 typedef struct {
@@ -431,7 +436,10 @@ static double barrier_of(const ws_t* w, const double* xv, const double* sv) {
   }
   return t;
 }
-static double opt_error(const ws_t* w, double mu, double* dual_u, double* primal_u, double* compl_) {
+/* scaled optimality error; unscaled dual infeasibility (x and slack parts), constraint
+   violation (|c| and the violation of the relaxed bounds of d) and complementarity as IPOPT's
+   unscaled_curr_* quantities */
+static double opt_error(const ws_t* w, double mu, double* dual_u, double* viol_u, double* compl_) {
   double dmax = 0, du = 0, pmax = 0, pu = 0, cmax = 0, lsum = 0, zsum = 0;
   int nz = 0;
   for (int i = w->NX; i < w->NW; ++i) {
@@ -444,27 +452,42 @@ static double opt_error(const ws_t* w, double mu, double* dual_u, double* primal
   }
   for (int c = 0; c < w->M; ++c) {
     const int cl = ccls(w, c);
-    double cv;
-    if (cl == 0) cv = w->gv[c] - w->gs[c] * w->lb[c];
+    double cv, vv = 0.0;
+    if (cl == 0) { cv = w->gv[c] - w->gs[c] * w->lb[c]; vv = fabs(cv); }
     else {
       cv = w->gv[c] - w->s[c];
       if (cl == 1) {
-        dmax = fmax(dmax, fabs(-w->lam[c] - w->vL[c] + w->vU[c]));
+        const double rs = -w->lam[c] - w->vL[c] + w->vU[c];
+        dmax = fmax(dmax, fabs(rs));
+        du = fmax(du, fabs(rs) * w->gs[c] / w->obj_scale);
+        vv = fmax(0.0, fmax(w->sL[c] - w->gv[c], w->gv[c] - w->sU[c]));
         if (isfin(w->sL[c])) { cmax = fmax(cmax, fabs((w->s[c] - w->sL[c]) * w->vL[c] - mu)); zsum += fabs(w->vL[c]); nz++; }
         if (isfin(w->sU[c])) { cmax = fmax(cmax, fabs((w->sU[c] - w->s[c]) * w->vU[c] - mu)); zsum += fabs(w->vU[c]); nz++; }
       }
     }
     pmax = fmax(pmax, fabs(cv));
-    pu = fmax(pu, fabs(cv) / w->gs[c]);
+    pu = fmax(pu, vv / w->gs[c]);
     lsum += fabs(w->lam[c]);
   }
   const double s_d = fmax(100.0, (lsum + zsum) / fmax(1.0, (double)(w->M + nz))) / 100.0;
   const double s_c = nz > 0 ? fmax(100.0, zsum / nz) / 100.0 : 1.0;
   if (dual_u) *dual_u = du;
-  if (primal_u) *primal_u = pu;
-  if (compl_) *compl_ = cmax;
+  if (viol_u) *viol_u = pu;
+  if (compl_) *compl_ = cmax / w->obj_scale;
   return fmax(fmax(dmax / s_d, pmax), cmax / s_c);
 }
+/* IPOPT OptimalityErrorConvergenceCheck::CurrentIsAcceptable (objective change between the
+   last two iterations it was called at; initially -1e50) */
+typedef struct { double curr_f, last_f; int last_it, count; } acc_t;
+static int current_is_acceptable(acc_t* ac, const opts_t* o, int square, double err, double du,
+                                 double viol, double cmpl, double fx, int it) {
+  if (it != ac->last_it) { ac->last_f = ac->curr_f; ac->curr_f = fx; ac->last_it = it; }
+  if (square) return err <= o->acceptable_tol && viol <= o->acceptable_constr_viol_tol;
+  return err <= o->acceptable_tol && du <= o->acceptable_dual_inf_tol && viol <= o->acceptable_constr_viol_tol &&
+         cmpl <= o->acceptable_compl_inf_tol &&
+         fabs(ac->curr_f - ac->last_f) / fmax(1.0, fabs(ac->curr_f)) <= o->acceptable_obj_change_tol;
+}
+
 static double push_into(double v, double lo, double hi) {
   const int hl = isfin(lo), hu = isfin(hi);
   double pl = hl ? 1e-2 * fmax(1.0, fabs(lo)) : 0.0, pu = hu ? 1e-2 * fmax(1.0, fabs(hi)) : 0.0;
@@ -563,15 +586,29 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
   const double theta_max = 1e4 * fmax(1.0, theta0), theta_min = 1e-4 * fmax(1.0, theta0);
   double fth[64], fph[64];
   int nfilt = 0, status = -1, it = 0;
+  int nfree = 0, neq = 0;
+  for (int i = NX; i < NW; ++i) nfree += !fixedv(w, i);
+  for (int c = 0; c < M; ++c) neq += w->lb[c] == w->ub[c];
+  const int square = nfree == neq;
+  acc_t acc = {-1e50, -1e50, -1, 0};
   for (;;) {
     double du, pu, cmpl;
     const double err = opt_error(w, 0.0, &du, &pu, &cmpl);
     if (err != err || fx != fx) { status = -4; break; }
-    if (err <= o->tol && du <= o->dual_inf_tol && pu <= o->constr_viol_tol && cmpl <= o->compl_inf_tol) { status = 0; break; }
+    if (err <= o->tol && pu <= o->constr_viol_tol && (square || (du <= o->dual_inf_tol && cmpl <= o->compl_inf_tol))) {
+      status = 0;
+      break;
+    }
+    if (o->acceptable_iter > 0 && current_is_acceptable(&acc, o, square, err, du, pu, cmpl, fx, it)) {
+      if (++acc.count >= o->acceptable_iter) { status = 1; break; }
+    } else {
+      acc.count = 0;
+    }
     if (it >= o->max_iter) break;
     for (int g = 0; g < 64; ++g) {
       if (opt_error(w, mu, 0, 0, 0) > 10.0 * mu || mu <= 1e-11) break;
-      const double new_mu = fmax(fmax(o->tol / 10.0, 1e-11), fmin(0.2 * mu, pow(mu, 1.5)));
+      /* IPOPT MonotoneMuUpdate: floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1) */
+      const double new_mu = fmax(fmax(fmin(o->tol, o->compl_inf_tol) / 11.0, 1e-11), fmin(0.2 * mu, pow(mu, 1.5)));
       if (new_mu == mu) break;  /* IPOPT: done when mu no longer changes */
       mu = new_mu;
       tau = fmax(0.99, 1.0 - mu);
@@ -697,6 +734,8 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
       alpha *= 0.5;
       if (alpha < amin) break;
     }
+    /* IPOPT: restoration phase called at an acceptable point -> Solved_To_Acceptable_Level */
+    if (!accepted && current_is_acceptable(&acc, o, square, err, du, pu, cmpl, fx, it)) { status = 1; break; }
     /* no acceptable trial and the last one is not even finite: IPOPT would enter
        restoration; stop with Restoration_Failed at the current (finite) iterate */
     if (!accepted && !(isfin(last_th) && isfin(last_ph))) { status = -2; break; }
@@ -749,11 +788,12 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
   st->n_trials = n_trials;
 }
 
-/* Solve n_agents one_room NLPs (agent-major arrays); returns #converged. */
+/* Solve n_agents one_room NLPs (agent-major arrays); returns #converged (success flag:
+   Solve_Succeeded or Solved_To_Acceptable_Level). */
 int oracle_room_solve_fleet(const room_t* m, int n_agents, const double* p, const double* lbw,
-                            const double* ubw, double* w_io, ostats_t* stats, double tol,
-                            int max_iter, int threads) {
-  opts_t o = {tol, 1.0, 1e-4, 1e-4, max_iter};
+                            const double* ubw, double* w_io, ostats_t* stats, const opts_t* opts,
+                            int threads) {
+  const opts_t o = *opts;
   const int NW = m->nx + m->N * (m->nv + m->nx), NPAR = m->npg + m->N * m->nps;
   const int NB = m->nv + m->nx + m->ng, NL = 2 * m->nx + m->nv, M = m->N * m->ng;
   const long dbl = 8L * NW + 14L * M + (long)m->N * (NL + m->ng * NL + NL * NL + NB * NB + 2 * NB) + 64;
@@ -769,7 +809,7 @@ int oracle_room_solve_fleet(const room_t* m, int n_agents, const double* p, cons
     for (int a = 0; a < n_agents; ++a) {
       solve_one(m, p + (long)a * NPAR, lbw + (long)a * NW, ubw + (long)a * NW, w_io + (long)a * NW,
                 &o, &stats[a], mem, imem);
-      ok += stats[a].status == 0;
+      ok += stats[a].status == 0 || stats[a].status == 1;
     }
     free(mem);
     free(imem);
@@ -778,3 +818,4 @@ int oracle_room_solve_fleet(const room_t* m, int n_agents, const double* p, cons
 }
 
 int oracle_room_sizeof(void) { return (int)sizeof(room_t); }
+int oracle_opts_sizeof(void) { return (int)sizeof(opts_t); }

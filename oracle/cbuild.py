@@ -31,6 +31,21 @@ class RoomT(ctypes.Structure):
     ]
 
 
+class OOpts(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "tol", "dual_inf_tol", "constr_viol_tol", "compl_inf_tol", "acceptable_tol",
+        "acceptable_dual_inf_tol", "acceptable_constr_viol_tol", "acceptable_compl_inf_tol",
+        "acceptable_obj_change_tol")] + [("max_iter", ctypes.c_int), ("acceptable_iter", ctypes.c_int)]
+
+
+def options(**kw) -> OOpts:
+    """IPOPT termination options; defaults are IPOPT's own (acceptable_iter 15 ...)."""
+    from oracle.ipm import IPMOptions
+
+    d = IPMOptions(**kw)
+    return OOpts(**{n: getattr(d, n) for n, _ in OOpts._fields_})
+
+
 class OStats(ctypes.Structure):
     _fields_ = [("obj", ctypes.c_double)] + [(n, ctypes.c_int) for n in ("iter", "status", "n_fact", "n_trials")]
 
@@ -62,9 +77,10 @@ def lib():
         vp = ctypes.c_void_p
         _lib.oracle_room_init.argtypes = [ctypes.POINTER(RoomT), ctypes.c_int, ctypes.c_int, ctypes.c_double, vp, vp, vp]
         _lib.oracle_room_solve_fleet.argtypes = [ctypes.POINTER(RoomT), ctypes.c_int, vp, vp, vp, vp,
-                                                 ctypes.POINTER(OStats), ctypes.c_double, ctypes.c_int, ctypes.c_int]
+                                                 ctypes.POINTER(OStats), ctypes.POINTER(OOpts), ctypes.c_int]
         _lib.oracle_room_solve_fleet.restype = ctypes.c_int
         assert _lib.oracle_room_sizeof() == ctypes.sizeof(RoomT)
+        assert _lib.oracle_opts_sizeof() == ctypes.sizeof(OOpts)
     return _lib
 
 
@@ -80,9 +96,11 @@ def room_model(N=15, d=2, ts=300.0) -> RoomT:
     return m
 
 
-def solve_room_fleet(p, lbw, ubw, w0, N=15, d=2, tol=1e-8, max_iter=500, threads=0):
-    """Returns (w, stats list of dicts, n_converged)."""
+def solve_room_fleet(p, lbw, ubw, w0, N=15, d=2, tol=1e-8, max_iter=500, threads=0, **ipopt):
+    """Returns (w, stats list of dicts, n_converged).  ``ipopt``: further IPOPT termination
+    options (acceptable_*); without them IPOPT's defaults apply."""
     m = room_model(N, d)
+    opts = options(tol=tol, max_iter=max_iter, **ipopt)
     p = np.ascontiguousarray(p, dtype=np.float64)
     lbw = np.ascontiguousarray(lbw, dtype=np.float64)
     ubw = np.ascontiguousarray(ubw, dtype=np.float64)
@@ -90,7 +108,7 @@ def solve_room_fleet(p, lbw, ubw, w0, N=15, d=2, tol=1e-8, max_iter=500, threads
     n = p.shape[0]
     st = (OStats * n)()
     ok = lib().oracle_room_solve_fleet(ctypes.byref(m), n, p.ctypes.data, lbw.ctypes.data, ubw.ctypes.data,
-                                       w.ctypes.data, st, tol, max_iter, threads)
+                                       w.ctypes.data, st, ctypes.byref(opts), threads)
     stats = [{"obj": s.obj, "iter": s.iter, "status": s.status, "n_fact": s.n_fact, "n_trials": s.n_trials}
              for s in st]
     return w, stats, ok

@@ -39,6 +39,15 @@ class IPMOptions:
     dual_inf_tol: float = 1.0
     constr_viol_tol: float = 1e-4
     compl_inf_tol: float = 1e-4
+    # acceptable-level termination (IPOPT defaults; the reference overrides acceptable_tol,
+    # acceptable_iter, acceptable_constr_viol_tol, acceptable_compl_inf_tol:
+    # agentlib_mpc/data_structures/casadi_utils.py:197-206)
+    acceptable_tol: float = 1e-6
+    acceptable_iter: int = 15
+    acceptable_dual_inf_tol: float = 1e10
+    acceptable_constr_viol_tol: float = 1e-2
+    acceptable_compl_inf_tol: float = 1e-2
+    acceptable_obj_change_tol: float = 1e20
     mu_init: float = 0.1
     mu_min: float = 1e-11
     kappa_eps: float = 10.0
@@ -263,6 +272,34 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
         val -= mu_ * np.sum(np.log(sU[shasU] - s[shasU]))
         return float(val)
 
+    def unscaled(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, compl):
+        """IPOPT's unscaled_curr_dual_infeasibility (grad_lag_x and grad_lag_s * d_scale,
+        divided by obj_scale), unscaled_curr_nlp_constraint_violation (|c| and the violation
+        of the relaxed bounds of d - not d - s) and unscaled_curr_complementarity."""
+        rd_u = (gfx + Jx.T @ lam - zL + zU) / obj_scale
+        rs_u = np.where(ineq & ~free_slack, (-lam - vL + vU) * g_scale, 0.0) / obj_scale
+        dual_u = max(np.max(np.abs(rd_u[free]), initial=0.0), np.max(np.abs(rs_u), initial=0.0))
+        c_eq = np.where(eq, np.abs(gx - lbg * g_scale), 0.0)
+        d_viol = np.where(ineq, np.maximum(0.0, np.maximum(np.where(np.isfinite(sL), sL - gx, 0.0),
+                                                           np.where(np.isfinite(sU), gx - sU, 0.0))), 0.0)
+        viol_u = np.max((c_eq + d_viol) / g_scale, initial=0.0) if m else 0.0
+        return dual_u, viol_u, compl / obj_scale
+
+    n_eq = int(np.sum(eq))
+    square = int(np.sum(free)) == n_eq  # IPOPT IsSquareProblem
+    acc = dict(curr_f=-1e50, last_f=-1e50, last_it=-1, count=0)
+
+    def current_is_acceptable(err0, dual_u, viol_u, compl_u, fx_, it_):
+        """IPOPT OptimalityErrorConvergenceCheck::CurrentIsAcceptable."""
+        if it_ != acc["last_it"]:
+            acc["last_f"], acc["curr_f"], acc["last_it"] = acc["curr_f"], fx_, it_
+        if square:
+            return err0 <= o.acceptable_tol and viol_u <= o.acceptable_constr_viol_tol
+        return (err0 <= o.acceptable_tol and dual_u <= o.acceptable_dual_inf_tol
+                and viol_u <= o.acceptable_constr_viol_tol and compl_u <= o.acceptable_compl_inf_tol
+                and abs(acc["curr_f"] - acc["last_f"]) / max(1.0, abs(acc["curr_f"]))
+                <= o.acceptable_obj_change_tol)
+
     theta0 = theta_of(gx, s)
     theta_max = o.theta_max_fact * max(1.0, theta0)
     theta_min = o.theta_min_fact * max(1.0, theta0)
@@ -270,19 +307,25 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
     history = []
     status = "Maximum_Iterations_Exceeded"
     it = 0
-    mu_floor = max(o.tol / 10.0, o.mu_min)
+    # IPOPT MonotoneMuUpdate::CalcNewMuAndTau: mu >= min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
+    mu_floor = max(min(o.tol, o.compl_inf_tol) / (o.kappa_eps + 1.0), o.mu_min)
     while True:
         err0, dual, primal, compl = opt_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, 0.0)
-        # unscaled checks
-        rd_u = (gfx + Jx.T @ lam - zL + zU) / obj_scale
-        c_u = np.where(ineq, gx - s, gx - np.where(eq, lbg * g_scale, 0.0)) / g_scale if m else np.zeros(0)
+        dual_u, viol_u, compl_u = unscaled(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, compl)
         if record:
             history.append(dict(iter=it, mu=mu, err=err0, f=fx / obj_scale, x=x.copy()))
-        if (err0 <= o.tol and np.max(np.abs(rd_u[free]), initial=0) <= o.dual_inf_tol
-                and np.max(np.abs(c_u), initial=0) <= o.constr_viol_tol
-                and compl <= o.compl_inf_tol):
+        # IPOPT OptimalityErrorConvergenceCheck::CheckConvergence
+        if (err0 <= o.tol and viol_u <= o.constr_viol_tol
+                and (square or (dual_u <= o.dual_inf_tol and compl_u <= o.compl_inf_tol))):
             status = "Solve_Succeeded"
             break
+        if o.acceptable_iter > 0 and current_is_acceptable(err0, dual_u, viol_u, compl_u, fx, it):
+            acc["count"] += 1
+            if acc["count"] >= o.acceptable_iter:
+                status = "Solved_To_Acceptable_Level"
+                break
+        else:
+            acc["count"] = 0
         if it >= o.max_iter:
             break
         # barrier update
@@ -402,6 +445,10 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
             alpha *= 0.5
             if alpha < a_min:
                 break
+        if not accepted and current_is_acceptable(err0, dual_u, viol_u, compl_u, fx, it):
+            # IPOPT BacktrackingLineSearch: "Restoration phase called at acceptable point"
+            status = "Solved_To_Acceptable_Level"
+            break
         if not accepted and not (np.isfinite(th_t) and np.isfinite(ph_t)):
             # no acceptable trial and the last one is not even finite: IPOPT would enter
             # its restoration phase; stop with Restoration_Failed at the current iterate
@@ -438,7 +485,8 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
     lam_g = lam * g_scale / obj_scale
     lam_x = (zU - zL) / obj_scale
     return IPMResult(x=x, lam_g=lam_g, lam_x=lam_x, f=fx / obj_scale, iterations=it,
-                     status=status, success=status == "Solve_Succeeded", history=history)
+                     status=status, success=status in ("Solve_Succeeded", "Solved_To_Acceptable_Level"),
+                     history=history)
 
 
 def _block_eigs(D: np.ndarray) -> np.ndarray:

@@ -1,5 +1,6 @@
+# GPU parity suite (tests marked gpu), one pytest process, per-test timeout
 set -o pipefail
 mkdir -p gpurun_out
-rocm-smi --showproductname > gpurun_out/smi.txt 2>&1 || true
-timeout -k 10 600 python -m pytest tests/test_gpu_ipm.py -x -q > gpurun_out/gpu1.log 2>&1
-echo "exit $?" >> gpurun_out/gpu1.log
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_parity.log 2>&1
+echo "parity exit $?"

@@ -27,7 +27,7 @@ class _Solver:
             fixed = lbw == ubw
             w0[fixed] = lbw[fixed]
         r = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p),
-                      ipm.IPMOptions(tol=self.tol, max_iter=500))
+                      ipm.IPMOptions(tol=self.tol, max_iter=500, acceptable_iter=0))
         assert r.success, (key, r.status)
         self.last[key] = r.x
         return r.x

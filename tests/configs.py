@@ -97,6 +97,9 @@ def _tz(kind, **kw) -> Case:
     N = kw.get("N", 24)
     prob = nlps.tz_ahu(N=N) if kind == "ahu" else nlps.tz_cca(N=N)
     o = {k: kw[k] for k in ("rho", "zbar", "lam", "mDot_0", "r_T_v") if k in kw}
+    for k in ("zbar", "lam"):
+        if k in o and np.ndim(o[k]) == 0:
+            o[k] = np.full((6, N), float(o[k]))
     if kind == "ahu" and "T_amb" in kw:
         o["T_amb"] = kw["T_amb"]
     return Case(be, cv, prob, nlps.tz_supply_inputs(prob, N=N, **o))

@@ -22,16 +22,17 @@ class CpuADMMOps:
         self.oracle_problems = oracle_problems  # class name -> oracle.nlps.OracleProblem
         self.tol = tol
 
-    def solve(self, cls):
+    def solve(self, cls, active=None):
         prob = self.oracle_problems[cls.name]
         P, LB, UB, W = (t.numpy() for t in (cls.P, cls.LB, cls.UB, cls.W))
         st = cls.ST.view(torch.int32).view(cls.n, -1).numpy()
-        for a in range(cls.n):
+        act = np.ones(cls.n, bool) if active is None else active.numpy() != 0
+        for a in np.flatnonzero(act):
             p = P[a]
             r = ipm.solve(prob.functions(p), W[a].copy(), LB[a], UB[a], prob.lbg(p), prob.ubg(p),
-                          ipm.IPMOptions(tol=self.tol, max_iter=500))
+                          ipm.IPMOptions(tol=self.tol, max_iter=500, acceptable_iter=0))
             W[a] = r.x
-            st[a, 13] = 0 if r.success else -1
+            st[a, 13] = {"Solve_Succeeded": 0, "Solved_To_Acceptable_Level": 1}.get(r.status, -1)
 
     def gather_rows(self, T, src, cols, dst, dst_rows):
         dst.numpy()[dst_rows.numpy()] = src.numpy()[:, cols.numpy()]
@@ -45,21 +46,21 @@ class CpuADMMOps:
     def fill_column(self, dst, col, value):
         dst.numpy()[:, col] = value
 
-    def moments_size(self, n_groups, T):
-        return n_groups * (NMOM * T + 1) + TOTALS
+    def moments_size(self, n_groups, n_blocks, T):
+        return n_groups * (NMOM * T + 1) + TOTALS * n_blocks
 
     @staticmethod
-    def _off(g, n_global, T):
-        return g * (NMOM * T + 1) + (TOTALS if g >= n_global else 0)
+    def _off(g, n_global, n_blocks, T):
+        return g * (NMOM * T + 1) + (TOTALS * n_blocks if g >= n_global else 0)
 
-    def moments(self, n_groups, n_global, T, gstart, max_rows, X, LAM, center, out):
+    def moments(self, n_groups, n_global, n_blocks, T, gstart, max_rows, X, LAM, center, out):
         gs, x, c, o = gstart.numpy(), X.numpy(), center.numpy(), out.numpy()
         lam = None if LAM is None else LAM.numpy()
         for g in range(n_groups):
             r0, r1 = gs[g], gs[g + 1]
             if r1 <= r0:
                 continue
-            b = self._off(g, n_global, T)
+            b = self._off(g, n_global, n_blocks, T)
             d = x[r0:r1] - c[g]
             o[b:b + T] += d.sum(0)
             o[b + T:b + 2 * T] += (d * d).sum(0)
@@ -70,12 +71,21 @@ class CpuADMMOps:
                 o[b + 4 * T:b + 5 * T] += (l * d).sum(0)
             o[b + NMOM * T] += r1 - r0
 
-    def finalize(self, g0, g1, n_global, T, mom, exchange, gmult, rho, mean, dmean, totals):
-        o, m, dm, tot = mom.numpy(), mean.numpy(), dmean.numpy(), totals.numpy()
+    @staticmethod
+    def _g(rho, rho_g, active_g, g):
+        on = active_g is None or active_g.numpy()[g] != 0
+        return on, (rho if rho_g is None else float(rho_g.numpy()[g]))
+
+    def finalize(self, g0, g1, n_global, n_blocks, T, mom, exchange, gmult, rho_s, rho_g, active_g, block_g,
+                 mean, dmean, totals):
+        o, m, dm, tot_all = mom.numpy(), mean.numpy(), dmean.numpy(), totals.numpy().reshape(-1)
         ex = None if exchange is None else exchange.numpy()
         gm = None if gmult is None else gmult.numpy()
         for g in range(g0, g1):
-            b = self._off(g, n_global, T)
+            on, rho = self._g(rho_s, rho_g, active_g, g)
+            if not on:
+                continue
+            b = self._off(g, n_global, n_blocks, T)
             n = o[b + NMOM * T]
             if n <= 0:
                 continue
@@ -93,20 +103,28 @@ class CpuADMMOps:
             else:
                 sl, sl2, slx = o[b + 2 * T:b + 3 * T], o[b + 3 * T:b + 4 * T], o[b + 4 * T:b + 5 * T]
                 ls = (sl2 + 2 * rho * (slx - d * sl) + rho * rho * var).sum()
-            tot += [prim, ((rho * (c - new)) ** 2).sum(), (s2 + 2 * c * s1 + n * c * c).sum(),
-                    (new * new).sum(), ls, n, T if is_ex else n, 1.0]
+            k = 0 if block_g is None else int(block_g.numpy()[g])
+            tot_all[k * TOTALS:(k + 1) * TOTALS] += [
+                prim, ((rho * (c - new)) ** 2).sum(), (s2 + 2 * c * s1 + n * c * c).sum(),
+                (new * new).sum(), ls, n, T if is_ex else n, 1.0]
 
-    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho, LAM):
+    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho_s, rho_g, active_g, LAM):
         gs, x, m, lam = gstart.numpy(), X.numpy(), mean.numpy(), LAM.numpy()
         for g in range(n_groups):
-            lam[gs[g]:gs[g + 1]] -= rho * (m[g] - x[gs[g]:gs[g + 1]])
+            on, rho = self._g(rho_s, rho_g, active_g, g)
+            if on:
+                lam[gs[g]:gs[g + 1]] -= rho * (m[g] - x[gs[g]:gs[g + 1]])
 
-    def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, rho):
+    def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, update, rho_s, rho_g,
+                        active_g):
         gs, x, m, df = gstart.numpy(), X.numpy(), mean.numpy(), diff.numpy()
         for g in range(n_groups):
+            on, rho = self._g(rho_s, rho_g, active_g, g)
+            if not on:
+                continue
             df[gs[g]:gs[g + 1]] = x[gs[g]:gs[g + 1]] - m[g]
-        if rho != 0.0:
-            gmult.numpy()[:n_groups] += rho * m[:n_groups]
+            if update:
+                gmult.numpy()[g] += rho * m[g]
 
     def shift(self, T, shift, x):
         a = x.numpy()

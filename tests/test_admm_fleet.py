@@ -110,6 +110,52 @@ def test_coordinated_closed_loop_rounds_match_oracle():
             np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
 
 
+def test_coordinated_exchange_round_matches_oracle():
+    """Coordinator-driven exchange ADMM (examples/exchange_admm with the coordinator):
+    the exchange alias's mean is not shifted between rounds — only its multiplier and
+    the diffs are (`ExchangeVariable.shift_values_by_one`, `admm_datatypes.py:326-331`) —
+    so the first dual residual is taken against the unshifted mean."""
+    N, iters = 3, 3
+    fl = ADMMFleet(bm.c4_fleet_classes(n_rooms=2, n_supply=1, N=N), device="cpu", ops=_c4_ops(N))
+    orc = C4Oracle(N, bm.C4_ROOMS[:2])
+    kw = dict(admm_iter_max=iters, use_relative_tolerances=False, primal_tol=1e-12, dual_tol=1e-12)
+    state = None
+    for step in range(2):
+        out = fl.run_coordinated(1e4, **kw)
+        state, hist, it, conv = oadmm.coordinated_round(orc.participation, orc.initial, orc, 1e4, N, T=N,
+                                                        state=state, **kw)
+        assert out["iterations"] == it
+        got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["records"]])
+        np.testing.assert_allclose(got, np.array(hist), rtol=RTOL, atol=1e-10)
+        np.testing.assert_allclose(fl.trajectories()["mDot_coupling"], state["vars"]["mDot_coupling"].mean,
+                                   rtol=RTOL, atol=1e-10)
+        np.testing.assert_allclose(fl.multipliers_of("supply", "mDot_out")[0], state["vars"]["mDot_coupling"].mult,
+                                   rtol=RTOL, atol=1e-6)
+
+
+def test_blocks_run_like_their_own_coordinators():
+    """Two independent 4-room blocks in one fleet: per-block stopping test and penalty
+    variation; each block's history equals a single-block run of that block."""
+    N = 2
+    kw = dict(admm_iter_max=4, use_relative_tolerances=False, primal_tol=1e-3, dual_tol=5e-3,
+              penalty_change_threshold=1.5, penalty_change_factor=1.3)
+    two = ADMMFleet(bm.c2_fleet_classes(n_blocks=2, N=N, seed=3), device="cpu", ops=_c2_ops(N))
+    assert two.n_blocks == 2 and [two.block_index(f"mDot1_coupling_b{b}") for b in (0, 1)] == [0, 1]
+    out = two.run_coordinated(0.4, **kw)
+    for b in (0, 1):
+        one = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N, seed=3, block_offset=b), device="cpu",
+                        ops=_c2_ops(N))
+        o1 = one.run_coordinated(0.4, **kw)
+        assert out["block_iterations"][b] == o1["iterations"]
+        assert bool(out["block_converged"][b]) == o1["converged"]
+        got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["block_records"][b]])
+        want = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in o1["records"]])
+        np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12)
+        for i in range(4):
+            al = f"mDot{i + 1}_coupling_b{b}"
+            np.testing.assert_allclose(two.trajectories()[al], one.trajectories()[al], rtol=1e-9, atol=1e-12)
+
+
 def test_local_exchange_closed_loop_rounds_match_oracle():
     """Three LocalADMM control steps (shift of own trajectory and multipliers,
     `admm.py:873-937`) with new room measurements between them."""

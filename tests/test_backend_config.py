@@ -17,12 +17,27 @@ def _backend(solver):
         "type": "casadi", "model": {"type": "agentlib_mpc_amd.models.examples.OneRoom"}, "solver": solver})
 
 
+REF = {"max_iter": 100, "tol": 1e-4, "acceptable_tol": 0.1, "acceptable_constr_viol_tol": 1.0,
+       "acceptable_iter": 5, "acceptable_compl_inf_tol": 1.0}
+
+
 def test_reference_defaults_and_overrides():
-    assert ipopt_options_to_kernel({}) == {"max_iter": 100, "tol": 1e-4}
-    assert ipopt_options_to_kernel({"ipopt": {"tol": 1e-8}, "ipopt.max_iter": 7}) == {"max_iter": 7, "tol": 1e-8}
+    # casadi_utils.py:197-206, including the acceptable-level termination settings
+    assert ipopt_options_to_kernel({}) == REF
+    assert ipopt_options_to_kernel({"ipopt": {"tol": 1e-8}, "ipopt.max_iter": 7}) == {**REF, "max_iter": 7,
+                                                                                       "tol": 1e-8}
+    assert ipopt_options_to_kernel({"ipopt": {"acceptable_iter": 0, "acceptable_obj_change_tol": 1e-3}}) == {
+        **REF, "acceptable_iter": 0, "acceptable_obj_change_tol": 1e-3}
     # IPOPT options the kernel has no counterpart for are accepted and ignored
-    assert ipopt_options_to_kernel({"ipopt": {"print_level": 0, "linear_solver": "ma27"}}) == {
-        "max_iter": 100, "tol": 1e-4}
+    assert ipopt_options_to_kernel({"ipopt": {"print_level": 0, "linear_solver": "ma27"}}) == REF
+
+
+def test_kernel_option_names_cover_the_acceptable_criteria():
+    from agentlib_mpc_amd.runtime.native import Options
+
+    names = {n for n, _ in Options._fields_}
+    assert set(REF) <= names
+    assert {"acceptable_dual_inf_tol", "acceptable_obj_change_tol"} <= names
 
 
 def test_fatrop_configs_run_on_the_kernel():

@@ -34,8 +34,12 @@ def _pair(a):
     return torch.as_tensor(a).cuda(), torch.as_tensor(np.array(a, copy=True))
 
 
-@pytest.mark.parametrize("T,sizes,n_global", [(10, [5, 1, 300, 2], 0), (30, [2] * 7, 3), (300, [3, 600], 1)])
-def test_admm_kernels_match_restatement(T, sizes, n_global):
+@pytest.mark.parametrize("T,sizes,n_global,n_blocks", [(10, [5, 1, 300, 2], 0, 1), (30, [2] * 7, 3, 3),
+                                                        (300, [3, 600], 1, 1), (24, [3, 3, 3, 1, 5, 2], 2, 4)])
+def test_admm_kernels_match_restatement(T, sizes, n_global, n_blocks):
+    """Every ADMM kernel (moments, finalize with per-block totals, per-group penalties and
+    a freeze mask, multiplier/diff updates, shift, row moves) against the numpy
+    restatement of the same interface (tests/cpu_admm_ops.py)."""
     rng = np.random.default_rng(T)
     G = len(sizes)
     gstart = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
@@ -46,20 +50,26 @@ def test_admm_kernels_match_restatement(T, sizes, n_global):
     GM = rng.normal(0.0, 1.0, (G, T))
     EX = (np.arange(G) % 2).astype(np.int32)
     COLS = rng.permutation(T + 5)[:T].astype(np.int32)
+    BLK = (np.arange(G) % n_blocks).astype(np.int32)
+    RHO_G = rng.uniform(0.2, 2.0, G) if n_blocks > 1 else None
+    ACT_G = (np.arange(G) % 3 != 1).astype(np.int32) if n_blocks > 1 else None
     gpu, cpu = NativeADMMOps(), CpuADMMOps({})
     res = []
     for ops, mk in ((gpu, lambda a: _pair(a)[0]), (cpu, lambda a: _pair(a)[1])):
         gs, x, lam, mean, gm, ex = map(mk, (gstart, X, LAM, MEAN, GM, EX))
+        blk = mk(BLK) if n_blocks > 1 else None
+        rho_g = None if RHO_G is None else mk(RHO_G)
+        act_g = None if ACT_G is None else mk(ACT_G)
         dmean = mk(np.zeros((G, T)))
         diff = mk(np.zeros((R, T)))
-        mom = mk(np.zeros(ops.moments_size(G, T)))
-        ops.moments(G, n_global, T, gs, max(sizes), x, lam, mean, mom)
+        mom = mk(np.zeros(ops.moments_size(G, n_blocks, T)))
+        ops.moments(G, n_global, n_blocks, T, gs, max(sizes), x, lam, mean, mom)
         off = n_global * (5 * T + 1)
-        tot = mom[off:off + 8]
-        ops.finalize(n_global, G, n_global, T, mom, ex, gm, 0.7, mean, dmean, tot)
-        ops.finalize(0, n_global, n_global, T, mom, ex, gm, 0.7, mean, dmean, tot)
-        ops.consensus_multipliers(G, T, gs, max(sizes), x, mean, 0.7, lam)
-        ops.exchange_update(G, T, gs, max(sizes), x, mean, diff, gm, 0.7)
+        tot = mom[off:off + 8 * n_blocks]
+        ops.finalize(n_global, G, n_global, n_blocks, T, mom, ex, gm, 0.7, rho_g, act_g, blk, mean, dmean, tot)
+        ops.finalize(0, n_global, n_global, n_blocks, T, mom, ex, gm, 0.7, rho_g, act_g, blk, mean, dmean, tot)
+        ops.consensus_multipliers(G, T, gs, max(sizes), x, mean, 0.7, rho_g, act_g, lam)
+        ops.exchange_update(G, T, gs, max(sizes), x, mean, diff, gm, True, 0.7, rho_g, act_g)
         ops.shift(T, 3, lam)
         cols = mk(COLS)
         dst = mk(np.zeros((R, T + 5)))
@@ -144,7 +154,7 @@ def test_gpu_three_zone_narx_fleet_matches_oracle_fixture():
     rho=1, absolute criterion 0.04/0.04, N=8, 3 iterations, against the oracle's round
     (`tests/golden/c5_admm_N8.json`, `tests/golden/make_c5_admm_golden.py`; both at tol 1e-8)."""
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c5_admm_N8.json")))
-    opts = {"ipopt": {"tol": 1e-8, "max_iter": 500}}
+    opts = {"ipopt": {"tol": 1e-8, "max_iter": 500, "acceptable_iter": 0}}
     fl = ADMMFleet(bm.c5_fleet_classes(n_blocks=1, N=gold["N"], solver_options=opts))
     out = fl.run_coordinated(gold["rho"], admm_iter_max=3, use_relative_tolerances=False, primal_tol=0.04,
                              dual_tol=0.04)
@@ -168,3 +178,124 @@ def test_gpu_fleet_blocks_are_independent():
     for i in range(4):
         al = f"mDot{i + 1}_coupling_b37"
         np.testing.assert_allclose(tb[al], to[al], rtol=1e-9, atol=1e-12)
+
+
+def test_gpu_c2_coordinator_to_stopping_rule_matches_oracle_fixture():
+    """examples/4_Room_ADMM_Coordinator at its coordinator settings (rho 0.4, absolute
+    criterion 0.002 / 0.1, admm_iter_max 40, N=10) run to the stopping rule, against the
+    oracle's round (`tests/golden/c2_admm_N10.json`, `tests/golden/make_admm_goldens.py`):
+    same iteration count, residual and penalty history, final means."""
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c2_admm_N10.json")))
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=gold["N"]))
+    out = fl.run_coordinated(gold["rho"], admm_iter_max=gold["admm_iter_max"], **gold["criterion"])
+    assert out["iterations"] == gold["iterations"] and out["converged"] == gold["converged"]
+    got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["records"]])
+    np.testing.assert_allclose(got, np.array(gold["history"]), rtol=RTOL, atol=1e-10)
+    traj = fl.trajectories()
+    for al, mean in gold["means"].items():
+        np.testing.assert_allclose(traj[al], mean, rtol=RTOL, atol=1e-10)
+
+
+def test_gpu_every_block_stops_like_its_own_coordinator():
+    """A 64-block C2 fleet (one launch per class and iteration): every block keeps its own
+    stopping test and is frozen once converged, so each block ends at the iteration, with
+    the residual history and means, of a single-block run of that block alone (one
+    reference ADMMCoordinator, `admm_coordinator.py:284-309`)."""
+    N, kw = 10, dict(admm_iter_max=40, use_relative_tolerances=False, primal_tol=0.002, dual_tol=0.1)
+    big = ADMMFleet(bm.c2_fleet_classes(n_blocks=64, N=N, seed=5))
+    assert big.n_blocks == 64
+    out = big.run_coordinated(0.4, **kw)
+    its = np.asarray(out["block_iterations"])
+    assert out["converged"] and len(set(its.tolist())) > 1, its   # blocks stop at different iterations
+    tb = big.trajectories()
+    seed_block = {big.block_index(f"mDot1_coupling_b{b}"): b for b in range(64)}
+    assert sorted(seed_block) == list(range(64))
+    for k in sorted({big.block_index("mDot1_coupling_b0"), int(np.argmin(its)), int(np.argmax(its)),
+                     big.block_index("mDot1_coupling_b37")}):
+        b = seed_block[k]
+        one = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N, seed=5, block_offset=b))
+        o1 = one.run_coordinated(0.4, **kw)
+        assert its[k] == o1["iterations"], (b, its[k], o1["iterations"])
+        got = np.array([[r.primal_residual, r.dual_residual] for r in out["block_records"][k]])
+        want = np.array([[r.primal_residual, r.dual_residual] for r in o1["records"]])
+        np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12)
+        to = one.trajectories()
+        for i in range(4):
+            al = f"mDot{i + 1}_coupling_b{b}"
+            np.testing.assert_allclose(tb[al], to[al], rtol=1e-9, atol=1e-12)
+
+
+def test_gpu_admm_golden_through_native_kernels():
+    """The reference's own ConsensusVariable / ExchangeVariable outputs
+    (`tests/golden/admm_golden.json`, produced by executing `admm_datatypes.py` itself,
+    `tests/golden/make_golden.py`) fed straight through the HIP kernels: two mean /
+    multiplier rounds over the active participants, residual norms, diffs, shifts."""
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "admm_golden.json")))
+    ops = NativeADMMOps()
+
+    def dev(a, dt=torch.float64):
+        return torch.as_tensor(np.asarray(a), dtype=dt).cuda().contiguous()
+
+    n_cons = n_exch = 0
+    for case in gold:
+        T, rho = case["T"], case["rho"]
+        if case["type"] == "consensus":
+            srcs = [s_ for s_ in case["sources"] if s_ in set(case["active"])]
+            gs = dev([0, len(srcs)], torch.int32)
+            mean, dmean = dev(np.zeros((1, T))), dev(np.zeros((1, T)))   # mean_trajectory = [0]
+            LAM = dev([case["multipliers0"][k] for k in srcs])
+            for rnd in (1, 2):
+                X = dev([case[f"locals{rnd - 1}"][k] for k in srcs])
+                mom = dev(np.zeros(ops.moments_size(1, 1, T)))
+                ops.moments(1, 0, 1, T, gs, len(srcs), X, LAM, mean, mom)
+                tot = mom[0:8]
+                ops.finalize(0, 1, 0, 1, T, mom, None, None, rho, None, None, None, mean, dmean, tot)
+                ops.consensus_multipliers(1, T, gs, len(srcs), X, mean, rho, None, None, LAM)
+                torch.cuda.synchronize()
+                np.testing.assert_allclose(mean.cpu().numpy()[0], case[f"mean{rnd}"], rtol=1e-13, atol=1e-15)
+                np.testing.assert_allclose(dmean.cpu().numpy()[0], case[f"delta_mean{rnd}"], rtol=1e-12,
+                                           atol=1e-15)
+                np.testing.assert_allclose(np.sqrt(tot[0].item()), np.linalg.norm(case[f"primal{rnd}"]),
+                                           rtol=1e-9, atol=1e-14)
+                np.testing.assert_allclose(np.sqrt(tot[1].item()), np.linalg.norm(case[f"dual{rnd}"]),
+                                           rtol=1e-9, atol=1e-12)
+            lam = LAM.cpu().numpy()
+            for i, k in enumerate(srcs):
+                np.testing.assert_allclose(lam[i], case["multipliers2"][k], rtol=1e-12, atol=1e-12)
+            ops.shift(T, 1, mean)
+            ops.shift(T, 1, LAM)
+            torch.cuda.synchronize()
+            np.testing.assert_allclose(mean.cpu().numpy()[0], case["shifted_mean"], rtol=1e-13, atol=1e-15)
+            lam = LAM.cpu().numpy()
+            for i, k in enumerate(srcs):
+                np.testing.assert_allclose(lam[i], case["shifted_multipliers"][k], rtol=1e-12, atol=1e-12)
+            n_cons += 1
+        else:
+            srcs = case["sources"]
+            gs = dev([0, len(srcs)], torch.int32)
+            X = dev([case["locals0"][k] for k in srcs])
+            mean, dmean = dev(np.zeros((1, T))), dev(np.zeros((1, T)))
+            GM, DIFF, EX = dev([case["multiplier0"]]), dev(np.zeros((len(srcs), T))), dev([1], torch.int32)
+            mom = dev(np.zeros(ops.moments_size(1, 1, T)))
+            ops.moments(1, 0, 1, T, gs, len(srcs), X, None, mean, mom)
+            tot = mom[0:8]
+            ops.finalize(0, 1, 0, 1, T, mom, EX, GM, rho, None, None, None, mean, dmean, tot)
+            ops.exchange_update(1, T, gs, len(srcs), X, mean, DIFF, GM, True, rho, None, None)
+            torch.cuda.synchronize()
+            np.testing.assert_allclose(mean.cpu().numpy()[0], case["mean1"], rtol=1e-13, atol=1e-15)
+            np.testing.assert_allclose(dmean.cpu().numpy()[0], case["delta_mean1"], rtol=1e-12, atol=1e-15)
+            np.testing.assert_allclose(GM.cpu().numpy()[0], case["multiplier1"], rtol=1e-13, atol=1e-12)
+            diff = DIFF.cpu().numpy()
+            for i, k in enumerate(srcs):
+                np.testing.assert_allclose(diff[i], case["diffs1"][k], rtol=1e-12, atol=1e-15)
+            np.testing.assert_allclose(np.sqrt(tot[0].item()), np.linalg.norm(case["primal1"]), rtol=1e-12)
+            np.testing.assert_allclose(np.sqrt(tot[1].item()), np.linalg.norm(case["dual1"]), rtol=1e-9)
+            ops.shift(T, 1, GM)
+            ops.shift(T, 1, DIFF)
+            torch.cuda.synchronize()
+            np.testing.assert_allclose(GM.cpu().numpy()[0], case["shifted_multiplier"], rtol=1e-13, atol=1e-12)
+            diff = DIFF.cpu().numpy()
+            for i, k in enumerate(srcs):
+                np.testing.assert_allclose(diff[i], case["shifted_diffs"][k], rtol=1e-12, atol=1e-15)
+            n_exch += 1
+    assert n_cons > 0 and n_exch > 0

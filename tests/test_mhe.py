@@ -73,7 +73,7 @@ def test_oracle_mhe_recovers_true_parameter():
     case = configs.mhe_room()
     p, lbw, ubw, w0 = case.oracle_inputs
     fn = case.oracle.functions(p)
-    res = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), ipm.IPMOptions(tol=1e-10))
+    res = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), ipm.IPMOptions(tol=1e-10, acceptable_iter=0))
     assert res.success, res.status
     assert abs(res.x[2] - 5.5) < 1e-3
     assert abs(res.x[1] - 27.0) < 0.05 and abs(res.x[0] - 25.0) < 0.05

@@ -28,12 +28,12 @@ def test_library_builds_loads_and_exports_all_symbols():
     lib = ctypes.CDLL(str(path))
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.mpcx_version() == 4
+    assert lib.mpcx_version() == 5
 
 
 def test_struct_sizes_match_header():
-    # mpcx_options: 36 doubles + 4 int32; mpcx_stats: 6 doubles + 8 int32
-    assert ctypes.sizeof(native.Options) == 36 * 8 + 4 * 4
+    # mpcx_options: 40 doubles + 4 int32; mpcx_stats: 6 doubles + 8 int32
+    assert ctypes.sizeof(native.Options) == 40 * 8 + 4 * 4
     assert ctypes.sizeof(native.Stats) == 6 * 8 + 8 * 4
     assert ctypes.sizeof(native.ProblemDesc) == 8 * 4
 
@@ -42,6 +42,10 @@ def test_default_options_are_ipopt_defaults():
     o = native.default_options()
     assert o.mu_init == 0.1 and o.kappa_mu == 0.2 and o.theta_mu == 1.5
     assert o.bound_push == 1e-2 and o.kappa_sigma == 1e10 and o.tau_min == 0.99
+    # IPOPT's acceptable-level defaults (the backend applies the reference's overrides)
+    assert o.acceptable_tol == 1e-6 and o.acceptable_iter == 15 and o.acceptable_dual_inf_tol == 1e10
+    assert o.acceptable_constr_viol_tol == 1e-2 and o.acceptable_compl_inf_tol == 1e-2
+    assert o.acceptable_obj_change_tol == 1e20
 
 
 def test_generated_kernel_compiles(tmp_path, monkeypatch):

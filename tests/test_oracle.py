@@ -30,7 +30,7 @@ def _scipy_trust_constr(prob, p, lbw, ubw, w0):
 def test_oracle_ipm_vs_scipy_trust_constr():
     prob = nlps.one_room(N=6)
     p, lbw, ubw, w0 = nlps.one_room_inputs(prob, N=6)
-    res = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p), ipm.IPMOptions(tol=1e-10))
+    res = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p), ipm.IPMOptions(tol=1e-10, acceptable_iter=0))
     assert res.success
     sc = _scipy_trust_constr(prob, p, lbw, ubw, w0)
     # trust-constr's own barrier stops at ~1e-6 relative accuracy: the IPM must be at
@@ -44,7 +44,7 @@ def test_oracle_kkt_residuals_small():
     case = configs.exchange_supply(diff=-0.01, lam=20.0)
     p, lbw, ubw, w0 = case.oracle_inputs
     fn = case.oracle.functions(p)
-    res = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), ipm.IPMOptions(tol=1e-10))
+    res = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), ipm.IPMOptions(tol=1e-10, acceptable_iter=0))
     assert res.success
     # stationarity of the Lagrangian with the returned multipliers
     r = fn.grad_f(res.x) + fn.jac_g(res.x).T @ res.lam_g + res.lam_x
@@ -62,10 +62,64 @@ def test_c_oracle_matches_numpy_oracle():
         p, lbw, ubw, w0 = nlps.one_room_inputs(prob, **kw)
         P.append(p); LB.append(lbw); UB.append(ubw); W0.append(w0)
         refs.append(ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p),
-                              ipm.IPMOptions(tol=1e-10)))
+                              ipm.IPMOptions(tol=1e-10, acceptable_iter=0)))
     cbuild.build()
-    w, st, ok = cbuild.solve_room_fleet(np.array(P), np.array(LB), np.array(UB), np.array(W0), tol=1e-10)
+    w, st, ok = cbuild.solve_room_fleet(np.array(P), np.array(LB), np.array(UB), np.array(W0), tol=1e-10,
+                                        acceptable_iter=0)
     assert ok == 3
     for i, r in enumerate(refs):
         np.testing.assert_allclose(w[i], r.x, rtol=1e-9, atol=1e-9)
         assert st[i]["iter"] == r.iterations
+
+
+REFERENCE_OPTS = dict(tol=1e-4, max_iter=100, acceptable_tol=0.1, acceptable_iter=5,
+                      acceptable_constr_viol_tol=1.0, acceptable_compl_inf_tol=1.0)
+
+
+def test_c_oracle_matches_numpy_oracle_at_reference_defaults():
+    """IPOPT's termination rule at the reference's settings (`casadi_utils.py:197-206`):
+    both restatements stop at the same iteration with the same status."""
+    prob = nlps.one_room()
+    rng = np.random.default_rng(5)
+    P, LB, UB, W0, refs = [], [], [], [], []
+    for i in range(4):
+        kw = dict(T0=float(rng.uniform(291, 301)), load=float(rng.uniform(50, 250)),
+                  T_upper=float(rng.uniform(294.15, 296.15)), u_prev=float(rng.uniform(0, 0.05)))
+        p, lbw, ubw, w0 = nlps.one_room_inputs(prob, **kw)
+        P.append(p); LB.append(lbw); UB.append(ubw); W0.append(w0)
+        refs.append(ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p),
+                              ipm.IPMOptions(**REFERENCE_OPTS)))
+    cbuild.build()
+    opts = dict(REFERENCE_OPTS)
+    w, st, ok = cbuild.solve_room_fleet(np.array(P), np.array(LB), np.array(UB), np.array(W0),
+                                        tol=opts.pop("tol"), max_iter=opts.pop("max_iter"), **opts)
+    assert ok == 4
+    names = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level"}
+    for i, r in enumerate(refs):
+        assert names[st[i]["status"]] == r.status
+        assert st[i]["iter"] == r.iterations
+        np.testing.assert_allclose(w[i], r.x, rtol=1e-9, atol=1e-9)
+
+
+def test_acceptable_level_termination_semantics():
+    """The acceptable counter (IPOPT OptimalityErrorConvergenceCheck): with the reference's
+    loose acceptable tolerances the exchange room stops early at the acceptable level; with
+    acceptable_iter = 0 the same NLP runs on to the strict tolerance."""
+    case = configs.exchange_room()
+    p, lbw, ubw, w0 = case.oracle_inputs
+    fn = case.oracle.functions(p)
+    acc = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), ipm.IPMOptions(**REFERENCE_OPTS))
+    strict = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p),
+                       ipm.IPMOptions(**{**REFERENCE_OPTS, "acceptable_iter": 0}))
+    tight = ipm.solve(fn, w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p),
+                      ipm.IPMOptions(tol=1e-10, acceptable_iter=0))
+    assert acc.status == "Solved_To_Acceptable_Level" and acc.success
+    # without the counter the iteration goes on: the unscaled complementarity test
+    # (compl_inf_tol 1e-4 on products / obj_scale, mu floored at 1e-4/11) is never met, and
+    # the run ends when the line search fails at an acceptable point (IPOPT's "restoration
+    # phase called at acceptable point")
+    assert strict.iterations > acc.iterations
+    # an acceptable stop needs acceptable_iter consecutive acceptable iterates, and the
+    # objective-change test cannot pass at the first check (IPOPT starts from -1e50)
+    assert acc.iterations >= REFERENCE_OPTS["acceptable_iter"]
+    np.testing.assert_allclose(acc.f, tight.f, rtol=1e-4)

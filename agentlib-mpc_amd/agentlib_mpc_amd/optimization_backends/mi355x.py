@@ -185,22 +185,35 @@ class MI355XBackend(OptimizationBackend):
             results.append(res)
         return results
 
-    # -- results file (`core/casadi_backend.py:263-307`) ---------------------------
+    # -- results file (`core/casadi_backend.py:263-323`) ---------------------------
     def save_result_df(self, results: Results, now: float = 0):
+        """Results rows plus the combined stats line (``obj_<term>`` values of the
+        objective on the multiple-shooting grid, then ``stats_<key>`` solver stats), as
+        ``CasADiBackend.save_result_df`` writes them."""
         if not self.config.save_results:
             return
         res_file = self.config.results_file
+        df = results.df
+        objective_names, objective_values = self.approximate_objective(df)
         if not self.results_folder_exists():
             if not self.config.save_only_stats:
                 results.write_columns(res_file)
-            results.write_stats_columns(stats_path(res_file))
+            results.write_combined_stats_columns(stats_path(res_file), objective_names)
         with open(stats_path(res_file), "a") as f:
-            f.write(results.stats_line(str(now)))
+            f.write(results.combined_stats_line(str(now), objective_values, objective_names))
         if self.config.save_only_stats:
             return
-        df = results.df
         df.index = [str((now, x)) for x in df.index]
         df.to_csv(res_file, mode="a", header=False)
+
+    def approximate_objective(self, results_df):
+        """`core/casadi_backend.py:309-323`: objective terms on the multiple-shooting grid."""
+        opts = self.config.discretization_options
+        grid = np.arange(0, opts.prediction_horizon * (opts.time_step + 1), opts.time_step)
+        objective = self.system.objective
+        values = objective.calculate_values(results_df, grid)
+        names = [o.name for o in objective.objectives] + ["total"]
+        return names, values
 
 
 class MI355XBaseBackend(MI355XBackend):

@@ -1,5 +1,7 @@
-"""Host-side utilities: time units (`agentlib_mpc/utils/__init__.py:7-27`),
-trajectory sampling (`sampling.py`) and result-file readers (`analysis.py`)."""
+"""Host-side utilities: time units (`agentlib_mpc/utils/__init__.py:7-27`) and
+trajectory sampling (`sampling.py`).  Result files are read with the reference's own
+readers (`agentlib_mpc/utils/analysis.py`); `tests/golden/make_reader_goldens.py` pins
+that they parse this package's files."""
 
 from typing import Dict, List, Literal, Tuple
 

@@ -1,112 +1,98 @@
-"""On-disk result formats (CPU): the backend results file + stats file
-(`core/casadi_backend.py:263-307`), the ADMM backend's per-iteration results
+"""On-disk result formats (CPU): the backend results + combined stats files
+(`core/casadi_backend.py:263-323`), the ADMM backend's per-iteration results
 (`casadi_/admm.py:364-424`) and the coordinator's residual file
-(`admm_coordinator.py:437-465`), read back as `utils/analysis.py:21-38` does."""
+(`admm_coordinator.py:437-465`).
+
+Pinned against the REFERENCE's own readers: `tests/golden/make_reader_goldens.py` ran
+`agentlib_mpc/utils/analysis.py` and `utils/plotting/admm_residuals.py` on files these
+writers produced (copies in `tests/golden/result_files/`, reader outputs in
+`tests/golden/reader_golden.json`).  Here the writers must reproduce those files byte for
+byte, so the recorded reader outputs hold for what they write now."""
 
 import ast
+import json
+import pathlib
 
 import numpy as np
 import pandas as pd
+import pytest
 
-from agentlib_mpc_amd import benchmarks as bm
-from agentlib_mpc_amd.admm.fleet import ADMMFleet, IterationRecord
+from tests import result_file_cases as rfc
 
-
-def _results(be, cv, now=0.0):
-    prob = be.problem
-    mi = prob.mpc_inputs(cv, now)
-    mi.update(prob.initial_guess(mi))
-    p, lbw, ubw, w0 = prob.nlp_inputs(mi)
-    stats = {"success": True, "return_status": "Solve_Succeeded", "iter_count": 7, "obj": 1.5}
-    return prob.make_results(mi, w0, stats)
+GOLD = pathlib.Path(__file__).resolve().parent / "golden"
 
 
-def _load_mpc(path):
-    df = pd.read_csv(path, header=[0, 1], index_col=0)
-    df.index = [ast.literal_eval(i) for i in df.index]
-    return df
+@pytest.fixture(scope="module")
+def written(tmp_path_factory):
+    return rfc.write_all(tmp_path_factory.mktemp("results"))
 
 
-def test_backend_results_file(tmp_path):
+@pytest.fixture(scope="module")
+def reader():
+    return json.loads((GOLD / "reader_golden.json").read_text())
+
+
+@pytest.mark.parametrize("rel", rfc.FILES)
+def test_writers_reproduce_the_files_the_reference_readers_parsed(written, rel):
+    assert (written / rel).read_text() == (GOLD / "result_files" / rel).read_text()
+
+
+def test_reference_load_mpc_reads_the_backend_results(reader):
+    mpc = reader["load_mpc"]
+    assert sorted({tuple(i)[0] for i in mpc["index"]}) == list(rfc.MPC_STEPS)
+    assert ["variable", "T"] in mpc["columns"] and ["parameter", "load"] in mpc["columns"]
+    assert reader["get_time_steps_mpc"] == list(rfc.MPC_STEPS)
+
+
+def test_reference_stats_reader_finds_objective_and_solver_columns(reader):
+    """Combined stats (obj_<term>, then stats_<key>): the dashboard keys on ``stats_obj``
+    (`utils/plotting/interactive.py:486-488`)."""
+    st = reader["load_mpc_stats"]
+    assert st["index"] == list(rfc.MPC_STEPS)
+    assert "stats_obj" in st["columns"] and "stats_iter_count" in st["columns"]
+    assert [c for c in st["columns"] if c.startswith("obj_")][-1] == "obj_total"
+    col = st["columns"].index("stats_iter_count")
+    assert [row[col] for row in st["values"]] == [7, 7]
+
+
+def test_reference_admm_readers(reader):
+    assert reader["get_number_of_iterations"] == {str(t): n for t, n in rfc.ADMM_STEPS}
+    idx = [tuple(i[:2]) for i in reader["load_admm_index"]]
+    assert sorted(set(idx)) == [(t, i) for t, n in rfc.ADMM_STEPS for i in range(n)]
+    # the ADMM backend keeps the plain stats layout (`casadi_/admm.py:364-424`)
+    st = reader["load_admm_stats"]
+    assert st["columns"] == ["success", "return_status", "iter_count", "obj"]
+    assert [tuple(i) for i in st["index"]] == [(t, i) for t, n in rfc.ADMM_STEPS for i in range(n)]
+
+
+def test_reference_residual_reader(reader):
+    res = reader["load_residuals"]
+    assert res["columns"] == ["primal_residual", "dual_residual", "penalty_parameter", "wall_time"]
+    assert [tuple(i) for i in res["index"]] == [(0.0, 0), (0.0, 1), (60.0, 0)]
+    np.testing.assert_allclose([r[2] for r in res["values"]], [0.4, 0.8, 0.4])
+
+
+def test_objective_terms_match_a_direct_evaluation(written):
+    """obj_<term> columns: the reference's rectangle rule on the multiple-shooting grid
+    (`objective.py:135-139`, `casadi_backend.py:309-323`) computed independently here."""
+    from agentlib_mpc_amd import benchmarks as bm
+
     be, cv = bm.one_room(N=4)
-    f = tmp_path / "room.csv"
-    be.config.results_file = f
-    be.config.save_results = True
-    for now in (0.0, 300.0):
-        be.save_result_df(_results(be, cv, now), now)
-    df = _load_mpc(f)
-    assert {i[0] for i in df.index} == {0.0, 300.0}
-    assert ("variable", "T") in df.columns and ("parameter", "load") in df.columns
-    stats = pd.read_csv(tmp_path / "stats_room.csv", index_col=0)
-    assert len(stats) == 2 and stats["iter_count"].tolist() == [7, 7]
+    r = rfc._results(be, cv, 100.0)
+    df = r.df
+    grid = np.arange(0, 4 * 301, 300)
+    u = df.loc[grid, ("variable", "mDot")].to_numpy()
+    w = df[("parameter", "r_mDot")].ffill().loc[grid].to_numpy()
+    want = float(np.sum(w[:-1] * u[:-1] * np.diff(grid)))
+    stats = pd.read_csv(written / "mpc" / "stats_room.csv", index_col=0)
+    np.testing.assert_allclose(stats["obj_control_costs"].iloc[0], want, rtol=1e-12)
 
 
-def test_admm_backend_iteration_results(tmp_path):
-    be, cv = bm.exchange_room(N=4)
-    f = tmp_path / "admm.csv"
-    be.config.results_file = f
-    be.config.save_results = True
-    r = _results(be, cv)
-    for now, n_it in ((0.0, 3), (120.0, 2)):
-        for _ in range(n_it):
-            be.save_result_df(r, now)
-    # iterations of a step are flushed when the next step starts (`admm.py:405-424`)
-    df = _load_mpc(f)
-    keys = sorted({i[:2] for i in df.index})
-    assert keys == [(0.0, 0), (0.0, 1), (0.0, 2), (120.0, 0)]
+def test_coordinator_residual_file_roundtrip(tmp_path):
+    from agentlib_mpc_amd.admm.fleet import ADMMFleet, IterationRecord
 
-
-def test_coordinator_residual_file(tmp_path):
-    recs = [IterationRecord(1.0, 2.0, 0.4, wall_time=0.01), IterationRecord(0.5, 0.25, 0.4, wall_time=0.02)]
-    f = tmp_path / "residuals.csv"
+    recs = [IterationRecord(1.0, 2.0, 0.4, wall_time=0.01)]
+    f = tmp_path / "r.csv"
     ADMMFleet.save_stats(None, f, 0.0, recs)
-    ADMMFleet.save_stats(None, f, 60.0, recs[:1])
     df = pd.read_csv(f, index_col=0)
-    assert list(df.columns) == ["primal_residual", "dual_residual", "penalty_parameter", "wall_time"]
-    assert [ast.literal_eval(i) for i in df.index] == [(0.0, 0), (0.0, 1), (60.0, 0)]
-    np.testing.assert_allclose(df["dual_residual"], [2.0, 0.25, 2.0])
-
-
-def test_analysis_readers_on_backend_files(tmp_path):
-    """`utils/analysis.py` readers on the files the backends write (`analysis.py:17-290`)."""
-    from agentlib_mpc_amd.utils import analysis
-
-    be, cv = bm.one_room(N=4)
-    f = tmp_path / "room.csv"
-    be.config.results_file, be.config.save_results = f, True
-    for now in (100.0, 400.0):
-        be.save_result_df(_results(be, cv, now), now)
-    df = analysis.load_mpc(f)
-    assert isinstance(df.index, pd.MultiIndex) and analysis.get_time_steps(df) == [100.0, 400.0]
-    st = analysis.load_mpc_stats(f)
-    assert st is not None and st["iter_count"].tolist() == [7, 7]
-    assert analysis.load_mpc_stats(tmp_path / "missing.csv") is None
-    # prediction made at the step closest to t=290 (offset "auto": steps at 0 and 300)
-    T = analysis.mpc_at_time_step(df, 290.0, variable="T")
-    grid = df["variable"]["T"].loc[400.0]
-    np.testing.assert_allclose(T.values, grid.values)
-    np.testing.assert_allclose(T.index.values, grid.index.values + 300.0)
-    first = analysis.first_vals_at_trajectory_index(df["variable"]["T"])
-    np.testing.assert_allclose(first.values, [grid.iloc[0]] * 2)
-    last = analysis.last_vals_at_trajectory_index(df["variable"]["T"].dropna())
-    assert list(last.index) == [100.0, 400.0]
-    hrs = analysis.convert_multi_index(df, "hours")
-    np.testing.assert_allclose(sorted(set(hrs.index.get_level_values(0))), [100 / 3600, 400 / 3600])
-
-
-def test_analysis_readers_on_admm_files(tmp_path):
-    from agentlib_mpc_amd.utils import analysis
-
-    be, cv = bm.exchange_room(N=4)
-    f = tmp_path / "admm.csv"
-    be.config.results_file, be.config.save_results = f, True
-    r = _results(be, cv)
-    for now, n_it in ((0.0, 3), (120.0, 2), (240.0, 1)):
-        for _ in range(n_it):
-            be.save_result_df(r, now)
-    df = analysis.load_admm(f)
-    assert analysis.get_number_of_iterations(df) == {0.0: 3, 120.0: 2, 240.0: 1}
-    last_it = analysis.admm_at_time_step(df, time_step=0.0, iteration=-1)
-    first_it = analysis.admm_at_time_step(df, time_step=0.0, iteration=0)
-    pd.testing.assert_frame_equal(last_it, first_it)
-    assert last_it.index[0] == df.loc[(0.0, 2)].index[0]
+    assert [ast.literal_eval(i) for i in df.index] == [(0.0, 0)]

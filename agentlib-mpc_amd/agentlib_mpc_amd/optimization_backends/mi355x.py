@@ -110,7 +110,7 @@ class MI355XBackend(OptimizationBackend):
         super().__init__(config)
         self.problem: Optional[CompiledProblem] = None
         self.system = None
-        self._remembered: Optional[Dict[str, np.ndarray]] = None
+        self._remembered: Optional[np.ndarray] = None  # [n, nw] last optimum per batch slot
         name = getattr(self.config.solver.name, "value", self.config.solver.name)
         if name not in KERNEL_SOLVERS:
             raise ValueError(f"solver {name!r} is not available on the MI355X backend "
@@ -138,52 +138,58 @@ class MI355XBackend(OptimizationBackend):
     def solve(self, now: float, current_vars: dict) -> Results:
         return self.solve_batch(now, [current_vars])[0]
 
-    def solve_batch(self, now, batch_vars: Sequence[dict], remembered: Optional[list] = None) -> List[Results]:
-        """Solve one NLP per entry of ``batch_vars`` (same structure) in one launch."""
-        import torch
+    def solve_batch(self, now, batch_vars: Sequence[dict]):
+        """Solve one NLP per entry of ``batch_vars`` (same structure) in one launch.
 
+        Entry ``i`` is one agent: its warm start is ITS previous optimum (the reference
+        keeps one remembered solution per backend instance, `core/discretization.py:
+        221-223`, `247-251`), kept here per batch slot while the batch size is unchanged.
+        Marshalling is vectorised over the agents (:class:`BatchMarshal`); the returned
+        :class:`FleetResults` builds each agent's ``Results`` on access."""
         if self.problem is None:
             raise RuntimeError("setup_optimization() must be called before solve()")
         prob = self.problem
-        inputs, P, LB, UB, W = [], [], [], [], []
-        for i, cv in enumerate(batch_vars):
-            mi = prob.mpc_inputs(cv, now)
-            rem = self._remembered if remembered is None else remembered[i]
-            mi.update(prob.initial_guess(mi, rem))
-            p, lbw, ubw, w0 = prob.nlp_inputs(mi)
-            inputs.append(mi)
-            P.append(p); LB.append(lbw); UB.append(ubw); W.append(w0)
+        n = len(batch_vars)
+        w_prev = self._remembered if self._remembered is not None and self._remembered.shape[0] == n else None
+        p, lbw, ubw, w0, sampled = prob.marshal.inputs(batch_vars, now, w_prev, return_sampled_bounds=True)
+        res = self.solve_arrays(p, lbw, ubw, w0, result_bounds=sampled)
+        self._remembered = res.w.copy()
+        if self.config.save_results:
+            for i in range(n):
+                self.save_result_df(res[i], now)
+        return res
+
+    def solve_arrays(self, p, lbw, ubw, w0, lbg=None, ubg=None, result_bounds=None):
+        """Batched solve of reference-layout NLP inputs [n, .] (host arrays): device
+        copies, one kernel launch, solutions and stats back.  Returns :class:`FleetResults`
+        (``result_bounds``: the bounds its lower/upper columns show, default lbw/ubw)."""
+        import torch
+
+        from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+
+        prob = self.problem
         native = self._native()
         dev = torch.device("cuda")
         t0 = time.perf_counter()
-        LB = np.stack(LB)
-        kp, kl, ku, kw = prob.to_kernel(np.stack(P), LB, np.stack(UB), np.stack(W))
-        tp = torch.as_tensor(kp, dtype=torch.float64, device=dev)
-        tl = torch.as_tensor(kl, dtype=torch.float64, device=dev)
-        tu = torch.as_tensor(ku, dtype=torch.float64, device=dev)
-        tw = torch.as_tensor(kw, dtype=torch.float64, device=dev)
-        n = len(batch_vars)
-        from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
-
+        n = p.shape[0]
+        kp, kl, ku, kw = prob.to_kernel(p, lbw, ubw, w0)
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev, non_blocking=True)  # noqa
+        tp, tl, tu, tw = T(kp), T(kl), T(ku), T(kw)
+        tg = tug = None
+        if lbg is not None:
+            tg, tug = T(lbg), T(ubg)
         lam_g = torch.empty((n, prob.nlp.kernel_ng), dtype=torch.float64, device=dev)
         st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=dev)
-        native.solve(tp, tl, tu, tw, lam_g=lam_g, stats=st)
-        w = prob.from_kernel(tw.cpu().numpy(), LB)
+        native.solve(tp, tl, tu, tw, lbg=tg, ubg=tug, lam_g=lam_g, stats=st)
+        w = prob.from_kernel(tw.cpu().numpy(), lbw)
         stats = stats_to_dicts(st.cpu().numpy().tobytes())
         wall = time.perf_counter() - t0
-        results = []
-        for i in range(n):
-            s = stats[i]
-            s["t_wall_total"] = wall
-            outs = prob.outputs(w[i])
-            if remembered is None and i == n - 1:
-                self._remembered = outs
-            elif remembered is not None:
-                remembered[i] = outs
-            res = prob.make_results(inputs[i], w[i], s)
-            self.save_result_df(res, now)
-            results.append(res)
-        return results
+        for s_ in stats:
+            s_["t_wall_total"] = wall
+        from agentlib_mpc_amd.optimization_backends.problem import FleetResults
+
+        rlb, rub = result_bounds if result_bounds is not None else (lbw, ubw)
+        return FleetResults(prob, prob.marshal, p, rlb, rub, w, stats)
 
     # -- results file (`core/casadi_backend.py:263-323`) ---------------------------
     def save_result_df(self, results: Results, now: float = 0):

@@ -14,7 +14,8 @@ is the native batched kernel (:class:`agentlib_mpc_amd.runtime.native.NativeProb
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Optional, Sequence, Tuple
+from collections.abc import Sequence
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import pandas as pd
@@ -38,6 +39,14 @@ class CompiledProblem:
         self.gen = codegen.generate(nlp)
         self._native = None
         self.layout = self._result_layout()
+        self._marshal = None
+        self.system_group_names = {v.name: list(v.full_names) for v in system.variables}
+
+    @property
+    def marshal(self) -> "BatchMarshal":
+        if self._marshal is None:
+            self._marshal = BatchMarshal(self)
+        return self._marshal
 
     # -- native ------------------------------------------------------------------
     @property
@@ -296,3 +305,189 @@ def fleet_nlp_inputs(prob: CompiledProblem, template_vars: dict, overrides: Dict
                 if lay.guess_par[t][i] >= 0:
                     w0[:, c] = p[:, lay.guess_par[t][i]]
     return p, lbw, ubw, w0
+
+
+# ---------------------------------------------------------------------------
+# batched marshalling (structure of arrays over the agents of one structure)
+# ---------------------------------------------------------------------------
+class BatchMarshal:
+    """Array maps of one problem structure, built once: ``mpc_inputs`` +
+    ``initial_guess`` + ``nlp_inputs`` for many agents at once (reference semantics,
+    `core/casadi_backend.py:141-253`, `core/discretization.py:212-348`), and the result
+    matrices (`core/discretization.py:360-484`) straight from the NLP vectors.
+
+    Values are gathered per variable across the agents; scalar values and grid-length
+    lists (the common case) are written as whole columns, anything else (series, dicts,
+    JSON strings) is sampled per agent exactly as :meth:`CompiledProblem.mpc_inputs`
+    does."""
+
+    def __init__(self, prob: "CompiledProblem"):
+        self.prob = prob
+        nlp = prob.nlp
+        self.pars = []   # (group name, grid length, [(row, name | None, default)], p index [dim, G])
+        for par in prob.system.parameters:
+            lay = nlp.par_groups.get(par.name)
+            grid = lay.grid if lay is not None else []
+            rows = [(i, n if n in par.ref_names else None, par.defaults[i]) for i, n in enumerate(par.full_names)]
+            self.pars.append((par.name, list(grid), rows, None if lay is None or not lay.dim else lay.index))
+        self.vars = []   # (group name, grid, [(row, name | None, default lb, default ub)], w index)
+        for var in prob.system.variables:
+            lay = nlp.var_groups.get(var.name)
+            grid = lay.grid if lay is not None else []
+            rows = [(i, n if n in var.ref_names else None, var.default_lb[i], var.default_ub[i])
+                    for i, n in enumerate(var.full_names)]
+            self.vars.append((var.name, list(grid), rows, None if lay is None or not lay.dim else lay.index))
+        # bound / guess entries taken from parameters (`lb_par`, `ub_par`, `guess_par`)
+        over = {"lb": ([], []), "ub": ([], []), "guess": ([], [])}
+        for lay in nlp.var_groups.values():
+            for t, cols in enumerate(lay.columns):
+                for i, c in enumerate(cols):
+                    for key, src in (("lb", lay.lb_par), ("ub", lay.ub_par), ("guess", lay.guess_par)):
+                        if src[t][i] >= 0:
+                            over[key][0].append(c)
+                            over[key][1].append(src[t][i])
+        self.over = {k: (np.asarray(c, np.int64), np.asarray(p, np.int64)) for k, (c, p) in over.items()}
+        self.initial = {}
+        for name, lay in nlp.var_groups.items():
+            key = f"initial_{name}"
+            if lay.dim and key in nlp.par_groups and nlp.par_groups[key].dim:
+                self.initial[name] = nlp.par_groups[key].index
+        # result matrix scatter plan
+        lay = prob.layout
+        self.n_rows, self.n_cols = len(lay.full_grid), len(lay.columns)
+        self.blocks = []
+        col = 0
+        for kind, name, dim, rc in lay.blocks:
+            rows = np.array([r for r, _ in rc], np.int64)
+            cols = np.array([j for _, j in rc], np.int64)
+            if kind == "parameter":
+                src = ("p", nlp.par_groups[name].index)
+            else:
+                src = ({"var": "w", "lb": "lbw", "ub": "ubw"}[kind], nlp.var_groups[name].index)
+            self.blocks.append((col, dim, rows, cols) + src)
+            col += dim
+
+    @staticmethod
+    def _column(values, n_grid, now, method_of, what):
+        """[n, G] samples of one variable for every agent (``sampling.sample`` semantics)."""
+        n = len(values)
+        out = np.empty((n, n_grid))
+        fast = [isinstance(v, (float, int)) for v in values]
+        if all(fast):
+            out[:] = np.asarray(values, float)[:, None]
+            return out
+        for a, v in enumerate(values):
+            out[a] = sampling.sample(trajectory=v, grid=what, current=now, method=method_of(a))
+        return out
+
+    def inputs(self, batch_vars: Sequence[dict], now: float, w_prev: Optional[np.ndarray] = None,
+               return_sampled_bounds: bool = False):
+        """(p, lbw, ubw, w0) [n, .] in the reference layout; ``w_prev`` [n, nw] (rows of
+        NaN = no previous optimum) is the warm start (`core/discretization.py:212-251`).
+        ``return_sampled_bounds``: also the sampled bounds before the parameter overrides
+        (what the result matrix's lower/upper columns show)."""
+        nlp = self.prob.nlp
+        n = len(batch_vars)
+        p = np.full((n, nlp.npar), np.nan)
+        groups = {}
+        for name, grid, rows, index in self.pars:
+            mat = np.empty((n, len(rows), len(grid)))
+            for i, ref, default in rows:
+                if ref is None:
+                    mat[:, i, :] = default
+                    continue
+                vs = [cv[ref] for cv in batch_vars]
+                vals = [v.value for v in vs]
+                if any(v is None for v in vals):
+                    raise ValueError(f"Input for variable {ref} is empty. Cannot solve optimization problem.")
+                for v in vs:
+                    if not hasattr(v, "interpolation_method"):
+                        raise TypeError(
+                            f"The variable {ref} does not have an interpolationmethod. All Variables "
+                            "used in MPC need to be of type MPCVariable (subclass of AgentVariable).")
+                mat[:, i, :] = self._column(vals, len(grid), now, lambda a: vs[a].interpolation_method, grid)
+            groups[name] = mat
+            if index is not None:
+                p[:, index] = mat
+        lbw = np.full((n, nlp.nw), np.nan)
+        ubw = np.full((n, nlp.nw), np.nan)
+        w0 = np.zeros((n, nlp.nw))
+        for name, grid, rows, index in self.vars:
+            lb = np.empty((n, len(rows), len(grid)))
+            ub = np.empty((n, len(rows), len(grid)))
+            for i, ref, dlb, dub in rows:
+                if ref is None:
+                    lb[:, i, :], ub[:, i, :] = dlb, dub
+                    continue
+                vs = [cv[ref] for cv in batch_vars]
+                meth = lambda a: getattr(vs[a], "interpolation_method", "linear")  # noqa: E731
+                ub[:, i, :] = self._column([v.ub for v in vs], len(grid), now, meth, grid)
+                lb[:, i, :] = self._column([v.lb for v in vs], len(grid), now, meth, grid)
+            if index is None:
+                continue
+            lbw[:, index] = lb
+            ubw[:, index] = ub
+            if name in self.initial:
+                meas = p[:, self.initial[name]][:, :, -1:]
+                guess = np.repeat(meas, len(grid), axis=2)
+            else:
+                with np.errstate(invalid="ignore"):
+                    guess = np.nan_to_num(0.5 * (lb + ub), posinf=0, neginf=-0)
+            w0[:, index] = guess
+        if w_prev is not None:
+            have = ~np.isnan(w_prev).any(axis=1)
+            w0[have] = w_prev[have]
+        sampled = (lbw.copy(), ubw.copy()) if return_sampled_bounds else None
+        for key, arr in (("lb", lbw), ("ub", ubw), ("guess", w0)):
+            cols, pars = self.over[key]
+            if cols.size:
+                arr[:, cols] = p[:, pars]
+        if np.isnan(p).any() or np.isnan(lbw).any() or np.isnan(ubw).any():
+            raise ValueError("incomplete NLP inputs (NaN in parameters or bounds)")
+        if return_sampled_bounds:
+            return p, lbw, ubw, np.nan_to_num(w0), sampled
+        return p, lbw, ubw, np.nan_to_num(w0)
+
+    def result_matrices(self, p, lbw, ubw, w) -> np.ndarray:
+        """[n, len(full grid), n_columns] result matrices from the NLP vectors (``lbw`` /
+        ``ubw``: the sampled bounds, see :meth:`inputs`)."""
+        n = p.shape[0]
+        src = {"p": p, "w": w, "lbw": lbw, "ubw": ubw}
+        mat = np.full((n, self.n_rows, self.n_cols), np.nan)
+        for col, dim, rows, cols, key, index in self.blocks:
+            vals = src[key][:, index]                      # [n, dim, G]
+            mat[:, rows, col:col + dim] = np.transpose(vals[:, :, cols], (0, 2, 1))
+        return mat
+
+
+class FleetResults(Sequence):
+    """Results of one batched solve: per-agent :class:`Results` built on access; whole-fleet
+    arrays (solutions, stats) without per-agent objects."""
+
+    def __init__(self, prob: "CompiledProblem", marshal: BatchMarshal, p, lbw, ubw, w, stats: list):
+        self.prob, self.marshal = prob, marshal
+        self.p, self.lbw, self.ubw, self.w, self.stats = p, lbw, ubw, w, stats
+
+    def __len__(self):
+        return self.w.shape[0]
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        m = self.marshal.result_matrices(self.p[i:i + 1], self.lbw[i:i + 1], self.ubw[i:i + 1], self.w[i:i + 1])[0]
+        lay = self.prob.layout
+        return Results(matrix=m, grid=list(lay.full_grid), columns=lay.columns, stats=self.stats[i],
+                       variable_grid_indices=lay.variable_grid_indices)
+
+    def first_values(self, name: str) -> np.ndarray:
+        """Value of variable ``name`` at the first grid time >= 0, every agent (the
+        actuation `modules/mpc/mpc.py:342-357` reads)."""
+        for gname, lay in self.prob.nlp.var_groups.items():
+            full = self.prob.system_group_names.get(gname, [])
+            if name in full:
+                comp = full.index(name)
+                j = next(j for j, t in enumerate(lay.grid) if t >= 0)
+                return self.w[:, lay.index[comp, j]]
+        raise KeyError(name)

@@ -34,11 +34,11 @@ def V(name, value=None, lb=-np.inf, ub=np.inf):
 
 
 def one_room(N=15, T0=298.16, load=150.0, T_in=290.15, T_upper=295.15, u_prev=0.02,
-             s_T=0.001, r_mDot=0.01, d=2, solver_options=TIGHT, method="legendre", r_delta_mDot=None):
+             s_T=0.001, r_mDot=0.01, d=2, solver_options=TIGHT, method="legendre", r_delta_mDot=None, model=None):
     """``r_delta_mDot``: use the change-penalty model (`with_change_control_penalty.py`)."""
     be = create_optimization_backend({
         "type": "mi355x",
-        "model": {"type": "agentlib_mpc_amd.models.examples."
+        "model": model or {"type": "agentlib_mpc_amd.models.examples."
                           + ("OneRoom" if r_delta_mDot is None else "OneRoomDU")},
         "discretization_options": {"collocation_order": d, "collocation_method": method,
                                    "prediction_horizon": N, "time_step": 300},
@@ -63,10 +63,10 @@ def _vals(v, n):
 
 
 def admm_room(N=10, T0=296.0, dist=150.0, T_set=296.0, rho=0.4, zbar=0.02, lam=0.0,
-              solver_options=TIGHT):
+              solver_options=TIGHT, model=None):
     be = create_optimization_backend({
         "type": "mi355x_admm",
-        "model": {"type": "agentlib_mpc_amd.models.examples.CooledRoom"},
+        "model": model or {"type": "agentlib_mpc_amd.models.examples.CooledRoom"},
         "discretization_options": {"prediction_horizon": N, "time_step": 60},
         "solver": {"name": "ipopt", "options": solver_options},
     })
@@ -85,10 +85,10 @@ def admm_room(N=10, T0=296.0, dist=150.0, T_set=296.0, rho=0.4, zbar=0.02, lam=0
     return be, cv
 
 
-def admm_ahu(N=10, rho=0.4, zbar=0.01, lam=0.0, solver_options=TIGHT):
+def admm_ahu(N=10, rho=0.4, zbar=0.01, lam=0.0, solver_options=TIGHT, model=None):
     be = create_optimization_backend({
         "type": "mi355x_admm",
-        "model": {"type": "agentlib_mpc_amd.models.examples.AirHandler"},
+        "model": model or {"type": "agentlib_mpc_amd.models.examples.AirHandler"},
         "discretization_options": {"prediction_horizon": N, "time_step": 60},
         "solver": {"name": "ipopt", "options": solver_options},
     })
@@ -109,10 +109,10 @@ def admm_ahu(N=10, rho=0.4, zbar=0.01, lam=0.0, solver_options=TIGHT):
 
 
 def exchange_room(N=10, T0=296.0, dist=150.0, rho=1e4, diff=0.0, lam=0.0, T_set=296.0,
-                  solver_options=TIGHT, integrator="euler"):
+                  solver_options=TIGHT, integrator="euler", model=None):
     be = create_optimization_backend({
         "type": "mi355x_admm",
-        "model": {"type": "agentlib_mpc_amd.models.examples.ExchangeRoom"},
+        "model": model or {"type": "agentlib_mpc_amd.models.examples.ExchangeRoom"},
         "discretization_options": {"method": "multiple_shooting", "integrator": integrator,
                                    "prediction_horizon": N, "time_step": 120},
         "solver": {"name": "ipopt", "options": solver_options},
@@ -133,10 +133,10 @@ def exchange_room(N=10, T0=296.0, dist=150.0, rho=1e4, diff=0.0, lam=0.0, T_set=
     return be, cv
 
 
-def exchange_supply(N=10, rho=1e4, diff=0.0, lam=0.0, penalty=0.1, solver_options=TIGHT):
+def exchange_supply(N=10, rho=1e4, diff=0.0, lam=0.0, penalty=0.1, solver_options=TIGHT, model=None):
     be = create_optimization_backend({
         "type": "mi355x_admm",
-        "model": {"type": "agentlib_mpc_amd.models.examples.ExchangeSupply"},
+        "model": model or {"type": "agentlib_mpc_amd.models.examples.ExchangeSupply"},
         "discretization_options": {"method": "multiple_shooting", "integrator": "euler",
                                    "prediction_horizon": N, "time_step": 120},
         "solver": {"name": "ipopt", "options": solver_options},

@@ -98,6 +98,10 @@ def custom_injection(config):
         mod, _, cls = config.rpartition(".")
         return getattr(importlib.import_module(mod), cls)
     if isinstance(config, dict):
+        # model files written against the reference import agentlib_mpc.models...
+        from agentlib_mpc_amd.compat import install_reference_aliases
+
+        install_reference_aliases()
         file = pathlib.Path(config["file"]).resolve()
         name = f"_mpcx_injected_{abs(hash(str(file)))}"
         if name in sys.modules:
@@ -146,6 +150,7 @@ class OptimizationBackend(_RefOptimizationBackend if _RefOptimizationBackend is 
         _type = model.pop("type")
         cls = custom_injection(_type)
         instance = cls(**model)
+        # `backend.py:94-100`: the reference checks the model against _supported_models
         if self._supported_models and not any(isinstance(instance, m) for m in self._supported_models.values()):
             raise TypeError(
                 f"Given model is of type {type(instance)} but should be instance of one of:"

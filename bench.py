@@ -370,6 +370,123 @@ def c5_admm_bench(args, world, rank, dev):
     }
 
 
+def e2e_bench(args, world, rank, dev):
+    """One closed-loop C3 control step END TO END through the plugin API
+    (``MI355XBackend.solve_batch``, the drop-in for ``OptimizationBackend.solve`` of every
+    agent): new per-agent measurements in the agents' MPCVariables -> vectorised
+    marshalling -> host->device copies -> one kernel launch -> solutions and stats back ->
+    first control per agent (the actuation of `modules/mpc/mpc.py:342-357`).  Warm
+    started from each agent's previous optimum after the first step.  The array path
+    (``solve_arrays`` on [n, .] inputs, no per-agent objects) is timed beside it."""
+    import copy
+
+    import torch
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+
+    n = args.agents
+    be, cv = bm.one_room(solver_options=solver_settings(args)[0])
+    vals = fleet_values(n, 20261015 + 2 + rank)
+    agents = []
+    for a in range(n):
+        c = copy.deepcopy(cv)
+        for k in ("T", "load", "T_in", "T_upper", "mDot"):
+            c[k].value = float(vals[k][a])
+        agents.append(c)
+    rng = np.random.default_rng(7 + rank)
+    steps = max(2, args.steps)
+    be.solve_batch(0.0, agents)  # warm-up (marshal maps, code object)
+    times, kernel = [], []
+    for k in range(1, steps + 1):
+        drift = rng.normal(0.0, 0.05, n)
+        for a, c in enumerate(agents):  # the agents' new measurements (data broker, untimed)
+            c["T"].value = float(vals["T"][a] + drift[a])
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        res = be.solve_batch(300.0 * k, agents)
+        lo, hi = cv["mDot"].lb, cv["mDot"].ub
+        u0 = np.clip(res.first_values("mDot"), lo, hi)
+        times.append(time.perf_counter() - t0)
+        kernel.append(res.stats[0]["t_wall_total"])
+    ok = sum(1 for s_ in res.stats if s_["success"])
+    # array path: [n, .] inputs straight from per-agent measurement arrays
+    prob = be.problem
+    t_arr = []
+    for k in range(steps):
+        t0 = time.perf_counter()
+        p, lbw, ubw, w0 = fleet_nlp_inputs(prob, cv, {key: vals[key] for key in ("T", "load", "T_in", "T_upper", "mDot")})
+        r2 = be.solve_arrays(p, lbw, ubw, w0)
+        u0_arr = r2.first_values("mDot")
+        t_arr.append(time.perf_counter() - t0)
+    return {
+        "workload": "C3 closed-loop step through the plugin API: MPCVariable measurements of every agent -> "
+                    "solve_batch (vectorised marshalling, H2D, kernel, D2H) -> first control per agent",
+        "agents": n, "steps": steps,
+        "ms_per_step_plugin_api": float(np.median(times) * 1e3),
+        "ms_per_step_solve_and_copies": float(np.median(kernel) * 1e3),
+        "ms_per_step_array_path": float(np.median(t_arr) * 1e3),
+        "solves_per_s_plugin_api": ok / float(np.median(times)),
+        "converged_fraction": ok / n,
+        "actuation_checksum": float(np.sum(u0)) + 0.0 * float(np.sum(u0_arr)),
+    }
+
+
+def c1_latency(args, dev):
+    """C1 single-agent latency (simple_mpc, one agent): ``backend.solve(now, current_vars)``
+    end to end (marshalling + copies + kernel + results), and the kernel alone (HIP events
+    on the launch stream); the C restatement of the oracle on one host core beside it."""
+    import torch
+    from agentlib_mpc_amd import benchmarks as bm
+
+    solver_opts, oracle_opts = solver_settings(args)
+    be, cv = bm.one_room(solver_options=solver_opts)
+    for _ in range(3):
+        be._remembered = None
+        be.solve(0.0, cv)
+    e2e = []
+    for _ in range(20):
+        be._remembered = None  # cold start each time (the reference's first solve)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r = be.solve(0.0, cv)
+        e2e.append(time.perf_counter() - t0)
+    prob = be.problem
+    p, lbw, ubw, w0 = prob.marshal.inputs([cv], 0.0)
+    native = be._native()
+    T = lambda a: torch.as_tensor(a, device=dev).contiguous()  # noqa: E731
+    tp, tl, tu, tw0 = T(p), T(lbw), T(ubw), T(w0)
+    tw = torch.empty_like(tw0)
+    stream = torch.cuda.current_stream(dev)
+    ks = []
+    for _ in range(20):
+        tw.copy_(tw0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        native.solve(tp, tl, tu, tw, stream=stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ks.append(e0.elapsed_time(e1))
+    out = {"workload": "C1: examples/one_room_mpc/physical/simple_mpc.py, one agent, cold start",
+           "ms_end_to_end": float(np.median(e2e) * 1e3), "ms_kernel": float(np.median(ks)),
+           "iter_count": int(r.stats["iter_count"]), "return_status": r.stats["return_status"]}
+    try:
+        from oracle import cbuild
+
+        cbuild.build()
+        opts = dict(oracle_opts)
+        tol, mi = opts.pop("tol"), opts.pop("max_iter")
+        t0 = time.perf_counter()
+        reps = 0
+        while reps < 200 and (reps == 0 or time.perf_counter() - t0 < 1.0):
+            cbuild.solve_room_fleet(p, lbw, ubw, w0, tol=tol, max_iter=mi, threads=1, **opts)
+            reps += 1
+        out["cpu_baseline_ms"] = (time.perf_counter() - t0) / reps * 1e3
+        out["cpu_baseline"] = "oracle/c/ipm_oracle.c, 1 thread, same NLP and IPOPT settings"
+    except Exception as e:  # pragma: no cover
+        out["cpu_baseline_error"] = repr(e)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -387,6 +504,7 @@ def main():
     ap.add_argument("--c5-iters", type=int, default=50)
     ap.add_argument("--mhe-agents", type=int, default=4096, help="MHE estimators per GPU (0: skip)")
     ap.add_argument("--c2-blocks", type=int, default=1024, help="C2 4-room+AHU blocks per GPU (0: skip)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the plugin-API end-to-end leg and C1 latency")
     args = ap.parse_args()
 
     import torch
@@ -457,6 +575,8 @@ def main():
     c5 = c5_admm_bench(args, world, rank, dev) if args.c5_blocks > 0 else None
     c2 = c2_admm_bench(args, world, rank, dev) if args.c2_blocks > 0 else None
     mhe = mhe_bench(args, world, rank, dev) if args.mhe_agents > 0 else None
+    e2e = e2e_bench(args, world, rank, dev) if not args.no_e2e else None
+    c1 = c1_latency(args, dev) if not args.no_e2e and rank == 0 else None
     stats = stats_to_dicts(st.cpu().numpy().tobytes())
     n_ok = sum(1 for s in stats if s["success"])
     arr = {"iter": np.array([s["iter_count"] for s in stats]),
@@ -530,6 +650,10 @@ def main():
             out["c2_admm"] = c2
         if mhe is not None:
             out["mhe"] = mhe
+        if e2e is not None:
+            out["e2e"] = e2e
+        if c1 is not None:
+            out["c1_latency"] = c1
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(p, lbw, ubw, w0, oracle_opts)

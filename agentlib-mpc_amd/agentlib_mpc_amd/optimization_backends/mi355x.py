@@ -165,7 +165,7 @@ class MI355XBackend(OptimizationBackend):
         (``result_bounds``: the bounds its lower/upper columns show, default lbw/ubw)."""
         import torch
 
-        from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+        from agentlib_mpc_amd.runtime.native import STATS_BYTES, StatsView, stats_array
 
         prob = self.problem
         native = self._native()
@@ -182,10 +182,9 @@ class MI355XBackend(OptimizationBackend):
         st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=dev)
         native.solve(tp, tl, tu, tw, lbg=tg, ubg=tug, lam_g=lam_g, stats=st)
         w = prob.from_kernel(tw.cpu().numpy(), lbw)
-        stats = stats_to_dicts(st.cpu().numpy().tobytes())
+        raw = st.cpu().numpy()
         wall = time.perf_counter() - t0
-        for s_ in stats:
-            s_["t_wall_total"] = wall
+        stats = StatsView(stats_array(raw), {"t_wall_total": wall})
         from agentlib_mpc_amd.optimization_backends.problem import FleetResults
 
         rlb, rub = result_bounds if result_bounds is not None else (lbw, ubw)

@@ -14,6 +14,7 @@ is the native batched kernel (:class:`agentlib_mpc_amd.runtime.native.NativeProb
 from __future__ import annotations
 
 import math
+import operator
 from collections.abc import Sequence
 from typing import Dict, List, Optional, Tuple
 
@@ -296,20 +297,26 @@ def fleet_nlp_inputs(prob: CompiledProblem, template_vars: dict, overrides: Dict
             with np.errstate(invalid="ignore"):
                 guess = np.nan_to_num(0.5 * (lb + ub), posinf=0, neginf=-0)
         w0[:, idx] = guess
-        for t, cols in enumerate(lay.columns):
-            for i, c in enumerate(cols):
-                if lay.lb_par[t][i] >= 0:
-                    lbw[:, c] = p[:, lay.lb_par[t][i]]
-                if lay.ub_par[t][i] >= 0:
-                    ubw[:, c] = p[:, lay.ub_par[t][i]]
-                if lay.guess_par[t][i] >= 0:
-                    w0[:, c] = p[:, lay.guess_par[t][i]]
+    for key, arr in (("lb", lbw), ("ub", ubw), ("guess", w0)):
+        cols, pars = prob.marshal.over[key]
+        if cols.size:
+            arr[:, cols] = p[:, pars]
     return p, lbw, ubw, w0
 
 
 # ---------------------------------------------------------------------------
 # batched marshalling (structure of arrays over the agents of one structure)
 # ---------------------------------------------------------------------------
+_FAST_TYPES = (float, int, np.float64, np.int64, list)
+_VLU = operator.attrgetter("value", "lb", "ub")
+
+
+def _first_of_each_type(objs):
+    seen = {}
+    for o in objs:
+        seen.setdefault(type(o), o)
+    return seen.values()
+
 class BatchMarshal:
     """Array maps of one problem structure, built once: ``mpc_inputs`` +
     ``initial_guess`` + ``nlp_inputs`` for many agents at once (reference semantics,
@@ -368,16 +375,23 @@ class BatchMarshal:
             col += dim
 
     @staticmethod
-    def _column(values, n_grid, now, method_of, what):
-        """[n, G] samples of one variable for every agent (``sampling.sample`` semantics)."""
-        n = len(values)
-        out = np.empty((n, n_grid))
-        fast = [isinstance(v, (float, int)) for v in values]
-        if all(fast):
-            out[:] = np.asarray(values, float)[:, None]
-            return out
+    def _column(values, grid, now, method_of):
+        """[n, G] samples of one variable for every agent (``sampling.sample`` semantics):
+        numbers are constant rows and grid-length lists are taken as they are, both in
+        one numpy conversion; anything else is sampled agent by agent."""
+        n, G = len(values), len(grid)
+        if all(type(v) in _FAST_TYPES for v in values):
+            try:
+                arr = np.array(values, dtype=float)
+            except (TypeError, ValueError):
+                arr = None
+            if arr is not None and arr.ndim == 1:
+                return np.repeat(arr[:, None], G, axis=1)
+            if arr is not None and arr.ndim == 2 and arr.shape[1] == G and all(type(v) is list for v in values):
+                return arr
+        out = np.empty((n, G))
         for a, v in enumerate(values):
-            out[a] = sampling.sample(trajectory=v, grid=what, current=now, method=method_of(a))
+            out[a] = sampling.sample(trajectory=v, grid=grid, current=now, method=method_of(a))
         return out
 
     def inputs(self, batch_vars: Sequence[dict], now: float, w_prev: Optional[np.ndarray] = None,
@@ -390,22 +404,33 @@ class BatchMarshal:
         n = len(batch_vars)
         p = np.full((n, nlp.npar), np.nan)
         groups = {}
+        cache = {}
+
+        def gather(ref):
+            """(variables, values, lbs, ubs) of one name over the agents, two passes."""
+            if ref not in cache:
+                vs = list(map(operator.itemgetter(ref), batch_vars))
+                try:
+                    vals, lbs, ubs = zip(*map(_VLU, vs))
+                except AttributeError:
+                    vals, lbs, ubs = [getattr(v, "value", None) for v in vs], None, None
+                cache[ref] = (vs, vals, lbs, ubs)
+            return cache[ref]
+
         for name, grid, rows, index in self.pars:
             mat = np.empty((n, len(rows), len(grid)))
             for i, ref, default in rows:
                 if ref is None:
                     mat[:, i, :] = default
                     continue
-                vs = [cv[ref] for cv in batch_vars]
-                vals = [v.value for v in vs]
+                vs, vals, _, _ = gather(ref)
                 if any(v is None for v in vals):
                     raise ValueError(f"Input for variable {ref} is empty. Cannot solve optimization problem.")
-                for v in vs:
-                    if not hasattr(v, "interpolation_method"):
-                        raise TypeError(
-                            f"The variable {ref} does not have an interpolationmethod. All Variables "
-                            "used in MPC need to be of type MPCVariable (subclass of AgentVariable).")
-                mat[:, i, :] = self._column(vals, len(grid), now, lambda a: vs[a].interpolation_method, grid)
+                if not all(hasattr(v, "interpolation_method") for v in _first_of_each_type(vs)):
+                    raise TypeError(
+                        f"The variable {ref} does not have an interpolationmethod. All Variables "
+                        "used in MPC need to be of type MPCVariable (subclass of AgentVariable).")
+                mat[:, i, :] = self._column(vals, grid, now, lambda a: vs[a].interpolation_method)
             groups[name] = mat
             if index is not None:
                 p[:, index] = mat
@@ -419,10 +444,10 @@ class BatchMarshal:
                 if ref is None:
                     lb[:, i, :], ub[:, i, :] = dlb, dub
                     continue
-                vs = [cv[ref] for cv in batch_vars]
+                vs, _, lbs, ubs = gather(ref)
                 meth = lambda a: getattr(vs[a], "interpolation_method", "linear")  # noqa: E731
-                ub[:, i, :] = self._column([v.ub for v in vs], len(grid), now, meth, grid)
-                lb[:, i, :] = self._column([v.lb for v in vs], len(grid), now, meth, grid)
+                ub[:, i, :] = self._column(ubs, grid, now, meth)
+                lb[:, i, :] = self._column(lbs, grid, now, meth)
             if index is None:
                 continue
             lbw[:, index] = lb

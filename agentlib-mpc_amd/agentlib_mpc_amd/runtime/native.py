@@ -281,6 +281,55 @@ class NativeProblem:
             raise NativeError(f"mpcx_batch_solve failed ({rc})")
 
 
+_STATS_DOUBLES = ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")
+_STATS_INTS = ("iter_count", "status", "n_inertia_corrections", "n_linesearch_fallbacks", "n_factorizations",
+               "n_trials", "n_block_chain", "reserved")
+
+
+def stats_array(raw_bytes):
+    """``mpcx_stats`` records as a numpy structured array (no per-agent objects)."""
+    import numpy as np
+
+    dt = np.dtype([(n, "<f8") for n in _STATS_DOUBLES] + [(n, "<i4") for n in _STATS_INTS])
+    assert dt.itemsize == STATS_BYTES
+    return np.frombuffer(bytes(raw_bytes), dtype=dt)
+
+
+class StatsView:
+    """Per-agent stats dicts (IPOPT ``stats()`` keys, `core/discretization.py:41-47`) built
+    on access from the structured array; ``array`` holds all agents' fields."""
+
+    def __init__(self, arr, extra: Optional[dict] = None):
+        self.array = arr
+        self.extra = extra or {}
+
+    def __len__(self):
+        return len(self.array)
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        s = self.array[i]
+        st = int(s["status"])
+        d = {"obj": float(s["obj"]), "primal_inf": float(s["primal_inf"]), "dual_inf": float(s["dual_inf"]),
+             "compl_inf": float(s["compl_inf"]), "mu": float(s["mu"]), "obj_scale": float(s["obj_scale"]),
+             "iter_count": int(s["iter_count"]), "status": st,
+             "return_status": STATUS_NAMES.get(st, str(st)), "success": st in (0, 1),
+             "n_inertia_corrections": int(s["n_inertia_corrections"]),
+             "n_linesearch_fallbacks": int(s["n_linesearch_fallbacks"]),
+             "n_factorizations": int(s["n_factorizations"]), "n_trials": int(s["n_trials"]),
+             "n_block_chain": int(s["n_block_chain"])}
+        d.update(self.extra)
+        return d
+
+    @property
+    def success(self):
+        return (self.array["status"] == 0) | (self.array["status"] == 1)
+
+
 def stats_to_dicts(raw_bytes) -> list:
     """Decode a uint8 tensor/bytes of n * sizeof(mpcx_stats) into dicts."""
     buf = bytes(raw_bytes)

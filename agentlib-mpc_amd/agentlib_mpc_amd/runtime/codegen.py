@@ -43,8 +43,10 @@ class GeneratedModel:
     dims: Dict[str, int]
     flops: Dict[str, int]
     nnz: Dict[str, int]
-    #: built with MPCX_FORCE_BLOCK_CHAIN (rank-deficient stage interiors, MHE lifts)
+    #: built with MPCX_FORCE_BLOCK_CHAIN (stage interiors singular even with bordered rows)
     block_chain_only: bool = False
+    #: stage rows kept in the border (their multipliers are chained with x_{k+1})
+    bordered_rows: list = dataclasses.field(default_factory=list)
 
 
 def _bindings(nlp: StageNLP) -> Dict[sx.Expr, str]:
@@ -77,14 +79,13 @@ def _structural_rank(rows: List[set], n_cols: int) -> int:
     return sum(1 for r in range(len(rows)) if augment(r, set()))
 
 
-def interior_rank_deficient(nlp: StageNLP) -> bool:
-    """True when the equality rows of a stage cannot all be matched to the stage's
-    own variables V (structural rank of their V-Jacobian below the row count), e.g.
-    more states than free inputs per interval (continuity rows), a carried
-    previous control, or an MHE link row.  The kernel's stage-parallel elimination
-    needs nonsingular stage interiors; near-singular ones are not always caught by
-    its zero-pivot test and give inaccurate Newton steps, so such structures are
-    factored by the sequential block chain from the start.  Equality rows are
+def interior_rank_deficient(nlp: StageNLP, bordered=()) -> bool:
+    """True when the equality rows of a stage (except the ``bordered`` ones) cannot all be
+    matched to the stage's own variables V (structural rank of their V-Jacobian below the
+    row count), e.g. more states than free inputs per interval (continuity rows), a
+    carried previous control, or an MHE link row.  The kernel's stage-parallel
+    elimination needs nonsingular stage interiors; near-singular ones are not always
+    caught by its zero-pivot test and give inaccurate Newton steps.  Equality rows are
     those whose bound expressions coincide at a random parameter point."""
     import numpy as np
 
@@ -98,14 +99,38 @@ def interior_rank_deficient(nlp: StageNLP) -> bool:
     ub = np.array(sx.evaluate(st.g_ub, vals), float)
     col = {v.uid: i for i, v in enumerate(st.V)}
     rows = []
+    skip = set(bordered)
     for i in np.flatnonzero(lb == ub):
+        if int(i) in skip:
+            continue
         rows.append({col[f.uid] for f in sx.free_symbols([st.g[i]]) if f.uid in col})
     return _structural_rank(rows, len(st.V)) < len(rows)
 
 
+def continuity_rows(nlp: StageNLP) -> list:
+    """Stage rows through x_{k+1} (the continuity / shift equations)."""
+    st = nlp.stage
+    x1 = {v.uid for v in st.X1}
+    return [r for r, g in enumerate(st.g) if any(f.uid in x1 for f in sx.free_symbols([g]))]
+
+
+def factorisation_plan(nlp: StageNLP):
+    """(bordered rows, block chain only): the kernel eliminates every stage interior in
+    parallel; when the interior would be singular with the continuity rows in it (more
+    states than free stage inputs: MHE lifts, change penalties, 2-state zone models) those
+    rows are kept in the border and their multipliers join x_{k+1} in the chain; only if
+    that still leaves the interior singular is the sequential block chain used."""
+    if not (nlp.force_block_chain or interior_rank_deficient(nlp)):
+        return [], False
+    cont = continuity_rows(nlp)
+    if nlp.nx > 0 and len(cont) == nlp.nx and not interior_rank_deficient(nlp, cont):
+        return cont, False
+    return [], True
+
+
 def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     st = nlp.stage
-    force_chain = nlp.force_block_chain or interior_rank_deficient(nlp)
+    bordered, force_chain = factorisation_plan(nlp)
     loc = st.local
     nl = len(loc)
     ng = nlp.ng
@@ -133,16 +158,28 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     cg = sx.CodeGen(bind, prefix="b")
     bd_lines = cg.emit([(f"lb[{i} * S]", e) for i, e in enumerate(st.g_lb)]
                        + [(f"ub[{i} * S]", e) for i, e in enumerate(st.g_ub)])
-    # local order of the kernel's stage system: [V (nv), lambda (ng), x_k (nx), x_{k+1} (nx), rhs]
+    # local order of the kernel's stage system:
+    #   [V (nv), lambda_rest (ng - nmu), x_k (nx), mu_k (nmu), x_{k+1} (nx), rhs]
     nx, nv = nlp.nx, nlp.nv
-    ni = nv + ng
+    nmu = len(bordered)
+    ni = nv + ng - nmu
+    rest = [r for r in range(ng) if r not in set(bordered)]
+    crow = [0] * ng
+    for q, r in enumerate(rest):
+        crow[r] = nv + q
+    for q, r in enumerate(bordered):
+        crow[r] = ni + nx + q
+    nloc = ni + 2 * nx + nmu
+    lrow = [-1] * (nloc + 1)
+    for r, li in enumerate(crow):
+        lrow[li] = r
 
     def lidx(n: int) -> int:
         if n < nx:
             return ni + n
         if n < nx + nv:
             return n - nx
-        return ni + nx + (n - nx - nv)
+        return ni + nx + nmu + (n - nx - nv)
 
     def pk(i: int, j: int) -> int:
         i, j = max(i, j), min(i, j)
@@ -156,7 +193,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     gb = dict(bind)
     for r, s_ in enumerate(gsym):
         gb[s_] = f"G[{r}]"
-    lp_j = [(f"lp[{pk(nv + i, lidx(j))}]", sx.mul(gsym[i], jac[i][j])) for i in range(ng) for j in range(nl)
+    lp_j = [(f"lp[{pk(crow[i], lidx(j))}]", sx.mul(gsym[i], jac[i][j])) for i in range(ng) for j in range(nl)
             if not jac[i][j].is_const(0.0)]
     cg = sx.CodeGen(gb, prefix="c")
     gj_lines = cg.emit(gj_assign + lp_j)
@@ -195,11 +232,13 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     # where not even two stage systems fit gets up to 40 KB (4 agents per CU) so
     # its stages are factorised in one or two rounds (mirrors SLOT_BYTES /
     # OTHER_BYTES in csrc/mpcx_ipm.hip)
-    N_, NX_, NI_ = nlp.N, nlp.nx, nv + ng
-    nxp = max(NX_, 1)
-    pks = ((NI_ + 2 * NX_ + 1) * (NI_ + 2 * NX_ + 2) // 2) | 1
+    N_, NX_, NI_ = nlp.N, nlp.nx, ni
+    nxp, ncp = max(NX_, 1), max(NX_ + nmu, 1)
+    pks = ((nloc + 1) * (nloc + 2) // 2) | 1
     slot = 8 * pks + 8 * NI_
-    other = 8 * (N_ * 4 * nxp * nxp + 3 * N_ * nxp + 3 * nxp * nxp + 64 + nlp.npg + N_ * nlp.nps + N_) + 8 * nxp + 64
+    soff = nxp * nxp + ncp * ncp + ncp * nxp
+    other = 8 * (N_ * soff + N_ * ncp * ncp + N_ * (NX_ + ncp) + N_ * ncp + 3 * ncp * ncp + 64 + nlp.npg
+                 + N_ * nlp.nps + N_) + 8 * ncp + 64
     need = other + N_ * slot
     lds_target = 9600 if other + 2 * slot <= 9600 else min(need, 40960)
 
@@ -216,6 +255,9 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         f"#define MPCX_ABI {KERNEL_ABI_VERSION}",
         f"#define MPCX_LDS_TARGET {lds_target}",
         *(["#define MPCX_FORCE_BLOCK_CHAIN 1"] if force_chain else []),
+        *([f"#define MPCX_NMU {nmu}",
+           f"#define MPCX_CROW_INIT {', '.join(map(str, crow))}",
+           f"#define MPCX_LROW_INIT {', '.join(map(str, lrow))}"] if nmu else []),
         "#include <hip/hip_runtime.h>",
         "#include <math.h>",
         "",
@@ -242,4 +284,5 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         src = src.replace('#include <math.h>\n', '#include <math.h>\n' + "\n".join(tables) + "\n", 1)
         src = re.sub(r"ANN(\d+)_", lambda m: f"ANN{local[int(m.group(1))]}_", src)
     key = hashlib.sha1(src.encode()).hexdigest()[:16]
-    return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz, block_chain_only=force_chain)
+    return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz, block_chain_only=force_chain,
+                          bordered_rows=list(bordered))

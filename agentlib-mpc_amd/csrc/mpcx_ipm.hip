@@ -67,16 +67,37 @@ typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(3))) double ldsd;
 typedef __attribute__((address_space(3))) int ldsi;
 
-// stage-local system [V_k, lambda_k | x_k, x_{k+1} | rhs]
-constexpr int NI = NV + NG;               // stage interior (eliminated in parallel)
+// stage-local system [V_k, lambda_rest | x_k | mu_k, x_{k+1} | rhs].  mu_k: the NMU
+// continuity rows of the stage (the rows through x_{k+1}) when they are kept in the border
+// (models with more states than free stage inputs): their multipliers join
+// x_{k+1} in the chain block c_k = [mu_k, x_{k+1}] (indefinite 2x2-pivoted BK); otherwise
+// NMU = 0 and every row is eliminated in the interior.
+#ifndef MPCX_NMU
+#define MPCX_NMU 0
+#endif
+constexpr int NMU = MPCX_NMU;
+constexpr int NI = NV + NG - NMU;         // stage interior (eliminated in parallel)
 constexpr int NXP = NX > 0 ? NX : 1;
 constexpr int NXX = NXP * NXP;
-constexpr int NLOC = NI + 2 * NX;         // local system size
+constexpr int NC = NX + NMU;              // chain block per stage boundary
+constexpr int NCP = NC > 0 ? NC : 1;
+constexpr int NCC = NCP * NCP;
+constexpr int SOFF = NXX + NCC + NCP * NXP;  // per stage: S00 (x_k), S11 (c_k), S10 (c_k x x_k)
+constexpr int NLOC = NI + NX + NC;        // local system size
 constexpr int RB = NLOC;                  // border row holding the right-hand side
-constexpr int NTR = 2 * NX + 1;           // trailing rows: x_k, x_{k+1}, border
+constexpr int NTR = NX + NC + 1;          // trailing rows: x_k, c_k, border
+constexpr int LMU = NI + NX;              // first local index of mu_k
+constexpr int LX1 = NI + NX + NMU;        // first local index of x_{k+1}
+static_assert(NMU == 0 || NMU == NX, "bordered continuity rows: one per state");
 constexpr int PKB = (NLOC + 1) * (NLOC + 2) / 2;  // packed lower triangle incl. border
 constexpr int PKS = PKB | 1;              // odd stride between stage slots
 static_assert(NI > 0, "stage interior must be non-empty");
+#ifndef MPCX_CROW_INIT  // identity: rows in stage order after V
+#define MPCX_CROW_INIT 0
+#define MPCX_LROW_INIT 0
+#endif
+__constant__ int kCROW[NG > 0 ? NG : 1] = {MPCX_CROW_INIT};    // row r -> local index
+__constant__ int kLROW[NLOC + 1] = {MPCX_LROW_INIT};           // local dual index -> row
 static_assert(NLOC < 64, "local fixed-variable masks are 64-bit");
 
 // workspace layout (doubles per agent)
@@ -195,8 +216,8 @@ __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // packed system + perm/piv
-constexpr int OTHER_BYTES = 8 * (N * 3 * NXX + N * NXX + 3 * N * NXP + 3 * NXX + 2 * MAXF + NPAR + N) +
-                            8 * NXP + 64;
+constexpr int OTHER_BYTES = 8 * (N * SOFF + N * NCC + N * (NX + NCP) + N * NCP + 3 * NCC + 2 * MAXF + NPAR + N) +
+                            8 * NCP + 64;
 #ifndef MPCX_LDS_TARGET
 #define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
 #endif
@@ -243,16 +264,16 @@ union LinLds {
 struct Lds {
   LinLds u;
   double par[NPAR];        // agent parameters (read by every evaluation)
-  double S[N * 3 * NXX];   // local Schur blocks per stage: S00 (x_k), S11 (x_{k+1}), S10
-  double Dinv[N * NXX];    // inverses of the state-chain pivots
-  double zx[N * 2 * NXP];  // forward-eliminated rhs of (x_k, x_{k+1}) per stage
-  double xs[N * NXP];      // state-chain rhs, then solution (x_1 .. x_N)
-  double C[NXX];
-  double CW[NXX];
-  double CY[NXX];
+  double S[N * SOFF];      // local Schur blocks per stage: S00 (x_k), S11 (c_k), S10 (c_k x x_k)
+  double Dinv[N * NCC];    // inverses of the chain pivots
+  double zx[N * (NX + NCP)];  // forward-eliminated rhs of (x_k, c_k) per stage
+  double xs[N * NCP];      // chain rhs, then solution (c_0 .. c_{N-1})
+  double C[NCC];
+  double CW[NCC];
+  double CY[NCC];
   unsigned long long fixm[N];  // per stage: local primal indices that are fixed variables
-  int cperm[NXP];
-  int cpiv[NXP];
+  int cperm[NCP];
+  int cpiv[NCP];
   int seq;                 // 1: last factorisation used the block chain
   int want_sdh;            // 1: keep the strided stage Hessians (block chain in use)
   int sdh_ok;              // 1: the workspace Hessians match the last eval_hess
@@ -786,23 +807,54 @@ __device__ __noinline__ void seq_solve(const Agent a) {
 // block-tridiagonal chain of nx x nx pivots (the only sequential part).
 __device__ __forceinline__ int pko(int i) { return (i * (i + 1)) >> 1; }
 
-// local index kinds: 0 primal V, 1 dual, 2 x_k, 3 x_{k+1}, 4 border (rhs)
+// local index kinds: 0 primal V, 1 dual (interior rows), 2 x_k, 5 dual mu_k (bordered
+// continuity rows), 3 x_{k+1}, 4 border (rhs)
 __device__ __forceinline__ int lkind(int i) {
-  return i < NV ? 0 : (i < NI ? 1 : (i < NI + NX ? 2 : (i < NLOC ? 3 : 4)));
+  return i < NV ? 0 : (i < NI ? 1 : (i < LMU ? 2 : (i < LX1 ? 5 : (i < NLOC ? 3 : 4))));
+}
+__device__ __forceinline__ bool kdual(int kind) { return kind == 1 || kind == 5; }
+// local index of constraint row r of a stage, and the row of a local dual index
+// (generated tables when continuity rows are bordered, else the identity order)
+__device__ __forceinline__ int crow(int r) {
+  if constexpr (NMU == 0) return NV + r; else return kCROW[r];
+}
+__device__ __forceinline__ int lrow(int i) {
+  if constexpr (NMU == 0) return i - NV; else return kLROW[i];
 }
 // index into the stage vector [X0, V, X1] of a primal local index
 __device__ __forceinline__ int lnl(int i, int kind) {
-  return kind == 0 ? NX + i : (kind == 2 ? i - NI : NX + NV + (i - NI - NX));
+  return kind == 0 ? NX + i : (kind == 2 ? i - NI : NX + NV + (i - LX1));
 }
 // NLP variable index of a primal local index of stage k
 __device__ __forceinline__ int lvar(int k, int i, int kind) {
   if (kind == 0) return NX + k * NP + i;
-  if (kind == 3) return NX + k * NP + NV + (i - NI - NX);
+  if (kind == 3) return NX + k * NP + NV + (i - LX1);
   return k == 0 ? (i - NI) : NX + (k - 1) * NP + NV + (i - NI);  // x_k
 }
-// block-order index ([V, X1, lambda]) of a local index of kind 0, 1, 3
+// block-order index ([V, X1, lambda]) of a local index of kind 0, 1, 3, 5
 __device__ __forceinline__ int lblk(int i, int kind) {
-  return kind == 0 ? i : (kind == 1 ? NP + i - NV : NV + (i - NI - NX));
+  return kind == 0 ? i : (kdual(kind) ? NP + lrow(i) : NV + (i - LX1));
+}
+
+// diagonal terms (barrier Sigma + delta_w, dual diagonal) and fixed variables
+__device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd* F, const KKTDiag kd,
+                                               unsigned long long fm) {
+  const gdbl* ws = a.ws;
+  for (int i = g; i < NLOC; i += G) {
+    const int ki = lkind(i);
+    const bool prim = (ki == 0 || ki == 3);
+    const bool fixd = (fm >> i) & 1ull;
+    const int vi = prim ? lvar(k, i, ki) : 0;
+    const int c = kdual(ki) ? k * NG + lrow(i) : 0;
+    const double xv = ws[O_X + vi], lo = ws[O_XL + vi], hi = ws[O_XU + vi];
+    const double zl = ws[O_ZL + vi], zu = ws[O_ZU + vi];
+    const double lbv = ws[O_LB + c], ubv = ws[O_UB + c], sv = ws[O_S + c];
+    const double sl = ws[O_SL + c], su = ws[O_SU + c], vl = ws[O_VL + c], vu = ws[O_VU + c];
+    const int ii = pko(i) + i;
+    if (prim && !fixd) F[ii] += (kd.mode == LSQ) ? 1.0 : sigma_x_v(xv, lo, hi, zl, zu) + kd.dw;
+    if (kdual(ki)) F[ii] = -dual_diag_v(cls_of(lbv, ubv, sl, su), sigma_s_v(sv, sl, su, vl, vu), kd);
+  }
+  wsync();
 }
 
 // assemble stage k's bordered local system into F (packed lower), G lanes: generic
@@ -821,13 +873,13 @@ __device__ __noinline__ void local_assemble_generic(const Agent a, int k, int g,
     const bool pi = (ki == 0 || ki == 2 || ki == 3), pj = (kj == 0 || kj == 2 || kj == 3);
     const bool fi = pi && ((fm >> i) & 1ull), fj = pj && ((fm >> j) & 1ull);
     const bool pp = pi && pj;
-    const bool dp = (ki == 1 && pj) || (kj == 1 && pi);
-    const bool bd = (ki == 4) && (kj == 0 || kj == 1 || kj == 3);
+    const bool dp = (kdual(ki) && pj) || (kdual(kj) && pi);
+    const bool bd = (ki == 4) && (kj != 2 && kj != 4);
     long off = 0, goff = O_GS;
     if (pp) {
       off = O_SDH + ((long)lnl(i, ki) * NL + lnl(j, kj)) * N + k;
     } else if (dp) {
-      const int r = (ki == 1 ? i : j) - NV, q = (ki == 1 ? j : i), kq = (ki == 1 ? kj : ki);
+      const int r = lrow(kdual(ki) ? i : j), q = (kdual(ki) ? j : i), kq = (kdual(ki) ? kj : ki);
       off = O_SDJ + ((long)r * NL + lnl(q, kq)) * N + k;
       goff = O_GS + k * NG + r;
     } else if (bd) {
@@ -843,42 +895,7 @@ __device__ __noinline__ void local_assemble_generic(const Agent a, int k, int g,
   }
   wsync();
   // pass 2: diagonal terms (barrier Sigma + delta_w, dual diagonal)
-  for (int i = g; i < NLOC; i += G) {
-    const int ki = lkind(i);
-    const bool prim = (ki == 0 || ki == 3);
-    const bool fixd = (fm >> i) & 1ull;
-    const int vi = prim ? lvar(k, i, ki) : 0;
-    const int c = (ki == 1) ? k * NG + i - NV : 0;
-    const double xv = ws[O_X + vi], lo = ws[O_XL + vi], hi = ws[O_XU + vi];
-    const double zl = ws[O_ZL + vi], zu = ws[O_ZU + vi];
-    const double lbv = ws[O_LB + c], ubv = ws[O_UB + c], sv = ws[O_S + c];
-    const double sl = ws[O_SL + c], su = ws[O_SU + c], vl = ws[O_VL + c], vu = ws[O_VU + c];
-    const int ii = pko(i) + i;
-    if (prim && !fixd) F[ii] += (kd.mode == LSQ) ? 1.0 : sigma_x_v(xv, lo, hi, zl, zu) + kd.dw;
-    if (ki == 1) F[ii] = -dual_diag_v(cls_of(lbv, ubv, sl, su), sigma_s_v(sv, sl, su, vl, vu), kd);
-  }
-  wsync();
-}
-
-// diagonal terms (barrier Sigma + delta_w, dual diagonal) and fixed variables
-__device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd* F, const KKTDiag kd,
-                                               unsigned long long fm) {
-  const gdbl* ws = a.ws;
-  for (int i = g; i < NLOC; i += G) {
-    const int ki = lkind(i);
-    const bool prim = (ki == 0 || ki == 3);
-    const bool fixd = (fm >> i) & 1ull;
-    const int vi = prim ? lvar(k, i, ki) : 0;
-    const int c = (ki == 1) ? k * NG + i - NV : 0;
-    const double xv = ws[O_X + vi], lo = ws[O_XL + vi], hi = ws[O_XU + vi];
-    const double zl = ws[O_ZL + vi], zu = ws[O_ZU + vi];
-    const double lbv = ws[O_LB + c], ubv = ws[O_UB + c], sv = ws[O_S + c];
-    const double sl = ws[O_SL + c], su = ws[O_SU + c], vl = ws[O_VL + c], vu = ws[O_VU + c];
-    const int ii = pko(i) + i;
-    if (prim && !fixd) F[ii] += (kd.mode == LSQ) ? 1.0 : sigma_x_v(xv, lo, hi, zl, zu) + kd.dw;
-    if (ki == 1) F[ii] = -dual_diag_v(cls_of(lbv, ubv, sl, su), sigma_s_v(sv, sl, su, vl, vu), kd);
-  }
-  wsync();
+  local_diagonal(a, k, g, F, kd, fm);
 }
 
 // Newton system of stage k: contiguous copy of the packed image the evaluators
@@ -1117,51 +1134,61 @@ __device__ __noinline__ void trailing_backsolve(ldsd* F, const ldsi* piv, int g)
   }
 }
 
-// State chain over x_1..x_N: D_j = S11^(j-1)... in chain index j (x_{j+1}):
-// D_j = S11^(j) + S00^(j+1) - S10^(j) D_{j-1}^{-1} S10^(j)^T,  S10^(j) couples x_{j+1}, x_j.
+// Chain over the stage boundaries, c_j = [mu_j, x_{j+1}] (NC = NMU + NX): block-tridiagonal
+// with the x-part of c_{j-1} coupling to c_j through S10^(j):
+//   D_j = S11^(j) + E S00^(j+1) E^T - S10^(j) [D_{j-1}^{-1}]_xx S10^(j)^T
+// (E embeds the NX states as the last NX entries of c).  Pivots are BK-factored (indefinite
+// when mu is bordered); fixed states are chained as identity rows.
+__device__ __forceinline__ const double* s00(int k) { return (const double*)(gL.S + k * SOFF); }
+__device__ __forceinline__ const double* s11(int k) { return (const double*)(gL.S + k * SOFF + NXX); }
+__device__ __forceinline__ const double* s10(int k) { return (const double*)(gL.S + k * SOFF + NXX + NCC); }
+
 __device__ __noinline__ Inertia chain_factor(const Agent a) {
   Lds& L = gL;
   Inertia in{0, 0, 0};
   const int lane = a.lane;
-  if constexpr (NX == 1) {
+  if constexpr (NX == 1 && NMU == 0) {
     double dprev = 0.0;
 #pragma unroll 1
     for (int j = 0; j < N; ++j) {
       double d;
-      if ((L.fixm[j] >> (NI + NX)) & 1ull) {
+      if ((L.fixm[j] >> LX1) & 1ull) {
         d = 1.0;
       } else {
-        d = L.S[j * 3 + 1] + (j + 1 < N ? L.S[(j + 1) * 3] : 0.0);
-        if (j > 0) { const double t = L.S[j * 3 + 2]; d -= t * t * dprev; }
+        d = s11(j)[0] + (j + 1 < N ? s00(j + 1)[0] : 0.0);
+        if (j > 0) { const double t = s10(j)[0]; d -= t * t * dprev; }
       }
       if (fabs(d) <= ZERO_PIVOT) { in.zero++; dprev = 0.0; }
       else { if (d > 0) in.pos++; else in.neg++; dprev = 1.0 / d; }
       if (lane == 0) L.Dinv[j] = dprev;
     }
-  } else if constexpr (NX > 1) {
+  } else if constexpr (NC > 0) {
+    constexpr int XO = NMU;  // offset of the states inside c
 #pragma unroll 1
     for (int j = 0; j < N; ++j) {
-      if (j > 0)
-        for (int e = lane; e < NXX; e += WAVE) {
+      if (j > 0)  // CW = S10^(j) [D_{j-1}^{-1}]_xx   (NC x NX)
+        for (int e = lane; e < NC * NX; e += WAVE) {
           const int r = e / NX, c = e % NX;
-          double s = 0.0;
-          for (int m = 0; m < NX; ++m) s += L.S[(j * 3 + 2) * NXX + r * NX + m] * L.Dinv[(j - 1) * NXX + m * NX + c];
-          L.CW[e] = s;
+          double sacc = 0.0;
+          for (int m = 0; m < NX; ++m) sacc += s10(j)[r * NX + m] * L.Dinv[(j - 1) * NCC + (XO + m) * NC + XO + c];
+          L.CW[e] = sacc;
         }
       wsync();
-      for (int e = lane; e < NXX; e += WAVE) {
-        const int r = e / NX, c = e % NX;
-        double v = L.S[(j * 3 + 1) * NXX + e] + (j + 1 < N ? L.S[((j + 1) * 3) * NXX + e] : 0.0);
+      for (int e = lane; e < NCC; e += WAVE) {
+        const int r = e / NC, c = e % NC;
+        double v = s11(j)[e];
+        if (j + 1 < N && r >= XO && c >= XO) v += s00(j + 1)[(r - XO) * NX + (c - XO)];
         if (j > 0)
-          for (int m = 0; m < NX; ++m) v -= L.CW[r * NX + m] * L.S[(j * 3 + 2) * NXX + c * NX + m];
-        const bool fr = (L.fixm[j] >> (NI + NX + r)) & 1ull, fc = (L.fixm[j] >> (NI + NX + c)) & 1ull;
+          for (int m = 0; m < NX; ++m) v -= L.CW[r * NX + m] * s10(j)[c * NX + m];
+        const bool fr = r >= XO && ((L.fixm[j] >> (LX1 + r - XO)) & 1ull);
+        const bool fc = c >= XO && ((L.fixm[j] >> (LX1 + c - XO)) & 1ull);
         if (fr || fc) v = (r == c) ? 1.0 : 0.0;
         L.C[e] = v;
       }
       wsync();
-      const Inertia bi = bk_factor<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), lane);
+      const Inertia bi = bk_factor<NC, NC>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), lane);
       in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
-      bk_inverse<NX, NX>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), LDSP(L.CW), LDSP(L.CY), LDSP(L.Dinv + j * NXX), lane);
+      bk_inverse<NC, NC>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), LDSP(L.CW), LDSP(L.CY), LDSP(L.Dinv + j * NCC), lane);
     }
   }
   wsync();
@@ -1171,14 +1198,15 @@ __device__ __noinline__ Inertia chain_factor(const Agent a) {
 __device__ __noinline__ void chain_solve(const Agent a) {
   Lds& L = gL;
   const int lane = a.lane;
-  // rho_j = z[x_{j+1}] of stage j + z[x_{j+1}] of stage j+1; forward y_j = rho_j - T_j Dinv_{j-1} y_{j-1}
-  if constexpr (NX == 1) {
+  constexpr int ZS = NX + NC;  // zx stride per stage: [x_k | c_k]
+  // rhs_j = z[c] of stage j + E z[x_k] of stage j+1
+  if constexpr (NX == 1 && NMU == 0) {
     if (lane == 0) {
       double y = 0.0;
 #pragma unroll 1
       for (int j = 0; j < N; ++j) {
         double r = L.zx[j * 2 + 1] + (j + 1 < N ? L.zx[(j + 1) * 2] : 0.0);
-        if (j > 0) r -= L.S[j * 3 + 2] * L.Dinv[j - 1] * y;
+        if (j > 0) r -= s10(j)[0] * L.Dinv[j - 1] * y;
         y = r;
         L.xs[j] = y;
       }
@@ -1186,42 +1214,44 @@ __device__ __noinline__ void chain_solve(const Agent a) {
 #pragma unroll 1
       for (int j = N - 1; j >= 0; --j) {
         double r = L.xs[j];
-        if (j + 1 < N) r -= L.S[(j + 1) * 3 + 2] * x;
+        if (j + 1 < N) r -= s10(j + 1)[0] * x;
         x = L.Dinv[j] * r;
         L.xs[j] = x;
       }
     }
-  } else if constexpr (NX > 1) {
-    for (int c = lane; c < NX; c += WAVE) L.xs[c] = L.zx[NX + c] + (N > 1 ? L.zx[2 * NX + c] : 0.0);
+  } else if constexpr (NC > 0) {
+    constexpr int XO = NMU;
+    for (int c = lane; c < NC; c += WAVE)
+      L.xs[c] = L.zx[NX + c] + (N > 1 && c >= XO ? L.zx[ZS + (c - XO)] : 0.0);
     wsync();
 #pragma unroll 1
     for (int j = 1; j < N; ++j) {
-      for (int r = lane; r < NX; r += WAVE) {  // CY = Dinv_{j-1} y_{j-1}
-        double s = 0.0;
-        for (int m = 0; m < NX; ++m) s += L.Dinv[(j - 1) * NXX + r * NX + m] * L.xs[(j - 1) * NX + m];
-        L.CY[r] = s;
+      for (int r = lane; r < NX; r += WAVE) {  // CY = [D_{j-1}^{-1} y_{j-1}]_x
+        double sacc = 0.0;
+        for (int m = 0; m < NC; ++m) sacc += L.Dinv[(j - 1) * NCC + (XO + r) * NC + m] * L.xs[(j - 1) * NC + m];
+        L.CY[r] = sacc;
       }
       wsync();
-      for (int r = lane; r < NX; r += WAVE) {
-        double v = L.zx[j * 2 * NX + NX + r] + (j + 1 < N ? L.zx[(j + 1) * 2 * NX + r] : 0.0);
-        for (int m = 0; m < NX; ++m) v -= L.S[(j * 3 + 2) * NXX + r * NX + m] * L.CY[m];
-        L.xs[j * NX + r] = v;
+      for (int r = lane; r < NC; r += WAVE) {
+        double v = L.zx[j * ZS + NX + r] + (j + 1 < N && r >= XO ? L.zx[(j + 1) * ZS + (r - XO)] : 0.0);
+        for (int m = 0; m < NX; ++m) v -= s10(j)[r * NX + m] * L.CY[m];
+        L.xs[j * NC + r] = v;
       }
       wsync();
     }
 #pragma unroll 1
     for (int j = N - 1; j >= 0; --j) {
-      for (int r = lane; r < NX; r += WAVE) {  // CY = y_j - T_{j+1}^T x_{j+1}
-        double v = L.xs[j * NX + r];
-        if (j + 1 < N)
-          for (int m = 0; m < NX; ++m) v -= L.S[((j + 1) * 3 + 2) * NXX + m * NX + r] * L.xs[(j + 1) * NX + m];
+      for (int r = lane; r < NC; r += WAVE) {  // CY = y_j - E S10^(j+1)^T c_{j+1}
+        double v = L.xs[j * NC + r];
+        if (j + 1 < N && r >= XO)
+          for (int m = 0; m < NC; ++m) v -= s10(j + 1)[m * NX + (r - XO)] * L.xs[(j + 1) * NC + m];
         L.CY[r] = v;
       }
       wsync();
-      for (int r = lane; r < NX; r += WAVE) {
-        double s = 0.0;
-        for (int m = 0; m < NX; ++m) s += L.Dinv[j * NXX + r * NX + m] * L.CY[m];
-        L.xs[j * NX + r] = s;
+      for (int r = lane; r < NC; r += WAVE) {
+        double sacc = 0.0;
+        for (int m = 0; m < NC; ++m) sacc += L.Dinv[j * NCC + r * NC + m] * L.CY[m];
+        L.xs[j * NC + r] = sacc;
       }
       wsync();
     }
@@ -1273,13 +1303,22 @@ __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
       }
     }
     if (act) {
-      if (NX > 0) {  // local Schur complement of the state blocks, eliminated rhs of the states
-        for (int e = g; e < 3 * NXX; e += G) {
-          const int blk = e / NXX, rr = (e % NXX) / NX, cc = e % NX;
-          const int ri = NI + (blk == 0 ? 0 : NX) + rr, ci = NI + (blk == 1 ? NX : 0) + cc;
-          L.S[(k * 3 + blk) * NXX + rr * NX + cc] = (ri >= ci) ? F[pko(ri) + ci] : F[pko(ci) + ri];
+      if (NC > 0) {  // local Schur complement on (x_k, c_k), eliminated rhs of those rows
+        constexpr int NS = NX * NX + NC * NC + NC * NX;
+        for (int e = g; e < NS; e += G) {
+          int ri, ci, o;
+          if (e < NX * NX) {
+            ri = NI + e / NX; ci = NI + e % NX; o = e;
+          } else if (e < NX * NX + NC * NC) {
+            const int f = e - NX * NX;
+            ri = LMU + f / NC; ci = LMU + f % NC; o = NXX + f;
+          } else {
+            const int f = e - NX * NX - NC * NC;
+            ri = LMU + f / NX; ci = NI + f % NX; o = NXX + NCC + f;
+          }
+          L.S[k * SOFF + o] = (ri >= ci) ? F[pko(ri) + ci] : F[pko(ci) + ri];
         }
-        for (int c = g; c < 2 * NX; c += G) L.zx[k * 2 * NX + c] = F[pko(RB) + NI + c];
+        for (int c = g; c < NX + NC; c += G) L.zx[k * (NX + NC) + c] = F[pko(RB) + NI + c];
       }
       trailing_backsolve(F, piv, g);
       // back-substitution operators, p-major, each lane stores (and later reads) its own p
@@ -1294,7 +1333,7 @@ __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   }
   Inertia in{wsumi(g == 0 ? gi.pos : 0), wsumi(g == 0 ? gi.neg : 0), wsumi(g == 0 ? gi.zero : 0)};
   if (lane == 0) L.seq = 0;
-  if (NX > 0) {
+  if (NC > 0) {
     const Inertia ci = chain_factor(a);
     in.pos += ci.pos; in.neg += ci.neg; in.zero += ci.zero;
   }
@@ -1308,27 +1347,29 @@ __device__ __noinline__ void solve(const Agent a) {
   if (L.seq) { seq_solve(a); return; }
   SPROF_DECL
   const int lane = a.lane, g = lane % G, slot = lane / G;
-  if (NX > 0) chain_solve(a);
+  if (NC > 0) chain_solve(a);
   SPROF(4);
 #pragma unroll 1
   for (int r = 0; r < ROUNDS; ++r) {
     const int k = r * SR + slot;
     if (!(slot < SR && k < N)) continue;
-    double xk[NXP], xk1[NXP];
+    double tv[NX + NC > 0 ? NX + NC : 1];  // [x_k, c_k]
 #pragma unroll
-    for (int c = 0; c < NX; ++c) {
-      xk[c] = (k > 0) ? L.xs[(k - 1) * NX + c] : 0.0;
-      xk1[c] = L.xs[k * NX + c];
-    }
+    for (int c = 0; c < NX; ++c) tv[c] = (k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) tv[NX + c] = L.xs[k * NC + c];
     for (int p = g; p < NI; p += G) {
       const gdbl* t = a.tr(k) + p * NTR;
-      double u = t[2 * NX];
+      double u = t[NX + NC];
 #pragma unroll
-      for (int c = 0; c < NX; ++c) u -= xk[c] * t[c] + xk1[c] * t[NX + c];
+      for (int c = 0; c < NX + NC; ++c) u -= tv[c] * t[c];
       const int o = a.prm(k)[p];
-      L.u.sol[k * NB + (o < NV ? o : NP + o - NV)] = u;
+      L.u.sol[k * NB + lblk(o, lkind(o))] = u;
     }
-    for (int c = g; c < NX; c += G) L.u.sol[k * NB + NV + c] = xk1[c];
+    for (int c = g; c < NC; c += G) {
+      const int li = LMU + c;
+      L.u.sol[k * NB + lblk(li, lkind(li))] = tv[NX + c];
+    }
   }
   wsync();
   SPROF(5);
@@ -1510,7 +1551,7 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
     unsigned long long m = 0ull;
     for (int i = 0; i < NLOC; ++i) {
       const int ki = lkind(i);
-      if (ki == 1) continue;
+      if (kdual(ki)) continue;
       const int vi = lvar(k, i, ki);
       if (a.xL()[vi] == a.xU()[vi]) m |= 1ull << i;
     }
@@ -1577,7 +1618,7 @@ __device__ __noinline__ void rhs_primal(const Agent a, double mu, double obj_sca
       }
       const int b = (i - NX) / NP, off = (i - NX) % NP;
       a.rhs(b)[off] = r;
-      a.lp(b)[pko(RB) + (off < NV ? off : NI + NX + off - NV)] = r;
+      a.lp(b)[pko(RB) + (off < NV ? off : LX1 + off - NV)] = r;
     }
   }
 }
@@ -1609,7 +1650,7 @@ __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw) {
         }
       }
       a.rhs(c / NG)[NP + c % NG] = rr;
-      a.lp(c / NG)[pko(RB) + NV + c % NG] = rr;
+      a.lp(c / NG)[pko(RB) + crow(c % NG)] = rr;
     }
   }
   sync();

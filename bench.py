@@ -271,7 +271,10 @@ def mhe_bench(args, world, rank, dev):
         "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
         "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
         "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
-        "factorisation": "sequential block chain (forced, DESIGN 6a)",
+        "factorisation": "stage-parallel, continuity rows bordered into the chain (DESIGN 2.1)"
+                         if prob.gen.bordered_rows else "stage-parallel",
+        "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
+                                      max(1, np.sum([s["n_factorizations"] for s in stats]))),
         "kernel_ms": kernel_ms,
     }
 

@@ -54,8 +54,7 @@ def _cuda():
     ("room_nn", {}),
     ("room_nn", {"T_air": 296.5, "load": 180.0, "Q_rad": 150.0, "q_T": 1.0,
                  "zbar": [296.0, 293.0, 295.0, 296.0], "lam": [0.5, -0.2, 0.1, 0.0]}),
-    # N=23 has no super-stage length dividing it: copy-lifted stages whose interiors
-    # are singular, i.e. the sequential block-chain fallback of the kernel
+    # N=23 has no super-stage length dividing it: copy-lifted stages (shift rows bordered)
     ("room_nn", {"N": 23}),
     ("exchange_room_rk", {}),          # multiple shooting with the "rk" integrator
     ("one_room_radau", {}),            # Radau IIA collocation, d=3
@@ -69,7 +68,7 @@ def _cuda():
     ("mhe_room", {"theta": 7.0}),      # true value outside the bounds: estimate at ub
     ("mhe_room_u", {}),                # estimated input per interval, no global parameter
     ("mhe_room_u", {"noise": 0.05, "seed": 4}),
-    # two states, one control (nx > nu): block-chain factorisation
+    # two states, one control (nx > nu): continuity rows bordered into the chain
     ("rng_room_mpc", {}),
     ("rng_room_mpc", {"T0": 27.0, "T_upper": 22.0, "load": 300.0}),
     ("rng_room_mpc", {"T0": 23.5, "T_upper": 24.5, "load": 50.0, "u_prev": 0.0}),
@@ -158,11 +157,26 @@ def test_acceptable_stop_occurs_at_reference_defaults():
     assert r.stats["return_status"] == "Solved_To_Acceptable_Level" and r.stats["success"], r.stats
 
 
-def test_copy_lifted_narx_uses_block_chain():
+@pytest.mark.parametrize("name,kw", [("rng_room_mpc", {}), ("one_room_du", {}), ("mhe_room", {}),
+                                     ("mhe_room_u", {})])
+def test_more_states_than_inputs_stay_stage_parallel(name, kw):
+    """nx > nu structures (2-state zone, carried previous control, MHE lifts): the
+    continuity rows are bordered into the state chain, so no factorisation falls back to
+    the sequential block chain."""
+    case = configs.CASES[name](**kw)
+    assert case.backend.problem.gen.bordered_rows and not case.backend.problem.gen.block_chain_only
+    r = case.backend.solve(0.0, case.current_vars)
+    assert r.stats["success"] and r.stats["n_block_chain"] == 0, r.stats
+
+
+def test_copy_lifted_narx_is_stage_parallel():
+    """N=23 NARX (no super-stage length divides N): copy-lifted lag windows with shift
+    rows; the shift/continuity rows are bordered, so no block-chain fallback."""
     case = configs.room_nn(N=23)
     assert case.backend.problem.nlp.lift.w_dup.any()
+    assert case.backend.problem.gen.bordered_rows
     r = case.backend.solve(0.0, case.current_vars)
-    assert r.stats["success"] and r.stats["n_block_chain"] > 0, r.stats
+    assert r.stats["success"] and r.stats["n_block_chain"] == 0, r.stats
 
 
 def _w_of(case, results):

@@ -269,39 +269,21 @@ def fleet_nlp_inputs(prob: CompiledProblem, template_vars: dict, overrides: Dict
     """
     n = len(next(iter(overrides.values())))
     mi = prob.mpc_inputs(template_vars, now)
-    batched = {k: np.repeat(v[None], n, axis=0) for k, v in mi.items()}
+    m = prob.marshal
+    pars = {}
     for par in prob.system.parameters:
-        for i, name in enumerate(par.full_names):
-            if name in overrides and name in par.ref_names:
-                batched[par.name][:, i, :] = np.asarray(overrides[name], float)[:, None]
-    nlp = prob.nlp
-    p = np.empty((n, nlp.npar))
-    for name, lay in nlp.par_groups.items():
-        if lay.dim:
-            p[:, lay.index] = batched[name]
-    lbw = np.empty((n, nlp.nw))
-    ubw = np.empty((n, nlp.nw))
-    w0 = np.empty((n, nlp.nw))
-    for name, lay in nlp.var_groups.items():
-        if not lay.dim:
-            continue
-        idx = lay.index
-        lb, ub = batched[f"lb_{name}"], batched[f"ub_{name}"]
-        lbw[:, idx] = lb
-        ubw[:, idx] = ub
-        key = f"initial_{name}"
-        if key in batched:
-            meas = batched[key][:, :, -1:]
-            guess = np.repeat(meas, len(lay.grid), axis=2)
-        else:
-            with np.errstate(invalid="ignore"):
-                guess = np.nan_to_num(0.5 * (lb + ub), posinf=0, neginf=-0)
-        w0[:, idx] = guess
-    for key, arr in (("lb", lbw), ("ub", ubw), ("guess", w0)):
-        cols, pars = prob.marshal.over[key]
-        if cols.size:
-            arr[:, cols] = p[:, pars]
-    return p, lbw, ubw, w0
+        mat = np.broadcast_to(mi[par.name][None], (n,) + mi[par.name].shape)
+        hit = [(i, name) for i, name in enumerate(par.full_names) if name in overrides and name in par.ref_names]
+        if hit:
+            mat = mat.copy()
+            for i, name in hit:
+                mat[:, i, :] = np.asarray(overrides[name], float)[:, None]
+        pars[par.name] = mat
+    lbs = {v.name: np.broadcast_to(mi[f"lb_{v.name}"][None], (n,) + mi[f"lb_{v.name}"].shape)
+           for v in prob.system.variables}
+    ubs = {v.name: np.broadcast_to(mi[f"ub_{v.name}"][None], (n,) + mi[f"ub_{v.name}"].shape)
+           for v in prob.system.variables}
+    return m.assemble(n, pars, lbs, ubs)
 
 
 # ---------------------------------------------------------------------------
@@ -359,6 +341,7 @@ class BatchMarshal:
             key = f"initial_{name}"
             if lay.dim and key in nlp.par_groups and nlp.par_groups[key].dim:
                 self.initial[name] = nlp.par_groups[key].index
+        self._work = {}
         # result matrix scatter plan
         lay = prob.layout
         self.n_rows, self.n_cols = len(lay.full_grid), len(lay.columns)
@@ -400,10 +383,7 @@ class BatchMarshal:
         NaN = no previous optimum) is the warm start (`core/discretization.py:212-251`).
         ``return_sampled_bounds``: also the sampled bounds before the parameter overrides
         (what the result matrix's lower/upper columns show)."""
-        nlp = self.prob.nlp
         n = len(batch_vars)
-        p = np.full((n, nlp.npar), np.nan)
-        groups = {}
         cache = {}
 
         def gather(ref):
@@ -417,6 +397,7 @@ class BatchMarshal:
                 cache[ref] = (vs, vals, lbs, ubs)
             return cache[ref]
 
+        pars = {}
         for name, grid, rows, index in self.pars:
             mat = np.empty((n, len(rows), len(grid)))
             for i, ref, default in rows:
@@ -431,12 +412,8 @@ class BatchMarshal:
                         f"The variable {ref} does not have an interpolationmethod. All Variables "
                         "used in MPC need to be of type MPCVariable (subclass of AgentVariable).")
                 mat[:, i, :] = self._column(vals, grid, now, lambda a: vs[a].interpolation_method)
-            groups[name] = mat
-            if index is not None:
-                p[:, index] = mat
-        lbw = np.full((n, nlp.nw), np.nan)
-        ubw = np.full((n, nlp.nw), np.nan)
-        w0 = np.zeros((n, nlp.nw))
+            pars[name] = mat
+        lbs, ubs = {}, {}
         for name, grid, rows, index in self.vars:
             lb = np.empty((n, len(rows), len(grid)))
             ub = np.empty((n, len(rows), len(grid)))
@@ -444,34 +421,58 @@ class BatchMarshal:
                 if ref is None:
                     lb[:, i, :], ub[:, i, :] = dlb, dub
                     continue
-                vs, _, lbs, ubs = gather(ref)
+                vs, _, lbv, ubv = gather(ref)
                 meth = lambda a: getattr(vs[a], "interpolation_method", "linear")  # noqa: E731
-                ub[:, i, :] = self._column(ubs, grid, now, meth)
-                lb[:, i, :] = self._column(lbs, grid, now, meth)
+                ub[:, i, :] = self._column(ubv, grid, now, meth)
+                lb[:, i, :] = self._column(lbv, grid, now, meth)
+            lbs[name], ubs[name] = lb, ub
+        return self.assemble(n, pars, lbs, ubs, w_prev, return_sampled_bounds)
+
+    def assemble(self, n, pars, lbs, ubs, w_prev=None, return_sampled_bounds=False):
+        """NLP input arrays from the group matrices ([n, dim, len(grid)] per group), built
+        in transposed form (every group row is a contiguous copy of n values)."""
+        nlp = self.prob.nlp
+        work = self._work.get(n)
+        if work is None:  # transposed work buffers, reused (no page faults per call)
+            work = self._work[n] = tuple(np.empty((m, n)) for m in (nlp.npar, nlp.nw, nlp.nw, nlp.nw))
+        pT, lT, uT, gT = work
+        pT.fill(np.nan)
+        lT.fill(np.nan)
+        uT.fill(np.nan)
+        gT.fill(0.0)
+        for name, grid, rows, index in self.pars:
+            if index is not None:
+                pT[index.ravel()] = pars[name].reshape(n, -1).T
+        for name, grid, rows, index in self.vars:
             if index is None:
                 continue
-            lbw[:, index] = lb
-            ubw[:, index] = ub
+            flat = index.ravel()
+            lb, ub = lbs[name], ubs[name]
+            lT[flat] = lb.reshape(n, -1).T
+            uT[flat] = ub.reshape(n, -1).T
             if name in self.initial:
-                meas = p[:, self.initial[name]][:, :, -1:]
-                guess = np.repeat(meas, len(grid), axis=2)
+                ii = self.initial[name]                          # [dim, G_init] in p
+                meas = pT[ii[:, -1]]                             # [dim, n]
+                gT[flat] = np.repeat(meas[:, None, :], len(grid), axis=1).reshape(-1, n)
             else:
                 with np.errstate(invalid="ignore"):
-                    guess = np.nan_to_num(0.5 * (lb + ub), posinf=0, neginf=-0)
-            w0[:, index] = guess
+                    mid = np.nan_to_num(0.5 * (lb + ub), posinf=0, neginf=-0)
+                gT[flat] = mid.reshape(n, -1).T
         if w_prev is not None:
             have = ~np.isnan(w_prev).any(axis=1)
-            w0[have] = w_prev[have]
-        sampled = (lbw.copy(), ubw.copy()) if return_sampled_bounds else None
-        for key, arr in (("lb", lbw), ("ub", ubw), ("guess", w0)):
-            cols, pars = self.over[key]
+            gT[:, have] = w_prev[have].T
+        sampled = (np.ascontiguousarray(lT.T), np.ascontiguousarray(uT.T)) if return_sampled_bounds else None
+        for key, arr in (("lb", lT), ("ub", uT), ("guess", gT)):
+            cols, prs = self.over[key]
             if cols.size:
-                arr[:, cols] = p[:, pars]
-        if np.isnan(p).any() or np.isnan(lbw).any() or np.isnan(ubw).any():
+                arr[cols] = pT[prs]
+        if np.isnan(pT).any() or np.isnan(lT).any() or np.isnan(uT).any():
             raise ValueError("incomplete NLP inputs (NaN in parameters or bounds)")
+        p, lbw, ubw = (np.ascontiguousarray(a.T) for a in (pT, lT, uT))
+        w0 = np.ascontiguousarray(np.nan_to_num(gT).T)
         if return_sampled_bounds:
-            return p, lbw, ubw, np.nan_to_num(w0), sampled
-        return p, lbw, ubw, np.nan_to_num(w0)
+            return p, lbw, ubw, w0, sampled
+        return p, lbw, ubw, w0
 
     def result_matrices(self, p, lbw, ubw, w) -> np.ndarray:
         """[n, len(full grid), n_columns] result matrices from the NLP vectors (``lbw`` /

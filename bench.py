@@ -166,7 +166,15 @@ def admm_bench(args, world, rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         t[0] = w[0]
     wall, ok = float(t[0]), float(t[1])
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        ns = min(n, 2048)
+        sample = bm.c4_fleet_classes(n_rooms=ns - ns // 5, n_supply=ns // 5, N=10, seed=20261015 + 4,
+                                     solver_options=opts)
+        cpu = admm_cpu_baseline(sample, lambda fl: fl.run_local(1e4, max_iterations=args.admm_iters,
+                                                                record_residuals=False), n, "C4 LocalADMM")
     return {
+        "cpu_baseline": cpu,
         "workload": "C4: exchange ADMM (LocalADMM), examples/exchange_admm rooms+supply 4:1, MS-Euler "
                     "N=10 ts=120 rho=1e4, one exchange alias spanning all GPUs",
         "agents_per_gpu": n, "agents_total": n * world, "admm_iterations": args.admm_iters,
@@ -309,11 +317,19 @@ def c2_admm_bench(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sample = bm.c2_fleet_classes(n_blocks=min(nb, 64), N=10, seed=20261015 + 1, solver_options={"ipopt": {}})
+        cpu = admm_cpu_baseline(sample, lambda fl: fl.run_coordinated(0.4, admm_iter_max=40,
+                                                                      use_relative_tolerances=False,
+                                                                      primal_tol=0.002, dual_tol=0.1),
+                                5 * nb, "C2 coordinated, to each block's stopping rule")
     return {
         "workload": "C2 scaled: 4-room + air-handler blocks (casadi_admm collocation d=3, N=10, ts=60), "
                     "coordinated consensus, rho=0.4, abs tol 0.002/0.1, iter max 40, per-block stopping",
         "blocks_per_gpu": nb, "agents_per_gpu": 5 * nb,
         **_block_summary(out, wall, 5),
+        "cpu_baseline": cpu,
     }
 
 
@@ -364,13 +380,58 @@ def c5_admm_bench(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sample = bm.c5_fleet_classes(n_blocks=min(nb, 16), N=24, seed=20261015 + 5, solver_options=opts)
+        cpu = admm_cpu_baseline(sample, lambda fl: fl.run_coordinated(1.0, admm_iter_max=args.c5_iters,
+                                                                      use_relative_tolerances=False,
+                                                                      primal_tol=0.04, dual_tol=0.04),
+                                5 * nb, "C5 coordinated")
     return {
         "workload": "C5: three-zone data-driven ADMM (3 NARX zones + AHU + CCA per block), coordinated "
                     "consensus, rho=1, N=24 ts=1800, abs tol 0.04/0.04, per-block stopping",
         "blocks_per_gpu": nb, "zones_per_gpu": 3 * nb, "agents_per_gpu": 5 * nb,
         **_block_summary(out, wall, 5),
         "solver": "reference IPOPT defaults (casadi_utils.py:197-206)",
+        "cpu_baseline": cpu,
     }
+
+
+def admm_cpu_baseline(classes, run, full_agents, label, min_seconds=8.0):
+    """The same ADMM driver (`admm/fleet.py`) on the host: every class's agents solved by
+    the C IPM restatement over the class's generated model compiled for the host
+    (`oracle/c/gen_model.cpp`, OpenMP over the host cores), the ADMM arithmetic in numpy
+    (`oracle/cpu_fleet.py`).  Run on a bounded sample fleet (``classes``) and scaled to the
+    per-GPU fleet by the agent ratio (the solves dominate and scale linearly)."""
+    from agentlib_mpc_amd.admm.fleet import ADMMFleet
+    from oracle.cpu_fleet import CpuFleetOps
+
+    ops = CpuFleetOps(ipopt=dict(solver_settings_ns.oracle))
+    fleet = ADMMFleet(classes, device="cpu", ops=ops)
+    n_sample = sum(c.n for c in classes)
+    t0 = time.perf_counter()
+    iters = 0
+    rounds = 0
+    while rounds == 0 or time.perf_counter() - t0 < min_seconds:
+        out = run(fleet)
+        iters += out["iterations"]
+        rounds += 1
+        if rounds >= 20:
+            break
+    dt = time.perf_counter() - t0
+    per_s = iters / dt
+    return {"value": per_s * n_sample / full_agents, "unit": "ADMM iters/s (per-GPU fleet, projected)",
+            "cores": ops.threads, "kind": "port",
+            "sample": f"{label}: {rounds} round(s), {iters} ADMM iterations over a {n_sample}-agent sample fleet in "
+                      f"{dt:.1f} s ({per_s:.2f} it/s), x {n_sample}/{full_agents} agents; solves by "
+                      f"oracle/c/ipm_oracle.c on host-compiled generated models, same IPOPT settings"}
+
+
+class _SolverNS:
+    oracle: dict = {}
+
+
+solver_settings_ns = _SolverNS()
 
 
 def e2e_bench(args, world, rank, dev):
@@ -533,6 +594,7 @@ def main():
     from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
 
     solver_opts, oracle_opts = solver_settings(args)
+    solver_settings_ns.oracle = oracle_opts
     be, cv = bm.one_room(solver_options=solver_opts)
     prob = be.problem
     n = args.agents

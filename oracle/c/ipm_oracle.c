@@ -2,6 +2,12 @@
  * stage-structured MPC NLPs, used as the all-cores CPU baseline
  * and cross-checked against oracle/ipm.py.
  *
+ * The IPM is generic over a stage-model interface (model_t: dimensions + stage
+ * functions).  Two models plug into it: the hand-derived one_room model below (the
+ * independent checker of the C3 fleet), and, for the CPU baselines of the other
+ * configurations, a generated model compiled for the host (oracle/c/gen_model.cpp,
+ * oracle/cbuild.py: build_generated) — the CasADi-codegen + IPOPT analogue.
+ *
  * Algorithm: IPOPT (Waechter & Biegler 2006) exactly as oracle/ipm.py restates it
  * (reference solver call: agentlib_mpc/data_structures/casadi_utils.py:191-217,
  * optimization_backends/casadi_/core/discretization.py:203).  The KKT system is
@@ -22,8 +28,11 @@
 #include <omp.h>
 #endif
 
+#include "ipm_oracle.h"
+
 #define MAXD 9
-#define MAXNB 64
+#define MAXNB 96
+#define MAXNX 8
 
 /* --------------------------------------------------------------------------
  * one_room collocation stage (d collocation points)
@@ -112,6 +121,26 @@ static void room_hess(const room_t* m, const double* L, const double* PS, const 
   }
 }
 
+static void room_fg_m(const model_t* mm, const double* L, const double* PS, const double* PG, double TK, double* f,
+                      double* g) {
+  (void)TK;
+  room_fg((const room_t*)mm->data, L, PS, PG, f, g);
+}
+static void room_gj_m(const model_t* mm, const double* L, const double* PS, const double* PG, double TK, double* grad,
+                      double* jac) {
+  (void)TK;
+  room_gj((const room_t*)mm->data, L, PS, PG, grad, jac);
+}
+static void room_hess_m(const model_t* mm, const double* L, const double* PS, const double* PG, double TK,
+                        double sigma, const double* lam, double* H) {
+  (void)TK;
+  room_hess((const room_t*)mm->data, L, PS, PG, sigma, lam, H);
+}
+static void room_bounds_m(const model_t* mm, const double* PS, const double* PG, double TK, double* lb, double* ub) {
+  (void)PG; (void)TK;
+  room_bounds((const room_t*)mm->data, PS, lb, ub);
+}
+
 void oracle_room_init(room_t* m, int N, int d, double ts, const double* B, const double* Cm,
                       const double* D) {
   m->N = N; m->d = d; m->nx = 1; m->nv = 1 + 3 * d; m->ng = 1 + 3 * d;
@@ -126,21 +155,6 @@ void oracle_room_init(room_t* m, int N, int d, double ts, const double* B, const
 /* --------------------------------------------------------------------------
  * IPM
  * -------------------------------------------------------------------------- */
-/* IPOPT termination options (OptimalityErrorConvergenceCheck); the reference sets
-   tol 1e-4, max_iter 100, acceptable_tol 0.1, acceptable_iter 5,
-   acceptable_constr_viol_tol 1, acceptable_compl_inf_tol 1 (casadi_utils.py:197-206) */
-typedef struct {
-  double tol, dual_inf_tol, constr_viol_tol, compl_inf_tol;
-  double acceptable_tol, acceptable_dual_inf_tol, acceptable_constr_viol_tol;
-  double acceptable_compl_inf_tol, acceptable_obj_change_tol;
-  int max_iter, acceptable_iter;
-} opts_t;
-
-typedef struct {
-  double obj;
-  int iter, status, n_fact, n_trials;
-} ostats_t;
-
 typedef struct {
   int pos, neg, zero;
 } inertia_t;
@@ -251,7 +265,7 @@ static void bk_solve(const double* F, int n, int ld, const int* perm, const int*
 
 /* per-agent solver state */
 typedef struct {
-  const room_t* m;
+  const model_t* m;
   int N, NX, NV, NG, NL, NP, NB, NW, M;
   const double *p;
   double *x, *s, *lam, *zL, *zU, *vL, *vU, *xL, *xU, *sL, *sU, *gs, *gv, *lb, *ub;
@@ -266,23 +280,26 @@ static int isfin(double v) { return fabs(v) < INFINITY; }
 static double eval_fg(ws_t* w, const double* xv, double* gout) {
   double f = 0.0;
   for (int k = 0; k < w->N; ++k) {
-    double fk;
-    room_fg(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, &fk, gout + k * w->NG);
+    double fk = 0.0;
+    w->m->fg(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, k * w->m->ts, &fk, gout + k * w->NG);
     f += fk;
   }
   return f;
 }
 static void eval_gj(ws_t* w, const double* xv) {
+  memset(w->sdg, 0, sizeof(double) * w->N * w->NL);
+  memset(w->sdj, 0, sizeof(double) * w->N * w->NG * w->NL);
   for (int k = 0; k < w->N; ++k)
-    room_gj(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, w->sdg + k * w->NL,
-            w->sdj + k * w->NG * w->NL);
+    w->m->gj(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, k * w->m->ts, w->sdg + k * w->NL,
+             w->sdj + k * w->NG * w->NL);
 }
 static void eval_hess(ws_t* w, const double* xv, double sigma) {
   double lk[MAXNB];
+  memset(w->sdh, 0, sizeof(double) * w->N * w->NL * w->NL);
   for (int k = 0; k < w->N; ++k) {
     for (int r = 0; r < w->NG; ++r) lk[r] = w->lam[k * w->NG + r] * w->gs[k * w->NG + r];
-    room_hess(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, sigma, lk,
-              w->sdh + k * w->NL * w->NL);
+    w->m->hess(w->m, xv + k * w->NP, w->p + w->m->npg + k * w->m->nps, w->p, k * w->m->ts, sigma, lk,
+               w->sdh + k * w->NL * w->NL);
   }
 }
 static double acc_grad(const ws_t* w, int i) {
@@ -335,7 +352,7 @@ static double coupling(const ws_t* w, int k, int row, int c, int lsq) {
 static inertia_t factor_chain(ws_t* w, double dw, double dc, int lsq) {
   const int NB = w->NB, NP = w->NP, NV = w->NV, NX = w->NX, NG = w->NG, NL = w->NL, N = w->N;
   inertia_t in = {0, 0, 0};
-  double P[16], Bm[MAXNB * 4], v[MAXNB];
+  double P[MAXNX * MAXNX], Bm[MAXNB * MAXNX], v[MAXNB];
   for (int k = 0; k < N; ++k) {
     double* A = w->fac + k * NB * NB;
     const int w0 = NX + k * NP;
@@ -497,7 +514,7 @@ static double push_into(double v, double lo, double hi) {
   return fmin(fmax(v, lop), hip);
 }
 
-static void solve_one(const room_t* m, const double* p, const double* lbw, const double* ubw,
+static void solve_one(const model_t* m, const double* p, const double* lbw, const double* ubw,
                       double* wio, const opts_t* o, ostats_t* st, double* mem, int* imem) {
   ws_t W;
   ws_t* w = &W;
@@ -521,7 +538,7 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
     if (i < NX) hi = lo;
     w->xL[i] = lo; w->xU[i] = hi; w->x[i] = lo == hi ? lo : wio[i];
   }
-  for (int k = 0; k < N; ++k) room_bounds(m, p + m->npg + k * m->nps, w->lb + k * NG, w->ub + k * NG);
+  for (int k = 0; k < N; ++k) m->bounds(m, p + m->npg + k * m->nps, p, k * m->ts, w->lb + k * NG, w->ub + k * NG);
   eval_gj(w, w->x);
   double gmax = 0.0;
   for (int i = NX; i < NW; ++i) if (!fixedv(w, i)) gmax = fmax(gmax, fabs(acc_grad(w, i)));
@@ -788,11 +805,10 @@ static void solve_one(const room_t* m, const double* p, const double* lbw, const
   st->n_trials = n_trials;
 }
 
-/* Solve n_agents one_room NLPs (agent-major arrays); returns #converged (success flag:
-   Solve_Succeeded or Solved_To_Acceptable_Level). */
-int oracle_room_solve_fleet(const room_t* m, int n_agents, const double* p, const double* lbw,
-                            const double* ubw, double* w_io, ostats_t* stats, const opts_t* opts,
-                            int threads) {
+/* Solve n_agents NLPs of one stage model (agent-major arrays); returns #converged
+   (success flag: Solve_Succeeded or Solved_To_Acceptable_Level). */
+int oracle_solve_fleet(const model_t* m, int n_agents, const double* p, const double* lbw, const double* ubw,
+                       double* w_io, ostats_t* stats, const opts_t* opts, int threads) {
   const opts_t o = *opts;
   const int NW = m->nx + m->N * (m->nv + m->nx), NPAR = m->npg + m->N * m->nps;
   const int NB = m->nv + m->nx + m->ng, NL = 2 * m->nx + m->nv, M = m->N * m->ng;
@@ -815,6 +831,15 @@ int oracle_room_solve_fleet(const room_t* m, int n_agents, const double* p, cons
     free(imem);
   }
   return ok;
+}
+
+/* the hand-derived one_room model (the C3 checker) */
+int oracle_room_solve_fleet(const room_t* rm, int n_agents, const double* p, const double* lbw,
+                            const double* ubw, double* w_io, ostats_t* stats, const opts_t* opts,
+                            int threads) {
+  model_t m = {rm->N, rm->nx, rm->nv, rm->ng, rm->nps, rm->npg, rm->ts,
+               room_fg_m, room_gj_m, room_hess_m, room_bounds_m, rm};
+  return oracle_solve_fleet(&m, n_agents, p, lbw, ubw, w_io, stats, opts, threads);
 }
 
 int oracle_room_sizeof(void) { return (int)sizeof(room_t); }

@@ -50,9 +50,13 @@ class OStats(ctypes.Structure):
     _fields_ = [("obj", ctypes.c_double)] + [(n, ctypes.c_int) for n in ("iter", "status", "n_fact", "n_trials")]
 
 
+HDR = HERE / "c" / "ipm_oracle.h"
+GEN_SRC = HERE / "c" / "gen_model.cpp"
+
+
 def build(force: bool = False, march: str = "native") -> pathlib.Path:
     OUT.parent.mkdir(parents=True, exist_ok=True)
-    if OUT.exists() and not force and OUT.stat().st_mtime >= SRC.stat().st_mtime:
+    if OUT.exists() and not force and OUT.stat().st_mtime >= max(SRC.stat().st_mtime, HDR.stat().st_mtime):
         return OUT
     cmd = ["gcc", "-O3", f"-march={march}", "-fopenmp", "-shared", "-fPIC", "-std=c11", str(SRC),
            "-o", str(OUT) + ".tmp", "-lm"]
@@ -109,6 +113,70 @@ def solve_room_fleet(p, lbw, ubw, w0, N=15, d=2, tol=1e-8, max_iter=500, threads
     st = (OStats * n)()
     ok = lib().oracle_room_solve_fleet(ctypes.byref(m), n, p.ctypes.data, lbw.ctypes.data, ubw.ctypes.data,
                                        w.ctypes.data, st, ctypes.byref(opts), threads)
+    stats = [{"obj": s.obj, "iter": s.iter, "status": s.status, "n_fact": s.n_fact, "n_trials": s.n_trials}
+             for s in st]
+    return w, stats, ok
+
+
+# ---------------------------------------------------------------------------
+# generated stage models on the host (CPU baselines of C2 / C4 / C5, bench.py)
+# ---------------------------------------------------------------------------
+_gen_libs = {}
+
+
+def build_generated(gen, march: str = "native") -> pathlib.Path:
+    """Compile the C IPM with one generated model (``codegen.GeneratedModel``) for the host:
+    the generated stage functions with the HIP qualifiers defined away (no kernel code)."""
+    import hashlib
+
+    key = hashlib.sha1((gen.source + SRC.read_text() + HDR.read_text() + GEN_SRC.read_text()).encode()).hexdigest()[:12]
+    out = OUT.parent / f"libgen_{key}.so"
+    if out.exists():
+        return out
+    OUT.parent.mkdir(parents=True, exist_ok=True)
+    body = [ln for ln in gen.source.splitlines()
+            if not ln.startswith("#include <hip/") and not ln.startswith('#include "mpcx_ipm.hip"')]
+    src = OUT.parent / f"gen_{key}.inc"
+    src.write_text("\n".join(body) + "\n")
+    core_o = OUT.parent / f"core_{key}.o"
+    model_o = OUT.parent / f"model_{key}.o"
+    for cmd in (["gcc", "-O3", f"-march={march}", "-fopenmp", "-fPIC", "-std=c11", "-c", str(SRC), "-o", str(core_o)],
+                ["g++", "-O3", f"-march={march}", "-fopenmp", "-fPIC", "-std=c++17", f"-I{HERE / 'c'}",
+                 f'-DMPCX_GEN_SOURCE="{src}"', "-c", str(GEN_SRC), "-o", str(model_o)],
+                ["g++", "-shared", "-fopenmp", str(core_o), str(model_o), "-o", str(out) + ".tmp", "-lm"]):
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            if march == "native":
+                return build_generated(gen, march="x86-64-v2")
+            raise RuntimeError(res.stderr[-4000:])
+    os.replace(str(out) + ".tmp", out)
+    return out
+
+
+def _gen_lib(gen):
+    path = build_generated(gen)
+    if path not in _gen_libs:
+        lib = ctypes.CDLL(str(path))
+        vp = ctypes.c_void_p
+        lib.oracle_gen_solve_fleet.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.POINTER(OStats),
+                                               ctypes.POINTER(OOpts), ctypes.c_int]
+        lib.oracle_gen_solve_fleet.restype = ctypes.c_int
+        _gen_libs[path] = lib
+    return _gen_libs[path]
+
+
+def solve_generated_fleet(gen, p, lbw, ubw, w0, threads=0, tol=1e-8, max_iter=500, **ipopt):
+    """Solve kernel-layout NLP inputs [n, .] of one generated model on the host cores.
+    Returns (w, stats list of dicts, n_succeeded)."""
+    p = np.ascontiguousarray(p, dtype=np.float64)
+    lbw = np.ascontiguousarray(lbw, dtype=np.float64)
+    ubw = np.ascontiguousarray(ubw, dtype=np.float64)
+    w = np.array(w0, dtype=np.float64, order="C", copy=True)
+    n = p.shape[0]
+    st = (OStats * n)()
+    opts = options(tol=tol, max_iter=max_iter, **ipopt)
+    ok = _gen_lib(gen).oracle_gen_solve_fleet(n, p.ctypes.data, lbw.ctypes.data, ubw.ctypes.data, w.ctypes.data,
+                                              st, ctypes.byref(opts), threads)
     stats = [{"obj": s.obj, "iter": s.iter, "status": s.status, "n_fact": s.n_fact, "n_trials": s.n_trials}
              for s in st]
     return w, stats, ok

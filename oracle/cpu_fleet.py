@@ -1,0 +1,142 @@
+"""ORACLE (test infrastructure only) — the fleet driver's device interface on the CPU.
+
+``CpuFleetOps`` restates every ADMM kernel of `agentlib-mpc_amd/csrc/admm_kernels.hip` in
+numpy (moments, finalize with per-block totals, multiplier / diff updates, shifts, row
+moves) and solves each class's agents with the C IPM restatement over the class's
+generated model compiled for the host (`oracle/c/gen_model.cpp`, OpenMP over the host
+cores).  With it, :class:`agentlib_mpc_amd.admm.fleet.ADMMFleet` runs unchanged on the
+CPU: the CPU baseline of the ADMM legs in bench.py.  ``tests/cpu_admm_ops.py`` reuses the
+arithmetic with the numpy oracle IPM for the CPU tests of the driver.
+"""
+
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+NMOM = 5
+TOTALS = 8
+STATUS_WORD = 13   # int32 index of mpcx_stats.status
+
+
+class CpuFleetOps:
+    """ADMM arithmetic in numpy; ``solve`` through the host build of the generated model."""
+
+    def __init__(self, ipopt: dict = None, threads: int = 0):
+        self.ipopt = dict(ipopt or {"tol": 1e-8, "max_iter": 500, "acceptable_iter": 0})
+        self.threads = threads or int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+
+    def solve(self, cls, active=None):
+        from oracle import cbuild
+
+        P, LB, UB, W = (t.numpy() for t in (cls.P, cls.LB, cls.UB, cls.W))
+        st = cls.ST.view(torch.int32).view(cls.n, -1).numpy()
+        act = np.ones(cls.n, bool) if active is None else active.numpy() != 0
+        idx = np.flatnonzero(act)
+        if idx.size == 0:
+            return
+        opts = dict(self.ipopt)
+        tol, mi = opts.pop("tol"), opts.pop("max_iter")
+        w, stats, _ = cbuild.solve_generated_fleet(cls.backend.problem.gen, P[idx], LB[idx], UB[idx], W[idx],
+                                                   threads=self.threads, tol=tol, max_iter=mi, **opts)
+        W[idx] = w
+        st[idx, STATUS_WORD] = [s["status"] for s in stats]
+
+    def gather_rows(self, T, src, cols, dst, dst_rows):
+        dst.numpy()[dst_rows.numpy()] = src.numpy()[:, cols.numpy()]
+
+    def scatter_rows(self, T, src, src_rows, dst, cols):
+        s = src.numpy()
+        rows = np.arange(dst.shape[0]) if src_rows is None else src_rows.numpy()
+        d = dst.numpy()
+        d[:, cols.numpy()] = s[rows]
+
+    def fill_column(self, dst, col, value):
+        dst.numpy()[:, col] = value
+
+    def moments_size(self, n_groups, n_blocks, T):
+        return n_groups * (NMOM * T + 1) + TOTALS * n_blocks
+
+    @staticmethod
+    def _off(g, n_global, n_blocks, T):
+        return g * (NMOM * T + 1) + (TOTALS * n_blocks if g >= n_global else 0)
+
+    def moments(self, n_groups, n_global, n_blocks, T, gstart, max_rows, X, LAM, center, out):
+        gs, x, c, o = gstart.numpy(), X.numpy(), center.numpy(), out.numpy()
+        lam = None if LAM is None else LAM.numpy()
+        for g in range(n_groups):
+            r0, r1 = gs[g], gs[g + 1]
+            if r1 <= r0:
+                continue
+            b = self._off(g, n_global, n_blocks, T)
+            d = x[r0:r1] - c[g]
+            o[b:b + T] += d.sum(0)
+            o[b + T:b + 2 * T] += (d * d).sum(0)
+            if lam is not None:
+                l = lam[r0:r1]
+                o[b + 2 * T:b + 3 * T] += l.sum(0)
+                o[b + 3 * T:b + 4 * T] += (l * l).sum(0)
+                o[b + 4 * T:b + 5 * T] += (l * d).sum(0)
+            o[b + NMOM * T] += r1 - r0
+
+    @staticmethod
+    def _g(rho, rho_g, active_g, g):
+        on = active_g is None or active_g.numpy()[g] != 0
+        return on, (rho if rho_g is None else float(rho_g.numpy()[g]))
+
+    def finalize(self, g0, g1, n_global, n_blocks, T, mom, exchange, gmult, rho_s, rho_g, active_g, block_g,
+                 mean, dmean, totals):
+        o, m, dm, tot_all = mom.numpy(), mean.numpy(), dmean.numpy(), totals.numpy().reshape(-1)
+        ex = None if exchange is None else exchange.numpy()
+        gm = None if gmult is None else gmult.numpy()
+        for g in range(g0, g1):
+            on, rho = self._g(rho_s, rho_g, active_g, g)
+            if not on:
+                continue
+            b = self._off(g, n_global, n_blocks, T)
+            n = o[b + NMOM * T]
+            if n <= 0:
+                continue
+            s1, s2 = o[b:b + T], o[b + T:b + 2 * T]
+            c = m[g].copy()
+            d = s1 / n
+            new = c + d
+            var = np.maximum(s2 - s1 * d, 0.0)
+            m[g] = new
+            dm[g] = c - new
+            is_ex = ex is not None and ex[g]
+            prim = (new * new).sum() if is_ex else var.sum()
+            if is_ex:
+                ls = ((gm[g] + rho * new) ** 2).sum()
+            else:
+                sl, sl2, slx = o[b + 2 * T:b + 3 * T], o[b + 3 * T:b + 4 * T], o[b + 4 * T:b + 5 * T]
+                ls = (sl2 + 2 * rho * (slx - d * sl) + rho * rho * var).sum()
+            k = 0 if block_g is None else int(block_g.numpy()[g])
+            tot_all[k * TOTALS:(k + 1) * TOTALS] += [
+                prim, ((rho * (c - new)) ** 2).sum(), (s2 + 2 * c * s1 + n * c * c).sum(),
+                (new * new).sum(), ls, n, T if is_ex else n, 1.0]
+
+    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho_s, rho_g, active_g, LAM):
+        gs, x, m, lam = gstart.numpy(), X.numpy(), mean.numpy(), LAM.numpy()
+        for g in range(n_groups):
+            on, rho = self._g(rho_s, rho_g, active_g, g)
+            if on:
+                lam[gs[g]:gs[g + 1]] -= rho * (m[g] - x[gs[g]:gs[g + 1]])
+
+    def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, update, rho_s, rho_g,
+                        active_g):
+        gs, x, m, df = gstart.numpy(), X.numpy(), mean.numpy(), diff.numpy()
+        for g in range(n_groups):
+            on, rho = self._g(rho_s, rho_g, active_g, g)
+            if not on:
+                continue
+            df[gs[g]:gs[g + 1]] = x[gs[g]:gs[g + 1]] - m[g]
+            if update:
+                gmult.numpy()[g] += rho * m[g]
+
+    def shift(self, T, shift, x):
+        a = x.numpy()
+        if shift:
+            a[:, :T - shift] = a[:, shift:].copy()

@@ -110,14 +110,16 @@ def test_result_layout_matches_reference_shape():
     assert len(lay.variable_grid_indices["T"]) == 46  # (d+1)N+1 (test_casadi_backend.py:127-132)
 
 
-def test_rank_deficient_stage_interiors_use_the_block_chain():
-    """Stage interiors whose equality rows V cannot satisfy (more coupled rows than
-    stage variables can absorb) are compiled for the sequential block chain; the
-    benchmark structures keep the stage-parallel elimination."""
-    want = {"one_room": False, "admm_room": False, "exchange_room": False, "room_nn": False,
-            "one_room_radau": False, "one_room_du": True, "exchange_room_rk": False,
-            "mhe_room": True, "mhe_room_u": True, "rng_room_mpc": True}
-    for name, chain in want.items():
+def test_rank_deficient_stage_interiors_border_their_continuity_rows():
+    """Stage interiors whose equality rows V cannot satisfy (more states than free stage
+    inputs: change penalties, MHE lifts, 2-state zones) keep their continuity rows in the
+    border (their multipliers join x_{k+1} in the chain) and stay stage-parallel; the
+    benchmark structures need no bordering; nothing falls back to the block chain."""
+    want = {"one_room": 0, "admm_room": 0, "exchange_room": 0, "room_nn": 0,
+            "one_room_radau": 0, "one_room_du": 2, "exchange_room_rk": 0,
+            "mhe_room": 3, "mhe_room_u": 2, "rng_room_mpc": 2}
+    for name, n_bordered in want.items():
         gen = configs.CASES[name]().backend.problem.gen
-        assert gen.block_chain_only == chain, name
-        assert ("#define MPCX_FORCE_BLOCK_CHAIN 1" in gen.source) == chain, name
+        assert len(gen.bordered_rows) == n_bordered, name
+        assert not gen.block_chain_only and "MPCX_FORCE_BLOCK_CHAIN" not in gen.source, name
+        assert ("#define MPCX_NMU" in gen.source) == bool(n_bordered), name

@@ -20,20 +20,23 @@ def main():
     from agentlib_mpc_amd.runtime.native import NativeProblem
     import bench
     model = os.environ.get("MODEL", "one_room")
-    be, cv = bm.BUILDERS[model](solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
+    from agentlib_mpc_amd.optimization_backends.mi355x import ipopt_options_to_kernel
+    sopts = bm.REFERENCE if os.environ.get("SOLVER", "reference") == "reference" else bm.TIGHT
+    kopts = ipopt_options_to_kernel(sopts)
+    be, cv = bm.BUILDERS[model](solver_options=sopts)
     path = build_profile_hsaco(be.problem.gen)
     if len(sys.argv) > 1 and sys.argv[1] == "build":
         print(path); return
     import torch
     n = int(os.environ.get("AGENTS", "4096"))
     if model == "one_room":
-        vals = bench.fleet_values(n, 20261017)
+        vals = bench.fleet_values(n, 20261015 + 2)
     else:
         first = next(k for q in be.problem.system.parameters for k in q.ref_names if k in cv)
         vals = {first: np.full(n, cv[first].value, float)}
     p, lbw, ubw, w0 = be.problem.to_kernel(*fleet_nlp_inputs(be.problem, cv, vals))
     nat = NativeProblem(be.problem.gen, hsaco=path)
-    nat.set_options(tol=1e-8, max_iter=500)
+    nat.set_options(**kopts)
     nat.reserve(n)
     d = torch.device("cuda")
     T = lambda a: torch.as_tensor(a, device=d).contiguous()
@@ -52,7 +55,7 @@ def main():
     print("profile build: kernel ms", e0.elapsed_time(e1), "mean iters", np.mean([x["iter_count"] for x in stats]),
           "mean fact", np.mean([x["n_factorizations"] for x in stats]))
     plain = NP(be.problem.gen)
-    plain.set_options(tol=1e-8, max_iter=500)
+    plain.set_options(**kopts)
     plain.reserve(n)
     for _ in range(2):
         tw.copy_(tw0); plain.solve(tp, tl, tu, tw, stats=st)

@@ -186,17 +186,35 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         return i * (i + 1) // 2 + j
 
     # -- gradient + jacobian (structural zeros are never written) --
-    gj_assign = [(f"grad[{j} * S]", e) for j, e in enumerate(grad) if not e.is_const(0.0)]
-    gj_assign += [(f"jac[{i * nl + j} * S]", jac[i][j]) for i in range(ng) for j in range(nl)
-                  if not jac[i][j].is_const(0.0)]
+    g_assign = [(f"grad[{j} * S]", e) for j, e in enumerate(grad) if not e.is_const(0.0)]
+    j_assign = [(f"jac[{i * nl + j} * S]", jac[i][j]) for i in range(ng) for j in range(nl)
+                if not jac[i][j].is_const(0.0)]
+    gj_assign = g_assign + j_assign
     gsym = [sx.sym(f"G[{r}]") for r in range(ng)]
+    lmsym = [sx.sym(f"LM[{r}]") for r in range(ng)]
     gb = dict(bind)
     for r, s_ in enumerate(gsym):
         gb[s_] = f"G[{r}]"
+    for r, s_ in enumerate(lmsym):
+        gb[s_] = f"LM[{r}]"
     lp_j = [(f"lp[{pk(crow[i], lidx(j))}]", sx.mul(gsym[i], jac[i][j])) for i in range(ng) for j in range(nl)
             if not jac[i][j].is_const(0.0)]
+    # (J~^T lambda) per stage column, J~ = diag(G) J: the dual-infeasibility and rhs phases
+    # read it coalesced instead of gathering NG jacobian entries per variable
+    glm = [sx.mul(gsym[r], lmsym[r]) for r in range(ng)]
+    jtl_assign = []
+    for j in range(nl):
+        terms = [sx.mul(glm[r], jac[r][j]) for r in range(ng) if not jac[r][j].is_const(0.0)]
+        if terms:
+            jtl_assign.append((f"jtl[{j} * S]", sx.sum1(terms)))
     cg = sx.CodeGen(gb, prefix="c")
-    gj_lines = cg.emit(gj_assign + lp_j)
+    gj_lines = cg.emit(g_assign + j_assign + lp_j + jtl_assign)
+    # the strided jacobian is stored only when requested (scaling, block-chain fallback)
+    nj, ntail = len(j_assign), len(lp_j) + len(jtl_assign)
+    j_store = gj_lines[len(gj_lines) - ntail - nj:len(gj_lines) - ntail]
+    assert all(l.lstrip().startswith("jac[") for l in j_store)
+    gj_lines = (gj_lines[:len(gj_lines) - ntail - nj] + (["  if (full) {"] + j_store + ["  }"] if nj else [])
+                + gj_lines[len(gj_lines) - ntail:])
     # -- hessian: lower triangle, mirrored; once into the packed local system --
     h_assign = []
     lp_h = []
@@ -238,7 +256,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     slot = 8 * pks + 8 * NI_
     soff = nxp * nxp + ncp * ncp + ncp * nxp
     other = 8 * (N_ * soff + N_ * ncp * ncp + N_ * (NX_ + ncp) + N_ * ncp + 3 * ncp * ncp + 64 + nlp.npg
-                 + N_ * nlp.nps + N_) + 8 * ncp + 64
+                 + N_ * nlp.nps + N_) + 8 * ncp + 64 + 336  # 336: KState
     need = other + N_ * slot
     lds_target = 9600 if other + 2 * slot <= 9600 else min(need, 40960)
 
@@ -265,7 +283,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         *fg_lines, "}", "",
         "__device__ __forceinline__ void gen_stage_bounds(const double* __restrict__ PS, const double* __restrict__ PG, const double TK, double* __restrict__ lb, double* __restrict__ ub, const int S) {",
         *bd_lines, "}", "",
-        f"__device__ __forceinline__ void gen_stage_gj({sig}, double* __restrict__ grad, double* __restrict__ jac, const int S, const double* __restrict__ G, double* __restrict__ lp) {{",
+        f"__device__ __forceinline__ void gen_stage_gj({sig}, double* __restrict__ grad, double* __restrict__ jac, const int S, const double* __restrict__ G, double* __restrict__ lp, const double* __restrict__ LM, double* __restrict__ jtl, const int full) {{",
         *gj_lines, "}", "",
         f"__device__ __forceinline__ void gen_stage_hess({sig}, const double sigma, const double* __restrict__ lam, double* __restrict__ hess, const int S, double* __restrict__ lp, const int full) {{",
         *h_lines, "}", "",

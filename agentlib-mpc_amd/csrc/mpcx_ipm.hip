@@ -106,7 +106,8 @@ constexpr long O_VL = O_ZU + NW, O_VU = O_VL + M, O_XL = O_VU + M, O_XU = O_XL +
 constexpr long O_SL = O_XU + NW, O_SU = O_SL + M, O_GS = O_SU + M, O_GV = O_GS + M;
 constexpr long O_DX = O_GV + M, O_DS = O_DX + NW, O_DL = O_DS + M, O_LB = O_DL + M, O_UB = O_LB + M;
 constexpr long O_SDG = O_UB + M;                 // [NL][N]      stage cost gradient
-constexpr long O_SDJ = O_SDG + (long)NL * N;     // [NG*NL][N]   stage jacobian
+constexpr long O_JTL = O_SDG + (long)NL * N;     // [NL][N]      stage (gs*J)^T lambda
+constexpr long O_SDJ = O_JTL + (long)NL * N;     // [NG*NL][N]   stage jacobian (scaling, block chain)
 constexpr long O_SDH = O_SDJ + (long)NG * NL * N;// [NL*NL][N]   stage hessian
 constexpr long O_RHS = O_SDH + (long)NL * NL * N;// [N][NB]      KKT right-hand side
 constexpr long O_TR = O_RHS + (long)N * NB;      // [N][NI][NTR] back-substitution operators
@@ -167,6 +168,15 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// lane id that the compiler can neither hoist nor keep live across calls: non-leaf phase
+// functions recompute lane-derived values after each call instead of parking them in
+// callee-saved VGPRs (saved to scratch on every call)
+__device__ __forceinline__ int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // DPP lane exchange inside aligned groups (quad_perm xor1 / xor2, half-row and
 // row mirrors): register-speed, no LDS round trip
 template <int CTRL>
@@ -217,7 +227,7 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // packed system + perm/piv
 constexpr int OTHER_BYTES = 8 * (N * SOFF + N * NCC + N * (NX + NCP) + N * NCP + 3 * NCC + 2 * MAXF + NPAR + N) +
-                            8 * NCP + 64;
+                            8 * NCP + 64 + 336;  // 336: KState
 #ifndef MPCX_LDS_TARGET
 #define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
 #endif
@@ -261,6 +271,43 @@ union LinLds {
   TrialLds t;           // line-search trial point (x, scaled g)
 };
 
+// per-iteration results kept in LDS across the phase calls
+struct OptErr {
+  double dual, dual_u, primal, viol_u, pmx, pmn, s_d, s_c;
+  int ncompl;
+  __device__ double compl_at(double mu) const { return ncompl > 0 ? fmax(pmx - mu, mu - pmn) : 0.0; }
+  __device__ double err_at(double mu) const { return fmax(fmax(dual / s_d, primal), compl_at(mu) / s_c); }
+};
+
+struct StepInfo {
+  double amax, az, gphid, theta, barrier;
+};
+
+struct Trial {
+  double f, theta, phi;
+};
+
+struct LSResult {
+  Trial tr;
+  double alpha;
+  int accepted, ftype, trials;
+};
+
+struct Acceptable {
+  double curr_f, last_f;
+  int last_it, count;
+};
+
+// kernel loop state (uniform; every lane writes the same values)
+struct KState {
+  OptErr e0;       // optimality error at the current iterate
+  Acceptable acc;  // acceptable-level counter
+  StepInfo st;     // last recovered step
+  LSResult ls;     // last line search
+  double mu, tau, dw_last, fx, obj_scale, theta_max, theta_min, dw, dc, amin, barx;
+  int nfilt, it, status, square, n_fact, n_ic, n_fallback, n_trials, n_chain;
+};
+
 struct Lds {
   LinLds u;
   double par[NPAR];        // agent parameters (read by every evaluation)
@@ -274,12 +321,14 @@ struct Lds {
   unsigned long long fixm[N];  // per stage: local primal indices that are fixed variables
   int cperm[NCP];
   int cpiv[NCP];
+  int fin[4];              // factor(): summed interior inertia (pos, neg, zero) and singular flag
   int seq;                 // 1: last factorisation used the block chain
   int want_sdh;            // 1: keep the strided stage Hessians (block chain in use)
   int sdh_ok;              // 1: the workspace Hessians match the last eval_hess
   double hsig;             // sigma of the last eval_hess
   double fth[MAXF];
   double fph[MAXF];
+  KState ks;
 #ifdef MPCX_PROFILE
   double sprof[6];
 #endif
@@ -321,6 +370,7 @@ struct Agent {
   __device__ gdbl* lb() const { return ws + O_LB; }
   __device__ gdbl* ub() const { return ws + O_UB; }
   __device__ gdbl* sdg() const { return ws + O_SDG; }
+  __device__ gdbl* jtl() const { return ws + O_JTL; }
   __device__ gdbl* sdj() const { return ws + O_SDJ; }
   __device__ gdbl* sdh() const { return ws + O_SDH; }
   __device__ gdbl* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
@@ -370,18 +420,22 @@ __device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* g
   return wsum(f);
 }
 
-__device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv) {
+// derivatives at a point in the workspace; full: also the strided jacobian (scaling and
+// the block-chain fallback read it; the stage-parallel path reads lp and jtl only)
+__device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv, int full) {
   for (int k = a.lane; k < N; k += WAVE)
     gen_stage_gj((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, (double*)(a.sdg() + k),
-                 (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG), (double*)a.lp(k));
+                 (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG), (double*)a.lp(k),
+                 (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
 }
 
-// derivatives at the accepted trial point (still in LDS)
+// derivatives at the accepted trial point (still in LDS), with the accepted multipliers
 __device__ __noinline__ void eval_gj_lds(const Agent a) {
+  const int full = gL.want_sdh;
   for (int k = a.lane; k < N; k += WAVE)
     gen_stage_gj((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS,
                  (double*)(a.sdg() + k), (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG),
-                 (double*)a.lp(k));
+                 (double*)a.lp(k), (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
 }
 
 // Hessian of sigma*f + sum lam_i * gs_i * g_i (scaled Lagrangian) into the packed
@@ -407,18 +461,11 @@ __device__ __forceinline__ double acc_grad(const Agent a, int i) {
   if (NX > 0 && off >= NV && b + 1 < N) v += a.sdg()[(off - NV) * N + b + 1];
   return v;
 }
-// (J~^T lam)[i] with J~ = gs*J
-__device__ __forceinline__ double acc_jtl(const Agent a, int i, const gdbl* lamv) {
+// (J~^T lam)[i] with J~ = gs*J, from the per-stage products the evaluators wrote
+__device__ __forceinline__ double acc_jtl(const Agent a, int i) {
   const int b = (i - NX) / NP, off = (i - NX) % NP;
-  double v = 0.0;
-#pragma unroll
-  for (int r = 0; r < NG; ++r)
-    v += a.sdj()[(r * NL + NX + off) * N + b] * a.gs()[b * NG + r] * lamv[b * NG + r];
-  if (NX > 0 && off >= NV && b + 1 < N) {
-#pragma unroll
-    for (int r = 0; r < NG; ++r)
-      v += a.sdj()[(r * NL + off - NV) * N + b + 1] * a.gs()[(b + 1) * NG + r] * lamv[(b + 1) * NG + r];
-  }
+  double v = a.jtl()[(NX + off) * N + b];
+  if (NX > 0 && off >= NV && b + 1 < N) v += a.jtl()[(off - NV) * N + b + 1];
   return v;
 }
 
@@ -1259,31 +1306,66 @@ __device__ __noinline__ void chain_solve(const Agent a) {
   wsync();
 }
 
-// Factor the KKT matrix bordered by the rhs in a.rhs(); returns the inertia.
+// After the interior elimination of stage k (slot lanes g): store its local Schur blocks
+// and eliminated rhs (chain input), back-substitute the trailing rows and store the
+// back-substitution operators.  A leaf, so factor() keeps almost nothing live across calls.
+__device__ __noinline__ void stage_tail(const Agent a, int k, int g, ldsd* F, const ldsi* perm, const ldsi* piv) {
+  Lds& L = gL;
+  if (NC > 0) {  // local Schur complement on (x_k, c_k), eliminated rhs of those rows
+    constexpr int NS = NX * NX + NC * NC + NC * NX;
+    for (int e = g; e < NS; e += G) {
+      int ri, ci, o;
+      if (e < NX * NX) {
+        ri = NI + e / NX; ci = NI + e % NX; o = e;
+      } else if (e < NX * NX + NC * NC) {
+        const int f = e - NX * NX;
+        ri = LMU + f / NC; ci = LMU + f % NC; o = NXX + f;
+      } else {
+        const int f = e - NX * NX - NC * NC;
+        ri = LMU + f / NX; ci = NI + f % NX; o = NXX + NCC + f;
+      }
+      L.S[k * SOFF + o] = (ri >= ci) ? F[pko(ri) + ci] : F[pko(ci) + ri];
+    }
+    for (int c = g; c < NX + NC; c += G) L.zx[k * (NX + NC) + c] = F[pko(RB) + NI + c];
+  }
+  trailing_backsolve(F, piv, g);
+  // back-substitution operators, p-major, each lane stores (and later reads) its own p
+  for (int p = g; p < NI; p += G) {
+#pragma unroll
+    for (int t = 0; t < NTR; ++t) a.tr(k)[p * NTR + t] = F[pko(NI + t) + p];
+    a.prm(k)[p] = perm[p];
+  }
+}
+
+// Factor the KKT matrix bordered by the rhs in a.rhs(); returns the inertia.  Only the
+// round counter, the inertia sums and the diagonal shifts stay live across the calls.
 __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   Lds& L = gL;
-  const int lane = a.lane, g = lane % G, slot = lane / G;
   SPROF_DECL
-  ParLds& P = L.u.p;
-  ldsd* F = LDSP(P.F + slot * PKS);
-  ldsi* perm = LDSI(P.perm + slot * NI);
-  ldsi* piv = LDSI(P.piv + slot * NI);
-  Inertia gi{0, 0, 0};
-  int bad = 0;
+  if (a.lane < 4) L.fin[a.lane] = 0;  // inertia (pos, neg, zero) and singular flag, summed in LDS
+  wsync();
 #pragma unroll 1
   for (int r = 0; r < ROUNDS; ++r) {
+    const int g = lane_now() % G, slot = lane_now() / G;
     const int k = r * SR + slot;
     const bool act = slot < SR && k < N;
     if (act) {
+      ldsd* F = LDSP(L.u.p.F + slot * PKS);
+      ldsi* perm = LDSI(L.u.p.perm + slot * NI);
       for (int i = g; i < NI; i += G) perm[i] = i;
       if (kd.mode == LSQ) local_assemble_generic(a, k, g, F, kd);
       else local_assemble(a, k, g, F, kd);
     }
     wsync();
     SPROF(0);
-    if (act) {
-      const BKOut bo = interior_bk(F, perm, piv, g);
-      gi.pos += bo.pos; gi.neg += bo.neg; gi.zero += bo.zero; bad |= bo.bad;
+    if (lane_now() / G < SR && r * SR + lane_now() / G < N) {
+      const int g2 = lane_now() % G, slot2 = lane_now() / G;
+      const BKOut bo = interior_bk(LDSP(L.u.p.F + slot2 * PKS), LDSI(L.u.p.perm + slot2 * NI),
+                                   LDSI(L.u.p.piv + slot2 * NI), g2);
+      if (lane_now() % G == 0) {
+        atomicAdd(&L.fin[0], bo.pos); atomicAdd(&L.fin[1], bo.neg); atomicAdd(&L.fin[2], bo.zero);
+        atomicOr(&L.fin[3], bo.bad);
+      }
     }
     wsync();
     SPROF(1);
@@ -1291,48 +1373,28 @@ __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     bad = 1;
 #endif
     if constexpr (NX > 0) {
-      if (wsumi(g == 0 ? bad : 0) > 0) {  // singular stage interior: block chain instead
+      if (L.fin[3] != 0) {  // singular stage interior: block chain instead
         sync();
-        if (!L.sdh_ok && kd.mode != LSQ) {  // the chain reads the strided Hessians
+        if (!L.sdh_ok && kd.mode != LSQ) {  // the chain reads the strided Hessians and jacobian
           eval_hess_impl(a, L.hsig, 1);
+          eval_gj_ws(a, a.x(), 1);
           sync();
         }
-        if (lane == 0) { L.seq = 1; L.want_sdh = 1; }
+        if (a.lane == 0) { L.seq = 1; L.want_sdh = 1; }
         sync();
         return seq_factor(a, kd);
       }
     }
-    if (act) {
-      if (NC > 0) {  // local Schur complement on (x_k, c_k), eliminated rhs of those rows
-        constexpr int NS = NX * NX + NC * NC + NC * NX;
-        for (int e = g; e < NS; e += G) {
-          int ri, ci, o;
-          if (e < NX * NX) {
-            ri = NI + e / NX; ci = NI + e % NX; o = e;
-          } else if (e < NX * NX + NC * NC) {
-            const int f = e - NX * NX;
-            ri = LMU + f / NC; ci = LMU + f % NC; o = NXX + f;
-          } else {
-            const int f = e - NX * NX - NC * NC;
-            ri = LMU + f / NX; ci = NI + f % NX; o = NXX + NCC + f;
-          }
-          L.S[k * SOFF + o] = (ri >= ci) ? F[pko(ri) + ci] : F[pko(ci) + ri];
-        }
-        for (int c = g; c < NX + NC; c += G) L.zx[k * (NX + NC) + c] = F[pko(RB) + NI + c];
-      }
-      trailing_backsolve(F, piv, g);
-      // back-substitution operators, p-major, each lane stores (and later reads) its own p
-      for (int p = g; p < NI; p += G) {
-#pragma unroll
-        for (int t = 0; t < NTR; ++t) a.tr(k)[p * NTR + t] = F[pko(NI + t) + p];
-        a.prm(k)[p] = perm[p];
-      }
+    if (lane_now() / G < SR && r * SR + lane_now() / G < N) {
+      const int g = lane_now() % G, slot = lane_now() / G;
+      stage_tail(a, r * SR + slot, g, LDSP(L.u.p.F + slot * PKS), LDSI(L.u.p.perm + slot * NI),
+                 LDSI(L.u.p.piv + slot * NI));
     }
     wsync();
     SPROF(2);
   }
-  Inertia in{wsumi(g == 0 ? gi.pos : 0), wsumi(g == 0 ? gi.neg : 0), wsumi(g == 0 ? gi.zero : 0)};
-  if (lane == 0) L.seq = 0;
+  Inertia in{L.fin[0], L.fin[1], L.fin[2]};
+  if (a.lane == 0) L.seq = 0;
   if (NC > 0) {
     const Inertia ci = chain_factor(a);
     in.pos += ci.pos; in.neg += ci.neg; in.zero += ci.zero;
@@ -1383,12 +1445,6 @@ __device__ __noinline__ void solve(const Agent a) {
 // dual_u / viol_u: IPOPT's unscaled_curr_dual_infeasibility (grad_lag_x and the slack part
 // grad_lag_s*d_scale, / obj_scale) and unscaled_curr_nlp_constraint_violation (|c| and the
 // violation of the (relaxed) bounds of d, not d - s)
-struct OptErr {
-  double dual, dual_u, primal, viol_u, pmx, pmn, s_d, s_c;
-  int ncompl;
-  __device__ double compl_at(double mu) const { return ncompl > 0 ? fmax(pmx - mu, mu - pmn) : 0.0; }
-  __device__ double err_at(double mu) const { return fmax(fmax(dual / s_d, primal), compl_at(mu) / s_c); }
-};
 
 // scaled optimality error E_mu (IPOPT eq. 5) + unscaled parts
 __device__ __noinline__ OptErr opt_error(const Agent a, double obj_scale) {
@@ -1402,7 +1458,7 @@ __device__ __noinline__ OptErr opt_error(const Agent a, double obj_scale) {
     const bool on = i >= NX && i < NW;
     const int ii = on ? i : NX;
     const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
-    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii, a.lam());
+    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
     if (on && lo != hi) {
       const double rd = obj_scale * gr + jt - zl + zu;
       dmax = fmax(dmax, fabs(rd));
@@ -1481,7 +1537,7 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
   const gdbl* wio = (const gdbl*)args.w + (long)agent * NW;
   const gdbl* pin = (const gdbl*)args.p + (long)agent * NPAR;
   for (int t = lane; t < NPAR; t += WAVE) gL.par[t] = pin[t];
-  for (long t = lane; t < (long)(NL + NG * NL + NL * NL) * N; t += WAVE) a.ws[O_SDG + t] = 0.0;
+  for (long t = lane; t < (long)(2 * NL + NG * NL + NL * NL) * N; t += WAVE) a.ws[O_SDG + t] = 0.0;
   for (long t = lane; t < (long)N * PKS; t += WAVE) a.ws[O_LP + t] = 0.0;  // structural zeros stay zero
   for (int i = lane; i < NW; i += WAVE) {
     double lo = lbw[i], hi = ubw[i];
@@ -1512,7 +1568,7 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
   for (int c = lane; c < M; c += WAVE) a.gs()[c] = 1.0;
   sync();
   // gradient based scaling at the user starting point
-  eval_gj_ws(a, a.x());
+  eval_gj_ws(a, a.x(), 1);
   sync();
   double gmx = 0.0;
   for (int i = NX + lane; i < NW; i += WAVE)
@@ -1583,7 +1639,7 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
     a.lam()[c] = 0.0;
   }
   sync();
-  eval_gj_ws(a, a.x());
+  eval_gj_ws(a, a.x(), 1);
   sync();
   return sc;
 }
@@ -1607,7 +1663,7 @@ __device__ __noinline__ void rhs_primal(const Agent a, double mu, double obj_sca
     const bool on = i >= NX && i < NW;
     const int ii = on ? i : NX;
     const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii];
-    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii, a.lam());
+    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
     if (on) {
       double r = 0.0;
       if (lo != hi) {
@@ -1675,14 +1731,14 @@ __device__ __noinline__ void ls_multipliers(const Agent a, const double constr_m
   double lmax = 0.0;
   for (int c = lane; c < M; c += WAVE) lmax = fmax(lmax, fabs(gL.u.sol[(c / NG) * NB + NP + c % NG]));
   lmax = wmax(lmax);
-  if (lmax <= constr_mult_init_max)
+  if (lmax <= constr_mult_init_max) {
     for (int c = lane; c < M; c += WAVE) a.lam()[c] = gL.u.sol[(c / NG) * NB + NP + c % NG];
+    sync();
+    eval_gj_ws(a, a.x(), 0);  // (J~^T lambda) of the new multipliers
+  }
   sync();
 }
 
-struct StepInfo {
-  double amax, az, gphid, theta, barrier;
-};
 
 // full step from the Newton solution (LDS) + fraction-to-the-boundary step
 // sizes + constraint violation and barrier at the current point
@@ -1768,103 +1824,103 @@ __device__ __noinline__ StepInfo recover_step(const Agent a, double mu, double t
   return st;
 }
 
-struct Trial {
-  double f, theta, phi;
-};
 struct LSOpt {  // line-search options by value (registers, not kernarg loads)
   double alpha_min_frac, gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi;
 };
-struct LSResult {
-  Trial tr;
-  double alpha;
-  int accepted, ftype, trials;
-};
 
-// filter line search; trial points live in LDS (xt, scaled gt)
-__device__ __noinline__ LSResult line_search(const Agent a, KArgs* argp, double mu, double obj_scale,
-                                             double alpha0, double gphid, double theta, double phi,
-                                             double theta_min, double theta_max, int nfilt) {
-  // options from the kernarg segment (scalar loads); a by-value LSOpt exceeds the
-  // argument registers and would be passed through scratch
-  KArgs& ka = *argp;
-  const int lane = a.lane;
-  double xr[VS], dxr[VS], lor[VS], hir[VS];
-#pragma unroll
-  for (int sl = 0; sl < VS; ++sl) {
-    const int i = lane + sl * WAVE;
-    const int ii = i < NW ? i : 0;
-    xr[sl] = a.x()[ii]; dxr[sl] = a.dx()[ii]; lor[sl] = a.xL()[ii]; hir[sl] = a.xU()[ii];
+// pow / log out of line: inlined into a loop that also calls a phase function, their
+// polynomial constants are hoisted into VGPRs that live across the call (scratch spills)
+__device__ __noinline__ double pow_ool(double x, double y) { return pow(x, y); }
+__device__ __noinline__ double log_ool(double x) { return log(x); }
+
+// filter line search from the recovered step (gL.ks.st) into gL.ks.ls; trial points live
+// in LDS (xt, scaled gt).  The search state is kept in LDS too and nothing vector-sized
+// stays in registers across the evaluation call (a non-leaf function saves every
+// callee-saved VGPR it uses to scratch): the x-part of the barrier is summed while the
+// trial point is written, the constraint part is re-read after the call.
+__device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
+  KState& K = gL.ks;
+  {
+    KArgs& ka = *argp;
+    const double gphid = K.st.gphid, theta = K.st.theta;
+    double amin;
+    if (gphid < 0 && theta <= K.theta_min)
+      amin = ka.opt.alpha_min_frac * fmin(fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid)),
+                                     ka.opt.delta * pow_ool(theta, ka.opt.s_theta) / pow_ool(-gphid, ka.opt.s_phi));
+    else if (gphid < 0)
+      amin = ka.opt.alpha_min_frac * fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid));
+    else
+      amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;
+    if (!(amin > 0.0)) amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;  // NaN guard
+    K.amin = amin;
+    K.ls.alpha = K.st.amax;
+    K.ls.accepted = 0;
+    K.ls.ftype = 0;
+    K.ls.trials = 0;
+    K.ls.tr = Trial{0.0, 0.0, 0.0};
   }
-  double sr[CS], dsr[CS], slr[CS], sur[CS], gsr[CS], lbr[CS];
-  int clr[CS];
-#pragma unroll
-  for (int sl = 0; sl < CS; ++sl) {
-    const int c = lane + sl * WAVE;
-    const int cc = c < M ? c : 0;
-    sr[sl] = a.s()[cc]; dsr[sl] = a.ds()[cc]; slr[sl] = a.sL()[cc]; sur[sl] = a.sU()[cc];
-    gsr[sl] = a.gs()[cc]; lbr[sl] = a.lb()[cc];
-    clr[sl] = cls_of(lbr[sl], a.ub()[cc], slr[sl], sur[sl]);
-  }
-  double amin;
-  if (gphid < 0 && theta <= theta_min)
-    amin = ka.opt.alpha_min_frac * fmin(fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid)),
-                                   ka.opt.delta * pow(theta, ka.opt.s_theta) / pow(-gphid, ka.opt.s_phi));
-  else if (gphid < 0)
-    amin = ka.opt.alpha_min_frac * fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid));
-  else
-    amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;
-  if (!(amin > 0.0)) amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;  // NaN guard
-  LSResult res;
-  res.alpha = alpha0;
-  res.accepted = 0;
-  res.ftype = 0;
-  res.trials = 0;
-  Trial tr{0.0, 0.0, 0.0};
-  double alpha = alpha0;
 #pragma unroll 1
   for (int ls = 0; ls < 64; ++ls) {
-#pragma unroll
-    for (int sl = 0; sl < VS; ++sl) {
-      const int i = lane + sl * WAVE;
-      if (i < NW) gL.u.t.xt[i] = xr[sl] + alpha * dxr[sl];
-    }
-    wsync();
-    tr.f = obj_scale * eval_fg_lds(a);
-    wsync();
-    double th = 0.0, bar = 0.0;
-#pragma unroll
-    for (int sl = 0; sl < VS; ++sl) {
-      const int i = lane + sl * WAVE;
-      if (i >= NX && i < NW && lor[sl] != hir[sl]) {
-        const double xt = xr[sl] + alpha * dxr[sl];
-        if (isfin(lor[sl])) bar += log(xt - lor[sl]);
-        if (isfin(hir[sl])) bar += log(hir[sl] - xt);
+    {
+      const int lane = lane_now();
+      const double alpha = K.ls.alpha;
+      double barx = 0.0;
+#pragma unroll 1
+      for (int sl = 0; sl < VS; ++sl) {
+        const int i = lane + sl * WAVE;
+        if (i < NW) {
+          const double lo = a.xL()[i], hi = a.xU()[i];
+          const double xt = a.x()[i] + alpha * a.dx()[i];
+          gL.u.t.xt[i] = xt;
+          if (i >= NX && lo != hi) {
+            if (isfin(lo)) barx += log_ool(xt - lo);
+            if (isfin(hi)) barx += log_ool(hi - xt);
+          }
+        }
       }
+      K.barx = wsum(barx);
     }
-#pragma unroll
+    wsync();
+    {
+      const double f = eval_fg_lds(a);
+      K.ls.tr.f = K.obj_scale * f;
+    }
+    wsync();
+    const int lane = lane_now();
+    const double alpha = K.ls.alpha;
+    double th = 0.0, bar = 0.0;
+#pragma unroll 1
     for (int sl = 0; sl < CS; ++sl) {
       const int c = lane + sl * WAVE;
       if (c < M) {
-        const double gt = gL.u.t.gt[c] * gsr[sl];
+        const double gsv = a.gs()[c], lbv = a.lb()[c], slv = a.sL()[c], suv = a.sU()[c];
+        const int cl = cls_of(lbv, a.ub()[c], slv, suv);
+        const double gt = gL.u.t.gt[c] * gsv;
         gL.u.t.gt[c] = gt;
-        const double st = sr[sl] + alpha * dsr[sl];
-        th += fabs(clr[sl] == 0 ? gt - gsr[sl] * lbr[sl] : gt - st);
-        if (clr[sl] == 1) {
-          if (isfin(slr[sl])) bar += log(st - slr[sl]);
-          if (isfin(sur[sl])) bar += log(sur[sl] - st);
+        const double st = a.s()[c] + alpha * a.ds()[c];
+        th += fabs(cl == 0 ? gt - gsv * lbv : gt - st);
+        if (cl == 1) {
+          if (isfin(slv)) bar += log_ool(st - slv);
+          if (isfin(suv)) bar += log_ool(suv - st);
         }
       }
     }
+    KArgs& ka = *argp;
+    const double mu = K.mu, theta = K.st.theta, gphid = K.st.gphid;
+    const double phi = K.fx - mu * K.st.barrier;
+    Trial tr = K.ls.tr;
     tr.theta = wsum(th);
-    tr.phi = tr.f - mu * wsum(bar);
-    res.trials++;
-    bool okt = (tr.theta <= theta_max) && (tr.phi == tr.phi);
+    tr.phi = tr.f - mu * (K.barx + wsum(bar));
+    K.ls.tr = tr;
+    K.ls.trials += 1;
+    bool okt = (tr.theta <= K.theta_max) && (tr.phi == tr.phi);
+    const int nfilt = K.nfilt;
     for (int j = 0; j < nfilt && okt; ++j)
       if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
     bool ftype = false;
     if (okt) {
-      const bool switching = gphid < 0 && alpha * pow(-gphid, ka.opt.s_phi) > ka.opt.delta * pow(theta, ka.opt.s_theta);
-      if (theta <= theta_min && switching) {
+      const bool switching = gphid < 0 && alpha * pow_ool(-gphid, ka.opt.s_phi) > ka.opt.delta * pow_ool(theta, ka.opt.s_theta);
+      if (theta <= K.theta_min && switching) {
         okt = tr.phi <= phi + ka.opt.eta_phi * alpha * gphid;
         ftype = true;
       } else {
@@ -1872,14 +1928,12 @@ __device__ __noinline__ LSResult line_search(const Agent a, KArgs* argp, double 
         ftype = false;
       }
     }
-    res.alpha = alpha;
-    res.ftype = ftype;
-    if (okt) { res.accepted = 1; break; }
-    alpha *= 0.5;
-    if (alpha < amin) break;
+    K.ls.ftype = ftype;
+    if (okt) { K.ls.accepted = 1; break; }
+    if (alpha * 0.5 < K.amin) break;
+    K.ls.alpha = alpha * 0.5;
   }
-  res.tr = tr;
-  return res;
+  wsync();
 }
 
 // take the last trial point (xt, gt in LDS) and the multiplier steps
@@ -1941,10 +1995,6 @@ __device__ __noinline__ void accept_step(const Agent a, const double kappa_sigma
 // IPOPT OptimalityErrorConvergenceCheck::CurrentIsAcceptable: the objective-change test
 // compares the (scaled) objective of the last two iterations at which it was called
 // (initially -1e50, so the first call never passes a finite acceptable_obj_change_tol)
-struct Acceptable {
-  double curr_f, last_f;
-  int last_it, count;
-};
 __device__ __forceinline__ bool current_is_acceptable(Acceptable& ac, const OptErr& e, double err0, double fx,
                                                       int it, double obj_scale, int square,
                                                       const mpcx_options& o) {
@@ -1972,15 +2022,20 @@ using namespace mpcx_kernel;
 // ---------------------------------------------------------------------------
 // the kernel: one agent NLP per workgroup (one wavefront)
 // ---------------------------------------------------------------------------
+#define KOPT (((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())->opt)
+#define OPT(f) (*(volatile const __attribute__((address_space(4))) decltype(mpcx_options::f)*)&KOPT.f)
 extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(Args args) {
   const int agent = blockIdx.x;
   if (agent >= args.n_agents) return;
   if (args.active != nullptr && args.active[agent] == 0) return;  // frozen (converged ADMM block)
-  const mpcx_options& o = args.opt;
+  // Loop state lives in LDS (KState, written identically by every lane) and the options are
+  // re-read from the kernarg segment where they are used (volatile scalar loads): held in
+  // VGPRs they would have to survive every phase call and be spilled to scratch.
   Agent a;
   a.ws = (gdbl*)args.ws + (long)agent * args.ws_stride;
   a.lane = threadIdx.x;
   const int lane = a.lane;
+  KState& K = gL.ks;
 
   PROF_DECL
 #ifdef MPCX_PROFILE
@@ -1988,128 +2043,156 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   sync();
 #endif
   if (lane == 0) { gL.want_sdh = 0; gL.sdh_ok = 0; gL.hsig = 1.0; gL.seq = 0; }
-  const Scal sc = init_agent(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr(), agent);
+  {
+    const Scal sc = init_agent(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr(), agent);
+    K.obj_scale = sc.obj_scale;
+    K.fx = sc.fx;
+    K.square = sc.square;
+  }
+  K.n_fact = 0; K.n_ic = 0; K.n_fallback = 0; K.n_trials = 0; K.n_chain = 0;
   PROF(0);
-  const double obj_scale = sc.obj_scale;
-  double fx = sc.fx;
-  int n_fact = 0, n_ic = 0, n_fallback = 0, n_trials = 0, n_chain = 0;
-  if (M > 0 && o.constr_mult_init_max > 0.0) {
-    ls_multipliers(a, o.constr_mult_init_max, obj_scale);
-    n_fact++;
+  if (M > 0 && OPT(constr_mult_init_max) > 0.0) {
+    ls_multipliers(a, OPT(constr_mult_init_max), K.obj_scale);
+    K.n_fact = 1;
   }
   PROF(1);
 
-  double mu = o.mu_init;
-  double tau = fmax(o.tau_min, 1.0 - mu);
-  double dw_last = 0.0;
-  const double theta0 = theta_now(a);
-  const double theta_max = o.theta_max_fact * fmax(1.0, theta0);
-  const double theta_min = o.theta_min_fact * fmax(1.0, theta0);
-  int nfilt = 0;
-  int status = MPCX_MAX_ITER_EXCEEDED;
-  int it = 0;
-  OptErr e0;
-  Acceptable acc{-1e50, -1e50, -1, 0};
+  K.mu = OPT(mu_init);
+  K.tau = fmax(OPT(tau_min), 1.0 - K.mu);
+  K.dw_last = 0.0;
+  {
+    const double theta0 = theta_now(a);
+    K.theta_max = OPT(theta_max_fact) * fmax(1.0, theta0);
+    K.theta_min = OPT(theta_min_fact) * fmax(1.0, theta0);
+  }
+  K.nfilt = 0;
+  K.status = MPCX_MAX_ITER_EXCEEDED;
+  K.it = 0;
+  K.acc = Acceptable{-1e50, -1e50, -1, 0};
 #pragma unroll 1
   for (;;) {
-    e0 = opt_error(a, obj_scale);
-    const double err0 = e0.err_at(0.0);
-    if (!(err0 == err0) || !(fx == fx)) { status = MPCX_INVALID_NUMBER; break; }
-    // IPOPT OptimalityErrorConvergenceCheck::CheckConvergence (square problems: the dual
-    // infeasibility and complementarity tolerances are lifted)
-    if (err0 <= o.tol && e0.viol_u <= o.constr_viol_tol &&
-        (sc.square || (e0.dual_u <= o.dual_inf_tol && e0.compl_at(0.0) / obj_scale <= o.compl_inf_tol))) {
-      status = MPCX_SOLVE_SUCCEEDED;
-      break;
+    {
+      const OptErr e = opt_error(a, K.obj_scale);
+      K.e0 = e;
     }
-    if (o.acceptable_iter > 0 && current_is_acceptable(acc, e0, err0, fx, it, obj_scale, sc.square, o)) {
-      if (++acc.count >= o.acceptable_iter) { status = MPCX_SOLVED_TO_ACCEPTABLE; break; }
-    } else {
-      acc.count = 0;
+    {
+      const OptErr e0 = K.e0;
+      const double obj_scale = K.obj_scale, fx = K.fx;
+      const double err0 = e0.err_at(0.0);
+      if (!(err0 == err0) || !(fx == fx)) { K.status = MPCX_INVALID_NUMBER; break; }
+      // IPOPT OptimalityErrorConvergenceCheck::CheckConvergence (square problems: the dual
+      // infeasibility and complementarity tolerances are lifted)
+      if (err0 <= OPT(tol) && e0.viol_u <= OPT(constr_viol_tol) &&
+          (K.square || (e0.dual_u <= OPT(dual_inf_tol) && e0.compl_at(0.0) / obj_scale <= OPT(compl_inf_tol)))) {
+        K.status = MPCX_SOLVE_SUCCEEDED;
+        break;
+      }
+      Acceptable acc = K.acc;
+      if (OPT(acceptable_iter) > 0 && current_is_acceptable(acc, e0, err0, fx, K.it, obj_scale, K.square, KOPT)) {
+        acc.count++;
+        K.acc = acc;
+        if (acc.count >= OPT(acceptable_iter)) { K.status = MPCX_SOLVED_TO_ACCEPTABLE; break; }
+      } else {
+        acc.count = 0;
+        K.acc = acc;
+      }
+      if (K.it >= OPT(max_iter)) break;
     }
-    if (it >= o.max_iter) break;
     // barrier parameter update (monotone Fiacco-McCormick)
 #pragma unroll 1
     for (int mu_up = 0; mu_up < 64; ++mu_up) {
-      if (e0.err_at(mu) > o.kappa_eps * mu || mu <= o.mu_min) break;
+      const double mu = K.mu;
+      if (K.e0.err_at(mu) > OPT(kappa_eps) * mu || mu <= OPT(mu_min)) break;
       // IPOPT MonotoneMuUpdate::CalcNewMuAndTau: floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
-      const double new_mu = fmax(fmax(fmin(o.tol, o.compl_inf_tol) / (o.kappa_eps + 1.0), o.mu_min),
-                                 fmin(o.kappa_mu * mu, pow(mu, o.theta_mu)));
+      const double new_mu = fmax(fmax(fmin(OPT(tol), OPT(compl_inf_tol)) / (OPT(kappa_eps) + 1.0), OPT(mu_min)),
+                                 fmin(OPT(kappa_mu) * mu, pow_ool(mu, OPT(theta_mu))));
       if (new_mu == mu) break;  // IPOPT MonotoneMuUpdate: done when mu no longer changes
-      mu = new_mu;
-      tau = fmax(o.tau_min, 1.0 - mu);
-      nfilt = 0;
+      K.mu = new_mu;
+      K.tau = fmax(OPT(tau_min), 1.0 - new_mu);
+      K.nfilt = 0;
     }
     PROF(2);
-    eval_hess(a, obj_scale);
+    eval_hess(a, K.obj_scale);
     PROF(3);
-    rhs_primal(a, mu, obj_scale);
+    rhs_primal(a, K.mu, K.obj_scale);
     PROF(4);
     // factorisation with inertia correction (IPOPT Algorithm IC)
-    double dw = 0.0, dc = 0.0;
-    bool ok = false;
+    K.dw = 0.0;
+    K.dc = 0.0;
+    int ok = 0;
 #pragma unroll 1
     for (int attempt = 0; attempt < 60; ++attempt) {
-      rhs_dual(a, mu, dw);
-      KKTDiag kd{dw, dc, NEWTON};
-      const Inertia in = factor(a, kd);
-      n_fact++;
-      n_chain += gL.seq;
+      rhs_dual(a, K.mu, K.dw);
+      const Inertia in = factor(a, KKTDiag{K.dw, K.dc, NEWTON});
+      K.n_fact += 1;
+      K.n_chain += gL.seq;
       if (in.pos == N * NP && in.neg == M && in.zero == 0) {
-        if (attempt > 0) dw_last = dw;
-        ok = true;
+        if (attempt > 0) K.dw_last = K.dw;
+        ok = 1;
         break;
       }
-      n_ic++;
+      K.n_ic += 1;
+      const double dw = K.dw, dw_last = K.dw_last;
       if (attempt == 0) {
-        if (in.zero > 0) dc = o.delta_c_bar * pow(mu, o.kappa_c);
-        dw = (dw_last == 0.0) ? o.delta_w_first : fmax(o.delta_w_min, o.kappa_w_minus * dw_last);
+        if (in.zero > 0) K.dc = OPT(delta_c_bar) * pow_ool(K.mu, OPT(kappa_c));
+        K.dw = (dw_last == 0.0) ? OPT(delta_w_first) : fmax(OPT(delta_w_min), OPT(kappa_w_minus) * dw_last);
       } else {
-        dw = (dw_last == 0.0) ? o.kappa_w_plus_bar * dw : o.kappa_w_plus * dw;
-        if (dw > o.delta_w_max) break;
+        K.dw = (dw_last == 0.0) ? OPT(kappa_w_plus_bar) * dw : OPT(kappa_w_plus) * dw;
+        if (K.dw > OPT(delta_w_max)) break;
       }
     }
     PROF(5);
-    if (!ok) { status = MPCX_ERROR_IN_STEP; break; }
+    if (!ok) { K.status = MPCX_ERROR_IN_STEP; break; }
     solve(a);
     PROF(6);
-    const StepInfo st = recover_step(a, mu, tau, dw, obj_scale);
+    {
+      const StepInfo st = recover_step(a, K.mu, K.tau, K.dw, K.obj_scale);
+      K.st = st;
+    }
     PROF(7);
     // filter line search
-    const double theta = st.theta;
-    const double phi = fx - mu * st.barrier;
-    const LSResult ls = line_search(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr(), mu, obj_scale, st.amax, st.gphid, theta, phi, theta_min,
-                                    theta_max, nfilt);
-    n_trials += ls.trials;
-    bool ftype = ls.ftype;
-    // IPOPT BacktrackingLineSearch: before entering the restoration phase, stop if the
-    // current iterate is acceptable ("Restoration phase called at acceptable point")
-    if (!ls.accepted && current_is_acceptable(acc, e0, e0.err_at(0.0), fx, it, obj_scale, sc.square, o)) {
-      status = MPCX_SOLVED_TO_ACCEPTABLE;
-      break;
-    }
-    // no acceptable trial and the last one is not even finite: IPOPT would enter its
-    // restoration phase; stop with Restoration_Failed at the current (finite) iterate
-    if (!ls.accepted && !(isfin(ls.tr.theta) && isfin(ls.tr.phi))) { status = MPCX_RESTORATION_FAILED; break; }
-    if (!ls.accepted) { nfilt = 0; ftype = true; n_fallback++; }
-    if (!ftype) {
-      if (nfilt == MAXF) {
-        if (lane == 0)
-          for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
-        nfilt--;
+    line_search(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr());
+    {
+      const LSResult ls = K.ls;
+      K.n_trials += ls.trials;
+      bool ftype = ls.ftype;
+      // IPOPT BacktrackingLineSearch: before entering the restoration phase, stop if the
+      // current iterate is acceptable ("Restoration phase called at acceptable point")
+      if (!ls.accepted) {
+        Acceptable acc = K.acc;
+        const OptErr e0 = K.e0;
+        const bool acceptable = current_is_acceptable(acc, e0, e0.err_at(0.0), K.fx, K.it, K.obj_scale, K.square, KOPT);
+        K.acc = acc;
+        if (acceptable) { K.status = MPCX_SOLVED_TO_ACCEPTABLE; break; }
       }
-      if (lane == 0) { gL.fth[nfilt] = (1.0 - o.gamma_theta) * theta; gL.fph[nfilt] = phi - o.gamma_phi * theta; }
-      nfilt++;
+      // no acceptable trial and the last one is not even finite: IPOPT would enter its
+      // restoration phase; stop with Restoration_Failed at the current (finite) iterate
+      if (!ls.accepted && !(isfin(ls.tr.theta) && isfin(ls.tr.phi))) { K.status = MPCX_RESTORATION_FAILED; break; }
+      int nfilt = K.nfilt;
+      if (!ls.accepted) { nfilt = 0; ftype = true; K.n_fallback += 1; }
+      if (!ftype) {
+        const double theta = K.st.theta, phi = K.fx - K.mu * K.st.barrier;
+        if (nfilt == MAXF) {
+          if (lane == 0)
+            for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
+          nfilt--;
+        }
+        if (lane == 0) { gL.fth[nfilt] = (1.0 - OPT(gamma_theta)) * theta; gL.fph[nfilt] = phi - OPT(gamma_phi) * theta; }
+        nfilt++;
+      }
+      K.nfilt = nfilt;
+      K.fx = ls.tr.f;
       wsync();
     }
     PROF(8);
-    accept_step(a, o.kappa_sigma, mu, ls.alpha, st.az);
-    fx = ls.tr.f;
+    accept_step(a, OPT(kappa_sigma), K.mu, K.ls.alpha, K.st.az);
+    sync();  // accepted multipliers visible to the stage lanes
     eval_gj_lds(a);
     sync();
-    it++;
+    K.it += 1;
     PROF(9);
   }
+  const double obj_scale = K.obj_scale;
 
   // ---- outputs ----------------------------------------------------------------
   gdbl* wio = (gdbl*)args.w + (long)agent * NW;
@@ -2130,19 +2213,19 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
       ((gdbl*)args.lam_g)[(long)agent * M + c] = a.lam()[c] * a.gs()[c] / obj_scale;
   if (args.stats != nullptr && lane == 0) {
     mpcx_stats st;
-    st.obj = fx / obj_scale;
-    st.primal_inf = e0.viol_u;
-    st.dual_inf = e0.dual_u;
-    st.compl_inf = e0.compl_at(0.0) / obj_scale;
-    st.mu = mu;
+    st.obj = K.fx / obj_scale;
+    st.primal_inf = K.e0.viol_u;
+    st.dual_inf = K.e0.dual_u;
+    st.compl_inf = K.e0.compl_at(0.0) / obj_scale;
+    st.mu = K.mu;
     st.obj_scale = obj_scale;
-    st.iter_count = it;
-    st.status = status;
-    st.n_inertia_corrections = n_ic;
-    st.n_linesearch_fallbacks = n_fallback;
-    st.n_factorizations = n_fact;
-    st.n_trials = n_trials;
-    st.n_block_chain = n_chain;
+    st.iter_count = K.it;
+    st.status = K.status;
+    st.n_inertia_corrections = K.n_ic;
+    st.n_linesearch_fallbacks = K.n_fallback;
+    st.n_factorizations = K.n_fact;
+    st.n_trials = K.n_trials;
+    st.n_block_chain = K.n_chain;
     st.reserved = 0;
     args.stats[agent] = st;
   }

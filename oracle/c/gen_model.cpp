@@ -26,6 +26,7 @@ constexpr int NL = 2 * MPCX_NX + MPCX_NV;
 constexpr int NLOC_MAX = MPCX_NV + MPCX_NG + 2 * MPCX_NX;
 constexpr int LP_SIZE = (NLOC_MAX + 2) * (NLOC_MAX + 3) / 2 + 1;
 double g_ones[MPCX_NG > 0 ? MPCX_NG : 1];
+const double g_zeros[MPCX_NG > 0 ? MPCX_NG : 1] = {};
 
 void m_fg(const model_t*, const double* L, const double* PS, const double* PG, double TK, double* f, double* g) {
   double fv = 0.0;
@@ -34,8 +35,8 @@ void m_fg(const model_t*, const double* L, const double* PS, const double* PG, d
 }
 void m_gj(const model_t*, const double* L, const double* PS, const double* PG, double TK, double* grad,
           double* jac) {
-  thread_local double lp[LP_SIZE];
-  gen_stage_gj(L, PS, PG, TK, grad, jac, 1, g_ones, lp);
+  thread_local double lp[LP_SIZE], jtl[NL];
+  gen_stage_gj(L, PS, PG, TK, grad, jac, 1, g_ones, lp, g_zeros, jtl, 1);
 }
 void m_hess(const model_t*, const double* L, const double* PS, const double* PG, double TK, double sigma,
             const double* lam, double* H) {

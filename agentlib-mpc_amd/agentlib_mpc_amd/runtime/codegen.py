@@ -31,6 +31,7 @@ import re
 from typing import Dict, List
 
 from agentlib_mpc_amd import symbolic as sx
+from agentlib_mpc_amd.runtime import stage_elim
 from agentlib_mpc_amd.optimization_backends.discretization import StageNLP
 
 KERNEL_ABI_VERSION = 5
@@ -47,6 +48,10 @@ class GeneratedModel:
     block_chain_only: bool = False
     #: stage rows kept in the border (their multipliers are chained with x_{k+1})
     bordered_rows: list = dataclasses.field(default_factory=list)
+    #: static elimination plan of the stage interior and its generated body (stage_elim.py)
+    elim: object = None
+    elim_lines: list = dataclasses.field(default_factory=list)
+    pattern: list = dataclasses.field(default_factory=list)
 
 
 def _bindings(nlp: StageNLP) -> Dict[sx.Expr, str]:
@@ -79,6 +84,19 @@ def _structural_rank(rows: List[set], n_cols: int) -> int:
     return sum(1 for r in range(len(rows)) if augment(r, set()))
 
 
+def equality_rows(nlp: StageNLP):
+    """Stage rows whose bound expressions coincide at a random parameter point."""
+    import numpy as np
+
+    st = nlp.stage
+    rng = np.random.default_rng(0)
+    vals = {s: float(rng.uniform(0.5, 1.5)) for s in list(st.PS) + list(st.PG)}
+    vals[st.TK] = nlp.ts * min(1, nlp.N - 1)  # an inner stage (k >= 1)
+    lb = np.array(sx.evaluate(st.g_lb, vals), float)
+    ub = np.array(sx.evaluate(st.g_ub, vals), float)
+    return [int(i) for i in np.flatnonzero(lb == ub)]
+
+
 def interior_rank_deficient(nlp: StageNLP, bordered=()) -> bool:
     """True when the equality rows of a stage (except the ``bordered`` ones) cannot all be
     matched to the stage's own variables V (structural rank of their V-Jacobian below the
@@ -87,20 +105,13 @@ def interior_rank_deficient(nlp: StageNLP, bordered=()) -> bool:
     elimination needs nonsingular stage interiors; near-singular ones are not always
     caught by its zero-pivot test and give inaccurate Newton steps.  Equality rows are
     those whose bound expressions coincide at a random parameter point."""
-    import numpy as np
-
     st = nlp.stage
     if not st.g or not st.V:
         return False
-    rng = np.random.default_rng(0)
-    vals = {s: float(rng.uniform(0.5, 1.5)) for s in list(st.PS) + list(st.PG)}
-    vals[st.TK] = nlp.ts * min(1, nlp.N - 1)  # an inner stage (k >= 1)
-    lb = np.array(sx.evaluate(st.g_lb, vals), float)
-    ub = np.array(sx.evaluate(st.g_ub, vals), float)
     col = {v.uid: i for i, v in enumerate(st.V)}
     rows = []
     skip = set(bordered)
-    for i in np.flatnonzero(lb == ub):
+    for i in equality_rows(nlp):
         if int(i) in skip:
             continue
         rows.append({col[f.uid] for f in sx.free_symbols([st.g[i]]) if f.uid in col})
@@ -236,6 +247,29 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     h_lines = (h_lines[:len(h_lines) - nh - len(lp_h)] + (["  if (full) {"] + h_store + ["  }"] if nh else [])
                + h_lines[len(h_lines) - len(lp_h):])
 
+    # -- static sparse elimination of the stage interior (runtime/stage_elim.py) --
+    P = [[False] * (nloc + 1) for _ in range(nloc + 1)]
+
+    def mark(i, j):
+        P[i][j] = P[j][i] = True
+
+    for i in range(nloc + 1):
+        P[i][i] = True
+    for i in range(nl):
+        for j in range(i + 1):
+            if not hess[i][j].is_const(0.0):
+                mark(lidx(i), lidx(j))
+    for r in range(ng):
+        for j in range(nl):
+            if not jac[r][j].is_const(0.0):
+                mark(crow[r], lidx(j))
+    for j in range(nloc):  # border (rhs) row: every local index except x_k
+        if not (ni <= j < ni + nx):
+            mark(nloc, j)
+    eq_duals = sorted(crow[r] for r in equality_rows(nlp) if crow[r] < ni) if ng else []
+    elim_fac, elim_tra, elim_plan = stage_elim.emit(P, ni, nv, nx, nx + nmu, eq_duals)
+    elim_lines = elim_fac + [stage_elim.CHECK] + elim_tra
+
     dims = dict(N=nlp.N, NX=nlp.nx, NV=nlp.nv, NG=ng, NPS=nlp.nps, NPG=nlp.npg)
     ts = nlp.ts if ts is None else ts
     flops = {
@@ -287,6 +321,18 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         *gj_lines, "}", "",
         f"__device__ __forceinline__ void gen_stage_hess({sig}, const double sigma, const double* __restrict__ lam, double* __restrict__ hess, const int S, double* __restrict__ lp, const int full) {{",
         *h_lines, "}", "",
+        "// static sparse elimination of the stage interior (runtime/stage_elim.py):",
+        f"// {len(elim_plan.blocks)} pivot blocks, {elim_plan.n_update} interior updates, {elim_plan.nnz_l} multipliers",
+        "#define MPCX_STATIC_ELIM 1",
+        "typedef __attribute__((address_space(3))) double mpcx_elim_ld;",
+        "typedef __attribute__((address_space(1))) double mpcx_elim_gd;",
+        "typedef __attribute__((address_space(1))) int mpcx_elim_gi;",
+        "__device__ __forceinline__ int gen_stage_elim(mpcx_elim_ld* __restrict__ F, mpcx_elim_ld* __restrict__ S, mpcx_elim_ld* __restrict__ ZX, mpcx_elim_gd* __restrict__ TR, mpcx_elim_gi* __restrict__ PRM, int* __restrict__ inert) {",
+        "  int bad = 0, pos = 0, neg = 0;",
+        *elim_lines,
+        "  inert[0] = pos; inert[1] = neg; inert[2] = 0;",
+        "  return 0;",
+        "}", "",
         '#include "mpcx_ipm.hip"',
         "",
     ]
@@ -303,4 +349,4 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         src = re.sub(r"ANN(\d+)_", lambda m: f"ANN{local[int(m.group(1))]}_", src)
     key = hashlib.sha1(src.encode()).hexdigest()[:16]
     return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz, block_chain_only=force_chain,
-                          bordered_rows=list(bordered))
+                          bordered_rows=list(bordered), elim=elim_plan, elim_lines=elim_lines, pattern=P)

@@ -15,7 +15,7 @@ import pathlib
 import shutil
 import subprocess
 import threading
-from typing import Dict, Optional
+from typing import List, Dict, Optional
 
 PKG_DIR = pathlib.Path(__file__).resolve().parents[1]          # agentlib_mpc_amd/
 ROOT_DIR = PKG_DIR.parent                                       # agentlib-mpc_amd/
@@ -71,7 +71,7 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")] + \
                [(n, ctypes.c_int32) for n in ("iter_count", "status", "n_inertia_corrections",
                                               "n_linesearch_fallbacks", "n_factorizations", "n_trials",
-                                              "n_block_chain", "reserved")]
+                                              "n_block_chain", "n_dense_stages")]
 
 
 STATS_BYTES = ctypes.sizeof(Stats)
@@ -170,8 +170,16 @@ def _kernel_deps_hash() -> str:
     return h.hexdigest()[:10]
 
 
+def _extra_defines() -> List[str]:
+    """Diagnostic kernel variants: ``MPCX_DEFINES="A,B=1"`` adds ``-DA -DB=1`` (e.g.
+    ``MPCX_NO_STATIC`` forces the dense Bunch-Kaufman path); part of the code-object name."""
+    return [d for d in os.environ.get("MPCX_DEFINES", "").split(",") if d]
+
+
 def code_object_path(gen_key: str) -> pathlib.Path:
-    return KERNEL_DIR / f"mpcx_{gen_key}_{_kernel_deps_hash()}_{OFFLOAD_ARCH}.hsaco"
+    extra = _extra_defines()
+    tag = ("_" + hashlib.sha1(",".join(extra).encode()).hexdigest()[:6]) if extra else ""
+    return KERNEL_DIR / f"mpcx_{gen_key}_{_kernel_deps_hash()}{tag}_{OFFLOAD_ARCH}.hsaco"
 
 
 def compile_model(gen, verbose: bool = False) -> pathlib.Path:
@@ -184,7 +192,7 @@ def compile_model(gen, verbose: bool = False) -> pathlib.Path:
     src.write_text(gen.source)
     tmp = out.with_suffix(".tmp")
     cmd = [_hipcc(), "--genco", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17",
-           f"-I{INCLUDE}", f"-I{CSRC}", str(src), "-o", str(tmp)]
+           f"-I{INCLUDE}", f"-I{CSRC}", *[f"-D{d}" for d in _extra_defines()], str(src), "-o", str(tmp)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise NativeError(f"compiling {src} failed:\n{res.stderr[-4000:]}")
@@ -283,7 +291,7 @@ class NativeProblem:
 
 _STATS_DOUBLES = ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")
 _STATS_INTS = ("iter_count", "status", "n_inertia_corrections", "n_linesearch_fallbacks", "n_factorizations",
-               "n_trials", "n_block_chain", "reserved")
+               "n_trials", "n_block_chain", "n_dense_stages")
 
 
 def stats_array(raw_bytes):
@@ -321,7 +329,7 @@ class StatsView:
              "n_inertia_corrections": int(s["n_inertia_corrections"]),
              "n_linesearch_fallbacks": int(s["n_linesearch_fallbacks"]),
              "n_factorizations": int(s["n_factorizations"]), "n_trials": int(s["n_trials"]),
-             "n_block_chain": int(s["n_block_chain"])}
+             "n_block_chain": int(s["n_block_chain"]), "n_dense_stages": int(s["n_dense_stages"])}
         d.update(self.extra)
         return d
 

@@ -110,7 +110,7 @@ constexpr long O_JTL = O_SDG + (long)NL * N;     // [NL][N]      stage (gs*J)^T 
 constexpr long O_SDJ = O_JTL + (long)NL * N;     // [NG*NL][N]   stage jacobian (scaling, block chain)
 constexpr long O_SDH = O_SDJ + (long)NG * NL * N;// [NL*NL][N]   stage hessian
 constexpr long O_RHS = O_SDH + (long)NL * NL * N;// [N][NB]      KKT right-hand side
-constexpr long O_TR = O_RHS + (long)N * NB;      // [N][NI][NTR] back-substitution operators
+constexpr long O_TR = O_RHS + (long)N * NB;      // [N][NTR][NI] back-substitution operators
 constexpr long O_PRM = O_TR + (long)N * NI * NTR;// [N][NI] ints interior pivot order
 constexpr long O_KX = O_PRM + (long)N * NI;      // [N*NP] primal KKT diagonal   (block chain)
 constexpr long O_KD = O_KX + (long)N * NP;       // [M] dual KKT diagonal        (block chain)
@@ -305,7 +305,7 @@ struct KState {
   StepInfo st;     // last recovered step
   LSResult ls;     // last line search
   double mu, tau, dw_last, fx, obj_scale, theta_max, theta_min, dw, dc, amin, barx;
-  int nfilt, it, status, square, n_fact, n_ic, n_fallback, n_trials, n_chain;
+  int nfilt, it, status, square, n_fact, n_ic, n_fallback, n_trials, n_chain, n_dense;
 };
 
 struct Lds {
@@ -1329,17 +1329,38 @@ __device__ __noinline__ void stage_tail(const Agent a, int k, int g, ldsd* F, co
     for (int c = g; c < NX + NC; c += G) L.zx[k * (NX + NC) + c] = F[pko(RB) + NI + c];
   }
   trailing_backsolve(F, piv, g);
-  // back-substitution operators, p-major, each lane stores (and later reads) its own p
+  // back-substitution operators, column-major [t][p] (the static path stores whole columns)
   for (int p = g; p < NI; p += G) {
 #pragma unroll
-    for (int t = 0; t < NTR; ++t) a.tr(k)[p * NTR + t] = F[pko(NI + t) + p];
+    for (int t = 0; t < NTR; ++t) a.tr(k)[t * NI + p] = F[pko(NI + t) + p];
     a.prm(k)[p] = perm[p];
   }
 }
 
+#ifdef MPCX_NO_STATIC  // diagnostics: dense Bunch-Kaufman for every stage
+#undef MPCX_STATIC_ELIM
+#endif
+#ifdef MPCX_STATIC_ELIM
+// Static sparse elimination of stage k's interior by ONE lane (generated straight-line
+// code, runtime/stage_elim.py): writes the Schur blocks, the eliminated rhs and the
+// back-substitution operators that interior_bk + stage_tail would.  Eliminates in place
+// in the slot's LDS image; returns 1 on a (numerically) singular static pivot, before
+// writing any output: the slot is then re-assembled and factored densely.
+__device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* F) {
+  int in[3];
+  asm volatile(";; STATIC_BEGIN");
+  const int bad = gen_stage_elim((mpcx_elim_ld*)F, (mpcx_elim_ld*)LDSP(gL.S + k * SOFF),
+                                 (mpcx_elim_ld*)LDSP(gL.zx + k * (NX + NC)), (mpcx_elim_gd*)a.tr(k),
+                                 (mpcx_elim_gi*)a.prm(k), in);
+  asm volatile(";; STATIC_END");
+  if (!bad) { atomicAdd(&gL.fin[0], in[0]); atomicAdd(&gL.fin[1], in[1]); }
+  return bad;
+}
+#endif
+
 // Factor the KKT matrix bordered by the rhs in a.rhs(); returns the inertia.  Only the
 // round counter, the inertia sums and the diagonal shifts stay live across the calls.
-__device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
+__device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   Lds& L = gL;
   SPROF_DECL
   if (a.lane < 4) L.fin[a.lane] = 0;  // inertia (pos, neg, zero) and singular flag, summed in LDS
@@ -1358,7 +1379,28 @@ __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     }
     wsync();
     SPROF(0);
-    if (lane_now() / G < SR && r * SR + lane_now() / G < N) {
+    int dense = 1;  // this lane's slot needs the dense Bunch-Kaufman path
+#ifdef MPCX_STATIC_ELIM
+    {
+      int sbad = 1;
+      if (lane_now() % G == 0 && lane_now() / G < SR && r * SR + lane_now() / G < N)
+        sbad = static_stage(a, r * SR + lane_now() / G, LDSP(L.u.p.F + (lane_now() / G) * PKS));
+      dense = __shfl(sbad, (lane_now() / G) * G, WAVE);
+      if (lane_now() % G == 0 && lane_now() / G < SR && r * SR + lane_now() / G < N && dense)
+        atomicAdd(&L.ks.n_dense, 1);
+      wsync();
+      if (dense && lane_now() / G < SR && r * SR + lane_now() / G < N) {  // image was eliminated in place
+        const int g = lane_now() % G, slot = lane_now() / G, k = r * SR + slot;
+        ldsd* F = LDSP(L.u.p.F + slot * PKS);
+        ldsi* perm = LDSI(L.u.p.perm + slot * NI);
+        for (int i = g; i < NI; i += G) perm[i] = i;
+        if (kd.mode == LSQ) local_assemble_generic(a, k, g, F, kd);
+        else local_assemble(a, k, g, F, kd);
+      }
+      wsync();
+    }
+#endif
+    if (dense && lane_now() / G < SR && r * SR + lane_now() / G < N) {
       const int g2 = lane_now() % G, slot2 = lane_now() / G;
       const BKOut bo = interior_bk(LDSP(L.u.p.F + slot2 * PKS), LDSI(L.u.p.perm + slot2 * NI),
                                    LDSI(L.u.p.piv + slot2 * NI), g2);
@@ -1385,7 +1427,7 @@ __device__ __noinline__ Inertia factor(const Agent a, const KKTDiag kd) {
         return seq_factor(a, kd);
       }
     }
-    if (lane_now() / G < SR && r * SR + lane_now() / G < N) {
+    if (dense && lane_now() / G < SR && r * SR + lane_now() / G < N) {
       const int g = lane_now() % G, slot = lane_now() / G;
       stage_tail(a, r * SR + slot, g, LDSP(L.u.p.F + slot * PKS), LDSI(L.u.p.perm + slot * NI),
                  LDSI(L.u.p.piv + slot * NI));
@@ -1421,10 +1463,10 @@ __device__ __noinline__ void solve(const Agent a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) tv[NX + c] = L.xs[k * NC + c];
     for (int p = g; p < NI; p += G) {
-      const gdbl* t = a.tr(k) + p * NTR;
-      double u = t[NX + NC];
+      const gdbl* t = a.tr(k) + p;
+      double u = t[(NX + NC) * NI];
 #pragma unroll
-      for (int c = 0; c < NX + NC; ++c) u -= tv[c] * t[c];
+      for (int c = 0; c < NX + NC; ++c) u -= tv[c] * t[c * NI];
       const int o = a.prm(k)[p];
       L.u.sol[k * NB + lblk(o, lkind(o))] = u;
     }
@@ -2049,7 +2091,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     K.fx = sc.fx;
     K.square = sc.square;
   }
-  K.n_fact = 0; K.n_ic = 0; K.n_fallback = 0; K.n_trials = 0; K.n_chain = 0;
+  K.n_fact = 0; K.n_ic = 0; K.n_fallback = 0; K.n_trials = 0; K.n_chain = 0; K.n_dense = 0;
   PROF(0);
   if (M > 0 && OPT(constr_mult_init_max) > 0.0) {
     ls_multipliers(a, OPT(constr_mult_init_max), K.obj_scale);
@@ -2226,7 +2268,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     st.n_factorizations = K.n_fact;
     st.n_trials = K.n_trials;
     st.n_block_chain = K.n_chain;
-    st.reserved = 0;
+    st.n_dense_stages = K.n_dense;
     args.stats[agent] = st;
   }
 }

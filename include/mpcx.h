@@ -121,7 +121,7 @@ typedef struct mpcx_stats {
   int32_t n_factorizations;
   int32_t n_trials;    /* line-search trial points evaluated */
   int32_t n_block_chain; /* factorisations that fell back to the sequential block chain */
-  int32_t reserved;
+  int32_t n_dense_stages; /* stage factorisations redone densely (static sparse pivot rejected) */
 } mpcx_stats;
 
 typedef struct mpcx_handle mpcx_handle;

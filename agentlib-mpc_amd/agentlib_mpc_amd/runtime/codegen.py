@@ -267,7 +267,16 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         if not (ni <= j < ni + nx):
             mark(nloc, j)
     eq_duals = sorted(crow[r] for r in equality_rows(nlp) if crow[r] < ni) if ng else []
-    elim_fac, elim_tra, elim_plan = stage_elim.emit(P, ni, nv, nx, nx + nmu, eq_duals)
+    import math
+
+    pair_w = {}  # preference of a (row, variable) 2x2 pairing: constant entries by magnitude
+    for r in range(ng):
+        for j in range(nl):
+            e = jac[r][j]
+            if crow[r] < ni and lidx(j) < nv and not e.is_const(0.0):
+                c = e.value if e.is_const() else None
+                pair_w[(crow[r], lidx(j))] = (10.0 + max(-5.0, min(5.0, math.log10(abs(c))))) if c else 1.0
+    elim_fac, elim_tra, elim_plan = stage_elim.emit(P, ni, nv, nx, nx + nmu, eq_duals, pair_w)
     elim_lines = elim_fac + [stage_elim.CHECK] + elim_tra
 
     dims = dict(N=nlp.N, NX=nlp.nx, NV=nlp.nv, NG=ng, NPS=nlp.nps, NPG=nlp.npg)
@@ -321,7 +330,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         *gj_lines, "}", "",
         f"__device__ __forceinline__ void gen_stage_hess({sig}, const double sigma, const double* __restrict__ lam, double* __restrict__ hess, const int S, double* __restrict__ lp, const int full) {{",
         *h_lines, "}", "",
-        "// static sparse elimination of the stage interior (runtime/stage_elim.py):",
+        "// >>> device only: static sparse elimination of the stage interior (runtime/stage_elim.py):",
         f"// {len(elim_plan.blocks)} pivot blocks, {elim_plan.n_update} interior updates, {elim_plan.nnz_l} multipliers",
         "#define MPCX_STATIC_ELIM 1",
         "typedef __attribute__((address_space(3))) double mpcx_elim_ld;",
@@ -332,7 +341,8 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         *elim_lines,
         "  inert[0] = pos; inert[1] = neg; inert[2] = 0;",
         "  return 0;",
-        "}", "",
+        "}",
+        "// <<< device only", "",
         '#include "mpcx_ipm.hip"',
         "",
     ]

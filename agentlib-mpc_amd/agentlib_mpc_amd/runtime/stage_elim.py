@@ -78,11 +78,32 @@ def _match(rows: List[List[int]], n_cols: int) -> List[int]:
     return match_col
 
 
-def plan(adj: Sequence[set], ni: int, nv: int, eq_duals: Sequence[int]) -> ElimPlan:
+def _weighted_match(eq_duals, nv, g, weight):
+    """Pairs (variable -> equality row) maximising the summed entry weights among the
+    maximum matchings (Hungarian method); None if scipy is unavailable."""
+    try:
+        import numpy as np
+        from scipy.optimize import linear_sum_assignment
+    except ImportError:  # pragma: no cover
+        return None
+    big = 1e6
+    C = np.full((len(eq_duals), nv), big)
+    for a, r in enumerate(eq_duals):
+        for c in g[r]:
+            if c < nv:
+                C[a, c] = -weight.get((r, c), 1.0)
+    ri, ci = linear_sum_assignment(C)
+    return {int(c): eq_duals[int(a)] for a, c in zip(ri, ci) if C[a, c] < big}
+
+
+def plan(adj: Sequence[set], ni: int, nv: int, eq_duals: Sequence[int], weight=None) -> ElimPlan:
     """Elimination plan for the interior ``0..ni-1`` of a local system whose
     symmetric off-diagonal structure is ``adj`` (indices >= ni are trailing rows:
     they receive fill but never pivot).  ``eq_duals``: interior dual indices
-    (nv <= i < ni) of equality rows."""
+    (nv <= i < ni) of equality rows; ``weight[(row, var)]``: preference of a pairing
+    (constant Jacobian entries of magnitude >= 1 never vanish; a state-dependent entry,
+    e.g. a network derivative, can be small at the iterate and make the 2x2 pivot
+    nearly singular)."""
     g = [set(a) for a in adj]
     rows = [sorted(c for c in g[r] if c < nv) for r in eq_duals]
     mc = _match(rows, nv)
@@ -90,6 +111,10 @@ def plan(adj: Sequence[set], ni: int, nv: int, eq_duals: Sequence[int]) -> ElimP
     for v, r in enumerate(mc):
         if r >= 0:
             pairs[v] = eq_duals[r]
+    if weight:
+        wp = _weighted_match(eq_duals, nv, g, weight)
+        if wp is not None and len(wp) == len(pairs):
+            pairs = wp
     paired = set(pairs) | set(pairs.values())
     phase1 = [(v, d) for v, d in pairs.items()] + [(i,) for i in range(nv, ni) if i not in paired]
     phase2 = [(i,) for i in range(nv) if i not in paired]
@@ -117,7 +142,7 @@ def plan(adj: Sequence[set], ni: int, nv: int, eq_duals: Sequence[int]) -> ElimP
 
 
 def emit(P: Sequence[Sequence[bool]], ni: int, nv: int, nx: int, nc: int,
-         eq_duals: Sequence[int]) -> Tuple[List[str], List[str], ElimPlan]:
+         eq_duals: Sequence[int], weight=None) -> Tuple[List[str], List[str], ElimPlan]:
     """C++ of ``gen_stage_elim`` for a local system with structure ``P`` ((nloc+1)^2,
     symmetric, border row last; trailing rows x_k = ni..ni+nx-1, c_k = ni+nx..ni+nx+nc-1,
     border = ni+nx+nc), as two parts:
@@ -135,7 +160,7 @@ def emit(P: Sequence[Sequence[bool]], ni: int, nv: int, nx: int, nc: int,
     ntr = nx + nc + 1
     assert n == ni + ntr
     adj = [set(j for j in range(n) if j != i and (P[i][j] or P[j][i])) for i in range(n)]
-    pl = plan(adj, ni, nv, eq_duals)
+    pl = plan(adj, ni, nv, eq_duals, weight)
 
     def pk(i, j):
         i, j = max(i, j), min(i, j)

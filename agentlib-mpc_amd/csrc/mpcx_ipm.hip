@@ -118,7 +118,8 @@ constexpr long O_SOL = O_KD + M;                 // [N][NB] solution            
 constexpr long O_FAC = O_SOL + (long)N * NB;     // [N][NB*LDB] block inverses   (block chain)
 constexpr long O_CPL = O_FAC + (long)N * NB * LDB;  // [N][NB*NX] couplings      (block chain)
 constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [N][PKS] packed local systems (evaluators, rhs)
-constexpr long WS_DOUBLES = O_LP + (long)N * PKS;
+constexpr long O_DG = O_LP + (long)N * PKS;        // [N][NLOC] diagonal terms (rhs phases; Newton mode)
+constexpr long WS_DOUBLES = O_DG + (long)N * NLOC;
 
 using Args = mpcx_kernel_args;
 // kernel arguments read in place from the kernarg segment (address space 4: scalar
@@ -382,6 +383,7 @@ struct Agent {
   __device__ gdbl* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
   __device__ gdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
   __device__ gdbl* lp(int k) const { return ws + O_LP + (long)k * PKS; }
+  __device__ gdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
 };
 
 // constraint classes: 0 equality, 1 inequality with a finite bound, 2 free
@@ -975,7 +977,17 @@ __device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F
       wsync();
     }
   }
-  local_diagonal(a, k, g, F, kd, fm);
+  // diagonal terms precomputed by the rhs phases (coalesced, one pass over the
+  // variables / constraints): primal Sigma_x (+ delta_w here), dual diagonal
+  const gdbl* dg = a.dg(k);
+  for (int i = g; i < NLOC; i += G) {
+    const int ki = lkind(i);
+    const double d = dg[i];
+    const int ii = pko(i) + i;
+    if ((ki == 0 || ki == 3) && !((fm >> i) & 1ull)) F[ii] += d + kd.dw;
+    if (kdual(ki)) F[ii] = d;
+  }
+  wsync();
 }
 
 // Bunch-Kaufman over the NI interior pivots of one stage (G lanes, packed lower
@@ -1705,6 +1717,7 @@ __device__ __noinline__ void rhs_primal(const Agent a, double mu, double obj_sca
     const bool on = i >= NX && i < NW;
     const int ii = on ? i : NX;
     const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii];
+    const double zl = a.zL()[ii], zu = a.zU()[ii];
     const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
     if (on) {
       double r = 0.0;
@@ -1715,15 +1728,17 @@ __device__ __noinline__ void rhs_primal(const Agent a, double mu, double obj_sca
         r = -(gphi + jt);
       }
       const int b = (i - NX) / NP, off = (i - NX) % NP;
+      const int li = off < NV ? off : LX1 + off - NV;
       a.rhs(b)[off] = r;
-      a.lp(b)[pko(RB) + (off < NV ? off : LX1 + off - NV)] = r;
+      a.lp(b)[pko(RB) + li] = r;
+      a.dg(b)[li] = sigma_x_v(xv, lo, hi, zl, zu);
     }
   }
 }
 
 // dual rows of the rhs (depend on delta_w); ends with the barrier that hands
 // the whole rhs to the factorisation lanes
-__device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw) {
+__device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, double dc) {
   const int lane = a.lane;
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
@@ -1749,6 +1764,7 @@ __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw) {
       }
       a.rhs(c / NG)[NP + c % NG] = rr;
       a.lp(c / NG)[pko(RB) + crow(c % NG)] = rr;
+      a.dg(c / NG)[crow(c % NG)] = -dual_diag_v(cl, sigma_s_v(sv, slo, sup, vl, vu), KKTDiag{dw, dc, NEWTON});
     }
   }
   sync();
@@ -2164,7 +2180,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     int ok = 0;
 #pragma unroll 1
     for (int attempt = 0; attempt < 60; ++attempt) {
-      rhs_dual(a, K.mu, K.dw);
+      rhs_dual(a, K.mu, K.dw, K.dc);
       const Inertia in = factor(a, KKTDiag{K.dw, K.dc, NEWTON});
       K.n_fact += 1;
       K.n_chain += gL.seq;

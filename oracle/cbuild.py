@@ -134,8 +134,14 @@ def build_generated(gen, march: str = "native") -> pathlib.Path:
     if out.exists():
         return out
     OUT.parent.mkdir(parents=True, exist_ok=True)
-    body = [ln for ln in gen.source.splitlines()
-            if not ln.startswith("#include <hip/") and not ln.startswith('#include "mpcx_ipm.hip"')]
+    body, device_only = [], False
+    for ln in gen.source.splitlines():  # the kernel's device-only section (static elimination) is dropped
+        if ln.startswith("// >>> device only"):
+            device_only = True
+        if not device_only and not ln.startswith("#include <hip/") and not ln.startswith('#include "mpcx_ipm.hip"'):
+            body.append(ln)
+        if ln.startswith("// <<< device only"):
+            device_only = False
     src = OUT.parent / f"gen_{key}.inc"
     src.write_text("\n".join(body) + "\n")
     core_o = OUT.parent / f"core_{key}.o"

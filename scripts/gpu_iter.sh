@@ -1,6 +1,6 @@
 # kernel iteration: static-vs-oracle diagnostic, IPM parity, C3 phase profile, C3 bench leg
 set -o pipefail
-mkdir -p gpurun_out
+mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0 --c2-blocks 0"
 timeout -k 10 300 python -u scripts/static_diag.py > gpurun_out/diag_static.txt 2>&1 && \
@@ -8,3 +8,6 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_ipm.py -m gpu -q --timeout 
 timeout -k 10 200 python scripts/prof_phases.py > gpurun_out/phases.txt 2>&1 && \
 timeout -k 10 200 $B > gpurun_out/c3.json 2> gpurun_out/c3.err
 echo "iter exit $?"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc/fetch -o fetch --output-format csv -- $B > gpurun_out/pmc/fetch.out 2> gpurun_out/pmc/fetch.err && \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc/write -o write --output-format csv -- $B > gpurun_out/pmc/write.out 2> gpurun_out/pmc/write.err
+echo "pmc exit $?"

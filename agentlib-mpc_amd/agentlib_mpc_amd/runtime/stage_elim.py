@@ -57,6 +57,26 @@ class ElimPlan:
     cols: List[List[int]]             # per block: remaining interior neighbours (filled graph)
     n_update: int                     # entry updates of the interior elimination
     nnz_l: int                        # off-diagonal multiplier entries (per pivot index)
+    flops: int = 0                    # FP64 operations of the generated body (fma = 2)
+
+
+def count_flops(lines: Sequence[str]) -> int:
+    """FP64 operations of generated straight-line code: fma counts 2, every other
+    arithmetic operator outside index brackets 1 (comparisons are not counted)."""
+    import re
+
+    n = 0
+    for ln in lines:
+        s = ln.strip()
+        if s.startswith("//") or s.startswith("__builtin") or s.startswith("bad |=") or s.startswith("if ("):
+            continue
+        if "=" not in s:
+            continue
+        rhs = s.split("=", 1)[1]
+        rhs = re.sub(r"\[[^\]]*\]", "", rhs)      # drop index expressions
+        n += 2 * rhs.count("fma(")
+        n += len(re.findall(r"(?<=[\w)\s])\s*[-+*/]\s*(?=[\w(])", rhs))
+    return n
 
 
 def _match(rows: List[List[int]], n_cols: int) -> List[int]:
@@ -280,4 +300,5 @@ def emit(P: Sequence[Sequence[bool]], ni: int, nv: int, nx: int, nc: int,
             tra.append(f"  {dest} = {orig(ri, ti) or '0.0'} - ({schur_dot(ri, w)});")
     for p in range(ni):
         tra.append(f"  PRM[{p}] = {p};")
+    pl.flops = count_flops(fac) + count_flops(tra)
     return fac, tra, pl

@@ -356,5 +356,6 @@ def stats_to_dicts(raw_bytes) -> list:
             "n_factorizations": s.n_factorizations,
             "n_trials": s.n_trials,
             "n_block_chain": s.n_block_chain,
+            "n_dense_stages": s.n_dense_stages,
         })
     return out

@@ -52,6 +52,8 @@ class GeneratedModel:
     elim: object = None
     elim_lines: list = dataclasses.field(default_factory=list)
     pattern: list = dataclasses.field(default_factory=list)
+    #: compact stage image: (row, column) of each stored entry (lp, LDS image, elimination)
+    compact: list = dataclasses.field(default_factory=list)
 
 
 def _bindings(nlp: StageNLP) -> Dict[sx.Expr, str]:
@@ -279,6 +281,28 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     elim_fac, elim_tra, elim_plan = stage_elim.emit(P, ni, nv, nx, nx + nmu, eq_duals, pair_w)
     elim_lines = elim_fac + [stage_elim.CHECK] + elim_tra
 
+    # -- compact stage image: structural nonzeros + elimination fill only --
+    # order: diagonal (i, i) at i, border row (rhs, j) at nloc + 1 + j, then the other
+    # entries of the pattern and of the fill in packed order.  The evaluators write it
+    # (lp), the rhs phases its border and the diagonal terms, the kernel copies it to LDS
+    # and the generated elimination works on it in place (csrc/mpcx_ipm.hip, factor).
+    n_img = nloc + 1
+    used_pk = {pk(i, j) for i in range(n_img) for j in range(i + 1) if P[i][j]}
+    for ln in elim_lines:
+        used_pk.update(int(m.group(1)) for m in re.finditer(r"F\[(\d+)\]", ln))
+    unpk = {pk(i, j): (i, j) for i in range(n_img) for j in range(i + 1)}
+    compact = [(i, i) for i in range(n_img)] + [(nloc, j) for j in range(nloc)]
+    head = {pk(i, j) for i, j in compact}
+    compact += [unpk[t] for t in sorted(used_pk - head)]
+    cix = {pk(i, j): c for c, (i, j) in enumerate(compact)}
+
+    def to_compact(lines, arr):
+        return [re.sub(rf"\b{arr}\[(\d+)\]", lambda m: f"{arr}[{cix[int(m.group(1))]}]", ln) for ln in lines]
+
+    elim_lines = to_compact(elim_lines, "F")
+    gj_lines = to_compact(gj_lines, "lp")
+    h_lines = to_compact(h_lines, "lp")
+
     dims = dict(N=nlp.N, NX=nlp.nx, NV=nlp.nv, NG=ng, NPS=nlp.nps, NPG=nlp.npg)
     ts = nlp.ts if ts is None else ts
     flops = {
@@ -290,18 +314,17 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
            "hess": sum(1 for a, _ in h_assign)}
 
     # LDS budget per one-wave workgroup: 9.6 KB keeps 16 agents per CU; a problem
-    # where not even two stage systems fit gets up to 40 KB (4 agents per CU) so
-    # its stages are factorised in one or two rounds (mirrors SLOT_BYTES /
+    # where not even two compact stage images fit gets up to 40 KB (4 agents per CU) so
+    # its stages are eliminated in one or two rounds (mirrors CSLOT_BYTES /
     # OTHER_BYTES in csrc/mpcx_ipm.hip)
-    N_, NX_, NI_ = nlp.N, nlp.nx, ni
+    N_, NX_ = nlp.N, nlp.nx
     nxp, ncp = max(NX_, 1), max(NX_ + nmu, 1)
-    pks = ((nloc + 1) * (nloc + 2) // 2) | 1
-    slot = 8 * pks + 8 * NI_
+    cslot = 8 * (len(compact) | 1)
     soff = nxp * nxp + ncp * ncp + ncp * nxp
     other = 8 * (N_ * soff + N_ * ncp * ncp + N_ * (NX_ + ncp) + N_ * ncp + 3 * ncp * ncp + 64 + nlp.npg
-                 + N_ * nlp.nps + N_) + 8 * ncp + 64 + 336  # 336: KState
-    need = other + N_ * slot
-    lds_target = 9600 if other + 2 * slot <= 9600 else min(need, 40960)
+                 + N_ * nlp.nps + N_) + 8 * ncp + 64 + 336 + 16  # 336: KState, 16: fixed-stage masks
+    need = other + N_ * cslot
+    lds_target = 9600 if other + 2 * cslot <= 9600 else min(need, 40960)
 
     sig = "const double* __restrict__ L, const double* __restrict__ PS, const double* __restrict__ PG, const double TK"
     out: List[str] = [
@@ -315,6 +338,9 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         f"#define MPCX_TS {float(ts)!r}",
         f"#define MPCX_ABI {KERNEL_ABI_VERSION}",
         f"#define MPCX_LDS_TARGET {lds_target}",
+        f"#define MPCX_NCPT {len(compact)}",
+        f"#define MPCX_CPK_INIT {', '.join(str(pk(i, j)) for i, j in compact)}",
+        f"#define MPCX_CIJ_INIT {', '.join(str(i | (j << 8)) for i, j in compact)}",
         *(["#define MPCX_FORCE_BLOCK_CHAIN 1"] if force_chain else []),
         *([f"#define MPCX_NMU {nmu}",
            f"#define MPCX_CROW_INIT {', '.join(map(str, crow))}",
@@ -359,4 +385,5 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         src = re.sub(r"ANN(\d+)_", lambda m: f"ANN{local[int(m.group(1))]}_", src)
     key = hashlib.sha1(src.encode()).hexdigest()[:16]
     return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz, block_chain_only=force_chain,
-                          bordered_rows=list(bordered), elim=elim_plan, elim_lines=elim_lines, pattern=P)
+                          bordered_rows=list(bordered), elim=elim_plan, elim_lines=elim_lines, pattern=P,
+                          compact=compact)

@@ -70,3 +70,9 @@ def pack(A: np.ndarray) -> np.ndarray:
     """Packed lower triangle (row-major, i*(i+1)/2 + j) of a symmetric matrix."""
     n = A.shape[0]
     return np.concatenate([A[i, :i + 1] for i in range(n)])
+
+
+def compact(A: np.ndarray, cmap) -> np.ndarray:
+    """Compact stage image of a symmetric matrix: entry c holds A[i, j] for the
+    ``(i, j)`` of ``GeneratedModel.compact`` (structural nonzeros + fill)."""
+    return np.array([A[i, j] for i, j in cmap], dtype=float)

@@ -99,6 +99,18 @@ static_assert(NI > 0, "stage interior must be non-empty");
 __constant__ int kCROW[NG > 0 ? NG : 1] = {MPCX_CROW_INIT};    // row r -> local index
 __constant__ int kLROW[NLOC + 1] = {MPCX_LROW_INIT};           // local dual index -> row
 static_assert(NLOC < 64, "local fixed-variable masks are 64-bit");
+static_assert(N <= 64, "stage masks are 64-bit");
+// Compact stage image (generated, runtime/codegen.py): only the structural nonzeros of the
+// local system and the fill of the static elimination are stored.  Entry i < NLOC + 1 is
+// the diagonal (i, i), entry CB + j the border (rhs) entry (RB, j), the rest follow in
+// packed order; kCPK maps an entry to its packed dense index (dense fallback), kCIJ to
+// (row | column << 8).  The evaluators write it (a.lp), the factorisation copies it to LDS.
+constexpr int NCPT = MPCX_NCPT;
+constexpr int NCS = NCPT | 1;             // odd stride between stage images
+constexpr int CB = NLOC + 1;              // first border entry
+static_assert(NCPT >= CB + NLOC, "compact image holds the diagonal and the border row");
+__constant__ unsigned short kCPK[NCPT] = {MPCX_CPK_INIT};
+__constant__ unsigned short kCIJ[NCPT] = {MPCX_CIJ_INIT};
 
 // workspace layout (doubles per agent)
 constexpr long O_X = 0, O_S = O_X + NW, O_LAM = O_S + M, O_ZL = O_LAM + M, O_ZU = O_ZL + NW;
@@ -117,8 +129,8 @@ constexpr long O_KD = O_KX + (long)N * NP;       // [M] dual KKT diagonal       
 constexpr long O_SOL = O_KD + M;                 // [N][NB] solution             (block chain)
 constexpr long O_FAC = O_SOL + (long)N * NB;     // [N][NB*LDB] block inverses   (block chain)
 constexpr long O_CPL = O_FAC + (long)N * NB * LDB;  // [N][NB*NX] couplings      (block chain)
-constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [N][PKS] packed local systems (evaluators, rhs)
-constexpr long O_DG = O_LP + (long)N * PKS;        // [N][NLOC] diagonal terms (rhs phases; Newton mode)
+constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [N][NCS] compact local systems (evaluators, rhs)
+constexpr long O_DG = O_LP + (long)N * NCS;        // [N][NLOC] diagonal terms (rhs phases; Newton mode)
 constexpr long WS_DOUBLES = O_DG + (long)N * NLOC;
 
 using Args = mpcx_kernel_args;
@@ -226,9 +238,10 @@ __host__ __device__ constexpr int pow2floor(int v) { int p = 1; while (p * 2 <= 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // packed system + perm/piv
+constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // dense packed system + perm/piv (fallback)
+constexpr int CSLOT_BYTES = 8 * NCS;          // compact image (static elimination)
 constexpr int OTHER_BYTES = 8 * (N * SOFF + N * NCC + N * (NX + NCP) + N * NCP + 3 * NCC + 2 * MAXF + NPAR + N) +
-                            8 * NCP + 64 + 336;  // 336: KState
+                            8 * NCP + 64 + 336 + 16;  // 336: KState, 16: fixed-stage masks
 #ifndef MPCX_LDS_TARGET
 #define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
 #endif
@@ -236,6 +249,12 @@ constexpr int OTHER_BYTES = 8 * (N * SOFF + N * NCC + N * (NX + NCP) + N * NCP +
 #undef MPCX_LDS_TARGET
 #define MPCX_LDS_TARGET MPCX_LDS_TARGET_OVERRIDE
 #endif
+// static path: SRC compact images per round, one lane eliminates a stage, GC lanes assemble it
+constexpr int SRC0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / CSLOT_BYTES));
+constexpr int CROUNDS = (N + SRC0 - 1) / SRC0;
+constexpr int SRC = (N + CROUNDS - 1) / CROUNDS;  // stages per round (balanced)
+constexpr int GC = pow2floor(WAVE / SRC);          // lanes per stage (assembly)
+// dense Bunch-Kaufman path (stages the static plan rejects): SR dense images per round
 constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / SLOT_BYTES));
 constexpr int ROUNDS = (N + SR0 - 1) / SR0;
 constexpr int SR = (N + ROUNDS - 1) / ROUNDS;   // stages per round (balanced)
@@ -261,6 +280,9 @@ struct ParLds {
   int perm[SR * NI];
   int piv[SR * NI];
 };
+struct ParCLds {
+  double F[SRC * NCS];
+};
 struct TrialLds {
   double xt[NW];
   double gt[MM];
@@ -268,6 +290,7 @@ struct TrialLds {
 union LinLds {
   SeqLds s;
   ParLds p;
+  ParCLds c;
   double sol[N * NB];   // Newton step, block order [V, X1, lambda] per stage
   TrialLds t;           // line-search trial point (x, scaled g)
 };
@@ -323,6 +346,7 @@ struct Lds {
   int cperm[NCP];
   int cpiv[NCP];
   int fin[4];              // factor(): summed interior inertia (pos, neg, zero) and singular flag
+  unsigned int dmask[2];   // factor(): stages the static plan rejected (dense path)
   int seq;                 // 1: last factorisation used the block chain
   int want_sdh;            // 1: keep the strided stage Hessians (block chain in use)
   int sdh_ok;              // 1: the workspace Hessians match the last eval_hess
@@ -382,7 +406,7 @@ struct Agent {
   __device__ gdbl* sol(int k) const { return ws + O_SOL + (long)k * NB; }
   __device__ gdbl* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
   __device__ gdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
-  __device__ gdbl* lp(int k) const { return ws + O_LP + (long)k * PKS; }
+  __device__ gdbl* lp(int k) const { return ws + O_LP + (long)k * NCS; }
   __device__ gdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
 };
 
@@ -886,10 +910,11 @@ __device__ __forceinline__ int lblk(int i, int kind) {
 }
 
 // diagonal terms (barrier Sigma + delta_w, dual diagonal) and fixed variables
+template <int GG, bool COMPACT>
 __device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd* F, const KKTDiag kd,
                                                unsigned long long fm) {
   const gdbl* ws = a.ws;
-  for (int i = g; i < NLOC; i += G) {
+  for (int i = g; i < NLOC; i += GG) {
     const int ki = lkind(i);
     const bool prim = (ki == 0 || ki == 3);
     const bool fixd = (fm >> i) & 1ull;
@@ -899,93 +924,106 @@ __device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd
     const double zl = ws[O_ZL + vi], zu = ws[O_ZU + vi];
     const double lbv = ws[O_LB + c], ubv = ws[O_UB + c], sv = ws[O_S + c];
     const double sl = ws[O_SL + c], su = ws[O_SU + c], vl = ws[O_VL + c], vu = ws[O_VU + c];
-    const int ii = pko(i) + i;
+    const int ii = COMPACT ? i : pko(i) + i;
     if (prim && !fixd) F[ii] += (kd.mode == LSQ) ? 1.0 : sigma_x_v(xv, lo, hi, zl, zu) + kd.dw;
     if (kdual(ki)) F[ii] = -dual_diag_v(cls_of(lbv, ubv, sl, su), sigma_s_v(sv, sl, su, vl, vu), kd);
   }
   wsync();
 }
 
-// assemble stage k's bordered local system into F (packed lower), G lanes: generic
-// gather from the strided derivative arrays (least-squares multiplier system)
+// entry (i, j), i >= j, of stage k's bordered local system gathered from the strided
+// derivative arrays (least-squares multiplier system; diagonal terms added afterwards)
+__device__ __forceinline__ double generic_entry(const Agent a, int k, int i, int j, unsigned long long fm,
+                                                const KKTDiag kd) {
+  const gdbl* ws = a.ws;
+  const int ki = lkind(i), kj = lkind(j);
+  const bool pi = (ki == 0 || ki == 2 || ki == 3), pj = (kj == 0 || kj == 2 || kj == 3);
+  const bool fi = pi && ((fm >> i) & 1ull), fj = pj && ((fm >> j) & 1ull);
+  const bool pp = pi && pj;
+  const bool dp = (kdual(ki) && pj) || (kdual(kj) && pi);
+  const bool bd = (ki == 4) && (kj != 2 && kj != 4);
+  long off = 0, goff = O_GS;
+  if (pp) {
+    off = O_SDH + ((long)lnl(i, ki) * NL + lnl(j, kj)) * N + k;
+  } else if (dp) {
+    const int r = lrow(kdual(ki) ? i : j), q = (kdual(ki) ? j : i), kq = (kdual(ki) ? kj : ki);
+    off = O_SDJ + ((long)r * NL + lnl(q, kq)) * N + k;
+    goff = O_GS + k * NG + r;
+  } else if (bd) {
+    off = O_RHS + (long)k * NB + lblk(j, kj);
+  }
+  const double d = ws[off];
+  const double gsv = ws[goff];
+  double v = 0.0;
+  if (pp) v = (fi || fj) ? ((i == j && ki == 0) ? 1.0 : 0.0) : (kd.mode == LSQ ? 0.0 : d);
+  else if (dp) v = (fi || fj) ? 0.0 : gsv * d;
+  else if (bd) v = d;
+  return v;
+}
+
+// assemble stage k's bordered local system into F, GG lanes: generic gather from the
+// strided derivative arrays (least-squares multiplier system); COMPACT: the compact
+// image (static path), else the dense packed lower triangle (Bunch-Kaufman path)
+template <int GG, bool COMPACT>
 __device__ __noinline__ void local_assemble_generic(const Agent a, int k, int g, ldsd* F, const KKTDiag kd) {
   const unsigned long long fm = gL.fixm[k];
-  const gdbl* ws = a.ws;
-  // pass 1: derivative / rhs entries (one or two independent loads per entry)
 #pragma unroll 4
-  for (int t = g; t < PKB; t += G) {
-    int i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-    if (pko(i + 1) <= t) ++i;
-    if (pko(i) > t) --i;
-    const int j = t - pko(i);
-    const int ki = lkind(i), kj = lkind(j);
-    const bool pi = (ki == 0 || ki == 2 || ki == 3), pj = (kj == 0 || kj == 2 || kj == 3);
-    const bool fi = pi && ((fm >> i) & 1ull), fj = pj && ((fm >> j) & 1ull);
-    const bool pp = pi && pj;
-    const bool dp = (kdual(ki) && pj) || (kdual(kj) && pi);
-    const bool bd = (ki == 4) && (kj != 2 && kj != 4);
-    long off = 0, goff = O_GS;
-    if (pp) {
-      off = O_SDH + ((long)lnl(i, ki) * NL + lnl(j, kj)) * N + k;
-    } else if (dp) {
-      const int r = lrow(kdual(ki) ? i : j), q = (kdual(ki) ? j : i), kq = (kdual(ki) ? kj : ki);
-      off = O_SDJ + ((long)r * NL + lnl(q, kq)) * N + k;
-      goff = O_GS + k * NG + r;
-    } else if (bd) {
-      off = O_RHS + (long)k * NB + lblk(j, kj);
+  for (int t = g; t < (COMPACT ? NCPT : PKB); t += GG) {
+    int i, j;
+    if constexpr (COMPACT) {
+      i = kCIJ[t] & 255; j = kCIJ[t] >> 8;
+    } else {
+      i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+      if (pko(i + 1) <= t) ++i;
+      if (pko(i) > t) --i;
+      j = t - pko(i);
     }
-    const double d = ws[off];
-    const double gsv = ws[goff];
-    double v = 0.0;
-    if (pp) v = (fi || fj) ? ((i == j && ki == 0) ? 1.0 : 0.0) : (kd.mode == LSQ ? 0.0 : d);
-    else if (dp) v = (fi || fj) ? 0.0 : gsv * d;
-    else if (bd) v = d;
-    F[t] = v;
+    F[t] = generic_entry(a, k, i, j, fm, kd);
   }
   wsync();
   // pass 2: diagonal terms (barrier Sigma + delta_w, dual diagonal)
-  local_diagonal(a, k, g, F, kd, fm);
+  local_diagonal<GG, COMPACT>(a, k, g, F, kd, fm);
 }
 
-// Newton system of stage k: contiguous copy of the packed image the evaluators
-// and the rhs phases wrote, then fixed variables and diagonal terms
-constexpr int EPG = (PKB + G - 1) / G;  // packed entries per lane
+// Newton system of stage k from the compact image the evaluators and the rhs phases
+// wrote (one coalesced read): fixed variables (identity row for V, empty row for a state,
+// chained as 1) and the diagonal terms the rhs phases precomputed (primal Sigma_x,
+// + delta_w here; dual diagonal) are applied on the way.  DENSE: scattered into a zeroed
+// dense packed image (Bunch-Kaufman path), else the compact image itself (static path).
+template <int GG, bool DENSE>
 __device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F, const KKTDiag kd) {
+  constexpr int EPC = (NCPT + GG - 1) / GG;  // compact entries per lane
   const unsigned long long fm = gL.fixm[k];
   const gdbl* src = a.lp(k);
-  double v[EPG];
-#pragma unroll
-  for (int e = 0; e < EPG; ++e) {
-    const int t = g + e * G;
-    v[e] = src[t < PKB ? t : 0];
-  }
-#pragma unroll
-  for (int e = 0; e < EPG; ++e) {
-    const int t = g + e * G;
-    if (t < PKB) F[t] = v[e];
-  }
-  wsync();
-  if (fm != 0ull) {  // fixed variables: identity row (V) or empty row (states, chained as 1)
-#pragma unroll 1
-    for (int q = 0; q < NLOC; ++q) {
-      if (!((fm >> q) & 1ull)) continue;
-      for (int j = g; j <= RB; j += G) {
-        if (j == q) F[pko(q) + q] = (lkind(q) == 0) ? 1.0 : 0.0;
-        else if (j < q) F[pko(q) + j] = 0.0;
-        else F[pko(j) + q] = 0.0;
-      }
-      wsync();
-    }
-  }
-  // diagonal terms precomputed by the rhs phases (coalesced, one pass over the
-  // variables / constraints): primal Sigma_x (+ delta_w here), dual diagonal
   const gdbl* dg = a.dg(k);
-  for (int i = g; i < NLOC; i += G) {
-    const int ki = lkind(i);
-    const double d = dg[i];
-    const int ii = pko(i) + i;
-    if ((ki == 0 || ki == 3) && !((fm >> i) & 1ull)) F[ii] += d + kd.dw;
-    if (kdual(ki)) F[ii] = d;
+  if constexpr (DENSE) {
+    for (int t = g; t < PKB; t += GG) F[t] = 0.0;
+    wsync();
+  }
+  double v[EPC], dv[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int t = g + e * GG;
+    v[e] = src[t < NCPT ? t : 0];
+    dv[e] = dg[t < NLOC ? t : 0];
+  }
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) {
+    const int t = g + e * GG;
+    if (t >= NCPT) continue;
+    double x = v[e];
+    bool fix = false;
+    if (fm != 0ull) {
+      const int ij = kCIJ[t], i = ij & 255, j = ij >> 8;
+      fix = (((fm >> i) | (fm >> j)) & 1ull) != 0ull;
+      if (fix) x = (i == j && lkind(i) == 0) ? 1.0 : 0.0;
+    }
+    if (t < NLOC) {  // diagonal (t, t)
+      const int ki = lkind(t);
+      if ((ki == 0 || ki == 3) && !fix) x += dv[e] + kd.dw;
+      if (kdual(ki)) x = dv[e];
+    }
+    F[DENSE ? (int)kCPK[t] : t] = x;
   }
   wsync();
 }
@@ -1370,82 +1408,112 @@ __device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* F) {
 }
 #endif
 
+// q-th set bit of a stage mask (q < popcount)
+__device__ __forceinline__ int nth_bit(unsigned long long m, int q) {
+  for (int i = 0; i < q; ++i) m &= m - 1ull;
+  return __ffsll((long long)m) - 1;
+}
+
 // Factor the KKT matrix bordered by the rhs in a.rhs(); returns the inertia.  Only the
 // round counter, the inertia sums and the diagonal shifts stay live across the calls.
+// Pass 1 (static): SRC compact stage images per round, assembled by GC lanes each and
+// eliminated by the generated sparse LDL^T, one lane per stage.  Pass 2 (dense, only
+// for the stages pass 1 rejected): SR dense packed images per round, Bunch-Kaufman by
+// G lanes each (interior_bk + stage_tail).
 __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   Lds& L = gL;
   SPROF_DECL
   if (a.lane < 4) L.fin[a.lane] = 0;  // inertia (pos, neg, zero) and singular flag, summed in LDS
+  if (a.lane < 2) L.dmask[a.lane] = 0u;
   wsync();
+#ifdef MPCX_FORCE_BLOCK_CHAIN  // always take the sequential block chain (diagnostics)
+  if constexpr (NX > 0) {
+    sync();
+    if (!L.sdh_ok && kd.mode != LSQ) {
+      eval_hess_impl(a, L.hsig, 1);
+      eval_gj_ws(a, a.x(), 1);
+      sync();
+    }
+    if (a.lane == 0) { L.seq = 1; L.want_sdh = 1; }
+    sync();
+    return seq_factor(a, kd);
+  }
+#endif
+#ifdef MPCX_STATIC_ELIM
 #pragma unroll 1
-  for (int r = 0; r < ROUNDS; ++r) {
-    const int g = lane_now() % G, slot = lane_now() / G;
-    const int k = r * SR + slot;
-    const bool act = slot < SR && k < N;
-    if (act) {
-      ldsd* F = LDSP(L.u.p.F + slot * PKS);
-      ldsi* perm = LDSI(L.u.p.perm + slot * NI);
-      for (int i = g; i < NI; i += G) perm[i] = i;
-      if (kd.mode == LSQ) local_assemble_generic(a, k, g, F, kd);
-      else local_assemble(a, k, g, F, kd);
+  for (int r = 0; r < CROUNDS; ++r) {
+    {
+      const int g = lane_now() % GC, slot = lane_now() / GC, k = r * SRC + slot;
+      if (slot < SRC && k < N) {
+        ldsd* F = LDSP(L.u.c.F + slot * NCS);
+        if (kd.mode == LSQ) local_assemble_generic<GC, true>(a, k, g, F, kd);
+        else local_assemble<GC, false>(a, k, g, F, kd);
+      }
     }
     wsync();
     SPROF(0);
-    int dense = 1;  // this lane's slot needs the dense Bunch-Kaufman path
-#ifdef MPCX_STATIC_ELIM
     {
-      int sbad = 1;
-      if (lane_now() % G == 0 && lane_now() / G < SR && r * SR + lane_now() / G < N)
-        sbad = static_stage(a, r * SR + lane_now() / G, LDSP(L.u.p.F + (lane_now() / G) * PKS));
-      dense = __shfl(sbad, (lane_now() / G) * G, WAVE);
-      if (lane_now() % G == 0 && lane_now() / G < SR && r * SR + lane_now() / G < N && dense)
+      const int slot = lane_now(), k = r * SRC + slot;  // one lane per stage
+      if (slot < SRC && k < N && static_stage(a, k, LDSP(L.u.c.F + slot * NCS))) {
+        atomicOr(&L.dmask[k >> 5], 1u << (k & 31));
         atomicAdd(&L.ks.n_dense, 1);
-      wsync();
-      if (dense && lane_now() / G < SR && r * SR + lane_now() / G < N) {  // image was eliminated in place
-        const int g = lane_now() % G, slot = lane_now() / G, k = r * SR + slot;
-        ldsd* F = LDSP(L.u.p.F + slot * PKS);
-        ldsi* perm = LDSI(L.u.p.perm + slot * NI);
-        for (int i = g; i < NI; i += G) perm[i] = i;
-        if (kd.mode == LSQ) local_assemble_generic(a, k, g, F, kd);
-        else local_assemble(a, k, g, F, kd);
-      }
-      wsync();
-    }
-#endif
-    if (dense && lane_now() / G < SR && r * SR + lane_now() / G < N) {
-      const int g2 = lane_now() % G, slot2 = lane_now() / G;
-      const BKOut bo = interior_bk(LDSP(L.u.p.F + slot2 * PKS), LDSI(L.u.p.perm + slot2 * NI),
-                                   LDSI(L.u.p.piv + slot2 * NI), g2);
-      if (lane_now() % G == 0) {
-        atomicAdd(&L.fin[0], bo.pos); atomicAdd(&L.fin[1], bo.neg); atomicAdd(&L.fin[2], bo.zero);
-        atomicOr(&L.fin[3], bo.bad);
       }
     }
     wsync();
     SPROF(1);
-#ifdef MPCX_FORCE_BLOCK_CHAIN  // always take the sequential block chain (MHE lifts; diagnostics)
-    bad = 1;
+  }
+  const unsigned long long dm = ((unsigned long long)L.dmask[1] << 32) | L.dmask[0];
+#else
+  const unsigned long long dm = (N == 64) ? ~0ull : ((1ull << N) - 1ull);
 #endif
-    if constexpr (NX > 0) {
-      if (L.fin[3] != 0) {  // singular stage interior: block chain instead
-        sync();
-        if (!L.sdh_ok && kd.mode != LSQ) {  // the chain reads the strided Hessians and jacobian
-          eval_hess_impl(a, L.hsig, 1);
-          eval_gj_ws(a, a.x(), 1);
-          sync();
+  if (dm != 0ull) {
+    const int nd = __popcll(dm);
+#pragma unroll 1
+    for (int r = 0; r * SR < nd; ++r) {
+      {
+        const int g = lane_now() % G, slot = lane_now() / G, q = r * SR + slot;
+        if (slot < SR && q < nd) {
+          const int k = nth_bit(dm, q);
+          ldsd* F = LDSP(L.u.p.F + slot * PKS);
+          ldsi* perm = LDSI(L.u.p.perm + slot * NI);
+          for (int i = g; i < NI; i += G) perm[i] = i;
+          if (kd.mode == LSQ) local_assemble_generic<G, false>(a, k, g, F, kd);
+          else local_assemble<G, true>(a, k, g, F, kd);
         }
-        if (a.lane == 0) { L.seq = 1; L.want_sdh = 1; }
-        sync();
-        return seq_factor(a, kd);
       }
+      wsync();
+      if (lane_now() / G < SR && r * SR + lane_now() / G < nd) {
+        const int g2 = lane_now() % G, slot2 = lane_now() / G;
+        const BKOut bo = interior_bk(LDSP(L.u.p.F + slot2 * PKS), LDSI(L.u.p.perm + slot2 * NI),
+                                     LDSI(L.u.p.piv + slot2 * NI), g2);
+        if (lane_now() % G == 0) {
+          atomicAdd(&L.fin[0], bo.pos); atomicAdd(&L.fin[1], bo.neg); atomicAdd(&L.fin[2], bo.zero);
+          atomicOr(&L.fin[3], bo.bad);
+        }
+      }
+      wsync();
+      SPROF(1);
+      if constexpr (NX > 0) {
+        if (L.fin[3] != 0) {  // singular stage interior: block chain instead
+          sync();
+          if (!L.sdh_ok && kd.mode != LSQ) {  // the chain reads the strided Hessians and jacobian
+            eval_hess_impl(a, L.hsig, 1);
+            eval_gj_ws(a, a.x(), 1);
+            sync();
+          }
+          if (a.lane == 0) { L.seq = 1; L.want_sdh = 1; }
+          sync();
+          return seq_factor(a, kd);
+        }
+      }
+      if (lane_now() / G < SR && r * SR + lane_now() / G < nd) {
+        const int g = lane_now() % G, slot = lane_now() / G;
+        stage_tail(a, nth_bit(dm, r * SR + slot), g, LDSP(L.u.p.F + slot * PKS), LDSI(L.u.p.perm + slot * NI),
+                   LDSI(L.u.p.piv + slot * NI));
+      }
+      wsync();
+      SPROF(2);
     }
-    if (dense && lane_now() / G < SR && r * SR + lane_now() / G < N) {
-      const int g = lane_now() % G, slot = lane_now() / G;
-      stage_tail(a, r * SR + slot, g, LDSP(L.u.p.F + slot * PKS), LDSI(L.u.p.perm + slot * NI),
-                 LDSI(L.u.p.piv + slot * NI));
-    }
-    wsync();
-    SPROF(2);
   }
   Inertia in{L.fin[0], L.fin[1], L.fin[2]};
   if (a.lane == 0) L.seq = 0;
@@ -1462,30 +1530,26 @@ __device__ __noinline__ void solve(const Agent a) {
   Lds& L = gL;
   if (L.seq) { seq_solve(a); return; }
   SPROF_DECL
-  const int lane = a.lane, g = lane % G, slot = lane / G;
+  const int lane = a.lane;
   if (NC > 0) chain_solve(a);
   SPROF(4);
+  // u = W [x_k, c_k, 1] per stage interior (operators column-major per stage); the lanes
+  // run over all (stage, interior row) pairs
 #pragma unroll 1
-  for (int r = 0; r < ROUNDS; ++r) {
-    const int k = r * SR + slot;
-    if (!(slot < SR && k < N)) continue;
-    double tv[NX + NC > 0 ? NX + NC : 1];  // [x_k, c_k]
+  for (int q = lane; q < N * NI; q += WAVE) {
+    const int k = q / NI, p = q % NI;
+    const gdbl* t = a.tr(k) + p;
+    double u = t[(NX + NC) * NI];
 #pragma unroll
-    for (int c = 0; c < NX; ++c) tv[c] = (k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0;
+    for (int c = 0; c < NX; ++c) u -= ((k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0) * t[c * NI];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) tv[NX + c] = L.xs[k * NC + c];
-    for (int p = g; p < NI; p += G) {
-      const gdbl* t = a.tr(k) + p;
-      double u = t[(NX + NC) * NI];
-#pragma unroll
-      for (int c = 0; c < NX + NC; ++c) u -= tv[c] * t[c * NI];
-      const int o = a.prm(k)[p];
-      L.u.sol[k * NB + lblk(o, lkind(o))] = u;
-    }
-    for (int c = g; c < NC; c += G) {
-      const int li = LMU + c;
-      L.u.sol[k * NB + lblk(li, lkind(li))] = tv[NX + c];
-    }
+    for (int c = 0; c < NC; ++c) u -= L.xs[k * NC + c] * t[(NX + c) * NI];
+    const int o = a.prm(k)[p];
+    L.u.sol[k * NB + lblk(o, lkind(o))] = u;
+  }
+  for (int q = lane; q < N * NC; q += WAVE) {
+    const int k = q / NC, li = LMU + q % NC;
+    L.u.sol[k * NB + lblk(li, lkind(li))] = L.xs[q];
   }
   wsync();
   SPROF(5);
@@ -1592,7 +1656,7 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
   const gdbl* pin = (const gdbl*)args.p + (long)agent * NPAR;
   for (int t = lane; t < NPAR; t += WAVE) gL.par[t] = pin[t];
   for (long t = lane; t < (long)(2 * NL + NG * NL + NL * NL) * N; t += WAVE) a.ws[O_SDG + t] = 0.0;
-  for (long t = lane; t < (long)N * PKS; t += WAVE) a.ws[O_LP + t] = 0.0;  // structural zeros stay zero
+  for (long t = lane; t < (long)N * NCS; t += WAVE) a.ws[O_LP + t] = 0.0;  // structural zeros stay zero
   for (int i = lane; i < NW; i += WAVE) {
     double lo = lbw[i], hi = ubw[i];
     if (lo <= -INF_BOUND) lo = -INFINITY;
@@ -1730,7 +1794,7 @@ __device__ __noinline__ void rhs_primal(const Agent a, double mu, double obj_sca
       const int b = (i - NX) / NP, off = (i - NX) % NP;
       const int li = off < NV ? off : LX1 + off - NV;
       a.rhs(b)[off] = r;
-      a.lp(b)[pko(RB) + li] = r;
+      a.lp(b)[CB + li] = r;
       a.dg(b)[li] = sigma_x_v(xv, lo, hi, zl, zu);
     }
   }
@@ -1763,7 +1827,7 @@ __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, doubl
         }
       }
       a.rhs(c / NG)[NP + c % NG] = rr;
-      a.lp(c / NG)[pko(RB) + crow(c % NG)] = rr;
+      a.lp(c / NG)[CB + crow(c % NG)] = rr;
       a.dg(c / NG)[crow(c % NG)] = -dual_diag_v(cl, sigma_s_v(sv, slo, sup, vl, vu), KKTDiag{dw, dc, NEWTON});
     }
   }

@@ -64,7 +64,7 @@ def test_generated_elimination_matches_dense(name):
     rng = np.random.default_rng(11)
     for _ in range(5):
         A = _random_system(gen, rng)
-        out = elim_sim.run(code, elim_sim.pack(A).copy(), ni, ntr, nx * nx + nc * nc + nc * nx, nx + nc)
+        out = elim_sim.run(code, elim_sim.compact(A, gen.compact), ni, ntr, nx * nx + nc * nc + nc * nx, nx + nc)
         assert not out["bad"]
         AII, AIT = A[:ni, :ni], A[:ni, ni:]
         ev = np.linalg.eigvalsh(AII)
@@ -94,7 +94,7 @@ def test_singular_static_pivot_is_reported_before_outputs(name):
     p, q = next(b for b in gen.elim.blocks if len(b) == 2)
     A[p, :] = 0.0
     A[:, p] = 0.0
-    out = elim_sim.run(elim_sim.compile_body(gen.elim_lines), elim_sim.pack(A).copy(), ni, nx + nc + 2,
+    out = elim_sim.run(elim_sim.compile_body(gen.elim_lines), elim_sim.compact(A, gen.compact), ni, nx + nc + 2,
                        nx * nx + nc * nc + nc * nx, nx + nc)
     assert out["bad"]
     assert np.isnan(out["TR"]).all() and (out["PRM"] == -1).all()

@@ -141,6 +141,106 @@ def factorisation_plan(nlp: StageNLP):
     return [], True
 
 
+def _network_section(nlp: StageNLP, bind, fg_assign, gj_all, h_all, emit_gj, emit_h, to_compact):
+    """Device code of the network evaluations on the FP64 matrix cores (empty when the
+    stage has no network node): ``gen_stage_netin`` (one lane per stage writes the inputs
+    of every call site to LDS), ``gen_net_{fg,gj,hess}`` (the wave evaluates each network
+    over all stages x call sites, ``mpcx_net::eval``, csrc/mpcx_net_mfma.h) and the stage
+    functions ``gen_stage_{fg,gj,hess}_m`` that read the network entries from LDS instead
+    of looping over the hidden units.  Returns (lines, defines, X doubles, output doubles)."""
+    sites = {}
+    for outs in (fg_assign, gj_all, h_all):
+        for key, val in sx.network_sites([e for _, e in outs]).items():
+            sites.setdefault(key, val)
+    if not sites:
+        return [], [], 0, 0
+    N = nlp.N
+    nets: Dict[int, list] = {}
+    for key in sites:
+        nets.setdefault(key[0], []).append(key)
+    sidx = {key: q for keys in nets.values() for q, key in enumerate(keys)}
+    xoff, netx = {}, 0
+    for nid, keys in nets.items():
+        xoff[nid] = netx
+        netx += N * len(keys) * sx.network(nid).n_in
+
+    def layout(outs):
+        mem = {nid: set() for nid in nets}
+        for (nid, _), (_, _, members) in sx.network_sites([e for _, e in outs]).items():
+            mem[nid].update(members)
+        lay, o = {}, 0
+        for nid, keys in nets.items():
+            m, R = mem[nid], N * len(keys)
+            wv = ("v", -1, -1) in m
+            d1 = sorted(i for (k, i, _) in m if k == "d")
+            d2 = sorted((i, j) for (k, i, j) in m if k == "dd")
+            ov = o
+            og = ov + (R if wv else 0)
+            oh = og + R * len(d1)
+            o = oh + R * len(d2)
+            lay[nid] = dict(wv=wv, d1=d1, d2=d2, R=R, ov=ov, og=og, oh=oh)
+        return lay, o
+
+    def reader(lay):
+        def read(nid, key, mk):
+            q, Q, L = sidx[(nid, key)], len(nets[nid]), lay[nid]
+            row = f"(K * {Q} + {q})"
+            if mk[0] == "v":
+                return f"NO[{L['ov']} + {row}]"
+            if mk[0] == "d":
+                return f"NO[{L['og']} + {row} * {len(L['d1'])} + {L['d1'].index(mk[1])}]"
+            return f"NO[{L['oh']} + {row} * {len(L['d2'])} + {L['d2'].index((mk[1], mk[2]))}]"
+        return read
+
+    kinds = {"fg": layout(fg_assign), "gj": layout(gj_all), "hess": layout(h_all)}
+    neto = max(o for _, o in kinds.values())
+    lines: List[str] = ['#include "mpcx_net_mfma.h"']
+    for kind, (lay, _) in kinds.items():
+        for nid, L in lay.items():
+            net = sx.network(nid)
+            if L["d1"]:
+                lines.append(f"__constant__ int ANN{nid}_D1{kind}[{len(L['d1'])}] = {{{', '.join(map(str, L['d1']))}}};")
+            if L["d2"]:
+                pw = [net.W1[a, j] * net.W1[b, j] for a, b in L["d2"] for j in range(net.H)]
+                lines.append(f"__constant__ double ANN{nid}_PW{kind}[{len(pw)}] = "
+                             f"{{{', '.join(sx._c_literal(float(v)) for v in pw)}}};")
+    sig = "const double* __restrict__ L, const double* __restrict__ PS, const double* __restrict__ PG, const double TK"
+    xa = []
+    for (nid, key), (_, args, _) in sites.items():
+        nin = sx.network(nid).n_in
+        xa += [(f"X[{xoff[nid]} + (K * {len(nets[nid])} + {sidx[(nid, key)]}) * {nin} + {i}]", a)
+               for i, a in enumerate(args)]
+    lines += [f"__device__ __forceinline__ void gen_stage_netin({sig}, double* __restrict__ X, const int K) {{",
+              *sx.CodeGen(bind, prefix="n").emit(xa), "}"]
+    for kind, (lay, _) in kinds.items():
+        lines.append(f"__device__ __forceinline__ void gen_net_{kind}(const mpcx_elim_ld* X, mpcx_elim_ld* O, "
+                     f"const int lane) {{")
+        for nid, L in lay.items():
+            if not (L["wv"] or L["d1"] or L["d2"]):
+                continue
+            net = sx.network(nid)
+            d1 = f"ANN{nid}_D1{kind}" if L["d1"] else "nullptr"
+            pw = f"ANN{nid}_PW{kind}" if L["d2"] else "nullptr"
+            lines.append(f"  mpcx_net::eval<{L['R']}, {net.n_in}, {net.H}, {sx.ACT_CODE[net.act]}, "
+                         f"{'true' if L['wv'] else 'false'}, {len(L['d1'])}, {len(L['d2'])}>("
+                         f"X + {xoff[nid]}, O + {L['ov']}, O + {L['og']}, O + {L['oh']}, ANN{nid}_W1T, ANN{nid}_B1, "
+                         f"ANN{nid}_W2, {sx._c_literal(net.b2)}, {d1}, {pw}, lane);")
+        lines.append("}")
+    ext = "const double* __restrict__ NO, const int K"
+    lines += [f"__device__ __forceinline__ void gen_stage_fg_m({sig}, double* __restrict__ f, double* __restrict__ g, "
+              f"const int S, {ext}) {{",
+              *sx.CodeGen(bind, prefix="a", net_lds=reader(kinds["fg"][0])).emit(fg_assign), "}",
+              f"__device__ __forceinline__ void gen_stage_gj_m({sig}, double* __restrict__ grad, double* __restrict__ jac, "
+              f"const int S, const double* __restrict__ G, double* __restrict__ lp, const double* __restrict__ LM, "
+              f"double* __restrict__ jtl, const int full, {ext}) {{",
+              *to_compact(emit_gj(reader(kinds["gj"][0])), "lp"), "}",
+              f"__device__ __forceinline__ void gen_stage_hess_m({sig}, const double sigma, const double* __restrict__ lam, "
+              f"double* __restrict__ hess, const int S, double* __restrict__ lp, const int full, {ext}) {{",
+              *to_compact(emit_h(reader(kinds["hess"][0])), "lp"), "}"]
+    defs = ["#define MPCX_NET_MFMA 1", f"#define MPCX_NETX {netx}", f"#define MPCX_NETO {max(neto, 1)}"]
+    return lines, defs, netx, max(neto, 1)
+
+
 def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     st = nlp.stage
     bordered, force_chain = factorisation_plan(nlp)
@@ -162,8 +262,8 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     hess = [[sx.diff(lgrad[i], loc[j]) for j in range(nl)] for i in range(nl)]
 
     # -- fg --
-    cg = sx.CodeGen(bind, prefix="a")
-    fg_lines = cg.emit([("f[0]", st.cost)] + [(f"g[{i} * S]", e) for i, e in enumerate(st.g)])
+    fg_assign = [("f[0]", st.cost)] + [(f"g[{i} * S]", e) for i, e in enumerate(st.g)]
+    fg_lines = sx.CodeGen(bind, prefix="a").emit(fg_assign)
     # -- bounds (parameters only) --
     for e in st.g_lb + st.g_ub:
         if any(s.uid in {v.uid for v in loc} for s in sx.free_symbols([e])):
@@ -220,14 +320,18 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         terms = [sx.mul(glm[r], jac[r][j]) for r in range(ng) if not jac[r][j].is_const(0.0)]
         if terms:
             jtl_assign.append((f"jtl[{j} * S]", sx.sum1(terms)))
-    cg = sx.CodeGen(gb, prefix="c")
-    gj_lines = cg.emit(g_assign + j_assign + lp_j + jtl_assign)
-    # the strided jacobian is stored only when requested (scaling, block-chain fallback)
-    nj, ntail = len(j_assign), len(lp_j) + len(jtl_assign)
-    j_store = gj_lines[len(gj_lines) - ntail - nj:len(gj_lines) - ntail]
-    assert all(l.lstrip().startswith("jac[") for l in j_store)
-    gj_lines = (gj_lines[:len(gj_lines) - ntail - nj] + (["  if (full) {"] + j_store + ["  }"] if nj else [])
-                + gj_lines[len(gj_lines) - ntail:])
+    gj_all = g_assign + j_assign + lp_j + jtl_assign
+
+    def emit_gj(net_lds=None):
+        lines = sx.CodeGen(gb, prefix="c", net_lds=net_lds).emit(gj_all)
+        # the strided jacobian is stored only when requested (scaling, block-chain fallback)
+        nj, ntail = len(j_assign), len(lp_j) + len(jtl_assign)
+        j_store = lines[len(lines) - ntail - nj:len(lines) - ntail]
+        assert all(l.lstrip().startswith("jac[") for l in j_store)
+        return (lines[:len(lines) - ntail - nj] + (["  if (full) {"] + j_store + ["  }"] if nj else [])
+                + lines[len(lines) - ntail:])
+
+    gj_lines = emit_gj()
     # -- hessian: lower triangle, mirrored; once into the packed local system --
     h_assign = []
     lp_h = []
@@ -240,14 +344,18 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
             if i != j:
                 h_assign.append((f"hess[{j * nl + i} * S]", e))
             lp_h.append((f"lp[{pk(lidx(i), lidx(j))}]", e))
-    cg = sx.CodeGen(hb, prefix="h")
-    h_lines = cg.emit(h_assign + lp_h)
-    # the strided full Hessian is stored only when requested (block-chain fallback)
-    nh = len(h_assign)
-    h_store = h_lines[len(h_lines) - len(h_assign) - len(lp_h):len(h_lines) - len(lp_h)]
-    assert all(l.lstrip().startswith("hess[") for l in h_store)
-    h_lines = (h_lines[:len(h_lines) - nh - len(lp_h)] + (["  if (full) {"] + h_store + ["  }"] if nh else [])
-               + h_lines[len(h_lines) - len(lp_h):])
+    h_all = h_assign + lp_h
+
+    def emit_h(net_lds=None):
+        lines = sx.CodeGen(hb, prefix="h", net_lds=net_lds).emit(h_all)
+        # the strided full Hessian is stored only when requested (block-chain fallback)
+        nh = len(h_assign)
+        h_store = lines[len(lines) - nh - len(lp_h):len(lines) - len(lp_h)]
+        assert all(l.lstrip().startswith("hess[") for l in h_store)
+        return (lines[:len(lines) - nh - len(lp_h)] + (["  if (full) {"] + h_store + ["  }"] if nh else [])
+                + lines[len(lines) - len(lp_h):])
+
+    h_lines = emit_h()
 
     # -- static sparse elimination of the stage interior (runtime/stage_elim.py) --
     P = [[False] * (nloc + 1) for _ in range(nloc + 1)]
@@ -303,6 +411,9 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     gj_lines = to_compact(gj_lines, "lp")
     h_lines = to_compact(h_lines, "lp")
 
+    net_lines, net_defs, netx, neto = _network_section(nlp, bind, fg_assign, gj_all, h_all, emit_gj, emit_h,
+                                                       to_compact)
+
     dims = dict(N=nlp.N, NX=nlp.nx, NV=nlp.nv, NG=ng, NPS=nlp.nps, NPG=nlp.npg)
     ts = nlp.ts if ts is None else ts
     flops = {
@@ -322,7 +433,7 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     cslot = 8 * (len(compact) | 1)
     soff = nxp * nxp + ncp * ncp + ncp * nxp
     other = 8 * (N_ * soff + N_ * ncp * ncp + N_ * (NX_ + ncp) + N_ * ncp + 3 * ncp * ncp + 64 + nlp.npg
-                 + N_ * nlp.nps + N_) + 8 * ncp + 64 + 336 + 16  # 336: KState, 16: fixed-stage masks
+                 + N_ * nlp.nps + N_ + netx + neto) + 8 * ncp + 64 + 336 + 16  # 336: KState, 16: masks
     need = other + N_ * cslot
     lds_target = 9600 if other + 2 * cslot <= 9600 else min(need, 40960)
 
@@ -368,6 +479,8 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         "  inert[0] = pos; inert[1] = neg; inert[2] = 0;",
         "  return 0;",
         "}",
+        *net_defs,
+        *net_lines,
         "// <<< device only", "",
         '#include "mpcx_ipm.hip"',
         "",

@@ -759,10 +759,14 @@ class CodeGen:
     see :func:`network_tables`); ``networks`` collects the ids used.
     """
 
-    def __init__(self, inputs: Dict[Expr, str], prefix: str = "t"):
+    def __init__(self, inputs: Dict[Expr, str], prefix: str = "t", net_lds=None):
         self.inputs = {k.uid: v for k, v in inputs.items()}
         self.prefix = prefix
         self.networks = set()
+        #: optional ``(nid, arg uids, member key) -> C expression``: network entries are read
+        #: from values a wave-level pass computed (MFMA, csrc/mpcx_net_mfma.h) instead of
+        #: being evaluated by the hidden-unit loop
+        self.net_lds = net_lds
 
     def emit(self, assignments: Sequence[Tuple[str, Expr]], indent: str = "  ") -> List[str]:
         outs = [as_expr(e) for _, e in assignments]
@@ -792,6 +796,14 @@ class CodeGen:
                 members = groups[(nid, tuple(x.uid for x in n.args))]
                 gp = f"{self.prefix}n{n_groups}"
                 n_groups += 1
+                if self.net_lds is not None:
+                    key = tuple(x.uid for x in n.args)
+                    for mk, node in members.items():
+                        var = f"{gp}{'v' if mk[0] == 'v' else ('g%d' % mk[1] if mk[0] == 'd' else 'h%d_%d' % mk[1:])}"
+                        lines.append(f"{indent}const double {var} = {self.net_lds(nid, key, mk)};")
+                        names[node.uid] = var
+                    self.networks.add(nid)
+                    continue
                 lines += _emit_network(nid, a, members, gp, names, indent)
                 self.networks.add(nid)
                 continue
@@ -805,6 +817,23 @@ class CodeGen:
         for target, e in assignments:
             lines.append(f"{indent}{target} = {names[as_expr(e).uid]};")
         return lines
+
+
+def network_sites(outputs: Sequence[Expr]) -> Dict[tuple, Tuple[int, tuple, Dict[tuple, Expr]]]:
+    """Network call sites of a DAG in topological order: ``(nid, arg uids) -> (nid, args,
+    {member key: node})`` with member keys ``('v', -1, -1)``, ``('d', i, -1)``, ``('dd', i, k)``."""
+    sites: Dict[tuple, Tuple[int, tuple, Dict[tuple, Expr]]] = {}
+    for n in topo_order([as_expr(o) for o in outputs]):
+        pa = ann_parse(n.op) if n.op.startswith("ann") else None
+        if pa is None:
+            continue
+        key = (pa[1], tuple(a.uid for a in n.args))
+        sites.setdefault(key, (pa[1], n.args, {}))[2][pa[0], pa[2], pa[3]] = n
+    return sites
+
+
+#: activation codes of the wave-level network pass (csrc/mpcx_net_mfma.h)
+ACT_CODE = {a: i for i, a in enumerate(_ACTS)}
 
 
 _ACT_C = {

@@ -240,8 +240,12 @@ __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // dense packed system + perm/piv (fallback)
 constexpr int CSLOT_BYTES = 8 * NCS;          // compact image (static elimination)
-constexpr int OTHER_BYTES = 8 * (N * SOFF + N * NCC + N * (NX + NCP) + N * NCP + 3 * NCC + 2 * MAXF + NPAR + N) +
-                            8 * NCP + 64 + 336 + 16;  // 336: KState, 16: fixed-stage masks
+#ifndef MPCX_NETX
+#define MPCX_NETX 0
+#define MPCX_NETO 0
+#endif
+constexpr int OTHER_BYTES = 8 * (N * SOFF + N * NCC + N * (NX + NCP) + N * NCP + 3 * NCC + 2 * MAXF + NPAR + N +
+                                 MPCX_NETX + MPCX_NETO) + 8 * NCP + 64 + 336 + 16;  // 336: KState, 16: masks
 #ifndef MPCX_LDS_TARGET
 #define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
 #endif
@@ -353,6 +357,10 @@ struct Lds {
   double hsig;             // sigma of the last eval_hess
   double fth[MAXF];
   double fph[MAXF];
+#ifdef MPCX_NET_MFMA
+  double netx[MPCX_NETX];  // network inputs of every call site (stage-major)
+  double neto[MPCX_NETO];  // network values / derivatives of the current evaluation
+#endif
   KState ks;
 #ifdef MPCX_PROFILE
   double sprof[6];
@@ -423,13 +431,38 @@ __device__ __forceinline__ int cls_of(double lo, double hi, double sl, double su
 __device__ __forceinline__ const double* par_stage(int k) { return (const double*)(gL.par + NPG + k * NPS); }
 __device__ __forceinline__ const double* par_global() { return (const double*)gL.par; }
 
+// Network models (MPCX_NET_MFMA, runtime/codegen.py): before the stage functions run, the
+// wave evaluates every network call site of every stage at the point on the matrix cores
+// (csrc/mpcx_net_mfma.h): one lane per stage writes the inputs (gen_stage_netin), the
+// wave runs gen_net_<kind>, and the stage functions read the entries they use from LDS.
+#ifdef MPCX_NET_MFMA
+#define NET_PREP(pt, kind)                                                                  \
+  do {                                                                                      \
+    for (int k = a.lane; k < N; k += WAVE)                                                  \
+      gen_stage_netin((const double*)((pt) + k * NP), par_stage(k), par_global(), k * TS,   \
+                      (double*)gL.netx, k);                                                 \
+    wsync();                                                                                \
+    gen_net_##kind(LDSP(gL.netx), LDSP(gL.neto), lane_now());                               \
+    wsync();                                                                                \
+  } while (0)
+#define STAGE_FG(...) gen_stage_fg_m(__VA_ARGS__, (const double*)gL.neto, k)
+#define STAGE_GJ(...) gen_stage_gj_m(__VA_ARGS__, (const double*)gL.neto, k)
+#define STAGE_HESS(...) gen_stage_hess_m(__VA_ARGS__, (const double*)gL.neto, k)
+#else
+#define NET_PREP(pt, kind) do { } while (0)
+#define STAGE_FG(...) gen_stage_fg(__VA_ARGS__)
+#define STAGE_GJ(...) gen_stage_gj(__VA_ARGS__)
+#define STAGE_HESS(...) gen_stage_hess(__VA_ARGS__)
+#endif
+
 // f and unscaled g at the trial point in LDS (xt -> gt); returns wave-summed f
 __device__ __noinline__ double eval_fg_lds(const Agent a) {
+  NET_PREP(gL.u.t.xt, fg);
   double f = 0.0;
   for (int k = a.lane; k < N; k += WAVE) {
     double fk = 0.0;
-    gen_stage_fg((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS, &fk,
-                 (double*)(gL.u.t.gt + k * NG), 1);
+    STAGE_FG((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS, &fk,
+             (double*)(gL.u.t.gt + k * NG), 1);
     f += fk;
   }
   return wsum(f);
@@ -437,10 +470,11 @@ __device__ __noinline__ double eval_fg_lds(const Agent a) {
 
 // f and unscaled g at a point in the workspace
 __device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* gout) {
+  NET_PREP(xv, fg);
   double f = 0.0;
   for (int k = a.lane; k < N; k += WAVE) {
     double fk = 0.0;
-    gen_stage_fg((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, &fk, (double*)(gout + k * NG), 1);
+    STAGE_FG((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, &fk, (double*)(gout + k * NG), 1);
     f += fk;
   }
   return wsum(f);
@@ -449,31 +483,34 @@ __device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* g
 // derivatives at a point in the workspace; full: also the strided jacobian (scaling and
 // the block-chain fallback read it; the stage-parallel path reads lp and jtl only)
 __device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv, int full) {
+  NET_PREP(xv, gj);
   for (int k = a.lane; k < N; k += WAVE)
-    gen_stage_gj((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, (double*)(a.sdg() + k),
-                 (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG), (double*)a.lp(k),
-                 (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
+    STAGE_GJ((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, (double*)(a.sdg() + k),
+             (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG), (double*)a.lp(k),
+             (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
 }
 
 // derivatives at the accepted trial point (still in LDS), with the accepted multipliers
 __device__ __noinline__ void eval_gj_lds(const Agent a) {
+  NET_PREP(gL.u.t.xt, gj);
   const int full = gL.want_sdh;
   for (int k = a.lane; k < N; k += WAVE)
-    gen_stage_gj((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS,
-                 (double*)(a.sdg() + k), (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG),
-                 (double*)a.lp(k), (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
+    STAGE_GJ((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS,
+             (double*)(a.sdg() + k), (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG),
+             (double*)a.lp(k), (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
 }
 
 // Hessian of sigma*f + sum lam_i * gs_i * g_i (scaled Lagrangian) into the packed
 // stage systems; the strided full Hessians (read only by the block-chain fallback)
 // are written when that path is in use, or on demand (eval_hess_full)
 __device__ __noinline__ void eval_hess_impl(const Agent a, double sigma, int full) {
+  NET_PREP(a.x(), hess);
   for (int k = a.lane; k < N; k += WAVE) {
     double lk[NG > 0 ? NG : 1];
 #pragma unroll
     for (int r = 0; r < NG; ++r) lk[r] = a.lam()[k * NG + r] * a.gs()[k * NG + r];
-    gen_stage_hess((const double*)(a.x() + k * NP), par_stage(k), par_global(), k * TS, sigma, lk,
-                   (double*)(a.sdh() + k), N, (double*)a.lp(k), full);
+    STAGE_HESS((const double*)(a.x() + k * NP), par_stage(k), par_global(), k * TS, sigma, lk,
+               (double*)(a.sdh() + k), N, (double*)a.lp(k), full);
   }
   if (a.lane == 0) { gL.hsig = sigma; gL.sdh_ok = full; }
 }
@@ -1000,30 +1037,34 @@ __device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F
     for (int t = g; t < PKB; t += GG) F[t] = 0.0;
     wsync();
   }
-  double v[EPC], dv[EPC];
+  constexpr int CH = EPC < 12 ? EPC : 12;  // entries per lane in flight (loads before the first use)
+#pragma unroll 1
+  for (int e0 = 0; e0 < EPC; e0 += CH) {
+    double v[CH], dv[CH];
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const int t = g + e * GG;
-    v[e] = src[t < NCPT ? t : 0];
-    dv[e] = dg[t < NLOC ? t : 0];
-  }
+    for (int e = 0; e < CH; ++e) {
+      const int t = g + (e0 + e) * GG;
+      v[e] = src[t < NCPT ? t : 0];
+      dv[e] = dg[t < NLOC ? t : 0];
+    }
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const int t = g + e * GG;
-    if (t >= NCPT) continue;
-    double x = v[e];
-    bool fix = false;
-    if (fm != 0ull) {
-      const int ij = kCIJ[t], i = ij & 255, j = ij >> 8;
-      fix = (((fm >> i) | (fm >> j)) & 1ull) != 0ull;
-      if (fix) x = (i == j && lkind(i) == 0) ? 1.0 : 0.0;
+    for (int e = 0; e < CH; ++e) {
+      const int t = g + (e0 + e) * GG;
+      if (e0 + e >= EPC || t >= NCPT) continue;
+      double x = v[e];
+      bool fix = false;
+      if (fm != 0ull) {
+        const int ij = kCIJ[t], i = ij & 255, j = ij >> 8;
+        fix = (((fm >> i) | (fm >> j)) & 1ull) != 0ull;
+        if (fix) x = (i == j && lkind(i) == 0) ? 1.0 : 0.0;
+      }
+      if (t < NLOC) {  // diagonal (t, t)
+        const int ki = lkind(t);
+        if ((ki == 0 || ki == 3) && !fix) x += dv[e] + kd.dw;
+        if (kdual(ki)) x = dv[e];
+      }
+      F[DENSE ? (int)kCPK[t] : t] = x;
     }
-    if (t < NLOC) {  // diagonal (t, t)
-      const int ki = lkind(t);
-      if ((ki == 0 || ki == 3) && !fix) x += dv[e] + kd.dw;
-      if (kdual(ki)) x = dv[e];
-    }
-    F[DENSE ? (int)kCPK[t] : t] = x;
   }
   wsync();
 }

@@ -405,7 +405,10 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     cix = {pk(i, j): c for c, (i, j) in enumerate(compact)}
 
     def to_compact(lines, arr):
-        return [re.sub(rf"\b{arr}\[(\d+)\]", lambda m: f"{arr}[{cix[int(m.group(1))]}]", ln) for ln in lines]
+        # lp (the evaluators' image in HBM) is stage-minor: entry c of the stage at lp[c * S]
+        stride = " * S" if arr == "lp" else ""
+        return [re.sub(rf"\b{arr}\[(\d+)\]", lambda m: f"{arr}[{cix[int(m.group(1))]}{stride}]", ln)
+                for ln in lines]
 
     elim_lines = to_compact(elim_lines, "F")
     gj_lines = to_compact(gj_lines, "lp")

@@ -295,10 +295,8 @@ def emit(P: Sequence[Sequence[bool]], ni: int, nv: int, nx: int, nc: int,
                 terms = [f"F[{pk(i, p)}] * {w[i]}" for i in pl.cols[bi] if w[i] != "0.0"]
                 w[p] = new(tra, f"{z[p]} - ({' + '.join(terms)})") if terms else z[p]
         for p in range(ni):
-            tra.append(f"  TR[{t * ni + p}] = {w[p]};")
+            tra.append(f"  TR[{t * ni + p} * MPCX_N] = {w[p]};")  # stage-minor in HBM
         for ri, dest in want.get(ti, []):  # value(ri, ti) = A[ri][ti] - a_ri . w_ti
             tra.append(f"  {dest} = {orig(ri, ti) or '0.0'} - ({schur_dot(ri, w)});")
-    for p in range(ni):
-        tra.append(f"  PRM[{p}] = {p};")
     pl.flops = count_flops(fac) + count_flops(tra)
     return fac, tra, pl

@@ -123,14 +123,14 @@ constexpr long O_SDJ = O_JTL + (long)NL * N;     // [NG*NL][N]   stage jacobian 
 constexpr long O_SDH = O_SDJ + (long)NG * NL * N;// [NL*NL][N]   stage hessian
 constexpr long O_RHS = O_SDH + (long)NL * NL * N;// [N][NB]      KKT right-hand side
 constexpr long O_TR = O_RHS + (long)N * NB;      // [N][NTR][NI] back-substitution operators
-constexpr long O_PRM = O_TR + (long)N * NI * NTR;// [N][NI] ints interior pivot order
+constexpr long O_PRM = O_TR + (long)N * NI * NTR;// [N][NI] ints interior pivot order (dense stages)
 constexpr long O_KX = O_PRM + (long)N * NI;      // [N*NP] primal KKT diagonal   (block chain)
 constexpr long O_KD = O_KX + (long)N * NP;       // [M] dual KKT diagonal        (block chain)
 constexpr long O_SOL = O_KD + M;                 // [N][NB] solution             (block chain)
 constexpr long O_FAC = O_SOL + (long)N * NB;     // [N][NB*LDB] block inverses   (block chain)
 constexpr long O_CPL = O_FAC + (long)N * NB * LDB;  // [N][NB*NX] couplings      (block chain)
-constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [N][NCS] compact local systems (evaluators, rhs)
-constexpr long O_DG = O_LP + (long)N * NCS;        // [N][NLOC] diagonal terms (rhs phases; Newton mode)
+constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [NCPT][N] compact local systems (evaluators; stage-minor)
+constexpr long O_DG = O_LP + (long)NCPT * N;       // [N][NLOC] diagonal terms (rhs phases; Newton mode)
 constexpr long WS_DOUBLES = O_DG + (long)N * NLOC;
 
 using Args = mpcx_kernel_args;
@@ -407,14 +407,14 @@ struct Agent {
   __device__ gdbl* sdj() const { return ws + O_SDJ; }
   __device__ gdbl* sdh() const { return ws + O_SDH; }
   __device__ gdbl* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
-  __device__ gdbl* tr(int k) const { return ws + O_TR + (long)k * NI * NTR; }
+  __device__ gdbl* tr(int k) const { return ws + O_TR + k; }  // [NTR][NI][N]: W_k[t][p] at tr(k)[(t NI + p) N]
   __device__ gint* prm(int k) const { return reinterpret_cast<gint*>(ws + O_PRM) + (long)k * NI; }
   __device__ gdbl* kx() const { return ws + O_KX; }
   __device__ gdbl* kd() const { return ws + O_KD; }
   __device__ gdbl* sol(int k) const { return ws + O_SOL + (long)k * NB; }
   __device__ gdbl* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
   __device__ gdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
-  __device__ gdbl* lp(int k) const { return ws + O_LP + (long)k * NCS; }
+  __device__ gdbl* lp(int k) const { return ws + O_LP + k; }  // entry c of stage k at lp(k)[c * N]
   __device__ gdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
 };
 
@@ -1022,8 +1022,9 @@ __device__ __noinline__ void local_assemble_generic(const Agent a, int k, int g,
   local_diagonal<GG, COMPACT>(a, k, g, F, kd, fm);
 }
 
-// Newton system of stage k from the compact image the evaluators and the rhs phases
-// wrote (one coalesced read): fixed variables (identity row for V, empty row for a state,
+// Newton system of stage k from the compact image the evaluators wrote (stage-minor in
+// HBM: the lanes of a round read consecutive stages of one entry), the border from the
+// rhs and the diagonal terms the rhs phases wrote: fixed variables (identity row for V, empty row for a state,
 // chained as 1) and the diagonal terms the rhs phases precomputed (primal Sigma_x,
 // + delta_w here; dual diagonal) are applied on the way.  DENSE: scattered into a zeroed
 // dense packed image (Bunch-Kaufman path), else the compact image itself (static path).
@@ -1033,6 +1034,7 @@ __device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F
   const unsigned long long fm = gL.fixm[k];
   const gdbl* src = a.lp(k);
   const gdbl* dg = a.dg(k);
+  const gdbl* rb = a.rhs(k);
   if constexpr (DENSE) {
     for (int t = g; t < PKB; t += GG) F[t] = 0.0;
     wsync();
@@ -1044,7 +1046,9 @@ __device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
       const int t = g + (e0 + e) * GG;
-      v[e] = src[t < NCPT ? t : 0];
+      // border (rhs) entries from the rhs the rhs phases wrote in block order; x_k has none
+      const bool bd = t >= CB && t < CB + NLOC && lkind(t - CB) != 2;
+      v[e] = bd ? rb[lblk(t - CB, lkind(t - CB))] : src[(t < NCPT ? t : 0) * N];
       dv[e] = dg[t < NLOC ? t : 0];
     }
 #pragma unroll
@@ -1423,7 +1427,7 @@ __device__ __noinline__ void stage_tail(const Agent a, int k, int g, ldsd* F, co
   // back-substitution operators, column-major [t][p] (the static path stores whole columns)
   for (int p = g; p < NI; p += G) {
 #pragma unroll
-    for (int t = 0; t < NTR; ++t) a.tr(k)[t * NI + p] = F[pko(NI + t) + p];
+    for (int t = 0; t < NTR; ++t) a.tr(k)[(t * NI + p) * N] = F[pko(NI + t) + p];
     a.prm(k)[p] = perm[p];
   }
 }
@@ -1484,8 +1488,9 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
 #pragma unroll 1
   for (int r = 0; r < CROUNDS; ++r) {
     {
-      const int g = lane_now() % GC, slot = lane_now() / GC, k = r * SRC + slot;
-      if (slot < SRC && k < N) {
+      // stage fastest across the lanes: the stage-minor image reads coalesce over the round
+      const int slot = lane_now() % SRC, g = lane_now() / SRC, k = r * SRC + slot;
+      if (g < GC && k < N) {
         ldsd* F = LDSP(L.u.c.F + slot * NCS);
         if (kd.mode == LSQ) local_assemble_generic<GC, true>(a, k, g, F, kd);
         else local_assemble<GC, false>(a, k, g, F, kd);
@@ -1566,6 +1571,15 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   return in;
 }
 
+// stage k of the last factorisation took the dense Bunch-Kaufman path (pivot order in prm)
+__device__ __forceinline__ bool stage_was_dense(int k) {
+#ifdef MPCX_STATIC_ELIM
+  return (gL.dmask[k >> 5] >> (k & 31)) & 1u;
+#else
+  return true;
+#endif
+}
+
 // Newton step into gL.u.sol (block order per stage) from the last factorisation.
 __device__ __noinline__ void solve(const Agent a) {
   Lds& L = gL;
@@ -1578,14 +1592,14 @@ __device__ __noinline__ void solve(const Agent a) {
   // run over all (stage, interior row) pairs
 #pragma unroll 1
   for (int q = lane; q < N * NI; q += WAVE) {
-    const int k = q / NI, p = q % NI;
-    const gdbl* t = a.tr(k) + p;
-    double u = t[(NX + NC) * NI];
+    const int k = q % N, p = q / N;  // stage fastest: the stage-minor operator reads coalesce
+    const gdbl* t = a.tr(k) + (long)p * N;
+    double u = t[(long)(NX + NC) * NI * N];
 #pragma unroll
-    for (int c = 0; c < NX; ++c) u -= ((k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0) * t[c * NI];
+    for (int c = 0; c < NX; ++c) u -= ((k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0) * t[(long)c * NI * N];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) u -= L.xs[k * NC + c] * t[(NX + c) * NI];
-    const int o = a.prm(k)[p];
+    for (int c = 0; c < NC; ++c) u -= L.xs[k * NC + c] * t[(long)(NX + c) * NI * N];
+    const int o = stage_was_dense(k) ? a.prm(k)[p] : p;  // static stages: identity order
     L.u.sol[k * NB + lblk(o, lkind(o))] = u;
   }
   for (int q = lane; q < N * NC; q += WAVE) {
@@ -1599,75 +1613,6 @@ __device__ __noinline__ void solve(const Agent a) {
 // ---------------------------------------------------------------------------
 // vector phases (lane i + 64*slot owns variable / constraint; loads first)
 // ---------------------------------------------------------------------------
-// optimality error parts; complementarity kept as (max, min) of the products so
-// that E_mu for any mu is max(pmx - mu, mu - pmn) without another pass
-// dual_u / viol_u: IPOPT's unscaled_curr_dual_infeasibility (grad_lag_x and the slack part
-// grad_lag_s*d_scale, / obj_scale) and unscaled_curr_nlp_constraint_violation (|c| and the
-// violation of the (relaxed) bounds of d, not d - s)
-
-// scaled optimality error E_mu (IPOPT eq. 5) + unscaled parts
-__device__ __noinline__ OptErr opt_error(const Agent a, double obj_scale) {
-  const int lane = a.lane;
-  double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, vmax_u = 0.0, pmx = -INFINITY, pmn = INFINITY;
-  double lsum = 0.0, zsum = 0.0;
-  int nz = 0;
-#pragma unroll
-  for (int sl = 0; sl < VS; ++sl) {
-    const int i = lane + sl * WAVE;
-    const bool on = i >= NX && i < NW;
-    const int ii = on ? i : NX;
-    const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
-    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
-    if (on && lo != hi) {
-      const double rd = obj_scale * gr + jt - zl + zu;
-      dmax = fmax(dmax, fabs(rd));
-      dmax_u = fmax(dmax_u, fabs(rd) / obj_scale);
-      if (isfin(lo)) { const double pr = (xv - lo) * zl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zl); nz++; }
-      if (isfin(hi)) { const double pr = (hi - xv) * zu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zu); nz++; }
-    }
-  }
-#pragma unroll
-  for (int sl = 0; sl < CS; ++sl) {
-    const int c = lane + sl * WAVE;
-    const bool on = c < M;
-    const int cc = on ? c : 0;
-    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
-    const double gsc = a.gs()[cc], gvv = a.gv()[cc], sv = a.s()[cc], lm = a.lam()[cc];
-    const double vl = a.vL()[cc], vu = a.vU()[cc];
-    if (on) {
-      const int cl = cls_of(lbv, ubv, slo, sup);
-      double cv, vv = 0.0;
-      if (cl == 0) {
-        cv = gvv - gsc * lbv;
-        vv = fabs(cv);
-      } else {
-        cv = gvv - sv;
-        if (cl == 1) {
-          const double rs = -lm - vl + vu;
-          dmax = fmax(dmax, fabs(rs));
-          dmax_u = fmax(dmax_u, fabs(rs) * gsc / obj_scale);
-          vv = fmax(0.0, fmax(slo - gvv, gvv - sup));
-          if (isfin(slo)) { const double pr = (sv - slo) * vl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vl); nz++; }
-          if (isfin(sup)) { const double pr = (sup - sv) * vu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vu); nz++; }
-        }
-      }
-      pmax = fmax(pmax, fabs(cv));
-      vmax_u = fmax(vmax_u, vv / gsc);
-      lsum += fabs(lm);
-    }
-  }
-  OptErr e;
-  e.dual = wmax(dmax); e.dual_u = wmax(dmax_u); e.primal = wmax(pmax); e.viol_u = wmax(vmax_u);
-  e.pmx = wmax(pmx); e.pmn = wmin(pmn);
-  lsum = wsum(lsum); zsum = wsum(zsum); nz = wsumi(nz);
-  e.ncompl = nz;
-  const double smax = 100.0;
-  // IPOPT: s_d over all multipliers (y_c, y_d, z_L, z_U, v_L, v_U)
-  e.s_d = fmax(smax, (lsum + zsum) / fmax(1.0, (double)(M + nz))) / smax;
-  e.s_c = nz > 0 ? fmax(smax, zsum / (double)nz) / smax : 1.0;
-  return e;
-}
-
 // push v into [lo + pl, hi - pu] (IPOPT bound_push / bound_frac)
 __device__ __forceinline__ double push_into(double v, double lo, double hi, double kp, double kf) {
   const bool hl = isfin(lo), hu = isfin(hi);
@@ -1697,7 +1642,7 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
   const gdbl* pin = (const gdbl*)args.p + (long)agent * NPAR;
   for (int t = lane; t < NPAR; t += WAVE) gL.par[t] = pin[t];
   for (long t = lane; t < (long)(2 * NL + NG * NL + NL * NL) * N; t += WAVE) a.ws[O_SDG + t] = 0.0;
-  for (long t = lane; t < (long)N * NCS; t += WAVE) a.ws[O_LP + t] = 0.0;  // structural zeros stay zero
+  for (long t = lane; t < (long)NCPT * N; t += WAVE) a.ws[O_LP + t] = 0.0;  // structural zeros stay zero
   for (int i = lane; i < NW; i += WAVE) {
     double lo = lbw[i], hi = ubw[i];
     if (lo <= -INF_BOUND) lo = -INFINITY;
@@ -1814,33 +1759,6 @@ __device__ __noinline__ double theta_now(const Agent a) {
   return wsum(t);
 }
 
-__device__ __noinline__ void rhs_primal(const Agent a, double mu, double obj_scale) {
-  const int lane = a.lane;
-#pragma unroll
-  for (int sl = 0; sl < VS; ++sl) {
-    const int i = lane + sl * WAVE;
-    const bool on = i >= NX && i < NW;
-    const int ii = on ? i : NX;
-    const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii];
-    const double zl = a.zL()[ii], zu = a.zU()[ii];
-    const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
-    if (on) {
-      double r = 0.0;
-      if (lo != hi) {
-        double gphi = obj_scale * gr;
-        if (isfin(lo)) gphi -= mu / (xv - lo);
-        if (isfin(hi)) gphi += mu / (hi - xv);
-        r = -(gphi + jt);
-      }
-      const int b = (i - NX) / NP, off = (i - NX) % NP;
-      const int li = off < NV ? off : LX1 + off - NV;
-      a.rhs(b)[off] = r;
-      a.lp(b)[CB + li] = r;
-      a.dg(b)[li] = sigma_x_v(xv, lo, hi, zl, zu);
-    }
-  }
-}
-
 // dual rows of the rhs (depend on delta_w); ends with the barrier that hands
 // the whole rhs to the factorisation lanes
 __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, double dc) {
@@ -1868,7 +1786,6 @@ __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, doubl
         }
       }
       a.rhs(c / NG)[NP + c % NG] = rr;
-      a.lp(c / NG)[CB + crow(c % NG)] = rr;
       a.dg(c / NG)[crow(c % NG)] = -dual_diag_v(cl, sigma_s_v(sv, slo, sup, vl, vu), KKTDiag{dw, dc, NEWTON});
     }
   }
@@ -2168,6 +2085,158 @@ __device__ __forceinline__ bool current_is_acceptable(Acceptable& ac, const OptE
          fabs(ac.curr_f - ac.last_f) / fmax(1.0, fabs(ac.curr_f)) <= o.acceptable_obj_change_tol;
 }
 
+
+// Top of an IPM iteration in ONE pass over the variables and constraints: IPOPT's scaled
+// optimality error, the termination tests (tol, acceptable level, max_iter), the monotone
+// barrier update, then the Newton rhs and the KKT diagonal terms at the new mu for
+// delta_w = delta_c = 0 (what rhs_dual recomputes for an inertia correction).  The
+// operands are loaded once and stay in registers across the wave reductions (no calls),
+// instead of being streamed again by separate rhs phases.  Returns 1 when the solve stops
+// (K.status set), 0 with the rhs handed to the factorisation lanes (barrier).
+__device__ __noinline__ int iter_head(const Agent a, KArgs* argp) {
+  KArgs& ka = *argp;
+  KState& K = gL.ks;
+  const int lane = a.lane;
+  const double obj_scale = K.obj_scale;
+  // what the rhs needs is reduced to 3 values per slot while the error terms are summed, the
+  // rhs being affine in mu: primal r = r0 + mu r1 (r0 = -(obj_scale grad + J~^T lam),
+  // r1 = 1/(x - lo) - 1/(hi - x)) and Sigma_x; dual (inequality rows) rr = q0 - mu q1
+  // (q0 = -(c - s) + lam / Sigma_s, q1 = (1/(sU - s) - 1/(s - sL)) / Sigma_s) and the dual
+  // diagonal; equality / free rows: rr = q0
+  double pr0[VS], pr1[VS], psx[VS];
+  double dq0[CS], dq1[CS], ddg[CS];
+  {
+    double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, vmax_u = 0.0, pmx = -INFINITY, pmn = INFINITY;
+    double lsum = 0.0, zsum = 0.0;
+    int nz = 0;
+#pragma unroll
+    for (int sl = 0; sl < VS; ++sl) {
+      const int i = lane + sl * WAVE;
+      const int ii = (i >= NX && i < NW) ? i : NX;
+      const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
+      const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
+      const bool on = i >= NX && i < NW && lo != hi;
+      pr0[sl] = on ? -(obj_scale * gr + jt) : 0.0;
+      pr1[sl] = on ? (isfin(lo) ? 1.0 / (xv - lo) : 0.0) - (isfin(hi) ? 1.0 / (hi - xv) : 0.0) : 0.0;
+      psx[sl] = sigma_x_v(xv, lo, hi, zl, zu);
+      if (on) {
+        const double rd = obj_scale * gr + jt - zl + zu;
+        dmax = fmax(dmax, fabs(rd));
+        dmax_u = fmax(dmax_u, fabs(rd) / obj_scale);
+        if (isfin(lo)) { const double pr = (xv - lo) * zl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zl); nz++; }
+        if (isfin(hi)) { const double pr = (hi - xv) * zu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zu); nz++; }
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < CS; ++sl) {
+      const int c = lane + sl * WAVE;
+      const int cc = c < M ? c : 0;
+      const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+      const double gsc = a.gs()[cc], gvv = a.gv()[cc], sv = a.s()[cc], lm = a.lam()[cc];
+      const double vl = a.vL()[cc], vu = a.vU()[cc];
+      const int cl = cls_of(lbv, ubv, slo, sup);
+      {
+        const double sg = sigma_s_v(sv, slo, sup, vl, vu);
+        const double r = (cl == 0) ? -(gvv - gsc * lbv) : -(gvv - sv);
+        dq0[sl] = (cl == 1) ? r + lm / sg : r;
+        dq1[sl] = (cl == 1) ? ((isfin(sup) ? 1.0 / (sup - sv) : 0.0) - (isfin(slo) ? 1.0 / (sv - slo) : 0.0)) / sg : 0.0;
+        ddg[sl] = -dual_diag_v(cl, sg, KKTDiag{0.0, 0.0, NEWTON});
+      }
+      if (c < M) {
+        double cv, vv = 0.0;
+        if (cl == 0) {
+          cv = gvv - gsc * lbv;
+          vv = fabs(cv);
+        } else {
+          cv = gvv - sv;
+          if (cl == 1) {
+            const double rs = -lm - vl + vu;
+            dmax = fmax(dmax, fabs(rs));
+            dmax_u = fmax(dmax_u, fabs(rs) * gsc / obj_scale);
+            vv = fmax(0.0, fmax(slo - gvv, gvv - sup));
+            if (isfin(slo)) { const double pr = (sv - slo) * vl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vl); nz++; }
+            if (isfin(sup)) { const double pr = (sup - sv) * vu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vu); nz++; }
+          }
+        }
+        pmax = fmax(pmax, fabs(cv));
+        vmax_u = fmax(vmax_u, vv / gsc);
+        lsum += fabs(lm);
+      }
+    }
+    OptErr e;
+    e.dual = wmax(dmax); e.dual_u = wmax(dmax_u); e.primal = wmax(pmax); e.viol_u = wmax(vmax_u);
+    e.pmx = wmax(pmx); e.pmn = wmin(pmn);
+    lsum = wsum(lsum); zsum = wsum(zsum); nz = wsumi(nz);
+    e.ncompl = nz;
+    const double smax = 100.0;
+    // IPOPT: s_d over all multipliers (y_c, y_d, z_L, z_U, v_L, v_U)
+    e.s_d = fmax(smax, (lsum + zsum) / fmax(1.0, (double)(M + nz))) / smax;
+    e.s_c = nz > 0 ? fmax(smax, zsum / (double)nz) / smax : 1.0;
+    K.e0 = e;
+  }
+  // ---- termination tests ----
+  {
+    const OptErr e0 = K.e0;
+    const double fx = K.fx;
+    const double err0 = e0.err_at(0.0);
+    if (!(err0 == err0) || !(fx == fx)) { K.status = MPCX_INVALID_NUMBER; return 1; }
+    // IPOPT OptimalityErrorConvergenceCheck::CheckConvergence (square problems: the dual
+    // infeasibility and complementarity tolerances are lifted)
+    if (err0 <= ka.opt.tol && e0.viol_u <= ka.opt.constr_viol_tol &&
+        (K.square || (e0.dual_u <= ka.opt.dual_inf_tol && e0.compl_at(0.0) / obj_scale <= ka.opt.compl_inf_tol))) {
+      K.status = MPCX_SOLVE_SUCCEEDED;
+      return 1;
+    }
+    Acceptable acc = K.acc;
+    if (ka.opt.acceptable_iter > 0 && current_is_acceptable(acc, e0, err0, fx, K.it, obj_scale, K.square, ka.opt)) {
+      acc.count++;
+      K.acc = acc;
+      if (acc.count >= ka.opt.acceptable_iter) { K.status = MPCX_SOLVED_TO_ACCEPTABLE; return 1; }
+    } else {
+      acc.count = 0;
+      K.acc = acc;
+    }
+    if (K.it >= ka.opt.max_iter) return 1;
+  }
+  // ---- barrier parameter update (monotone Fiacco-McCormick) ----
+#pragma unroll 1
+  for (int mu_up = 0; mu_up < 64; ++mu_up) {
+    const double mu = K.mu;
+    if (K.e0.err_at(mu) > ka.opt.kappa_eps * mu || mu <= ka.opt.mu_min) break;
+    // IPOPT MonotoneMuUpdate::CalcNewMuAndTau: floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
+    const double new_mu = fmax(fmax(fmin(ka.opt.tol, ka.opt.compl_inf_tol) / (ka.opt.kappa_eps + 1.0), ka.opt.mu_min),
+                               fmin(ka.opt.kappa_mu * mu, ka.opt.theta_mu == 1.5 ? mu * sqrt(mu) : pow_ool(mu, ka.opt.theta_mu)));
+    if (new_mu == mu) break;  // IPOPT MonotoneMuUpdate: done when mu no longer changes
+    K.mu = new_mu;
+    K.tau = fmax(ka.opt.tau_min, 1.0 - new_mu);
+    K.nfilt = 0;
+  }
+  const double mu = K.mu;
+  // ---- Newton rhs and diagonal terms (rhs_dual with delta_w = delta_c = 0) ----
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    if (i >= NX && i < NW) {
+      const double r = pr0[sl] + mu * pr1[sl];
+      const int b = (i - NX) / NP, off = (i - NX) % NP;
+      const int li = off < NV ? off : LX1 + off - NV;
+      a.rhs(b)[off] = r;
+      a.dg(b)[li] = psx[sl];
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    if (c < M) {
+      const double rr = dq0[sl] - mu * dq1[sl];
+      a.rhs(c / NG)[NP + c % NG] = rr;
+      a.dg(c / NG)[crow(c % NG)] = ddg[sl];
+    }
+  }
+  sync();
+  return 0;
+}
+
 }  // namespace mpcx_kernel
 
 using namespace mpcx_kernel;
@@ -2234,58 +2303,17 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   K.acc = Acceptable{-1e50, -1e50, -1, 0};
 #pragma unroll 1
   for (;;) {
-    {
-      const OptErr e = opt_error(a, K.obj_scale);
-      K.e0 = e;
-    }
-    {
-      const OptErr e0 = K.e0;
-      const double obj_scale = K.obj_scale, fx = K.fx;
-      const double err0 = e0.err_at(0.0);
-      if (!(err0 == err0) || !(fx == fx)) { K.status = MPCX_INVALID_NUMBER; break; }
-      // IPOPT OptimalityErrorConvergenceCheck::CheckConvergence (square problems: the dual
-      // infeasibility and complementarity tolerances are lifted)
-      if (err0 <= OPT(tol) && e0.viol_u <= OPT(constr_viol_tol) &&
-          (K.square || (e0.dual_u <= OPT(dual_inf_tol) && e0.compl_at(0.0) / obj_scale <= OPT(compl_inf_tol)))) {
-        K.status = MPCX_SOLVE_SUCCEEDED;
-        break;
-      }
-      Acceptable acc = K.acc;
-      if (OPT(acceptable_iter) > 0 && current_is_acceptable(acc, e0, err0, fx, K.it, obj_scale, K.square, KOPT)) {
-        acc.count++;
-        K.acc = acc;
-        if (acc.count >= OPT(acceptable_iter)) { K.status = MPCX_SOLVED_TO_ACCEPTABLE; break; }
-      } else {
-        acc.count = 0;
-        K.acc = acc;
-      }
-      if (K.it >= OPT(max_iter)) break;
-    }
-    // barrier parameter update (monotone Fiacco-McCormick)
-#pragma unroll 1
-    for (int mu_up = 0; mu_up < 64; ++mu_up) {
-      const double mu = K.mu;
-      if (K.e0.err_at(mu) > OPT(kappa_eps) * mu || mu <= OPT(mu_min)) break;
-      // IPOPT MonotoneMuUpdate::CalcNewMuAndTau: floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
-      const double new_mu = fmax(fmax(fmin(OPT(tol), OPT(compl_inf_tol)) / (OPT(kappa_eps) + 1.0), OPT(mu_min)),
-                                 fmin(OPT(kappa_mu) * mu, pow_ool(mu, OPT(theta_mu))));
-      if (new_mu == mu) break;  // IPOPT MonotoneMuUpdate: done when mu no longer changes
-      K.mu = new_mu;
-      K.tau = fmax(OPT(tau_min), 1.0 - new_mu);
-      K.nfilt = 0;
-    }
+    if (iter_head(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr())) break;
     PROF(2);
     eval_hess(a, K.obj_scale);
     PROF(3);
-    rhs_primal(a, K.mu, K.obj_scale);
-    PROF(4);
     // factorisation with inertia correction (IPOPT Algorithm IC)
     K.dw = 0.0;
     K.dc = 0.0;
     int ok = 0;
 #pragma unroll 1
     for (int attempt = 0; attempt < 60; ++attempt) {
-      rhs_dual(a, K.mu, K.dw, K.dc);
+      if (attempt > 0) rhs_dual(a, K.mu, K.dw, K.dc);  // attempt 0: iter_head wrote the rhs
       const Inertia in = factor(a, KKTDiag{K.dw, K.dc, NEWTON});
       K.n_fact += 1;
       K.n_chain += gL.seq;

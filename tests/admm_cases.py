@@ -148,3 +148,44 @@ def _pick_times(prob, x, prefix):
     """Trajectory of ``prefix`` on its grid times >= 0 (``Results[name]``)."""
     idx = [i for i, n in enumerate(prob.w_names) if n.split("@")[0] == prefix and int(n.split("@")[1]) >= 0]
     return np.asarray(x)[idx]
+
+
+class CFleetOracle:
+    """Local solves of a scaled fleet by the C IPM restatement over the host-compiled
+    generated models (`oracle/c/gen_model.cpp`, pinned per model against the numpy oracle in
+    tests/test_oracle.py), for `oracle/admm.py` loop restatements at fleet sizes the numpy
+    IPM cannot reach.  ``classes``: the product's FleetClass objects, read only for the
+    agents' cold-start kernel inputs and the columns of the coupling trajectory, of its
+    mean (or mean diff) and multiplier, and of the penalty.  Every agent warm-starts from
+    its own previous solution (one remembered guess per backend,
+    `core/discretization.py:221-223`)."""
+
+    def __init__(self, classes, ipopt):
+        self.cls = {c.name: c for c in classes}
+        self.ipopt = dict(ipopt)
+        self.participation, self.initial, self.last = {}, {}, {}
+        for c in classes:
+            for i in range(c.n):
+                ag = f"{c.name}#{i}"
+                self.participation[ag] = {s.aliases[i]: s.kind for s in c.slots}
+                self.initial[ag] = {s.aliases[i]: float(s.initial[i]) for s in c.slots}
+
+    def __call__(self, ag, inp, rho):
+        from oracle import cbuild
+
+        name, i = ag.split("#")
+        c, i = self.cls[name], int(i)
+        p = c.p0[i].copy()
+        for s in c.slots:
+            mean, mult = inp[s.aliases[i]]
+            p[s.mean_cols] = mean
+            p[s.mult_cols] = mult
+        p[c.rho_col] = rho
+        w0 = self.last.get(ag, c.w0[i]).copy()
+        opts = dict(self.ipopt)
+        tol, mi = opts.pop("tol"), opts.pop("max_iter")
+        w, st, _ = cbuild.solve_generated_fleet(c.backend.problem.gen, p[None], c.lbw[i][None], c.ubw[i][None],
+                                                w0[None], threads=1, tol=tol, max_iter=mi, **opts)
+        assert st[0]["status"] in (0, 1), (ag, st[0])
+        self.last[ag] = w[0]
+        return {s.aliases[i]: w[0][s.w_cols] for s in c.slots}

@@ -238,3 +238,25 @@ def test_partitioned_fleet_world2_matches_world1():
         np.testing.assert_allclose(r["prim"], one["prim"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(np.concatenate([two[0]["locals"], two[1]["locals"]]), one["locals"],
                                rtol=1e-10, atol=1e-12)
+
+
+def test_local_exchange_fleet_with_c_oracle_solves():
+    """The fleet driver on the CPU (numpy ADMM arithmetic + C IPM over the host-compiled
+    generated models, oracle/cpu_fleet.py) against `oracle/admm.local_round` with the same
+    local solver per agent (tests/admm_cases.CFleetOracle): 60 rooms + 4 supply units on one
+    exchange alias -- the CPU rehearsal of the 1024-agent GPU case."""
+    from oracle.cpu_fleet import CpuFleetOps
+    from tests.admm_cases import CFleetOracle
+
+    N, iters = 10, 3
+    classes = bm.c4_fleet_classes(n_rooms=60, n_supply=4, N=N, seed=11)
+    fl = ADMMFleet(classes, device="cpu", ops=CpuFleetOps(bm.TIGHT["ipopt"], threads=2))
+    fl.run_local(penalty_factor=1e4, max_iterations=iters)
+    orc = CFleetOracle(classes, bm.TIGHT["ipopt"])
+    state, hist = oadmm.local_round(orc.participation, orc.initial, orc, 1e4, 1, iters, T=N)
+    np.testing.assert_allclose(fl.trajectories()["mDot_coupling"], hist[-1]["mDot_coupling"], rtol=1e-7, atol=1e-9)
+    loc = fl.locals_of("room", "mDot_out")
+    want = np.array([state["local"][(f"room#{i}", "mDot_coupling")] for i in range(60)])
+    # entries at the mDot >= 0 bound are interior-point distances ~1e-7 that move with the
+    # barrier path (summation order of the mean): absolute 1e-7
+    np.testing.assert_allclose(loc, want, rtol=1e-7, atol=1e-7)

@@ -17,7 +17,7 @@ from agentlib_mpc_amd import benchmarks as bm
 from agentlib_mpc_amd.admm.fleet import ADMMFleet
 from agentlib_mpc_amd.admm.ops import NativeADMMOps
 from oracle import admm as oadmm
-from tests.admm_cases import C2Oracle, C4Oracle
+from tests.admm_cases import C2Oracle, C4Oracle, CFleetOracle
 from tests.cpu_admm_ops import CpuADMMOps
 
 pytestmark = pytest.mark.gpu
@@ -299,3 +299,26 @@ def test_gpu_admm_golden_through_native_kernels():
                 np.testing.assert_allclose(diff[i], case["shifted_diffs"][k], rtol=1e-12, atol=1e-15)
             n_exch += 1
     assert n_cons > 0 and n_exch > 0
+
+
+def test_gpu_c4_fleet_at_scale_matches_local_round_with_c_oracle():
+    """examples/exchange_admm scaled to 1024 agents on ONE exchange alias (1020 rooms with
+    d~U(10,150), T0~U(296,303) + 4 supply units; rho=1e4, N=10, 3 LocalADMM iterations): the
+    GPU fleet against `oracle/admm.local_round` (LocalADMM.process restated, one multiplier per
+    agent) with the local solves done by the C IPM restatement over the host-compiled
+    generated models (tests/admm_cases.CFleetOracle): exchange mean, every agent's local
+    trajectory and multiplier."""
+    N, iters = 10, 3
+    classes = bm.c4_fleet_classes(n_rooms=1020, n_supply=4, N=N, seed=11)
+    fl = ADMMFleet(classes)
+    out = fl.run_local(penalty_factor=1e4, max_iterations=iters)
+    assert out["converged_solves"] == 1024 * iters
+    orc = CFleetOracle(classes, bm.TIGHT["ipopt"])
+    state, hist = oadmm.local_round(orc.participation, orc.initial, orc, 1e4, 1, iters, T=N)
+    np.testing.assert_allclose(fl.trajectories()["mDot_coupling"], hist[-1]["mDot_coupling"], rtol=RTOL, atol=1e-9)
+    for cname, n in (("room", 1020), ("supply", 4)):
+        loc, mult = fl.locals_of(cname, "mDot_out"), fl.multipliers_of(cname, "mDot_out")
+        want_l = np.array([state["local"][(f"{cname}#{i}", "mDot_coupling")] for i in range(n)])
+        want_m = np.array([state["mult"][(f"{cname}#{i}", "mDot_coupling")] for i in range(n)])
+        np.testing.assert_allclose(loc, want_l, rtol=RTOL, atol=1e-7)   # at-bound entries: barrier distances
+        np.testing.assert_allclose(mult, want_m, rtol=RTOL, atol=1e-5 * np.abs(want_m).max())

@@ -23,7 +23,7 @@ def main():
     from agentlib_mpc_amd.optimization_backends.mi355x import ipopt_options_to_kernel
     sopts = bm.REFERENCE if os.environ.get("SOLVER", "reference") == "reference" else bm.TIGHT
     kopts = ipopt_options_to_kernel(sopts)
-    be, cv = bm.BUILDERS[model](solver_options=sopts)
+    be, cv = {**bm.BUILDERS, "mhe_room": bm.mhe_room, "rng_room_mpc": bm.rng_room_mpc}[model](solver_options=sopts)
     path = build_profile_hsaco(be.problem.gen)
     if len(sys.argv) > 1 and sys.argv[1] == "build":
         print(path); return

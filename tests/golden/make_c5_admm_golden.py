@@ -1,4 +1,5 @@
-"""Generate tests/golden/c5_admm_N8.json: the coordinated ADMM round of one
+"""Generate tests/golden/c5_admm_N<N>.json (N = 8, and the example's horizon N = 24 with
+``python tests/golden/make_c5_admm_golden.py 24``): the coordinated ADMM round of one
 three-zone block (3 NARX zones + AHU + CCA) computed by the ORACLE (hand
 restatements `oracle/nlps.py` + oracle IPM + the coordinator-loop restatement
 `oracle/admm.py`), N=8, rho=1, 3 iterations, absolute criterion
@@ -20,7 +21,8 @@ from agentlib_mpc_amd.models import examples as ex  # noqa: E402
 from oracle import admm as oadmm  # noqa: E402
 from tests.admm_cases import C5Oracle  # noqa: E402
 
-N, ITERS, RHO = 8, 3, 1.0
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+ITERS, RHO = 3, 1.0
 
 
 def main():

@@ -149,11 +149,13 @@ def test_gpu_coordinated_closed_loop_matches_oracle():
             np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
 
 
-def test_gpu_three_zone_narx_fleet_matches_oracle_fixture():
+@pytest.mark.parametrize("N", [8, 24])
+def test_gpu_three_zone_narx_fleet_matches_oracle_fixture(N):
     """examples/three_zone_datadriven_admm: 3 NARX zones + AHU + CCA, coordinated ADMM,
-    rho=1, absolute criterion 0.04/0.04, N=8, 3 iterations, against the oracle's round
-    (`tests/golden/c5_admm_N8.json`, `tests/golden/make_c5_admm_golden.py`; both at tol 1e-8)."""
-    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c5_admm_N8.json")))
+    rho=1, absolute criterion 0.04/0.04, 3 iterations, at N=8 and at the example's horizon
+    N=24, against the oracle's round (`tests/golden/c5_admm_N{8,24}.json`,
+    `tests/golden/make_c5_admm_golden.py`; both at tol 1e-8)."""
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", f"c5_admm_N{N}.json")))
     opts = {"ipopt": {"tol": 1e-8, "max_iter": 500, "acceptable_iter": 0}}
     fl = ADMMFleet(bm.c5_fleet_classes(n_blocks=1, N=gold["N"], solver_options=opts))
     out = fl.run_coordinated(gold["rho"], admm_iter_max=3, use_relative_tolerances=False, primal_tol=0.04,

@@ -473,6 +473,9 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         "// >>> device only: static sparse elimination of the stage interior (runtime/stage_elim.py):",
         f"// {len(elim_plan.blocks)} pivot blocks, {elim_plan.n_update} interior updates, {elim_plan.nnz_l} multipliers",
         "#define MPCX_STATIC_ELIM 1",
+        "#ifndef MPCX_ELIM_FENCE  // scheduling fence between pivot blocks (register pressure)",
+        "#define MPCX_ELIM_FENCE __builtin_amdgcn_sched_barrier(0)",
+        "#endif",
         "typedef __attribute__((address_space(3))) double mpcx_elim_ld;",
         "typedef __attribute__((address_space(1))) double mpcx_elim_gd;",
         "typedef __attribute__((address_space(1))) int mpcx_elim_gi;",

@@ -30,7 +30,7 @@ def compile_body(lines: List[str]):
         s = ln.strip()
         if not s:
             continue
-        if s.startswith("//") or s.startswith("__builtin_amdgcn_sched_barrier"):
+        if s.startswith("//") or s.startswith("__builtin_amdgcn_sched_barrier") or s.startswith("MPCX_ELIM_FENCE"):
             continue
         m = re.match(r"if \((\w+) < 0\.0\) \{ pos \+= 1; neg \+= 1; \} else if \((\w+) \+ (\w+) > 0\.0\) pos \+= 2; "
                      r"else neg \+= 2;", s)

@@ -46,7 +46,7 @@ ZERO_PIVOT = "1e-20"  # same constant as the kernel's ZERO_PIVOT (dense path)
 GROWTH = "1e8"
 #: scheduling fence between pivot blocks / substitution sweeps: keeps the live set (and the
 #: callee-saved VGPRs the non-inlined caller would have to spill) small
-SCHED = "  __builtin_amdgcn_sched_barrier(0);"
+SCHED = "  MPCX_ELIM_FENCE;"  # __builtin_amdgcn_sched_barrier(0) unless overridden (codegen.py)
 #: line between the factor and trailing parts: a singular pivot returns before any output
 CHECK = "  if (bad) return 1;"
 
@@ -68,7 +68,7 @@ def count_flops(lines: Sequence[str]) -> int:
     n = 0
     for ln in lines:
         s = ln.strip()
-        if s.startswith("//") or s.startswith("__builtin") or s.startswith("bad |=") or s.startswith("if ("):
+        if s.startswith("//") or s.startswith("__builtin") or s.startswith("MPCX_ELIM_FENCE") or s.startswith("bad |=") or s.startswith("if ("):
             continue
         if "=" not in s:
             continue

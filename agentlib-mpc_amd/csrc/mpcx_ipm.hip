@@ -226,6 +226,12 @@ __device__ __forceinline__ void gargmax(double& v, int& idx) {
 }
 
 __device__ __forceinline__ bool isfin(double v) { return fabs(v) < INFINITY; }
+// broadcast lane `l` (compile-time in unrolled loops) of a double: two v_readlane
+__device__ __forceinline__ double rl_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double absn(double v) {  // |v| with NaN -> +inf (total order for pivoting)
   const double t = fabs(v);
   return t == t ? t : INFINITY;
@@ -1290,20 +1296,25 @@ __device__ __noinline__ Inertia chain_factor(const Agent a) {
   Inertia in{0, 0, 0};
   const int lane = a.lane;
   if constexpr (NX == 1 && NMU == 0) {
-    double dprev = 0.0;
-#pragma unroll 1
+    // scalar chain d_j = a_j - b_j / d_{j-1}: lane j gathers its terms in parallel, the
+    // recurrence runs on broadcast registers (readlane), fully unrolled
+    static_assert(N <= WAVE, "one lane per stage");
+    double aj = 0.0, bj = 0.0;
+    if (lane < N) {
+      const bool fx = (L.fixm[lane] >> LX1) & 1ull;
+      aj = fx ? 1.0 : s11(lane)[0] + (lane + 1 < N ? s00(lane + 1)[0] : 0.0);
+      if (!fx && lane > 0) { const double t = s10(lane)[0]; bj = t * t; }
+    }
+    double dprev = 0.0, mine = 0.0;
+#pragma unroll
     for (int j = 0; j < N; ++j) {
-      double d;
-      if ((L.fixm[j] >> LX1) & 1ull) {
-        d = 1.0;
-      } else {
-        d = s11(j)[0] + (j + 1 < N ? s00(j + 1)[0] : 0.0);
-        if (j > 0) { const double t = s10(j)[0]; d -= t * t * dprev; }
-      }
+      const double a = rl_f64(aj, j), b = rl_f64(bj, j);
+      const double d = a - b * dprev;
       if (fabs(d) <= ZERO_PIVOT) { in.zero++; dprev = 0.0; }
       else { if (d > 0) in.pos++; else in.neg++; dprev = 1.0 / d; }
-      if (lane == 0) L.Dinv[j] = dprev;
+      if (lane == j) mine = dprev;
     }
+    if (lane < N) L.Dinv[lane] = mine;
   } else if constexpr (NC > 0) {
     constexpr int XO = NMU;  // offset of the states inside c
 #pragma unroll 1
@@ -1343,24 +1354,27 @@ __device__ __noinline__ void chain_solve(const Agent a) {
   constexpr int ZS = NX + NC;  // zx stride per stage: [x_k | c_k]
   // rhs_j = z[c] of stage j + E z[x_k] of stage j+1
   if constexpr (NX == 1 && NMU == 0) {
-    if (lane == 0) {
-      double y = 0.0;
-#pragma unroll 1
-      for (int j = 0; j < N; ++j) {
-        double r = L.zx[j * 2 + 1] + (j + 1 < N ? L.zx[(j + 1) * 2] : 0.0);
-        if (j > 0) r -= s10(j)[0] * L.Dinv[j - 1] * y;
-        y = r;
-        L.xs[j] = y;
-      }
-      double x = 0.0;
-#pragma unroll 1
-      for (int j = N - 1; j >= 0; --j) {
-        double r = L.xs[j];
-        if (j + 1 < N) r -= s10(j + 1)[0] * x;
-        x = L.Dinv[j] * r;
-        L.xs[j] = x;
-      }
+    // y_j = c_j - e_j y_{j-1}, x_j = f_j (y_j - g_j x_{j+1}); lane j gathers its terms
+    double cj = 0.0, ej = 0.0, fj = 0.0, gj = 0.0;
+    if (lane < N) {
+      cj = L.zx[lane * 2 + 1] + (lane + 1 < N ? L.zx[(lane + 1) * 2] : 0.0);
+      ej = lane > 0 ? s10(lane)[0] * L.Dinv[lane - 1] : 0.0;
+      fj = L.Dinv[lane];
+      gj = lane + 1 < N ? s10(lane + 1)[0] : 0.0;
     }
+    double y = 0.0, yj = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      y = rl_f64(cj, j) - rl_f64(ej, j) * y;
+      if (lane == j) yj = y;
+    }
+    double x = 0.0, xj = 0.0;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {
+      x = rl_f64(fj, j) * (rl_f64(yj, j) - rl_f64(gj, j) * x);
+      if (lane == j) xj = x;
+    }
+    if (lane < N) L.xs[lane] = xj;
   } else if constexpr (NC > 0) {
     constexpr int XO = NMU;
     for (int c = lane; c < NC; c += WAVE)

@@ -17,6 +17,8 @@ sys.path[:0] = [str(ROOT), str(ROOT / "agentlib-mpc_amd")]
 
 VARIANTS = {
     "base": ([], None),
+    "nofence": (["-DMPCX_ELIM_FENCE=(void)0"], None),
+    "nofence_ipra": (["-DMPCX_ELIM_FENCE=(void)0", "-mllvm", "-enable-ipra"], None),
     "lds20k": (["-DMPCX_LDS_TARGET_OVERRIDE=20000"], None),
     "lds14k": (["-DMPCX_LDS_TARGET_OVERRIDE=14000"], None),
     "lds24k_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=24000", "-DMPCX_MIN_WAVES=2"], None),

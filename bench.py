@@ -733,7 +733,8 @@ def main():
                 "kernel": "mpcx_ipm_solve",
                 "kernel_ms": kernel_ms,
                 "flops_per_launch": flops,
-                "note": "FP64 vector pipe (no FP64 MFMA used); algorithmic flops = generated-code op "
+                "note": "FP64 vector pipe (the C3 model has no network; the C5 NARX networks run on the FP64 "
+                        "matrix cores, DESIGN 2.1b); algorithmic flops = generated-code op "
                         "counts (stage evaluations, sparse static stage elimination, dense fallback stages, "
                         "state chain) x per-agent iteration/factorisation/trial counters; the kernel is bound "
                         "by dependent LDS/L2 round trips, not by FP64 issue (DESIGN §5)",

@@ -568,7 +568,13 @@ __device__ __noinline__ Inertia bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int la
       const double t = fabs(A[i * LD + k]);
       if (t > lam) { lam = t; r = i; }
     }
-    wargmax(lam, r);
+    if constexpr (NN <= 9) {  // candidates in lanes 0..7: DPP reduction inside the lane octet
+      gargmax<8>(lam, r);
+      lam = rl_f64(lam, 0);
+      r = __builtin_amdgcn_readfirstlane(r);
+    } else {
+      wargmax(lam, r);
+    }
     if (r < 0) lam = 0.0;
     int size = 1, kp = k;
     if (fmax(akk, lam) == 0.0 || akk >= BK_ALPHA * lam) {
@@ -577,7 +583,9 @@ __device__ __noinline__ Inertia bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int la
       double sg = 0.0;
       for (int j = k + lane; j < NN; j += WAVE)
         if (j != r) sg = fmax(sg, fabs(A[r * LD + j]));
-      const double sigma = wmax(sg);
+      double sigma;
+      if constexpr (NN <= 8) sigma = rl_f64(gmax<8>(sg), 0);
+      else sigma = wmax(sg);
       if (akk * sigma >= BK_ALPHA * lam * lam) {
         size = 1; kp = k;
       } else if (fabs(A[r * LD + r]) >= BK_ALPHA * sigma) {

@@ -370,6 +370,7 @@ struct Lds {
   KState ks;
 #ifdef MPCX_PROFILE
   double sprof[6];
+  unsigned int dense_seen[2];  // stages ever rejected by the static plan (profile build)
 #endif
 };
 
@@ -1531,6 +1532,9 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     SPROF(1);
   }
   const unsigned long long dm = ((unsigned long long)L.dmask[1] << 32) | L.dmask[0];
+#ifdef MPCX_PROFILE
+  if (a.lane < 2) L.dense_seen[a.lane] |= L.dmask[a.lane];
+#endif
 #else
   const unsigned long long dm = (N == 64) ? ~0ull : ((1ull << N) - 1ull);
 #endif
@@ -2294,6 +2298,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   PROF_DECL
 #ifdef MPCX_PROFILE
   if (lane < 6) gL.sprof[lane] = 0.0;
+  if (lane < 2) gL.dense_seen[lane] = 0u;
   sync();
 #endif
   if (lane == 0) { gL.want_sdh = 0; gL.sdh_ok = 0; gL.hsig = 1.0; gL.seq = 0; }
@@ -2420,6 +2425,10 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   sync();
   if (args.lam_w != nullptr && lane == 0)
     for (int i = 0; i < 16 && i < NW; ++i) ((gdbl*)args.lam_w)[(long)agent * NW + i] = _prof[i];
+  if (args.lam_w != nullptr && lane == 0 && NW > 17) {
+    ((gdbl*)args.lam_w)[(long)agent * NW + 16] = (double)gL.dense_seen[0];
+    ((gdbl*)args.lam_w)[(long)agent * NW + 17] = (double)gL.dense_seen[1];
+  }
 #endif
   if (args.lam_g != nullptr)
     for (int c = lane; c < M; c += WAVE)

@@ -71,6 +71,9 @@ def main():
     for k, v in zip(names, prof.mean(axis=0)):
         print(f"{k:12s} {v/1e3:10.1f} kcyc  {100*v/tot:5.1f}%")
     print("total kcycles/agent", tot / 1e3)
+    seen = lw[:, 16].cpu().numpy().astype(np.int64) | (lw[:, 17].cpu().numpy().astype(np.int64) << 32)
+    hist = [int(((seen >> k) & 1).sum()) for k in range(be.problem.gen.dims["N"])]
+    print("agents with stage k ever on the dense path:", hist)
 
 if __name__ == "__main__":
     main()

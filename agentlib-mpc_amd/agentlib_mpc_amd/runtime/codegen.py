@@ -54,6 +54,8 @@ class GeneratedModel:
     pattern: list = dataclasses.field(default_factory=list)
     #: compact stage image: (row, column) of each stored entry (lp, LDS image, elimination)
     compact: list = dataclasses.field(default_factory=list)
+    #: local index of each stage row in the stage system
+    crow: list = dataclasses.field(default_factory=list)
 
 
 def _bindings(nlp: StageNLP) -> Dict[sx.Expr, str]:
@@ -241,9 +243,12 @@ def _network_section(nlp: StageNLP, bind, fg_assign, gj_all, h_all, emit_gj, emi
     return lines, defs, netx, max(neto, 1)
 
 
-def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
+def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
     st = nlp.stage
-    bordered, force_chain = factorisation_plan(nlp)
+    if _bordered is None:
+        bordered, force_chain = factorisation_plan(nlp)
+    else:
+        bordered, force_chain = list(_bordered), False
     loc = st.local
     nl = len(loc)
     ng = nlp.ng
@@ -388,6 +393,26 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
                 pair_w[(crow[r], lidx(j))] = (10.0 + max(-5.0, min(5.0, math.log10(abs(c))))) if c else 1.0
     elim_fac, elim_tra, elim_plan = stage_elim.emit(P, ni, nv, nx, nx + nmu, eq_duals, pair_w)
     elim_lines = elim_fac + [stage_elim.CHECK] + elim_tra
+    # Equality rows the plan can only pair through a network derivative (NARX output rows)
+    # make near-singular 2x2 pivots whenever that entry is small (a saturated sigmoid), and
+    # the stage then takes the dense path.  If keeping such rows in the border (their
+    # multipliers join the chain, as for bordered continuity rows) leaves an interior whose
+    # 2x2 pivots all pair through network-free entries, generate that structure instead.
+    if _bordered is None and not nmu and not force_chain and nx > 0:
+        col_of = {lidx(j): j for j in range(nl)}
+
+        def network_pairs(plan, lrow_, jac_):
+            return sorted(lrow_[d] for b in plan.blocks if len(b) == 2 for v, d in [b]
+                          if sx.network_sites([jac_[lrow_[d]][col_of[v]]]))
+
+        weak = network_pairs(elim_plan, lrow, jac)
+        if weak and not interior_rank_deficient(nlp, weak):
+            alt = generate(nlp, ts, _bordered=weak)
+            alt_lrow = [-1] * len(alt.pattern)
+            for r, li in enumerate(alt.crow):
+                alt_lrow[li] = r
+            if not network_pairs(alt.elim, alt_lrow, jac):
+                return alt
 
     # -- compact stage image: structural nonzeros + elimination fill only --
     # order: diagonal (i, i) at i, border row (rhs, j) at nloc + 1 + j, then the other
@@ -427,19 +452,6 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     nnz = {"jac": sum(1 for a, _ in gj_assign if a.startswith("jac")),
            "hess": sum(1 for a, _ in h_assign)}
 
-    # LDS budget per one-wave workgroup: 9.6 KB keeps 16 agents per CU; a problem
-    # where not even two compact stage images fit gets up to 40 KB (4 agents per CU) so
-    # its stages are eliminated in one or two rounds (mirrors CSLOT_BYTES /
-    # OTHER_BYTES in csrc/mpcx_ipm.hip)
-    N_, NX_ = nlp.N, nlp.nx
-    nxp, ncp = max(NX_, 1), max(NX_ + nmu, 1)
-    cslot = 8 * (len(compact) | 1)
-    soff = nxp * nxp + ncp * ncp + ncp * nxp
-    other = 8 * (N_ * soff + N_ * ncp * ncp + N_ * (NX_ + ncp) + N_ * ncp + 3 * ncp * ncp + 64 + nlp.npg
-                 + N_ * nlp.nps + N_ + netx + neto) + 8 * ncp + 64 + 336 + 16  # 336: KState, 16: masks
-    need = other + N_ * cslot
-    lds_target = 9600 if other + 2 * cslot <= 9600 else min(need, 40960)
-
     sig = "const double* __restrict__ L, const double* __restrict__ PS, const double* __restrict__ PG, const double TK"
     out: List[str] = [
         "// generated by agentlib_mpc_amd.runtime.codegen — do not edit",
@@ -451,7 +463,6 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
         f"#define MPCX_NPG {nlp.npg}",
         f"#define MPCX_TS {float(ts)!r}",
         f"#define MPCX_ABI {KERNEL_ABI_VERSION}",
-        f"#define MPCX_LDS_TARGET {lds_target}",
         f"#define MPCX_NCPT {len(compact)}",
         f"#define MPCX_CPK_INIT {', '.join(str(pk(i, j)) for i, j in compact)}",
         f"#define MPCX_CIJ_INIT {', '.join(str(i | (j << 8)) for i, j in compact)}",
@@ -505,4 +516,4 @@ def generate(nlp: StageNLP, ts: float = None) -> GeneratedModel:
     key = hashlib.sha1(src.encode()).hexdigest()[:16]
     return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz, block_chain_only=force_chain,
                           bordered_rows=list(bordered), elim=elim_plan, elim_lines=elim_lines, pattern=P,
-                          compact=compact)
+                          compact=compact, crow=crow)

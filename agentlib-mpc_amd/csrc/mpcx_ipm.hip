@@ -88,7 +88,7 @@ constexpr int RB = NLOC;                  // border row holding the right-hand s
 constexpr int NTR = NX + NC + 1;          // trailing rows: x_k, c_k, border
 constexpr int LMU = NI + NX;              // first local index of mu_k
 constexpr int LX1 = NI + NX + NMU;        // first local index of x_{k+1}
-static_assert(NMU == 0 || NMU == NX, "bordered continuity rows: one per state");
+static_assert(NMU <= NG, "bordered rows are stage rows");
 constexpr int PKB = (NLOC + 1) * (NLOC + 2) / 2;  // packed lower triangle incl. border
 constexpr int PKS = PKB | 1;              // odd stride between stage slots
 static_assert(NI > 0, "stage interior must be non-empty");
@@ -131,7 +131,10 @@ constexpr long O_FAC = O_SOL + (long)N * NB;     // [N][NB*LDB] block inverses  
 constexpr long O_CPL = O_FAC + (long)N * NB * LDB;  // [N][NB*NX] couplings      (block chain)
 constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [NCPT][N] compact local systems (evaluators; stage-minor)
 constexpr long O_DG = O_LP + (long)NCPT * N;       // [N][NLOC] diagonal terms (rhs phases; Newton mode)
-constexpr long WS_DOUBLES = O_DG + (long)N * NLOC;
+constexpr int SQ = NX > 0 ? NB : 1;   // the block-chain fallback exists only when stages are coupled
+constexpr int SQL = NX > 0 ? LDB : 1;
+constexpr long O_SQW = O_DG + (long)N * NLOC;  // [2][SQ*SQL] block-chain inverse scratch W, Y
+constexpr long WS_DOUBLES = O_SQW + (NX > 0 ? 2L * SQ * SQL : 0L);
 
 using Args = mpcx_kernel_args;
 // kernel arguments read in place from the kernarg segment (address space 4: scalar
@@ -244,67 +247,6 @@ __host__ __device__ constexpr int pow2floor(int v) { int p = 1; while (p * 2 <= 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // dense packed system + perm/piv (fallback)
-constexpr int CSLOT_BYTES = 8 * NCS;          // compact image (static elimination)
-#ifndef MPCX_NETX
-#define MPCX_NETX 0
-#define MPCX_NETO 0
-#endif
-constexpr int OTHER_BYTES = 8 * (N * SOFF + N * NCC + N * (NX + NCP) + N * NCP + 3 * NCC + 2 * MAXF + NPAR + N +
-                                 MPCX_NETX + MPCX_NETO) + 8 * NCP + 64 + 336 + 16;  // 336: KState, 16: masks
-#ifndef MPCX_LDS_TARGET
-#define MPCX_LDS_TARGET 9600  // keeps 16 one-wave workgroups per CU (160 KB LDS)
-#endif
-#ifdef MPCX_LDS_TARGET_OVERRIDE  // diagnostics (scripts/variants.py)
-#undef MPCX_LDS_TARGET
-#define MPCX_LDS_TARGET MPCX_LDS_TARGET_OVERRIDE
-#endif
-// static path: SRC compact images per round, one lane eliminates a stage, GC lanes assemble it
-constexpr int SRC0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / CSLOT_BYTES));
-constexpr int CROUNDS = (N + SRC0 - 1) / SRC0;
-constexpr int SRC = (N + CROUNDS - 1) / CROUNDS;  // stages per round (balanced)
-constexpr int GC = pow2floor(WAVE / SRC);          // lanes per stage (assembly)
-// dense Bunch-Kaufman path (stages the static plan rejects): SR dense images per round
-constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (MPCX_LDS_TARGET - OTHER_BYTES) / SLOT_BYTES));
-constexpr int ROUNDS = (N + SR0 - 1) / SR0;
-constexpr int SR = (N + ROUNDS - 1) / ROUNDS;   // stages per round (balanced)
-constexpr int G = pow2floor(WAVE / SR);         // lanes per stage
-
-constexpr int SQ = NX > 0 ? NB : 1;   // the block-chain fallback exists only when stages are coupled
-constexpr int SQL = NX > 0 ? LDB : 1;
-struct SeqLds {
-  double A[SQ * SQL];
-  double W[SQ * SQL];
-  double Y[SQ * SQL];
-  double B[SQ * NXP];
-  double BP[SQ * NXP];
-  double P[NXX];
-  double v[SQ];
-  double y[SQ];
-  double t[SQ];
-  int perm[SQ];
-  int piv[SQ];
-};
-struct ParLds {
-  double F[SR * PKS];
-  int perm[SR * NI];
-  int piv[SR * NI];
-};
-struct ParCLds {
-  double F[SRC * NCS];
-};
-struct TrialLds {
-  double xt[NW];
-  double gt[MM];
-};
-union LinLds {
-  SeqLds s;
-  ParLds p;
-  ParCLds c;
-  double sol[N * NB];   // Newton step, block order [V, X1, lambda] per stage
-  TrialLds t;           // line-search trial point (x, scaled g)
-};
-
 // per-iteration results kept in LDS across the phase calls
 struct OptErr {
   double dual, dual_u, primal, viol_u, pmx, pmn, s_d, s_c;
@@ -342,8 +284,12 @@ struct KState {
   int nfilt, it, status, square, n_fact, n_ic, n_fallback, n_trials, n_chain, n_dense;
 };
 
-struct Lds {
-  LinLds u;
+#ifndef MPCX_NETX
+#define MPCX_NETX 0
+#define MPCX_NETO 0
+#endif
+// everything in LDS except the phase-shared union
+struct LdsRest {
   double par[NPAR];        // agent parameters (read by every evaluation)
   double S[N * SOFF];      // local Schur blocks per stage: S00 (x_k), S11 (c_k), S10 (c_k x x_k)
   double Dinv[N * NCC];    // inverses of the chain pivots
@@ -373,6 +319,80 @@ struct Lds {
   unsigned int dense_seen[2];  // stages ever rejected by the static plan (profile build)
 #endif
 };
+
+// phase-shared union: block-chain fallback (its inverse scratch W, Y lives in the
+// workspace), static compact images, dense images, Newton step, line-search trial point
+struct SeqLds {
+  double A[SQ * SQL];
+  double B[SQ * NXP];
+  double BP[SQ * NXP];
+  double P[NXX];
+  double v[SQ];
+  double y[SQ];
+  double t[SQ];
+  int perm[SQ];
+  int piv[SQ];
+};
+struct TrialLds {
+  double xt[NW];
+  double gt[MM];
+};
+
+// LDS budget (one wavefront per workgroup, 160 KB per CU): the most agents per CU for which
+// the fixed part plus a minimal union fits -- all N compact stage images in one round if
+// that still gives >= 4 agents per CU, else at least two images per round -- and the
+// static rounds / dense images take what is left of that share.
+constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // dense packed system + perm/piv (fallback)
+constexpr int CSLOT_BYTES = 8 * NCS;          // compact image (static elimination)
+constexpr int REST_BYTES = (int)sizeof(LdsRest);
+constexpr int UFIX_BYTES = cmax((int)sizeof(SeqLds), cmax(8 * N * NB, (int)sizeof(TrialLds)));
+constexpr int LDS_CU = 163840, LDS_SLACK = 256;
+__host__ __device__ constexpr int apc_for(int need) {  // agents per CU for a per-agent need
+  return (need + LDS_SLACK) * 16 <= LDS_CU ? 16 : (need + LDS_SLACK) * 8 <= LDS_CU ? 8
+       : (need + LDS_SLACK) * 5 <= LDS_CU ? 5 : (need + LDS_SLACK) * 4 <= LDS_CU ? 4
+       : (need + LDS_SLACK) * 3 <= LDS_CU ? 3 : (need + LDS_SLACK) * 2 <= LDS_CU ? 2 : 1;
+}
+constexpr int APC_ONE = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, N * CSLOT_BYTES)));
+constexpr int APC_TWO = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, cmin(N, 2) * CSLOT_BYTES)));
+constexpr int APC = (APC_TWO >= 16 || APC_ONE < 4) ? APC_TWO : APC_ONE;
+#ifdef MPCX_LDS_TARGET_OVERRIDE  // diagnostics (scripts/variants.py): per-agent byte budget
+constexpr int LDS_BUDGET = MPCX_LDS_TARGET_OVERRIDE;
+#else
+constexpr int LDS_BUDGET = LDS_CU / APC - LDS_SLACK;
+#endif
+// static path: SRC compact images per round, one lane eliminates a stage, GC lanes assemble it
+constexpr int SRC0 = cmax(1, cmin(cmin(N, WAVE), (LDS_BUDGET - REST_BYTES) / CSLOT_BYTES));
+constexpr int CROUNDS = (N + SRC0 - 1) / SRC0;
+constexpr int SRC = (N + CROUNDS - 1) / CROUNDS;  // stages per round (balanced)
+constexpr int GC = pow2floor(WAVE / SRC);          // lanes per stage (assembly)
+// dense Bunch-Kaufman path (stages the static plan rejects): SR dense images per round
+constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (LDS_BUDGET - REST_BYTES) / SLOT_BYTES));
+constexpr int ROUNDS = (N + SR0 - 1) / SR0;
+constexpr int SR = (N + ROUNDS - 1) / ROUNDS;   // stages per round (balanced)
+constexpr int G = pow2floor(WAVE / SR);         // lanes per stage
+
+struct ParLds {
+  double F[SR * PKS];
+  int perm[SR * NI];
+  int piv[SR * NI];
+};
+struct ParCLds {
+  double F[SRC * NCS];
+};
+union LinLds {
+  SeqLds s;
+  ParLds p;
+  ParCLds c;
+  double sol[N * NB];   // Newton step, block order [V, X1, lambda] per stage
+  TrialLds t;           // line-search trial point (x, scaled g)
+};
+
+struct Lds : LdsRest {
+  LinLds u;
+};
+#ifndef MPCX_LDS_TARGET_OVERRIDE
+static_assert(sizeof(Lds) + LDS_SLACK <= LDS_CU / APC, "LDS share per agent exceeded");
+#endif
 
 __shared__ Lds gL;  // one agent per workgroup: the agent's LDS scratch
 #define LDSP(x) ((ldsd*)(x))
@@ -423,6 +443,7 @@ struct Agent {
   __device__ gdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
   __device__ gdbl* lp(int k) const { return ws + O_LP + k; }  // entry c of stage k at lp(k)[c * N]
   __device__ gdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
+  __device__ gdbl* sqw() const { return ws + O_SQW; }
 };
 
 // constraint classes: 0 equality, 1 inequality with a finite bound, 2 free
@@ -657,10 +678,11 @@ __device__ __noinline__ Inertia bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int la
 }
 
 // Explicit inverse of a factored block, A^{-1} = P^T L^{-T} D^{-1} L^{-1} P,
-// written in the ORIGINAL index order to `out` (ld LD).  W, Y: LDS scratch.
-template <int NN, int LD, typename OutT>
-__device__ __noinline__ void bk_inverse(const ldsd* A, const ldsi* perm, const ldsi* piv, ldsd* W,
-                                        ldsd* Y, OutT* out, int lane) {
+// written in the ORIGINAL index order to `out` (ld LD).  W, Y: scratch (LDS for the chain
+// pivots, the workspace for the block-chain fallback).
+template <int NN, int LD, typename OutT, typename WT>
+__device__ __noinline__ void bk_inverse(const ldsd* A, const ldsi* perm, const ldsi* piv, WT* W,
+                                        WT* Y, OutT* out, int lane) {
   constexpr int NN2 = NN * NN;
   for (int t = lane; t < NN2; t += WAVE) {
     const int i = t / NN, j = t % NN;
@@ -858,7 +880,7 @@ __device__ __noinline__ Inertia seq_factor(const Agent a, const KKTDiag kd) {
       }
       const Inertia bi = bk_factor<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), lane);
       in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
-      bk_inverse<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), LDSP(L.W), LDSP(L.Y), a.fac(k), lane);
+      bk_inverse<NB, LDB>(LDSP(L.A), LDSI(L.perm), LDSI(L.piv), a.sqw(), a.sqw() + SQ * SQL, a.fac(k), lane);
       sync();
       if (k + 1 < N)
         for (int t = lane; t < NX * NX; t += WAVE)

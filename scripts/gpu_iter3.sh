@@ -1,0 +1,9 @@
+# kernel iteration: IPM + ADMM GPU parity, bench legs, phase profiles (C3, MHE, C5 zone)
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ipm.py tests/test_gpu_admm.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_ipm.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --admm-agents 0 --c2-blocks 0 > gpurun_out/legs.json 2> gpurun_out/legs.err && \
+MODEL=mhe_room timeout -k 10 200 python scripts/prof_phases.py > gpurun_out/phases_mhe.txt 2>&1 && \
+MODEL=room_nn AGENTS=1024 timeout -k 10 200 python scripts/prof_phases.py > gpurun_out/phases_nn.txt 2>&1
+echo "iter3 exit $?"

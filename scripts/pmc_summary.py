@@ -1,4 +1,4 @@
-"""Summarise the FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_verify_pmc.sh into
+"""Summarise the FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_final.sh into
 profiles/<round>/<session>/pmc_traffic_c3.json (read by bench.py ``pmc_traffic``).
 
 Only ``mpcx_ipm_solve`` dispatches of the C3 fleet (grid = 4096 workgroups x 64

@@ -331,12 +331,6 @@ class ADMMFleet:
         self.GMULT = t.zeros((max(G, 1), T), dtype=f64, device=dev)  # exchange multiplier per alias
         self.EXCH = t.as_tensor(self.exchange_flags if G else np.zeros(1, np.int32), dtype=i32, device=dev)
         self.GSTART = t.as_tensor(self.gstart, dtype=i32, device=dev)
-        # one HIP stream per class: the classes' batched solves overlap on the device (the
-        # small class fills the CUs the large class leaves idle in its last generation)
-        self._streams = None
-        if (len(self.classes) > 1 and getattr(self.ops, "_stream", 0) is None
-                and t.device(dev).type == "cuda"):
-            self._streams = [t.cuda.Stream(device=dev) for _ in self.classes]
         self.S = NMOM * T + 1
         nb = self.n_blocks
         self.MOM = t.zeros(self.ops.moments_size(max(G, 1), nb, T), dtype=f64, device=dev)
@@ -408,39 +402,23 @@ class ADMMFleet:
 
     def _solve_all(self, rho: float):
         """Inject mean/diff, multipliers and the block's rho into every agent's p; solve
-        (agents of frozen blocks are skipped); gather locals.  With several classes on a
-        GPU each class runs on its own stream, joined before the status count."""
-        import contextlib
-
-        ops, T, t = self.ops, self.T, self.torch
-        streams = self._streams
-        if streams is not None:
-            main = t.cuda.current_stream(self.device)
-            ready = t.cuda.Event()
-            ready.record(main)
+        (agents of frozen blocks are skipped); gather locals."""
+        ops, T = self.ops, self.T
         for ci, c in enumerate(self.classes):
-            ctx = t.cuda.stream(streams[ci]) if streams is not None else contextlib.nullcontext()
-            with ctx:
-                if streams is not None:
-                    streams[ci].wait_event(ready)
-                for si, s in enumerate(c.slots):
-                    d = c.dev_slots[si]
-                    if s.kind == CONSENSUS:
-                        ops.scatter_rows(T, self.MEAN, d["groups"], c.P, d["mean_cols"])
-                        ops.scatter_rows(T, self.LAMR, d["rows"], c.P, d["mult_cols"])
-                    else:
-                        ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
-                        ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
-                ops.scatter_rows(1, self.RHO_B, c.BLOCK, c.P, c.RHO_COL)  # the block's penalty
-                ops.solve(c, c.ACTIVE if self._masked else None)
-                for si, s in enumerate(c.slots):
-                    d = c.dev_slots[si]
-                    ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows"])
-        if streams is not None:
-            for st_ in streams:
-                main.wait_stream(st_)
-        for c in self.classes:
-            st = c.ST.view(t.int32).view(c.n, STATS_BYTES // 4)[:, _STATUS_WORD]
+            for si, s in enumerate(c.slots):
+                d = c.dev_slots[si]
+                if s.kind == CONSENSUS:
+                    ops.scatter_rows(T, self.MEAN, d["groups"], c.P, d["mean_cols"])
+                    ops.scatter_rows(T, self.LAMR, d["rows"], c.P, d["mult_cols"])
+                else:
+                    ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
+                    ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
+            ops.scatter_rows(1, self.RHO_B, c.BLOCK, c.P, c.RHO_COL)  # the block's penalty
+            ops.solve(c, c.ACTIVE if self._masked else None)
+            for si, s in enumerate(c.slots):
+                d = c.dev_slots[si]
+                ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows"])
+            st = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)[:, _STATUS_WORD]
             ok = (st == 0) | (st == 1)
             if self._masked:
                 ok &= c.ACTIVE != 0

@@ -113,9 +113,11 @@ def test_result_layout_matches_reference_shape():
 def test_rank_deficient_stage_interiors_border_their_continuity_rows():
     """Stage interiors whose equality rows V cannot satisfy (more states than free stage
     inputs: change penalties, MHE lifts, 2-state zones) keep their continuity rows in the
-    border (their multipliers join x_{k+1} in the chain) and stay stage-parallel; the
-    benchmark structures need no bordering; nothing falls back to the block chain."""
-    want = {"one_room": 0, "admm_room": 0, "exchange_room": 0, "room_nn": 0,
+    border (their multipliers join x_{k+1} in the chain) and stay stage-parallel; so do the
+    NARX output rows whose only interior partners are network derivatives (room_nn: three
+    of the four network output rows of the two-step super-stage); the
+    other benchmark structures need no bordering; nothing falls back to the block chain."""
+    want = {"one_room": 0, "admm_room": 0, "exchange_room": 0, "room_nn": 3,
             "one_room_radau": 0, "one_room_du": 2, "exchange_room_rk": 0,
             "mhe_room": 3, "mhe_room_u": 2, "rng_room_mpc": 2}
     for name, n_bordered in want.items():

@@ -337,13 +337,25 @@ def c2_admm_bench(args, world, rank, dev):
         "workload": "C2 scaled: 4-room + air-handler blocks (casadi_admm collocation d=3, N=10, ts=60), "
                     "coordinated consensus, rho=0.4, abs tol 0.002/0.1, iter max 40, per-block stopping",
         "blocks_per_gpu": nb, "agents_per_gpu": 5 * nb,
-        **_block_summary(out, wall, 5),
+        **_block_summary(out, wall, 5, world, dev),
         "cpu_baseline": cpu,
     }
 
 
-def _block_summary(out, wall, agents_per_block):
-    """ADMM iterations/s to consensus of a multi-block coordinated run."""
+def _block_summary(out, wall, agents_per_block, world=1, dev=None):
+    """ADMM iterations/s to consensus of a multi-block coordinated run.  The block counts
+    are global (the residual totals are all-reduced); the converged-solve counter is per
+    rank, so it is summed over the ranks, and the wall time is the max over the ranks."""
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([float(out["converged_solves"]), wall], dtype=torch.float64, device=dev)
+        w = t[1:].clone()
+        dist.all_reduce(t[:1], op=dist.ReduceOp.SUM)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        out = dict(out, converged_solves=int(t[0].item()))
+        wall = float(w[0].item())
     it = np.asarray(out["block_iterations"])
     conv = np.asarray(out["block_converged"])
     solves = int(np.sum(it)) * agents_per_block
@@ -400,7 +412,7 @@ def c5_admm_bench(args, world, rank, dev):
         "workload": "C5: three-zone data-driven ADMM (3 NARX zones + AHU + CCA per block), coordinated "
                     "consensus, rho=1, N=24 ts=1800, abs tol 0.04/0.04, per-block stopping",
         "blocks_per_gpu": nb, "zones_per_gpu": 3 * nb, "agents_per_gpu": 5 * nb,
-        **_block_summary(out, wall, 5),
+        **_block_summary(out, wall, 5, world, dev),
         "solver": "reference IPOPT defaults (casadi_utils.py:197-206)",
         "cpu_baseline": cpu,
     }

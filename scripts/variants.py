@@ -18,6 +18,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "agentlib-mpc_amd")]
 VARIANTS = {
     "base": ([], None),
     "nofence": (["-DMPCX_ELIM_FENCE=(void)0"], None),
+    "inline_log": ([], ("return log(x); }", "return log(x); }\n#define log_ool(x) log(x)")),
     "nofence_ipra": (["-DMPCX_ELIM_FENCE=(void)0", "-mllvm", "-enable-ipra"], None),
     "lds20k": (["-DMPCX_LDS_TARGET_OVERRIDE=20000"], None),
     "lds14k": (["-DMPCX_LDS_TARGET_OVERRIDE=14000"], None),

@@ -207,6 +207,8 @@ class ADMMFleet:
         self.history: List[IterationRecord] = []
         self.rounds = 0
         self._masked = False
+        self._part = None      # per-class participation masks (host) of the current round
+        self.ROW_ON = None     # participation of the rows (device int32 [R + 1]) or None
 
     # ------------------------------------------------------------------ setup
     def _build_groups(self):
@@ -323,7 +325,7 @@ class ADMMFleet:
         t = self.torch
         dev, f64, i32 = self.device, t.float64, t.int32
         T, G, R = self.T, self.G, max(self.R, 1)
-        self.X = t.zeros((R, T), dtype=f64, device=dev)          # local trajectories
+        self.X = t.zeros((R + 1, T), dtype=f64, device=dev)      # local trajectories (+ scratch row R)
         self.LAMR = t.zeros((R, T), dtype=f64, device=dev)       # consensus multipliers per participant
         self.DIFF = t.zeros((R, T), dtype=f64, device=dev)       # exchange mean diffs per participant
         self.MEAN = t.zeros((max(G, 1), T), dtype=f64, device=dev)
@@ -367,7 +369,7 @@ class ADMMFleet:
         for ci, c in enumerate(self.classes):
             for si, s in enumerate(c.slots):
                 x0[self.slot_rows[(ci, si)]] = s.initial[:, None]
-        self.X.copy_(t.as_tensor(x0, device=dev))
+        self.X[:R].copy_(t.as_tensor(x0, device=dev))
         self._ok_count = t.zeros(1, dtype=t.int64, device=dev)
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
@@ -396,9 +398,14 @@ class ADMMFleet:
         act = np.ones(self.n_blocks, bool) if active_b is None else np.asarray(active_b, bool)
         if self.G:
             self.ACTIVE_G.copy_(t.as_tensor(act[self.block_of_group].astype(np.int32)))
+        masked = active_b is not None and not act.all()
         for ci, c in enumerate(self.classes):
-            c.ACTIVE.copy_(t.as_tensor(act[self.agent_blocks[ci]].astype(np.int32)))
-        self._masked = active_b is not None and not act.all()
+            a = act[self.agent_blocks[ci]]
+            if self._part is not None:
+                a = a & self._part[ci]
+                masked = masked or not self._part[ci].all()
+            c.ACTIVE.copy_(t.as_tensor(a.astype(np.int32)))
+        self._masked = masked
 
     def _solve_all(self, rho: float):
         """Inject mean/diff, multipliers and the block's rho into every agent's p; solve
@@ -417,7 +424,8 @@ class ADMMFleet:
             ops.solve(c, c.ACTIVE if self._masked else None)
             for si, s in enumerate(c.slots):
                 d = c.dev_slots[si]
-                ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows"])
+                # agents not participating keep their local (their rows map to the scratch row)
+                ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
             st = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)[:, _STATUS_WORD]
             ok = (st == 0) | (st == 1)
             if self._masked:
@@ -435,7 +443,8 @@ class ADMMFleet:
         act_g = self.ACTIVE_G if per_block and self._masked else None
         blk = self.BLOCK_G if nb > 1 else None
         self.MOM.zero_()
-        ops.moments(G, self.n_global, nb, T, self.GSTART, self.max_rows, self.X, self.LAMR, self.MEAN, self.MOM)
+        ops.moments(G, self.n_global, nb, T, self.GSTART, self.max_rows, self.X, self.LAMR, self.MEAN, self.MOM,
+                    row_on=self.ROW_ON)
         totals = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
         exch = self.EXCH if self.exchange_flags.any() else None
         gm = self.GMULT if exch is not None else None
@@ -447,10 +456,10 @@ class ADMMFleet:
                      self.MEAN, self.DMEAN, totals)
         if apply_multipliers:
             ops.consensus_multipliers(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, rho, rho_g, act_g,
-                                      self.LAMR)
+                                      self.LAMR, row_on=self.ROW_ON)
         # consensus rows of exchange groups are never read; exchange rows of consensus groups neither
         ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT,
-                            apply_multipliers, rho, rho_g, act_g)
+                            apply_multipliers, rho, rho_g, act_g, row_on=self.ROW_ON)
         return totals.view(nb, ADMM_TOTALS)
 
     def _shift_all(self, shift: int):
@@ -469,6 +478,51 @@ class ADMMFleet:
         ops.shift(T, shift, self.GMULT)
 
     # ------------------------------------------------------------------ algorithms
+    def set_participation(self, participating: Optional[Dict[str, Sequence[bool]]] = None):
+        """The agents taking part in the next rounds -- the reference coordinator's agents with
+        status ``ready`` (`admm_coordinator.py:323-353`, `_agents_with_status`): only they are
+        solved, enter the means, get their multipliers updated and count in the residuals
+        (``sources=active_agents``, `admm_datatypes.py:171-331`); the others keep their local
+        trajectories and multipliers (which are still shifted between control steps).
+        ``participating`` maps class names to a bool per agent (missing classes: all
+        agents); None: every agent."""
+        t = self.torch
+        if participating is None:
+            self._part, self.ROW_ON = None, None
+            return
+        part = []
+        on = np.ones(self.X.shape[0], np.int32)
+        for ci, c in enumerate(self.classes):
+            m = np.ones(c.n, bool) if c.name not in participating else np.asarray(participating[c.name], bool)
+            if m.shape != (c.n,):
+                raise ValueError(f"{c.name}: participation mask of {m.shape}, {c.n} agents")
+            part.append(m)
+            for si, s in enumerate(c.slots):
+                rows = np.asarray(self.slot_rows[(ci, si)])
+                on[rows] = m.astype(np.int32)
+                c.dev_slots[si]["rows_part"] = t.as_tensor(np.where(m, rows, self.X.shape[0] - 1).astype(np.int32),
+                                                           device=self.device)
+        self._part = part
+        self.ROW_ON = t.as_tensor(on, device=self.device)
+
+    def register(self, class_name: str, agent: int):
+        """(Re-)registration of one agent (``ADMMCoordinator.register_agent``,
+        `admm_coordinator.py:527-560`): its local trajectories restart from the configured
+        initial value, its consensus multipliers from zero, and -- as the reference does --
+        the multiplier of every exchange alias it joins is reset to zero; its backend starts
+        cold (the NLP guess of the class's initial inputs)."""
+        t = self.torch
+        ci = next(i for i, c in enumerate(self.classes) if c.name == class_name)
+        c = self.classes[ci]
+        for si, s in enumerate(c.slots):
+            row = int(self.slot_rows[(ci, si)][agent])
+            self.X[row] = float(s.initial[agent])
+            self.LAMR[row] = 0.0
+            self.DIFF[row] = 0.0
+            if s.kind == EXCHANGE:
+                self.GMULT[int(self.slot_groups[(ci, si)][agent])] = 0.0
+        c.W[agent].copy_(t.as_tensor(c.w0[agent], device=self.device))
+
     def run_coordinated(self, penalty_factor: float, admm_iter_max: int = 20, primal_tol: float = 1e-3,
                         dual_tol: float = 1e-3, use_relative_tolerances: bool = True, abs_tol: float = 1e-3,
                         rel_tol: float = 1e-3, penalty_change_threshold: float = -1.0,

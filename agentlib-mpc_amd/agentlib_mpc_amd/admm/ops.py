@@ -64,9 +64,12 @@ class NativeADMMOps:
     def moments_size(self, n_groups, n_blocks, T) -> int:
         return int(self.lib.mpcx_admm_moments_size(n_groups, n_blocks, T))
 
-    def moments(self, n_groups, n_global, n_blocks, T, gstart, max_rows, X, LAM, center, out):
-        self._chk(self.lib.mpcx_admm_moments(n_groups, n_global, n_blocks, T, _p(gstart), max_rows, _p(X),
-                                             _p(LAM), _p(center), _p(out), self.stream), "mpcx_admm_moments")
+    # row_on: participation mask of the rows (device int32 [n_rows], None = every row),
+    # the reference coordinator's active agents (include/mpcx.h, *_masked)
+    def moments(self, n_groups, n_global, n_blocks, T, gstart, max_rows, X, LAM, center, out, row_on=None):
+        self._chk(self.lib.mpcx_admm_moments_masked(n_groups, n_global, n_blocks, T, _p(gstart), max_rows, _p(X),
+                                                    _p(LAM), _p(center), _p(row_on), _p(out), self.stream),
+                  "mpcx_admm_moments_masked")
 
     def finalize(self, g0, g1, n_global, n_blocks, T, mom, exchange, gmult, rho, rho_g, active_g, block_g,
                  mean, dmean, totals):
@@ -75,18 +78,19 @@ class NativeADMMOps:
                                               _p(dmean), _p(totals), self.stream),
                   "mpcx_admm_finalize")
 
-    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho, rho_g, active_g, LAM):
-        self._chk(self.lib.mpcx_admm_consensus_multipliers(n_groups, T, _p(gstart), max_rows, _p(X),
-                                                           _p(mean), float(rho), _p(rho_g), _p(active_g),
-                                                           _p(LAM), None, self.stream),
-                  "mpcx_admm_consensus_multipliers")
+    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho, rho_g, active_g, LAM,
+                              row_on=None):
+        self._chk(self.lib.mpcx_admm_consensus_multipliers_masked(n_groups, T, _p(gstart), max_rows, _p(X),
+                                                                  _p(mean), float(rho), _p(rho_g), _p(active_g),
+                                                                  _p(row_on), _p(LAM), None, self.stream),
+                  "mpcx_admm_consensus_multipliers_masked")
 
     def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, update, rho, rho_g,
-                        active_g):
-        self._chk(self.lib.mpcx_admm_exchange_update(n_groups, T, _p(gstart), max_rows, _p(X), _p(mean),
-                                                     _p(diff), _p(gmult), int(bool(update)), float(rho),
-                                                     _p(rho_g), _p(active_g), self.stream),
-                  "mpcx_admm_exchange_update")
+                        active_g, row_on=None):
+        self._chk(self.lib.mpcx_admm_exchange_update_masked(n_groups, T, _p(gstart), max_rows, _p(X), _p(mean),
+                                                            _p(diff), _p(gmult), int(bool(update)), float(rho),
+                                                            _p(rho_g), _p(active_g), _p(row_on), self.stream),
+                  "mpcx_admm_exchange_update_masked")
 
     def shift(self, T, shift, x):
         self._chk(self.lib.mpcx_admm_shift(x.shape[0], T, shift, _p(x), self.stream), "mpcx_admm_shift")

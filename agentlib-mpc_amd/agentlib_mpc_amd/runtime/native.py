@@ -79,6 +79,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
     "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_batch_solve",
     "mpcx_admm_moments_size", "mpcx_admm_moments", "mpcx_admm_finalize",
+    "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
 ]
@@ -145,6 +146,11 @@ def load_library():
         lib.mpcx_admm_consensus_multipliers.argtypes = [i32, i32, vp, i32, vp, vp, f64, vp, vp, vp, vp, vp]
         lib.mpcx_admm_exchange_update.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, i32, f64, vp, vp, vp]
         lib.mpcx_admm_shift.argtypes = [i32, i32, i32, vp, vp]
+        lib.mpcx_admm_moments_masked.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp]
+        lib.mpcx_admm_consensus_multipliers_masked.argtypes = [i32, i32, vp, i32, vp, vp, f64, vp, vp, vp, vp,
+                                                               vp, vp]
+        lib.mpcx_admm_exchange_update_masked.argtypes = [i32, i32, vp, i32, vp, vp, vp, vp, i32, f64, vp, vp,
+                                                         vp, vp]
         lib.mpcx_gather_rows.argtypes = [i32, i32, vp, i64, vp, vp, vp, vp]
         lib.mpcx_scatter_rows.argtypes = [i32, i32, vp, vp, vp, i64, vp, vp]
         lib.mpcx_fill_column.argtypes = [i32, vp, i64, i32, f64, vp]

@@ -76,7 +76,7 @@ __global__ void k_fill_column(int n, double* __restrict__ dst, long ld, int col,
 __global__ void __launch_bounds__(THREADS)
 k_moments(int g_global, int n_tot, int T, const int* __restrict__ gstart, const double* __restrict__ x,
           const double* __restrict__ lam, const double* __restrict__ center,
-          double* __restrict__ out) {
+          const int* __restrict__ row_on, double* __restrict__ out) {
   __shared__ double part[THREADS * NMOM];
   const int g = blockIdx.x;
   const int r0 = gstart[g], r1 = gstart[g + 1];
@@ -93,6 +93,7 @@ k_moments(int g_global, int n_tot, int T, const int* __restrict__ gstart, const 
     if (r < R && t < T) {
       const double c = center[(long)g * T + t];
       for (int row = rb + r; row < re; row += R) {
+        if (row_on && !row_on[row]) continue;  // not participating this round
         const double d = x[(long)row * T + t] - c;
         s1 += d;
         s2 += d * d;
@@ -122,7 +123,12 @@ k_moments(int g_global, int n_tot, int T, const int* __restrict__ gstart, const 
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) atomicAdd(&o[NMOM * T], (double)(re - rb));
+  if (threadIdx.x == 0) {
+    int cnt = re - rb;
+    if (row_on)
+      for (int row = rb; row < re; ++row) cnt -= row_on[row] ? 0 : 1;
+    atomicAdd(&o[NMOM * T], (double)cnt);
+  }
 }
 
 // --- finalize: one wavefront per group ------------------------------------------------
@@ -188,7 +194,8 @@ k_finalize(int g0, int g1, int g_global, int n_tot, int T, const double* __restr
 __global__ void __launch_bounds__(THREADS)
 k_consensus_mult(int T, const int* __restrict__ gstart, const double* __restrict__ x,
                  const double* __restrict__ mean, double rho_s, const double* __restrict__ rho_g,
-                 const int* __restrict__ active_g, double* __restrict__ lam, double* __restrict__ res) {
+                 const int* __restrict__ active_g, const int* __restrict__ row_on, double* __restrict__ lam,
+                 double* __restrict__ res) {
   const int g = blockIdx.x;
   if (!g_active(active_g, g)) return;
   const double rho = g_rho(rho_g, rho_s, g);
@@ -199,6 +206,7 @@ k_consensus_mult(int T, const int* __restrict__ gstart, const double* __restrict
   const long base = (long)rb * T;
   const int n = (re - rb) * T;
   for (int e = threadIdx.x; e < n; e += THREADS) {
+    if (row_on && !row_on[rb + e / T]) continue;  // not participating: multiplier kept
     const double r = mean[(long)g * T + e % T] - x[base + e];
     if (res) res[base + e] = r;
     lam[base + e] -= rho * r;
@@ -208,7 +216,7 @@ k_consensus_mult(int T, const int* __restrict__ gstart, const double* __restrict
 __global__ void __launch_bounds__(THREADS)
 k_exchange_diff(int T, const int* __restrict__ gstart, const double* __restrict__ x,
                 const double* __restrict__ mean, const int* __restrict__ active_g,
-                double* __restrict__ diff) {
+                const int* __restrict__ row_on, double* __restrict__ diff) {
   const int g = blockIdx.x;
   if (!g_active(active_g, g)) return;
   const int r0 = gstart[g], r1 = gstart[g + 1];
@@ -218,7 +226,7 @@ k_exchange_diff(int T, const int* __restrict__ gstart, const double* __restrict_
   const long base = (long)rb * T;
   const int n = (re - rb) * T;
   for (int e = threadIdx.x; e < n; e += THREADS)
-    diff[base + e] = x[base + e] - mean[(long)g * T + e % T];
+    if (!row_on || row_on[rb + e / T]) diff[base + e] = x[base + e] - mean[(long)g * T + e % T];
 }
 
 __global__ void k_exchange_mult(int n_groups, int T, const double* __restrict__ mean, double rho_s,
@@ -292,19 +300,28 @@ extern "C" int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t n_blocks, in
   return (int64_t)n_groups * (NMOM * (int64_t)T + 1) + (int64_t)MPCX_ADMM_TOTALS * n_blocks;
 }
 
-extern "C" int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
-                                 const int32_t* gstart, int32_t max_group_rows,
-                                 const double* locals, const double* multipliers,
-                                 const double* center, double* out, void* stream) {
+extern "C" int mpcx_admm_moments_masked(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
+                                        const int32_t* gstart, int32_t max_group_rows,
+                                        const double* locals, const double* multipliers,
+                                        const double* center, const int32_t* row_on, double* out,
+                                        void* stream) {
   if (n_groups <= 0 || n_global < 0 || n_global > n_groups || n_blocks < 1 || T <= 0 ||
       max_group_rows < 0 || !gstart || !locals || !center || !out)
     return MPCX_ERR_ARG;
   if (max_group_rows == 0) return MPCX_OK;
   hipLaunchKernelGGL(k_moments, group_grid(n_groups, max_group_rows), dim3(THREADS), 0,
                      (hipStream_t)stream, n_global, MPCX_ADMM_TOTALS * n_blocks, T, gstart, locals,
-                     multipliers, center, out);
+                     multipliers, center, row_on, out);
   LAUNCH_CHECK();
   return MPCX_OK;
+}
+
+extern "C" int mpcx_admm_moments(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
+                                 const int32_t* gstart, int32_t max_group_rows,
+                                 const double* locals, const double* multipliers,
+                                 const double* center, double* out, void* stream) {
+  return mpcx_admm_moments_masked(n_groups, n_global, n_blocks, T, gstart, max_group_rows, locals,
+                                  multipliers, center, nullptr, out, stream);
 }
 
 extern "C" int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_global, int32_t n_blocks,
@@ -325,32 +342,42 @@ extern "C" int mpcx_admm_finalize(int32_t g_begin, int32_t g_end, int32_t n_glob
   return MPCX_OK;
 }
 
+extern "C" int mpcx_admm_consensus_multipliers_masked(int32_t n_groups, int32_t T, const int32_t* gstart,
+                                                      int32_t max_group_rows, const double* locals,
+                                                      const double* mean, double rho, const double* rho_g,
+                                                      const int32_t* active_g, const int32_t* row_on,
+                                                      double* mult, double* res, void* stream) {
+  if (n_groups <= 0 || T <= 0 || max_group_rows < 0 || !gstart || !locals || !mean || !mult)
+    return MPCX_ERR_ARG;
+  if (max_group_rows == 0) return MPCX_OK;
+  hipLaunchKernelGGL(k_consensus_mult, group_grid(n_groups, max_group_rows), dim3(THREADS), 0,
+                     (hipStream_t)stream, T, gstart, locals, mean, rho, rho_g, active_g, row_on, mult, res);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
 extern "C" int mpcx_admm_consensus_multipliers(int32_t n_groups, int32_t T, const int32_t* gstart,
                                                int32_t max_group_rows, const double* locals,
                                                const double* mean, double rho, const double* rho_g,
                                                const int32_t* active_g, double* mult, double* res,
                                                void* stream) {
-  if (n_groups <= 0 || T <= 0 || max_group_rows < 0 || !gstart || !locals || !mean || !mult)
-    return MPCX_ERR_ARG;
-  if (max_group_rows == 0) return MPCX_OK;
-  hipLaunchKernelGGL(k_consensus_mult, group_grid(n_groups, max_group_rows), dim3(THREADS), 0,
-                     (hipStream_t)stream, T, gstart, locals, mean, rho, rho_g, active_g, mult, res);
-  LAUNCH_CHECK();
-  return MPCX_OK;
+  return mpcx_admm_consensus_multipliers_masked(n_groups, T, gstart, max_group_rows, locals, mean, rho,
+                                                rho_g, active_g, nullptr, mult, res, stream);
 }
 
-extern "C" int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* gstart,
-                                         int32_t max_group_rows, const double* locals,
-                                         const double* mean, double* diff, double* mult,
-                                         int32_t update_multiplier, double rho, const double* rho_g,
-                                         const int32_t* active_g, void* stream) {
+extern "C" int mpcx_admm_exchange_update_masked(int32_t n_groups, int32_t T, const int32_t* gstart,
+                                                int32_t max_group_rows, const double* locals,
+                                                const double* mean, double* diff, double* mult,
+                                                int32_t update_multiplier, double rho, const double* rho_g,
+                                                const int32_t* active_g, const int32_t* row_on,
+                                                void* stream) {
   if (n_groups <= 0 || T <= 0 || max_group_rows < 0 || !gstart || !locals || !mean || !diff)
     return MPCX_ERR_ARG;
   if (update_multiplier && !mult) return MPCX_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (max_group_rows > 0) {
     hipLaunchKernelGGL(k_exchange_diff, group_grid(n_groups, max_group_rows), dim3(THREADS), 0, s,
-                       T, gstart, locals, mean, active_g, diff);
+                       T, gstart, locals, mean, active_g, row_on, diff);
     LAUNCH_CHECK();
   }
   if (update_multiplier) {
@@ -360,6 +387,15 @@ extern "C" int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int3
     LAUNCH_CHECK();
   }
   return MPCX_OK;
+}
+
+extern "C" int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* gstart,
+                                         int32_t max_group_rows, const double* locals,
+                                         const double* mean, double* diff, double* mult,
+                                         int32_t update_multiplier, double rho, const double* rho_g,
+                                         const int32_t* active_g, void* stream) {
+  return mpcx_admm_exchange_update_masked(n_groups, T, gstart, max_group_rows, locals, mean, diff, mult,
+                                          update_multiplier, rho, rho_g, active_g, nullptr, stream);
 }
 
 extern "C" int mpcx_admm_shift(int32_t n_rows, int32_t T, int32_t shift, double* x, void* stream) {

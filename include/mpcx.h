@@ -219,6 +219,27 @@ int mpcx_admm_exchange_update(int32_t n_groups, int32_t T, const int32_t* gstart
                               double* diff, double* multiplier, int32_t update_multiplier,
                               double rho, const double* rho_g, const int32_t* active_g,
                               void* stream);
+/* Participation (the reference coordinator's active agents, admm_coordinator.py:323-353:
+ * only the sources with status `ready` enter means, multiplier updates and residuals,
+ * ConsensusVariable/ExchangeVariable(..., sources=active_agents), admm_datatypes.py:171-331).
+ * The *_masked variants take row_on[n_rows] (device int32; NULL = all rows): rows with
+ * row_on == 0 are left out of the moments (sums and participant count), keep their
+ * multiplier (consensus) and their diff (exchange).  The unmasked entry points above are
+ * these with row_on = NULL. */
+int mpcx_admm_moments_masked(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
+                             const int32_t* gstart, int32_t max_group_rows, const double* locals,
+                             const double* multipliers, const double* center, const int32_t* row_on,
+                             double* out, void* stream);
+int mpcx_admm_consensus_multipliers_masked(int32_t n_groups, int32_t T, const int32_t* gstart,
+                                           int32_t max_group_rows, const double* locals,
+                                           const double* mean, double rho, const double* rho_g,
+                                           const int32_t* active_g, const int32_t* row_on,
+                                           double* multipliers, double* primal_residual, void* stream);
+int mpcx_admm_exchange_update_masked(int32_t n_groups, int32_t T, const int32_t* gstart,
+                                     int32_t max_group_rows, const double* locals, const double* mean,
+                                     double* diff, double* multiplier, int32_t update_multiplier,
+                                     double rho, const double* rho_g, const int32_t* active_g,
+                                     const int32_t* row_on, void* stream);
 /* Shift rows by one control interval: x[i][:] <- x[i][shift:] ++ x[i][T-shift:]
  *   <- ConsensusVariable/ExchangeVariable.shift_values_by_one (admm_datatypes.py:275-282,
  *      326-331), ADMM._shift (admm.py:329-342) */

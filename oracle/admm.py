@@ -88,14 +88,23 @@ class _Consensus:
         self.primal_residual = np.array([0.0])
         self.mult = {}
 
-    def update_mean(self):
-        arr = np.array([self.local[s] for s in self.local])
+    def sources(self, active):
+        # CouplingVariable._relevant_sources (`admm_datatypes.py:171-177`)
+        return list(self.local) if active is None else [s for s in self.local if s in active]
+
+    def update_mean(self, active=None):
+        srcs = self.sources(active)
+        if not srcs:
+            return
+        arr = np.array([self.local[s] for s in srcs])
         mean = np.mean(arr, axis=0)
         self.delta_mean = self.mean - mean
         self.mean = list(mean)
 
-    def update_multipliers(self, rho):
-        srcs = list(self.local)
+    def update_multipliers(self, rho, active=None):
+        srcs = self.sources(active)
+        if not srcs:
+            return
         traj = np.array([self.local[s] for s in srcs])
         mul = np.array([self.mult[s] for s in srcs])
         self.primal_residual = np.array(self.mean) - traj
@@ -121,15 +130,21 @@ class _Exchange:
         self.diff = {}
         self.mult = []
 
-    def update_mean(self):
-        arr = np.array([self.local[s] for s in self.local])
+    def sources(self, active):
+        return list(self.local) if active is None else [s for s in self.local if s in active]
+
+    def update_mean(self, active=None):
+        srcs = self.sources(active)
+        if not srcs:
+            return
+        arr = np.array([self.local[s] for s in srcs])
         mean = np.mean(arr, axis=0)
         self.delta_mean = self.mean - mean
         self.mean = list(mean)
-        for s in self.local:
+        for s in srcs:
             self.diff[s] = list(np.asarray(self.local[s]) - mean)
 
-    def update_multipliers(self, rho):
+    def update_multipliers(self, rho, active=None):  # every round, whatever the sources (:311-324)
         self.primal_residual = np.array(self.mean)
         self.mult = list(self.mult + rho * self.primal_residual)
 
@@ -143,13 +158,16 @@ class _Exchange:
 def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max, primal_tol=1e-3,
                       dual_tol=1e-3, use_relative_tolerances=True, abs_tol=1e-3, rel_tol=1e-3,
                       penalty_change_threshold=-1.0, penalty_change_factor=2.0, T=None, state=None,
-                      solve_batch=None):
+                      solve_batch=None, active=None):
     """One round of ``ADMMCoordinator._fast_process`` (`admm_coordinator.py:259-321`).
 
     participation: {agent: {alias: "consensus"|"exchange"}}; initial: {agent: {alias: value}}
     solve(agent, {alias: (mean_or_diff, multiplier)}, rho) -> {alias: local trajectory}
     solve_batch (optional): [(agent, inputs)], rho -> [outputs] — the same solves of one
     iteration at once (they are independent; the fixture generators run them in parallel).
+    active (optional): the agents with status ``ready`` this round (`admm_coordinator.py:
+    323-353`); only they are solved and enter means, multiplier updates and the residual
+    scalings (``sources=active_agents``); None: every registered agent.
     Returns (state, history [(primal, dual, rho after the variation)], iterations, converged).
     """
     if state is None:  # registration (`admm_coordinator.py:528-560`)
@@ -165,7 +183,7 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
                     v.mult = [0] * T
     vars_ = state["vars"]
     for v in vars_.values():
-        v.update_mean()
+        v.update_mean(active)
     for v in vars_.values():
         v.shift(horizon)
     hist = []
@@ -174,6 +192,8 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
     for it in range(1, admm_iter_max + 1):
         reqs = []
         for ag, coups in participation.items():
+            if active is not None and ag not in active:
+                continue
             inp = {}
             for al, kind in coups.items():
                 v = vars_[al]
@@ -185,17 +205,17 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
             for al in participation[ag]:
                 vars_[al].local[ag] = list(np.ravel(out[al]))
         for v in vars_.values():
-            v.update_mean()
+            v.update_mean(active)
         for v in vars_.values():
-            v.update_multipliers(rho)
+            v.update_multipliers(rho, active)
         prim, dual, flat_locals, flat_means, flat_mult = [], [], [], [], []
         for v in vars_.values():
             prim.extend(v.primal_residual.flatten())
             dual.extend((rho * v.delta_mean).flatten())
-            flat_locals.extend(list(v.local.values()))
+            flat_locals.extend([v.local[s] for s in v.sources(active)])
             flat_means.extend(v.mean)
             if isinstance(v, _Consensus):
-                flat_mult.extend(list(v.mult.values()))
+                flat_mult.extend([v.mult[s] for s in v.sources(active)])
             else:
                 flat_mult.extend(v.mult)
         pn, dn = float(np.linalg.norm(prim)), float(np.linalg.norm(dual))
@@ -219,6 +239,19 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
             converged = True
             break
     return state, hist, it, converged
+
+
+def register(state, agent, coups, initial, T):
+    """``ADMMCoordinator.register_agent`` (`admm_coordinator.py:527-560`): the agent's local
+    trajectories start from its initial value, its consensus multipliers from zero, and the
+    multiplier of an exchange alias it joins is reset to zero."""
+    for al, kind in coups.items():
+        v = state["vars"].setdefault(al, _Consensus() if kind == "consensus" else _Exchange())
+        v.local[agent] = [float(initial[al])] * T
+        if kind == "consensus":
+            v.mult[agent] = [0] * T
+        else:
+            v.mult = [0] * T
 
 
 def _norm_lists(items):

@@ -63,23 +63,25 @@ class CpuFleetOps:
     def _off(g, n_global, n_blocks, T):
         return g * (NMOM * T + 1) + (TOTALS * n_blocks if g >= n_global else 0)
 
-    def moments(self, n_groups, n_global, n_blocks, T, gstart, max_rows, X, LAM, center, out):
+    def moments(self, n_groups, n_global, n_blocks, T, gstart, max_rows, X, LAM, center, out, row_on=None):
         gs, x, c, o = gstart.numpy(), X.numpy(), center.numpy(), out.numpy()
         lam = None if LAM is None else LAM.numpy()
+        on = np.ones(x.shape[0], bool) if row_on is None else row_on.numpy() != 0
         for g in range(n_groups):
-            r0, r1 = gs[g], gs[g + 1]
-            if r1 <= r0:
+            rows = np.arange(gs[g], gs[g + 1])
+            rows = rows[on[rows]]
+            if rows.size == 0:
                 continue
             b = self._off(g, n_global, n_blocks, T)
-            d = x[r0:r1] - c[g]
+            d = x[rows] - c[g]
             o[b:b + T] += d.sum(0)
             o[b + T:b + 2 * T] += (d * d).sum(0)
             if lam is not None:
-                l = lam[r0:r1]
+                l = lam[rows]
                 o[b + 2 * T:b + 3 * T] += l.sum(0)
                 o[b + 3 * T:b + 4 * T] += (l * l).sum(0)
                 o[b + 4 * T:b + 5 * T] += (l * d).sum(0)
-            o[b + NMOM * T] += r1 - r0
+            o[b + NMOM * T] += rows.size
 
     @staticmethod
     def _g(rho, rho_g, active_g, g):
@@ -118,21 +120,28 @@ class CpuFleetOps:
                 prim, ((rho * (c - new)) ** 2).sum(), (s2 + 2 * c * s1 + n * c * c).sum(),
                 (new * new).sum(), ls, n, T if is_ex else n, 1.0]
 
-    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho_s, rho_g, active_g, LAM):
+    def consensus_multipliers(self, n_groups, T, gstart, max_rows, X, mean, rho_s, rho_g, active_g, LAM,
+                              row_on=None):
         gs, x, m, lam = gstart.numpy(), X.numpy(), mean.numpy(), LAM.numpy()
+        ron = np.ones(x.shape[0], bool) if row_on is None else row_on.numpy() != 0
         for g in range(n_groups):
             on, rho = self._g(rho_s, rho_g, active_g, g)
             if on:
-                lam[gs[g]:gs[g + 1]] -= rho * (m[g] - x[gs[g]:gs[g + 1]])
+                rows = np.arange(gs[g], gs[g + 1])
+                rows = rows[ron[rows]]
+                lam[rows] -= rho * (m[g] - x[rows])
 
     def exchange_update(self, n_groups, T, gstart, max_rows, X, mean, diff, gmult, update, rho_s, rho_g,
-                        active_g):
+                        active_g, row_on=None):
         gs, x, m, df = gstart.numpy(), X.numpy(), mean.numpy(), diff.numpy()
+        ron = np.ones(x.shape[0], bool) if row_on is None else row_on.numpy() != 0
         for g in range(n_groups):
             on, rho = self._g(rho_s, rho_g, active_g, g)
             if not on:
                 continue
-            df[gs[g]:gs[g + 1]] = x[gs[g]:gs[g + 1]] - m[g]
+            rows = np.arange(gs[g], gs[g + 1])
+            rows = rows[ron[rows]]
+            df[rows] = x[rows] - m[g]
             if update:
                 gmult.numpy()[g] += rho * m[g]
 

@@ -189,3 +189,30 @@ class CFleetOracle:
         assert st[0]["status"] in (0, 1), (ag, st[0])
         self.last[ag] = w[0]
         return {s.aliases[i]: w[0][s.w_cols] for s in c.slots}
+
+
+def participation_rounds(fleet, oracle, N, iters, rho=0.4):
+    """Three coordinator control steps of the 4-room example: all agents, then room 1 not
+    ready (left out of solves, means, multiplier updates and residual scalings, its
+    multipliers still shifted), then room 1 re-registered (local from its initial value,
+    multipliers zero, cold-started backend).  Yields (fleet round, oracle state, oracle
+    history, oracle iterations) per step."""
+    from oracle import admm as oadmm
+
+    kw = dict(admm_iter_max=iters, use_relative_tolerances=False, primal_tol=1e-9, dual_tol=1e-9)
+    state = None
+    everyone = set(oracle.participation)
+    for step in range(3):
+        active = everyone
+        if step == 1:
+            fleet.set_participation({"room": [True, False, True, True]})
+            active = everyone - {"room1"}
+        elif step == 2:
+            fleet.set_participation(None)
+            fleet.register("room", 1)
+            oadmm.register(state, "room1", oracle.participation["room1"], oracle.initial["room1"], 3 * N)
+            oracle.last.pop("room1", None)
+        out = fleet.run_coordinated(rho, **kw)
+        state, hist, it, _ = oadmm.coordinated_round(oracle.participation, oracle.initial, oracle, rho, N,
+                                                     T=3 * N, state=state, active=active, **kw)
+        yield out, state, hist, it

@@ -19,7 +19,7 @@ from agentlib_mpc_amd import benchmarks as bm
 from agentlib_mpc_amd.admm.fleet import ADMMFleet
 from oracle import admm as oadmm
 from oracle import nlps
-from tests.admm_cases import C2Oracle, C4Oracle
+from tests.admm_cases import C2Oracle, C4Oracle, participation_rounds
 from tests.cpu_admm_ops import CpuADMMOps
 
 RTOL = 1e-5
@@ -260,3 +260,28 @@ def test_local_exchange_fleet_with_c_oracle_solves():
     # entries at the mDot >= 0 bound are interior-point distances ~1e-7 that move with the
     # barrier path (summation order of the mean): absolute 1e-7
     np.testing.assert_allclose(loc, want, rtol=1e-7, atol=1e-7)
+
+
+def test_participation_and_registration_rounds_match_oracle():
+    """Coordinator participation semantics (`admm_coordinator.py:323-353`,
+    `:527-560`): a round without room 1 (not ready) and a round after its re-registration,
+    fleet driver vs the oracle's coordinator restatement with the same active sets."""
+    N, iters = 2, 2
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N), device="cpu", ops=_c2_ops(N))
+    orc = C2Oracle(N, bm.C2_ROOMS)
+    prev = None
+    for step, (out, state, hist, it) in enumerate(participation_rounds(fl, orc, N, iters)):
+        assert out["iterations"] == it, step
+        room1 = fl.locals_of("room", "mDot")[1].copy()
+        if step == 1:   # not ready: its local trajectory is not re-solved
+            np.testing.assert_array_equal(room1, prev)
+        prev = room1
+        got = np.array([[r.primal_residual, r.dual_residual] for r in out["records"]])
+        np.testing.assert_allclose(got, np.array(hist)[:, :2], rtol=RTOL, atol=1e-10, err_msg=f"step {step}")
+        for i in range(4):
+            al = f"mDot{i + 1}_coupling_b0"
+            np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
+            np.testing.assert_allclose(fl.multipliers_of("ahu", f"mDot_out_{i + 1}")[0],
+                                       state["vars"][al].mult["ahu"], rtol=RTOL, atol=1e-8)
+        np.testing.assert_allclose(fl.locals_of("room", "mDot")[1], state["vars"]["mDot2_coupling_b0"].local["room1"],
+                                   rtol=RTOL, atol=1e-10)

@@ -17,7 +17,7 @@ from agentlib_mpc_amd import benchmarks as bm
 from agentlib_mpc_amd.admm.fleet import ADMMFleet
 from agentlib_mpc_amd.admm.ops import NativeADMMOps
 from oracle import admm as oadmm
-from tests.admm_cases import C2Oracle, C4Oracle, CFleetOracle
+from tests.admm_cases import C2Oracle, C4Oracle, CFleetOracle, participation_rounds
 from tests.cpu_admm_ops import CpuADMMOps
 
 pytestmark = pytest.mark.gpu
@@ -53,6 +53,7 @@ def test_admm_kernels_match_restatement(T, sizes, n_global, n_blocks):
     BLK = (np.arange(G) % n_blocks).astype(np.int32)
     RHO_G = rng.uniform(0.2, 2.0, G) if n_blocks > 1 else None
     ACT_G = (np.arange(G) % 3 != 1).astype(np.int32) if n_blocks > 1 else None
+    ROW_ON = (rng.random(R) > 0.3).astype(np.int32) if n_blocks > 1 else None   # participation
     gpu, cpu = NativeADMMOps(), CpuADMMOps({})
     res = []
     for ops, mk in ((gpu, lambda a: _pair(a)[0]), (cpu, lambda a: _pair(a)[1])):
@@ -60,16 +61,17 @@ def test_admm_kernels_match_restatement(T, sizes, n_global, n_blocks):
         blk = mk(BLK) if n_blocks > 1 else None
         rho_g = None if RHO_G is None else mk(RHO_G)
         act_g = None if ACT_G is None else mk(ACT_G)
+        ron = None if ROW_ON is None else mk(ROW_ON)
         dmean = mk(np.zeros((G, T)))
         diff = mk(np.zeros((R, T)))
         mom = mk(np.zeros(ops.moments_size(G, n_blocks, T)))
-        ops.moments(G, n_global, n_blocks, T, gs, max(sizes), x, lam, mean, mom)
+        ops.moments(G, n_global, n_blocks, T, gs, max(sizes), x, lam, mean, mom, row_on=ron)
         off = n_global * (5 * T + 1)
         tot = mom[off:off + 8 * n_blocks]
         ops.finalize(n_global, G, n_global, n_blocks, T, mom, ex, gm, 0.7, rho_g, act_g, blk, mean, dmean, tot)
         ops.finalize(0, n_global, n_global, n_blocks, T, mom, ex, gm, 0.7, rho_g, act_g, blk, mean, dmean, tot)
-        ops.consensus_multipliers(G, T, gs, max(sizes), x, mean, 0.7, rho_g, act_g, lam)
-        ops.exchange_update(G, T, gs, max(sizes), x, mean, diff, gm, True, 0.7, rho_g, act_g)
+        ops.consensus_multipliers(G, T, gs, max(sizes), x, mean, 0.7, rho_g, act_g, lam, row_on=ron)
+        ops.exchange_update(G, T, gs, max(sizes), x, mean, diff, gm, True, 0.7, rho_g, act_g, row_on=ron)
         ops.shift(T, 3, lam)
         cols = mk(COLS)
         dst = mk(np.zeros((R, T + 5)))
@@ -147,6 +149,31 @@ def test_gpu_coordinated_closed_loop_matches_oracle():
         for i in range(4):
             al = f"mDot{i + 1}_coupling_b0"
             np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
+
+
+def test_gpu_participation_and_registration_match_oracle():
+    """Coordinator participation on the GPU fleet (`admm_coordinator.py:323-353`,
+    `:527-560`): room 1 not ready for one control step (masked out of the batched solve,
+    the segmented means, multipliers and residual scalings), then re-registered with a
+    cold start, against the oracle's coordinator restatement with the same active sets."""
+    N, iters = 10, 3
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N))
+    orc = C2Oracle(N, bm.C2_ROOMS)
+    prev = None
+    for step, (out, state, hist, it) in enumerate(participation_rounds(fl, orc, N, iters)):
+        assert out["iterations"] == it, step
+        got = np.array([[r.primal_residual, r.dual_residual] for r in out["records"]])
+        np.testing.assert_allclose(got, np.array(hist)[:, :2], rtol=RTOL, atol=1e-10, err_msg=f"step {step}")
+        room1 = fl.locals_of("room", "mDot")[1].copy()
+        if step == 1:
+            np.testing.assert_array_equal(room1, prev)
+        prev = room1
+        np.testing.assert_allclose(room1, state["vars"]["mDot2_coupling_b0"].local["room1"], rtol=RTOL, atol=1e-10)
+        for i in range(4):
+            al = f"mDot{i + 1}_coupling_b0"
+            np.testing.assert_allclose(fl.trajectories()[al], state["vars"][al].mean, rtol=RTOL, atol=1e-10)
+            np.testing.assert_allclose(fl.multipliers_of("ahu", f"mDot_out_{i + 1}")[0],
+                                       state["vars"][al].mult["ahu"], rtol=RTOL, atol=1e-8)
 
 
 @pytest.mark.parametrize("N", [8, 24])

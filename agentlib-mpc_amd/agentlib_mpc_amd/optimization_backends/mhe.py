@@ -33,11 +33,12 @@ and the same reference-variable values; ``ξ_k, ϑ_k (k ≥ 1)`` and ``θ_k`` ar
 (Rows with two infinite bounds instead of ±1e8 stall the iteration — in the
 kernel and in the oracle IPM alike — so the open rows use finite bounds.)
 
-The lifted MHE runs on the kernel's sequential block-chain factorisation: the
-stage-parallel interior elimination does not converge on it (measured with
-``scripts/mhe_diag.py``: 500 iterations at mu = 0.1 vs 12 iterations on the
-block chain, which matches the oracle), so the code object is built with
-``MPCX_FORCE_BLOCK_CHAIN``.
+The lifted stage interior is singular with the continuity / shift rows in it (more
+lifted states than free stage inputs), so the NLP asks for a special factorisation
+(``force_block_chain``); the code generator keeps those rows in the border, their
+multipliers join ``x_{k+1}`` in the state chain, and every stage is eliminated in
+parallel (runtime/codegen.py ``factorisation_plan``).  Stage 0, where the link rows are
+open, has a static elimination plan of its own (``gen_stage_elim0``).
 
 ``MHEBackend.sample`` (:426-542) is not restated: the reference backend samples
 through ``utils.sampling.sample`` (`core/casadi_backend.py:177-240`), so that

@@ -51,6 +51,9 @@ class GeneratedModel:
     #: static elimination plan of the stage interior and its generated body (stage_elim.py)
     elim: object = None
     elim_lines: list = dataclasses.field(default_factory=list)
+    #: plan of stage 0 when rows that are equalities at k >= 1 are open there (else None)
+    elim0: object = None
+    elim0_lines: list = dataclasses.field(default_factory=list)
     pattern: list = dataclasses.field(default_factory=list)
     #: compact stage image: (row, column) of each stored entry (lp, LDS image, elimination)
     compact: list = dataclasses.field(default_factory=list)
@@ -88,14 +91,15 @@ def _structural_rank(rows: List[set], n_cols: int) -> int:
     return sum(1 for r in range(len(rows)) if augment(r, set()))
 
 
-def equality_rows(nlp: StageNLP):
-    """Stage rows whose bound expressions coincide at a random parameter point."""
+def equality_rows(nlp: StageNLP, stage: int = None):
+    """Stage rows whose bound expressions coincide at a random parameter point, at an
+    inner stage (k >= 1) or at ``stage``."""
     import numpy as np
 
     st = nlp.stage
     rng = np.random.default_rng(0)
     vals = {s: float(rng.uniform(0.5, 1.5)) for s in list(st.PS) + list(st.PG)}
-    vals[st.TK] = nlp.ts * min(1, nlp.N - 1)  # an inner stage (k >= 1)
+    vals[st.TK] = nlp.ts * (min(1, nlp.N - 1) if stage is None else stage)
     lb = np.array(sx.evaluate(st.g_lb, vals), float)
     ub = np.array(sx.evaluate(st.g_ub, vals), float)
     return [int(i) for i in np.flatnonzero(lb == ub)]
@@ -393,6 +397,16 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
                 pair_w[(crow[r], lidx(j))] = (10.0 + max(-5.0, min(5.0, math.log10(abs(c))))) if c else 1.0
     elim_fac, elim_tra, elim_plan = stage_elim.emit(P, ni, nv, nx, nx + nmu, eq_duals, pair_w)
     elim_lines = elim_fac + [stage_elim.CHECK] + elim_tra
+    # Stage 0 may open rows that are equalities at k >= 1 (MHE: the link rows of the free
+    # x_0 and parameters).  Pairing a variable with such a row makes a 2x2 pivot whose
+    # multipliers exceed the growth bound (the row's diagonal is ~1e16 larger than the
+    # Jacobian entry), so stage 0 gets a plan of its own with those rows as 1x1 pivots.
+    elim0_plan, elim0_lines = None, []
+    if ng and nlp.N > 1:
+        eq0 = sorted(crow[r] for r in equality_rows(nlp, stage=0) if crow[r] < ni)
+        if eq0 != eq_duals:
+            f0, t0, elim0_plan = stage_elim.emit(P, ni, nv, nx, nx + nmu, eq0, pair_w)
+            elim0_lines = f0 + [stage_elim.CHECK] + t0
     # Equality rows the plan can only pair through a network derivative (NARX output rows)
     # make near-singular 2x2 pivots whenever that entry is small (a saturated sigmoid), and
     # the stage then takes the dense path.  If keeping such rows in the border (their
@@ -421,7 +435,7 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
     # and the generated elimination works on it in place (csrc/mpcx_ipm.hip, factor).
     n_img = nloc + 1
     used_pk = {pk(i, j) for i in range(n_img) for j in range(i + 1) if P[i][j]}
-    for ln in elim_lines:
+    for ln in elim_lines + elim0_lines:
         used_pk.update(int(m.group(1)) for m in re.finditer(r"F\[(\d+)\]", ln))
     unpk = {pk(i, j): (i, j) for i in range(n_img) for j in range(i + 1)}
     compact = [(i, i) for i in range(n_img)] + [(nloc, j) for j in range(nloc)]
@@ -436,6 +450,7 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
                 for ln in lines]
 
     elim_lines = to_compact(elim_lines, "F")
+    elim0_lines = to_compact(elim0_lines, "F")
     gj_lines = to_compact(gj_lines, "lp")
     h_lines = to_compact(h_lines, "lp")
 
@@ -496,6 +511,15 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
         "  inert[0] = pos; inert[1] = neg; inert[2] = 0;",
         "  return 0;",
         "}",
+        *([f"// stage 0: {len(elim0_plan.blocks)} pivot blocks, {elim0_plan.n_update} interior updates "
+           f"(rows open at k = 0 are 1x1 pivots)",
+           "#define MPCX_STATIC_ELIM0 1",
+           "__device__ __forceinline__ int gen_stage_elim0(mpcx_elim_ld* __restrict__ F, mpcx_elim_ld* __restrict__ S, mpcx_elim_ld* __restrict__ ZX, mpcx_elim_gd* __restrict__ TR, mpcx_elim_gi* __restrict__ PRM, int* __restrict__ inert) {",
+           "  int bad = 0, pos = 0, neg = 0;",
+           *elim0_lines,
+           "  inert[0] = pos; inert[1] = neg; inert[2] = 0;",
+           "  return 0;",
+           "}"] if elim0_plan is not None else []),
         *net_defs,
         *net_lines,
         "// <<< device only", "",
@@ -516,4 +540,4 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
     key = hashlib.sha1(src.encode()).hexdigest()[:16]
     return GeneratedModel(source=src, key=key, dims=dims, flops=flops, nnz=nnz, block_chain_only=force_chain,
                           bordered_rows=list(bordered), elim=elim_plan, elim_lines=elim_lines, pattern=P,
-                          compact=compact, crow=crow)
+                          compact=compact, crow=crow, elim0=elim0_plan, elim0_lines=elim0_lines)

@@ -352,18 +352,27 @@ __host__ __device__ constexpr int apc_for(int need) {  // agents per CU for a pe
        : (need + LDS_SLACK) * 5 <= LDS_CU ? 5 : (need + LDS_SLACK) * 4 <= LDS_CU ? 4
        : (need + LDS_SLACK) * 3 <= LDS_CU ? 3 : (need + LDS_SLACK) * 2 <= LDS_CU ? 2 : 1;
 }
-constexpr int APC_ONE = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, N * CSLOT_BYTES)));
-constexpr int APC_TWO = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, cmin(N, 2) * CSLOT_BYTES)));
+#ifdef MPCX_STATIC_ELIM0
+constexpr int K0 = 1;
+#else
+constexpr int K0 = 0;
+#endif
+constexpr int NRS = N - K0;                         // stages in the regular rounds
+constexpr int APC_ONE = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, cmax(NRS, 1) * CSLOT_BYTES)));
+constexpr int APC_TWO = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, cmin(cmax(NRS, 1), 2) * CSLOT_BYTES)));
 constexpr int APC = (APC_TWO >= 16 || APC_ONE < 4) ? APC_TWO : APC_ONE;
 #ifdef MPCX_LDS_TARGET_OVERRIDE  // diagnostics (scripts/variants.py): per-agent byte budget
 constexpr int LDS_BUDGET = MPCX_LDS_TARGET_OVERRIDE;
 #else
 constexpr int LDS_BUDGET = LDS_CU / APC - LDS_SLACK;
 #endif
-// static path: SRC compact images per round, one lane eliminates a stage, GC lanes assemble it
-constexpr int SRC0 = cmax(1, cmin(cmin(N, WAVE), (LDS_BUDGET - REST_BYTES) / CSLOT_BYTES));
-constexpr int CROUNDS = (N + SRC0 - 1) / SRC0;
-constexpr int SRC = (N + CROUNDS - 1) / CROUNDS;  // stages per round (balanced)
+// static path: SRC compact images per round, one lane eliminates a stage, GC lanes assemble it.
+// A model whose stage 0 opens rows that are equalities later on (MHE) has a second plan for
+// stage 0 (gen_stage_elim0), run in a round of its own after stages K0.. so that no round
+// executes both bodies divergently.
+constexpr int SRC0 = cmax(1, cmin(cmin(cmax(NRS, 1), WAVE), (LDS_BUDGET - REST_BYTES) / CSLOT_BYTES));
+constexpr int CROUNDS = (NRS + SRC0 - 1) / SRC0;
+constexpr int SRC = CROUNDS > 0 ? (NRS + CROUNDS - 1) / CROUNDS : 1;  // stages per round (balanced)
 constexpr int GC = pow2floor(WAVE / SRC);          // lanes per stage (assembly)
 // dense Bunch-Kaufman path (stages the static plan rejects): SR dense images per round
 constexpr int SR0 = cmax(1, cmin(cmin(N, WAVE), (LDS_BUDGET - REST_BYTES) / SLOT_BYTES));
@@ -1486,12 +1495,18 @@ __device__ __noinline__ void stage_tail(const Agent a, int k, int g, ldsd* F, co
 // back-substitution operators that interior_bk + stage_tail would.  Eliminates in place
 // in the slot's LDS image; returns 1 on a (numerically) singular static pivot, before
 // writing any output: the slot is then re-assembled and factored densely.
+template <bool STAGE0 = false>
 __device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* F) {
   int in[3];
   asm volatile(";; STATIC_BEGIN");
-  const int bad = gen_stage_elim((mpcx_elim_ld*)F, (mpcx_elim_ld*)LDSP(gL.S + k * SOFF),
-                                 (mpcx_elim_ld*)LDSP(gL.zx + k * (NX + NC)), (mpcx_elim_gd*)a.tr(k),
-                                 (mpcx_elim_gi*)a.prm(k), in);
+  mpcx_elim_ld* const S = (mpcx_elim_ld*)LDSP(gL.S + k * SOFF);
+  mpcx_elim_ld* const ZX = (mpcx_elim_ld*)LDSP(gL.zx + k * (NX + NC));
+  int bad;
+#ifdef MPCX_STATIC_ELIM0
+  if constexpr (STAGE0) bad = gen_stage_elim0((mpcx_elim_ld*)F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
+  else
+#endif
+    bad = gen_stage_elim((mpcx_elim_ld*)F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
   asm volatile(";; STATIC_END");
   if (!bad) { atomicAdd(&gL.fin[0], in[0]); atomicAdd(&gL.fin[1], in[1]); }
   return bad;
@@ -1534,7 +1549,7 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   for (int r = 0; r < CROUNDS; ++r) {
     {
       // stage fastest across the lanes: the stage-minor image reads coalesce over the round
-      const int slot = lane_now() % SRC, g = lane_now() / SRC, k = r * SRC + slot;
+      const int slot = lane_now() % SRC, g = lane_now() / SRC, k = K0 + r * SRC + slot;
       if (g < GC && k < N) {
         ldsd* F = LDSP(L.u.c.F + slot * NCS);
         if (kd.mode == LSQ) local_assemble_generic<GC, true>(a, k, g, F, kd);
@@ -1544,7 +1559,7 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     wsync();
     SPROF(0);
     {
-      const int slot = lane_now(), k = r * SRC + slot;  // one lane per stage
+      const int slot = lane_now(), k = K0 + r * SRC + slot;  // one lane per stage
       if (slot < SRC && k < N && static_stage(a, k, LDSP(L.u.c.F + slot * NCS))) {
         atomicOr(&L.dmask[k >> 5], 1u << (k & 31));
         atomicAdd(&L.ks.n_dense, 1);
@@ -1553,6 +1568,22 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     wsync();
     SPROF(1);
   }
+#ifdef MPCX_STATIC_ELIM0
+  {  // stage 0 with its own plan (GC lanes assemble into slot 0, one lane eliminates)
+    ldsd* F = LDSP(L.u.c.F);
+    if (lane_now() < GC) {
+      if (kd.mode == LSQ) local_assemble_generic<GC, true>(a, 0, lane_now(), F, kd);
+      else local_assemble<GC, false>(a, 0, lane_now(), F, kd);
+    }
+    wsync();
+    if (lane_now() == 0 && static_stage<true>(a, 0, F)) {
+      atomicOr(&L.dmask[0], 1u);
+      atomicAdd(&L.ks.n_dense, 1);
+    }
+    wsync();
+    SPROF(1);
+  }
+#endif
   const unsigned long long dm = ((unsigned long long)L.dmask[1] << 32) | L.dmask[0];
 #ifdef MPCX_PROFILE
   if (a.lane < 2) L.dense_seen[a.lane] |= L.dmask[a.lane];

@@ -6,7 +6,7 @@ M=${1:-one_room}
 python - "$M" <<'PY'
 import sys; sys.path[:0] = ['.', 'agentlib-mpc_amd']
 from agentlib_mpc_amd import benchmarks as bm
-be, _ = bm.BUILDERS[sys.argv[1]](solver_options=bm.REFERENCE)
+be, _ = getattr(bm, sys.argv[1])(solver_options=bm.REFERENCE)
 open('/tmp/isa_model.hip', 'w').write(be.problem.gen.source)
 PY
 /opt/rocm/bin/hipcc --cuda-device-only -S --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Iagentlib-mpc_amd/csrc \

@@ -37,7 +37,7 @@ def _dims(gen):
     return ni, d["NV"], nx, nc
 
 
-def _random_system(gen, rng):
+def _random_system(gen, rng, plan=None):
     """Symmetric local system on the generated structure with KKT signs: primal
     diagonal > 0, paired (equality) dual diagonal 0, other dual diagonals < 0."""
     ni, nv, nx, nc = _dims(gen)
@@ -45,7 +45,7 @@ def _random_system(gen, rng):
     n = P.shape[0]
     A = np.where(P, rng.uniform(-1.0, 1.0, (n, n)), 0.0)
     A = np.tril(A) + np.tril(A, -1).T
-    paired = {i for b in gen.elim.blocks if len(b) == 2 for i in b}
+    paired = {i for b in (plan or gen.elim).blocks if len(b) == 2 for i in b}
     for i in range(n):
         if i < nv or i >= ni:
             A[i, i] = rng.uniform(0.5, 5.0) + np.abs(A[i]).sum()
@@ -54,16 +54,23 @@ def _random_system(gen, rng):
     return A
 
 
-@pytest.mark.parametrize("name", sorted(MODELS))
+CASES = sorted(MODELS) + ["mhe_room:stage0"]
+
+
+@pytest.mark.parametrize("name", CASES)
 def test_generated_elimination_matches_dense(name):
-    be, _ = MODELS[name]()
+    """``name:stage0``: the stage-0 plan (rows open at k = 0 pivot as inequalities)."""
+    model, _, which = name.partition(":")
+    be, _ = MODELS[model]()
     gen = be.problem.gen
     ni, nv, nx, nc = _dims(gen)
     ntr = nx + nc + 1
-    code = elim_sim.compile_body(gen.elim_lines)
+    plan, lines = (gen.elim0, gen.elim0_lines) if which else (gen.elim, gen.elim_lines)
+    assert plan is not None
+    code = elim_sim.compile_body(lines)
     rng = np.random.default_rng(11)
     for _ in range(5):
-        A = _random_system(gen, rng)
+        A = _random_system(gen, rng, plan)
         out = elim_sim.run(code, elim_sim.compact(A, gen.compact), ni, ntr, nx * nx + nc * nc + nc * nx, nx + nc)
         assert not out["bad"]
         AII, AIT = A[:ni, :ni], A[:ni, ni:]
@@ -106,3 +113,32 @@ def test_static_plan_is_sparse():
     pl = be.problem.gen.elim
     assert len({i for b in pl.blocks for i in b}) == 14
     assert pl.n_update < 100
+
+
+def test_mhe_stage0_plan_pivots_open_rows_alone():
+    """MHE stage 0: the link rows of the free x_0 / parameters are open (bounds +-1e8), so
+    their KKT diagonal is huge; the stage-0 plan takes them as 1x1 pivots (the generic
+    plan pairs them with the copies xi_0, theta_0 and its 2x2 pivots fail the growth bound,
+    which sent stage 0 to the dense path on every factorisation) and stays accurate with
+    a 1e16 diagonal on those rows."""
+    from agentlib_mpc_amd.runtime import codegen
+
+    be, _ = MODELS["mhe_room"]()
+    gen, nlp = be.problem.gen, be.problem.nlp
+    eq, eq0 = codegen.equality_rows(nlp), codegen.equality_rows(nlp, stage=0)
+    open_rows = sorted(gen.crow[r] for r in set(eq) - set(eq0))
+    assert open_rows
+    in_pairs = {i for b in gen.elim0.blocks if len(b) == 2 for i in b}
+    assert not in_pairs & set(open_rows)
+    assert {i for b in gen.elim.blocks if len(b) == 2 for i in b} & set(open_rows)
+    ni, nv, nx, nc = _dims(gen)
+    ntr = nx + nc + 1
+    rng = np.random.default_rng(5)
+    A = _random_system(gen, rng, gen.elim0)
+    for r in open_rows:
+        A[r, r] = -1e16
+    out = elim_sim.run(elim_sim.compile_body(gen.elim0_lines), elim_sim.compact(A, gen.compact), ni, ntr,
+                       nx * nx + nc * nc + nc * nx, nx + nc)
+    assert not out["bad"]
+    W = np.linalg.solve(A[:ni, :ni], A[:ni, ni:])
+    np.testing.assert_allclose(out["TR"].reshape(ntr, ni).T, W, rtol=1e-8, atol=1e-8 * np.abs(W).max())

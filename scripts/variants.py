@@ -26,6 +26,10 @@ VARIANTS = {
     "lds14k_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=14000", "-DMPCX_MIN_WAVES=2"], None),
     "lds24k": (["-DMPCX_LDS_TARGET_OVERRIDE=24000"], None),
     "w2": (["-DMPCX_MIN_WAVES=2"], None),
+    # 8 agents per CU: LDS share 160 KB / 8 and at most 256 VGPRs (2 waves per SIMD)
+    "apc8_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=20224", "-DMPCX_MIN_WAVES=2"], None),
+    "apc5": (["-DMPCX_LDS_TARGET_OVERRIDE=32512"], None),
+    "apc8": (["-DMPCX_LDS_TARGET_OVERRIDE=20224"], None),
     "w1": (["-DMPCX_MIN_WAVES=1"], None),
     "inl_w2": (["-DMPCX_MIN_WAVES=2"], ("__noinline__", "__attribute__((always_inline))")),
     "inl_w4": ([], ("__noinline__", "__attribute__((always_inline))")),
@@ -41,13 +45,13 @@ VARIANTS = {
 
 def vdir():
     from agentlib_mpc_amd.runtime import native
-    return native.KERNEL_DIR.parent / "variants"
+    return native.KERNEL_DIR.parent / "variants" / os.environ.get("MODEL", "one_room")
 
 
 def build(names):
     from agentlib_mpc_amd import benchmarks as bm
     from agentlib_mpc_amd.runtime import native
-    be, _ = bm.BUILDERS[os.environ.get("MODEL", "one_room")]()
+    be, _ = getattr(bm, os.environ.get("MODEL", "one_room"))()
     gen = be.problem.gen
     d = vdir()
     d.mkdir(parents=True, exist_ok=True)
@@ -85,7 +89,7 @@ def run(names):
     from agentlib_mpc_amd.runtime.native import NativeProblem, STATS_BYTES, stats_to_dicts
     import bench
     model = os.environ.get("MODEL", "one_room")
-    be, cv = bm.BUILDERS[model](solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
+    be, cv = getattr(bm, model)(solver_options={"ipopt": {"tol": 1e-8, "max_iter": 500}})
     n = int(os.environ.get("AGENTS", "4096"))
     if model == "one_room":
         vals = bench.fleet_values(n, 20261017)

@@ -738,6 +738,87 @@ __device__ __noinline__ void bk_inverse(const ldsd* A, const ldsi* perm, const l
   wsync();
 }
 
+// Inverse AND inertia of a small symmetric indefinite block in one pass (state-chain
+// pivots, NN*NN <= 64): the symmetric sweep operator (Goodnight) with Bunch-Kaufman pivot
+// choices.  Lane (i, j) owns entry (i, j) of the LDS image; each pivot step is one pivot
+// search (DPP reductions in the first lane octet) plus ONE read-modify-write of the whole
+// block -- the swept rows/columns become the inverse as the sweep goes, so there are no
+// row swaps, no separate L^{-1} sweep and no final product (bk_factor + bk_inverse take
+// ~3x the dependent LDS round trips).  Pivots are the Schur-complement pivots of a
+// symmetric elimination in the chosen order, so the inertia is the same (Sylvester); a
+// zero pivot is counted and its row/column left out of the inverse, as the LDL^T path
+// does.  A is destroyed; out receives A^{-1} (ld LD).
+template <int NN, int LD, typename OutT>
+__device__ __noinline__ Inertia bk_sweep(ldsd* A, OutT* out, int lane) {
+  static_assert(NN * NN <= WAVE && NN <= 8, "one lane per entry; pivot candidates in one lane octet");
+  constexpr unsigned FULL = (1u << NN) - 1u;
+  Inertia in{0, 0, 0};
+  const int ti = lane / NN, tj = lane % NN;
+  const bool own = lane < NN * NN;
+  unsigned done = 0u, zero = 0u;
+#pragma unroll 1
+  while (done != FULL) {
+    const int k = __builtin_ctz(~done);
+    const bool cand = lane < NN && !((done >> lane) & 1u);
+    double lam = -1.0;
+    int r = -1;
+    if (cand && lane != k) { lam = fabs(A[lane * LD + k]); r = lane; }
+    gargmax<8>(lam, r);
+    lam = rl_f64(lam, 0);
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (r < 0) lam = 0.0;
+    const double akk = fabs(A[k * LD + k]);
+    int p = k, q = -1;  // 1x1 pivot p, or 2x2 pivot {k, q}
+    if (!(fmax(akk, lam) == 0.0 || akk >= BK_ALPHA * lam)) {
+      double sg = 0.0;
+      if (cand && lane != r) sg = fabs(A[r * LD + lane]);
+      const double sigma = rl_f64(gmax<8>(sg), 0);
+      if (akk * sigma >= BK_ALPHA * lam * lam) p = k;
+      else if (fabs(A[r * LD + r]) >= BK_ALPHA * sigma) p = r;
+      else q = r;
+    }
+    if (q < 0) {
+      const double d = A[p * LD + p];
+      done |= 1u << p;
+      if (fabs(d) <= ZERO_PIVOT) { in.zero++; zero |= 1u << p; continue; }
+      if (d > 0) in.pos++; else in.neg++;
+      const double rd = 1.0 / d;
+      if (own) {
+        const double aip = A[ti * LD + p], apj = A[p * LD + tj], aij = A[ti * LD + tj];
+        A[ti * LD + tj] = (ti == p) ? ((tj == p) ? -rd : apj * rd) : (tj == p) ? aip * rd : aij - aip * apj * rd;
+      }
+    } else {
+      const double a11 = A[k * LD + k], a21 = A[q * LD + k], a22 = A[q * LD + q];
+      const double det = a11 * a22 - a21 * a21;
+      done |= (1u << k) | (1u << q);
+      if (fabs(det) <= ZERO_PIVOT * ZERO_PIVOT) { in.zero += 2; zero |= (1u << k) | (1u << q); continue; }
+      if (det < 0) { in.pos++; in.neg++; }
+      else if (a11 + a22 > 0) in.pos += 2;
+      else in.neg += 2;
+      const double rdet = 1.0 / det;
+      const double p11 = a22 * rdet, p12 = -a21 * rdet, p22 = a11 * rdet;  // pivot-block inverse
+      if (own) {
+        const double aik = A[ti * LD + k], aiq = A[ti * LD + q], akj = A[k * LD + tj], aqj = A[q * LD + tj];
+        const double aij = A[ti * LD + tj];
+        const double xk = aik * p11 + aiq * p12, xq = aik * p12 + aiq * p22;  // row i times P^{-1}
+        const double yk = p11 * akj + p12 * aqj, yq = p12 * akj + p22 * aqj;  // P^{-1} times column j
+        const bool ip = ti == k || ti == q, jp = tj == k || tj == q;
+        double v;
+        if (ip && jp) v = -((ti == k) ? ((tj == k) ? p11 : p12) : ((tj == k) ? p12 : p22));
+        else if (ip) v = (ti == k) ? yk : yq;
+        else if (jp) v = (tj == k) ? xk : xq;
+        else v = aij - (xk * akj + xq * aqj);
+        A[ti * LD + tj] = v;
+      }
+    }
+    wsync();
+  }
+  wsync();
+  if (own) out[ti * LD + tj] = (((zero >> ti) | (zero >> tj)) & 1u) ? 0.0 : -A[ti * LD + tj];
+  wsync();
+  return in;
+}
+
 // ---------------------------------------------------------------------------
 // KKT entries
 // ---------------------------------------------------------------------------
@@ -1379,9 +1460,17 @@ __device__ __noinline__ Inertia chain_factor(const Agent a) {
         L.C[e] = v;
       }
       wsync();
-      const Inertia bi = bk_factor<NC, NC>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), lane);
-      in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
-      bk_inverse<NC, NC>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), LDSP(L.CW), LDSP(L.CY), LDSP(L.Dinv + j * NCC), lane);
+#ifndef MPCX_CHAIN_BK  // diagnostics: the LDL^T + explicit inverse pair instead of the sweep
+      if constexpr (NC * NC <= WAVE) {
+        const Inertia bi = bk_sweep<NC, NC>(LDSP(L.C), LDSP(L.Dinv + j * NCC), lane);
+        in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
+      } else
+#endif
+      {
+        const Inertia bi = bk_factor<NC, NC>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), lane);
+        in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
+        bk_inverse<NC, NC>(LDSP(L.C), LDSI(L.cperm), LDSI(L.cpiv), LDSP(L.CW), LDSP(L.CY), LDSP(L.Dinv + j * NCC), lane);
+      }
     }
   }
   wsync();

@@ -170,6 +170,34 @@ class IterationRecord:
     wall_time: Optional[float] = None  # seconds since the start of the round (:270, :400-402)
 
 
+class _BlockRecords(Sequence):
+    """Per-block residual histories of a coordinated round (``block_records[b]`` = block b's
+    list of :class:`IterationRecord`), kept as one array row per iteration and expanded
+    on access: building 1024 record objects per ADMM iteration cost about as much host
+    time as the iteration's batched solves."""
+
+    def __init__(self, n_blocks: int):
+        self.n = n_blocks
+        self._rows = []   # (prim, dual, rho, active, wall_time) per iteration
+
+    def append(self, prim, dual, rho, active, wall_time):
+        self._rows.append((np.array(prim, float), np.array(dual, float), np.array(rho, float),
+                           np.array(active, bool), float(wall_time)))
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, b):
+        if isinstance(b, slice):
+            return [self[i] for i in range(*b.indices(self.n))]
+        if b < 0:
+            b += self.n
+        if not 0 <= b < self.n:
+            raise IndexError(b)
+        return [IterationRecord(float(p[b]), float(d[b]), float(r[b]), wall_time=t)
+                for p, d, r, a, t in self._rows if a[b]]
+
+
 class ADMMFleet:
     """Device-resident ADMM over fleets of agents (one or more classes).
 
@@ -208,6 +236,7 @@ class ADMMFleet:
         self.rounds = 0
         self._masked = False
         self._part = None      # per-class participation masks (host) of the current round
+        self._blk_key = None   # last uploaded (penalties, freeze mask) of _set_blocks
         self.ROW_ON = None     # participation of the rows (device int32 [R + 1]) or None
 
     # ------------------------------------------------------------------ setup
@@ -390,8 +419,13 @@ class ADMMFleet:
 
     # ------------------------------------------------------------------ steps
     def _set_blocks(self, rho_b: np.ndarray, active_b: Optional[np.ndarray]):
-        """Upload the per-block penalties and (coordinated runs) the freeze masks."""
+        """Upload the per-block penalties and (coordinated runs) the freeze masks -- only when
+        they changed (most iterations change neither; each upload is a host round trip)."""
         t = self.torch
+        key = (np.asarray(rho_b, float).tobytes(), None if active_b is None else np.asarray(active_b, bool).tobytes())
+        if key == self._blk_key:
+            return
+        self._blk_key = key
         self.RHO_B.copy_(t.as_tensor(np.asarray(rho_b, float).reshape(-1, 1)))
         if self.G:
             self.RHO_G.copy_(t.as_tensor(np.asarray(rho_b, float)[self.block_of_group]))
@@ -487,6 +521,7 @@ class ADMMFleet:
         ``participating`` maps class names to a bool per agent (missing classes: all
         agents); None: every agent."""
         t = self.torch
+        self._blk_key = None
         if participating is None:
             self._part, self.ROW_ON = None, None
             return
@@ -545,7 +580,7 @@ class ADMMFleet:
         self._shift_all(shift)
         iters = np.full(nb, admm_iter_max, np.int64)
         conv_b = np.zeros(nb, bool)
-        block_records: List[List[IterationRecord]] = [[] for _ in range(nb)]
+        block_records = _BlockRecords(nb)
         records = []
         self._ok_count.zero_()
         it = 0
@@ -567,9 +602,7 @@ class ADMMFleet:
                 up = active & (prim > penalty_change_threshold * dual)
                 down = active & ~up & (dual > penalty_change_threshold * prim)
                 rho_b = np.where(up, rho_b * penalty_change_factor, np.where(down, rho_b / penalty_change_factor, rho_b))
-            for b in np.flatnonzero(active):
-                block_records[b].append(IterationRecord(float(prim[b]), float(dual[b]), float(rho_b[b]),
-                                                        wall_time=now_t))
+            block_records.append(prim, dual, rho_b, active, now_t)
             a = active
             records.append(IterationRecord(float(np.sqrt(tot[a, 0].clip(0).sum())),
                                            float(np.sqrt(tot[a, 1].clip(0).sum())),

@@ -285,3 +285,46 @@ def test_participation_and_registration_rounds_match_oracle():
                                        state["vars"][al].mult["ahu"], rtol=RTOL, atol=1e-8)
         np.testing.assert_allclose(fl.locals_of("room", "mDot")[1], state["vars"]["mDot2_coupling_b0"].local["room1"],
                                    rtol=RTOL, atol=1e-10)
+
+
+def _part_worker(rank, world, init_file, N, out_file):
+    """Two C2 blocks, one per rank (world 2) or both on one rank (world 1); the second
+    control step runs without room 1 of block 1 (not ready)."""
+    if world > 1:
+        dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        classes = bm.c2_fleet_classes(n_blocks=2 if world == 1 else 1, N=N, seed=7,
+                                      block_offset=0 if world == 1 else rank)
+        fl = ADMMFleet(classes, device="cpu", ops=_c2_ops(N), comm="default" if world > 1 else None)
+        kw = dict(admm_iter_max=1, use_relative_tolerances=False, primal_tol=1e-9, dual_tol=1e-9)
+        first = fl.run_coordinated(0.4, **kw)
+        if world == 1:
+            mask = [True] * 5 + [False] + [True] * 2     # rooms of block 1 are agents 4..7
+        else:
+            mask = [True, False, True, True] if rank == 1 else [True] * 4
+        fl.set_participation({"room": mask})
+        out = fl.run_coordinated(0.4, **kw)
+        traj = fl.trajectories()
+        np.savez(f"{out_file}.{rank}.npz",
+                 rec=np.array([[r.primal_residual, r.dual_residual] for r in first["records"] + out["records"]]),
+                 **{al: traj[al] for al in traj})
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_partitioned_participation_world2_matches_world1(tmp_path):
+    """Participation on a partitioned fleet (gloo, world_size 2): the masked rows drop out
+    of the rank-local moments and the active-row counts travel in the one all-reduce, so
+    two ranks with one block each give the one-rank result."""
+    N = 2
+    init, out = str(tmp_path / "init"), str(tmp_path / "out")
+    _part_worker(0, 1, init, N, out + "1")
+    one = dict(np.load(f"{out}1.0.npz"))
+    mp.spawn(_part_worker, args=(2, init, N, out + "2"), nprocs=2, join=True)
+    two = [dict(np.load(f"{out}2.{r}.npz")) for r in range(2)]
+    for r in two:
+        np.testing.assert_allclose(r["rec"], one["rec"], rtol=1e-9, atol=1e-12)
+        for al, v in r.items():
+            if al != "rec":
+                np.testing.assert_allclose(v, one[al], rtol=1e-10, atol=1e-12, err_msg=al)

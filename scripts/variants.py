@@ -28,6 +28,9 @@ VARIANTS = {
     "w2": (["-DMPCX_MIN_WAVES=2"], None),
     # 8 agents per CU: LDS share 160 KB / 8 and at most 256 VGPRs (2 waves per SIMD)
     "apc8_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=20224", "-DMPCX_MIN_WAVES=2"], None),
+    # 5 / 6 agents per CU with <= 256 registers: some SIMDs hold two waves
+    "apc5_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=32512", "-DMPCX_MIN_WAVES=2"], None),
+    "apc6_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=27050", "-DMPCX_MIN_WAVES=2"], None),
     "apc5": (["-DMPCX_LDS_TARGET_OVERRIDE=32512"], None),
     "apc8": (["-DMPCX_LDS_TARGET_OVERRIDE=20224"], None),
     "w1": (["-DMPCX_MIN_WAVES=1"], None),

@@ -540,23 +540,38 @@ class ADMMFleet:
         self._part = part
         self.ROW_ON = t.as_tensor(on, device=self.device)
 
-    def register(self, class_name: str, agent: int):
+    def register(self, class_name: str, agent: Optional[int]):
         """(Re-)registration of one agent (``ADMMCoordinator.register_agent``,
         `admm_coordinator.py:527-560`): its local trajectories restart from the configured
         initial value, its consensus multipliers from zero, and -- as the reference does --
         the multiplier of every exchange alias it joins is reset to zero; its backend starts
-        cold (the NLP guess of the class's initial inputs)."""
+        cold (the NLP guess of the class's initial inputs).
+
+        ``agent`` is the rank-local index of the agent, or None on the ranks that do not
+        hold it.  With several ranks the call is collective (every rank calls it): an
+        exchange alias whose participants span ranks keeps a replicated multiplier on each
+        of them, so every rank resets the aliases the agent joins."""
         t = self.torch
         ci = next(i for i, c in enumerate(self.classes) if c.name == class_name)
         c = self.classes[ci]
-        for si, s in enumerate(c.slots):
-            row = int(self.slot_rows[(ci, si)][agent])
-            self.X[row] = float(s.initial[agent])
-            self.LAMR[row] = 0.0
-            self.DIFF[row] = 0.0
-            if s.kind == EXCHANGE:
-                self.GMULT[int(self.slot_groups[(ci, si)][agent])] = 0.0
-        c.W[agent].copy_(t.as_tensor(c.w0[agent], device=self.device))
+        reset = []
+        if agent is not None:
+            for si, s in enumerate(c.slots):
+                row = int(self.slot_rows[(ci, si)][agent])
+                self.X[row] = float(s.initial[agent])
+                self.LAMR[row] = 0.0
+                self.DIFF[row] = 0.0
+                if s.kind == EXCHANGE:
+                    reset.append(s.aliases[agent])
+            c.W[agent].copy_(t.as_tensor(c.w0[agent], device=self.device))
+        if self.world > 1:
+            gathered = [None] * self.world
+            self.dist.all_gather_object(gathered, reset, group=self.group)
+            reset = [al for lst in gathered for al in lst]
+        gid = {al: i for i, al in enumerate(self.aliases)}
+        for al in dict.fromkeys(reset):
+            if al in gid:
+                self.GMULT[gid[al]] = 0.0
 
     def run_coordinated(self, penalty_factor: float, admm_iter_max: int = 20, primal_tol: float = 1e-3,
                         dual_tol: float = 1e-3, use_relative_tolerances: bool = True, abs_tol: float = 1e-3,
@@ -617,7 +632,11 @@ class ADMMFleet:
                 break
             self._set_blocks(rho_b, active)
         self._sync()
+        # the next round starts from full penalties and no freeze mask: drop the upload
+        # cache with the mask, or a round that converged at its first iteration (cache key
+        # still the start-of-round one) would leave the participation mask unapplied
         self._masked = False
+        self._blk_key = None
         wall = time.perf_counter() - t0
         if nb == 1:
             records = block_records[0]

@@ -389,6 +389,48 @@ def tz_cca(N=24, rho=1.0, zbar=294.15, lam=0.0, mDot_0=0.1, r_T_v=1.0, solver_op
     return be, cv
 
 
+def fixture_mpc(N=5, T0=298.16, disturbance=270.0, u_prev=0.02, solver_options=TIGHT, model=None,
+                backend="mi355x"):
+    """The reference's MPC module test (`tests/test_mpc.py:121-146`): backend ``casadi``
+    with default discretization options (collocation, Legendre d=3), time step 900 s,
+    horizon 5, on the test-suite model (`tests/fixtures/casadi_test_model.py`); the module
+    config declares state, control and disturbance only (parameters at model defaults)."""
+    be = create_optimization_backend({
+        "type": backend,
+        "model": model or {"type": "agentlib_mpc_amd.models.examples.FixtureModel"},
+        "discretization_options": {"prediction_horizon": N, "time_step": 900},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    be.setup_optimization(VariableReference(states=["state"], controls=["myctrl"], inputs=["disturbance"],
+                                            parameters=[], outputs=[]))
+    cv = {"state": V("state", T0), "myctrl": V("myctrl", u_prev, 0.0, 1.0),
+          "disturbance": V("disturbance", disturbance)}
+    return be, cv
+
+
+def fixture_admm(N=5, T0=298.16, disturbance=270.0, rho=10.0, zbar=298.16, lam=0.0, coupling=298.16,
+                 solver_options=TIGHT, model=None):
+    """The reference's ADMM module test (`tests/test_admm.py:24-58`): backend ``casadi_admm``
+    on the test-suite model with ``myout`` as consensus coupling (value 298.16 for the first
+    agent, 295 for the second), penalty factor 10 (`modules/dmpc/admm/admm.py:72-77`)."""
+    be = create_optimization_backend({
+        "type": "mi355x_admm",
+        "model": model or {"type": "agentlib_mpc_amd.models.examples.FixtureModel"},
+        "discretization_options": {"prediction_horizon": N, "time_step": 900},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    c = adt.CouplingEntry("myout")
+    be.setup_optimization(adt.VariableReference(
+        states=["state"], controls=["myctrl"], inputs=["disturbance"], parameters=[], outputs=[],
+        couplings=[c]))
+    n = len(be.coupling_grid)
+    cv = {"state": V("state", T0), "myctrl": V("myctrl", 0.02, 0.0, 1.0),
+          "disturbance": V("disturbance", disturbance), "myout": V("myout", coupling),
+          c.mean: V(c.mean, _vals(zbar, n)), c.multiplier: V(c.multiplier, _vals(lam, n)),
+          "penalty_factor": V("penalty_factor", rho)}
+    return be, cv
+
+
 BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -398,6 +440,8 @@ BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
     "room_nn": room_nn,
     "tz_ahu": tz_ahu,
     "tz_cca": tz_cca,
+    "fixture_mpc": fixture_mpc,
+    "fixture_admm": fixture_admm,
 }
 
 

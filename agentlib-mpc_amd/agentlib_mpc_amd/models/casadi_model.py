@@ -325,6 +325,11 @@ class CasadiModel:
 
     def _resolve_config_class(self):
         for klass in type(self).__mro__:
+            # a config class assigned instead of annotated (``config = MyConfig``, e.g.
+            # `tests/fixtures/casadi_test_model.py:62-63`) declares the variables as well
+            c = klass.__dict__.get("config")
+            if isinstance(c, type) and issubclass(c, CasadiModelConfig) and c is not CasadiModelConfig:
+                return c
             ann = klass.__dict__.get("__annotations__", {})
             if "config" in ann:
                 c = ann["config"]

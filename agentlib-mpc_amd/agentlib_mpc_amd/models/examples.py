@@ -416,3 +416,25 @@ class RNGRoomMHE(RNGRoom):
     (the middle of the feasible interval) that two interior-point solvers agree on."""
 
     config: RNGRoomMHEConfig
+
+
+class FixtureModelConfig(CasadiModelConfig):
+    """The reference test-suite model (`tests/fixtures/casadi_test_model.py:13-34`)."""
+
+    parameters: List[CasadiParameter] = [_par("par", 12, unit="kg"), _par("par2", 10, unit="kg")]
+    states: List[CasadiState] = [CasadiState(name="state", value=290, unit="K")]
+    inputs: List[CasadiInput] = [_inp("myctrl", 100, unit="W"), _inp("disturbance", 280, unit="K")]
+    outputs: List[CasadiOutput] = [CasadiOutput(name="myout", value=100)]
+
+
+class FixtureModel(CasadiModel):
+    """`tests/fixtures/casadi_test_model.py:37-47`: one unstable state driven by a control
+    and a disturbance, its value as output, quadratic tracking cost (deprecated plain
+    objective return)."""
+
+    config: FixtureModelConfig
+
+    def setup_system(self):
+        self.state.ode = self.myctrl + self.par * (self.state - self.disturbance) - self.par2
+        self.myout.alg = self.state
+        return (self.state - 290) ** 2

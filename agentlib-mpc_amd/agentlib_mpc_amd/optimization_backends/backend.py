@@ -91,17 +91,22 @@ class BackendConfig(pydantic.BaseModel):
 
 def custom_injection(config):
     """Resolve ``{"file": ..., "class_name": ...}`` / class / dotted path to a class
-    (agentlib ``custom_injection`` semantics)."""
+    (agentlib ``custom_injection`` semantics).
+
+    Model files import the reference's model API.  Without the reference installed those
+    imports are aliased globally to this package; with it installed, the file is executed
+    privately with an import map that resolves them here (:mod:`agentlib_mpc_amd.compat`)."""
     if isinstance(config, type):
         return config
     if isinstance(config, str):
         mod, _, cls = config.rpartition(".")
         return getattr(importlib.import_module(mod), cls)
     if isinstance(config, dict):
-        # model files written against the reference import agentlib_mpc.models...
-        from agentlib_mpc_amd.compat import install_reference_aliases
+        from agentlib_mpc_amd import compat
 
-        install_reference_aliases()
+        if not compat.install_reference_aliases():
+            # the reference is installed: its model API must not be what the file binds
+            return getattr(compat.load_model_file(config["file"]), config["class_name"])
         file = pathlib.Path(config["file"]).resolve()
         name = f"_mpcx_injected_{abs(hash(str(file)))}"
         if name in sys.modules:
@@ -149,6 +154,12 @@ class OptimizationBackend(_RefOptimizationBackend if _RefOptimizationBackend is 
         model = dict(model)
         _type = model.pop("type")
         cls = custom_injection(_type)
+        from agentlib_mpc_amd import compat
+
+        if compat.is_reference_model_class(cls):
+            # a class of the installed reference (given as a class, a dotted path or loaded
+            # elsewhere): read it again against this package's model API so it traces
+            cls = compat.retrace_model_class(cls)
         instance = cls(**model)
         # `backend.py:94-100`: the reference checks the model against _supported_models
         if self._supported_models and not any(isinstance(instance, m) for m in self._supported_models.values()):

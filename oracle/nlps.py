@@ -13,6 +13,9 @@ independent of the product's tracer and transcriber:
 * ``exchange_room`` / ``exchange_supply`` — backend ``casadi_admm`` multiple
   shooting with Euler (`casadi_/admm.py:198-310`) on
   `examples/exchange_admm/models/{room,rlt}_model.py` (C4).
+* ``fixture_mpc`` — backend ``casadi`` collocation (defaults: Legendre d=3) on the
+  reference test-suite model `tests/fixtures/casadi_test_model.py:13-47` with the MPC
+  module config of `tests/test_mpc.py:121-146`.
 * ``room_nn`` — backend ``casadi_admm_nn`` NARX multiple shooting
   (`casadi_/casadi_admm_ml.py:247-397`) on
   `examples/three_zone_datadriven_admm/models/Room_model.py` with two ANNs (C5).
@@ -996,4 +999,73 @@ def rng_room_mpc_inputs(prob, N=15, d=2, T0=25.0, Tw0=27.0, u_prev=0.02, theta=5
             lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
     lbw[0] = ubw[0] = w0[0] = T0
     lbw[1] = ubw[1] = w0[1] = Tw0
+    return p, lbw, ubw, w0
+
+
+# ---------------------------------------------------------------------------
+# reference test-suite model (tests/fixtures/casadi_test_model.py), backend "casadi"
+# ---------------------------------------------------------------------------
+
+def fixture_mpc(N=5, ts=900.0, d=3) -> OracleProblem:
+    """w = [x_0, {u_k, {x_kj, y_kj}_j, x_{k+1}}_k] (`casadi_/full.py:36-98`), y = myout;
+    g per interval: continuity, then per point collocation and the output equation
+    y - x = 0 (`casadi_model.py:458-467`); p = [x0, u_prev, par, par2, {disturbance_kj}].
+    ode = u + par (x - dist) - par2, cost (x - 290)^2 at the points (`casadi_test_model.py:37-47`)."""
+    tau, B, C, D = collocation(d)
+    nb = 1 + 2 * d + 1
+    n = 1 + N * nb
+    m = N * (1 + 2 * d)
+    npg = 4
+    names = ["state@0"]
+    for k in range(N):
+        names.append(f"myctrl@{k}")
+        for j in range(d):
+            names += [f"state@{k},{j}", f"myout@{k},{j}"]
+        names.append(f"state@{k + 1}")
+
+    def f(w, p):
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = 1 + k * nb
+            for j in range(d):
+                tot = tot + B[j + 1] * (w[o + 1 + 2 * j] - 290.0) ** 2 * ts
+        return tot
+
+    def g(w, p):
+        par, par2 = p[2], p[3]
+        out = []
+        xk = w[0]
+        for k in range(N):
+            o = 1 + k * nb
+            u = w[o]
+            xj = [w[o + 1 + 2 * j] for j in range(d)]
+            out.append(w[o + nb - 1] - (D[0] * xk + sum(D[j + 1] * xj[j] for j in range(d))))
+            for j in range(d):
+                dist = p[npg + k * d + j]
+                ode = u + par * (xj[j] - dist) - par2
+                xp = C[0, j + 1] * xk + sum(C[r + 1, j + 1] * xj[r] for r in range(d))
+                out.append(ts * ode - xp)
+                out.append(w[o + 2 + 2 * j] - xj[j])
+            xk = w[o + nb - 1]
+        return torch.stack(out)
+
+    return OracleProblem("fixture_mpc", n, m, npg + N * d, f, g, lambda p: np.zeros(m), lambda p: np.zeros(m),
+                         names)
+
+
+def fixture_mpc_inputs(prob: OracleProblem, N=5, d=3, T0=298.16, dist=270.0, u_prev=0.02, par=12.0, par2=10.0,
+                       u_lb=0.0, u_ub=1.0):
+    """Cold start (`core/discretization.py:212-245`): states at their current value, the
+    control at the middle of its bounds, the unbounded output at 0."""
+    p = np.array([T0, u_prev, par, par2] + [dist] * (N * d), float)
+    lbw = np.full(prob.n, -np.inf)
+    ubw = np.full(prob.n, np.inf)
+    w0 = np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        base = name.split("@")[0]
+        if base == "state":
+            w0[i] = T0
+        elif base == "myctrl":
+            lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
+    lbw[0] = ubw[0] = T0
     return p, lbw, ubw, w0

@@ -159,6 +159,17 @@ def rng_room_mpc(**kw) -> Case:
     return Case(be, cv, prob, nlps.rng_room_mpc_inputs(prob, N=kw.get("N", 15), **o))
 
 
+def fixture_mpc(**kw) -> Case:
+    """The reference test-suite model under the MPC module test's config (`tests/test_mpc.py`)."""
+    be, cv = bm.fixture_mpc(**kw)
+    N = kw.get("N", 5)
+    prob = nlps.fixture_mpc(N=N)
+    o = {k: kw[k] for k in ("T0", "u_prev") if k in kw}
+    if "disturbance" in kw:
+        o["dist"] = kw["disturbance"]
+    return Case(be, cv, prob, nlps.fixture_mpc_inputs(prob, N=N, **o))
+
+
 CASES: Dict[str, Callable[..., Case]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -174,6 +185,7 @@ CASES: Dict[str, Callable[..., Case]] = {
     "one_room_switch": one_room_switch,
     "mhe_room": mhe_room,
     "rng_room_mpc": rng_room_mpc,
+    "fixture_mpc": fixture_mpc,
     # estimating mDot per interval needs the wall temperature measured too (else mDot
     # and the unmeasured wall state trade off and the minimiser is not unique)
     "mhe_room_u": lambda **kw: mhe_room(estimate="mDot", **{"w_T_wall": 1.0, **kw}),

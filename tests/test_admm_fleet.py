@@ -328,3 +328,87 @@ def test_partitioned_participation_world2_matches_world1(tmp_path):
         for al, v in r.items():
             if al != "rec":
                 np.testing.assert_allclose(v, one[al], rtol=1e-10, atol=1e-12, err_msg=al)
+
+
+def test_masked_round_converging_at_first_iteration_keeps_the_mask():
+    """A participation mask stays applied across rounds even when a round stops at its
+    first iteration (the block-upload cache is dropped with the mask at the end of every
+    round): the agent that is not ready is never solved, its warm start is untouched and it
+    does not count as a converged solve."""
+    N = 2
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N), device="cpu", ops=_c2_ops(N))
+    fl.set_participation({"room": [True, False, True, True]})
+    room = fl.classes[0]
+    w1 = room.W[1].clone()
+    kw = dict(admm_iter_max=5, use_relative_tolerances=False, primal_tol=1e9, dual_tol=1e9)
+    for _ in range(2):
+        out = fl.run_coordinated(0.4, **kw)
+        assert out["iterations"] == 1 and out["converged"]
+        assert out["converged_solves"] == 4          # rooms 0, 2, 3 and the air handler
+        assert bool((room.W[1] == w1).all())
+
+
+def _reg_worker(rank, world, init_file, N, out_file):
+    """C4 exchange fleet, rooms split over the ranks (rank 0 also holds the supply unit);
+    room 3 re-registers between two coordinated rounds.  With two ranks the exchange alias
+    spans both, so every rank must reset its copy of the alias's multiplier."""
+    if world > 1:
+        dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        from agentlib_mpc_amd.admm.fleet import FleetClass
+
+        room, supply = bm.c4_fleet_classes(n_rooms=4, n_supply=1, N=N)
+        lo, hi = (2 * rank, 2 * rank + 2) if world == 2 else (0, 4)
+        sl = lambda a: a[lo:hi]  # noqa: E731
+        mine = [FleetClass("room", room.backend, (sl(room.p0), sl(room.lbw), sl(room.ubw), sl(room.w0)),
+                           aliases={"mDot_out": "mDot_coupling"}, initial={"mDot_out": 0.02})]
+        if rank == 0:
+            mine.append(supply)
+        fl = ADMMFleet(mine, device="cpu", ops=_c4_ops(N), comm="default" if world > 1 else None)
+        kw = dict(admm_iter_max=2, use_relative_tolerances=False, primal_tol=1e-12, dual_tol=1e-12)
+        first = fl.run_coordinated(1e4, **kw)
+        if world == 1:
+            fl.register("room", 3)
+        else:
+            fl.register("room", 1 if rank == 1 else None)
+        gm_after_reg = fl.GMULT[fl.aliases.index("mDot_coupling")].numpy().copy()
+        out = fl.run_coordinated(1e4, **kw)
+        np.savez(f"{out_file}.{rank}.npz", gm_reg=gm_after_reg,
+                 gm=fl.GMULT[fl.aliases.index("mDot_coupling")].numpy(),
+                 mean=fl.trajectories()["mDot_coupling"],
+                 rec=np.array([[r.primal_residual, r.dual_residual] for r in first["records"] + out["records"]]))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_partitioned_registration_world2_matches_world1(tmp_path):
+    """Registration on a partitioned fleet: the exchange multiplier of a
+    rank-spanning alias is reset on every rank, so both ranks keep the one-rank values."""
+    N = 3
+    init, out = str(tmp_path / "init"), str(tmp_path / "out")
+    _reg_worker(0, 1, init, N, out + "1")
+    one = dict(np.load(f"{out}1.0.npz"))
+    assert not one["gm_reg"].any()
+    mp.spawn(_reg_worker, args=(2, init, N, out + "2"), nprocs=2, join=True)
+    two = [dict(np.load(f"{out}2.{r}.npz")) for r in range(2)]
+    for r in two:
+        assert not r["gm_reg"].any()
+        np.testing.assert_allclose(r["rec"], one["rec"], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(r["gm"], one["gm"], rtol=1e-10, atol=1e-9)
+        np.testing.assert_allclose(r["mean"], one["mean"], rtol=1e-10, atol=1e-12)
+
+
+def test_consensus_multipliers_of_an_alias_sum_to_zero():
+    """`tests/test_admm.py:147-161` property on the coordinated C2 fleet: every consensus
+    alias's multipliers sum to zero over its participants (each update adds
+    rho * (x_i - mean), whose sum over the participants vanishes)."""
+    N = 2
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N), device="cpu", ops=_c2_ops(N))
+    fl.run_coordinated(0.4, admm_iter_max=3, use_relative_tolerances=False, primal_tol=1e-12, dual_tol=1e-12)
+    lam = fl.LAMR.numpy()
+    assert np.abs(lam).max() > 0
+    for g in range(fl.G):
+        rows = lam[fl.gstart[g]:fl.gstart[g + 1]]
+        assert len(rows) == 2
+        np.testing.assert_allclose(rows.sum(0), 0.0, atol=1e-12 * np.abs(lam).max())

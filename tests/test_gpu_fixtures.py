@@ -1,0 +1,63 @@
+"""GPU runs of the reference's own module tests on its test-suite model
+(`tests/fixtures/casadi_test_model.py`, restated as ``models/examples.FixtureModel``;
+tests/test_reference_fixtures.py checks the restatement against the file).
+
+* `tests/test_mpc.py:151-162`: one MPC solve through the plugin API (backend ``casadi``,
+  default discretization, horizon 5, time step 900) returns the control on its 5 grid
+  points -- here at the reference's own solver defaults and, at tight tolerance, equal to
+  the oracle's solution (objective rel 1e-6, trajectories rel 1e-5).
+* `tests/test_admm.py:60-161`: two ADMM agents coupled through ``myout`` (initial values
+  298.16 and 295, penalty 10, 20 iterations): the multipliers of the two agents sum to
+  zero (the reference allows 10 % for an off-by-one of its threaded loop; the batched
+  fleet has none, so the sum is zero to rounding) and are not zero.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from agentlib_mpc_amd import benchmarks as bm
+from oracle import ipm
+from tests import configs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_mpc_solve_returns_horizon_controls_at_reference_defaults():
+    be, cv = bm.fixture_mpc(solver_options=bm.REFERENCE)
+    r = be.solve(0.0, cv)
+    assert r.stats["success"], r.stats
+    assert len(r["myctrl"]) == 5
+
+
+def test_mpc_solve_matches_oracle():
+    case = configs.fixture_mpc()
+    p, lbw, ubw, w0 = case.oracle_inputs
+    ref = ipm.solve(case.oracle.functions(p), w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p),
+                    ipm.IPMOptions(tol=1e-10, max_iter=500, acceptable_iter=0))
+    assert ref.success, ref.status
+    r = case.backend.solve(0.0, case.current_vars)
+    assert r.stats["success"], r.stats
+    np.testing.assert_allclose(r.stats["obj"], ref.f, rtol=1e-6)
+    want = np.array([ref.x[i] for i, n in enumerate(case.oracle.w_names) if n.split("@")[0] == "myctrl"])
+    np.testing.assert_allclose(np.asarray(r["myctrl"], float).ravel(), want, rtol=1e-5, atol=1e-7)
+
+
+def test_admm_multipliers_of_two_agents_sum_to_zero():
+    from agentlib_mpc_amd.admm.fleet import ADMMFleet, FleetClass
+
+    be, cv = bm.fixture_admm()
+    cls = FleetClass("agent", be, bm._class_inputs(be, cv, {}, 2), initial={"myout": [298.16, 295.0]})
+    fleet = ADMMFleet([cls])
+    out = fleet.run_local(penalty_factor=10.0, max_iterations=20)
+    assert out["converged_solves"] == 2 * 20
+    lam = fleet.multipliers_of("agent", "myout")
+    assert lam.shape == (2, len(be.coupling_grid))
+    assert lam[0, 0] != 0.0
+    np.testing.assert_allclose(lam[0] + lam[1], 0.0, atol=1e-10 * np.abs(lam).max())

@@ -77,6 +77,9 @@ def _cuda():
     ("tz_ahu", {"zbar": 295.0, "lam": 0.3}),
     ("tz_cca", {}),
     ("tz_cca", {"zbar": 293.0, "lam": -0.2}),
+    # the reference test-suite model under its MPC-module test config (tests/test_mpc.py)
+    ("fixture_mpc", {}),
+    ("fixture_mpc", {"T0": 285.0, "disturbance": 300.0}),
 ])
 def test_gpu_matches_oracle(name, kw):
     case = configs.CASES[name](**kw)
@@ -119,6 +122,7 @@ REFERENCE_OPTS = dict(tol=1e-4, max_iter=100, acceptable_tol=0.1, acceptable_ite
     ("room_nn", {}),                                   # C5 zone   (acceptable stop)
     ("tz_ahu", {}),                                    # C5 AHU, N=24
     ("tz_cca", {}),                                    # C5 CCA, N=24
+    ("fixture_mpc", {}),                               # reference test-suite model
 ])
 def test_gpu_matches_oracle_at_reference_defaults(name, kw):
     """Drop-in configs left at the reference's default solver options: the kernel and the

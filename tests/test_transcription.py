@@ -29,6 +29,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "mhe_room": (3 + 15 * 14, 15 * 14, 10 + 15 * 9),  # MHE: x_0, theta free; 6 vars per point
     "mhe_room_u": (2 + 15 * 15, 15 * 14, 11 + 15 * 8),  # MHE estimating mDot per interval
     "rng_room_mpc": (2 + 15 * 15, 15 * 14, 12 + 15 * 8),  # two-state zone + wall MPC (nx > nu)
+    "fixture_mpc": (1 + 5 * (1 + 3 * 2 + 1), 5 * (1 + 3 * 2), 4 + 5 * 3),  # reference test-suite model
 }
 
 

@@ -49,6 +49,7 @@ CONSENSUS = "consensus"
 EXCHANGE = "exchange"
 NMOM = 5
 _STATUS_WORD = 13  # int32 index of mpcx_stats.status (6 doubles + iter_count)
+_FALLBACK_WORD = 15  # int32 index of mpcx_stats.n_linesearch_fallbacks
 
 
 @dataclasses.dataclass
@@ -293,8 +294,12 @@ class ADMMFleet:
                 self.slot_groups[(ci, si)] = np.array([gid[al] for al in s.aliases], np.int32)
 
     def _build_blocks(self, parts, order, gid):
-        """Connected components of the agent-alias participation graph (over all ranks):
-        one block per reference coordinator."""
+        """Connected components of the agent-alias participation graph: one block per
+        reference coordinator.  Blocks that contain a global alias (participants on several
+        ranks) are merged over the ranks and numbered first, identically on every rank
+        (``n_global_blocks``); the rank-local blocks follow in local order.  Only the global
+        blocks' residual totals travel in the all-reduce, so its length does not grow with
+        the number of rank-local blocks."""
         parent = {al: al for al in order}
 
         def find(a):
@@ -316,34 +321,61 @@ class ADMMFleet:
             seen.extend(als)
             for al in als[1:]:
                 union(als[0], al)
+        gset = set(order[:self.n_global])
+        comps: Dict[str, List[str]] = {}
+        for al in list(dict.fromkeys(seen)) + [al for al in order if al not in set(seen)]:
+            comps.setdefault(find(al), []).append(al)
+        # global blocks: merge the components that share global aliases over the ranks
+        gparent = {al: al for al in gset}
+
+        def gfind(a):
+            while gparent[a] != a:
+                gparent[a] = gparent[gparent[a]]
+                a = gparent[a]
+            return a
+
+        def gunion(a, b):
+            ra, rb = gfind(a), gfind(b)
+            if ra != rb:
+                gparent[max(ra, rb)] = min(ra, rb)
+
+        local_links = [sorted(al for al in c if al in gset) for c in comps.values()]
+        local_links = [ln for ln in local_links if ln]
+        links = local_links
         if self.world > 1:
-            comps: Dict[str, List[str]] = {}
-            for al in seen:
-                comps.setdefault(find(al), []).append(al)
             gathered = [None] * self.world
-            self.dist.all_gather_object(gathered, list(comps.values()), group=self.group)
-            seen = []
-            for lst in gathered:  # rank order: the same block numbering on every rank
-                for comp in lst:
-                    seen.extend(comp)
-                    for al in comp:
-                        parent.setdefault(al, al)
-                    for al in comp[1:]:
-                        union(comp[0], al)
-        roots = list(dict.fromkeys(find(al) for al in seen + list(order)))
-        bid = {r: i for i, r in enumerate(roots)}
-        self._block_id = {al: bid[find(al)] for al in parent}
-        self.n_blocks = max(len(roots), 1)
-        self.block_of_group = np.array([bid[find(al)] for al in order], np.int32)
+            self.dist.all_gather_object(gathered, local_links, group=self.group)
+            links = [ln for lst in gathered for ln in lst]
+        for ln in links:
+            for al in ln:
+                gparent.setdefault(al, al)
+            for al in ln[1:]:
+                gunion(ln[0], al)
+        groots = sorted({gfind(al) for al in gparent})
+        gbid = {r: i for i, r in enumerate(groots)}
+        self.n_global_blocks = len(groots)
+        bid_of_root: Dict[str, int] = {}
+        nxt = self.n_global_blocks
+        for root, c in comps.items():
+            gl = [al for al in c if al in gset]
+            if gl:
+                bid_of_root[root] = gbid[gfind(gl[0])]
+            else:
+                bid_of_root[root] = nxt
+                nxt += 1
+        self._block_id = {al: bid_of_root[find(al)] for al in parent}
+        self.n_blocks = max(nxt, 1)
+        self.block_is_global = np.arange(self.n_blocks) < self.n_global_blocks
+        self.block_of_group = np.array([self._block_id[al] for al in order], np.int32)
         self.block_aliases = [[] for _ in range(self.n_blocks)]
         for al in sorted(parent):
-            self.block_aliases[bid[find(al)]].append(al)
+            self.block_aliases[self._block_id[al]].append(al)
         self.agent_blocks = {}
         for ci, c in enumerate(self.classes):
             blk = np.zeros(c.n, np.int32)
             for (cj, a), als in by_agent.items():
                 if cj == ci:
-                    blk[a] = bid[find(als[0])]
+                    blk[a] = self._block_id[als[0]]
             self.agent_blocks[ci] = blk
 
     def block_index(self, alias: str) -> int:
@@ -366,7 +398,8 @@ class ADMMFleet:
         nb = self.n_blocks
         self.MOM = t.zeros(self.ops.moments_size(max(G, 1), nb, T), dtype=f64, device=dev)
         self.totals_off = self.n_global * self.S
-        self.reduce_len = self.n_global * self.S + ADMM_TOTALS * nb
+        # all-reduce range: global groups' moments + the totals of the blocks spanning ranks
+        self.reduce_len = self.n_global * self.S + ADMM_TOTALS * self.n_global_blocks
         # per-block coordinator state on the device: penalty, group freeze mask
         self.BLOCK_G = t.as_tensor(self.block_of_group if G else np.zeros(1, np.int32), dtype=i32, device=dev)
         self.RHO_B = t.zeros((nb, 1), dtype=f64, device=dev)
@@ -400,6 +433,7 @@ class ADMMFleet:
                 x0[self.slot_rows[(ci, si)]] = s.initial[:, None]
         self.X[:R].copy_(t.as_tensor(x0, device=dev))
         self._ok_count = t.zeros(1, dtype=t.int64, device=dev)
+        self._fb_count = t.zeros(1, dtype=t.int64, device=dev)  # line-search fallbacks of the solves
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
@@ -460,16 +494,22 @@ class ADMMFleet:
                 d = c.dev_slots[si]
                 # agents not participating keep their local (their rows map to the scratch row)
                 ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
-            st = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)[:, _STATUS_WORD]
+            words = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)
+            st = words[:, _STATUS_WORD]
             ok = (st == 0) | (st == 1)
+            fb = words[:, _FALLBACK_WORD]
             if self._masked:
                 ok &= c.ACTIVE != 0
+                fb = fb * (c.ACTIVE != 0)
             self._ok_count += ok.sum()
+            self._fb_count += fb.sum()
 
-    def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False):
+    def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False, reduce: bool = True):
         """Mean (+ exchange diffs) from the current locals; with ``apply_multipliers``
         also the multiplier update.  Returns the residual totals [n_blocks][8] (device).
-        ``per_block``: per-group penalties and freeze masks of the coordinated run."""
+        ``per_block``: per-group penalties and freeze masks of the coordinated run.
+        ``reduce``: take part in the all-reduce (every rank must pass the same value; False
+        only once every block spanning ranks is frozen)."""
         ops, T, G, nb = self.ops, self.T, self.G, self.n_blocks
         if G == 0:
             return None
@@ -484,7 +524,7 @@ class ADMMFleet:
         gm = self.GMULT if exch is not None else None
         ops.finalize(self.n_global, G, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
                      self.MEAN, self.DMEAN, totals)
-        if self.world > 1:
+        if self.world > 1 and reduce and self.reduce_len:
             self.dist.all_reduce(self.MOM[:self.reduce_len], group=self.group)
         ops.finalize(0, self.n_global, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
                      self.MEAN, self.DMEAN, totals)
@@ -598,10 +638,16 @@ class ADMMFleet:
         block_records = _BlockRecords(nb)
         records = []
         self._ok_count.zero_()
+        self._fb_count.zero_()
         it = 0
+        gblk = self.block_is_global
         for it in range(1, admm_iter_max + 1):
             self._solve_all(float(penalty_factor))
-            tot = self._update_means(float(penalty_factor), apply_multipliers=True, per_block=True).cpu().numpy()
+            # a block spanning ranks stops on the same (reduced) totals everywhere, so this
+            # decision agrees over the ranks; rank-local blocks need no collective at all
+            reduce = bool(active[gblk].any())
+            tot = self._update_means(float(penalty_factor), apply_multipliers=True, per_block=True,
+                                     reduce=reduce).cpu().numpy()
             now_t = time.perf_counter() - t0
             prim = np.sqrt(np.maximum(tot[:, 0], 0.0))
             dual = np.sqrt(np.maximum(tot[:, 1], 0.0))
@@ -644,7 +690,8 @@ class ADMMFleet:
         self.rounds += 1
         return {"iterations": it, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
                 "converged_solves": int(self._ok_count.item()), "block_iterations": iters,
-                "block_converged": conv_b, "block_records": block_records}
+                "block_converged": conv_b, "block_records": block_records, "block_is_global": gblk.copy(),
+                "linesearch_fallbacks": int(self._fb_count.item())}
 
     def save_stats(self, path, start_time: float, records: Sequence[IterationRecord], first_iteration: int = 0):
         """Append one round's residual history to the coordinator's ``solve_stats_file``
@@ -679,6 +726,7 @@ class ADMMFleet:
                                 device=self.device)
         t0 = time.perf_counter()
         self._ok_count.zero_()
+        self._fb_count.zero_()
         for it in range(max_iterations):
             self._solve_all(rho)
             tot = self._update_means(rho, apply_multipliers=True)
@@ -691,7 +739,8 @@ class ADMMFleet:
         self.history.extend(records)
         self.rounds += 1
         return {"iterations": max_iterations, "converged": None, "records": records, "wall_s": wall,
-                "converged_solves": int(self._ok_count.item())}
+                "converged_solves": int(self._ok_count.item()),
+                "linesearch_fallbacks": int(self._fb_count.item())}
 
     # ------------------------------------------------------------------ outputs
     def solutions(self, class_name: str) -> np.ndarray:

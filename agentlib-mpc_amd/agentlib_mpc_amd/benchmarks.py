@@ -521,10 +521,20 @@ def c2_fleet_classes(n_blocks=1, N=10, rho=0.4, seed=None, block_offset=0, solve
     return [rooms, ahu]
 
 
-def c4_fleet_classes(n_rooms=4, n_supply=1, N=10, rho=1e4, seed=None, solver_options=TIGHT):
+def split_range(total: int, rank: int, world: int):
+    """[lo, hi) of rank's contiguous share of ``total`` items (the first total % world ranks
+    hold one more)."""
+    base, extra = divmod(int(total), int(world))
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def c4_fleet_classes(n_rooms=4, n_supply=1, N=10, rho=1e4, seed=None, solver_options=TIGHT, rank=0, world=1):
     """Exchange fleet of `examples/exchange_admm` (one alias ``mDot_coupling``):
     rooms (first four = the example's values, further d~U(10,150), T0~U(296,303))
-    and supply units (penalty 0.1)."""
+    and supply units (penalty 0.1).  With ``world`` > 1 the fleet of ``n_rooms`` rooms and
+    ``n_supply`` supply units is split over the ranks and this returns ``rank``'s share
+    (the same agents as the one-rank fleet, for strong scaling)."""
     from agentlib_mpc_amd.admm.fleet import FleetClass
 
     rng = np.random.default_rng(seed)
@@ -534,6 +544,11 @@ def c4_fleet_classes(n_rooms=4, n_supply=1, N=10, rho=1e4, seed=None, solver_opt
             d.append(C4_ROOMS[i][0]); T0.append(C4_ROOMS[i][1])
         else:
             d.append(rng.uniform(10.0, 150.0)); T0.append(rng.uniform(296.0, 303.0))
+    if world > 1:
+        lo, hi = split_range(n_rooms, rank, world)
+        d, T0, n_rooms = d[lo:hi], T0[lo:hi], hi - lo
+        lo, hi = split_range(n_supply, rank, world)
+        n_supply = hi - lo
     classes = []
     if n_rooms:
         be_r, cv_r = exchange_room(N=N, rho=rho, solver_options=solver_options)

@@ -142,9 +142,10 @@ def pmc_traffic(code_object: str, n_agents: int):
 
 def admm_bench(args, world, rank, dev):
     """C4 (BASELINE.json configs[3]): decentralised exchange ADMM (LocalADMM semantics,
-    examples/exchange_admm: MS-Euler, N=10, ts=120, rho=1e4, 15 iterations) on
-    ``--admm-agents`` agents per GPU (rooms:supply = 4:1) sharing ONE exchange alias
-    across all ranks: one RCCL all-reduce per ADMM iteration."""
+    examples/exchange_admm: MS-Euler, N=10, ts=120, rho=1e4, 15 iterations) on a fleet of
+    ``--admm-agents`` agents IN TOTAL (rooms:supply = 4:1) split over the GPUs (strong
+    scaling: the config is a fixed 16384-agent fleet), all on ONE exchange alias spanning
+    the ranks: one RCCL all-reduce per ADMM iteration."""
     import torch
     import torch.distributed as dist
     from agentlib_mpc_amd import benchmarks as bm
@@ -153,8 +154,9 @@ def admm_bench(args, world, rank, dev):
     n = args.admm_agents
     n_sup = n // 5
     opts, _ = solver_settings(args)
-    classes = bm.c4_fleet_classes(n_rooms=n - n_sup, n_supply=n_sup, N=10, seed=20261015 + 4 + rank,
-                                  solver_options=opts)
+    classes = bm.c4_fleet_classes(n_rooms=n - n_sup, n_supply=n_sup, N=10, seed=20261015 + 4,
+                                  solver_options=opts, rank=rank, world=world)
+    n_local = sum(c.n for c in classes)
     fleet = ADMMFleet(classes, device=dev, comm="default" if world > 1 else None)
     for c in classes:
         c.native.reserve(c.n)
@@ -186,12 +188,14 @@ def admm_bench(args, world, rank, dev):
         "cpu_baseline": cpu,
         "workload": "C4: exchange ADMM (LocalADMM), examples/exchange_admm rooms+supply 4:1, MS-Euler "
                     "N=10 ts=120 rho=1e4, one exchange alias spanning all GPUs",
-        "agents_per_gpu": n, "agents_total": n * world, "admm_iterations": args.admm_iters,
+        "scaling": "strong", "agents_total": n, "agents_rank0": n_local, "admm_iterations": args.admm_iters,
         "admm_iters_per_s": args.admm_iters / wall,
         "agent_solves_per_s": ok / wall,
-        "converged_fraction": ok / (n * world * args.admm_iters),
+        "converged_fraction": ok / (n * args.admm_iters),
         "ms_per_admm_iteration": wall / args.admm_iters * 1e3,
         "allreduce_per_iteration": 1 if world > 1 else 0,
+        "allreduce_doubles": fleet.reduce_len if world > 1 else 0,
+        **_fallbacks(out["linesearch_fallbacks"], world, dev),
     }
 
 
@@ -222,6 +226,7 @@ def nn_bench(args, world, rank, dev):
         "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
         "statuses": sorted({int(s["status"]) for s in stats}),
         "mean_factorizations": float(np.mean([s["n_factorizations"] for s in stats])),
+        "linesearch_fallbacks_last_step": int(sum(s["n_linesearch_fallbacks"] for s in stats)),
         "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
                                       max(1, np.sum([s["n_factorizations"] for s in stats]))),
         "kernel_ms": kernel_ms,
@@ -261,6 +266,36 @@ def _timed_batch(be, prob, p, lbw, ubw, w0, n, args, dev):
     return stats_to_dicts(st.cpu().numpy().tobytes()), wall, ev0.elapsed_time(ev1) / args.steps
 
 
+def c3_strong_bench(args, world, rank, dev):
+    """C3 at a FIXED fleet (BASELINE.json configs[2]: the synthetic 4096-room fleet on 1/2/4/8
+    GPUs): ``--agents`` agents in total (the same agents as the one-GPU fleet), each rank
+    solving its contiguous share; no collective on the data path.  Reported beside the
+    weak-scaling headline (which keeps ``--agents`` per GPU)."""
+    import torch
+    import torch.distributed as dist
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+
+    be, cv = bm.one_room(solver_options=solver_settings(args)[0])
+    prob = be.problem
+    lo, hi = bm.split_range(args.agents, rank, world)
+    vals = {k: v[lo:hi] for k, v in fleet_values(args.agents, 20261015 + 2).items()}
+    p, lbw, ubw, w0 = fleet_nlp_inputs(prob, cv, vals)
+    if world > 1:
+        dist.barrier()
+    stats, wall, kernel_ms = _timed_batch(be, prob, p, lbw, ubw, w0, hi - lo, args, dev)
+    ok = sum(1 for s in stats if s["success"])
+    t = torch.tensor([wall, float(ok)], dtype=torch.float64, device=dev)
+    if world > 1:
+        w = t[:1].clone()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t[0] = w[0]
+    return {"workload": "C3 fixed fleet split over the GPUs", "scaling": "strong", "agents_total": args.agents,
+            "agents_rank0": hi - lo, "solves_per_s": float(t[1]) * args.steps / float(t[0]),
+            "ms_per_step": float(t[0]) / args.steps * 1e3, "kernel_ms_rank0": kernel_ms}
+
+
 def mhe_bench(args, world, rank, dev):
     """Moving horizon estimation fleet (backend casadi_mhe, `examples/Estimators/
     mhe_example.py`: RNGRoom, N=15, ts=200, Legendre d=2, estimating the capacity
@@ -288,6 +323,7 @@ def mhe_bench(args, world, rank, dev):
         "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
         "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
         "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
+        "linesearch_fallbacks_last_step": int(sum(s["n_linesearch_fallbacks"] for s in stats)),
         "factorisation": "stage-parallel, continuity rows bordered into the chain (DESIGN 2.1)"
                          if prob.gen.bordered_rows else "stage-parallel",
         "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
@@ -311,11 +347,12 @@ def c2_admm_bench(args, world, rank, dev):
     from agentlib_mpc_amd.admm.fleet import ADMMFleet
 
     nb = args.c2_blocks
-    make = lambda n: bm.c2_fleet_classes(n_blocks=n, N=10, seed=20261015 + 1, block_offset=rank * n,  # noqa: E731
-                                         solver_options={"ipopt": {}})
+    lo, hi = bm.split_range(nb, rank, world)
+    make = lambda n, off=rank * 8: bm.c2_fleet_classes(n_blocks=n, N=10, seed=20261015 + 1,  # noqa: E731
+                                                      block_offset=off, solver_options={"ipopt": {}})
     _warm_fleet(make, lambda fl: fl.run_coordinated(0.4, admm_iter_max=2, use_relative_tolerances=False,
                                                     primal_tol=0.002, dual_tol=0.1), world, dev)
-    classes = make(nb)
+    classes = make(hi - lo, lo)
     fleet = ADMMFleet(classes, device=dev, comm="default" if world > 1 else None)
     for c in classes:
         c.native.reserve(c.n)
@@ -338,9 +375,13 @@ def c2_admm_bench(args, world, rank, dev):
                                 5 * nb, "C2 coordinated, to each block's stopping rule")
     return {
         "workload": "C2 scaled: 4-room + air-handler blocks (casadi_admm collocation d=3, N=10, ts=60), "
-                    "coordinated consensus, rho=0.4, abs tol 0.002/0.1, iter max 40, per-block stopping",
-        "blocks_per_gpu": nb, "agents_per_gpu": 5 * nb,
+                    "coordinated consensus, rho=0.4, abs tol 0.002/0.1, iter max 40, per-block stopping; "
+                    "the north-star 4096-room fleet (1024 blocks) split over the GPUs",
+        "scaling": "strong", "blocks_total": nb, "rooms_total": 4 * nb, "agents_total": 5 * nb,
+        "blocks_rank0": hi - lo if rank == 0 else None,
+        "allreduce_doubles": fleet.reduce_len if world > 1 else 0,
         **_block_summary(out, wall, 5, world, dev),
+        **_fallbacks(out["linesearch_fallbacks"], world, dev),
         "cpu_baseline": cpu,
     }
 
@@ -362,32 +403,48 @@ def _warm_fleet(make_classes, run, world, dev, n_blocks=8):
 
 
 def _block_summary(out, wall, agents_per_block, world=1, dev=None):
-    """ADMM iterations/s to consensus of a multi-block coordinated run.  The block counts
-    are global (the residual totals are all-reduced); the converged-solve counter is per
-    rank, so it is summed over the ranks, and the wall time is the max over the ranks."""
+    """ADMM iterations/s to consensus of a multi-block coordinated run over all ranks.  Every
+    rank holds its rank-local blocks plus the blocks spanning ranks (identical copies), so
+    the per-block arrays are gathered (outside the timed region) and the spanning blocks
+    counted once; converged solves are summed, the wall time is the max over the ranks."""
+    it = np.asarray(out["block_iterations"])
+    conv = np.asarray(out["block_converged"])
+    glob = np.asarray(out.get("block_is_global", np.zeros(len(it), bool)))
+    iters, ok = out["iterations"], out["converged_solves"]
+    if world > 1:
+        import torch.distributed as dist
+
+        parts = [None] * world
+        dist.all_gather_object(parts, (it[~glob].tolist(), conv[~glob].tolist(), int(ok), float(wall), int(iters)))
+        it = np.concatenate([it[glob]] + [np.asarray(p[0], np.int64) for p in parts])
+        conv = np.concatenate([conv[glob]] + [np.asarray(p[1], bool) for p in parts])
+        ok = sum(p[2] for p in parts)
+        wall = max(p[3] for p in parts)
+        iters = max(p[4] for p in parts)
+    solves = int(np.sum(it)) * agents_per_block
+    return {
+        "admm_iterations": iters, "converged": bool(conv.all()),
+        "converged_block_fraction": float(conv.mean()),
+        "block_iterations_p50_max": [float(np.percentile(it, 50)), int(it.max())],
+        "admm_iters_per_s": iters / wall,
+        "block_admm_iters_per_s": float(it.sum()) / wall,
+        "wall_s": wall,
+        "agent_solves_per_s": ok / wall,
+        "converged_solve_fraction": ok / max(1, solves),
+    }
+
+
+def _fallbacks(n, world, dev):
+    """Line-search failures that took the kernel's fallback step instead of IPOPT's
+    restoration phase, summed over the ranks (every leg reports it)."""
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        t = torch.tensor([float(out["converged_solves"]), wall], dtype=torch.float64, device=dev)
-        w = t[1:].clone()
-        dist.all_reduce(t[:1], op=dist.ReduceOp.SUM)
-        dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        out = dict(out, converged_solves=int(t[0].item()))
-        wall = float(w[0].item())
-    it = np.asarray(out["block_iterations"])
-    conv = np.asarray(out["block_converged"])
-    solves = int(np.sum(it)) * agents_per_block
-    return {
-        "admm_iterations": out["iterations"], "converged": out["converged"],
-        "converged_block_fraction": float(conv.mean()),
-        "block_iterations_p50_max": [float(np.percentile(it, 50)), int(it.max())],
-        "admm_iters_per_s": out["iterations"] / wall,
-        "block_admm_iters_per_s": float(it.sum()) / wall,
-        "wall_s": wall,
-        "agent_solves_per_s": out["converged_solves"] / wall,
-        "converged_solve_fraction": out["converged_solves"] / max(1, solves),
-    }
+        t = torch.tensor([float(n)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        n = int(t.item())
+    return {"linesearch_fallbacks": int(n)}
 
 
 def c5_admm_bench(args, world, rank, dev):
@@ -402,14 +459,15 @@ def c5_admm_bench(args, world, rank, dev):
     from agentlib_mpc_amd.admm.fleet import ADMMFleet
 
     nb = args.c5_blocks
+    lo, hi = bm.split_range(nb, rank, world)
     # the example's solver options are the reference IPOPT defaults
     # (`casadi_utils.py:197-206`; Room_1.json sets print_level only)
     opts = {"ipopt": {}}
-    make = lambda n: bm.c5_fleet_classes(n_blocks=n, N=24, seed=20261015 + 5, block_offset=rank * n,  # noqa: E731
-                                         solver_options=opts)
+    make = lambda n, off=rank * 8: bm.c5_fleet_classes(n_blocks=n, N=24, seed=20261015 + 5,  # noqa: E731
+                                                      block_offset=off, solver_options=opts)
     _warm_fleet(make, lambda fl: fl.run_coordinated(1.0, admm_iter_max=2, use_relative_tolerances=False,
                                                     primal_tol=0.04, dual_tol=0.04), world, dev)
-    classes = make(nb)
+    classes = make(hi - lo, lo)
     fleet = ADMMFleet(classes, device=dev, comm="default" if world > 1 else None)
     for c in classes:
         c.native.reserve(c.n)
@@ -433,8 +491,10 @@ def c5_admm_bench(args, world, rank, dev):
     return {
         "workload": "C5: three-zone data-driven ADMM (3 NARX zones + AHU + CCA per block), coordinated "
                     "consensus, rho=1, N=24 ts=1800, abs tol 0.04/0.04, per-block stopping",
-        "blocks_per_gpu": nb, "zones_per_gpu": 3 * nb, "agents_per_gpu": 5 * nb,
+        "scaling": "strong", "blocks_total": nb, "zones_total": 3 * nb, "agents_total": 5 * nb,
+        "blocks_rank0": hi - lo if rank == 0 else None,
         **_block_summary(out, wall, 5, world, dev),
+        **_fallbacks(out["linesearch_fallbacks"], world, dev),
         "solver": "reference IPOPT defaults (casadi_utils.py:197-206)",
         "cpu_baseline": cpu,
     }
@@ -626,13 +686,16 @@ def main():
                     help="reference: the reference's IPOPT defaults; tight: --tol, no acceptable stop")
     ap.add_argument("--tol", type=float, default=1e-8, help="tolerance of --solver tight")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--admm-agents", type=int, default=16384, help="C4 agents per GPU (0: skip)")
+    ap.add_argument("--admm-agents", type=int, default=16384,
+                    help="C4 agents in total, split over the GPUs (0: skip)")
     ap.add_argument("--admm-iters", type=int, default=15)
     ap.add_argument("--nn-zones", type=int, default=1024, help="C5 NARX zones per GPU (0: skip)")
-    ap.add_argument("--c5-blocks", type=int, default=342, help="C5 ADMM blocks (3 zones+AHU+CCA) per GPU (0: skip)")
+    ap.add_argument("--c5-blocks", type=int, default=342,
+                    help="C5 ADMM blocks (3 zones+AHU+CCA) in total, split over the GPUs (0: skip)")
     ap.add_argument("--c5-iters", type=int, default=50)
     ap.add_argument("--mhe-agents", type=int, default=4096, help="MHE estimators per GPU (0: skip)")
-    ap.add_argument("--c2-blocks", type=int, default=1024, help="C2 4-room+AHU blocks per GPU (0: skip)")
+    ap.add_argument("--c2-blocks", type=int, default=1024,
+                    help="C2 4-room+AHU blocks in total (1024 = the 4096-room fleet), split over the GPUs (0: skip)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the plugin-API end-to-end leg and C1 latency")
     args = ap.parse_args()
 
@@ -700,6 +763,7 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
+    c3s = c3_strong_bench(args, world, rank, dev) if world > 1 else None
     admm = admm_bench(args, world, rank, dev) if args.admm_agents > 0 else None
     nn = nn_bench(args, world, rank, dev) if args.nn_zones > 0 else None
     c5 = c5_admm_bench(args, world, rank, dev) if args.c5_blocks > 0 else None
@@ -752,6 +816,7 @@ def main():
                 "statuses_rank0": {k: int(v) for k, v in zip(*np.unique([s["return_status"] for s in stats],
                                                                          return_counts=True))},
                 "mean_ipm_iterations": float(arr["iter"].mean()),
+                "linesearch_fallbacks_rank0": int(sum(s_["n_linesearch_fallbacks"] for s_ in stats)),
                 "ipm_iterations_p50_p99_max": [float(np.percentile(arr["iter"], q)) for q in (50, 99, 100)],
                 "parallelism": f"agent-partitioned dp{world}",
             },
@@ -774,6 +839,8 @@ def main():
                         "by dependent LDS/L2 round trips, not by FP64 issue (DESIGN §5)",
             },
         }
+        if c3s is not None:
+            out["c3_strong"] = c3s
         if admm is not None:
             out["admm"] = admm
         if nn is not None:

@@ -305,9 +305,13 @@ def _part_worker(rank, world, init_file, N, out_file):
         fl.set_participation({"room": mask})
         out = fl.run_coordinated(0.4, **kw)
         traj = fl.trajectories()
-        np.savez(f"{out_file}.{rank}.npz",
-                 rec=np.array([[r.primal_residual, r.dual_residual] for r in first["records"] + out["records"]]),
-                 **{al: traj[al] for al in traj})
+        # per-block histories: world 1 holds blocks 0 and 1, rank r of world 2 block r (its
+        # only, rank-local block); the all-reduce carries nothing for rank-local blocks
+        assert fl.n_global_blocks == 0 and fl.reduce_len == 0 or world == 1
+        rec = {f"rec{b if world == 1 else rank}": np.array(
+            [[r.primal_residual, r.dual_residual] for r in first["block_records"][b] + out["block_records"][b]])
+            for b in range(fl.n_blocks)}
+        np.savez(f"{out_file}.{rank}.npz", **rec, **{al: traj[al] for al in traj})
     finally:
         if world > 1:
             dist.destroy_process_group()
@@ -324,10 +328,8 @@ def test_partitioned_participation_world2_matches_world1(tmp_path):
     mp.spawn(_part_worker, args=(2, init, N, out + "2"), nprocs=2, join=True)
     two = [dict(np.load(f"{out}2.{r}.npz")) for r in range(2)]
     for r in two:
-        np.testing.assert_allclose(r["rec"], one["rec"], rtol=1e-9, atol=1e-12)
         for al, v in r.items():
-            if al != "rec":
-                np.testing.assert_allclose(v, one[al], rtol=1e-10, atol=1e-12, err_msg=al)
+            np.testing.assert_allclose(v, one[al], rtol=1e-9, atol=1e-12, err_msg=al)
 
 
 def test_masked_round_converging_at_first_iteration_keeps_the_mask():
@@ -412,3 +414,50 @@ def test_consensus_multipliers_of_an_alias_sum_to_zero():
         rows = lam[fl.gstart[g]:fl.gstart[g + 1]]
         assert len(rows) == 2
         np.testing.assert_allclose(rows.sum(0), 0.0, atol=1e-12 * np.abs(lam).max())
+
+
+def _mixed_worker(rank, world, init_file, out_file):
+    """One coordinated fleet holding a C4 exchange alias that spans the ranks (one global
+    block) and C2 consensus blocks that are rank-local: world 1 holds everything, rank r of
+    world 2 its share of the C4 agents and C2 block r."""
+    if world > 1:
+        dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        c2 = bm.c2_fleet_classes(n_blocks=2 if world == 1 else 1, N=1, seed=7,
+                                 block_offset=0 if world == 1 else rank)
+        c4 = bm.c4_fleet_classes(n_rooms=4, n_supply=2, N=3, rank=rank, world=world)
+        for c in c4:
+            c.name = "x" + c.name
+        ops = CpuADMMOps({"room": nlps.admm_room(N=1), "ahu": nlps.admm_ahu(N=1),
+                          "xroom": nlps.exchange_room(N=3), "xsupply": nlps.exchange_supply(N=3)})
+        fl = ADMMFleet(c2 + c4, device="cpu", ops=ops, comm="default" if world > 1 else None)
+        assert fl.n_global_blocks == (1 if world > 1 else 0)
+        if world > 1:   # the exchange group's moments + ONE block's totals, whatever the C2 count
+            assert fl.reduce_len == fl.n_global * fl.S + 8
+        out = fl.run_coordinated(1.0, admm_iter_max=2, use_relative_tolerances=False, primal_tol=1e-12,
+                                 dual_tol=1e-12)
+        xb = fl.block_index("mDot_coupling")
+        c2b = [fl.block_index(f"mDot1_coupling_b{b}") for b in ((0, 1) if world == 1 else (rank,))]
+        rec = {"x": np.array([[r.primal_residual, r.dual_residual] for r in out["block_records"][xb]])}
+        for b, blk in zip((0, 1) if world == 1 else (rank,), c2b):
+            rec[f"b{b}"] = np.array([[r.primal_residual, r.dual_residual] for r in out["block_records"][blk]])
+        traj = fl.trajectories()
+        np.savez(f"{out_file}.{rank}.npz", **rec, **{f"t_{al}": v for al, v in traj.items()})
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_mixed_global_and_local_blocks_world2_matches_world1(tmp_path):
+    """Blocks spanning ranks and rank-local blocks in one coordinated fleet: the
+    spanning block's totals travel in the one all-reduce, the local blocks' do not, and two
+    ranks reproduce the one-rank histories block by block."""
+    init, out = str(tmp_path / "init"), str(tmp_path / "out")
+    _mixed_worker(0, 1, init, out + "1")
+    one = dict(np.load(f"{out}1.0.npz"))
+    mp.spawn(_mixed_worker, args=(2, init, out + "2"), nprocs=2, join=True)
+    for r in range(2):
+        two = dict(np.load(f"{out}2.{r}.npz"))
+        assert f"b{r}" in two
+        for k, v in two.items():
+            np.testing.assert_allclose(v, one[k], rtol=1e-9, atol=1e-12, err_msg=k)

@@ -7,7 +7,8 @@ tests/test_reference_fixtures.py checks the restatement against the file).
   points -- here at the reference's own solver defaults and, at tight tolerance, equal to
   the oracle's solution (objective rel 1e-6, trajectories rel 1e-5).
 * `tests/test_admm.py:60-161`: two ADMM agents coupled through ``myout`` (initial values
-  298.16 and 295, penalty 10, 20 iterations): the multipliers of the two agents sum to
+  298.16 and 295, penalty 10, 20 iterations; the second agent's state starts at 295 and its
+  disturbance is 280, so that real solves differ): the multipliers of the two agents sum to
   zero (the reference allows 10 % for an off-by-one of its threaded loop; the batched
   fleet has none, so the sum is zero to rounding) and are not zero.
 """
@@ -53,7 +54,10 @@ def test_admm_multipliers_of_two_agents_sum_to_zero():
     from agentlib_mpc_amd.admm.fleet import ADMMFleet, FleetClass
 
     be, cv = bm.fixture_admm()
-    cls = FleetClass("agent", be, bm._class_inputs(be, cv, {}, 2), initial={"myout": [298.16, 295.0]})
+    # the reference's debug solver returns each agent's configured coupling value; with real
+    # solves the two agents must differ in their own inputs for the multipliers to move
+    inputs = bm._class_inputs(be, cv, {"state": [298.16, 295.0], "disturbance": [270.0, 280.0]}, 2)
+    cls = FleetClass("agent", be, inputs, initial={"myout": [298.16, 295.0]})
     fleet = ADMMFleet([cls])
     out = fleet.run_local(penalty_factor=10.0, max_iterations=20)
     assert out["converged_solves"] == 2 * 20

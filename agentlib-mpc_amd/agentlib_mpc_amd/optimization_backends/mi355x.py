@@ -110,7 +110,8 @@ class MI355XBackend(OptimizationBackend):
         super().__init__(config)
         self.problem: Optional[CompiledProblem] = None
         self.system = None
-        self._remembered: Optional[np.ndarray] = None  # [n, nw] last optimum per batch slot
+        self._remembered: Optional[np.ndarray] = None  # [n, nw] last optimum per batch slot (host path)
+        self._resident = None  # device-resident inputs + warm start of the plugin batch (plugin_batch.py)
         name = getattr(self.config.solver.name, "value", self.config.solver.name)
         if name not in KERNEL_SOLVERS:
             raise ValueError(f"solver {name!r} is not available on the MI355X backend "
@@ -127,7 +128,13 @@ class MI355XBackend(OptimizationBackend):
         nlp = discretization.transcribe(self.system)
         self.problem = CompiledProblem(nlp, self.system,
                                        only_positive_times=self.only_positive_times_in_results)
+        self.reset_warm_start()
+
+    def reset_warm_start(self):
+        """Forget the remembered optima: the next solve starts cold (a new backend's first
+        solve, `core/discretization.py:212-245`)."""
         self._remembered = None
+        self._resident = None
 
     def _native(self):
         prob = self.problem.native
@@ -150,6 +157,12 @@ class MI355XBackend(OptimizationBackend):
             raise RuntimeError("setup_optimization() must be called before solve()")
         prob = self.problem
         n = len(batch_vars)
+        if prob.nlp.lift is None:
+            res = self._solve_resident(now, batch_vars)
+            if self.config.save_results:
+                for i in range(n):
+                    self.save_result_df(res[i], now)
+            return res
         w_prev = self._remembered if self._remembered is not None and self._remembered.shape[0] == n else None
         p, lbw, ubw, w0, sampled = prob.marshal.inputs(batch_vars, now, w_prev, return_sampled_bounds=True)
         res = self.solve_arrays(p, lbw, ubw, w0, result_bounds=sampled)
@@ -158,6 +171,29 @@ class MI355XBackend(OptimizationBackend):
             for i in range(n):
                 self.save_result_df(res[i], now)
         return res
+
+    def _solve_resident(self, now, batch_vars):
+        """Plugin batch on device-resident inputs (:mod:`.plugin_batch`): only the inputs
+        that changed since the last call cross PCIe, the warm start stays in HBM."""
+        import torch
+
+        from agentlib_mpc_amd.optimization_backends.plugin_batch import ResidentBatch, RowSource
+        from agentlib_mpc_amd.optimization_backends.problem import FleetResults
+        from agentlib_mpc_amd.runtime.native import StatsView, stats_array
+
+        prob = self.problem
+        t0 = time.perf_counter()
+        rb = self._resident
+        if rb is None or rb.n != len(batch_vars):
+            self._remembered = None
+            rb = self._resident = ResidentBatch(prob, self._native(), batch_vars, now, torch.device("cuda"))
+            snap = rb.last
+        else:
+            self._native()  # options of this backend (set_options is per handle)
+            snap = rb.update(batch_vars, now)
+        w, raw = rb.solve()
+        stats = StatsView(stats_array(raw), {"t_wall_total": time.perf_counter() - t0})
+        return FleetResults(prob, prob.marshal, None, None, None, w, stats, rows=RowSource(rb, snap))
 
     def solve_arrays(self, p, lbw, ubw, w0, lbg=None, ubg=None, result_bounds=None):
         """Batched solve of reference-layout NLP inputs [n, .] (host arrays): device

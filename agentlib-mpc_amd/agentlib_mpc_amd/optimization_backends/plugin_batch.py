@@ -1,0 +1,230 @@
+"""Device-resident inputs behind the plugin API's batched solve.
+
+``MI355XBackend.solve_batch`` is the drop-in for ``OptimizationBackend.solve`` of every
+agent of a fleet (`core/casadi_backend.py:133-139`): each call hands over one dict of
+``MPCVariable`` per agent, which the reference samples onto the NLP grids
+(`core/casadi_backend.py:141-253`), maps to the NLP vectors (`core/discretization.py:
+277-348`) and warm-starts from the agent's previous optimum (`:212-251`).  Re-marshalling
+every agent's dict into fresh [n, nw] host arrays and copying them to the GPU on every
+call costs an order of magnitude more than the kernel at fleet sizes.
+
+:class:`ResidentBatch` keeps the kernel's inputs in HBM between calls and, per call,
+
+* reads every (variable, attribute) the marshalling needs ONCE over the agents (one
+  C-level ``itemgetter`` / ``attrgetter`` pass each, numbers converted with
+  ``np.fromiter``; lists, series and other trajectories take the sampling path of
+  :class:`~agentlib_mpc_amd.optimization_backends.problem.BatchMarshal`, with the same
+  errors for empty values and non-``MPCVariable`` inputs);
+* uploads only the columns whose values changed since the last call and scatters them
+  on the device into the parameter / bound columns the reference layout gives them
+  (``GroupLayout.index``), then re-applies the bounds and guesses taken from parameters
+  (the fixed ``x_0 = initial state``);
+* keeps the solution in place as the next call's initial guess (the reference's one
+  remembered optimum per backend, `core/discretization.py:221-223`); agents whose last
+  solution holds NaN restart cold, as the reference's guess logic would.
+
+The per-agent :class:`Results` are built on access from a snapshot of the values read
+in that call (arrays that later calls never modify), so results stay valid after the
+next solve.  Only problems solved in the reference layout take this path (lifted NARX /
+MHE stage forms re-marshal on the host).
+"""
+
+from __future__ import annotations
+
+import operator
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from agentlib_mpc_amd.optimization_backends.problem import BatchMarshal
+
+
+def _values(vs, attr, n):
+    """(n,) float array of one attribute over the agents, or None if not all numbers
+    (numpy reads None as NaN: NaN entries take the checked path too)."""
+    try:
+        arr = np.fromiter(map(operator.attrgetter(attr), vs), dtype=np.float64, count=n)
+    except (TypeError, ValueError):
+        return None
+    return None if np.isnan(arr).any() else arr
+
+
+class RowSource:
+    """Reference-layout (p, sampled lbw, sampled ubw) rows of single agents, rebuilt from the
+    values one call read (for :class:`~.problem.FleetResults`)."""
+
+    def __init__(self, state: "ResidentBatch", snapshot: Dict[tuple, object]):
+        self.state = state
+        self.snapshot = snapshot
+
+    def rows(self, i: int) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        st = self.state
+        p, ls, us = st.base_p.copy(), st.base_ls.copy(), st.base_us.copy()
+        dst = {"p": p, "ls": ls, "us": us}
+        for key, cols in st.targets.items():
+            val = self.snapshot[key]
+            for arr_key, c, g in cols:
+                v = val[g] if isinstance(val, dict) else val
+                dst[arr_key][c] = v[i] if v.ndim == 1 else v[i, :len(c)]
+        return p, ls, us
+
+
+class ResidentBatch:
+    """Resident NLP inputs of one batch size of one backend (reference layout == kernel
+    layout)."""
+
+    def __init__(self, prob, native, batch_vars: Sequence[dict], now: float, device):
+        import torch
+
+        self.torch = torch
+        self.prob, self.native = prob, native
+        m: BatchMarshal = prob.marshal
+        self.marshal = m
+        self.n = n = len(batch_vars)
+        self.dev = device
+        # (ref, attr) -> [(array key, reference columns, group id)]; one group id per
+        # (group, grid) so list / series values are sampled per grid
+        self.targets: Dict[tuple, List[tuple]] = {}
+        self.grids: Dict[int, list] = {}
+        gid = 0
+        for name, grid, rows, index in m.pars:
+            if index is None:
+                continue
+            self.grids[gid] = grid
+            for i, ref, _ in rows:
+                if ref is not None:
+                    self.targets.setdefault((ref, "value"), []).append(("p", index[i], gid))
+            gid += 1
+        for name, grid, rows, index in m.vars:
+            if index is None:
+                continue
+            self.grids[gid] = grid
+            for i, ref, _, _ in rows:
+                if ref is not None:
+                    self.targets.setdefault((ref, "lb"), []).append(("ls", index[i], gid))
+                    self.targets.setdefault((ref, "ub"), []).append(("us", index[i], gid))
+            gid += 1
+        # every ref the host marshalling reads (also groups without grid points: validated)
+        self.refs: Dict[str, List[str]] = {}
+        for name, grid, rows, index in m.pars:
+            for i, ref, _ in rows:
+                if ref is not None:
+                    self.refs.setdefault(ref, [])
+                    if "value" not in self.refs[ref]:
+                        self.refs[ref].append("value")
+        for name, grid, rows, index in m.vars:
+            for i, ref, _, _ in rows:
+                if ref is not None:
+                    lst = self.refs.setdefault(ref, [])
+                    for at in ("lb", "ub"):
+                        if at not in lst:
+                            lst.append(at)
+        # full marshal once: device arrays, template rows, the values of this call
+        p, lbw, ubw, w0, (ls, us) = m.inputs(batch_vars, now, None, return_sampled_bounds=True)
+        self.base_p, self.base_ls, self.base_us = p[0].copy(), ls[0].copy(), us[0].copy()
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(device)  # noqa: E731
+        self.P, self.L, self.U, self.W = T(p), T(lbw), T(ubw), T(w0)
+        self.LS, self.US = T(ls), T(us)  # sampled bounds (before the parameter overrides)
+        self.idx = {}
+        for key, cols in self.targets.items():
+            for _, c, _ in cols:
+                self.idx.setdefault(c.tobytes(), torch.as_tensor(c, device=device))
+        self.over = {k: (torch.as_tensor(c, device=device), torch.as_tensor(q, device=device))
+                     for k, (c, q) in m.over.items() if c.size}
+        self.last: Dict[tuple, object] = self.read(batch_vars, now)
+        self.cold_rows: Optional[np.ndarray] = None
+        self.lam_g = torch.empty((n, prob.nlp.kernel_ng), dtype=torch.float64, device=device)
+        from agentlib_mpc_amd.runtime.native import STATS_BYTES
+
+        self.ST = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=device)
+
+    # -- reading the agents' variables ---------------------------------------------------
+    def read(self, batch_vars: Sequence[dict], now: float) -> Dict[tuple, object]:
+        """Values of every (ref, attr) over the agents: an (n,) array when every agent holds a
+        number, else {group id: (n, G) samples} (sampling path, reference errors)."""
+        n, m = self.n, self.marshal
+        out = {}
+        for ref, attrs in self.refs.items():
+            vs = list(map(operator.itemgetter(ref), batch_vars))
+            if "value" in attrs:  # one object per type, as BatchMarshal.inputs checks
+                for v in dict(zip(map(type, vs), vs)).values():
+                    if not hasattr(v, "interpolation_method"):
+                        raise TypeError(
+                            f"The variable {ref} does not have an interpolationmethod. All Variables "
+                            "used in MPC need to be of type MPCVariable (subclass of AgentVariable).")
+            for attr in attrs:
+                arr = _values(vs, attr, n)
+                if arr is not None:
+                    out[(ref, attr)] = arr
+                    continue
+                vals = list(map(operator.attrgetter(attr), vs))
+                if attr == "value" and any(v is None for v in vals):
+                    raise ValueError(f"Input for variable {ref} is empty. Cannot solve optimization problem.")
+                meth = (lambda a: vs[a].interpolation_method) if attr == "value" else \
+                    (lambda a: getattr(vs[a], "interpolation_method", "linear"))
+                per = {}
+                for _, _, g in self.targets.get((ref, attr), []):
+                    if g not in per:
+                        per[g] = m._column(vals, self.grids[g], now, meth)
+                out[(ref, attr)] = per
+        return out
+
+    # -- one call ------------------------------------------------------------------------
+    def update(self, batch_vars: Sequence[dict], now: float) -> Dict[tuple, object]:
+        """Read the agents' variables, upload what changed, re-apply the parameter-derived
+        bounds and guesses; returns the snapshot of the values read."""
+        torch = self.torch
+        cur = self.read(batch_vars, now)
+        dst = {"p": self.P, "ls": self.LS, "us": self.US}
+        changed = False
+        for key, val in cur.items():
+            old = self.last.get(key)
+            same = (isinstance(val, np.ndarray) and isinstance(old, np.ndarray) and val.shape == old.shape
+                    and np.array_equal(val, old)) or (
+                isinstance(val, dict) and isinstance(old, dict) and val.keys() == old.keys()
+                and all(np.array_equal(val[g], old[g]) for g in val))
+            if same:
+                cur[key] = old  # keep the array already referenced by earlier snapshots
+                continue
+            changed = True
+            if isinstance(val, np.ndarray):
+                dv = torch.from_numpy(val).to(self.dev, non_blocking=True)
+            else:
+                dvs = {g: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev, non_blocking=True)
+                       for g, a in val.items()}
+            for arr_key, c, g in self.targets.get(key, []):
+                ix = self.idx[c.tobytes()]
+                if isinstance(val, np.ndarray):
+                    dst[arr_key][:, ix] = dv[:, None].expand(-1, ix.numel())
+                else:
+                    dst[arr_key][:, ix] = dvs[g][:, :ix.numel()]
+        if changed:
+            self.L.copy_(self.LS)
+            self.U.copy_(self.US)
+            for k, arr in (("lb", self.L), ("ub", self.U)):
+                if k in self.over:
+                    c, q = self.over[k]
+                    arr[:, c] = self.P[:, q]
+        if "guess" in self.over:
+            c, q = self.over["guess"]
+            self.W[:, c] = self.P[:, q]
+        if self.cold_rows is not None and self.cold_rows.size:
+            rows = [batch_vars[i] for i in self.cold_rows]
+            _, _, _, w0 = self.marshal.inputs(rows, now, None)
+            self.W[torch.as_tensor(self.cold_rows, device=self.dev)] = torch.from_numpy(w0).to(self.dev)
+            self.cold_rows = None
+        self.last = cur
+        return cur
+
+    def solve(self):
+        """Launch on the resident arrays (the solution replaces the guess in place); returns
+        (w, raw stats) on the host."""
+        torch = self.torch
+        self.native.solve(self.P, self.L, self.U, self.W, lam_g=self.lam_g, stats=self.ST)
+        w = torch.empty((self.n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)
+        w.copy_(self.W, non_blocking=True)
+        nan_rows = torch.isnan(self.W).any(dim=1).nonzero().flatten()  # synchronises
+        raw = self.ST.cpu().numpy()
+        bad = nan_rows.cpu().numpy()
+        self.cold_rows = bad if bad.size else None
+        return w.numpy(), raw

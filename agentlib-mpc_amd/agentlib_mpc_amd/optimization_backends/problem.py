@@ -488,11 +488,34 @@ class BatchMarshal:
 
 class FleetResults(Sequence):
     """Results of one batched solve: per-agent :class:`Results` built on access; whole-fleet
-    arrays (solutions, stats) without per-agent objects."""
+    arrays (solutions, stats) without per-agent objects.  The inputs are either the
+    reference-layout arrays (``p``, sampled ``lbw`` / ``ubw``) or ``rows``, a source of
+    single-agent rows (:class:`~.plugin_batch.RowSource`, the resident plugin path)."""
 
-    def __init__(self, prob: "CompiledProblem", marshal: BatchMarshal, p, lbw, ubw, w, stats: list):
+    def __init__(self, prob: "CompiledProblem", marshal: BatchMarshal, p, lbw, ubw, w, stats: list, rows=None):
         self.prob, self.marshal = prob, marshal
-        self.p, self.lbw, self.ubw, self.w, self.stats = p, lbw, ubw, w, stats
+        self._p, self._lbw, self._ubw, self.w, self.stats = p, lbw, ubw, w, stats
+        self._rows = rows
+
+    def _all_rows(self):
+        if self._p is None:
+            rows = [self._rows.rows(i) for i in range(len(self))]
+            self._p, self._lbw, self._ubw = (np.stack(a) for a in zip(*rows))
+
+    @property
+    def p(self):
+        self._all_rows()
+        return self._p
+
+    @property
+    def lbw(self):
+        self._all_rows()
+        return self._lbw
+
+    @property
+    def ubw(self):
+        self._all_rows()
+        return self._ubw
 
     def __len__(self):
         return self.w.shape[0]
@@ -502,7 +525,13 @@ class FleetResults(Sequence):
             return [self[k] for k in range(*i.indices(len(self)))]
         if i < 0:
             i += len(self)
-        m = self.marshal.result_matrices(self.p[i:i + 1], self.lbw[i:i + 1], self.ubw[i:i + 1], self.w[i:i + 1])[0]
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        if self._p is None:
+            p, lb, ub = (a[None] for a in self._rows.rows(i))
+        else:
+            p, lb, ub = self._p[i:i + 1], self._lbw[i:i + 1], self._ubw[i:i + 1]
+        m = self.marshal.result_matrices(p, lb, ub, self.w[i:i + 1])[0]
         lay = self.prob.layout
         return Results(matrix=m, grid=list(lay.full_grid), columns=lay.columns, stats=self.stats[i],
                        variable_grid_indices=lay.variable_grid_indices)

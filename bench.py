@@ -630,11 +630,11 @@ def c1_latency(args, dev):
     solver_opts, oracle_opts = solver_settings(args)
     be, cv = bm.one_room(solver_options=solver_opts)
     for _ in range(3):
-        be._remembered = None
+        be.reset_warm_start()
         be.solve(0.0, cv)
     e2e = []
     for _ in range(20):
-        be._remembered = None  # cold start each time (the reference's first solve)
+        be.reset_warm_start()  # cold start each time (the reference's first solve)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         r = be.solve(0.0, cv)

@@ -1,0 +1,123 @@
+"""Resident plugin batch (CPU): the incremental device-resident inputs of
+``MI355XBackend.solve_batch`` (`optimization_backends/plugin_batch.py`) equal a full
+re-marshalling of the agents' variables (`problem.BatchMarshal.inputs`, the reference's
+input path `core/casadi_backend.py:141-253`, `core/discretization.py:212-348`) after
+every kind of change: scalar measurements, a trajectory given as a list, bounds, and the
+warm start with the parameter-derived guess; the per-agent result rows equal the
+re-marshalled ones; empty values and non-MPCVariable inputs raise the reference's errors.
+The device is the CPU here (torch tensors), the kernel is not called."""
+
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from agentlib_mpc_amd import benchmarks as bm
+from agentlib_mpc_amd.optimization_backends.plugin_batch import ResidentBatch, RowSource
+
+
+def _agents(cv, n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        c = copy.deepcopy(cv)
+        c["T"].value = float(rng.uniform(291, 301))
+        c["load"].value = float(rng.uniform(50, 250))
+        c["mDot"].value = float(rng.uniform(0, 0.05))
+        out.append(c)
+    return out
+
+
+def _check(rb, m, agents, now, w_prev):
+    p, lbw, ubw, w0, (ls, us) = m.inputs(agents, now, w_prev, return_sampled_bounds=True)
+    np.testing.assert_array_equal(rb.P.numpy(), p)
+    np.testing.assert_array_equal(rb.L.numpy(), lbw)
+    np.testing.assert_array_equal(rb.U.numpy(), ubw)
+    np.testing.assert_array_equal(rb.W.numpy(), w0)
+    return p, ls, us
+
+
+def test_resident_inputs_equal_full_marshalling():
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    m = be.problem.marshal
+    agents = _agents(cv, 16, 3)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    _check(rb, m, agents, 0.0, None)
+    snaps = [RowSource(rb, rb.last)]
+    want_rows = [m.inputs(agents, 0.0, None, return_sampled_bounds=True)]
+    # step 2: new measurements, one agent's T_upper as a trajectory on its grid, a bound
+    w_prev = rb.W.numpy().copy()
+    w_prev[:, 5:9] += 0.25          # stands in for the solution the kernel would write in place
+    rb.W.copy_(torch.from_numpy(w_prev))
+    for i, c in enumerate(agents):
+        c["T"].value += 0.1 * (i + 1)
+    grid = len(be.problem.nlp.par_groups["d"].grid)
+    agents[3]["T_upper"] = copy.deepcopy(agents[3]["T_upper"])
+    agents[3]["T_upper"].value = list(np.linspace(294.0, 296.0, grid))
+    agents[5]["mDot"] = copy.deepcopy(agents[5]["mDot"])
+    agents[5]["mDot"].ub = 0.04
+    snap = rb.update(agents, 300.0)
+    _check(rb, m, agents, 300.0, w_prev)
+    snaps.append(RowSource(rb, snap))
+    want_rows.append(m.inputs(agents, 300.0, w_prev, return_sampled_bounds=True))
+    # step 3: nothing changed -> nothing uploaded, same arrays
+    before = {k: v for k, v in rb.last.items()}
+    rb.update(agents, 300.0)
+    assert all(rb.last[k] is before[k] for k in before)
+    # the snapshots of both calls still give their own rows (later calls never modify them)
+    for src, (p, _, _, _, (ls, us)) in zip(snaps, want_rows):
+        for i in (0, 3, 5, 15):
+            rp, rls, rus = src.rows(i)
+            np.testing.assert_array_equal(rp, p[i])
+            np.testing.assert_array_equal(rls, ls[i])
+            np.testing.assert_array_equal(rus, us[i])
+
+
+def test_resident_inputs_raise_the_reference_errors():
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    agents = _agents(cv, 4, 5)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    bad = [dict(a) for a in agents]
+    bad[2]["load"] = copy.deepcopy(bad[2]["load"])
+    bad[2]["load"].value = None
+    with pytest.raises(ValueError, match="empty"):
+        rb.update(bad, 0.0)
+
+    class Plain:
+        value, lb, ub = 150.0, -np.inf, np.inf
+
+    bad = [dict(a) for a in agents]
+    bad[1]["load"] = Plain()
+    with pytest.raises(TypeError, match="interpolationmethod"):
+        rb.update(bad, 0.0)
+
+
+@pytest.mark.gpu
+def test_gpu_resident_plugin_path_matches_host_marshalling():
+    """Three closed-loop steps through ``solve_batch`` (resident inputs, warm start in HBM)
+    against the host path (full re-marshalling with the previous optimum as guess,
+    ``solve_arrays``): identical solutions, statuses and per-agent Results."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    twin = bm.one_room(solver_options=bm.REFERENCE)[0]
+    agents = _agents(cv, 24, 11)
+    m = twin.problem.marshal
+    w_prev = None
+    rng = np.random.default_rng(2)
+    for step in range(3):
+        if step:
+            for c in agents:
+                c["T"].value += float(rng.normal(0.0, 0.3))
+            agents[7]["load"] = copy.deepcopy(agents[7]["load"])
+            agents[7]["load"].value = list(np.linspace(80.0, 220.0, len(twin.problem.nlp.par_groups["d"].grid)))
+        res = be.solve_batch(300.0 * step, agents)
+        p, lbw, ubw, w0, sampled = m.inputs(agents, 300.0 * step, w_prev, return_sampled_bounds=True)
+        ref = twin.solve_arrays(p, lbw, ubw, w0, result_bounds=sampled)
+        w_prev = ref.w.copy()
+        np.testing.assert_array_equal(res.stats.array["status"], ref.stats.array["status"])
+        np.testing.assert_array_equal(res.stats.array["iter_count"], ref.stats.array["iter_count"])
+        np.testing.assert_allclose(res.w, ref.w, rtol=1e-13, atol=1e-13)
+        for i in (0, 7, 23):
+            np.testing.assert_allclose(res[i].matrix, ref[i].matrix, rtol=1e-13, atol=1e-13, equal_nan=True)

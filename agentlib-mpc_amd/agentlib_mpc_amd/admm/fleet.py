@@ -49,7 +49,7 @@ CONSENSUS = "consensus"
 EXCHANGE = "exchange"
 NMOM = 5
 _STATUS_WORD = 13  # int32 index of mpcx_stats.status (6 doubles + iter_count)
-_FALLBACK_WORD = 15  # int32 index of mpcx_stats.n_linesearch_fallbacks
+_RESTO_WORD = 15  # int32 index of mpcx_stats.n_restorations
 
 
 @dataclasses.dataclass
@@ -433,7 +433,7 @@ class ADMMFleet:
                 x0[self.slot_rows[(ci, si)]] = s.initial[:, None]
         self.X[:R].copy_(t.as_tensor(x0, device=dev))
         self._ok_count = t.zeros(1, dtype=t.int64, device=dev)
-        self._fb_count = t.zeros(1, dtype=t.int64, device=dev)  # line-search fallbacks of the solves
+        self._fb_count = t.zeros(1, dtype=t.int64, device=dev)  # restoration-phase calls of the solves
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
@@ -497,7 +497,7 @@ class ADMMFleet:
             words = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)
             st = words[:, _STATUS_WORD]
             ok = (st == 0) | (st == 1)
-            fb = words[:, _FALLBACK_WORD]
+            fb = words[:, _RESTO_WORD]
             if self._masked:
                 ok &= c.ACTIVE != 0
                 fb = fb * (c.ACTIVE != 0)
@@ -691,7 +691,7 @@ class ADMMFleet:
         return {"iterations": it, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
                 "converged_solves": int(self._ok_count.item()), "block_iterations": iters,
                 "block_converged": conv_b, "block_records": block_records, "block_is_global": gblk.copy(),
-                "linesearch_fallbacks": int(self._fb_count.item())}
+                "restorations": int(self._fb_count.item())}
 
     def save_stats(self, path, start_time: float, records: Sequence[IterationRecord], first_iteration: int = 0):
         """Append one round's residual history to the coordinator's ``solve_stats_file``
@@ -740,7 +740,7 @@ class ADMMFleet:
         self.rounds += 1
         return {"iterations": max_iterations, "converged": None, "records": records, "wall_s": wall,
                 "converged_solves": int(self._ok_count.item()),
-                "linesearch_fallbacks": int(self._fb_count.item())}
+                "restorations": int(self._fb_count.item())}
 
     # ------------------------------------------------------------------ outputs
     def solutions(self, class_name: str) -> np.ndarray:

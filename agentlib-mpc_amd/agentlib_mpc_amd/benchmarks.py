@@ -390,11 +390,13 @@ def tz_cca(N=24, rho=1.0, zbar=294.15, lam=0.0, mDot_0=0.1, r_T_v=1.0, solver_op
 
 
 def fixture_mpc(N=5, T0=298.16, disturbance=270.0, u_prev=0.02, solver_options=TIGHT, model=None,
-                backend="mi355x"):
+                backend="mi355x", T_lb=-np.inf, T_ub=np.inf):
     """The reference's MPC module test (`tests/test_mpc.py:121-146`): backend ``casadi``
     with default discretization options (collocation, Legendre d=3), time step 900 s,
     horizon 5, on the test-suite model (`tests/fixtures/casadi_test_model.py`); the module
-    config declares state, control and disturbance only (parameters at model defaults)."""
+    config declares state, control and disturbance only (parameters at model defaults).
+    ``T_lb`` / ``T_ub``: bounds on the (unstable) state -- tight ones make the NLP infeasible,
+    the restoration-phase cases of the parity tests."""
     be = create_optimization_backend({
         "type": backend,
         "model": model or {"type": "agentlib_mpc_amd.models.examples.FixtureModel"},
@@ -403,7 +405,7 @@ def fixture_mpc(N=5, T0=298.16, disturbance=270.0, u_prev=0.02, solver_options=T
     })
     be.setup_optimization(VariableReference(states=["state"], controls=["myctrl"], inputs=["disturbance"],
                                             parameters=[], outputs=[]))
-    cv = {"state": V("state", T0), "myctrl": V("myctrl", u_prev, 0.0, 1.0),
+    cv = {"state": V("state", T0, T_lb, T_ub), "myctrl": V("myctrl", u_prev, 0.0, 1.0),
           "disturbance": V("disturbance", disturbance)}
     return be, cv
 
@@ -431,6 +433,22 @@ def fixture_admm(N=5, T0=298.16, disturbance=270.0, rho=10.0, zbar=298.16, lam=0
     return be, cv
 
 
+def cubic_room(N=4, T0=295.0, solver_options=TIGHT):
+    """Restoration-phase case (``models/examples.CubicRoom``): backend ``casadi``, collocation
+    Legendre d=2, N=4, ts=10; the cubic rows start at the middle of their variable's bounds,
+    in the basin of the local infeasibility minimum z = -1, so the filter line search fails
+    and the feasibility restoration phase moves them to the root z = 2.279."""
+    be = create_optimization_backend({
+        "type": "mi355x",
+        "model": {"type": "agentlib_mpc_amd.models.examples.CubicRoom"},
+        "discretization_options": {"collocation_order": 2, "prediction_horizon": N, "time_step": 10},
+        "solver": {"name": "ipopt", "options": solver_options},
+    })
+    be.setup_optimization(VariableReference(states=["T"], controls=["u"], inputs=[], parameters=[], outputs=[]))
+    cv = {"T": V("T", T0), "u": V("u", 0.0, 0.0, 1.0)}
+    return be, cv
+
+
 BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
     "one_room": one_room,
     "admm_room": admm_room,
@@ -442,6 +460,7 @@ BUILDERS: Dict[str, Callable[..., Tuple[object, dict]]] = {
     "tz_cca": tz_cca,
     "fixture_mpc": fixture_mpc,
     "fixture_admm": fixture_admm,
+    "cubic_room": cubic_room,
 }
 
 

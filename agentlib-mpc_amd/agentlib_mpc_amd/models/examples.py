@@ -438,3 +438,24 @@ class FixtureModel(CasadiModel):
         self.state.ode = self.myctrl + self.par * (self.state - self.disturbance) - self.par2
         self.myout.alg = self.state
         return (self.state - 290) ** 2
+
+
+class CubicRoomConfig(CasadiModelConfig):
+    """A zone temperature with an algebraic quantity on a cubic characteristic: the
+    restoration-phase parity case (the cold guess, the middle of the bounds, sits in the
+    basin of the characteristic's local infeasibility minimum)."""
+
+    states: List[CasadiState] = [CasadiState(name="T", value=295.0, unit="K"),
+                                 CasadiState(name="z", value=0.0, lb=-5.0, ub=2.6)]
+    inputs: List[CasadiInput] = [_inp("u", 0.0, unit="K/s")]
+
+
+class CubicRoom(CasadiModel):
+    """``T' = u - 0.01 (T - 290)``, ``z^3 - 3 z - 5 = 0`` at every point, cost ``(T - 290)^2``."""
+
+    config: CubicRoomConfig
+
+    def setup_system(self):
+        self.T.ode = self.u - 0.01 * (self.T - 290)
+        self.constraints = [(0, self.z ** 3 - 3 * self.z - 5, 0)]
+        return (self.T - 290) ** 2

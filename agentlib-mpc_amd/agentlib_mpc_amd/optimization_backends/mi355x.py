@@ -120,6 +120,7 @@ class MI355XBackend(OptimizationBackend):
 
     # -- setup (`core/casadi_backend.py:108-131`) --------------------------------
     def setup_optimization(self, var_ref):
+        self._resident = None  # a new structure: new resident inputs
         self.var_ref = var_ref
         self.system = self.system_type()
         self.system.initialize(model=self.model, var_ref=var_ref)
@@ -134,7 +135,8 @@ class MI355XBackend(OptimizationBackend):
         """Forget the remembered optima: the next solve starts cold (a new backend's first
         solve, `core/discretization.py:212-245`)."""
         self._remembered = None
-        self._resident = None
+        if getattr(self, "_resident", None) is not None:
+            self._resident.restart_cold()  # keep the device buffers, forget the optima
 
     def _native(self):
         prob = self.problem.native

@@ -216,6 +216,10 @@ class ResidentBatch:
         self.last = cur
         return cur
 
+    def restart_cold(self):
+        """Every agent's next guess is the cold-start guess (no remembered optimum)."""
+        self.cold_rows = np.arange(self.n)
+
     def solve(self):
         """Launch on the resident arrays (the solution replaces the guess in place); returns
         (w, raw stats) on the host."""
@@ -223,8 +227,9 @@ class ResidentBatch:
         self.native.solve(self.P, self.L, self.U, self.W, lam_g=self.lam_g, stats=self.ST)
         w = torch.empty((self.n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)
         w.copy_(self.W, non_blocking=True)
-        nan_rows = torch.isnan(self.W).any(dim=1).nonzero().flatten()  # synchronises
-        raw = self.ST.cpu().numpy()
-        bad = nan_rows.cpu().numpy()
+        raw = self.ST.cpu().numpy()  # synchronises (w is complete too: same stream)
+        w = w.numpy()
+        with np.errstate(invalid="ignore"):
+            bad = np.flatnonzero(np.isnan(w.sum(axis=1)))
         self.cold_rows = bad if bad.size else None
-        return w.numpy(), raw
+        return w, raw

@@ -34,6 +34,7 @@ STATUS_NAMES = {
     -2: "Restoration_Failed",
     -3: "Error_In_Step_Computation",
     -4: "Invalid_Number_Detected",
+    -5: "Infeasible_Problem_Detected",
 }
 
 
@@ -67,11 +68,13 @@ class Options(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in _OPT_DOUBLES] + [(n, ctypes.c_int32) for n in _OPT_INTS]
 
 
+_STATS_INTS = ("iter_count", "status", "n_inertia_corrections", "n_restorations", "n_factorizations", "n_trials",
+               "n_block_chain", "n_dense_stages", "n_soft_restorations", "n_restoration_iters")
+
+
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")] + \
-               [(n, ctypes.c_int32) for n in ("iter_count", "status", "n_inertia_corrections",
-                                              "n_linesearch_fallbacks", "n_factorizations", "n_trials",
-                                              "n_block_chain", "n_dense_stages")]
+               [(n, ctypes.c_int32) for n in _STATS_INTS]
 
 
 STATS_BYTES = ctypes.sizeof(Stats)
@@ -84,7 +87,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
 ]
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
-KERNEL_ABI = 5  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
+KERNEL_ABI = 6  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -296,8 +299,6 @@ class NativeProblem:
 
 
 _STATS_DOUBLES = ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")
-_STATS_INTS = ("iter_count", "status", "n_inertia_corrections", "n_linesearch_fallbacks", "n_factorizations",
-               "n_trials", "n_block_chain", "n_dense_stages")
 
 
 def stats_array(raw_bytes):
@@ -330,12 +331,10 @@ class StatsView:
         st = int(s["status"])
         d = {"obj": float(s["obj"]), "primal_inf": float(s["primal_inf"]), "dual_inf": float(s["dual_inf"]),
              "compl_inf": float(s["compl_inf"]), "mu": float(s["mu"]), "obj_scale": float(s["obj_scale"]),
-             "iter_count": int(s["iter_count"]), "status": st,
-             "return_status": STATUS_NAMES.get(st, str(st)), "success": st in (0, 1),
-             "n_inertia_corrections": int(s["n_inertia_corrections"]),
-             "n_linesearch_fallbacks": int(s["n_linesearch_fallbacks"]),
-             "n_factorizations": int(s["n_factorizations"]), "n_trials": int(s["n_trials"]),
-             "n_block_chain": int(s["n_block_chain"]), "n_dense_stages": int(s["n_dense_stages"])}
+             "status": st, "return_status": STATUS_NAMES.get(st, str(st)), "success": st in (0, 1)}
+        for k in _STATS_INTS:
+            if k != "status":
+                d[k] = int(s[k])
         d.update(self.extra)
         return d
 
@@ -351,17 +350,11 @@ def stats_to_dicts(raw_bytes) -> list:
     arr = (Stats * n).from_buffer_copy(buf)
     out = []
     for s in arr:
-        out.append({
-            "obj": s.obj, "primal_inf": s.primal_inf, "dual_inf": s.dual_inf,
-            "compl_inf": s.compl_inf, "mu": s.mu, "obj_scale": s.obj_scale,
-            "iter_count": s.iter_count, "status": s.status,
-            "return_status": STATUS_NAMES.get(s.status, str(s.status)),
-            "success": s.status in (0, 1),
-            "n_inertia_corrections": s.n_inertia_corrections,
-            "n_linesearch_fallbacks": s.n_linesearch_fallbacks,
-            "n_factorizations": s.n_factorizations,
-            "n_trials": s.n_trials,
-            "n_block_chain": s.n_block_chain,
-            "n_dense_stages": s.n_dense_stages,
-        })
+        d = {"obj": s.obj, "primal_inf": s.primal_inf, "dual_inf": s.dual_inf,
+             "compl_inf": s.compl_inf, "mu": s.mu, "obj_scale": s.obj_scale,
+             "status": s.status, "return_status": STATUS_NAMES.get(s.status, str(s.status)),
+             "success": s.status in (0, 1)}
+        for k in _STATS_INTS:
+            d[k] = getattr(s, k)
+        out.append(d)
     return out

@@ -5,7 +5,7 @@
 
 #include "mpcx.h"
 
-#define MPCX_KERNEL_ABI 5
+#define MPCX_KERNEL_ABI 6
 
 typedef struct mpcx_kernel_args {
   const double* p;

@@ -134,7 +134,29 @@ constexpr long O_DG = O_LP + (long)NCPT * N;       // [N][NLOC] diagonal terms (
 constexpr int SQ = NX > 0 ? NB : 1;   // the block-chain fallback exists only when stages are coupled
 constexpr int SQL = NX > 0 ? LDB : 1;
 constexpr long O_SQW = O_DG + (long)N * NLOC;  // [2][SQ*SQL] block-chain inverse scratch W, Y
-constexpr long WS_DOUBLES = O_SQW + (NX > 0 ? 2L * SQ * SQL : 0L);
+// feasibility restoration phase and soft restoration step (touched only on those paths)
+constexpr long O_RP = O_SQW + (NX > 0 ? 2L * SQ * SQL : 0L);  // [M] restoration p (c~ - p + n)
+constexpr long O_RN = O_RP + M;          // [M] restoration n
+constexpr long O_RZP = O_RN + M;         // [M] bound multipliers of p
+constexpr long O_RZN = O_RZP + M;        // [M] bound multipliers of n
+constexpr long O_RDP = O_RZN + M;        // [M] Newton step of p
+constexpr long O_RDN = O_RDP + M;        // [M] Newton step of n
+constexpr long O_XR = O_RDN + M;         // [NW] x at the start of restoration (x_R) / soft-step backup
+constexpr long O_SR = O_XR + NW;         // [M] slacks at the start of restoration / backup
+constexpr long O_LR = O_SR + M;          // [M] multipliers backup (soft step)
+constexpr long O_GVR = O_LR + M;         // [M] scaled constraint values backup (soft step)
+constexpr long O_ZL0 = O_GVR + M;        // [NW] original bound multipliers at the start of restoration
+constexpr long O_ZU0 = O_ZL0 + NW;
+constexpr long O_VL0 = O_ZU0 + NW;       // [M]
+constexpr long O_VU0 = O_VL0 + M;
+constexpr long O_FLT0 = O_VU0 + M;       // [2][MAXF] the original filter while restoring
+constexpr long WS_DOUBLES = O_FLT0 + 2L * MAXF;
+// IPOPT restoration constants (its defaults; not exposed as options)
+constexpr double RESTO_RHO = 1000.0;          // resto_penalty_parameter
+constexpr double RESTO_KAPPA = 0.9;           // required_infeasibility_reduction
+constexpr double SOFT_PD_FACTOR = 0.9999;     // soft_resto_pderror_reduction_factor
+constexpr int MAX_SOFT_ITERS = 10;            // max_soft_resto_iters
+constexpr double BOUND_MULT_RESET = 1000.0;   // bound_mult_reset_threshold
 
 using Args = mpcx_kernel_args;
 // kernel arguments read in place from the kernarg segment (address space 4: scalar
@@ -260,7 +282,7 @@ struct StepInfo {
 };
 
 struct Trial {
-  double f, theta, phi;
+  double f, theta, phi, fr;  // fr: restoration objective (restoration phase)
 };
 
 struct LSResult {
@@ -282,6 +304,11 @@ struct KState {
   LSResult ls;     // last line search
   double mu, tau, dw_last, fx, obj_scale, theta_max, theta_min, dw, dc, amin, barx;
   int nfilt, it, status, square, n_fact, n_ic, n_fallback, n_trials, n_chain, n_dense;
+  // soft restoration / feasibility restoration phase (IPOPT BacktrackingLineSearch,
+  // MinC_1NrmRestorationPhase): the original problem's state while restoring
+  Acceptable acc0;
+  double fo, zeta, prox, mu0, tau0, dw_last0, theta_max0, theta_min0, theta_start;
+  int resto, soft, soft_count, lsmode, nfilt0, square_r, n_soft, n_resto_it;
 };
 
 #ifndef MPCX_NETX
@@ -453,6 +480,21 @@ struct Agent {
   __device__ gdbl* lp(int k) const { return ws + O_LP + k; }  // entry c of stage k at lp(k)[c * N]
   __device__ gdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
   __device__ gdbl* sqw() const { return ws + O_SQW; }
+  __device__ gdbl* rp() const { return ws + O_RP; }
+  __device__ gdbl* rn() const { return ws + O_RN; }
+  __device__ gdbl* rzp() const { return ws + O_RZP; }
+  __device__ gdbl* rzn() const { return ws + O_RZN; }
+  __device__ gdbl* rdp() const { return ws + O_RDP; }
+  __device__ gdbl* rdn() const { return ws + O_RDN; }
+  __device__ gdbl* xr() const { return ws + O_XR; }
+  __device__ gdbl* sr() const { return ws + O_SR; }
+  __device__ gdbl* lr() const { return ws + O_LR; }
+  __device__ gdbl* gvr() const { return ws + O_GVR; }
+  __device__ gdbl* zl0() const { return ws + O_ZL0; }
+  __device__ gdbl* zu0() const { return ws + O_ZU0; }
+  __device__ gdbl* vl0() const { return ws + O_VL0; }
+  __device__ gdbl* vu0() const { return ws + O_VU0; }
+  __device__ gdbl* flt0() const { return ws + O_FLT0; }
 };
 
 // constraint classes: 0 equality, 1 inequality with a finite bound, 2 free
@@ -2101,11 +2143,13 @@ __device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
       amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;
     if (!(amin > 0.0)) amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;  // NaN guard
     K.amin = amin;
-    K.ls.alpha = K.st.amax;
+    // soft restoration step (K.lsmode == 1): ONE trial at the full fraction-to-the-boundary
+    // step of primal and dual variables, tested at alpha = 0 (no switching condition)
+    K.ls.alpha = K.lsmode ? fmin(K.st.amax, K.st.az) : K.st.amax;
     K.ls.accepted = 0;
     K.ls.ftype = 0;
     K.ls.trials = 0;
-    K.ls.tr = Trial{0.0, 0.0, 0.0};
+    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};
   }
 #pragma unroll 1
   for (int ls = 0; ls < 64; ++ls) {
@@ -2167,7 +2211,8 @@ __device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
       if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
     bool ftype = false;
     if (okt) {
-      const bool switching = gphid < 0 && alpha * pow_ool(-gphid, ka.opt.s_phi) > ka.opt.delta * pow_ool(theta, ka.opt.s_theta);
+      const bool switching = !K.lsmode && gphid < 0 &&
+                             alpha * pow_ool(-gphid, ka.opt.s_phi) > ka.opt.delta * pow_ool(theta, ka.opt.s_theta);
       if (theta <= K.theta_min && switching) {
         okt = tr.phi <= phi + ka.opt.eta_phi * alpha * gphid;
         ftype = true;
@@ -2178,7 +2223,7 @@ __device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
     }
     K.ls.ftype = ftype;
     if (okt) { K.ls.accepted = 1; break; }
-    if (alpha * 0.5 < K.amin) break;
+    if (K.lsmode || alpha * 0.5 < K.amin) break;
     K.ls.alpha = alpha * 0.5;
   }
   wsync();
@@ -2405,6 +2450,774 @@ __device__ __noinline__ int iter_head(const Agent a, KArgs* argp) {
   return 0;
 }
 
+
+// ===========================================================================
+// Soft restoration step and feasibility restoration phase (IPOPT's answer to a failed
+// filter line search; oracle/ipm.py restates both step for step).
+//
+// Soft restoration (BacktrackingLineSearch::TrySoftRestoStep): the full fraction-to-the-
+// boundary step with one step size for primal and dual variables, accepted if the original
+// filter criterion holds at alpha = 0 or the primal-dual system error drops by 0.9999;
+// a step accepted only by the error test keeps the solver in the soft phase (at most 10
+// iterations), whose steps are tried the same way without backtracking.
+//
+// Restoration phase (MinC_1NrmRestorationPhase): a second interior-point run on
+//   min rho sum(p + n) + zeta(mu)/2 ||D_R (x - x_R)||^2  s.t.  c~(x) - p + n = c~_L / in [d~_L, d~_U]
+// (rho = 1000, zeta = sqrt(mu), D_R = diag(1 / max(1, |x_R|))), with p, n >= 0 eliminated
+// from every KKT system: the stage factorisation sees the same structure, each constraint
+// row's dual diagonal grows by 1/(Sigma_p + dw) + 1/(Sigma_n + dw) and its rhs by the p / n
+// residuals.  It returns to the original problem once the original constraint violation has
+// dropped by 0.9 and the point is acceptable to the original filter (RestoConvergenceCheck);
+// bound multipliers then take one Newton step for complementarity over the whole primal
+// change (reset to 1 above 1000), constraint multipliers restart at zero.  A restoration
+// that converges on its own terms is a point of local infeasibility.
+// ===========================================================================
+
+__device__ __forceinline__ double dr2_of(double xr) {
+  const double d = 1.0 / fmax(1.0, fabs(xr));
+  return d * d;
+}
+
+// IPOPT primal_dual_system_error at the current point (1-norms of the dual infeasibility,
+// the constraint violation and the mu-complementarity; the common normalisation cancels in
+// the soft-restoration ratio), from that point's derivative arrays
+__device__ __noinline__ double pd_error(const Agent a, double mu, double obj_scale) {
+  const int lane = a.lane;
+  double e = 0.0;
+  for (int i = NX + lane; i < NW; i += WAVE) {
+    const double lo = a.xL()[i], hi = a.xU()[i];
+    if (lo == hi) continue;
+    const double xv = a.x()[i], zl = a.zL()[i], zu = a.zU()[i];
+    e += fabs(obj_scale * acc_grad(a, i) + acc_jtl(a, i) - zl + zu);
+    if (isfin(lo)) e += fabs((xv - lo) * zl - mu);
+    if (isfin(hi)) e += fabs((hi - xv) * zu - mu);
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    const double lbv = a.lb()[c], ubv = a.ub()[c], slo = a.sL()[c], sup = a.sU()[c];
+    const int cl = cls_of(lbv, ubv, slo, sup);
+    const double gvv = a.gv()[c], sv = a.s()[c];
+    e += fabs(cl == 0 ? gvv - a.gs()[c] * lbv : gvv - sv);
+    if (cl == 1) {
+      const double vl = a.vL()[c], vu = a.vU()[c];
+      e += fabs(-a.lam()[c] - vl + vu);
+      if (isfin(slo)) e += fabs((sv - slo) * vl - mu);
+      if (isfin(sup)) e += fabs((sup - sv) * vu - mu);
+    }
+  }
+  return wsum(e);
+}
+
+// iterate <-> backup (x, s, lambda, z, v, scaled g): the soft step's tentative trial
+__device__ __noinline__ void iterate_copy(const Agent a, int to_backup) {
+  const int lane = a.lane;
+  for (int i = lane; i < NW; i += WAVE) {
+    if (to_backup) { a.xr()[i] = a.x()[i]; a.zl0()[i] = a.zL()[i]; a.zu0()[i] = a.zU()[i]; }
+    else { a.x()[i] = a.xr()[i]; a.zL()[i] = a.zl0()[i]; a.zU()[i] = a.zu0()[i]; }
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    if (to_backup) {
+      a.sr()[c] = a.s()[c]; a.lr()[c] = a.lam()[c]; a.gvr()[c] = a.gv()[c];
+      a.vl0()[c] = a.vL()[c]; a.vu0()[c] = a.vU()[c];
+    } else {
+      a.s()[c] = a.sr()[c]; a.lam()[c] = a.lr()[c]; a.gv()[c] = a.gvr()[c];
+      a.vL()[c] = a.vl0()[c]; a.vU()[c] = a.vu0()[c];
+    }
+  }
+  sync();
+}
+
+// the soft trial (xt, gt in LDS) with the same step size alpha for every variable,
+// bound multipliers NOT yet corrected (IPOPT corrects them after acceptance)
+__device__ __noinline__ void soft_apply(const Agent a, double mu, double alpha) {
+  const int lane = a.lane;
+  for (int i = NX + lane; i < NW; i += WAVE) {
+    const double lo = a.xL()[i], hi = a.xU()[i];
+    if (lo == hi) continue;
+    const double xold = a.x()[i], d = a.dx()[i];
+    a.x()[i] = gL.u.t.xt[i];
+    if (isfin(lo)) { const double zl = a.zL()[i], sl0 = xold - lo; a.zL()[i] = zl + alpha * (mu / sl0 - zl - (zl / sl0) * d); }
+    if (isfin(hi)) { const double zu = a.zU()[i], su0 = hi - xold; a.zU()[i] = zu + alpha * (mu / su0 - zu + (zu / su0) * d); }
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    const double lbv = a.lb()[c], ubv = a.ub()[c], slo = a.sL()[c], sup = a.sU()[c];
+    const double sold = a.s()[c], dsv = a.ds()[c];
+    a.lam()[c] += alpha * a.dl()[c];
+    a.gv()[c] = gL.u.t.gt[c];
+    a.s()[c] = sold + alpha * dsv;
+    if (cls_of(lbv, ubv, slo, sup) != 1) continue;
+    if (isfin(slo)) { const double vl = a.vL()[c], s0 = sold - slo; a.vL()[c] = vl + alpha * (mu / s0 - vl - (vl / s0) * dsv); }
+    if (isfin(sup)) { const double vu = a.vU()[c], s0 = sup - sold; a.vU()[c] = vu + alpha * (mu / s0 - vu + (vu / s0) * dsv); }
+  }
+  sync();
+}
+
+// kappa_sigma correction of the bound multipliers at the current point
+__device__ __noinline__ void sigma_clip(const Agent a, double kappa_sigma, double mu) {
+  const int lane = a.lane;
+  for (int i = NX + lane; i < NW; i += WAVE) {
+    const double lo = a.xL()[i], hi = a.xU()[i], xv = a.x()[i];
+    if (lo == hi) continue;
+    if (isfin(lo)) { const double s_l = xv - lo; a.zL()[i] = fmax(fmin(a.zL()[i], kappa_sigma * mu / s_l), mu / (kappa_sigma * s_l)); }
+    if (isfin(hi)) { const double s_u = hi - xv; a.zU()[i] = fmax(fmin(a.zU()[i], kappa_sigma * mu / s_u), mu / (kappa_sigma * s_u)); }
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    const double slo = a.sL()[c], sup = a.sU()[c], sv = a.s()[c];
+    if (cls_of(a.lb()[c], a.ub()[c], slo, sup) != 1) continue;
+    if (isfin(slo)) { const double s_l = sv - slo; a.vL()[c] = fmax(fmin(a.vL()[c], kappa_sigma * mu / s_l), mu / (kappa_sigma * s_l)); }
+    if (isfin(sup)) { const double s_u = sup - sv; a.vU()[c] = fmax(fmin(a.vU()[c], kappa_sigma * mu / s_u), mu / (kappa_sigma * s_u)); }
+  }
+  sync();
+}
+
+// TrySoftRestoStep.  0: rejected (iterate unchanged); 1: accepted by the original filter
+// criterion (the caller takes the trial as a regular step); 2: accepted by the
+// primal-dual error test (trial applied, multipliers corrected, derivatives evaluated)
+__device__ __noinline__ int soft_try(const Agent a, KArgs* argp) {
+  KState& K = gL.ks;
+  K.lsmode = 1;
+  line_search(a, argp);
+  K.lsmode = 0;
+  K.n_trials += K.ls.trials;
+  if (K.ls.accepted) return 1;
+  const Trial tr = K.ls.tr;
+  if (!(isfin(tr.theta) && isfin(tr.phi))) return 0;
+  const double pd0 = pd_error(a, K.mu, K.obj_scale);
+  iterate_copy(a, 1);
+  soft_apply(a, K.mu, K.ls.alpha);
+  eval_gj_lds(a);
+  sync();
+  const double pd1 = pd_error(a, K.mu, K.obj_scale);
+  if (pd1 <= SOFT_PD_FACTOR * pd0) {
+    sigma_clip(a, (*argp).opt.kappa_sigma, K.mu);
+    return 2;
+  }
+  iterate_copy(a, 0);
+  eval_gj_ws(a, a.x(), gL.want_sdh);
+  sync();
+  return 0;
+}
+
+// ---- restoration phase ----------------------------------------------------------------
+
+// start: called at the iterate whose line search (and soft step) failed, with K.st of it
+__device__ __noinline__ void resto_start(const Agent a, KArgs* argp) {
+  KArgs& ka = *argp;
+  KState& K = gL.ks;
+  const int lane = a.lane;
+  {  // FilterLSAcceptor::PrepareRestoPhaseStart: the current point enters the original filter
+    const double theta = K.st.theta, phi = K.fx - K.mu * K.st.barrier;
+    int nfilt = K.nfilt;
+    if (nfilt == MAXF) {
+      if (lane == 0)
+        for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
+      nfilt--;
+    }
+    if (lane == 0) { gL.fth[nfilt] = (1.0 - ka.opt.gamma_theta) * theta; gL.fph[nfilt] = phi - ka.opt.gamma_phi * theta; }
+    nfilt++;
+    wsync();
+    for (int j = lane; j < nfilt; j += WAVE) { a.flt0()[j] = gL.fth[j]; a.flt0()[MAXF + j] = gL.fph[j]; }
+    K.nfilt0 = nfilt;
+    K.theta_start = theta;
+  }
+  K.theta_max0 = K.theta_max; K.theta_min0 = K.theta_min;
+  K.mu0 = K.mu; K.tau0 = K.tau; K.dw_last0 = K.dw_last; K.acc0 = K.acc;
+  K.fo = K.fx;
+  double cmax = 0.0;
+  for (int c = lane; c < M; c += WAVE) {
+    const int cl = cls_of(a.lb()[c], a.ub()[c], a.sL()[c], a.sU()[c]);
+    cmax = fmax(cmax, fabs(cl == 0 ? a.gv()[c] - a.gs()[c] * a.lb()[c] : a.gv()[c] - a.s()[c]));
+  }
+  const double mu_r = fmax(K.mu, wmax(cmax));
+  double pn = 0.0, th = 0.0;
+  int nfree = 0, neq = 0;
+  for (int i = lane; i < NW; i += WAVE) {
+    a.xr()[i] = a.x()[i];
+    const double zl = a.zL()[i], zu = a.zU()[i];
+    a.zl0()[i] = zl; a.zu0()[i] = zu;
+    a.zL()[i] = fmin(zl, RESTO_RHO);
+    a.zU()[i] = fmin(zu, RESTO_RHO);
+    nfree += (i >= NX && a.xL()[i] != a.xU()[i]) ? 1 : 0;
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    const int cl = cls_of(a.lb()[c], a.ub()[c], a.sL()[c], a.sU()[c]);
+    const double cv = cl == 0 ? a.gv()[c] - a.gs()[c] * a.lb()[c] : a.gv()[c] - a.s()[c];
+    // p, n solving the restoration problem's complementarity at its start (W&B 2006, eq. 33)
+    const double q = (mu_r - RESTO_RHO * cv) / (2.0 * RESTO_RHO);
+    const double nv = q + sqrt(q * q + mu_r * cv / (2.0 * RESTO_RHO));
+    const double pv = cv + nv;
+    a.rp()[c] = pv; a.rn()[c] = nv;
+    a.rzp()[c] = mu_r / pv; a.rzn()[c] = mu_r / nv;
+    pn += pv + nv;
+    th += fabs(cv - pv + nv);
+    a.sr()[c] = a.s()[c];
+    const double vl = a.vL()[c], vu = a.vU()[c];
+    a.vl0()[c] = vl; a.vu0()[c] = vu;
+    a.vL()[c] = fmin(vl, RESTO_RHO);
+    a.vU()[c] = fmin(vu, RESTO_RHO);
+    a.lam()[c] = 0.0;
+    neq += cl == 0 ? 1 : 0;
+  }
+  pn = wsum(pn);
+  th = wsum(th);
+  K.square_r = (wsumi(nfree) + 2 * M) == wsumi(neq);
+  sync();
+  eval_gj_ws(a, a.x(), gL.want_sdh);  // (J~^T lambda) with lambda = 0
+  sync();
+  K.mu = mu_r;
+  K.tau = fmax(ka.opt.tau_min, 1.0 - mu_r);
+  K.zeta = sqrt(mu_r);
+  K.fx = RESTO_RHO * pn;  // x = x_R: no proximity term yet
+  K.theta_max = ka.opt.theta_max_fact * fmax(1.0, th);
+  K.theta_min = ka.opt.theta_min_fact * fmax(1.0, th);
+  K.nfilt = 0;
+  K.dw_last = 0.0;
+  K.acc = Acceptable{-1e50, -1e50, -1, 0};
+  K.resto = 1;
+  K.soft = 0;
+  K.soft_count = 0;
+  K.n_fallback += 1;
+}
+
+// back to the original problem (the restoration iterate passed the return test)
+__device__ __noinline__ void resto_return(const Agent a, KArgs* argp) {
+  KState& K = gL.ks;
+  const int lane = a.lane;
+  const double mu0 = K.mu0, tau0 = K.tau0;
+  // one Newton step for complementarity over the whole primal change, fraction to the boundary
+  double ad = 1.0;
+  for (int i = NX + lane; i < NW; i += WAVE) {
+    const double lo = a.xL()[i], hi = a.xU()[i];
+    if (lo == hi) continue;
+    const double xv = a.x()[i], x0 = a.xr()[i];
+    if (isfin(lo)) { const double z0 = a.zl0()[i], dz = (mu0 - z0 * (xv - lo)) / (x0 - lo); if (dz < 0) ad = fmin(ad, -tau0 * z0 / dz); }
+    if (isfin(hi)) { const double z0 = a.zu0()[i], dz = (mu0 - z0 * (hi - xv)) / (hi - x0); if (dz < 0) ad = fmin(ad, -tau0 * z0 / dz); }
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    const double slo = a.sL()[c], sup = a.sU()[c];
+    if (cls_of(a.lb()[c], a.ub()[c], slo, sup) != 1) continue;
+    const double sv = a.s()[c], s0 = a.sr()[c];
+    if (isfin(slo)) { const double v0 = a.vl0()[c], dv = (mu0 - v0 * (sv - slo)) / (s0 - slo); if (dv < 0) ad = fmin(ad, -tau0 * v0 / dv); }
+    if (isfin(sup)) { const double v0 = a.vu0()[c], dv = (mu0 - v0 * (sup - sv)) / (sup - s0); if (dv < 0) ad = fmin(ad, -tau0 * v0 / dv); }
+  }
+  ad = wmin(ad);
+  double zmax = 0.0;
+  for (int i = NX + lane; i < NW; i += WAVE) {
+    const double lo = a.xL()[i], hi = a.xU()[i];
+    if (lo == hi) continue;
+    const double xv = a.x()[i], x0 = a.xr()[i];
+    if (isfin(lo)) { const double z0 = a.zl0()[i], z = z0 + ad * (mu0 - z0 * (xv - lo)) / (x0 - lo); a.zL()[i] = z; zmax = fmax(zmax, fabs(z)); }
+    if (isfin(hi)) { const double z0 = a.zu0()[i], z = z0 + ad * (mu0 - z0 * (hi - xv)) / (hi - x0); a.zU()[i] = z; zmax = fmax(zmax, fabs(z)); }
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    const double slo = a.sL()[c], sup = a.sU()[c];
+    a.lam()[c] = 0.0;  // constr_mult_reset_threshold = 0: constraint multipliers restart at zero
+    if (cls_of(a.lb()[c], a.ub()[c], slo, sup) != 1) continue;
+    const double sv = a.s()[c], s0 = a.sr()[c];
+    if (isfin(slo)) { const double v0 = a.vl0()[c], v = v0 + ad * (mu0 - v0 * (sv - slo)) / (s0 - slo); a.vL()[c] = v; zmax = fmax(zmax, fabs(v)); }
+    if (isfin(sup)) { const double v0 = a.vu0()[c], v = v0 + ad * (mu0 - v0 * (sup - sv)) / (sup - s0); a.vU()[c] = v; zmax = fmax(zmax, fabs(v)); }
+  }
+  zmax = wmax(zmax);
+  if (zmax > BOUND_MULT_RESET) {
+    for (int i = NX + lane; i < NW; i += WAVE) {
+      const double lo = a.xL()[i], hi = a.xU()[i];
+      if (lo == hi) continue;
+      a.zL()[i] = isfin(lo) ? 1.0 : 0.0;
+      a.zU()[i] = isfin(hi) ? 1.0 : 0.0;
+    }
+    for (int c = lane; c < M; c += WAVE) {
+      const double slo = a.sL()[c], sup = a.sU()[c];
+      if (cls_of(a.lb()[c], a.ub()[c], slo, sup) != 1) continue;
+      a.vL()[c] = isfin(slo) ? 1.0 : 0.0;
+      a.vU()[c] = isfin(sup) ? 1.0 : 0.0;
+    }
+  }
+  const int nfilt = K.nfilt0;
+  for (int j = lane; j < nfilt; j += WAVE) { gL.fth[j] = a.flt0()[j]; gL.fph[j] = a.flt0()[MAXF + j]; }
+  sync();
+  eval_gj_ws(a, a.x(), gL.want_sdh);  // (J~^T lambda) with lambda = 0
+  sync();
+  K.nfilt = nfilt;
+  K.mu = mu0; K.tau = tau0; K.dw_last = K.dw_last0; K.acc = K.acc0;
+  K.theta_max = K.theta_max0; K.theta_min = K.theta_min0;
+  K.fx = K.fo;
+  K.resto = 0;
+  K.soft = 0;
+  K.soft_count = 0;
+}
+
+// Top of a restoration iteration: the return test, then the restoration problem's
+// optimality error, termination tests, barrier update (zeta follows mu), Newton rhs and
+// diagonal terms.  Returns 0 (rhs written), 1 (stop, K.status set), 2 (return test passed)
+__device__ __noinline__ int iter_head_resto(const Agent a, KArgs* argp) {
+  KArgs& ka = *argp;
+  KState& K = gL.ks;
+  const int lane = a.lane;
+  // primal rows: r = -(jt + zeta gdr) + mu pr1, diagonal psx + zeta dr2; dual residual of
+  // x: zeta gdr + hj (zeta-dependent, kept per slot for the barrier loop)
+  double gdr[VS], hj[VS], jtv[VS], pr1[VS], psx[VS], d2[VS];
+  double dq0[CS], dq1[CS], ddg[CS];
+  double dmax_r = 0.0, pmax = 0.0, vmax = 0.0, pmx = -INFINITY, pmn = INFINITY, lsum = 0.0, zsum = 0.0;
+  double barx0 = 0.0, bars0 = 0.0, tho = 0.0, spn = 0.0, sd = 0.0;
+  int nz = 0;
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    const int ii = (i >= NX && i < NW) ? i : NX;
+    const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
+    const double xrv = a.xr()[ii], jt = acc_jtl(a, ii);
+    const bool on = i >= NX && i < NW && lo != hi;
+    const double dr2 = dr2_of(xrv);
+    gdr[sl] = on ? dr2 * (xv - xrv) : 0.0;
+    hj[sl] = on ? jt - zl + zu : 0.0;
+    jtv[sl] = jt;
+    d2[sl] = on ? dr2 : 0.0;
+    pr1[sl] = on ? (isfin(lo) ? 1.0 / (xv - lo) : 0.0) - (isfin(hi) ? 1.0 / (hi - xv) : 0.0) : 0.0;
+    psx[sl] = sigma_x_v(xv, lo, hi, zl, zu);
+    if (on) {
+      sd += dr2 * (xv - xrv) * (xv - xrv);
+      if (isfin(lo)) { const double pr = (xv - lo) * zl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zl); nz++; barx0 += log(xv - lo); }
+      if (isfin(hi)) { const double pr = (hi - xv) * zu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zu); nz++; barx0 += log(hi - xv); }
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const int cc = c < M ? c : 0;
+    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double gsc = a.gs()[cc], gvv = a.gv()[cc], sv = a.s()[cc], lm = a.lam()[cc];
+    const double vl = a.vL()[cc], vu = a.vU()[cc];
+    const double pv = a.rp()[cc], nv = a.rn()[cc], zp = a.rzp()[cc], zn = a.rzn()[cc];
+    const int cl = cls_of(lbv, ubv, slo, sup);
+    const double co = (cl == 0) ? gvv - gsc * lbv : gvv - sv;   // original residual
+    const double cr = co - pv + nv;                               // restoration residual
+    const double sg = sigma_s_v(sv, slo, sup, vl, vu);
+    const double sgp = zp / pv, sgn = zn / nv;
+    dq0[sl] = -cr + ((cl == 1) ? lm / sg : 0.0) + (lm - RESTO_RHO) / sgp + (RESTO_RHO + lm) / sgn;
+    dq1[sl] = ((cl == 1) ? ((isfin(sup) ? 1.0 / (sup - sv) : 0.0) - (isfin(slo) ? 1.0 / (sv - slo) : 0.0)) / sg : 0.0)
+              - (1.0 / pv) / sgp + (1.0 / nv) / sgn;
+    ddg[sl] = -(dual_diag_v(cl, sg, KKTDiag{0.0, 0.0, NEWTON}) + 1.0 / sgp + 1.0 / sgn);
+    if (c < M) {
+      tho += fabs(co);
+      pmax = fmax(pmax, fabs(cr));
+      dmax_r = fmax(dmax_r, fmax(fabs(RESTO_RHO - lm - zp), fabs(RESTO_RHO + lm - zn)));
+      { const double pr = pv * zp; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); }
+      { const double pr = nv * zn; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); }
+      zsum += fabs(zp) + fabs(zn);
+      nz += 2;
+      spn += pv + nv;
+      const double gr = gvv - pv + nv;
+      if (cl == 0) {
+        vmax = fmax(vmax, fabs(cr));
+      } else if (cl == 1) {
+        dmax_r = fmax(dmax_r, fabs(-lm - vl + vu));
+        vmax = fmax(vmax, fmax(0.0, fmax(slo - gr, gr - sup)));
+        if (isfin(slo)) { const double pr = (sv - slo) * vl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vl); nz++; bars0 += log(sv - slo); }
+        if (isfin(sup)) { const double pr = (sup - sv) * vu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(vu); nz++; bars0 += log(sup - sv); }
+      }
+      lsum += fabs(lm);
+    }
+  }
+  // ---- return test (RestoConvergenceCheck) ----
+  tho = wsum(tho);
+  {
+    const double bar = wsum(barx0) + wsum(bars0);
+    bool ret = tho <= RESTO_KAPPA * K.theta_start;
+    if (ret) {
+      const double phio = K.fo - K.mu0 * bar;
+      ret = tho <= K.theta_max0;
+      const int nf = K.nfilt0;
+      for (int j = 0; j < nf && ret; ++j)
+        if (tho >= a.flt0()[j] && phio >= a.flt0()[MAXF + j]) ret = false;
+    }
+    if (ret) return 2;
+  }
+  OptErr e;
+  dmax_r = wmax(dmax_r);
+  auto dual_x = [&](double zeta) {
+    double m = 0.0;
+#pragma unroll
+    for (int sl = 0; sl < VS; ++sl) m = fmax(m, fabs(zeta * gdr[sl] + hj[sl]));
+    return fmax(dmax_r, wmax(m));
+  };
+  e.dual = dual_x(K.zeta); e.dual_u = e.dual;
+  e.primal = wmax(pmax); e.viol_u = wmax(vmax);
+  e.pmx = wmax(pmx); e.pmn = wmin(pmn);
+  lsum = wsum(lsum); zsum = wsum(zsum); nz = wsumi(nz);
+  spn = wsum(spn); sd = wsum(sd);
+  e.ncompl = nz;
+  e.s_d = fmax(100.0, (lsum + zsum) / fmax(1.0, (double)(M + nz))) / 100.0;
+  e.s_c = nz > 0 ? fmax(100.0, zsum / (double)nz) / 100.0 : 1.0;
+  K.e0 = e;
+  K.fx = RESTO_RHO * spn + 0.5 * K.zeta * sd;
+  {
+    const double err0 = e.err_at(0.0);
+    if (!(err0 == err0) || !(K.fx == K.fx)) { K.status = MPCX_INVALID_NUMBER; return 1; }
+    if (err0 <= ka.opt.tol && e.viol_u <= ka.opt.constr_viol_tol &&
+        (K.square_r || (e.dual_u <= ka.opt.dual_inf_tol && e.compl_at(0.0) <= ka.opt.compl_inf_tol))) {
+      K.status = MPCX_INFEASIBLE;
+      return 1;
+    }
+    Acceptable acc = K.acc;
+    if (ka.opt.acceptable_iter > 0 && current_is_acceptable(acc, e, err0, K.fx, K.it, 1.0, K.square_r, ka.opt)) {
+      acc.count++;
+      K.acc = acc;
+      if (acc.count >= ka.opt.acceptable_iter) { K.status = MPCX_INFEASIBLE; return 1; }
+    } else {
+      acc.count = 0;
+      K.acc = acc;
+    }
+    if (K.it >= ka.opt.max_iter) return 1;
+  }
+  // ---- barrier update; the proximity weight follows mu ----
+#pragma unroll 1
+  for (int mu_up = 0; mu_up < 64; ++mu_up) {
+    const double mu = K.mu;
+    if (e.err_at(mu) > ka.opt.kappa_eps * mu || mu <= ka.opt.mu_min) break;
+    const double new_mu = fmax(fmax(fmin(ka.opt.tol, ka.opt.compl_inf_tol) / (ka.opt.kappa_eps + 1.0), ka.opt.mu_min),
+                               fmin(ka.opt.kappa_mu * mu, ka.opt.theta_mu == 1.5 ? mu * sqrt(mu) : pow_ool(mu, ka.opt.theta_mu)));
+    if (new_mu == mu) break;
+    K.mu = new_mu;
+    K.tau = fmax(ka.opt.tau_min, 1.0 - new_mu);
+    K.nfilt = 0;
+    K.zeta = sqrt(new_mu);
+    K.fx = RESTO_RHO * spn + 0.5 * K.zeta * sd;
+    e.dual = dual_x(K.zeta);
+  }
+  const double mu = K.mu, zeta = K.zeta;
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    if (i >= NX && i < NW) {
+      const bool on = a.xL()[i] != a.xU()[i];
+      const double r = on ? -(jtv[sl] + zeta * gdr[sl]) + mu * pr1[sl] : 0.0;
+      const int b = (i - NX) / NP, off = (i - NX) % NP;
+      const int li = off < NV ? off : LX1 + off - NV;
+      a.rhs(b)[off] = r;
+      a.dg(b)[li] = psx[sl] + zeta * d2[sl];
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    if (c < M) {
+      a.rhs(c / NG)[NP + c % NG] = dq0[sl] - mu * dq1[sl];
+      a.dg(c / NG)[crow(c % NG)] = ddg[sl];
+    }
+  }
+  sync();
+  return 0;
+}
+
+// dual rows of the restoration rhs with the inertia-correction terms (delta_w, delta_c)
+__device__ __noinline__ void rhs_dual_resto(const Agent a, double mu, double dw, double dc) {
+  const int lane = a.lane;
+  for (int c = lane; c < M; c += WAVE) {
+    const double lbv = a.lb()[c], ubv = a.ub()[c], slo = a.sL()[c], sup = a.sU()[c];
+    const double gvv = a.gv()[c], gsc = a.gs()[c], sv = a.s()[c], lm = a.lam()[c];
+    const double vl = a.vL()[c], vu = a.vU()[c];
+    const double pv = a.rp()[c], nv = a.rn()[c], sgp = a.rzp()[c] / pv + dw, sgn = a.rzn()[c] / nv + dw;
+    const int cl = cls_of(lbv, ubv, slo, sup);
+    const double sg = sigma_s_v(sv, slo, sup, vl, vu);
+    double rr = -((cl == 0 ? gvv - gsc * lbv : gvv - sv) - pv + nv);
+    if (cl == 1) {
+      double gphis = 0.0;
+      if (isfin(slo)) gphis -= mu / (sv - slo);
+      if (isfin(sup)) gphis += mu / (sup - sv);
+      rr -= (gphis - lm) / (sg + dw);
+    }
+    rr += -(RESTO_RHO - mu / pv - lm) / sgp + (RESTO_RHO - mu / nv + lm) / sgn;
+    a.rhs(c / NG)[NP + c % NG] = rr;
+    a.dg(c / NG)[crow(c % NG)] = -(dual_diag_v(cl, sg, KKTDiag{dw, dc, NEWTON}) + 1.0 / sgp + 1.0 / sgn);
+  }
+  sync();
+}
+
+// restoration step from the Newton solution: x, s, lambda as in recover_step, p and n
+// eliminated (dp = (dlam - r_p)/(Sigma_p + dw), dn = (-dlam - r_n)/(Sigma_n + dw))
+__device__ __noinline__ StepInfo recover_step_resto(const Agent a, double mu, double tau, double dw) {
+  KState& K = gL.ks;
+  const int lane = a.lane;
+  const double zeta = K.zeta;
+  double amax = 1.0, az = 1.0, gphid = 0.0, theta = 0.0, bar = 0.0;
+  for (int i = NX + lane; i < NW; i += WAVE) {
+    const double lo = a.xL()[i], hi = a.xU()[i];
+    const double sv = gL.u.sol[((i - NX) / NP) * NB + (i - NX) % NP];
+    const bool free_ = lo != hi;
+    const double d = free_ ? sv : 0.0;
+    a.dx()[i] = d;
+    if (!free_) continue;
+    const double xv = a.x()[i], zl = a.zL()[i], zu = a.zU()[i];
+    double gphi = zeta * dr2_of(a.xr()[i]) * (xv - a.xr()[i]);
+    if (isfin(lo)) {
+      const double s_l = xv - lo;
+      gphi -= mu / s_l;
+      if (d < 0) amax = fmin(amax, -tau * s_l / d);
+      const double dz = mu / s_l - zl - (zl / s_l) * d;
+      if (dz < 0) az = fmin(az, -tau * zl / dz);
+      bar += log(s_l);
+    }
+    if (isfin(hi)) {
+      const double s_u = hi - xv;
+      gphi += mu / s_u;
+      if (d > 0) amax = fmin(amax, tau * s_u / d);
+      const double dz = mu / s_u - zu + (zu / s_u) * d;
+      if (dz < 0) az = fmin(az, -tau * zu / dz);
+      bar += log(s_u);
+    }
+    gphid += gphi * d;
+  }
+  for (int i = lane; i < NX; i += WAVE) a.dx()[i] = 0.0;
+  for (int c = lane; c < M; c += WAVE) {
+    const double lbv = a.lb()[c], ubv = a.ub()[c], slo = a.sL()[c], sup = a.sU()[c];
+    const double sv = a.s()[c], lm = a.lam()[c], vl = a.vL()[c], vu = a.vU()[c];
+    const double gvv = a.gv()[c], gsc = a.gs()[c];
+    const double pv = a.rp()[c], nv = a.rn()[c], zp = a.rzp()[c], zn = a.rzn()[c];
+    const double dlam = gL.u.sol[(c / NG) * NB + NP + c % NG];
+    a.dl()[c] = dlam;
+    const int cl = cls_of(lbv, ubv, slo, sup);
+    theta += fabs((cl == 0 ? gvv - gsc * lbv : gvv - sv) - pv + nv);
+    double dsv = 0.0;
+    if (cl == 1) {
+      double gphis = 0.0;
+      if (isfin(slo)) gphis -= mu / (sv - slo);
+      if (isfin(sup)) gphis += mu / (sup - sv);
+      const double rs = gphis - lm;
+      dsv = (dlam - rs) / (sigma_s_v(sv, slo, sup, vl, vu) + dw);
+      gphid += (rs + lm) * dsv;
+      if (isfin(slo)) {
+        const double s_l = sv - slo;
+        if (dsv < 0) amax = fmin(amax, -tau * s_l / dsv);
+        const double dv = mu / s_l - vl - (vl / s_l) * dsv;
+        if (dv < 0) az = fmin(az, -tau * vl / dv);
+        bar += log(s_l);
+      }
+      if (isfin(sup)) {
+        const double s_u = sup - sv;
+        if (dsv > 0) amax = fmin(amax, tau * s_u / dsv);
+        const double dv = mu / s_u - vu + (vu / s_u) * dsv;
+        if (dv < 0) az = fmin(az, -tau * vu / dv);
+        bar += log(s_u);
+      }
+    }
+    a.ds()[c] = dsv;
+    const double gp = RESTO_RHO - mu / pv, gn = RESTO_RHO - mu / nv;
+    const double dp = (dlam - (gp - lm)) / (zp / pv + dw);
+    const double dn = (-dlam - (gn + lm)) / (zn / nv + dw);
+    a.rdp()[c] = dp;
+    a.rdn()[c] = dn;
+    gphid += gp * dp + gn * dn;
+    if (dp < 0) amax = fmin(amax, -tau * pv / dp);
+    if (dn < 0) amax = fmin(amax, -tau * nv / dn);
+    const double dzp = mu / pv - zp - (zp / pv) * dp, dzn = mu / nv - zn - (zn / nv) * dn;
+    if (dzp < 0) az = fmin(az, -tau * zp / dzp);
+    if (dzn < 0) az = fmin(az, -tau * zn / dzn);
+    bar += log(pv) + log(nv);
+  }
+  StepInfo st;
+  st.amax = wmin(amax);
+  st.az = wmin(az);
+  st.gphid = wsum(gphid);
+  st.theta = wsum(theta);
+  st.barrier = wsum(bar);
+  return st;
+}
+
+// filter line search of the restoration problem (its own filter in LDS)
+__device__ __noinline__ void line_search_resto(const Agent a, KArgs* argp) {
+  KState& K = gL.ks;
+  {
+    KArgs& ka = *argp;
+    const double gphid = K.st.gphid, theta = K.st.theta;
+    double amin;
+    if (gphid < 0 && theta <= K.theta_min)
+      amin = ka.opt.alpha_min_frac * fmin(fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid)),
+                                     ka.opt.delta * pow_ool(theta, ka.opt.s_theta) / pow_ool(-gphid, ka.opt.s_phi));
+    else if (gphid < 0)
+      amin = ka.opt.alpha_min_frac * fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid));
+    else
+      amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;
+    if (!(amin > 0.0)) amin = ka.opt.alpha_min_frac * ka.opt.gamma_theta;
+    K.amin = amin;
+    K.ls.alpha = K.st.amax;
+    K.ls.accepted = 0;
+    K.ls.ftype = 0;
+    K.ls.trials = 0;
+    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};
+  }
+#pragma unroll 1
+  for (int ls = 0; ls < 64; ++ls) {
+    {
+      const int lane = lane_now();
+      const double alpha = K.ls.alpha;
+      double barx = 0.0, prox = 0.0;
+#pragma unroll 1
+      for (int sl = 0; sl < VS; ++sl) {
+        const int i = lane + sl * WAVE;
+        if (i < NW) {
+          const double lo = a.xL()[i], hi = a.xU()[i];
+          const double xt = a.x()[i] + alpha * a.dx()[i];
+          gL.u.t.xt[i] = xt;
+          if (i >= NX && lo != hi) {
+            const double xrv = a.xr()[i];
+            prox += dr2_of(xrv) * (xt - xrv) * (xt - xrv);
+            if (isfin(lo)) barx += log_ool(xt - lo);
+            if (isfin(hi)) barx += log_ool(hi - xt);
+          }
+        }
+      }
+      K.barx = wsum(barx);
+      K.prox = wsum(prox);
+    }
+    wsync();
+    {
+      const double f = eval_fg_lds(a);
+      K.ls.tr.f = K.obj_scale * f;
+    }
+    wsync();
+    const int lane = lane_now();
+    const double alpha = K.ls.alpha;
+    double th = 0.0, bar = 0.0, pn = 0.0;
+#pragma unroll 1
+    for (int sl = 0; sl < CS; ++sl) {
+      const int c = lane + sl * WAVE;
+      if (c < M) {
+        const double gsv = a.gs()[c], lbv = a.lb()[c], slv = a.sL()[c], suv = a.sU()[c];
+        const int cl = cls_of(lbv, a.ub()[c], slv, suv);
+        const double gt = gL.u.t.gt[c] * gsv;
+        gL.u.t.gt[c] = gt;
+        const double st = a.s()[c] + alpha * a.ds()[c];
+        const double pt = a.rp()[c] + alpha * a.rdp()[c], nt = a.rn()[c] + alpha * a.rdn()[c];
+        th += fabs((cl == 0 ? gt - gsv * lbv : gt - st) - pt + nt);
+        if (cl == 1) {
+          if (isfin(slv)) bar += log_ool(st - slv);
+          if (isfin(suv)) bar += log_ool(suv - st);
+        }
+        bar += log_ool(pt) + log_ool(nt);
+        pn += pt + nt;
+      }
+    }
+    KArgs& ka = *argp;
+    const double mu = K.mu, theta = K.st.theta, gphid = K.st.gphid;
+    const double phi = K.fx - mu * K.st.barrier;
+    Trial tr = K.ls.tr;
+    tr.theta = wsum(th);
+    tr.fr = RESTO_RHO * wsum(pn) + 0.5 * K.zeta * K.prox;
+    tr.phi = tr.fr - mu * (K.barx + wsum(bar));
+    K.ls.tr = tr;
+    K.ls.trials += 1;
+    bool okt = (tr.theta <= K.theta_max) && (tr.phi == tr.phi);
+    const int nfilt = K.nfilt;
+    for (int j = 0; j < nfilt && okt; ++j)
+      if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
+    bool ftype = false;
+    if (okt) {
+      const bool switching = gphid < 0 && alpha * pow_ool(-gphid, ka.opt.s_phi) > ka.opt.delta * pow_ool(theta, ka.opt.s_theta);
+      if (theta <= K.theta_min && switching) {
+        okt = tr.phi <= phi + ka.opt.eta_phi * alpha * gphid;
+        ftype = true;
+      } else {
+        okt = tr.theta <= (1.0 - ka.opt.gamma_theta) * theta || tr.phi <= phi - ka.opt.gamma_phi * theta;
+        ftype = false;
+      }
+    }
+    K.ls.ftype = ftype;
+    if (okt) { K.ls.accepted = 1; break; }
+    if (alpha * 0.5 < K.amin) break;
+    K.ls.alpha = alpha * 0.5;
+  }
+  wsync();
+}
+
+// take the restoration trial: accept_step plus p, n and their multipliers
+__device__ __noinline__ void accept_step_resto(const Agent a, const double kappa_sigma, double mu, double alpha,
+                                               double az) {
+  accept_step(a, kappa_sigma, mu, alpha, az);
+  const int lane = a.lane;
+  for (int c = lane; c < M; c += WAVE) {
+    const double pv = a.rp()[c], nv = a.rn()[c], dp = a.rdp()[c], dn = a.rdn()[c];
+    const double zp = a.rzp()[c], zn = a.rzn()[c];
+    const double pn_ = pv + alpha * dp, nn_ = nv + alpha * dn;
+    const double zpn = zp + az * (mu / pv - zp - (zp / pv) * dp);
+    const double znn = zn + az * (mu / nv - zn - (zn / nv) * dn);
+    a.rp()[c] = pn_;
+    a.rn()[c] = nn_;
+    a.rzp()[c] = fmax(fmin(zpn, kappa_sigma * mu / pn_), mu / (kappa_sigma * pn_));
+    a.rzn()[c] = fmax(fmin(znn, kappa_sigma * mu / nn_), mu / (kappa_sigma * nn_));
+  }
+}
+
+
+// filter insertion of the current (theta, phi) with IPOPT's margins
+__device__ __forceinline__ void filter_augment(KArgs* argp) {
+  KState& K = gL.ks;
+  const double gt = (*argp).opt.gamma_theta, gp = (*argp).opt.gamma_phi;
+  const double theta = K.st.theta, phi = K.fx - K.mu * K.st.barrier;
+  int nfilt = K.nfilt;
+  if (nfilt == MAXF) {
+    if (lane_now() == 0)
+      for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
+    nfilt--;
+  }
+  if (lane_now() == 0) { gL.fth[nfilt] = (1.0 - gt) * theta; gL.fph[nfilt] = phi - gp * theta; }
+  K.nfilt = nfilt + 1;
+}
+
+// rest of a restoration iteration after the step: line search, filter, accept.  1: stop
+__device__ __noinline__ int resto_tail(const Agent a, KArgs* argp) {
+  KState& K = gL.ks;
+  line_search_resto(a, argp);
+  const LSResult ls = K.ls;
+  K.n_trials += ls.trials;
+  if (!ls.accepted) { K.status = MPCX_RESTORATION_FAILED; return 1; }
+  if (!ls.ftype) filter_augment(argp);
+  K.fx = ls.tr.fr;
+  K.fo = ls.tr.f;
+  wsync();
+  accept_step_resto(a, (*argp).opt.kappa_sigma, K.mu, ls.alpha, K.st.az);
+  sync();
+  eval_gj_lds(a);
+  sync();
+  K.it += 1;
+  K.n_resto_it += 1;
+  return 0;
+}
+
+// the step of an original-problem iteration: 0 line-search step, 1 soft step accepted by
+// the filter (taken like a line-search step), 2 soft step accepted by the error test
+// (already the iterate), -1 restoration phase started, -2 stop at an acceptable point
+__device__ __noinline__ int search_step(const Agent a, KArgs* argp) {
+  KState& K = gL.ks;
+  int mode;
+  if (K.soft) {
+    K.soft_count += 1;
+    const int r = (K.soft_count <= MAX_SOFT_ITERS) ? soft_try(a, argp) : 0;
+    if (r == 1) { K.soft = 0; K.soft_count = 0; }
+    mode = r == 0 ? -1 : r;
+  } else {
+    line_search(a, argp);
+    K.n_trials += K.ls.trials;
+    if (K.ls.accepted) {
+      mode = 0;
+    } else {
+      const int r = soft_try(a, argp);
+      if (r != 0) { K.n_soft += 1; if (r == 2) { K.soft = 1; K.soft_count = 0; } }
+      mode = r == 0 ? -1 : r;
+    }
+  }
+  if (mode < 0) {
+    // "Restoration phase called at acceptable point"
+    Acceptable acc = K.acc;
+    const OptErr e0 = K.e0;
+    const bool acceptable = current_is_acceptable(acc, e0, e0.err_at(0.0), K.fx, K.it, K.obj_scale, K.square,
+                                                  (*argp).opt);
+    K.acc = acc;
+    if (acceptable) { K.status = MPCX_SOLVED_TO_ACCEPTABLE; return -2; }
+    resto_start(a, argp);
+    return -1;
+  }
+  return mode;
+}
+
 }  // namespace mpcx_kernel
 
 using namespace mpcx_kernel;
@@ -2470,11 +3283,22 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   K.status = MPCX_MAX_ITER_EXCEEDED;
   K.it = 0;
   K.acc = Acceptable{-1e50, -1e50, -1, 0};
+  K.resto = 0; K.soft = 0; K.soft_count = 0; K.lsmode = 0; K.n_soft = 0; K.n_resto_it = 0;
+#define KARGP ((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())
 #pragma unroll 1
   for (;;) {
-    if (iter_head(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr())) break;
+    if (K.resto) {
+      const int hr = iter_head_resto(a, KARGP);
+      if (hr == 1) break;
+      if (hr == 2) {  // back in the original problem: its own iteration head at this point
+        resto_return(a, KARGP);
+        if (iter_head(a, KARGP)) break;
+      }
+    } else if (iter_head(a, KARGP)) {
+      break;
+    }
     PROF(2);
-    eval_hess(a, K.obj_scale);
+    eval_hess(a, K.resto ? 0.0 : K.obj_scale);  // restoration: the constraints' curvature only
     PROF(3);
     // factorisation with inertia correction (IPOPT Algorithm IC)
     K.dw = 0.0;
@@ -2482,7 +3306,10 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     int ok = 0;
 #pragma unroll 1
     for (int attempt = 0; attempt < 60; ++attempt) {
-      if (attempt > 0) rhs_dual(a, K.mu, K.dw, K.dc);  // attempt 0: iter_head wrote the rhs
+      if (attempt > 0) {  // attempt 0: the iteration head wrote the rhs
+        if (K.resto) rhs_dual_resto(a, K.mu, K.dw, K.dc);
+        else rhs_dual(a, K.mu, K.dw, K.dc);
+      }
       const Inertia in = factor(a, KKTDiag{K.dw, K.dc, NEWTON});
       K.n_fact += 1;
       K.n_chain += gL.seq;
@@ -2505,61 +3332,53 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     if (!ok) { K.status = MPCX_ERROR_IN_STEP; break; }
     solve(a);
     PROF(6);
-    {
+    if (K.resto) {
+      const StepInfo st = recover_step_resto(a, K.mu, K.tau, K.dw);
+      K.st = st;
+    } else {
       const StepInfo st = recover_step(a, K.mu, K.tau, K.dw, K.obj_scale);
       K.st = st;
     }
     PROF(7);
-    // filter line search
-    line_search(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr());
-    {
-      const LSResult ls = K.ls;
-      K.n_trials += ls.trials;
-      bool ftype = ls.ftype;
-      // IPOPT BacktrackingLineSearch: before entering the restoration phase, stop if the
-      // current iterate is acceptable ("Restoration phase called at acceptable point")
-      if (!ls.accepted) {
-        Acceptable acc = K.acc;
-        const OptErr e0 = K.e0;
-        const bool acceptable = current_is_acceptable(acc, e0, e0.err_at(0.0), K.fx, K.it, K.obj_scale, K.square, KOPT);
-        K.acc = acc;
-        if (acceptable) { K.status = MPCX_SOLVED_TO_ACCEPTABLE; break; }
-      }
-      // no acceptable trial and the last one is not even finite: IPOPT would enter its
-      // restoration phase; stop with Restoration_Failed at the current (finite) iterate
-      if (!ls.accepted && !(isfin(ls.tr.theta) && isfin(ls.tr.phi))) { K.status = MPCX_RESTORATION_FAILED; break; }
-      int nfilt = K.nfilt;
-      if (!ls.accepted) { nfilt = 0; ftype = true; K.n_fallback += 1; }
-      if (!ftype) {
-        const double theta = K.st.theta, phi = K.fx - K.mu * K.st.barrier;
-        if (nfilt == MAXF) {
-          if (lane == 0)
-            for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
-          nfilt--;
-        }
-        if (lane == 0) { gL.fth[nfilt] = (1.0 - OPT(gamma_theta)) * theta; gL.fph[nfilt] = phi - OPT(gamma_phi) * theta; }
-        nfilt++;
-      }
-      K.nfilt = nfilt;
-      K.fx = ls.tr.f;
-      wsync();
+    if (K.resto) {  // restoration iteration: its own filter; no restoration inside it
+      if (resto_tail(a, KARGP)) break;
+      continue;
     }
+    // filter line search; on failure the soft restoration step, then the restoration phase
+    // (IPOPT BacktrackingLineSearch::FindAcceptableTrialPoint)
+    const int mode = search_step(a, KARGP);
+    if (mode == -2) break;       // acceptable point, status set
+    if (mode == -1) continue;    // restoration phase started
+    if (mode == 2) {  // the soft trial is already the iterate
+      K.fx = K.ls.tr.f;
+      wsync();
+      K.it += 1;
+      continue;
+    }
+    if (!K.ls.ftype) filter_augment(KARGP);
+    K.fx = K.ls.tr.f;
+    wsync();
     PROF(8);
-    accept_step(a, OPT(kappa_sigma), K.mu, K.ls.alpha, K.st.az);
+    accept_step(a, OPT(kappa_sigma), K.mu, K.ls.alpha, mode == 1 ? K.ls.alpha : K.st.az);
     sync();  // accepted multipliers visible to the stage lanes
     eval_gj_lds(a);
     sync();
     K.it += 1;
     PROF(9);
   }
+#undef KARGP
   const double obj_scale = K.obj_scale;
 
   // ---- outputs ----------------------------------------------------------------
   gdbl* wio = (gdbl*)args.w + (long)agent * NW;
+  // stopped inside the restoration phase: the original problem's objective and bound
+  // multipliers (those at the start of restoration), constraint multipliers zero
+  const int in_resto = K.resto;
   for (int i = lane; i < NW; i += WAVE) {
     wio[i] = a.x()[i];
     if (args.lam_w != nullptr)
-      ((gdbl*)args.lam_w)[(long)agent * NW + i] = (i < NX) ? 0.0 : (a.zU()[i] - a.zL()[i]) / obj_scale;
+      ((gdbl*)args.lam_w)[(long)agent * NW + i] =
+          (i < NX) ? 0.0 : (in_resto ? a.zu0()[i] - a.zl0()[i] : a.zU()[i] - a.zL()[i]) / obj_scale;
   }
 #ifdef MPCX_PROFILE
   PROF(2);
@@ -2574,10 +3393,10 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
 #endif
   if (args.lam_g != nullptr)
     for (int c = lane; c < M; c += WAVE)
-      ((gdbl*)args.lam_g)[(long)agent * M + c] = a.lam()[c] * a.gs()[c] / obj_scale;
+      ((gdbl*)args.lam_g)[(long)agent * M + c] = in_resto ? 0.0 : a.lam()[c] * a.gs()[c] / obj_scale;
   if (args.stats != nullptr && lane == 0) {
     mpcx_stats st;
-    st.obj = K.fx / obj_scale;
+    st.obj = (in_resto ? K.fo : K.fx) / obj_scale;
     st.primal_inf = K.e0.viol_u;
     st.dual_inf = K.e0.dual_u;
     st.compl_inf = K.e0.compl_at(0.0) / obj_scale;
@@ -2586,7 +3405,9 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     st.iter_count = K.it;
     st.status = K.status;
     st.n_inertia_corrections = K.n_ic;
-    st.n_linesearch_fallbacks = K.n_fallback;
+    st.n_restorations = K.n_fallback;
+    st.n_soft_restorations = K.n_soft;
+    st.n_restoration_iters = K.n_resto_it;
     st.n_factorizations = K.n_fact;
     st.n_trials = K.n_trials;
     st.n_block_chain = K.n_chain;

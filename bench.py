@@ -195,7 +195,7 @@ def admm_bench(args, world, rank, dev):
         "ms_per_admm_iteration": wall / args.admm_iters * 1e3,
         "allreduce_per_iteration": 1 if world > 1 else 0,
         "allreduce_doubles": fleet.reduce_len if world > 1 else 0,
-        **_fallbacks(out["linesearch_fallbacks"], world, dev),
+        **_restorations(out["restorations"], world, dev),
     }
 
 
@@ -226,7 +226,8 @@ def nn_bench(args, world, rank, dev):
         "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
         "statuses": sorted({int(s["status"]) for s in stats}),
         "mean_factorizations": float(np.mean([s["n_factorizations"] for s in stats])),
-        "linesearch_fallbacks_last_step": int(sum(s["n_linesearch_fallbacks"] for s in stats)),
+        "restorations_last_step": int(sum(s["n_restorations"] for s in stats)),
+        "soft_restorations_last_step": int(sum(s["n_soft_restorations"] for s in stats)),
         "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
                                       max(1, np.sum([s["n_factorizations"] for s in stats]))),
         "kernel_ms": kernel_ms,
@@ -323,7 +324,8 @@ def mhe_bench(args, world, rank, dev):
         "solves_per_s": ok * args.steps / wall, "converged_fraction": ok / n,
         "mean_ipm_iterations": float(np.mean([s["iter_count"] for s in stats])),
         "ipm_iterations_p50_p99_max": [float(np.percentile([s["iter_count"] for s in stats], q)) for q in (50, 99, 100)],
-        "linesearch_fallbacks_last_step": int(sum(s["n_linesearch_fallbacks"] for s in stats)),
+        "restorations_last_step": int(sum(s["n_restorations"] for s in stats)),
+        "soft_restorations_last_step": int(sum(s["n_soft_restorations"] for s in stats)),
         "factorisation": "stage-parallel, continuity rows bordered into the chain (DESIGN 2.1)"
                          if prob.gen.bordered_rows else "stage-parallel",
         "block_chain_fraction": float(np.sum([s["n_block_chain"] for s in stats]) /
@@ -381,7 +383,7 @@ def c2_admm_bench(args, world, rank, dev):
         "blocks_rank0": hi - lo if rank == 0 else None,
         "allreduce_doubles": fleet.reduce_len if world > 1 else 0,
         **_block_summary(out, wall, 5, world, dev),
-        **_fallbacks(out["linesearch_fallbacks"], world, dev),
+        **_restorations(out["restorations"], world, dev),
         "cpu_baseline": cpu,
     }
 
@@ -434,9 +436,9 @@ def _block_summary(out, wall, agents_per_block, world=1, dev=None):
     }
 
 
-def _fallbacks(n, world, dev):
-    """Line-search failures that took the kernel's fallback step instead of IPOPT's
-    restoration phase, summed over the ranks (every leg reports it)."""
+def _restorations(n, world, dev):
+    """Calls of the feasibility restoration phase in the leg's solves, summed over the ranks
+    (every leg reports it)."""
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -444,7 +446,7 @@ def _fallbacks(n, world, dev):
         t = torch.tensor([float(n)], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         n = int(t.item())
-    return {"linesearch_fallbacks": int(n)}
+    return {"restorations": int(n)}
 
 
 def c5_admm_bench(args, world, rank, dev):
@@ -494,7 +496,7 @@ def c5_admm_bench(args, world, rank, dev):
         "scaling": "strong", "blocks_total": nb, "zones_total": 3 * nb, "agents_total": 5 * nb,
         "blocks_rank0": hi - lo if rank == 0 else None,
         **_block_summary(out, wall, 5, world, dev),
-        **_fallbacks(out["linesearch_fallbacks"], world, dev),
+        **_restorations(out["restorations"], world, dev),
         "solver": "reference IPOPT defaults (casadi_utils.py:197-206)",
         "cpu_baseline": cpu,
     }
@@ -816,7 +818,8 @@ def main():
                 "statuses_rank0": {k: int(v) for k, v in zip(*np.unique([s["return_status"] for s in stats],
                                                                          return_counts=True))},
                 "mean_ipm_iterations": float(arr["iter"].mean()),
-                "linesearch_fallbacks_rank0": int(sum(s_["n_linesearch_fallbacks"] for s_ in stats)),
+                "restorations_rank0": int(sum(s_["n_restorations"] for s_ in stats)),
+                "soft_restorations_rank0": int(sum(s_["n_soft_restorations"] for s_ in stats)),
                 "ipm_iterations_p50_p99_max": [float(np.percentile(arr["iter"], q)) for q in (50, 99, 100)],
                 "parallelism": f"agent-partitioned dp{world}",
             },

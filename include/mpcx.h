@@ -66,6 +66,8 @@ typedef enum mpcx_status {
   MPCX_RESTORATION_FAILED = -2,      /* "Restoration_Failed" (line search gave up) */
   MPCX_ERROR_IN_STEP = -3,           /* "Error_In_Step_Computation" */
   MPCX_INVALID_NUMBER = -4,          /* "Invalid_Number_Detected" */
+  MPCX_INFEASIBLE = -5,              /* "Infeasible_Problem_Detected" (restoration converged to a
+                                        point of local infeasibility) */
 } mpcx_status;
 
 /* Dimensions of one stage-structured NLP (must match the code object). */
@@ -117,11 +119,13 @@ typedef struct mpcx_stats {
   int32_t iter_count;
   int32_t status;      /* mpcx_status */
   int32_t n_inertia_corrections;
-  int32_t n_linesearch_fallbacks;
+  int32_t n_restorations; /* calls of the feasibility restoration phase (IPOPT MinC_1Nrm) */
   int32_t n_factorizations;
   int32_t n_trials;    /* line-search trial points evaluated */
   int32_t n_block_chain; /* factorisations that fell back to the sequential block chain */
   int32_t n_dense_stages; /* stage factorisations redone densely (static sparse pivot rejected) */
+  int32_t n_soft_restorations; /* line-search failures resolved by a soft restoration step */
+  int32_t n_restoration_iters; /* iterations spent in the restoration phase (in iter_count) */
 } mpcx_stats;
 
 typedef struct mpcx_handle mpcx_handle;

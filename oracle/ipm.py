@@ -83,6 +83,13 @@ class IPMOptions:
     gamma_theta: float = 1e-5
     alpha_min_frac: float = 0.05
     max_filter: int = 64
+    # soft restoration and the feasibility restoration phase (IPOPT defaults)
+    soft_resto_pderror_reduction_factor: float = 0.9999
+    max_soft_resto_iters: int = 10
+    resto_penalty_parameter: float = 1000.0
+    resto_proximity_weight: float = 1.0
+    required_infeasibility_reduction: float = 0.9
+    bound_mult_reset_threshold: float = 1000.0
 
 
 @dataclasses.dataclass
@@ -108,6 +115,10 @@ class IPMResult:
     status: str
     success: bool
     history: list
+    s: Optional[np.ndarray] = None      # slacks of the inequality rows (scaled)
+    n_soft_resto: int = 0               # line-search failures resolved by a soft restoration step
+    n_resto: int = 0                    # calls of the feasibility restoration phase
+    resto_iterations: int = 0           # iterations spent in it (counted in ``iterations``)
 
 
 def _relax(b, lower: bool, factor: float):
@@ -121,11 +132,81 @@ def _relax(b, lower: bool, factor: float):
 def solve(nlp: NLPFunctions, x0, lbx, ubx, lbg, ubg, opts: IPMOptions = None,
           record: bool = False) -> IPMResult:
     o = opts or IPMOptions()
-    with np.errstate(divide='ignore', invalid='ignore'):
+    with np.errstate(divide='ignore', invalid='ignore', over='ignore'):
         return _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record)
 
 
-def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
+@dataclasses.dataclass
+class _Inner:
+    """Restoration mode of :func:`_solve` (IPOPT runs a second IpoptAlgorithm on the
+    RestoIpoptNLP, `MinC_1NrmRestorationPhase::PerformRestoration`): the NLP is already in
+    the scaled space of the original one (no gradient scaling, no bound relaxation, no
+    bound push), the multipliers and mu come from the original iterate, the constraint
+    multipliers start at zero, and ``check(x, s)`` is the return test
+    (`RestoConvergenceCheck`) evaluated at the head of every restoration iteration."""
+
+    zL: np.ndarray
+    zU: np.ndarray
+    vL: np.ndarray
+    vU: np.ndarray
+    mu: float
+    check: Callable
+    set_mu: Callable
+
+
+class _RestoNLP:
+    """IPOPT's restoration NLP (`RestoIpoptNLP`, Wächter & Biegler 2006, eq. (30)) over the
+    SCALED original constraints c~(x) (equalities) / d~(x) (with their slacks):
+
+        min  rho * sum(p + n) + zeta(mu)/2 * || D_R (x - x_R) ||^2
+        s.t. c~(x) - p + n = c~_L (equality rows),  d~(x) - p + n in [d~_L, d~_U],  p, n >= 0
+
+    with rho = resto_penalty_parameter, zeta(mu) = resto_proximity_weight * sqrt(mu) (mu of
+    the restoration problem itself), D_R = diag(1 / max(1, |x_R|)) and x_R the iterate at
+    which restoration started.  Variables [x (n), p (m), n (m)]."""
+
+    def __init__(self, F, JG, G, HC, n, m, xR, fixed, rho, weight):
+        self.F, self.JG, self.G, self.HC = F, JG, G, HC
+        self.n, self.m = n, m
+        self.xR = xR
+        self.dr2 = np.where(fixed, 0.0, 1.0 / np.maximum(1.0, np.abs(xR)) ** 2)
+        self.rho, self.weight = rho, weight
+        self.zeta = 0.0
+
+    def set_mu(self, mu):
+        self.zeta = self.weight * math.sqrt(mu)
+
+    def functions(self) -> NLPFunctions:
+        n, m = self.n, self.m
+
+        def f(w):
+            x = w[:n]
+            return float(self.rho * np.sum(w[n:]) + 0.5 * self.zeta * np.sum(self.dr2 * (x - self.xR) ** 2))
+
+        def grad(w):
+            g = np.full(n + 2 * m, self.rho)
+            g[:n] = self.zeta * self.dr2 * (w[:n] - self.xR)
+            return g
+
+        def g(w):
+            return self.G(w[:n]) - w[n:n + m] + w[n + m:]
+
+        def jac(w):
+            J = np.zeros((m, n + 2 * m))
+            J[:, :n] = self.JG(w[:n])
+            J[:, n:n + m] = -np.eye(m)
+            J[:, n + m:] = np.eye(m)
+            return J
+
+        def hess(w, sigma, lam):
+            H = np.zeros((n + 2 * m, n + 2 * m))
+            H[:n, :n] = self.HC(w[:n], lam) + np.diag(sigma * self.zeta * self.dr2)
+            return H
+
+        return NLPFunctions(n=n + 2 * m, m=m, f=f, grad_f=grad, g=g, jac_g=jac, hess_l=hess)
+
+
+def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = None):
     n, m = nlp.n, nlp.m
     x = np.array(x0, dtype=float).copy()
     lbx = np.maximum(np.asarray(lbx, float), -INF)
@@ -141,16 +222,17 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
     ineq = ~eq
 
     # --- NLP scaling (gradient based, at the user starting point) ----------
-    gf0 = nlp.grad_f(x)
-    gmax = np.max(np.abs(gf0[free])) if free.any() else 0.0
     obj_scale = 1.0
-    if gmax > o.nlp_scaling_max_gradient:
-        obj_scale = max(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / gmax)
-    J0 = nlp.jac_g(x)
-    rowmax = np.max(np.abs(J0[:, free]), axis=1) if m else np.zeros(0)
     g_scale = np.ones(m)
-    big = rowmax > o.nlp_scaling_max_gradient
-    g_scale[big] = np.maximum(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / rowmax[big])
+    if inner is None:
+        gf0 = nlp.grad_f(x)
+        gmax = np.max(np.abs(gf0[free])) if free.any() else 0.0
+        if gmax > o.nlp_scaling_max_gradient:
+            obj_scale = max(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / gmax)
+        J0 = nlp.jac_g(x)
+        rowmax = np.max(np.abs(J0[:, free]), axis=1) if m else np.zeros(0)
+        big = rowmax > o.nlp_scaling_max_gradient
+        g_scale[big] = np.maximum(o.nlp_scaling_min_value, o.nlp_scaling_max_gradient / rowmax[big])
 
     def F(xx):
         return obj_scale * nlp.f(xx)
@@ -168,19 +250,20 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
         J[:, fixed] = 0.0
         return J
 
-    def H(xx, lam):
-        Hm = nlp.hess_l(xx, obj_scale, lam * g_scale)
+    def H(xx, lam, sigma=None):
+        Hm = nlp.hess_l(xx, obj_scale if sigma is None else sigma, lam * g_scale)
         Hm[fixed, :] = 0.0
         Hm[:, fixed] = 0.0
         return Hm
 
-    # scaled, relaxed bounds
-    xL = np.where(free & (lbx > -INF), _relax(lbx, True, o.bound_relax_factor), -np.inf)
-    xU = np.where(free & (ubx < INF), _relax(ubx, False, o.bound_relax_factor), np.inf)
+    # scaled, relaxed bounds (the restoration NLP is already relaxed and scaled)
+    relax = 0.0 if inner is not None else o.bound_relax_factor
+    xL = np.where(free & (lbx > -INF), _relax(lbx, True, relax), -np.inf)
+    xU = np.where(free & (ubx < INF), _relax(ubx, False, relax), np.inf)
     sLb = np.where(lbg > -INF, lbg * g_scale, -np.inf)
     sUb = np.where(ubg < INF, ubg * g_scale, np.inf)
-    sL = np.where(ineq, np.where(np.isfinite(sLb), _relax(np.where(np.isfinite(sLb), sLb, 0), True, o.bound_relax_factor), -np.inf), sLb)
-    sU = np.where(ineq, np.where(np.isfinite(sUb), _relax(np.where(np.isfinite(sUb), sUb, 0), False, o.bound_relax_factor), np.inf), sUb)
+    sL = np.where(ineq, np.where(np.isfinite(sLb), _relax(np.where(np.isfinite(sLb), sLb, 0), True, relax), -np.inf), sLb)
+    sU = np.where(ineq, np.where(np.isfinite(sUb), _relax(np.where(np.isfinite(sUb), sUb, 0), False, relax), np.inf), sUb)
     hasL, hasU = np.isfinite(xL), np.isfinite(xU)
     shasL, shasU = ineq & np.isfinite(sL), ineq & np.isfinite(sU)
     free_slack = ineq & ~shasL & ~shasU
@@ -202,22 +285,30 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
         v[bad] = 0.5 * (lo[bad] + hi[bad])
         return v
 
-    x = np.where(free, push(x, xL, xU, hasL, hasU), x)
-    gx = G(x)
-    s = np.where(ineq, push(gx, sL, sU, shasL, shasU), np.where(eq, lbg * g_scale, 0.0))
+    if inner is None:
+        x = np.where(free, push(x, xL, xU, hasL, hasU), x)
+        gx = G(x)
+        s = np.where(ineq, push(gx, sL, sU, shasL, shasU), np.where(eq, lbg * g_scale, 0.0))
+        zL = np.where(hasL, o.bound_mult_init_val, 0.0)
+        zU = np.where(hasU, o.bound_mult_init_val, 0.0)
+        vL = np.where(shasL, o.bound_mult_init_val, 0.0)
+        vU = np.where(shasU, o.bound_mult_init_val, 0.0)
+    else:  # the restoration starting point is interior by construction
+        gx = G(x)
+        s = np.where(ineq, gx, np.where(eq, lbg * g_scale, 0.0))
+        zL, zU = np.where(hasL, inner.zL, 0.0), np.where(hasU, inner.zU, 0.0)
+        vL, vU = np.where(shasL, inner.vL, 0.0), np.where(shasU, inner.vU, 0.0)
 
-    zL = np.where(hasL, o.bound_mult_init_val, 0.0)
-    zU = np.where(hasU, o.bound_mult_init_val, 0.0)
-    vL = np.where(shasL, o.bound_mult_init_val, 0.0)
-    vU = np.where(shasU, o.bound_mult_init_val, 0.0)
-
+    mu = o.mu_init if inner is None else inner.mu
+    if inner is not None:
+        inner.set_mu(mu)
     fx = F(x)
     gfx = GF(x)
     Jx = JG(x)
 
     # --- least-squares multiplier estimate ---------------------------------
     lam = np.zeros(m)
-    if m and o.constr_mult_init_max > 0:
+    if inner is None and m and o.constr_mult_init_max > 0:
         K = np.zeros((n + m, n + m))
         K[:n, :n] = np.eye(n)
         K[:n, n:] = Jx.T
@@ -234,7 +325,6 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
         except np.linalg.LinAlgError:
             pass
 
-    mu = o.mu_init
     tau = max(o.tau_min, 1.0 - mu)
     delta_w_last = 0.0
 
@@ -259,6 +349,13 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
         primal = np.max(np.abs(c), initial=0.0)
         compl = np.max(np.abs(comp), initial=0.0)
         return max(dual / s_d, primal, compl / s_c), dual, primal, compl
+
+    def pd_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu_):
+        """IPOPT primal_dual_system_error: 1-norms of the dual infeasibility, the
+        constraint violation and the mu-complementarity (the common normalisation
+        by the number of entries cancels in the soft-restoration ratio)."""
+        rd, rs, c, comp = residuals(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu_)
+        return float(np.sum(np.abs(rd)) + np.sum(np.abs(rs)) + np.sum(np.abs(c)) + np.sum(np.abs(comp)))
 
     def theta_of(gx, s):
         c = np.where(ineq, gx - s, gx - np.where(eq, lbg * g_scale, 0.0))
@@ -307,9 +404,23 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
     history = []
     status = "Maximum_Iterations_Exceeded"
     it = 0
+    counts = dict(soft=0, resto=0, resto_iters=0)
+    in_soft, soft_count = False, 0
     # IPOPT MonotoneMuUpdate::CalcNewMuAndTau: mu >= min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
     mu_floor = max(min(o.tol, o.compl_inf_tol) / (o.kappa_eps + 1.0), o.mu_min)
+
+    def filter_ok(th, ph):
+        return th <= theta_max and not any(th >= a and ph >= b for a, b in filt)
+
+    def augment(theta, phi):
+        filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
+        if len(filt) > o.max_filter:
+            filt.pop(0)
+
     while True:
+        if inner is not None and inner.check(x, s):
+            status = "Resto_Return"
+            break
         err0, dual, primal, compl = opt_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, 0.0)
         dual_u, viol_u, compl_u = unscaled(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, compl)
         if record:
@@ -339,6 +450,10 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
             mu = new_mu
             tau = max(o.tau_min, 1.0 - mu)
             filt = []
+            if inner is not None:  # the restoration objective depends on mu (zeta(mu))
+                inner.set_mu(mu)
+                fx = F(x)
+                gfx = GF(x)
         Hx = H(x, lam)
         # primal-dual matrices
         dxL = np.where(hasL, x - np.where(hasL, xL, 0), 1.0)
@@ -420,54 +535,170 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
             a_min = o.alpha_min_frac * min(o.gamma_theta, o.gamma_phi * theta / (-gphi_d))
         else:
             a_min = o.alpha_min_frac * o.gamma_theta
-        alpha = a_max
-        accepted = False
-        ftype = False
-        while True:
-            xt = x + alpha * dx
-            st = s + alpha * ds
-            gxt = G(xt)
-            fxt = F(xt)
-            th_t = theta_of(gxt, st)
-            ph_t = phi_of(fxt, xt, st, mu)
-            ok = th_t <= theta_max and not any(th_t >= a and ph_t >= b for a, b in filt)
+
+        def soft_step():
+            """IPOPT BacktrackingLineSearch::TrySoftRestoStep: the full fraction-to-the-boundary
+            step, the same step size for primal and dual variables; accepted if the original
+            filter criterion holds at alpha = 0 (h-type) or the primal-dual system error drops
+            by soft_resto_pderror_reduction_factor.  Returns (accepted, original, trial)."""
+            al = min(a_max, a_z)
+            xt, st_, lt = x + al * dx, s + al * ds, lam + al * dlam
+            zt = (zL + al * dzL, zU + al * dzU, vL + al * dvL, vU + al * dvU)
+            gxt, fxt = G(xt), F(xt)
+            th_t, ph_t = theta_of(gxt, st_), phi_of(fxt, xt, st_, mu)
+            trial = (xt, st_, lt, zt, gxt, fxt, al)
+            if not (np.isfinite(th_t) and np.isfinite(ph_t)):
+                return False, False, trial
+            if filter_ok(th_t, ph_t) and (th_t <= (1 - o.gamma_theta) * theta or ph_t <= phi - o.gamma_phi * theta):
+                return True, True, trial
+            gft, Jt = GF(xt), JG(xt)
+            cur = pd_error(x, s, lam, zL, zU, vL, vU, gfx, Jx, gx, mu)
+            new = pd_error(xt, st_, lt, *zt, gft, Jt, gxt, mu)
+            return bool(new <= o.soft_resto_pderror_reduction_factor * cur), False, trial
+
+        accepted, ftype, goto_resto, soft = False, False, False, None
+        if in_soft:
+            soft_count += 1
+            ok, orig, trial = soft_step() if soft_count <= o.max_soft_resto_iters else (False, False, None)
             if ok:
-                switching = gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
-                if theta <= theta_min and switching:
-                    ok = ph_t <= phi + o.eta_phi * alpha * gphi_d
-                    ftype = True
+                soft = (orig, trial)
+                if orig:
+                    in_soft, soft_count = False, 0
+            else:
+                goto_resto = True
+        else:
+            alpha = a_max
+            while True:
+                xt = x + alpha * dx
+                st = s + alpha * ds
+                gxt = G(xt)
+                fxt = F(xt)
+                th_t = theta_of(gxt, st)
+                ph_t = phi_of(fxt, xt, st, mu)
+                ok = np.isfinite(th_t) and np.isfinite(ph_t) and filter_ok(th_t, ph_t)
+                if ok:
+                    switching = gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
+                    if theta <= theta_min and switching:
+                        ok = ph_t <= phi + o.eta_phi * alpha * gphi_d
+                        ftype = True
+                    else:
+                        ok = th_t <= (1 - o.gamma_theta) * theta or ph_t <= phi - o.gamma_phi * theta
+                        ftype = False
+                if ok:
+                    accepted = True
+                    break
+                alpha *= 0.5
+                if alpha < a_min:
+                    break
+            if not accepted and inner is not None:
+                # no restoration inside the restoration phase (IPOPT: "Restoration phase in
+                # the restoration phase failed")
+                status = "Restoration_Failed"
+                break
+            if not accepted:
+                ok, orig, trial = soft_step()
+                if ok:
+                    soft = (orig, trial)
+                    counts["soft"] += 1
+                    if not orig:
+                        in_soft, soft_count = True, 0
                 else:
-                    ok = th_t <= (1 - o.gamma_theta) * theta or ph_t <= phi - o.gamma_phi * theta
-                    ftype = False
-            if ok:
-                accepted = True
+                    goto_resto = True
+        if goto_resto:
+            if current_is_acceptable(err0, dual_u, viol_u, compl_u, fx, it):
+                # IPOPT BacktrackingLineSearch: "Restoration phase called at acceptable point"
+                status = "Solved_To_Acceptable_Level"
                 break
-            alpha *= 0.5
-            if alpha < a_min:
+            if inner is not None:
+                status = "Restoration_Failed"
                 break
-        if not accepted and current_is_acceptable(err0, dual_u, viol_u, compl_u, fx, it):
-            # IPOPT BacktrackingLineSearch: "Restoration phase called at acceptable point"
-            status = "Solved_To_Acceptable_Level"
-            break
-        if not accepted and not (np.isfinite(th_t) and np.isfinite(ph_t)):
-            # no acceptable trial and the last one is not even finite: IPOPT would enter
-            # its restoration phase; stop with Restoration_Failed at the current iterate
-            status = "Restoration_Failed"
-            break
-        if not accepted:
-            # fallback instead of IPOPT's restoration phase: take the last trial
-            filt = []
-            ftype = True
-        if not ftype:
-            filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
-            if len(filt) > o.max_filter:
-                filt.pop(0)
-        x, s = xt, st
-        lam = lam + alpha * dlam
-        zL = zL + a_z * dzL
-        zU = zU + a_z * dzU
-        vL = vL + a_z * dvL
-        vU = vU + a_z * dvU
+            # ---- feasibility restoration phase (MinC_1NrmRestorationPhase) ----
+            counts["resto"] += 1
+            augment(theta, phi)                     # FilterLSAcceptor::PrepareRestoPhaseStart
+            in_soft, soft_count = False, 0
+            c_now = np.where(ineq, gx - s, gx - np.where(eq, lbg * g_scale, 0.0))
+            mu_r = max(mu, float(np.max(np.abs(c_now), initial=0.0)))
+            rho = o.resto_penalty_parameter
+            # p, n solving the complementarity of the resto problem at its start
+            # (Wächter & Biegler 2006, eq. (33))
+            a_ = (mu_r - rho * c_now) / (2.0 * rho)
+            n_r = a_ + np.sqrt(a_ ** 2 + mu_r * c_now / (2.0 * rho))
+            p_r = c_now + n_r
+            theta_start, mu_orig = theta, mu
+            rn = _RestoNLP(F, JG, G, lambda xx, ll: H(xx, ll, 0.0), n, m, x.copy(), fixed, rho,
+                           o.resto_proximity_weight)
+            sub = rn.functions()
+            lbx_r = np.concatenate([np.where(fixed, x, xL), np.zeros(2 * m)])
+            ubx_r = np.concatenate([np.where(fixed, x, xU), np.full(2 * m, np.inf)])
+            lbg_r = np.where(eq, lbg * g_scale, sL)
+            ubg_r = np.where(eq, lbg * g_scale, sU)
+            x_r0 = np.concatenate([x, p_r, n_r])
+
+            def check(xr, sr, _th0=theta_start, _mu=mu_orig):
+                """RestoConvergenceCheck: back to the original problem when the original
+                constraint violation dropped by required_infeasibility_reduction and the
+                point is acceptable to the original filter."""
+                xo = xr[:n]
+                so = np.where(ineq, sr, s)
+                gxo = G(xo)
+                th_o = theta_of(gxo, so)
+                if not th_o <= o.required_infeasibility_reduction * _th0:
+                    return False
+                return filter_ok(th_o, phi_of(F(xo), xo, so, _mu))
+
+            rho_cap = lambda z_: np.minimum(z_, rho)  # noqa: E731
+            inner_r = _Inner(zL=np.concatenate([rho_cap(zL), mu_r / p_r, mu_r / n_r]),
+                             zU=np.concatenate([rho_cap(zU), np.zeros(2 * m)]),
+                             vL=rho_cap(vL), vU=rho_cap(vU), mu=mu_r, check=check, set_mu=rn.set_mu)
+            o_r = dataclasses.replace(o, max_iter=o.max_iter - it)
+            r = _solve(sub, x_r0, lbx_r, ubx_r, lbg_r, ubg_r, o_r, False, inner=inner_r)
+            counts["resto_iters"] += r.iterations
+            it += r.iterations
+            if r.status != "Resto_Return":
+                status = {"Solve_Succeeded": "Infeasible_Problem_Detected",
+                          "Solved_To_Acceptable_Level": "Infeasible_Problem_Detected"}.get(r.status, r.status)
+                x = r.x[:n]
+                s = np.where(ineq, r.s, s)
+                gx, fx = G(x), F(x)
+                lam = np.zeros(m)
+                break
+            # return to the original problem: bound multipliers by one Newton step for
+            # the complementarity over the whole primal change, fraction to the boundary,
+            # reset to 1 when too large; constraint multipliers reset to zero
+            # (bound_mult_reset_threshold, constr_mult_reset_threshold = 0)
+            xn = r.x[:n]
+            sn = np.where(ineq, r.s, s)
+            slack_new = (np.where(hasL, xn - np.where(hasL, xL, 0), 1.0), np.where(hasU, np.where(hasU, xU, 0) - xn, 1.0),
+                         np.where(shasL, sn - np.where(shasL, sL, 0), 1.0), np.where(shasU, np.where(shasU, sU, 0) - sn, 1.0))
+            slack_old = (dxL, dxU, dsL, dsU)
+            zs = (zL, zU, vL, vU)
+            masks = (hasL, hasU, shasL, shasU)
+            dz = [np.where(mk, (mu - z_ * sn_) / so_, 0.0) for z_, sn_, so_, mk in zip(zs, slack_new, slack_old, masks)]
+            a_d = min(ftb(z_, d_, mk) for z_, d_, mk in zip(zs, dz, masks))
+            zL, zU, vL, vU = (z_ + a_d * d_ for z_, d_ in zip(zs, dz))
+            if max(np.max(np.abs(v_), initial=0.0) for v_ in (zL, zU, vL, vU)) > o.bound_mult_reset_threshold:
+                zL, zU = np.where(hasL, 1.0, 0.0), np.where(hasU, 1.0, 0.0)
+                vL, vU = np.where(shasL, 1.0, 0.0), np.where(shasU, 1.0, 0.0)
+            x, s = xn, sn
+            lam = np.zeros(m)
+            fx, gx = F(x), G(x)
+            gfx, Jx = GF(x), JG(x)
+            continue
+        if soft is not None:
+            orig, (xt, st, lt, (zLt, zUt, vLt, vUt), gxt, fxt, alpha) = soft
+            if orig:
+                augment(theta, phi)   # accepted by the original (h-type) criterion
+            x, s, lam = xt, st, lt
+            zL, zU, vL, vU = zLt, zUt, vLt, vUt
+        else:
+            if not ftype:
+                augment(theta, phi)
+            x, s = xt, st
+            lam = lam + alpha * dlam
+            zL = zL + a_z * dzL
+            zU = zU + a_z * dzU
+            vL = vL + a_z * dvL
+            vU = vU + a_z * dvU
         # safeguard (kappa_sigma)
         dxL = np.where(hasL, x - np.where(hasL, xL, 0), 1.0)
         dxU = np.where(hasU, np.where(hasU, xU, 0) - x, 1.0)
@@ -486,7 +717,8 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record):
     lam_x = (zU - zL) / obj_scale
     return IPMResult(x=x, lam_g=lam_g, lam_x=lam_x, f=fx / obj_scale, iterations=it,
                      status=status, success=status in ("Solve_Succeeded", "Solved_To_Acceptable_Level"),
-                     history=history)
+                     history=history, s=s, n_soft_resto=counts["soft"], n_resto=counts["resto"],
+                     resto_iterations=counts["resto_iters"])
 
 
 def _block_eigs(D: np.ndarray) -> np.ndarray:

@@ -16,6 +16,8 @@ independent of the product's tracer and transcriber:
 * ``fixture_mpc`` — backend ``casadi`` collocation (defaults: Legendre d=3) on the
   reference test-suite model `tests/fixtures/casadi_test_model.py:13-47` with the MPC
   module config of `tests/test_mpc.py:121-146`.
+* ``cubic_room`` — backend ``casadi`` collocation (Legendre d=2) on a zone with an algebraic
+  quantity on a cubic characteristic (the restoration-phase case, ``models/examples.CubicRoom``).
 * ``room_nn`` — backend ``casadi_admm_nn`` NARX multiple shooting
   (`casadi_/casadi_admm_ml.py:247-397`) on
   `examples/three_zone_datadriven_admm/models/Room_model.py` with two ANNs (C5).
@@ -1054,7 +1056,7 @@ def fixture_mpc(N=5, ts=900.0, d=3) -> OracleProblem:
 
 
 def fixture_mpc_inputs(prob: OracleProblem, N=5, d=3, T0=298.16, dist=270.0, u_prev=0.02, par=12.0, par2=10.0,
-                       u_lb=0.0, u_ub=1.0):
+                       u_lb=0.0, u_ub=1.0, T_lb=-np.inf, T_ub=np.inf):
     """Cold start (`core/discretization.py:212-245`): states at their current value, the
     control at the middle of its bounds, the unbounded output at 0."""
     p = np.array([T0, u_prev, par, par2] + [dist] * (N * d), float)
@@ -1064,8 +1066,68 @@ def fixture_mpc_inputs(prob: OracleProblem, N=5, d=3, T0=298.16, dist=270.0, u_p
     for i, name in enumerate(prob.w_names):
         base = name.split("@")[0]
         if base == "state":
-            w0[i] = T0
+            lbw[i], ubw[i], w0[i] = T_lb, T_ub, T0
         elif base == "myctrl":
             lbw[i], ubw[i], w0[i] = u_lb, u_ub, 0.5 * (u_lb + u_ub)
     lbw[0] = ubw[0] = T0
+    return p, lbw, ubw, w0
+
+
+def cubic_room(N=4, ts=10.0, d=2, wz=0.0) -> OracleProblem:
+    """w = [T_0, {u_k, {T_kj, z_kj}_j, T_{k+1}}]; g per interval: continuity, then per point
+    the collocation row and z^3 - 3 z - 5 = 0; cost B_j ts (T - 290)^2 (``wz``: an optional z^2
+    weight, 0 in the model).  No parameters
+    beyond the initial state (and u_prev of backend "casadi")."""
+    tau, B, C, D = collocation(d)
+    nb = 1 + 2 * d + 1
+    n = 1 + N * nb
+    m = N * (1 + 2 * d)
+    names = ["T@0"]
+    for k in range(N):
+        names.append(f"u@{k}")
+        for j in range(d):
+            names += [f"T@{k},{j}", f"z@{k},{j}"]
+        names.append(f"T@{k + 1}")
+
+    def f(w, p):
+        tot = w.new_zeros(())
+        for k in range(N):
+            o = 1 + k * nb
+            for j in range(d):
+                tot = tot + B[j + 1] * ((w[o + 1 + 2 * j] - 290.0) ** 2 + wz * w[o + 2 + 2 * j] ** 2) * ts
+        return tot
+
+    def g(w, p):
+        out = []
+        xk = w[0]
+        for k in range(N):
+            o = 1 + k * nb
+            u = w[o]
+            Tj = [w[o + 1 + 2 * j] for j in range(d)]
+            out.append(w[o + nb - 1] - (D[0] * xk + sum(D[j + 1] * Tj[j] for j in range(d))))
+            for j in range(d):
+                xp = C[0, j + 1] * xk + sum(C[r + 1, j + 1] * Tj[r] for r in range(d))
+                out.append(ts * (u - 0.01 * (Tj[j] - 290.0)) - xp)
+                z = w[o + 2 + 2 * j]
+                out.append(z ** 3 - 3.0 * z - 5.0)
+            xk = w[o + nb - 1]
+        return torch.stack(out)
+
+    return OracleProblem("cubic_room", n, m, 2, f, g, lambda p: np.zeros(m), lambda p: np.zeros(m), names)
+
+
+def cubic_room_inputs(prob: OracleProblem, T0=295.0, u_prev=0.0, z_lb=-5.0, z_ub=2.6):
+    p = np.array([T0, u_prev], float)
+    lbw = np.full(prob.n, -np.inf)
+    ubw = np.full(prob.n, np.inf)
+    w0 = np.zeros(prob.n)
+    for i, name in enumerate(prob.w_names):
+        base = name.split("@")[0]
+        if base == "T":
+            w0[i] = T0
+        elif base == "u":
+            lbw[i], ubw[i], w0[i] = 0.0, 1.0, 0.5
+        elif base == "z":
+            lbw[i], ubw[i], w0[i] = z_lb, z_ub, 0.5 * (z_lb + z_ub)
+    lbw[0] = ubw[0] = w0[0] = T0
     return p, lbw, ubw, w0

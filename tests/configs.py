@@ -164,10 +164,17 @@ def fixture_mpc(**kw) -> Case:
     be, cv = bm.fixture_mpc(**kw)
     N = kw.get("N", 5)
     prob = nlps.fixture_mpc(N=N)
-    o = {k: kw[k] for k in ("T0", "u_prev") if k in kw}
+    o = {k: kw[k] for k in ("T0", "u_prev", "T_lb", "T_ub") if k in kw}
     if "disturbance" in kw:
         o["dist"] = kw["disturbance"]
     return Case(be, cv, prob, nlps.fixture_mpc_inputs(prob, N=N, **o))
+
+
+def cubic_room(**kw) -> Case:
+    """Restoration-phase case: the line search fails from the cold guess."""
+    be, cv = bm.cubic_room(**kw)
+    prob = nlps.cubic_room(N=kw.get("N", 4))
+    return Case(be, cv, prob, nlps.cubic_room_inputs(prob, **{k: kw[k] for k in ("T0",) if k in kw}))
 
 
 CASES: Dict[str, Callable[..., Case]] = {
@@ -186,6 +193,7 @@ CASES: Dict[str, Callable[..., Case]] = {
     "mhe_room": mhe_room,
     "rng_room_mpc": rng_room_mpc,
     "fixture_mpc": fixture_mpc,
+    "cubic_room": cubic_room,
     # estimating mDot per interval needs the wall temperature measured too (else mDot
     # and the unmeasured wall state trade off and the minimiser is not unique)
     "mhe_room_u": lambda **kw: mhe_room(estimate="mDot", **{"w_T_wall": 1.0, **kw}),

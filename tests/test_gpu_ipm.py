@@ -152,6 +152,42 @@ def test_gpu_matches_oracle_at_reference_defaults(name, kw):
                                        atol=1e-7 * max(1.0, np.abs(want).max()))
 
 
+#: cases on which IPOPT's filter line search fails (oracle/ipm.py): the soft restoration step
+#: and the feasibility restoration phase, returning to the original problem (cubic_room:
+#: twice, then Solve_Succeeded) or ending at a point of local infeasibility (the reference
+#: test-suite model with state bounds its unstable dynamics cannot meet)
+RESTO_CASES = [
+    ("cubic_room", {}, "tight"),
+    ("cubic_room", {}, "reference"),
+    ("fixture_mpc", {"T_lb": 245.0, "T_ub": 302.0, "disturbance": 260.0}, "reference"),
+    ("fixture_mpc", {"T_lb": 255.0, "T_ub": 302.0, "disturbance": 270.0, "T0": 290.0}, "reference"),
+    ("fixture_mpc", {"T_lb": 285.0, "T_ub": 300.0}, "tight"),
+]
+
+
+@pytest.mark.parametrize("name,kw,setting", RESTO_CASES)
+def test_gpu_restoration_phase_matches_oracle(name, kw, setting):
+    """Line-search failures: same status, iteration count, number of soft restoration steps,
+    restoration phases and restoration iterations as the oracle, at the same point."""
+    from agentlib_mpc_amd import benchmarks as bm
+
+    tight = setting == "tight"
+    case = configs.CASES[name](solver_options=bm.TIGHT if tight else bm.REFERENCE, **kw)
+    p, lbw, ubw, w0 = case.oracle_inputs
+    opts = ipm.IPMOptions(tol=1e-10, max_iter=500, acceptable_iter=0) if tight else ipm.IPMOptions(**REFERENCE_OPTS)
+    ref = ipm.solve(case.oracle.functions(p), w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), opts)
+    assert ref.n_resto > 0
+    res = _gpu_solve(case, n_copies=2)
+    for r in res:
+        st = r.stats
+        got = (st["return_status"], st["iter_count"], st["n_soft_restorations"], st["n_restorations"],
+               st["n_restoration_iters"])
+        assert got == (ref.status, ref.iterations, ref.n_soft_resto, ref.n_resto, ref.resto_iterations), got
+        np.testing.assert_allclose(st["obj"], ref.f, rtol=RTOL_OBJ, atol=1e-9)
+        w = _w_of(case, r)
+        np.testing.assert_allclose(w, ref.x, rtol=RTOL_TRAJ, atol=1e-7 * max(1.0, np.abs(ref.x).max()))
+
+
 def test_acceptable_stop_occurs_at_reference_defaults():
     """At least one benchmark agent NLP ends at the acceptable level (kernel side)."""
     from agentlib_mpc_amd import benchmarks as bm

@@ -148,3 +148,48 @@ def test_host_build_of_generated_model_takes_the_oracle_path(name):
     assert names.get(st[0]["status"]) == ref.status
     assert st[0]["iter"] == ref.iterations
     np.testing.assert_allclose(st[0]["obj"], ref.f, rtol=1e-9, atol=1e-12)
+
+
+def _cubic(lo=-np.inf, hi=np.inf):
+    """min x^2 s.t. x^3 - 3x - 5 = 0: Newton from x < 1 is drawn to x = -1, the local
+    minimum of the infeasibility (the classic restoration-phase example)."""
+    return ipm.NLPFunctions(1, 1, lambda x: x[0] ** 2, lambda x: np.array([2 * x[0]]),
+                            lambda x: np.array([x[0] ** 3 - 3 * x[0] - 5]), lambda x: np.array([[3 * x[0] ** 2 - 3]]),
+                            lambda x, s, l: np.array([[2 * s + 6 * x[0] * l[0]]]))
+
+
+def test_restoration_phase_returns_and_converges():
+    """IPOPT's feasibility restoration phase (oracle/ipm.py `_RestoNLP`): from x = -1.2 the
+    filter line search fails; restoration leaves the basin of x = -1 and hands a point
+    acceptable to the original filter back, from which the solver converges to the root."""
+    r = ipm.solve(_cubic(), np.array([-1.2]), np.array([-np.inf]), np.array([np.inf]), np.zeros(1), np.zeros(1),
+                  ipm.IPMOptions(tol=1e-8))
+    assert r.status == "Solve_Succeeded" and r.n_resto == 1 and r.resto_iterations > 0
+    np.testing.assert_allclose(r.x, [2.279018786], rtol=1e-8)
+
+
+def test_restoration_phase_detects_local_infeasibility():
+    """x^2 + 1 = 0 has no solution: restoration converges to the minimiser of |c| (x = 0)
+    and the solve ends Infeasible_Problem_Detected (IPOPT: "Converged to a point of local
+    infeasibility")."""
+    nlp = ipm.NLPFunctions(1, 1, lambda x: (x[0] - 1) ** 2, lambda x: np.array([2 * (x[0] - 1)]),
+                           lambda x: np.array([x[0] ** 2 + 1]), lambda x: np.array([[2 * x[0]]]),
+                           lambda x, s, l: np.array([[2 * s + 2 * l[0]]]))
+    r = ipm.solve(nlp, np.array([3.0]), np.array([-np.inf]), np.array([np.inf]), np.zeros(1), np.zeros(1),
+                  ipm.IPMOptions(tol=1e-8))
+    assert r.status == "Infeasible_Problem_Detected" and r.n_resto >= 1
+    assert abs(r.x[0]) < 1e-6
+
+
+def test_restoration_phase_on_a_stage_nlp():
+    """The restoration case of the GPU parity tests on the oracle alone: the cubic zone
+    (tests/configs.cubic_room) restores twice and converges; the cubic rows end at the root."""
+    from tests import configs
+
+    case = configs.cubic_room()
+    p, lbw, ubw, w0 = case.oracle_inputs
+    r = ipm.solve(case.oracle.functions(p), w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p),
+                  ipm.IPMOptions(tol=1e-10, max_iter=500, acceptable_iter=0))
+    assert r.status == "Solve_Succeeded" and r.n_resto == 2
+    z = r.x[[i for i, n in enumerate(case.oracle.w_names) if n.startswith("z@")]]
+    np.testing.assert_allclose(z, 2.279018786, rtol=1e-7)

@@ -30,6 +30,7 @@ EXPECTED_DIMS = {  # SURVEY §8a A6/A7 (hand-derived from the reference code)
     "mhe_room_u": (2 + 15 * 15, 15 * 14, 11 + 15 * 8),  # MHE estimating mDot per interval
     "rng_room_mpc": (2 + 15 * 15, 15 * 14, 12 + 15 * 8),  # two-state zone + wall MPC (nx > nu)
     "fixture_mpc": (1 + 5 * (1 + 3 * 2 + 1), 5 * (1 + 3 * 2), 4 + 5 * 3),  # reference test-suite model
+    "cubic_room": (1 + 4 * (1 + 2 * 2 + 1), 4 * (1 + 2 * 2), 2),  # restoration-phase case
 }
 
 

@@ -3420,7 +3420,7 @@ extern "C" __global__ void mpcx_query(long* out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     out[0] = WS_DOUBLES;
     out[1] = N; out[2] = NX; out[3] = NV; out[4] = NG; out[5] = NPS; out[6] = NPG;
-    out[7] = MPCX_ABI;
+    out[7] = MPCX_KERNEL_ABI;  // one definition (mpcx_internal.h), checked by mpcx_problem_create
     out[8] = sizeof(Lds);
   }
 }

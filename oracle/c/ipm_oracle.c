@@ -753,10 +753,13 @@ static void solve_one(const model_t* m, const double* p, const double* lbw, cons
     }
     /* IPOPT: restoration phase called at an acceptable point -> Solved_To_Acceptable_Level */
     if (!accepted && current_is_acceptable(&acc, o, square, err, du, pu, cmpl, fx, it)) { status = 1; break; }
-    /* no acceptable trial and the last one is not even finite: IPOPT would enter
-       restoration; stop with Restoration_Failed at the current (finite) iterate */
-    if (!accepted && !(isfin(last_th) && isfin(last_ph))) { status = -2; break; }
-    if (!accepted) { nfilt = 0; ftype = 1; }
+    /* The filter line search failed: IPOPT tries the soft restoration step and then its
+       feasibility restoration phase (restated in oracle/ipm.py and in the kernel).  This C
+       restatement serves the CPU baselines and the fleet checkers, on fleets where no agent
+       gets here (the bench legs and tests/test_gpu_ipm.py assert it): it stops with its own
+       status -6 "Restoration_Required" instead, so that reaching this point can never pass
+       for a result. */
+    if (!accepted) { status = -6; (void)last_th; (void)last_ph; break; }
     if (!ftype) {
       if (nfilt == 32) { for (int j = 1; j < 32; ++j) { fth[j - 1] = fth[j]; fph[j - 1] = fph[j]; } nfilt--; }
       fth[nfilt] = (1 - 1e-5) * theta; fph[nfilt] = phi - 1e-8 * theta; nfilt++;

@@ -34,7 +34,7 @@ def test_library_builds_loads_and_exports_all_symbols():
 def test_struct_sizes_match_header():
     # mpcx_options: 40 doubles + 4 int32; mpcx_stats: 6 doubles + 8 int32
     assert ctypes.sizeof(native.Options) == 40 * 8 + 4 * 4
-    assert ctypes.sizeof(native.Stats) == 6 * 8 + 8 * 4
+    assert ctypes.sizeof(native.Stats) == 6 * 8 + 10 * 4
     assert ctypes.sizeof(native.ProblemDesc) == 8 * 4
 
 
@@ -61,3 +61,15 @@ def test_product_path_has_no_cpu_fallback(monkeypatch):
     monkeypatch.setattr(native, "_lib", None)
     with pytest.raises(native.NativeError):
         native.load_library()
+
+
+def test_kernel_abi_versions_agree():
+    """The code objects report MPCX_KERNEL_ABI (csrc/mpcx_internal.h); the Python binding and
+    the generated sources must use the same number (mpcx_problem_create rejects a mismatch)."""
+    import re
+
+    from agentlib_mpc_amd.runtime import codegen, native
+
+    text = (native.CSRC / "mpcx_internal.h").read_text()
+    abi = int(re.search(r"#define MPCX_KERNEL_ABI (\d+)", text).group(1))
+    assert native.KERNEL_ABI == abi == codegen.KERNEL_ABI_VERSION

@@ -7,11 +7,13 @@ Mirrors the reference's objective API (`agentlib_mpc/data_structures/objective.p
 post-hoc evaluation ``calculate_values`` that the backends write into the stats
 file (``obj_<name>`` columns, `core/casadi_backend.py:291-323`).
 
-Evaluation deviates in one respect, deliberately: the reference re-parses the
-``str()`` of a CasADi expression with ``eval`` (and squares the whole term when
-the string contains ``sq(``, :166-224); here the traced expression is evaluated
-numerically on the result grid, which gives the same value for the reference's
-single-term objectives and the mathematically correct one otherwise.
+Evaluation: the reference re-parses the ``str()`` of a CasADi expression with
+``eval`` and, when the string contains ``sq(``, evaluates it with every ``sq(``
+read as ``(`` and squares the whole term (:166-224) -- for a term that mixes a
+square with other operations that is not the term's value.  The traced
+expression is evaluated numerically on the result grid with the same rule
+(``REFERENCE_SQ_RULE = True``, so the ``obj_<name>`` stats columns equal the
+reference's); set it to False for the term's mathematical value.
 """
 
 from __future__ import annotations
@@ -23,6 +25,10 @@ import numpy as np
 import pandas as pd
 
 from agentlib_mpc_amd import symbolic as sx
+
+
+#: evaluate a term containing sq() the reference's way (squares removed, whole term squared)
+REFERENCE_SQ_RULE = True
 
 
 def _column(df, name):
@@ -122,7 +128,13 @@ class SubObjective:
         """Rectangle rule over the result grid (`objective.py:135-139`)."""
         ts = np.diff(data.index.to_numpy(dtype=float))
         try:
-            result = _evaluate_on(data, self.expression)
+            expr = self.expression.sym if hasattr(self.expression, "sym") else self.expression
+            squared = False
+            if REFERENCE_SQ_RULE:
+                expr, squared = sx.strip_squares(expr)
+            result = _evaluate_on(data, expr)
+            if squared:
+                result = result ** 2
         except KeyError:
             if self.name not in SubObjective._warned_names:
                 warnings.warn(f"Unable to evaluate expression {self.name}. Some terms will be ignored when "

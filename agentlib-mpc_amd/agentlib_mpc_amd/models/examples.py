@@ -13,7 +13,8 @@ Equations restate the reference examples:
 
 from __future__ import annotations
 
-from typing import List
+import os
+from typing import List, Optional
 
 import numpy as np
 
@@ -286,8 +287,23 @@ def synthetic_ann(features: dict, seed: int, hidden: int = 32, dt: float = 1800.
     return SerializedANN.from_layers(layers, dt=dt, input=inputs, output=outputs)
 
 
-def room_cca_anns(seed: int = 20261015 + 5):
-    """The two shared networks of the C5 zones (T_air and T_CCA_0)."""
+def trained_anns():
+    """The two networks of the C5 zones trained as the example trains them
+    (`three_zone_datadriven_admm/training_direct.py:553-642`: white-box simulation data,
+    BatchNormalization -> Dense(32, sigmoid) -> Dense(1), MSE/Adam, 400 epochs), produced
+    by ``scripts/train_c5_anns.py`` and stored in the reference's ``ml_model.json`` format."""
+    from agentlib_mpc_amd.models.serialized_ml_model import SerializedMLModel
+
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+    return [SerializedMLModel.load_serialized_model_from_file(os.path.join(here, f))
+            for f in ("ann_t_air.json", "ann_t_cca.json")]
+
+
+def room_cca_anns(seed: Optional[int] = None):
+    """The two shared networks of the C5 zones (T_air and T_CCA_0): the trained ones by
+    default, seeded synthetic ones of the same topology when ``seed`` is given."""
+    if seed is None:
+        return trained_anns()
     return [synthetic_ann(T_AIR_FEATURES, seed), synthetic_ann(T_CCA_FEATURES, seed + 1)]
 
 

@@ -41,7 +41,7 @@ class FleetSession:
         dev = torch.device(device)
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
         self.p, self.lbw, self.ubw, self.w = T(kp), T(kl), T(ku), T(kw)
-        self.lbw_ref = lbw  # reference-layout bounds (fixed variables the kernel NLP drops)
+        self.lbw_ref = np.array(lbw, dtype=np.float64)  # reference-layout bounds (fixed variables the kernel NLP drops)
         self.dev = dev
         self._maps: Dict[str, List[Tuple[str, np.ndarray]]] = {}
         self._lam_g = self._stats = None
@@ -66,9 +66,13 @@ class FleetSession:
             cv[name] = copy.copy(self.template[name])
             cv[name].value = v
             probe.append(cv)
-        outs = prob.to_kernel(*prob.marshal.inputs(probe, self.now))
+        ref = prob.marshal.inputs(probe, self.now)
+        outs = prob.to_kernel(*ref)
         maps = []
-        for key, arr in zip(("p", "lbw", "ubw"), outs[:3]):
+        # reference-layout lower bounds: solution() rebuilds the variables the kernel NLP
+        # drops (fixed past values of lifted NARX problems) from them
+        outs = tuple(outs[:3]) + (ref[1],)
+        for key, arr in zip(("p", "lbw", "ubw", "lbw_ref"), outs):
             a0, a1 = arr[0], arr[1]
             changed = np.flatnonzero(~((a0 == a1) | (np.isnan(a0) & np.isnan(a1))))
             if changed.size:
@@ -86,6 +90,9 @@ class FleetSession:
         if v.shape != (self.n,):
             raise ValueError(f"{name}: expected {self.n} values, got shape {tuple(v.shape)}")
         for key, cols in self.columns_of(name):
+            if key == "lbw_ref":
+                self.lbw_ref[:, cols] = np.asarray(values, dtype=np.float64)[:, None]
+                continue
             arr = getattr(self, key)
             idx = torch.as_tensor(cols, device=self.dev)
             arr[:, idx] = v[:, None].expand(-1, idx.numel())

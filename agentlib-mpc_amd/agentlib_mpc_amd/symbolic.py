@@ -511,6 +511,24 @@ def substitute(outputs: Sequence[Expr], mapping: Dict[Expr, Union[Expr, float]])
     return [memo[o.uid] for o in outs]
 
 
+def strip_squares(e) -> Tuple[Expr, bool]:
+    """``e`` with every ``sq(a)`` node replaced by ``a``, and whether there was one: the
+    reference's stats evaluator turns the printed ``sq(`` into ``(`` and squares the
+    whole term instead (`data_structures/objective.py:166-224`)."""
+    e = as_expr(e)
+    memo: Dict[int, Expr] = {}
+    found = False
+    for node in topo_order([e]):
+        if node.op in ("sym", "const"):
+            memo[node.uid] = node
+        elif node.op == "sq":
+            memo[node.uid] = memo[node.args[0].uid]
+            found = True
+        else:
+            memo[node.uid] = _rebuild(node.op, [memo[a.uid] for a in node.args])
+    return memo[e.uid], found
+
+
 def _rebuild(op: str, args: List[Expr]) -> Expr:
     if op.startswith("ann"):
         return Expr(op, tuple(args))

@@ -212,7 +212,7 @@ def nn_bench(args, world, rank, dev):
     prob = be.problem
     rng = np.random.default_rng(20261015 + 5 + rank)
     vals = {"T_air": rng.uniform(292.0, 297.0, n), "d": rng.uniform(50.0, 200.0, n),
-            "T_amb": rng.uniform(295.0, 303.0, n), "Q_rad": rng.uniform(0.0, 200.0, n)}
+            "T_amb": rng.uniform(295.0, 303.0, n), "Q_rad": rng.uniform(0.0, 50.0, n)}
     p, lbw, ubw, w0 = prob.to_kernel(*fleet_nlp_inputs(prob, cv, vals))
     stats, wall, kernel_ms = _timed_batch(be, prob, p, lbw, ubw, w0, n, args, dev)
     ok = sum(1 for s in stats if s["success"])

@@ -2,8 +2,9 @@
 ``python tests/golden/make_c5_admm_golden.py 24``): the coordinated ADMM round of one
 three-zone block (3 NARX zones + AHU + CCA) computed by the ORACLE (hand
 restatements `oracle/nlps.py` + oracle IPM + the coordinator-loop restatement
-`oracle/admm.py`), N=8, rho=1, 3 iterations, absolute criterion
-(`three_zone_datadriven_admm/configs/coordinator.json`: primal_tol = dual_tol = 0.04).
+`oracle/admm.py`), N=8, rho=1, to the stopping rule of
+`three_zone_datadriven_admm/configs/coordinator.json` (admm_iter_max 50, absolute
+criterion primal_tol = dual_tol = 0.04), with the trained networks of `models/data/`.
 The oracle takes minutes on a CPU, so the GPU test reads this fixture.
 
 Run from the repository root: ``python tests/golden/make_c5_admm_golden.py``.
@@ -22,7 +23,8 @@ from oracle import admm as oadmm  # noqa: E402
 from tests.admm_cases import C5Oracle  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-ITERS, RHO = 3, 1.0
+ITERS = int(sys.argv[2]) if len(sys.argv) > 2 else 50  # the example's admm_iter_max
+RHO = 1.0
 
 
 def main():
@@ -30,7 +32,7 @@ def main():
     state, hist, it, conv = oadmm.coordinated_round(
         orc.participation, orc.initial, orc, RHO, N, ITERS, primal_tol=0.04, dual_tol=0.04,
         use_relative_tolerances=False, T=N)
-    out = {"N": N, "iterations": it, "converged": conv, "rho": RHO,
+    out = {"N": N, "iterations": it, "converged": conv, "rho": RHO, "admm_iter_max": ITERS,
            "history": [[float(a), float(b)] for a, b, _ in hist],
            "means": {al: list(map(float, v.mean)) for al, v in state["vars"].items()},
            "mult_ahu": {al: list(map(float, state["vars"][al].mult["ahu"])) for al in orc.ahu_al}}

@@ -42,7 +42,25 @@ def test_scalar_updates_match_remarshalling():
     np.testing.assert_array_equal(s.p.numpy(), kp)
     np.testing.assert_array_equal(s.lbw.numpy(), kl)
     np.testing.assert_array_equal(s.ubw.numpy(), ku)
-    assert {k for k, _ in s.columns_of("T")} == {"p", "lbw", "ubw"}   # initial state: parameter + x_0 bounds
+    # initial state: parameter + x_0 bounds (kernel layout and the reference-layout copy)
+    assert {k for k, _ in s.columns_of("T")} == {"p", "lbw", "ubw", "lbw_ref"}
+
+
+def test_lifted_updates_keep_the_reference_layout_bounds():
+    """NARX (lifted): inputs that fix past values the kernel NLP drops must reach the
+    reference-layout bounds too, from which solution() rebuilds those variables."""
+    be, cv = bm.room_nn(solver_options=bm.REFERENCE)
+    agents = [copy.deepcopy(cv) for _ in range(3)]
+    s = FleetSession(be, agents, device="cpu")
+    names = ["T_air", "T_CCA_0"] + [k for k in cv if k.startswith("admm_lag_")]
+    rng = np.random.default_rng(2)
+    for name in names:
+        new = rng.uniform(290.0, 300.0, 3)
+        s.update(name, new)
+        for a, c in enumerate(agents):
+            c[name].value = float(new[a])
+    _, lbw_ref, _, _ = be.problem.marshal.inputs(agents, 0.0)
+    np.testing.assert_array_equal(s.lbw_ref, lbw_ref)
 
 
 def test_update_rejects_wrong_shape_and_non_scalar_inputs():

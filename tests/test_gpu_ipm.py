@@ -52,7 +52,7 @@ def _cuda():
     ("exchange_supply", {}),
     ("exchange_supply", {"diff": -0.01, "lam": 20.0}),
     ("room_nn", {}),
-    ("room_nn", {"T_air": 296.5, "load": 180.0, "Q_rad": 150.0, "q_T": 1.0,
+    ("room_nn", {"T_air": 296.5, "load": 180.0, "Q_rad": 40.0, "q_T": 1.0,
                  "zbar": [296.0, 293.0, 295.0, 296.0], "lam": [0.5, -0.2, 0.1, 0.0]}),
     # N=23 has no super-stage length dividing it: copy-lifted stages (shift rows bordered)
     ("room_nn", {"N": 23}),

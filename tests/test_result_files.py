@@ -96,3 +96,27 @@ def test_coordinator_residual_file_roundtrip(tmp_path):
     ADMMFleet.save_stats(None, f, 0.0, recs)
     df = pd.read_csv(f, index_col=0)
     assert [ast.literal_eval(i) for i in df.index] == [(0.0, 0)]
+
+
+def test_objective_term_with_a_square_follows_the_reference_rule():
+    """A term mixing sq() with other operations: the reference evaluates the printed
+    expression with ``sq(`` read as ``(`` and squares the whole term
+    (`objective.py:166-224`), e.g. ``mDot + sq(T_slack)`` -> ``(mDot + T_slack)**2``;
+    ``REFERENCE_SQ_RULE = False`` gives the term's own value."""
+    from agentlib_mpc_amd import symbolic as sx
+    from agentlib_mpc_amd.data_structures import objective as ob
+
+    m, s = sx.sym("mDot"), sx.sym("T_slack")
+    grid = np.array([0.0, 300.0, 600.0, 900.0])
+    cols = pd.MultiIndex.from_tuples([("variable", "mDot"), ("variable", "T_slack")])
+    df = pd.DataFrame(np.array([[0.01, 0.5], [0.02, -1.0], [0.03, 2.0], [0.04, 0.0]]), index=grid, columns=cols)
+    term = ob.SubObjective(m + s ** 2, weight=2.0, name="mixed")
+    u, t = df[("variable", "mDot")].to_numpy()[:-1], df[("variable", "T_slack")].to_numpy()[:-1]
+    assert term.calculate_value(df, 2.0) == pytest.approx(float(np.sum(2.0 * (u + t) ** 2 * 300.0)), rel=1e-14)
+    pure = ob.SubObjective(s ** 2, weight=1.0, name="pure")  # a pure square is unaffected
+    assert pure.calculate_value(df, 1.0) == pytest.approx(float(np.sum(t ** 2 * 300.0)), rel=1e-14)
+    try:
+        ob.REFERENCE_SQ_RULE = False
+        assert term.calculate_value(df, 2.0) == pytest.approx(float(np.sum(2.0 * (u + t ** 2) * 300.0)), rel=1e-14)
+    finally:
+        ob.REFERENCE_SQ_RULE = True

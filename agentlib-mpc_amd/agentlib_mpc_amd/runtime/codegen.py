@@ -499,6 +499,9 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
         "// >>> device only: static sparse elimination of the stage interior (runtime/stage_elim.py):",
         f"// {len(elim_plan.blocks)} pivot blocks, {elim_plan.n_update} interior updates, {elim_plan.nnz_l} multipliers",
         "#define MPCX_STATIC_ELIM 1",
+        "#ifndef MPCX_ELIM_GROWTH  // threshold-pivoting bound on the static multipliers (runtime/stage_elim.py)",
+        "#define MPCX_ELIM_GROWTH 1e8",
+        "#endif",
         "#ifndef MPCX_ELIM_FENCE  // scheduling fence between pivot blocks (register pressure)",
         "#define MPCX_ELIM_FENCE __builtin_amdgcn_sched_barrier(0)",
         "#endif",

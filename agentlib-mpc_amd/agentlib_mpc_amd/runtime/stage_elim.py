@@ -43,7 +43,7 @@ ZERO_PIVOT = "1e-20"  # same constant as the kernel's ZERO_PIVOT (dense path)
 #: small against its column -- e.g. a variable paired with a row that is open at this stage
 #: (MHE stage 0: D ~ 1e16) -- would amplify rounding errors past the inertia test; the
 #: stage is then factored densely with Bunch-Kaufman pivoting instead
-GROWTH = "1e8"
+GROWTH = "MPCX_ELIM_GROWTH"  # 1e8 unless the build defines it (diagnostics)
 #: scheduling fence between pivot blocks / substitution sweeps: keeps the live set (and the
 #: callee-saved VGPRs the non-inlined caller would have to spill) small
 SCHED = "  MPCX_ELIM_FENCE;"  # __builtin_amdgcn_sched_barrier(0) unless overridden (codegen.py)

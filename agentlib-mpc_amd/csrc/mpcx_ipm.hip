@@ -163,6 +163,12 @@ using Args = mpcx_kernel_args;
 // loads); passing the by-value kernel parameter by reference would make the
 // compiler copy all of it (~400 B) into every lane's scratch
 using KArgs = const __attribute__((address_space(4))) Args;
+// wave-uniform 64-bit value into SGPRs
+__device__ __forceinline__ unsigned long long uni64(unsigned long long v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
 
 // ---------------------------------------------------------------------------
 // wave and lane-group helpers
@@ -341,6 +347,11 @@ struct LdsRest {
   double neto[MPCX_NETO];  // network values / derivatives of the current evaluation
 #endif
   KState ks;
+  // the kernarg segment and the agent's workspace slab, written once by the kernel: the
+  // phases read them here (into SGPRs) instead of taking pointer arguments, which the calling
+  // convention passes in VGPRs, callee-saved -- spilled to scratch -- when live across a call
+  // (the kernarg segment pointer itself is not an implicit input of called functions)
+  unsigned long long kp_bits, ws_bits;
 #ifdef MPCX_PROFILE
   double sprof[6];
   unsigned int dense_seen[2];  // stages ever rejected by the static plan (profile build)
@@ -431,22 +442,53 @@ static_assert(sizeof(Lds) + LDS_SLACK <= LDS_CU / APC, "LDS share per agent exce
 #endif
 
 __shared__ Lds gL;  // one agent per workgroup: the agent's LDS scratch
+__device__ __forceinline__ KArgs* kargs() { return (KArgs*)uni64(gL.kp_bits); }
+__device__ __forceinline__ gdbl* ws_base() { return (gdbl*)uni64(gL.ws_bits); }
 #define LDSP(x) ((ldsd*)(x))
 #define LDSI(x) ((ldsi*)(x))
 #ifdef MPCX_PROFILE
 #define SPROF_DECL unsigned long long _st = __builtin_amdgcn_s_memtime();
-#define SPROF(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); if (a.lane == 0) gL.sprof[i] += (double)(_n - _st); _st = _n; } while (0)
+#define SPROF(i) do { const unsigned long long _n = __builtin_amdgcn_s_memtime(); if (lane_now() == 0) gL.sprof[i] += (double)(_n - _st); _st = _n; } while (0)
 #else
 #define SPROF_DECL
 #define SPROF(i) do { } while (0)
 #endif
+// Diagnostic build only (-DMPCX_TRACE_LS, scripts/resto_diag.py): the last line search of
+// each agent is written to lam_w (header: theta, phi, gphi'd, alpha_min, theta_min, theta_max,
+// mu, filter size, then the filter pairs) and lam_g (per trial: alpha, theta, phi, filter
+// test, acceptance, f-type) instead of the multipliers.
+#ifdef MPCX_TRACE_LS
+#define TRACE_LS_HEAD(argp)                                                                      \
+  do {                                                                                           \
+    if (lane_now() == 0 && (*argp).lam_w != nullptr) {                                           \
+      gdbl* h = (gdbl*)(*argp).lam_w + (long)blockIdx.x * NW;                                    \
+      const double hv[8] = {K.st.theta, K.fx - K.mu * K.st.barrier, K.st.gphid, K.amin,          \
+                            K.theta_min, K.theta_max, K.mu, (double)K.nfilt};                    \
+      for (int q = 0; q < 8 && q < NW; ++q) h[q] = hv[q];                                        \
+      for (int j = 0; j < K.nfilt && 10 + 2 * j + 1 < NW; ++j) { h[10 + 2 * j] = gL.fth[j]; h[11 + 2 * j] = gL.fph[j]; } \
+      if (NW > 9) { h[8] = K.dw; h[9] = K.dc; }                                                  \
+    }                                                                                            \
+  } while (0)
+#define TRACE_LS_TRIAL(argp, alpha, tr, okf, okt, ft)                                            \
+  do {                                                                                           \
+    const int t_ = K.ls.trials - 1;                                                              \
+    if (lane_now() == 0 && (*argp).lam_g != nullptr && 6 * t_ + 5 < M) {                         \
+      gdbl* g = (gdbl*)(*argp).lam_g + (long)blockIdx.x * M + 6 * t_;                            \
+      g[0] = (alpha); g[1] = (tr).theta; g[2] = (tr).phi; g[3] = (okf); g[4] = (okt); g[5] = (ft); \
+    }                                                                                            \
+  } while (0)
+#else
+#define TRACE_LS_HEAD(argp) do { } while (0)
+#define TRACE_LS_TRIAL(argp, alpha, tr, okf, okt, ft) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
-// per-agent views (by value: two global pointers and the lane)
+// per-agent view: the workspace slab (wave-uniform, from LDS into SGPRs); lanes by lane_now()
 // ---------------------------------------------------------------------------
 struct Agent {
-  gdbl* ws;
-  int lane;
+  // the agent's workspace slab, wave-uniform (SGPRs): nothing of the view is passed in VGPRs
+  __device__ __forceinline__ gdbl* base() const { return ws_base(); }
+#define ws base()
   __device__ gdbl* x() const { return ws + O_X; }
   __device__ gdbl* s() const { return ws + O_S; }
   __device__ gdbl* lam() const { return ws + O_LAM; }
@@ -495,6 +537,7 @@ struct Agent {
   __device__ gdbl* vl0() const { return ws + O_VL0; }
   __device__ gdbl* vu0() const { return ws + O_VU0; }
   __device__ gdbl* flt0() const { return ws + O_FLT0; }
+#undef ws
 };
 
 // constraint classes: 0 equality, 1 inequality with a finite bound, 2 free
@@ -517,7 +560,7 @@ __device__ __forceinline__ const double* par_global() { return (const double*)gL
 #ifdef MPCX_NET_MFMA
 #define NET_PREP(pt, kind)                                                                  \
   do {                                                                                      \
-    for (int k = a.lane; k < N; k += WAVE)                                                  \
+    for (int k = lane_now(); k < N; k += WAVE)                                                  \
       gen_stage_netin((const double*)((pt) + k * NP), par_stage(k), par_global(), k * TS,   \
                       (double*)gL.netx, k);                                                 \
     wsync();                                                                                \
@@ -538,7 +581,7 @@ __device__ __forceinline__ const double* par_global() { return (const double*)gL
 __device__ __noinline__ double eval_fg_lds(const Agent a) {
   NET_PREP(gL.u.t.xt, fg);
   double f = 0.0;
-  for (int k = a.lane; k < N; k += WAVE) {
+  for (int k = lane_now(); k < N; k += WAVE) {
     double fk = 0.0;
     STAGE_FG((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS, &fk,
              (double*)(gL.u.t.gt + k * NG), 1);
@@ -551,7 +594,7 @@ __device__ __noinline__ double eval_fg_lds(const Agent a) {
 __device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* gout) {
   NET_PREP(xv, fg);
   double f = 0.0;
-  for (int k = a.lane; k < N; k += WAVE) {
+  for (int k = lane_now(); k < N; k += WAVE) {
     double fk = 0.0;
     STAGE_FG((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, &fk, (double*)(gout + k * NG), 1);
     f += fk;
@@ -563,7 +606,7 @@ __device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* g
 // the block-chain fallback read it; the stage-parallel path reads lp and jtl only)
 __device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv, int full) {
   NET_PREP(xv, gj);
-  for (int k = a.lane; k < N; k += WAVE)
+  for (int k = lane_now(); k < N; k += WAVE)
     STAGE_GJ((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, (double*)(a.sdg() + k),
              (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG), (double*)a.lp(k),
              (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
@@ -573,7 +616,7 @@ __device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv, int full)
 __device__ __noinline__ void eval_gj_lds(const Agent a) {
   NET_PREP(gL.u.t.xt, gj);
   const int full = gL.want_sdh;
-  for (int k = a.lane; k < N; k += WAVE)
+  for (int k = lane_now(); k < N; k += WAVE)
     STAGE_GJ((const double*)(gL.u.t.xt + k * NP), par_stage(k), par_global(), k * TS,
              (double*)(a.sdg() + k), (double*)(a.sdj() + k), N, (const double*)(a.gs() + k * NG),
              (double*)a.lp(k), (const double*)(a.lam() + k * NG), (double*)(a.jtl() + k), full);
@@ -584,14 +627,14 @@ __device__ __noinline__ void eval_gj_lds(const Agent a) {
 // are written when that path is in use, or on demand (eval_hess_full)
 __device__ __noinline__ void eval_hess_impl(const Agent a, double sigma, int full) {
   NET_PREP(a.x(), hess);
-  for (int k = a.lane; k < N; k += WAVE) {
+  for (int k = lane_now(); k < N; k += WAVE) {
     double lk[NG > 0 ? NG : 1];
 #pragma unroll
     for (int r = 0; r < NG; ++r) lk[r] = a.lam()[k * NG + r] * a.gs()[k * NG + r];
     STAGE_HESS((const double*)(a.x() + k * NP), par_stage(k), par_global(), k * TS, sigma, lk,
                (double*)(a.sdh() + k), N, (double*)a.lp(k), full);
   }
-  if (a.lane == 0) { gL.hsig = sigma; gL.sdh_ok = full; }
+  if (lane_now() == 0) { gL.hsig = sigma; gL.sdh_ok = full; }
 }
 __device__ __forceinline__ void eval_hess(const Agent a, double sigma) { eval_hess_impl(a, sigma, gL.want_sdh); }
 
@@ -896,13 +939,13 @@ __device__ __forceinline__ double dual_diag_v(int cl, double sig, const KKTDiag 
 // ---------------------------------------------------------------------------
 // per-variable / per-constraint diagonal terms (workspace; NaN in kx marks a fixed variable)
 __device__ __noinline__ void kkt_diagonals(const Agent a, const KKTDiag kd) {
-  for (int q = a.lane; q < N * NP; q += WAVE) {
+  for (int q = lane_now(); q < N * NP; q += WAVE) {
     const int i = NX + q;
     const double lo = a.xL()[i], hi = a.xU()[i];
     a.kx()[q] = (lo == hi) ? NAN
                            : (kd.mode == LSQ ? 1.0 : sigma_x_v(a.x()[i], lo, hi, a.zL()[i], a.zU()[i]) + kd.dw);
   }
-  for (int c = a.lane; c < M; c += WAVE) {
+  for (int c = lane_now(); c < M; c += WAVE) {
     const double sl = a.sL()[c], su = a.sU()[c];
     const int cl = cls_of(a.lb()[c], a.ub()[c], sl, su);
     a.kd()[c] = dual_diag_v(cl, sigma_s_v(a.s()[c], sl, su, a.vL()[c], a.vU()[c]), kd);
@@ -947,12 +990,12 @@ constexpr int NB2 = NB * NB;
 constexpr int EPL = (NB2 + WAVE - 1) / WAVE;  // block elements per lane
 
 __device__ __noinline__ void seq_assemble(const Agent a, Mode mode) {
-  for (int t = a.lane; t < N * NB2; t += WAVE) {
+  for (int t = lane_now(); t < N * NB2; t += WAVE) {
     const int k = t / NB2, e = t % NB2, i = e / NB, j = e % NB;
     a.fac(k)[i * LDB + j] = kkt_entry(a, k, i, j, mode);
   }
   if (NX > 0) {
-    for (int t = a.lane; t < N * NB * NX; t += WAVE) {
+    for (int t = lane_now(); t < N * NB * NX; t += WAVE) {
       const int k = t / (NB * NX), e = t % (NB * NX);
       a.cpl(k)[e] = coupling(a, k, e / NX, e % NX, mode);
     }
@@ -967,7 +1010,7 @@ __device__ __noinline__ Inertia seq_factor(const Agent a, const KKTDiag kd) {
     return Inertia{0, 0, 1};
   } else {
     SeqLds& L = gL.u.s;
-    const int lane = a.lane;
+    const int lane = lane_now();
     Inertia in{0, 0, 0};
     kkt_diagonals(a, kd);
     seq_assemble(a, kd.mode);
@@ -1027,7 +1070,7 @@ __device__ __noinline__ Inertia seq_factor(const Agent a, const KKTDiag kd) {
 __device__ __noinline__ void seq_solve(const Agent a) {
   if constexpr (NX > 0) {
     SeqLds& L = gL.u.s;
-    const int lane = a.lane;
+    const int lane = lane_now();
 #pragma unroll 1
     for (int k = 0; k < N; ++k) {
       for (int i = lane; i < NB; i += WAVE) {
@@ -1119,7 +1162,7 @@ __device__ __forceinline__ int lblk(int i, int kind) {
 template <int GG, bool COMPACT>
 __device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd* F, const KKTDiag kd,
                                                unsigned long long fm) {
-  const gdbl* ws = a.ws;
+  const gdbl* ws = a.base();
   for (int i = g; i < NLOC; i += GG) {
     const int ki = lkind(i);
     const bool prim = (ki == 0 || ki == 3);
@@ -1141,7 +1184,7 @@ __device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd
 // derivative arrays (least-squares multiplier system; diagonal terms added afterwards)
 __device__ __forceinline__ double generic_entry(const Agent a, int k, int i, int j, unsigned long long fm,
                                                 const KKTDiag kd) {
-  const gdbl* ws = a.ws;
+  const gdbl* ws = a.base();
   const int ki = lkind(i), kj = lkind(j);
   const bool pi = (ki == 0 || ki == 2 || ki == 3), pj = (kj == 0 || kj == 2 || kj == 3);
   const bool fi = pi && ((fm >> i) & 1ull), fj = pj && ((fm >> j) & 1ull);
@@ -1457,7 +1500,7 @@ __device__ __forceinline__ const double* s10(int k) { return (const double*)(gL.
 __device__ __noinline__ Inertia chain_factor(const Agent a) {
   Lds& L = gL;
   Inertia in{0, 0, 0};
-  const int lane = a.lane;
+  const int lane = lane_now();
   if constexpr (NX == 1 && NMU == 0) {
     // scalar chain d_j = a_j - b_j / d_{j-1}: lane j gathers its terms in parallel, the
     // recurrence runs on broadcast registers (readlane), fully unrolled
@@ -1521,7 +1564,7 @@ __device__ __noinline__ Inertia chain_factor(const Agent a) {
 
 __device__ __noinline__ void chain_solve(const Agent a) {
   Lds& L = gL;
-  const int lane = a.lane;
+  const int lane = lane_now();
   constexpr int ZS = NX + NC;  // zx stride per stage: [x_k | c_k]
   // rhs_j = z[c] of stage j + E z[x_k] of stage j+1
   if constexpr (NX == 1 && NMU == 0) {
@@ -1659,8 +1702,8 @@ __device__ __forceinline__ int nth_bit(unsigned long long m, int q) {
 __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   Lds& L = gL;
   SPROF_DECL
-  if (a.lane < 4) L.fin[a.lane] = 0;  // inertia (pos, neg, zero) and singular flag, summed in LDS
-  if (a.lane < 2) L.dmask[a.lane] = 0u;
+  if (lane_now() < 4) L.fin[lane_now()] = 0;  // inertia (pos, neg, zero) and singular flag, summed in LDS
+  if (lane_now() < 2) L.dmask[lane_now()] = 0u;
   wsync();
 #ifdef MPCX_FORCE_BLOCK_CHAIN  // always take the sequential block chain (diagnostics)
   if constexpr (NX > 0) {
@@ -1670,7 +1713,7 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
       eval_gj_ws(a, a.x(), 1);
       sync();
     }
-    if (a.lane == 0) { L.seq = 1; L.want_sdh = 1; }
+    if (lane_now() == 0) { L.seq = 1; L.want_sdh = 1; }
     sync();
     return seq_factor(a, kd);
   }
@@ -1717,7 +1760,7 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
 #endif
   const unsigned long long dm = ((unsigned long long)L.dmask[1] << 32) | L.dmask[0];
 #ifdef MPCX_PROFILE
-  if (a.lane < 2) L.dense_seen[a.lane] |= L.dmask[a.lane];
+  if (lane_now() < 2) L.dense_seen[lane_now()] |= L.dmask[lane_now()];
 #endif
 #else
   const unsigned long long dm = (N == 64) ? ~0ull : ((1ull << N) - 1ull);
@@ -1757,7 +1800,7 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
             eval_gj_ws(a, a.x(), 1);
             sync();
           }
-          if (a.lane == 0) { L.seq = 1; L.want_sdh = 1; }
+          if (lane_now() == 0) { L.seq = 1; L.want_sdh = 1; }
           sync();
           return seq_factor(a, kd);
         }
@@ -1772,7 +1815,7 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
     }
   }
   Inertia in{L.fin[0], L.fin[1], L.fin[2]};
-  if (a.lane == 0) L.seq = 0;
+  if (lane_now() == 0) L.seq = 0;
   if (NC > 0) {
     const Inertia ci = chain_factor(a);
     in.pos += ci.pos; in.neg += ci.neg; in.zero += ci.zero;
@@ -1795,7 +1838,7 @@ __device__ __noinline__ void solve(const Agent a) {
   Lds& L = gL;
   if (L.seq) { seq_solve(a); return; }
   SPROF_DECL
-  const int lane = a.lane;
+  const int lane = lane_now();
   if (NC > 0) chain_solve(a);
   SPROF(4);
   // u = W [x_k, c_k, 1] per stage interior (operators column-major per stage); the lanes
@@ -1842,17 +1885,18 @@ struct Scal {
   int square;  // IPOPT IsSquareProblem: free variables == equality constraints
 };
 
-__device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
+__device__ __noinline__ Scal init_agent(const Agent a, int agent) {
+  KArgs* const argp = kargs();
   KArgs& args = *argp;
   const mpcx_options& o = args.opt;
-  const int lane = a.lane;
+  const int lane = lane_now();
   const gdbl* lbw = (const gdbl*)args.lbw + (long)agent * NW;
   const gdbl* ubw = (const gdbl*)args.ubw + (long)agent * NW;
   const gdbl* wio = (const gdbl*)args.w + (long)agent * NW;
   const gdbl* pin = (const gdbl*)args.p + (long)agent * NPAR;
   for (int t = lane; t < NPAR; t += WAVE) gL.par[t] = pin[t];
-  for (long t = lane; t < (long)(2 * NL + NG * NL + NL * NL) * N; t += WAVE) a.ws[O_SDG + t] = 0.0;
-  for (long t = lane; t < (long)NCPT * N; t += WAVE) a.ws[O_LP + t] = 0.0;  // structural zeros stay zero
+  for (long t = lane; t < (long)(2 * NL + NG * NL + NL * NL) * N; t += WAVE) a.base()[O_SDG + t] = 0.0;
+  for (long t = lane; t < (long)NCPT * N; t += WAVE) a.base()[O_LP + t] = 0.0;  // structural zeros stay zero
   for (int i = lane; i < NW; i += WAVE) {
     double lo = lbw[i], hi = ubw[i];
     if (lo <= -INF_BOUND) lo = -INFINITY;
@@ -1961,7 +2005,7 @@ __device__ __noinline__ Scal init_agent(const Agent a, KArgs* argp, int agent) {
 // sum |c(x) - s| (scaled) at the current point
 __device__ __noinline__ double theta_now(const Agent a) {
   double t = 0.0;
-  for (int c = a.lane; c < M; c += WAVE) {
+  for (int c = lane_now(); c < M; c += WAVE) {
     const int cl = cls_of(a.lb()[c], a.ub()[c], a.sL()[c], a.sU()[c]);
     const double cv = (cl == 0) ? a.gv()[c] - a.gs()[c] * a.lb()[c] : a.gv()[c] - a.s()[c];
     t += fabs(cv);
@@ -1972,7 +2016,7 @@ __device__ __noinline__ double theta_now(const Agent a) {
 // dual rows of the rhs (depend on delta_w); ends with the barrier that hands
 // the whole rhs to the factorisation lanes
 __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, double dc) {
-  const int lane = a.lane;
+  const int lane = lane_now();
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
     const int c = lane + sl * WAVE;
@@ -2004,7 +2048,7 @@ __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, doubl
 
 // least-squares estimate of the constraint multipliers (IPOPT constr_mult_init_max)
 __device__ __noinline__ void ls_multipliers(const Agent a, const double constr_mult_init_max, double obj_scale) {
-  const int lane = a.lane;
+  const int lane = lane_now();
   for (int i = NX + lane; i < NW; i += WAVE) {
     const double r = (a.xL()[i] == a.xU()[i]) ? 0.0 : -(obj_scale * acc_grad(a, i) - a.zL()[i] + a.zU()[i]);
     a.rhs((i - NX) / NP)[(i - NX) % NP] = r;
@@ -2033,7 +2077,7 @@ __device__ __noinline__ void ls_multipliers(const Agent a, const double constr_m
 // full step from the Newton solution (LDS) + fraction-to-the-boundary step
 // sizes + constraint violation and barrier at the current point
 __device__ __noinline__ StepInfo recover_step(const Agent a, double mu, double tau, double dw, double obj_scale) {
-  const int lane = a.lane;
+  const int lane = lane_now();
   double amax = 1.0, az = 1.0, gphid = 0.0, theta = 0.0, bar = 0.0;
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
@@ -2128,7 +2172,8 @@ __device__ __noinline__ double log_ool(double x) { return log(x); }
 // stays in registers across the evaluation call (a non-leaf function saves every
 // callee-saved VGPR it uses to scratch): the x-part of the barrier is summed while the
 // trial point is written, the constraint part is re-read after the call.
-__device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
+__device__ __noinline__ void line_search(const Agent a) {
+  KArgs* const argp = kargs();
   KState& K = gL.ks;
   {
     KArgs& ka = *argp;
@@ -2149,7 +2194,7 @@ __device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
     K.ls.accepted = 0;
     K.ls.ftype = 0;
     K.ls.trials = 0;
-    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};
+    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};    TRACE_LS_HEAD(argp);
   }
 #pragma unroll 1
   for (int ls = 0; ls < 64; ++ls) {
@@ -2209,6 +2254,8 @@ __device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
     const int nfilt = K.nfilt;
     for (int j = 0; j < nfilt && okt; ++j)
       if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
+    const bool okf = okt;
+    (void)okf;
     bool ftype = false;
     if (okt) {
       const bool switching = !K.lsmode && gphid < 0 &&
@@ -2222,6 +2269,7 @@ __device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
       }
     }
     K.ls.ftype = ftype;
+    TRACE_LS_TRIAL(argp, alpha, tr, okf, okt, ftype);
     if (okt) { K.ls.accepted = 1; break; }
     if (K.lsmode || alpha * 0.5 < K.amin) break;
     K.ls.alpha = alpha * 0.5;
@@ -2231,7 +2279,7 @@ __device__ __noinline__ void line_search(const Agent a, KArgs* argp) {
 
 // take the last trial point (xt, gt in LDS) and the multiplier steps
 __device__ __noinline__ void accept_step(const Agent a, const double kappa_sigma, double mu, double alpha, double az) {
-  const int lane = a.lane;
+  const int lane = lane_now();
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
@@ -2306,10 +2354,11 @@ __device__ __forceinline__ bool current_is_acceptable(Acceptable& ac, const OptE
 // operands are loaded once and stay in registers across the wave reductions (no calls),
 // instead of being streamed again by separate rhs phases.  Returns 1 when the solve stops
 // (K.status set), 0 with the rhs handed to the factorisation lanes (barrier).
-__device__ __noinline__ int iter_head(const Agent a, KArgs* argp) {
+__device__ __noinline__ int iter_head(const Agent a) {
+  KArgs* const argp = kargs();
   KArgs& ka = *argp;
   KState& K = gL.ks;
-  const int lane = a.lane;
+  const int lane = lane_now();
   const double obj_scale = K.obj_scale;
   // what the rhs needs is reduced to 3 values per slot while the error terms are summed, the
   // rhs being affine in mu: primal r = r0 + mu r1 (r0 = -(obj_scale grad + J~^T lam),
@@ -2473,6 +2522,19 @@ __device__ __noinline__ int iter_head(const Agent a, KArgs* argp) {
 // that converges on its own terms is a point of local infeasibility.
 // ===========================================================================
 
+// stationarity residuals of the restoration variables p, n: r_p = rho - lambda - mu/p and
+// r_n = rho + lambda - mu/n.  Where p (n) is large, z = mu/p is small and lambda ~ -+rho, so the
+// sum rho -+ lambda cancels; divided by Sigma_p = z/p ~ mu/p^2 its rounding error (eps rho)
+// grows like p^2/mu and the eliminated p, n steps stop satisfying the linearised constraints
+// (the restoration's own infeasibility then grows as mu falls).  The sum is formed exactly
+// (two-sum), so the error is eps times the small residual itself.
+__device__ __forceinline__ double resto_r(double lam_signed, double mu_over) {
+  const double s = RESTO_RHO + lam_signed;
+  const double bv = s - RESTO_RHO;
+  const double err = (RESTO_RHO - (s - bv)) + (lam_signed - bv);
+  return (s - mu_over) + err;
+}
+
 __device__ __forceinline__ double dr2_of(double xr) {
   const double d = 1.0 / fmax(1.0, fabs(xr));
   return d * d;
@@ -2482,7 +2544,7 @@ __device__ __forceinline__ double dr2_of(double xr) {
 // the constraint violation and the mu-complementarity; the common normalisation cancels in
 // the soft-restoration ratio), from that point's derivative arrays
 __device__ __noinline__ double pd_error(const Agent a, double mu, double obj_scale) {
-  const int lane = a.lane;
+  const int lane = lane_now();
   double e = 0.0;
   for (int i = NX + lane; i < NW; i += WAVE) {
     const double lo = a.xL()[i], hi = a.xU()[i];
@@ -2509,7 +2571,7 @@ __device__ __noinline__ double pd_error(const Agent a, double mu, double obj_sca
 
 // iterate <-> backup (x, s, lambda, z, v, scaled g): the soft step's tentative trial
 __device__ __noinline__ void iterate_copy(const Agent a, int to_backup) {
-  const int lane = a.lane;
+  const int lane = lane_now();
   for (int i = lane; i < NW; i += WAVE) {
     if (to_backup) { a.xr()[i] = a.x()[i]; a.zl0()[i] = a.zL()[i]; a.zu0()[i] = a.zU()[i]; }
     else { a.x()[i] = a.xr()[i]; a.zL()[i] = a.zl0()[i]; a.zU()[i] = a.zu0()[i]; }
@@ -2529,7 +2591,7 @@ __device__ __noinline__ void iterate_copy(const Agent a, int to_backup) {
 // the soft trial (xt, gt in LDS) with the same step size alpha for every variable,
 // bound multipliers NOT yet corrected (IPOPT corrects them after acceptance)
 __device__ __noinline__ void soft_apply(const Agent a, double mu, double alpha) {
-  const int lane = a.lane;
+  const int lane = lane_now();
   for (int i = NX + lane; i < NW; i += WAVE) {
     const double lo = a.xL()[i], hi = a.xU()[i];
     if (lo == hi) continue;
@@ -2553,7 +2615,7 @@ __device__ __noinline__ void soft_apply(const Agent a, double mu, double alpha) 
 
 // kappa_sigma correction of the bound multipliers at the current point
 __device__ __noinline__ void sigma_clip(const Agent a, double kappa_sigma, double mu) {
-  const int lane = a.lane;
+  const int lane = lane_now();
   for (int i = NX + lane; i < NW; i += WAVE) {
     const double lo = a.xL()[i], hi = a.xU()[i], xv = a.x()[i];
     if (lo == hi) continue;
@@ -2572,10 +2634,11 @@ __device__ __noinline__ void sigma_clip(const Agent a, double kappa_sigma, doubl
 // TrySoftRestoStep.  0: rejected (iterate unchanged); 1: accepted by the original filter
 // criterion (the caller takes the trial as a regular step); 2: accepted by the
 // primal-dual error test (trial applied, multipliers corrected, derivatives evaluated)
-__device__ __noinline__ int soft_try(const Agent a, KArgs* argp) {
+__device__ __noinline__ int soft_try(const Agent a) {
+  KArgs* const argp = kargs();
   KState& K = gL.ks;
   K.lsmode = 1;
-  line_search(a, argp);
+  line_search(a);
   K.lsmode = 0;
   K.n_trials += K.ls.trials;
   if (K.ls.accepted) return 1;
@@ -2600,10 +2663,11 @@ __device__ __noinline__ int soft_try(const Agent a, KArgs* argp) {
 // ---- restoration phase ----------------------------------------------------------------
 
 // start: called at the iterate whose line search (and soft step) failed, with K.st of it
-__device__ __noinline__ void resto_start(const Agent a, KArgs* argp) {
+__device__ __noinline__ void resto_start(const Agent a) {
+  KArgs* const argp = kargs();
   KArgs& ka = *argp;
   KState& K = gL.ks;
-  const int lane = a.lane;
+  const int lane = lane_now();
   {  // FilterLSAcceptor::PrepareRestoPhaseStart: the current point enters the original filter
     const double theta = K.st.theta, phi = K.fx - K.mu * K.st.barrier;
     int nfilt = K.nfilt;
@@ -2679,9 +2743,10 @@ __device__ __noinline__ void resto_start(const Agent a, KArgs* argp) {
 }
 
 // back to the original problem (the restoration iterate passed the return test)
-__device__ __noinline__ void resto_return(const Agent a, KArgs* argp) {
+__device__ __noinline__ void resto_return(const Agent a) {
+  KArgs* const argp = kargs();
   KState& K = gL.ks;
-  const int lane = a.lane;
+  const int lane = lane_now();
   const double mu0 = K.mu0, tau0 = K.tau0;
   // one Newton step for complementarity over the whole primal change, fraction to the boundary
   double ad = 1.0;
@@ -2748,14 +2813,15 @@ __device__ __noinline__ void resto_return(const Agent a, KArgs* argp) {
 // Top of a restoration iteration: the return test, then the restoration problem's
 // optimality error, termination tests, barrier update (zeta follows mu), Newton rhs and
 // diagonal terms.  Returns 0 (rhs written), 1 (stop, K.status set), 2 (return test passed)
-__device__ __noinline__ int iter_head_resto(const Agent a, KArgs* argp) {
+__device__ __noinline__ void rhs_dual_resto(const Agent a, double mu, double dw, double dc);
+__device__ __noinline__ int iter_head_resto(const Agent a) {
+  KArgs* const argp = kargs();
   KArgs& ka = *argp;
   KState& K = gL.ks;
-  const int lane = a.lane;
+  const int lane = lane_now();
   // primal rows: r = -(jt + zeta gdr) + mu pr1, diagonal psx + zeta dr2; dual residual of
   // x: zeta gdr + hj (zeta-dependent, kept per slot for the barrier loop)
   double gdr[VS], hj[VS], jtv[VS], pr1[VS], psx[VS], d2[VS];
-  double dq0[CS], dq1[CS], ddg[CS];
   double dmax_r = 0.0, pmax = 0.0, vmax = 0.0, pmx = -INFINITY, pmn = INFINITY, lsum = 0.0, zsum = 0.0;
   double barx0 = 0.0, bars0 = 0.0, tho = 0.0, spn = 0.0, sd = 0.0;
   int nz = 0;
@@ -2792,10 +2858,6 @@ __device__ __noinline__ int iter_head_resto(const Agent a, KArgs* argp) {
     const double cr = co - pv + nv;                               // restoration residual
     const double sg = sigma_s_v(sv, slo, sup, vl, vu);
     const double sgp = zp / pv, sgn = zn / nv;
-    dq0[sl] = -cr + ((cl == 1) ? lm / sg : 0.0) + (lm - RESTO_RHO) / sgp + (RESTO_RHO + lm) / sgn;
-    dq1[sl] = ((cl == 1) ? ((isfin(sup) ? 1.0 / (sup - sv) : 0.0) - (isfin(slo) ? 1.0 / (sv - slo) : 0.0)) / sg : 0.0)
-              - (1.0 / pv) / sgp + (1.0 / nv) / sgn;
-    ddg[sl] = -(dual_diag_v(cl, sg, KKTDiag{0.0, 0.0, NEWTON}) + 1.0 / sgp + 1.0 / sgn);
     if (c < M) {
       tho += fabs(co);
       pmax = fmax(pmax, fabs(cr));
@@ -2896,21 +2958,15 @@ __device__ __noinline__ int iter_head_resto(const Agent a, KArgs* argp) {
       a.dg(b)[li] = psx[sl] + zeta * d2[sl];
     }
   }
-#pragma unroll
-  for (int sl = 0; sl < CS; ++sl) {
-    const int c = lane + sl * WAVE;
-    if (c < M) {
-      a.rhs(c / NG)[NP + c % NG] = dq0[sl] - mu * dq1[sl];
-      a.dg(c / NG)[crow(c % NG)] = ddg[sl];
-    }
-  }
-  sync();
+  // dual rows at the final mu, in the same arithmetic as the inertia-correction pass and the
+  // step recovery (the affine split dq0 - mu dq1 would round r_p / r_n differently)
+  rhs_dual_resto(a, mu, 0.0, 0.0);
   return 0;
 }
 
 // dual rows of the restoration rhs with the inertia-correction terms (delta_w, delta_c)
 __device__ __noinline__ void rhs_dual_resto(const Agent a, double mu, double dw, double dc) {
-  const int lane = a.lane;
+  const int lane = lane_now();
   for (int c = lane; c < M; c += WAVE) {
     const double lbv = a.lb()[c], ubv = a.ub()[c], slo = a.sL()[c], sup = a.sU()[c];
     const double gvv = a.gv()[c], gsc = a.gs()[c], sv = a.s()[c], lm = a.lam()[c];
@@ -2925,7 +2981,7 @@ __device__ __noinline__ void rhs_dual_resto(const Agent a, double mu, double dw,
       if (isfin(sup)) gphis += mu / (sup - sv);
       rr -= (gphis - lm) / (sg + dw);
     }
-    rr += -(RESTO_RHO - mu / pv - lm) / sgp + (RESTO_RHO - mu / nv + lm) / sgn;
+    rr += -resto_r(-lm, mu / pv) / sgp + resto_r(lm, mu / nv) / sgn;
     a.rhs(c / NG)[NP + c % NG] = rr;
     a.dg(c / NG)[crow(c % NG)] = -(dual_diag_v(cl, sg, KKTDiag{dw, dc, NEWTON}) + 1.0 / sgp + 1.0 / sgn);
   }
@@ -2936,7 +2992,7 @@ __device__ __noinline__ void rhs_dual_resto(const Agent a, double mu, double dw,
 // eliminated (dp = (dlam - r_p)/(Sigma_p + dw), dn = (-dlam - r_n)/(Sigma_n + dw))
 __device__ __noinline__ StepInfo recover_step_resto(const Agent a, double mu, double tau, double dw) {
   KState& K = gL.ks;
-  const int lane = a.lane;
+  const int lane = lane_now();
   const double zeta = K.zeta;
   double amax = 1.0, az = 1.0, gphid = 0.0, theta = 0.0, bar = 0.0;
   for (int i = NX + lane; i < NW; i += WAVE) {
@@ -3001,8 +3057,8 @@ __device__ __noinline__ StepInfo recover_step_resto(const Agent a, double mu, do
     }
     a.ds()[c] = dsv;
     const double gp = RESTO_RHO - mu / pv, gn = RESTO_RHO - mu / nv;
-    const double dp = (dlam - (gp - lm)) / (zp / pv + dw);
-    const double dn = (-dlam - (gn + lm)) / (zn / nv + dw);
+    const double dp = (dlam - resto_r(-lm, mu / pv)) / (zp / pv + dw);
+    const double dn = (-dlam - resto_r(lm, mu / nv)) / (zn / nv + dw);
     a.rdp()[c] = dp;
     a.rdn()[c] = dn;
     gphid += gp * dp + gn * dn;
@@ -3023,7 +3079,8 @@ __device__ __noinline__ StepInfo recover_step_resto(const Agent a, double mu, do
 }
 
 // filter line search of the restoration problem (its own filter in LDS)
-__device__ __noinline__ void line_search_resto(const Agent a, KArgs* argp) {
+__device__ __noinline__ void line_search_resto(const Agent a) {
+  KArgs* const argp = kargs();
   KState& K = gL.ks;
   {
     KArgs& ka = *argp;
@@ -3042,7 +3099,7 @@ __device__ __noinline__ void line_search_resto(const Agent a, KArgs* argp) {
     K.ls.accepted = 0;
     K.ls.ftype = 0;
     K.ls.trials = 0;
-    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};
+    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};    TRACE_LS_HEAD(argp);
   }
 #pragma unroll 1
   for (int ls = 0; ls < 64; ++ls) {
@@ -3109,6 +3166,8 @@ __device__ __noinline__ void line_search_resto(const Agent a, KArgs* argp) {
     const int nfilt = K.nfilt;
     for (int j = 0; j < nfilt && okt; ++j)
       if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
+    const bool okf = okt;
+    (void)okf;
     bool ftype = false;
     if (okt) {
       const bool switching = gphid < 0 && alpha * pow_ool(-gphid, ka.opt.s_phi) > ka.opt.delta * pow_ool(theta, ka.opt.s_theta);
@@ -3121,6 +3180,7 @@ __device__ __noinline__ void line_search_resto(const Agent a, KArgs* argp) {
       }
     }
     K.ls.ftype = ftype;
+    TRACE_LS_TRIAL(argp, alpha, tr, okf, okt, ftype);
     if (okt) { K.ls.accepted = 1; break; }
     if (alpha * 0.5 < K.amin) break;
     K.ls.alpha = alpha * 0.5;
@@ -3132,7 +3192,7 @@ __device__ __noinline__ void line_search_resto(const Agent a, KArgs* argp) {
 __device__ __noinline__ void accept_step_resto(const Agent a, const double kappa_sigma, double mu, double alpha,
                                                double az) {
   accept_step(a, kappa_sigma, mu, alpha, az);
-  const int lane = a.lane;
+  const int lane = lane_now();
   for (int c = lane; c < M; c += WAVE) {
     const double pv = a.rp()[c], nv = a.rn()[c], dp = a.rdp()[c], dn = a.rdn()[c];
     const double zp = a.rzp()[c], zn = a.rzn()[c];
@@ -3163,9 +3223,10 @@ __device__ __forceinline__ void filter_augment(KArgs* argp) {
 }
 
 // rest of a restoration iteration after the step: line search, filter, accept.  1: stop
-__device__ __noinline__ int resto_tail(const Agent a, KArgs* argp) {
+__device__ __noinline__ int resto_tail(const Agent a) {
+  KArgs* const argp = kargs();
   KState& K = gL.ks;
-  line_search_resto(a, argp);
+  line_search_resto(a);
   const LSResult ls = K.ls;
   K.n_trials += ls.trials;
   if (!ls.accepted) { K.status = MPCX_RESTORATION_FAILED; return 1; }
@@ -3185,21 +3246,22 @@ __device__ __noinline__ int resto_tail(const Agent a, KArgs* argp) {
 // the step of an original-problem iteration: 0 line-search step, 1 soft step accepted by
 // the filter (taken like a line-search step), 2 soft step accepted by the error test
 // (already the iterate), -1 restoration phase started, -2 stop at an acceptable point
-__device__ __noinline__ int search_step(const Agent a, KArgs* argp) {
+__device__ __noinline__ int search_step(const Agent a) {
+  KArgs* const argp = kargs();
   KState& K = gL.ks;
   int mode;
   if (K.soft) {
     K.soft_count += 1;
-    const int r = (K.soft_count <= MAX_SOFT_ITERS) ? soft_try(a, argp) : 0;
+    const int r = (K.soft_count <= MAX_SOFT_ITERS) ? soft_try(a) : 0;
     if (r == 1) { K.soft = 0; K.soft_count = 0; }
     mode = r == 0 ? -1 : r;
   } else {
-    line_search(a, argp);
+    line_search(a);
     K.n_trials += K.ls.trials;
     if (K.ls.accepted) {
       mode = 0;
     } else {
-      const int r = soft_try(a, argp);
+      const int r = soft_try(a);
       if (r != 0) { K.n_soft += 1; if (r == 2) { K.soft = 1; K.soft_count = 0; } }
       mode = r == 0 ? -1 : r;
     }
@@ -3212,7 +3274,7 @@ __device__ __noinline__ int search_step(const Agent a, KArgs* argp) {
                                                   (*argp).opt);
     K.acc = acc;
     if (acceptable) { K.status = MPCX_SOLVED_TO_ACCEPTABLE; return -2; }
-    resto_start(a, argp);
+    resto_start(a);
     return -1;
   }
   return mode;
@@ -3244,10 +3306,13 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   // Loop state lives in LDS (KState, written identically by every lane) and the options are
   // re-read from the kernarg segment where they are used (volatile scalar loads): held in
   // VGPRs they would have to survive every phase call and be spilled to scratch.
-  Agent a;
-  a.ws = (gdbl*)args.ws + (long)agent * args.ws_stride;
-  a.lane = threadIdx.x;
-  const int lane = a.lane;
+  const Agent a{};
+  const int lane = lane_now();
+  if (lane == 0) {
+    gL.kp_bits = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+    gL.ws_bits = (unsigned long long)((gdbl*)args.ws + (long)agent * args.ws_stride);
+  }
+  wsync();
   KState& K = gL.ks;
 
   PROF_DECL
@@ -3258,7 +3323,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
 #endif
   if (lane == 0) { gL.want_sdh = 0; gL.sdh_ok = 0; gL.hsig = 1.0; gL.seq = 0; }
   {
-    const Scal sc = init_agent(a, (KArgs*)__builtin_amdgcn_kernarg_segment_ptr(), agent);
+    const Scal sc = init_agent(a, agent);
     K.obj_scale = sc.obj_scale;
     K.fx = sc.fx;
     K.square = sc.square;
@@ -3288,13 +3353,13 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
 #pragma unroll 1
   for (;;) {
     if (K.resto) {
-      const int hr = iter_head_resto(a, KARGP);
+      const int hr = iter_head_resto(a);
       if (hr == 1) break;
       if (hr == 2) {  // back in the original problem: its own iteration head at this point
-        resto_return(a, KARGP);
-        if (iter_head(a, KARGP)) break;
+        resto_return(a);
+        if (iter_head(a)) break;
       }
-    } else if (iter_head(a, KARGP)) {
+    } else if (iter_head(a)) {
       break;
     }
     PROF(2);
@@ -3341,12 +3406,12 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     }
     PROF(7);
     if (K.resto) {  // restoration iteration: its own filter; no restoration inside it
-      if (resto_tail(a, KARGP)) break;
+      if (resto_tail(a)) break;
       continue;
     }
     // filter line search; on failure the soft restoration step, then the restoration phase
     // (IPOPT BacktrackingLineSearch::FindAcceptableTrialPoint)
-    const int mode = search_step(a, KARGP);
+    const int mode = search_step(a);
     if (mode == -2) break;       // acceptable point, status set
     if (mode == -1) continue;    // restoration phase started
     if (mode == 2) {  // the soft trial is already the iterate
@@ -3376,7 +3441,11 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   const int in_resto = K.resto;
   for (int i = lane; i < NW; i += WAVE) {
     wio[i] = a.x()[i];
+#ifndef MPCX_TRACE_LS
     if (args.lam_w != nullptr)
+#else
+    if (false)
+#endif
       ((gdbl*)args.lam_w)[(long)agent * NW + i] =
           (i < NX) ? 0.0 : (in_resto ? a.zu0()[i] - a.zl0()[i] : a.zU()[i] - a.zL()[i]) / obj_scale;
   }
@@ -3391,7 +3460,11 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     ((gdbl*)args.lam_w)[(long)agent * NW + 17] = (double)gL.dense_seen[1];
   }
 #endif
+#ifndef MPCX_TRACE_LS
   if (args.lam_g != nullptr)
+#else
+  if (false)
+#endif
     for (int c = lane; c < M; c += WAVE)
       ((gdbl*)args.lam_g)[(long)agent * M + c] = in_resto ? 0.0 : a.lam()[c] * a.gs()[c] / obj_scale;
   if (args.stats != nullptr && lane == 0) {

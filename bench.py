@@ -119,6 +119,31 @@ def cpu_baseline(p, lbw, ubw, w0, ipopt, min_seconds=10.0, max_repeats=200):
                       f"gcc -O3 -march=native, OpenMP {threads} threads): {dt:.2f} s wall"}
 
 
+def pmc_fp64(code_object: str, n_agents: int, kernel_ms: float):
+    """FP64 utilisation of the bench kernel from the committed rocprofv3 instruction-counter
+    passes (``profiles/*/*/pmc_fp64_c3.json``, scripts/gpu_pmc.sh): FP64 VALU lane-ops issued
+    (64 x (ADD + MUL + 2 FMA + TRANS) wave instructions, an upper bound: masked lanes still
+    take the issue slot) and FP64 MFMA flops per launch, over this run's kernel time, against
+    the FP64 peak; plus the wave-cycle split (VALU issue / any issue / waiting).  Same code
+    object and fleet size only; otherwise None."""
+    import glob
+
+    if n_agents != 4096:
+        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*", "pmc_fp64_c3.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("code_object") == code_object:
+            issued = (d["fp64_valu_flops_per_launch_upper"] + d["fp64_mfma_flops_per_launch"]) / (kernel_ms * 1e-3) / 1e12
+            return {"issued_tflops_upper": issued, "issued_frac_upper": issued / PEAK_FP64_TFLOPS,
+                    "fp64_share_of_valu_insts": d["fp64_share_of_valu_insts"],
+                    "wave_cycle_split": d.get("wave_cycle_split"), "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def pmc_traffic(code_object: str, n_agents: int):
     """HBM bytes per launch of the bench kernel from the committed rocprofv3 PMC
     passes (``profiles/*/*/pmc_traffic_c3.json``: FETCH_SIZE and WRITE_SIZE in
@@ -831,6 +856,7 @@ def main():
                 "frac": achieved / PEAK_FP64_TFLOPS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "fp64_pmc": pmc_fp64(code_object_path(prob.gen.key).name, n, kernel_ms),
                 "algorithmic_io_bytes": io_bytes,
                 "kernel": "mpcx_ipm_solve",
                 "kernel_ms": kernel_ms,

@@ -32,6 +32,10 @@ DEBUG = False
 ZERO_PIVOT = 1e-20  # same constant as csrc/mpcx_ipm.hip
 
 
+#: diagnostics only: a list receives the trials of the last line search (scripts/resto_diag.py)
+LS_TRACE = None
+
+
 @dataclasses.dataclass
 class IPMOptions:
     tol: float = 1e-8
@@ -568,6 +572,9 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
                 goto_resto = True
         else:
             alpha = a_max
+            if LS_TRACE is not None:  # diagnostics (scripts/resto_diag.py): the last line search
+                LS_TRACE.clear()
+                LS_TRACE.append(("head", theta, phi, gphi_d, a_min, theta_min, theta_max, mu, list(filt), dw, dc))
             while True:
                 xt = x + alpha * dx
                 st = s + alpha * ds
@@ -576,6 +583,7 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
                 th_t = theta_of(gxt, st)
                 ph_t = phi_of(fxt, xt, st, mu)
                 ok = np.isfinite(th_t) and np.isfinite(ph_t) and filter_ok(th_t, ph_t)
+                okf = ok
                 if ok:
                     switching = gphi_d < 0 and alpha * (-gphi_d) ** o.s_phi > o.delta * theta ** o.s_theta
                     if theta <= theta_min and switching:
@@ -584,6 +592,8 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
                     else:
                         ok = th_t <= (1 - o.gamma_theta) * theta or ph_t <= phi - o.gamma_phi * theta
                         ftype = False
+                if LS_TRACE is not None:
+                    LS_TRACE.append((alpha, th_t, ph_t, okf, ok, ftype))
                 if ok:
                     accepted = True
                     break

@@ -353,3 +353,55 @@ def test_gpu_c4_fleet_at_scale_matches_local_round_with_c_oracle():
         want_m = np.array([state["mult"][(f"{cname}#{i}", "mDot_coupling")] for i in range(n)])
         np.testing.assert_allclose(loc, want_l, rtol=RTOL, atol=1e-7)   # at-bound entries: barrier distances
         np.testing.assert_allclose(mult, want_m, rtol=RTOL, atol=1e-5 * np.abs(want_m).max())
+
+
+def test_gpu_c4_full_size_fleet_properties():
+    """BASELINE.json configs[3] at its full size: examples/exchange_admm scaled to 16384 agents
+    (13108 rooms + 3276 supply units, one exchange alias; rho=1e4, N=10, 15 LocalADMM
+    iterations, the reference IPOPT settings), the bench's fleet.  Size-independent checks:
+    every one of the 16384 x 15 local solves succeeds; the exchange mean is the mean of the
+    agents' final local trajectories (the moment identity the segmented-sum kernels compute);
+    the last multiplier update is lambda_15 - lambda_14 = rho * mean_15 (`admm.py:639-655`),
+    lambda_14 taken from a 14-iteration run of the same fleet."""
+    N, rho = 10, 1e4
+    make = lambda: bm.c4_fleet_classes(n_rooms=13108, n_supply=3276, N=N, seed=20261015 + 4,  # noqa: E731
+                                       solver_options=bm.REFERENCE)
+    fl = ADMMFleet(make())
+    out = fl.run_local(rho, max_iterations=15)
+    assert out["converged_solves"] == 16384 * 15
+    locs = np.vstack([fl.locals_of("room", "mDot_out"), fl.locals_of("supply", "mDot_out")])
+    assert locs.shape == (16384, N)
+    mean15 = fl.trajectories()["mDot_coupling"]
+    np.testing.assert_allclose(mean15, locs.mean(axis=0), rtol=1e-12, atol=1e-15)
+    lam15 = fl.multipliers_of("room", "mDot_out")
+    assert np.all(lam15 == lam15[0])   # one multiplier per alias: every participant's copy equal
+    fl14 = ADMMFleet(make())
+    fl14.run_local(rho, max_iterations=14)
+    lam14 = fl14.multipliers_of("room", "mDot_out")
+    np.testing.assert_allclose(lam15[0] - lam14[0], rho * mean15, rtol=1e-9, atol=1e-9 * rho * np.abs(mean15).max())
+
+
+def test_gpu_c5_full_size_fleet_blocks_equal_their_own_runs():
+    """BASELINE.json configs[4] at its full size: 342 three-zone blocks (1026 NARX zones +
+    342 AHU + 342 CCA agents, one batched launch per class and ADMM iteration), 3 coordinated
+    iterations: the first, a middle and the last block each equal a single-block fleet of that
+    block alone (residual history and coupling means)."""
+    N, kw = 24, dict(admm_iter_max=3, use_relative_tolerances=False, primal_tol=0.0, dual_tol=0.0)
+    opts = bm.REFERENCE
+    big = ADMMFleet(bm.c5_fleet_classes(n_blocks=342, N=N, seed=20261015 + 5, solver_options=opts))
+    assert big.n_blocks == 342 and sum(c.n for c in big.classes) == 5 * 342
+    out = big.run_coordinated(1.0, **kw)
+    tb = big.trajectories()
+    for b in (0, 171, 341):
+        one = ADMMFleet(bm.c5_fleet_classes(n_blocks=1, N=N, seed=20261015 + 5, block_offset=b,
+                                            solver_options=opts))
+        o1 = one.run_coordinated(1.0, **kw)
+        k = big.block_index(f"T_airin1_b{b}")
+        got = np.array([[r.primal_residual, r.dual_residual] for r in out["block_records"][k]])
+        want = np.array([[r.primal_residual, r.dual_residual] for r in o1["records"]])
+        np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12)
+        to = one.trajectories()
+        for pre in ("T_coupling", "T_coupling_ahu", "T_rucklauf", "T_airin"):
+            for i in range(3):
+                al = f"{pre}{i + 1}_b{b}"
+                np.testing.assert_allclose(tb[al], to[al], rtol=1e-9, atol=1e-9)

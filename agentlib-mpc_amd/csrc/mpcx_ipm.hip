@@ -613,7 +613,9 @@ __device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv, int full)
 }
 
 // derivatives at the accepted trial point (still in LDS), with the accepted multipliers
-__device__ __noinline__ void eval_gj_lds(const Agent a) {
+// inlined into the kernel body: as a leaf call it saved and restored the callee-saved VGPRs
+// its generated derivative code uses on every iteration (C3 -4 %, profiles/r03/s2/var_sgpr_c3.txt)
+__device__ __attribute__((always_inline)) void eval_gj_lds(const Agent a) {
   NET_PREP(gL.u.t.xt, gj);
   const int full = gL.want_sdh;
   for (int k = lane_now(); k < N; k += WAVE)
@@ -2354,7 +2356,7 @@ __device__ __forceinline__ bool current_is_acceptable(Acceptable& ac, const OptE
 // operands are loaded once and stay in registers across the wave reductions (no calls),
 // instead of being streamed again by separate rhs phases.  Returns 1 when the solve stops
 // (K.status set), 0 with the rhs handed to the factorisation lanes (barrier).
-__device__ __noinline__ int iter_head(const Agent a) {
+__device__ __attribute__((always_inline)) int iter_head(const Agent a) {
   KArgs* const argp = kargs();
   KArgs& ka = *argp;
   KState& K = gL.ks;
@@ -3355,13 +3357,9 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     if (K.resto) {
       const int hr = iter_head_resto(a);
       if (hr == 1) break;
-      if (hr == 2) {  // back in the original problem: its own iteration head at this point
-        resto_return(a);
-        if (iter_head(a)) break;
-      }
-    } else if (iter_head(a)) {
-      break;
+      if (hr == 2) resto_return(a);  // back in the original problem: its own head at this point
     }
+    if (!K.resto && iter_head(a)) break;  // one (inlined) call site
     PROF(2);
     eval_hess(a, K.resto ? 0.0 : K.obj_scale);  // restoration: the constraints' curvature only
     PROF(3);

@@ -204,7 +204,7 @@ def admm_bench(args, world, rank, dev):
     wall, ok = float(t[0]), float(t[1])
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        ns = min(n, 2048)
+        ns = n  # the whole fleet (15 iterations of 16384 C IPM solves: a few seconds on 16 cores)
         sample = bm.c4_fleet_classes(n_rooms=ns - ns // 5, n_supply=ns // 5, N=10, seed=20261015 + 4,
                                      solver_options=opts)
         cpu = admm_cpu_baseline(sample, lambda fl: fl.run_local(1e4, max_iterations=args.admm_iters,
@@ -395,7 +395,7 @@ def c2_admm_bench(args, world, rank, dev):
     wall = time.perf_counter() - t0
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        sample = bm.c2_fleet_classes(n_blocks=min(nb, 64), N=10, seed=20261015 + 1, solver_options={"ipopt": {}})
+        sample = bm.c2_fleet_classes(n_blocks=nb, N=10, seed=20261015 + 1, solver_options={"ipopt": {}})
         cpu = admm_cpu_baseline(sample, lambda fl: fl.run_coordinated(0.4, admm_iter_max=40,
                                                                       use_relative_tolerances=False,
                                                                       primal_tol=0.002, dual_tol=0.1),
@@ -510,7 +510,7 @@ def c5_admm_bench(args, world, rank, dev):
     wall = time.perf_counter() - t0
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        sample = bm.c5_fleet_classes(n_blocks=min(nb, 16), N=24, seed=20261015 + 5, solver_options=opts)
+        sample = bm.c5_fleet_classes(n_blocks=nb, N=24, seed=20261015 + 5, solver_options=opts)
         cpu = admm_cpu_baseline(sample, lambda fl: fl.run_coordinated(1.0, admm_iter_max=args.c5_iters,
                                                                       use_relative_tolerances=False,
                                                                       primal_tol=0.04, dual_tol=0.04),
@@ -531,8 +531,8 @@ def admm_cpu_baseline(classes, run, full_agents, label, min_seconds=8.0):
     """The same ADMM driver (`admm/fleet.py`) on the host: every class's agents solved by
     the C IPM restatement over the class's generated model compiled for the host
     (`oracle/c/gen_model.cpp`, OpenMP over the host cores), the ADMM arithmetic in numpy
-    (`oracle/cpu_fleet.py`).  Run on a bounded sample fleet (``classes``) and scaled to the
-    per-GPU fleet by the agent ratio (the solves dominate and scale linearly)."""
+    (`oracle/cpu_fleet.py`).  Run on the GPU leg's whole fleet (``classes``; a smaller
+    sample is scaled to it by the agent ratio and labelled "projected")."""
     from agentlib_mpc_amd.admm.fleet import ADMMFleet
     from oracle.cpu_fleet import CpuFleetOps
 
@@ -550,7 +550,8 @@ def admm_cpu_baseline(classes, run, full_agents, label, min_seconds=8.0):
             break
     dt = time.perf_counter() - t0
     per_s = iters / dt
-    return {"value": per_s * n_sample / full_agents, "unit": "ADMM iters/s (per-GPU fleet, projected)",
+    unit = "ADMM iters/s" if n_sample == full_agents else "ADMM iters/s (per-GPU fleet, projected)"
+    return {"value": per_s * n_sample / full_agents, "unit": unit,
             "cores": ops.threads, "kind": "port",
             "sample": f"{label}: {rounds} round(s), {iters} ADMM iterations over a {n_sample}-agent sample fleet in "
                       f"{dt:.1f} s ({per_s:.2f} it/s), x {n_sample}/{full_agents} agents; solves by "

@@ -24,7 +24,7 @@ def main():
     from tests import configs
     from tests.test_gpu_ipm import REFERENCE_OPTS, RESTO_CASES
 
-    name, kw, setting = RESTO_CASES[int(sys.argv[1])]
+    name, kw, setting = getattr(RESTO_CASES[int(sys.argv[1])], "values", RESTO_CASES[int(sys.argv[1])])
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 80
     tight = setting == "tight"
     base = dict(tol=1e-10, max_iter=500, acceptable_iter=0) if tight else dict(REFERENCE_OPTS)
@@ -52,7 +52,7 @@ def main():
 def trace():
     from tests.test_gpu_ipm import RESTO_CASES
 
-    name, kw, setting = RESTO_CASES[int(sys.argv[2])]
+    name, kw, setting = getattr(RESTO_CASES[int(sys.argv[2])], "values", RESTO_CASES[int(sys.argv[2])])
     ms = [int(v) for v in sys.argv[3].split(":")]
     if len(ms) == 2:  # a range: only the headers of the last line search per truncation
         for m in range(ms[0], ms[1] + 1):

@@ -191,7 +191,10 @@ def test_gpu_three_zone_narx_fleet_matches_oracle_fixture(N):
                              use_relative_tolerances=False, primal_tol=0.04, dual_tol=0.04)
     assert out["iterations"] == gold["iterations"] and out["converged"] == gold["converged"]
     got = np.array([[r.primal_residual, r.dual_residual] for r in out["records"]])
-    np.testing.assert_allclose(got, np.array(gold["history"])[:, :2], rtol=RTOL, atol=1e-8)
+    want = np.array(gold["history"])[:, :2]
+    rel = np.max(np.abs(got - want) / np.maximum(np.abs(want), 1e-3), axis=1)
+    print("C5 N=%d per-iteration relative residual difference:" % N, np.array2string(rel, precision=2))
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-8)
     traj = fl.trajectories()
     for al, mean in gold["means"].items():
         np.testing.assert_allclose(traj[al], mean, rtol=RTOL, atol=1e-6)
@@ -372,7 +375,8 @@ def test_gpu_c4_full_size_fleet_properties():
     locs = np.vstack([fl.locals_of("room", "mDot_out"), fl.locals_of("supply", "mDot_out")])
     assert locs.shape == (16384, N)
     mean15 = fl.trajectories()["mDot_coupling"]
-    np.testing.assert_allclose(mean15, locs.mean(axis=0), rtol=1e-12, atol=1e-15)
+    # the kernel's segmented sums add 16384 signed terms in atomic (unordered) order
+    np.testing.assert_allclose(mean15, locs.mean(axis=0), rtol=1e-12, atol=1e-12 * np.abs(locs).max())
     lam15 = fl.multipliers_of("room", "mDot_out")
     assert np.all(lam15 == lam15[0])   # one multiplier per alias: every participant's copy equal
     fl14 = ADMMFleet(make())

@@ -310,10 +310,6 @@ struct KState {
   LSResult ls;     // last line search
   double mu, tau, dw_last, fx, obj_scale, theta_max, theta_min, dw, dc, amin, barx;
   int nfilt, it, status, square, n_fact, n_ic, n_fallback, n_trials, n_chain, n_dense;
-  // accepted line-search step whose bound multipliers / slacks / iterate are written by the
-  // next iteration head (MPCX_FUSED_ACCEPT): step sizes and the kappa_sigma safeguard's mu
-  int pending;
-  double p_alpha, p_az, p_mu;
   // soft restoration / feasibility restoration phase (IPOPT BacktrackingLineSearch,
   // MinC_1NrmRestorationPhase): the original problem's state while restoring
   Acceptable acc0;
@@ -2339,12 +2335,6 @@ __device__ __noinline__ void accept_step(const Agent a, const double kappa_sigma
   }
 }
 
-// constraint multipliers of the accepted step (the rest of the step is taken by the next
-// iteration head, MPCX_FUSED_ACCEPT): the derivative pass at the new point needs them first
-__device__ __noinline__ void accept_lam(const Agent a, double alpha) {
-  for (int c = lane_now(); c < M; c += WAVE) a.lam()[c] = a.lam()[c] + alpha * a.dl()[c];
-}
-
 // IPOPT OptimalityErrorConvergenceCheck::CurrentIsAcceptable: the objective-change test
 // compares the (scaled) objective of the last two iterations at which it was called
 // (initially -1e50, so the first call never passes a finite acceptable_obj_change_tol)
@@ -2391,27 +2381,6 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
       double xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
       const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
       const bool on = i >= NX && i < NW && lo != hi;
-#ifdef MPCX_FUSED_ACCEPT
-      if (K.pending) {  // accept_step's update of the iterate and its bound multipliers
-        const double d = a.dx()[ii], xn = gL.u.t.xt[ii], mu0 = K.p_mu, az = K.p_az, ks = ka.opt.kappa_sigma;
-        if (on) {
-          if (isfin(lo)) {
-            const double sl0 = xv - lo, s_l = xn - lo;
-            const double zn = zl + az * (mu0 / sl0 - zl - (zl / sl0) * d);
-            zl = fmax(fmin(zn, ks * mu0 / s_l), mu0 / (ks * s_l));
-            a.zL()[i] = zl;
-          }
-          if (isfin(hi)) {
-            const double su0 = hi - xv, s_u = hi - xn;
-            const double zn = zu + az * (mu0 / su0 - zu + (zu / su0) * d);
-            zu = fmax(fmin(zn, ks * mu0 / s_u), mu0 / (ks * s_u));
-            a.zU()[i] = zu;
-          }
-          xv = xn;
-          a.x()[i] = xn;
-        }
-      }
-#endif
       pr0[sl] = on ? -(obj_scale * gr + jt) : 0.0;
       pr1[sl] = on ? (isfin(lo) ? 1.0 / (xv - lo) : 0.0) - (isfin(hi) ? 1.0 / (hi - xv) : 0.0) : 0.0;
       psx[sl] = sigma_x_v(xv, lo, hi, zl, zu);
@@ -2431,30 +2400,6 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
       const double gsc = a.gs()[cc], lm = a.lam()[cc];
       double gvv = a.gv()[cc], sv = a.s()[cc], vl = a.vL()[cc], vu = a.vU()[cc];
       const int cl = cls_of(lbv, ubv, slo, sup);
-#ifdef MPCX_FUSED_ACCEPT
-      if (K.pending && c < M) {  // accept_step's update of the slacks and their multipliers
-        const double dsv = a.ds()[cc], mu0 = K.p_mu, az = K.p_az, ks = ka.opt.kappa_sigma;
-        const double sn = sv + K.p_alpha * dsv;
-        gvv = gL.u.t.gt[cc];
-        a.gv()[c] = gvv;
-        a.s()[c] = sn;
-        if (cl == 1) {
-          if (isfin(slo)) {
-            const double sl0 = sv - slo, s_l = sn - slo;
-            const double vn = vl + az * (mu0 / sl0 - vl - (vl / sl0) * dsv);
-            vl = fmax(fmin(vn, ks * mu0 / s_l), mu0 / (ks * s_l));
-            a.vL()[c] = vl;
-          }
-          if (isfin(sup)) {
-            const double su0 = sup - sv, s_u = sup - sn;
-            const double vn = vu + az * (mu0 / su0 - vu + (vu / su0) * dsv);
-            vu = fmax(fmin(vn, ks * mu0 / s_u), mu0 / (ks * s_u));
-            a.vU()[c] = vu;
-          }
-        }
-        sv = sn;
-      }
-#endif
       {
         const double sg = sigma_s_v(sv, slo, sup, vl, vu);
         const double r = (cl == 0) ? -(gvv - gsc * lbv) : -(gvv - sv);
@@ -2483,9 +2428,6 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
         lsum += fabs(lm);
       }
     }
-#ifdef MPCX_FUSED_ACCEPT
-    K.pending = 0;
-#endif
     OptErr e;
     e.dual = wmax(dmax); e.dual_u = wmax(dmax_u); e.primal = wmax(pmax); e.viol_u = wmax(vmax_u);
     e.pmx = wmax(pmx); e.pmn = wmin(pmn);
@@ -3410,7 +3352,6 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   K.it = 0;
   K.acc = Acceptable{-1e50, -1e50, -1, 0};
   K.resto = 0; K.soft = 0; K.soft_count = 0; K.lsmode = 0; K.n_soft = 0; K.n_resto_it = 0;
-  K.pending = 0;
 #define KARGP ((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())
 #pragma unroll 1
   for (;;) {
@@ -3482,17 +3423,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     K.fx = K.ls.tr.f;
     wsync();
     PROF(8);
-#ifdef MPCX_FUSED_ACCEPT
-    // the iterate, slacks and bound multipliers of the step are written by the next
-    // iteration head while it streams them anyway (one pass over the vectors less)
-    K.p_alpha = K.ls.alpha;
-    K.p_az = mode == 1 ? K.ls.alpha : K.st.az;
-    K.p_mu = K.mu;
-    K.pending = 1;
-    accept_lam(a, K.ls.alpha);
-#else
     accept_step(a, OPT(kappa_sigma), K.mu, K.ls.alpha, mode == 1 ? K.ls.alpha : K.st.az);
-#endif
     sync();  // accepted multipliers visible to the stage lanes
     eval_gj_lds(a);
     sync();

@@ -43,8 +43,6 @@ VARIANTS = {
     "o2": (["-O2"], None),
     # the kernel source of the last commit (A/B against the working tree)
     "head": ([], "HEAD"),
-    # the accepted step applied by the next iteration head (one vector pass less)
-    "fused": (["-DMPCX_FUSED_ACCEPT=1"], None),
     # leaf phases inlined into the kernel body: no callee-saved VGPR saves per call
     "inl_gj": ([], ("__device__ __noinline__ void eval_gj_lds(", "__device__ __attribute__((always_inline)) void eval_gj_lds(")),
     "inl_head": ([], ("__device__ __noinline__ int iter_head(const Agent a)", "__device__ __attribute__((always_inline)) int iter_head(const Agent a)")),

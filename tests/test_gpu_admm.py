@@ -194,10 +194,13 @@ def test_gpu_three_zone_narx_fleet_matches_oracle_fixture(N):
     want = np.array(gold["history"])[:, :2]
     rel = np.max(np.abs(got - want) / np.maximum(np.abs(want), 1e-3), axis=1)
     print("C5 N=%d per-iteration relative residual difference:" % N, np.array2string(rel, precision=2))
-    # the nonconvex NARX zone solves (tol 1e-8 on both sides) agree to ~1e-12 through the first
-    # 11 iterations of the N=8 run; at iteration 12 one local solve ends elsewhere and the two
-    # consensus paths part (by ~1e-2 .. 1e-1 relative, both still unconverged at the cap of 50):
-    # the tight comparison covers that prefix, the rest only the stopping outcome and the level
+    # the two runs agree to ~1e-12 through the first 11 iterations of the N=8 run; the supply
+    # agents' nearly non-smooth costs (sqrt(W^2 + 0.02) at objective scale ~1e6) already take
+    # different line-search paths to the same solutions from iteration 10 on, and at iteration
+    # 12 the kernel's CCA solve enters restoration and stops at a nearby point where the oracle
+    # converges directly (scripts/c5_diverge.py, profiles/r03/s3/c5_diverge_*.txt): the
+    # consensus paths then differ by ~1e-3..1e-1 relative, both unconverged at the cap of 50.
+    # The tight comparison covers the matching prefix, the rest the outcome and the level.
     tight = min(len(want), 11)
     np.testing.assert_allclose(got[:tight], want[:tight], rtol=RTOL, atol=1e-8)
     np.testing.assert_allclose(got[tight:], want[tight:], rtol=0.15)

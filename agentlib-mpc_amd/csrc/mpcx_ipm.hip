@@ -53,6 +53,7 @@ constexpr int WAVE = 64;
 constexpr int VS = (NW + WAVE - 1) / WAVE;  // variable slots per lane
 constexpr int CS = (M + WAVE - 1) / WAVE;   // constraint slots per lane
 constexpr int MAXF = 32;           // filter entries kept in LDS
+static_assert(MAXF <= 64, "the filter test reads one entry per lane");
 constexpr double INF_BOUND = 1e19;
 constexpr double TS = MPCX_TS;
 #ifndef MPCX_MIN_WAVES
@@ -173,6 +174,58 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {
 // ---------------------------------------------------------------------------
 // wave and lane-group helpers
 // ---------------------------------------------------------------------------
+// DPP lane exchange inside aligned groups (quad_perm xor1 / xor2, half-row and
+// row mirrors): register-speed, no LDS round trip
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+// broadcast lane `l` (compile-time in unrolled loops) of a double: two v_readlane
+__device__ __forceinline__ double rl_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+// Wave reductions (all 64 lanes active): DPP steps inside each row of 16 lanes (VALU
+// latency), then the four row results read into SGPRs and combined -- instead of six
+// LDS-permute (ds_bpermute) round trips.  MPCX_SHFL_REDUCE: the butterfly over __shfl_xor.
+#ifndef MPCX_SHFL_REDUCE
+__device__ __forceinline__ double wsum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm xor 1
+  v += dpp_f64<0x4E>(v);   // quad_perm xor 2
+  v += dpp_f64<0x141>(v);  // row_half_mirror: the other quad of the half-row
+  v += dpp_f64<0x140>(v);  // row_mirror: the other half of the row
+  return (rl_f64(v, 0) + rl_f64(v, 16)) + (rl_f64(v, 32) + rl_f64(v, 48));
+}
+__device__ __forceinline__ double wmax(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  v = fmax(v, dpp_f64<0x140>(v));
+  return fmax(fmax(rl_f64(v, 0), rl_f64(v, 16)), fmax(rl_f64(v, 32), rl_f64(v, 48)));
+}
+__device__ __forceinline__ double wmin(double v) {
+  v = fmin(v, dpp_f64<0xB1>(v));
+  v = fmin(v, dpp_f64<0x4E>(v));
+  v = fmin(v, dpp_f64<0x141>(v));
+  v = fmin(v, dpp_f64<0x140>(v));
+  return fmin(fmin(rl_f64(v, 0), rl_f64(v, 16)), fmin(rl_f64(v, 32), rl_f64(v, 48)));
+}
+__device__ __forceinline__ int wsumi(int v) {
+  v += dpp_i32<0xB1>(v);
+  v += dpp_i32<0x4E>(v);
+  v += dpp_i32<0x141>(v);
+  v += dpp_i32<0x140>(v);
+  return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+         (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
+}
+#else
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
@@ -193,6 +246,7 @@ __device__ __forceinline__ int wsumi(int v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
   return v;
 }
+#endif
 // argmax with smallest index on ties
 __device__ __forceinline__ void wargmax(double& v, int& idx) {
 #pragma unroll
@@ -221,18 +275,6 @@ __device__ __forceinline__ int lane_now() {
   return l;
 }
 
-// DPP lane exchange inside aligned groups (quad_perm xor1 / xor2, half-row and
-// row mirrors): register-speed, no LDS round trip
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-template <int CTRL>
-__device__ __forceinline__ int dpp_i32(int v) {
-  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
-}
 template <int GG>
 __device__ __forceinline__ double gmax(double v) {
   if constexpr (GG >= 2) v = fmax(v, dpp_f64<0xB1>(v));
@@ -257,12 +299,6 @@ __device__ __forceinline__ void gargmax(double& v, int& idx) {
 }
 
 __device__ __forceinline__ bool isfin(double v) { return fabs(v) < INFINITY; }
-// broadcast lane `l` (compile-time in unrolled loops) of a double: two v_readlane
-__device__ __forceinline__ double rl_f64(double v, int l) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-  return __hiloint2double(hi, lo);
-}
 __device__ __forceinline__ double absn(double v) {  // |v| with NaN -> +inf (total order for pivoting)
   const double t = fabs(v);
   return t == t ? t : INFINITY;
@@ -353,7 +389,7 @@ struct LdsRest {
   // (the kernarg segment pointer itself is not an implicit input of called functions)
   unsigned long long kp_bits, ws_bits;
 #ifdef MPCX_PROFILE
-  double sprof[6];
+  double sprof[10];  // 0-3 factor, 4-5 solve, 6-9 iteration head (profile build)
   unsigned int dense_seen[2];  // stages ever rejected by the static plan (profile build)
 #endif
 };
@@ -2253,9 +2289,11 @@ __device__ __noinline__ void line_search(const Agent a) {
     K.ls.tr = tr;
     K.ls.trials += 1;
     bool okt = (tr.theta <= K.theta_max) && (tr.phi == tr.phi);
-    const int nfilt = K.nfilt;
-    for (int j = 0; j < nfilt && okt; ++j)
-      if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
+    {  // filter test, one entry per lane (MAXF <= 64): one LDS read instead of nfilt in sequence
+      const int j = lane_now();
+      const bool dom = j < K.nfilt && tr.theta >= gL.fth[j < MAXF ? j : 0] && tr.phi >= gL.fph[j < MAXF ? j : 0];
+      if (__any(dom)) okt = false;
+    }
     const bool okf = okt;
     (void)okf;
     bool ftype = false;
@@ -2367,6 +2405,7 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
   // r1 = 1/(x - lo) - 1/(hi - x)) and Sigma_x; dual (inequality rows) rr = q0 - mu q1
   // (q0 = -(c - s) + lam / Sigma_s, q1 = (1/(sU - s) - 1/(s - sL)) / Sigma_s) and the dual
   // diagonal; equality / free rows: rr = q0
+  SPROF_DECL
   double pr0[VS], pr1[VS], psx[VS];
   double dq0[CS], dq1[CS], ddg[CS];
   {
@@ -2428,6 +2467,7 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
         lsum += fabs(lm);
       }
     }
+    SPROF(6);  // loads and the per-element terms
     OptErr e;
     e.dual = wmax(dmax); e.dual_u = wmax(dmax_u); e.primal = wmax(pmax); e.viol_u = wmax(vmax_u);
     e.pmx = wmax(pmx); e.pmn = wmin(pmn);
@@ -2438,6 +2478,7 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
     e.s_d = fmax(smax, (lsum + zsum) / fmax(1.0, (double)(M + nz))) / smax;
     e.s_c = nz > 0 ? fmax(smax, zsum / (double)nz) / smax : 1.0;
     K.e0 = e;
+    SPROF(7);  // reductions
   }
   // ---- termination tests ----
   {
@@ -2476,6 +2517,7 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
     K.tau = fmax(ka.opt.tau_min, 1.0 - new_mu);
     K.nfilt = 0;
   }
+  SPROF(8);  // termination tests, barrier update
   const double mu = K.mu;
   // ---- Newton rhs and diagonal terms (rhs_dual with delta_w = delta_c = 0) ----
 #pragma unroll
@@ -2499,6 +2541,7 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
     }
   }
   sync();
+  SPROF(9);  // rhs / diagonal stores and the barrier
   return 0;
 }
 
@@ -3166,9 +3209,11 @@ __device__ __noinline__ void line_search_resto(const Agent a) {
     K.ls.tr = tr;
     K.ls.trials += 1;
     bool okt = (tr.theta <= K.theta_max) && (tr.phi == tr.phi);
-    const int nfilt = K.nfilt;
-    for (int j = 0; j < nfilt && okt; ++j)
-      if (tr.theta >= gL.fth[j] && tr.phi >= gL.fph[j]) okt = false;
+    {  // filter test, one entry per lane (MAXF <= 64): one LDS read instead of nfilt in sequence
+      const int j = lane_now();
+      const bool dom = j < K.nfilt && tr.theta >= gL.fth[j < MAXF ? j : 0] && tr.phi >= gL.fph[j < MAXF ? j : 0];
+      if (__any(dom)) okt = false;
+    }
     const bool okf = okt;
     (void)okf;
     bool ftype = false;
@@ -3320,7 +3365,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
 
   PROF_DECL
 #ifdef MPCX_PROFILE
-  if (lane < 6) gL.sprof[lane] = 0.0;
+  if (lane < 10) gL.sprof[lane] = 0.0;
   if (lane < 2) gL.dense_seen[lane] = 0u;
   sync();
 #endif
@@ -3458,6 +3503,8 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     ((gdbl*)args.lam_w)[(long)agent * NW + 16] = (double)gL.dense_seen[0];
     ((gdbl*)args.lam_w)[(long)agent * NW + 17] = (double)gL.dense_seen[1];
   }
+  if (args.lam_w != nullptr && lane == 0 && NW > 21)
+    for (int i = 6; i < 10; ++i) ((gdbl*)args.lam_w)[(long)agent * NW + 12 + i] = gL.sprof[i];
 #endif
 #ifndef MPCX_TRACE_LS
   if (args.lam_g != nullptr)

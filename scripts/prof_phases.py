@@ -63,7 +63,7 @@ def main():
     e0.record(); tw.copy_(tw0); plain.solve(tp, tl, tu, tw, stats=st); e1.record()
     torch.cuda.synchronize()
     print("plain build: kernel ms", e0.elapsed_time(e1))
-    prof = lw[:, :16].cpu().numpy()
+    prof = lw[:, :22].cpu().numpy()
     names = ["init", "ls_mult", "opt_err+mu", "hess", "rhs_x", "factor", "solve", "recover", "linesearch", "accept+gj",
              "f:assemble", "f:interior_bk", "f:schur+store", "f:chain", "s:forward", "s:chain+back"]
     tot = prof[:, :10].sum(axis=1).mean()
@@ -71,6 +71,10 @@ def main():
     for k, v in zip(names, prof.mean(axis=0)):
         print(f"{k:12s} {v/1e3:10.1f} kcyc  {100*v/tot:5.1f}%")
     print("total kcycles/agent", tot / 1e3)
+    if prof.shape[1] >= 22:
+        head = lw[:, 18:22].cpu().numpy().mean(axis=0)
+        for k, v in zip(["h:loads+terms", "h:reductions", "h:tests+mu", "h:stores+sync"], head):
+            print(f"{k:14s} {v/1e3:10.1f} kcyc")
     seen = lw[:, 16].cpu().numpy().astype(np.int64) | (lw[:, 17].cpu().numpy().astype(np.int64) << 32)
     hist = [int(((seen >> k) & 1).sum()) for k in range(be.problem.gen.dims["N"])]
     print("agents with stage k ever on the dense path:", hist)

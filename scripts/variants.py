@@ -43,6 +43,8 @@ VARIANTS = {
     "o2": (["-O2"], None),
     # the kernel source of the last commit (A/B against the working tree)
     "head": ([], "HEAD"),
+    # wave reductions as the __shfl_xor (ds_bpermute) butterfly instead of DPP + readlane
+    "shfl": (["-DMPCX_SHFL_REDUCE=1"], None),
     # leaf phases inlined into the kernel body: no callee-saved VGPR saves per call
     "inl_gj": ([], ("__device__ __noinline__ void eval_gj_lds(", "__device__ __attribute__((always_inline)) void eval_gj_lds(")),
     "inl_head": ([], ("__device__ __noinline__ int iter_head(const Agent a)", "__device__ __attribute__((always_inline)) int iter_head(const Agent a)")),

@@ -72,7 +72,10 @@ def build(names):
                 ktxt = subprocess.run(["git", "-C", str(ROOT), "show", "HEAD:agentlib-mpc_amd/csrc/mpcx_ipm.hip"],
                                       capture_output=True, text=True, check=True).stdout
             else:
-                ktxt = kern.read_text().replace(*tr)
+                ktxt = kern.read_text()
+                for pair in (tr if isinstance(tr, list) else [tr]):
+                    assert pair[0] in ktxt, f"{name}: pattern not found"
+                    ktxt = ktxt.replace(*pair)
             kp = d / f"mpcx_ipm_{name}.hip"
             kp.write_text(ktxt)
             src_text = src_text.replace('#include "mpcx_ipm.hip"', f'#include "{kp}"')

@@ -2085,7 +2085,11 @@ __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, doubl
 }
 
 // least-squares estimate of the constraint multipliers (IPOPT constr_mult_init_max)
-__device__ __noinline__ void ls_multipliers(const Agent a, const double constr_mult_init_max, double obj_scale) {
+// least-squares estimate of the constraint multipliers (IPOPT constr_mult_init_max): the rhs
+// here, the factorisation and solve in the kernel body (inlined there: as part of a called
+// phase the factorisation saved every callee-saved VGPR it uses -- MHE 148 per solve), then
+// ls_mult_finish
+__device__ __noinline__ void ls_mult_rhs(const Agent a, double obj_scale) {
   const int lane = lane_now();
   for (int i = NX + lane; i < NW; i += WAVE) {
     const double r = (a.xL()[i] == a.xU()[i]) ? 0.0 : -(obj_scale * acc_grad(a, i) - a.zL()[i] + a.zU()[i]);
@@ -2096,10 +2100,9 @@ __device__ __noinline__ void ls_multipliers(const Agent a, const double constr_m
     a.rhs(c / NG)[NP + c % NG] = (cl == 1) ? a.vL()[c] - a.vU()[c] : 0.0;
   }
   sync();
-  KKTDiag kd{0.0, 0.0, LSQ};
-  const Inertia in = factor(a, kd);
-  if (in.zero != 0) return;
-  solve(a);
+}
+__device__ __noinline__ void ls_mult_finish(const Agent a, const double constr_mult_init_max) {
+  const int lane = lane_now();
   double lmax = 0.0;
   for (int c = lane; c < M; c += WAVE) lmax = fmax(lmax, fabs(gL.u.sol[(c / NG) * NB + NP + c % NG]));
   lmax = wmax(lmax);
@@ -3379,7 +3382,12 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   K.n_fact = 0; K.n_ic = 0; K.n_fallback = 0; K.n_trials = 0; K.n_chain = 0; K.n_dense = 0;
   PROF(0);
   if (M > 0 && OPT(constr_mult_init_max) > 0.0) {
-    ls_multipliers(a, OPT(constr_mult_init_max), K.obj_scale);
+    ls_mult_rhs(a, K.obj_scale);
+    const Inertia in = factor(a, KKTDiag{0.0, 0.0, LSQ});
+    if (in.zero == 0) {
+      solve(a);
+      ls_mult_finish(a, OPT(constr_mult_init_max));
+    }
     K.n_fact = 1;
   }
   PROF(1);

@@ -16,9 +16,11 @@ from oracle import ipm, nlps
 
 class _Solver:
     tol = 1e-10
+    allow_failed = False
 
     def __init__(self):
         self.last = {}
+        self.failed = 0
 
     def _run(self, key, prob, p, lbw, ubw, w0):
         guess = self.last.get(key)
@@ -28,7 +30,12 @@ class _Solver:
             w0[fixed] = lbw[fixed]
         r = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p),
                       ipm.IPMOptions(tol=self.tol, max_iter=500, acceptable_iter=0))
-        assert r.success, (key, r.status)
+        # the reference's ADMM modules go on with whatever the local solve returned (stats only
+        # record the failure); the tests' fixtures are only made from rounds where every solve
+        # succeeded unless ``allow_failed`` (long fixture runs: tests/golden/make_admm_goldens.py)
+        if not self.allow_failed:
+            assert r.success, (key, r.status)
+        self.failed += 0 if r.success else 1
         self.last[key] = r.x
         return r.x
 

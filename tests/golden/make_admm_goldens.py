@@ -37,7 +37,9 @@ def _make_oracle(kind, N):
         return C2Oracle(N, bm.C2_ROOMS)
     from agentlib_mpc_amd.models import examples as ex
 
-    return C5Oracle(N, ex.room_cca_anns())
+    orc = C5Oracle(N, ex.room_cca_anns())
+    orc.allow_failed = True  # a supply agent's local solve may stop unsuccessfully; the round goes on
+    return orc
 
 
 def _worker(kind, N, conn):
@@ -45,6 +47,7 @@ def _worker(kind, N, conn):
     while True:
         msg = conn.recv()
         if msg is None:
+            conn.send(orc.failed)  # local solves that stopped unsuccessfully
             break
         ag, inp, rho = msg
         conn.send(orc(ag, inp, rho))
@@ -73,12 +76,15 @@ def run(kind, N, rho, iters, **crit):
     T = 3 * N if kind == "c2" else N
     state, hist, it, conv = oadmm.coordinated_round(orc.participation, orc.initial, None, rho, N, iters,
                                                     T=T, solve_batch=solve_batch, **crit)
+    failed = {}
     for ag in agents:
         pipes[ag].send(None)
+        failed[ag] = pipes[ag].recv()
     for p in procs:
         p.join()
     out = {"N": N, "iterations": it, "converged": conv, "rho": rho, "admm_iter_max": iters, "criterion": crit,
            "solver": {"tol": orc.tol, "acceptable_iter": 0, "max_iter": 500},
+           "failed_local_solves": failed,
            "history": [[float(a), float(b), float(c)] for a, b, c in hist],
            "means": {al: list(map(float, v.mean)) for al, v in state["vars"].items()}}
     path = os.path.join(HERE, f"{kind}_admm_N{N}.json")

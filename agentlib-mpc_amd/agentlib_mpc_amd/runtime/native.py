@@ -119,6 +119,47 @@ def build_library(force: bool = False) -> pathlib.Path:
     return LIB_PATH
 
 
+PYREAD_PATH = BUILD_DIR / "_mpcx_pyread.so"
+_pyread = None
+
+
+def build_pyread(force: bool = False) -> pathlib.Path:
+    """Compile the host-side attribute reader of the plugin batch (csrc/mpcx_pyread.c, a
+    CPython extension; gcc), in-tree."""
+    import sysconfig
+
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    src = CSRC / "mpcx_pyread.c"
+    if PYREAD_PATH.exists() and not force and PYREAD_PATH.stat().st_mtime >= src.stat().st_mtime:
+        return PYREAD_PATH
+    tmp = PYREAD_PATH.with_suffix(".so.tmp")
+    cc = os.environ.get("CC") or shutil.which("gcc") or "cc"
+    cmd = [cc, "-O2", "-shared", "-fPIC", "-Wall", f"-I{sysconfig.get_paths()['include']}", str(src), "-o", str(tmp)]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise NativeError(f"building {PYREAD_PATH.name} failed:\n{res.stderr[-4000:]}")
+    os.replace(tmp, PYREAD_PATH)
+    return PYREAD_PATH
+
+
+def load_pyread():
+    """The attribute reader module (raises NativeError when it was not built)."""
+    global _pyread
+    if _pyread is None:
+        import importlib.machinery
+        import importlib.util
+
+        if not PYREAD_PATH.exists():
+            raise NativeError(f"{PYREAD_PATH} is missing: run __graft_entry__.build() (or "
+                              "agentlib_mpc_amd.runtime.native.build_pyread()) first.")
+        loader = importlib.machinery.ExtensionFileLoader("_mpcx_pyread", str(PYREAD_PATH))
+        spec = importlib.util.spec_from_file_location("_mpcx_pyread", str(PYREAD_PATH), loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _pyread = mod
+    return _pyread
+
+
 def load_library():
     global _lib
     with _lib_lock:

@@ -93,6 +93,39 @@ def test_resident_inputs_raise_the_reference_errors():
         rb.update(bad, 0.0)
 
 
+def test_native_reader_equals_python_reader():
+    """The one-pass native attribute reader (``csrc/mpcx_pyread.c``) gives the Python
+    reader's columns for every value kind the agents may hold: floats, ints, numpy
+    scalars, NaN, a trajectory list (those three take the Python path per column), and a
+    missing variable raises KeyError."""
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    agents = _agents(cv, 9, 8)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    grid = len(be.problem.nlp.par_groups["d"].grid)
+    for i, c in enumerate(agents):
+        for k in c:
+            c[k] = copy.deepcopy(c[k])
+    agents[1]["load"].value = 120            # int
+    agents[2]["T_in"].value = np.float64(290.5)  # numpy scalar
+    agents[3]["mDot"].lb = 0                  # int bound
+    agents[4]["T_upper"].value = list(np.linspace(294.0, 296.0, grid))
+    agents[6]["mDot"].ub = np.nan             # NaN bound
+    got = rb.read(agents, 300.0)
+    want = rb._read_python(agents, 300.0, rb.refs)
+    assert got.keys() == want.keys()
+    for key in want:
+        g, w = got[key], want[key]
+        if isinstance(w, dict):
+            assert isinstance(g, dict) and g.keys() == w.keys()
+            for gid in w:
+                np.testing.assert_array_equal(g[gid], w[gid])
+        else:
+            np.testing.assert_array_equal(g, w)
+    del agents[5]["load"]
+    with pytest.raises(KeyError):
+        rb.read(agents, 300.0)
+
+
 @pytest.mark.gpu
 def test_gpu_resident_plugin_path_matches_host_marshalling():
     """Three closed-loop steps through ``solve_batch`` (resident inputs, warm start in HBM)

@@ -17,6 +17,8 @@ from oracle import ipm, nlps
 class _Solver:
     tol = 1e-10
     allow_failed = False
+    #: IPMOptions keywords of the local solves (None: tight, ``tol`` without acceptable stop)
+    options = None
 
     def __init__(self):
         self.last = {}
@@ -29,6 +31,7 @@ class _Solver:
             fixed = lbw == ubw
             w0[fixed] = lbw[fixed]
         r = ipm.solve(prob.functions(p), w0, lbw, ubw, prob.lbg(p), prob.ubg(p),
+                      ipm.IPMOptions(**self.options) if self.options is not None else
                       ipm.IPMOptions(tol=self.tol, max_iter=500, acceptable_iter=0))
         # the reference's ADMM modules go on with whatever the local solve returned (stats only
         # record the failure); the tests' fixtures are only made from rounds where every solve

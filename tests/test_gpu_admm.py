@@ -242,6 +242,33 @@ def test_gpu_c2_coordinator_to_stopping_rule_matches_oracle_fixture():
         np.testing.assert_allclose(traj[al], mean, rtol=RTOL, atol=1e-10)
 
 
+def test_gpu_stalled_c2_block_matches_oracle_fixture():
+    """A block of the bench's scaled C2 fleet that does NOT converge within the coordinator's
+    40 iterations (block 3 of seed 20261015 + 1, local solves at the reference's IPOPT
+    settings as in the bench leg), against the oracle's round of the same block
+    (`tests/golden/c2_admm_N10_b3.json`: hand-restated NLPs, oracle IPM at the same
+    settings, oracle coordinator): same outcome, residual history, final means.  With the
+    reference's acceptable-level local solves the primal residual levels off near 0.003,
+    above the 0.002 tolerance; with tight local solves 99 % of the blocks converge
+    (profiles/r03/s5/c2_conv.txt) -- the stall is the reference's settings, not the fleet."""
+    path = os.path.join(os.path.dirname(__file__), "golden", "c2_admm_N10_b3.json")
+    gold = json.load(open(path))
+    b = gold["block"]
+    fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=gold["N"], seed=gold["seed"], block_offset=b,
+                                       solver_options={"ipopt": {}}))
+    out = fl.run_coordinated(gold["rho"], admm_iter_max=gold["admm_iter_max"], **gold["criterion"])
+    assert out["iterations"] == gold["iterations"] and out["converged"] == gold["converged"]
+    assert not gold["converged"] and gold["iterations"] == gold["admm_iter_max"]
+    got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["records"]])
+    want = np.array(gold["history"])
+    rel = np.max(np.abs(got - want) / np.maximum(np.abs(want), 1e-4), axis=1)
+    print("C2 block %d per-iteration relative residual difference:" % b, np.array2string(rel, precision=2))
+    np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-9)
+    traj = fl.trajectories()
+    for al, mean in gold["means"].items():
+        np.testing.assert_allclose(traj[al.replace("_b0", f"_b{b}")], mean, rtol=1e-6, atol=1e-9)
+
+
 def test_gpu_every_block_stops_like_its_own_coordinator():
     """A 64-block C2 fleet (one launch per class and iteration): every block keeps its own
     stopping test and is frozen once converged, so each block ends at the iteration, with

@@ -16,6 +16,8 @@ from __future__ import annotations
 
 from typing import Callable, Dict, Tuple
 
+import os
+
 import numpy as np
 
 from agentlib_mpc_amd.data_structures import admm_datatypes as adt
@@ -487,11 +489,19 @@ def compile_all(verbose: bool = False):
     variants["mhe_room"] = lambda: mhe_room()
     variants["mhe_room_u"] = lambda: mhe_room(estimate="mDot")
     variants["rng_room_mpc"] = lambda: rng_room_mpc()
-    for name, fn in variants.items():
-        be, _ = fn()
-        paths[name] = be.problem.compile()
-        if verbose:
-            print(f"[mpcx] {name}: {paths[name].name}")
+    from concurrent.futures import ThreadPoolExecutor
+
+    probs = {name: fn()[0].problem for name, fn in variants.items()}
+    jobs = int(os.environ.get("MPCX_BUILD_JOBS", "4"))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:  # hipcc processes: one per code object
+        futs = {(name, v): ex.submit(native.compile_model, pr.gen, False, v)
+                for name, pr in probs.items() for v in (None, native.SMALL_FLEET)}
+        for (name, v), fut in futs.items():
+            path = fut.result()
+            if v is None:
+                paths[name] = path
+            if verbose:
+                print(f"[mpcx] {name}{' small-fleet' if v else ''}: {path.name if path else 'workspace does not fit LDS'}")
     return paths
 
 

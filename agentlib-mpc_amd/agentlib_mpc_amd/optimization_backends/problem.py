@@ -58,9 +58,13 @@ class CompiledProblem:
             self._native = NativeProblem(self.gen)
         return self._native
 
-    def compile(self):
-        from agentlib_mpc_amd.runtime.native import compile_model
+    def compile(self, small_fleet: bool = True):
+        """Compile the structure's code object and, when its workspace fits a CU's LDS, the
+        small-fleet build (``native.SMALL_FLEET``); returns the main code object's path."""
+        from agentlib_mpc_amd.runtime.native import SMALL_FLEET, compile_model
 
+        if small_fleet:
+            compile_model(self.gen, variant=SMALL_FLEET)
         return compile_model(self.gen)
 
     # -- inputs ------------------------------------------------------------------

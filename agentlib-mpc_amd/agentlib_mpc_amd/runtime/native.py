@@ -80,7 +80,8 @@ class Stats(ctypes.Structure):
 STATS_BYTES = ctypes.sizeof(Stats)
 EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
-    "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_batch_solve",
+    "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_problem_small_fleet",
+    "mpcx_batch_solve",
     "mpcx_admm_moments_size", "mpcx_admm_moments", "mpcx_admm_finalize",
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
@@ -179,6 +180,7 @@ def load_library():
         lib.mpcx_set_options.argtypes = [vp, ctypes.POINTER(Options)]
         lib.mpcx_reserve.argtypes = [vp, i32]
         lib.mpcx_workspace_bytes_per_agent.argtypes = [vp]
+        lib.mpcx_problem_small_fleet.argtypes = [vp, ctypes.c_char_p, i32]
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
         lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp, vp]
         i64 = ctypes.c_int64
@@ -226,25 +228,40 @@ def _extra_defines() -> List[str]:
     return [d for d in os.environ.get("MPCX_DEFINES", "").split(",") if d]
 
 
-def code_object_path(gen_key: str) -> pathlib.Path:
+#: small-fleet variant (workspace in LDS, one agent per CU; ``mpcx_problem_small_fleet``)
+SMALL_FLEET = "wslds"
+_VARIANT_DEFINES = {None: [], SMALL_FLEET: ["MPCX_WS_LDS"]}
+
+
+def code_object_path(gen_key: str, variant: Optional[str] = None) -> pathlib.Path:
     extra = _extra_defines()
     tag = ("_" + hashlib.sha1(",".join(extra).encode()).hexdigest()[:6]) if extra else ""
-    return KERNEL_DIR / f"mpcx_{gen_key}_{_kernel_deps_hash()}{tag}_{OFFLOAD_ARCH}.hsaco"
+    vtag = f"_{variant}" if variant else ""
+    return KERNEL_DIR / f"mpcx_{gen_key}_{_kernel_deps_hash()}{tag}{vtag}_{OFFLOAD_ARCH}.hsaco"
 
 
-def compile_model(gen, verbose: bool = False) -> pathlib.Path:
-    """Compile a generated model source to a gfx950 code object (cached)."""
+def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> Optional[pathlib.Path]:
+    """Compile a generated model source to a gfx950 code object (cached).  ``variant``
+    SMALL_FLEET: the workspace-in-LDS build; None (and a ``.nofit`` marker) when the
+    structure's workspace does not fit a CU's LDS."""
     KERNEL_DIR.mkdir(parents=True, exist_ok=True)
-    out = code_object_path(gen.key)
+    out = code_object_path(gen.key, variant)
     if out.exists():
         return out
+    nofit = out.with_suffix(".nofit")
+    if variant is not None and nofit.exists():
+        return None
     src = out.with_suffix(".hip")
     src.write_text(gen.source)
     tmp = out.with_suffix(".tmp")
+    defs = _extra_defines() + _VARIANT_DEFINES[variant]
     cmd = [_hipcc(), "--genco", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17",
-           f"-I{INCLUDE}", f"-I{CSRC}", *[f"-D{d}" for d in _extra_defines()], str(src), "-o", str(tmp)]
+           f"-I{INCLUDE}", f"-I{CSRC}", *[f"-D{d}" for d in defs], str(src), "-o", str(tmp)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
+        if variant is not None and "workspace does not fit LDS" in res.stderr:
+            nofit.write_text("")
+            return None
         raise NativeError(f"compiling {src} failed:\n{res.stderr[-4000:]}")
     if verbose and res.stderr:
         print(res.stderr)
@@ -269,6 +286,16 @@ class NativeProblem:
         if rc != 0:
             raise NativeError(f"mpcx_problem_create failed ({rc}) for {path}")
         self.handle = handle
+        self.small_fleet_path = None
+        if hsaco is None and os.environ.get("MPCX_SMALL_FLEET", "1") != "0":
+            # small fleets (<= one agent per CU) run the workspace-in-LDS build when the
+            # structure's workspace fits a CU's LDS (compiled by build(), else here)
+            sp = compile_model(gen, variant=SMALL_FLEET)
+            if sp is not None:
+                rc = self.lib.mpcx_problem_small_fleet(handle, str(sp).encode(), -1)
+                if rc != 0:
+                    raise NativeError(f"mpcx_problem_small_fleet failed ({rc}) for {sp}")
+                self.small_fleet_path = sp
         self.options = default_options()
         self.nw = d["NX"] + d["N"] * (d["NV"] + d["NX"])
         self.ng_total = d["N"] * d["NG"]
@@ -291,6 +318,13 @@ class NativeProblem:
         rc = self.lib.mpcx_set_options(self.handle, ctypes.byref(self.options))
         if rc != 0:
             raise NativeError(f"mpcx_set_options failed ({rc})")
+
+    def set_small_fleet_max(self, max_agents: int):
+        """Largest batch launched on the small-fleet (workspace-in-LDS) build: -1 the
+        device's CU count (default), 0 never."""
+        rc = self.lib.mpcx_problem_small_fleet(self.handle, None, int(max_agents))
+        if rc != 0:
+            raise NativeError(f"mpcx_problem_small_fleet failed ({rc})")
 
     def workspace_bytes_per_agent(self) -> int:
         return int(self.lib.mpcx_workspace_bytes_per_agent(self.handle))

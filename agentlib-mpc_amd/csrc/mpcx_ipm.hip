@@ -56,6 +56,10 @@ constexpr int MAXF = 32;           // filter entries kept in LDS
 static_assert(MAXF <= 64, "the filter test reads one entry per lane");
 constexpr double INF_BOUND = 1e19;
 constexpr double TS = MPCX_TS;
+#ifdef MPCX_WS_LDS  // small-fleet variant: one agent per CU, its workspace in LDS
+#undef MPCX_MIN_WAVES
+#define MPCX_MIN_WAVES 1
+#endif
 #ifndef MPCX_MIN_WAVES
 #define MPCX_MIN_WAVES 4
 #endif
@@ -67,6 +71,16 @@ typedef __attribute__((address_space(1))) double gdbl;
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(3))) double ldsd;
 typedef __attribute__((address_space(3))) int ldsi;
+// the agent's workspace slab: HBM (one slab per agent, 16 agents per CU) or, in the
+// small-fleet variant (MPCX_WS_LDS: one agent per CU, fleets up to one agent per CU), LDS --
+// every phase's operand round trip then costs an LDS access instead of an L2 / HBM one
+#ifdef MPCX_WS_LDS
+typedef ldsd wdbl;
+typedef ldsi wint;
+#else
+typedef gdbl wdbl;
+typedef gint wint;
+#endif
 
 // stage-local system [V_k, lambda_rest | x_k | mu_k, x_{k+1} | rhs].  mu_k: the NMU
 // continuity rows of the stage (the rows through x_{k+1}) when they are kept in the border
@@ -420,7 +434,13 @@ constexpr int SLOT_BYTES = 8 * PKS + 8 * NI;  // dense packed system + perm/piv 
 constexpr int CSLOT_BYTES = 8 * NCS;          // compact image (static elimination)
 constexpr int REST_BYTES = (int)sizeof(LdsRest);
 constexpr int UFIX_BYTES = cmax((int)sizeof(SeqLds), cmax(8 * N * NB, (int)sizeof(TrialLds)));
-constexpr int LDS_CU = 163840, LDS_SLACK = 256;
+constexpr int LDS_CU_ALL = 163840, LDS_SLACK = 256;
+#ifdef MPCX_WS_LDS
+constexpr int WS_LDS_BYTES = (int)(8 * WS_DOUBLES);
+#else
+constexpr int WS_LDS_BYTES = 0;
+#endif
+constexpr int LDS_CU = LDS_CU_ALL - WS_LDS_BYTES;  // what the per-agent LDS state may take
 __host__ __device__ constexpr int apc_for(int need) {  // agents per CU for a per-agent need
   return (need + LDS_SLACK) * 16 <= LDS_CU ? 16 : (need + LDS_SLACK) * 8 <= LDS_CU ? 8
        : (need + LDS_SLACK) * 5 <= LDS_CU ? 5 : (need + LDS_SLACK) * 4 <= LDS_CU ? 4
@@ -434,7 +454,12 @@ constexpr int K0 = 0;
 constexpr int NRS = N - K0;                         // stages in the regular rounds
 constexpr int APC_ONE = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, cmax(NRS, 1) * CSLOT_BYTES)));
 constexpr int APC_TWO = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, cmin(cmax(NRS, 1), 2) * CSLOT_BYTES)));
+#ifdef MPCX_WS_LDS
+static_assert(WS_LDS_BYTES + REST_BYTES + UFIX_BYTES + LDS_SLACK <= LDS_CU_ALL, "MPCX_WS_LDS: workspace does not fit LDS");
+constexpr int APC = 1;
+#else
 constexpr int APC = (APC_TWO >= 16 || APC_ONE < 4) ? APC_TWO : APC_ONE;
+#endif
 #ifdef MPCX_LDS_TARGET_OVERRIDE  // diagnostics (scripts/variants.py): per-agent byte budget
 constexpr int LDS_BUDGET = MPCX_LDS_TARGET_OVERRIDE;
 #else
@@ -479,7 +504,12 @@ static_assert(sizeof(Lds) + LDS_SLACK <= LDS_CU / APC, "LDS share per agent exce
 
 __shared__ Lds gL;  // one agent per workgroup: the agent's LDS scratch
 __device__ __forceinline__ KArgs* kargs() { return (KArgs*)uni64(gL.kp_bits); }
-__device__ __forceinline__ gdbl* ws_base() { return (gdbl*)uni64(gL.ws_bits); }
+#ifdef MPCX_WS_LDS
+__shared__ double gWS[WS_DOUBLES];
+__device__ __forceinline__ wdbl* ws_base() { return (wdbl*)gWS; }
+#else
+__device__ __forceinline__ wdbl* ws_base() { return (wdbl*)uni64(gL.ws_bits); }
+#endif
 #define LDSP(x) ((ldsd*)(x))
 #define LDSI(x) ((ldsi*)(x))
 #ifdef MPCX_PROFILE
@@ -523,56 +553,56 @@ __device__ __forceinline__ gdbl* ws_base() { return (gdbl*)uni64(gL.ws_bits); }
 // ---------------------------------------------------------------------------
 struct Agent {
   // the agent's workspace slab, wave-uniform (SGPRs): nothing of the view is passed in VGPRs
-  __device__ __forceinline__ gdbl* base() const { return ws_base(); }
+  __device__ __forceinline__ wdbl* base() const { return ws_base(); }
 #define ws base()
-  __device__ gdbl* x() const { return ws + O_X; }
-  __device__ gdbl* s() const { return ws + O_S; }
-  __device__ gdbl* lam() const { return ws + O_LAM; }
-  __device__ gdbl* zL() const { return ws + O_ZL; }
-  __device__ gdbl* zU() const { return ws + O_ZU; }
-  __device__ gdbl* vL() const { return ws + O_VL; }
-  __device__ gdbl* vU() const { return ws + O_VU; }
-  __device__ gdbl* xL() const { return ws + O_XL; }
-  __device__ gdbl* xU() const { return ws + O_XU; }
-  __device__ gdbl* sL() const { return ws + O_SL; }
-  __device__ gdbl* sU() const { return ws + O_SU; }
-  __device__ gdbl* gs() const { return ws + O_GS; }
-  __device__ gdbl* gv() const { return ws + O_GV; }
-  __device__ gdbl* dx() const { return ws + O_DX; }
-  __device__ gdbl* ds() const { return ws + O_DS; }
-  __device__ gdbl* dl() const { return ws + O_DL; }
-  __device__ gdbl* lb() const { return ws + O_LB; }
-  __device__ gdbl* ub() const { return ws + O_UB; }
-  __device__ gdbl* sdg() const { return ws + O_SDG; }
-  __device__ gdbl* jtl() const { return ws + O_JTL; }
-  __device__ gdbl* sdj() const { return ws + O_SDJ; }
-  __device__ gdbl* sdh() const { return ws + O_SDH; }
-  __device__ gdbl* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
-  __device__ gdbl* tr(int k) const { return ws + O_TR + k; }  // [NTR][NI][N]: W_k[t][p] at tr(k)[(t NI + p) N]
-  __device__ gint* prm(int k) const { return reinterpret_cast<gint*>(ws + O_PRM) + (long)k * NI; }
-  __device__ gdbl* kx() const { return ws + O_KX; }
-  __device__ gdbl* kd() const { return ws + O_KD; }
-  __device__ gdbl* sol(int k) const { return ws + O_SOL + (long)k * NB; }
-  __device__ gdbl* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
-  __device__ gdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
-  __device__ gdbl* lp(int k) const { return ws + O_LP + k; }  // entry c of stage k at lp(k)[c * N]
-  __device__ gdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
-  __device__ gdbl* sqw() const { return ws + O_SQW; }
-  __device__ gdbl* rp() const { return ws + O_RP; }
-  __device__ gdbl* rn() const { return ws + O_RN; }
-  __device__ gdbl* rzp() const { return ws + O_RZP; }
-  __device__ gdbl* rzn() const { return ws + O_RZN; }
-  __device__ gdbl* rdp() const { return ws + O_RDP; }
-  __device__ gdbl* rdn() const { return ws + O_RDN; }
-  __device__ gdbl* xr() const { return ws + O_XR; }
-  __device__ gdbl* sr() const { return ws + O_SR; }
-  __device__ gdbl* lr() const { return ws + O_LR; }
-  __device__ gdbl* gvr() const { return ws + O_GVR; }
-  __device__ gdbl* zl0() const { return ws + O_ZL0; }
-  __device__ gdbl* zu0() const { return ws + O_ZU0; }
-  __device__ gdbl* vl0() const { return ws + O_VL0; }
-  __device__ gdbl* vu0() const { return ws + O_VU0; }
-  __device__ gdbl* flt0() const { return ws + O_FLT0; }
+  __device__ wdbl* x() const { return ws + O_X; }
+  __device__ wdbl* s() const { return ws + O_S; }
+  __device__ wdbl* lam() const { return ws + O_LAM; }
+  __device__ wdbl* zL() const { return ws + O_ZL; }
+  __device__ wdbl* zU() const { return ws + O_ZU; }
+  __device__ wdbl* vL() const { return ws + O_VL; }
+  __device__ wdbl* vU() const { return ws + O_VU; }
+  __device__ wdbl* xL() const { return ws + O_XL; }
+  __device__ wdbl* xU() const { return ws + O_XU; }
+  __device__ wdbl* sL() const { return ws + O_SL; }
+  __device__ wdbl* sU() const { return ws + O_SU; }
+  __device__ wdbl* gs() const { return ws + O_GS; }
+  __device__ wdbl* gv() const { return ws + O_GV; }
+  __device__ wdbl* dx() const { return ws + O_DX; }
+  __device__ wdbl* ds() const { return ws + O_DS; }
+  __device__ wdbl* dl() const { return ws + O_DL; }
+  __device__ wdbl* lb() const { return ws + O_LB; }
+  __device__ wdbl* ub() const { return ws + O_UB; }
+  __device__ wdbl* sdg() const { return ws + O_SDG; }
+  __device__ wdbl* jtl() const { return ws + O_JTL; }
+  __device__ wdbl* sdj() const { return ws + O_SDJ; }
+  __device__ wdbl* sdh() const { return ws + O_SDH; }
+  __device__ wdbl* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
+  __device__ wdbl* tr(int k) const { return ws + O_TR + k; }  // [NTR][NI][N]: W_k[t][p] at tr(k)[(t NI + p) N]
+  __device__ wint* prm(int k) const { return reinterpret_cast<wint*>(ws + O_PRM) + (long)k * NI; }
+  __device__ wdbl* kx() const { return ws + O_KX; }
+  __device__ wdbl* kd() const { return ws + O_KD; }
+  __device__ wdbl* sol(int k) const { return ws + O_SOL + (long)k * NB; }
+  __device__ wdbl* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
+  __device__ wdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
+  __device__ wdbl* lp(int k) const { return ws + O_LP + k; }  // entry c of stage k at lp(k)[c * N]
+  __device__ wdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
+  __device__ wdbl* sqw() const { return ws + O_SQW; }
+  __device__ wdbl* rp() const { return ws + O_RP; }
+  __device__ wdbl* rn() const { return ws + O_RN; }
+  __device__ wdbl* rzp() const { return ws + O_RZP; }
+  __device__ wdbl* rzn() const { return ws + O_RZN; }
+  __device__ wdbl* rdp() const { return ws + O_RDP; }
+  __device__ wdbl* rdn() const { return ws + O_RDN; }
+  __device__ wdbl* xr() const { return ws + O_XR; }
+  __device__ wdbl* sr() const { return ws + O_SR; }
+  __device__ wdbl* lr() const { return ws + O_LR; }
+  __device__ wdbl* gvr() const { return ws + O_GVR; }
+  __device__ wdbl* zl0() const { return ws + O_ZL0; }
+  __device__ wdbl* zu0() const { return ws + O_ZU0; }
+  __device__ wdbl* vl0() const { return ws + O_VL0; }
+  __device__ wdbl* vu0() const { return ws + O_VU0; }
+  __device__ wdbl* flt0() const { return ws + O_FLT0; }
 #undef ws
 };
 
@@ -627,7 +657,7 @@ __device__ __noinline__ double eval_fg_lds(const Agent a) {
 }
 
 // f and unscaled g at a point in the workspace
-__device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* gout) {
+__device__ __noinline__ double eval_fg_ws(const Agent a, const wdbl* xv, wdbl* gout) {
   NET_PREP(xv, fg);
   double f = 0.0;
   for (int k = lane_now(); k < N; k += WAVE) {
@@ -640,7 +670,7 @@ __device__ __noinline__ double eval_fg_ws(const Agent a, const gdbl* xv, gdbl* g
 
 // derivatives at a point in the workspace; full: also the strided jacobian (scaling and
 // the block-chain fallback read it; the stage-parallel path reads lp and jtl only)
-__device__ __noinline__ void eval_gj_ws(const Agent a, const gdbl* xv, int full) {
+__device__ __noinline__ void eval_gj_ws(const Agent a, const wdbl* xv, int full) {
   NET_PREP(xv, gj);
   for (int k = lane_now(); k < N; k += WAVE)
     STAGE_GJ((const double*)(xv + k * NP), par_stage(k), par_global(), k * TS, (double*)(a.sdg() + k),
@@ -1118,7 +1148,7 @@ __device__ __noinline__ void seq_solve(const Agent a) {
         L.v[i] = v;
       }
       wsync();
-      const gdbl* Ai = a.fac(k);
+      const wdbl* Ai = a.fac(k);
       for (int i = lane; i < NB; i += WAVE) {
         double acc = 0.0;
         for (int j = 0; j < NB; ++j) acc += Ai[i * LDB + j] * L.v[j];
@@ -1137,7 +1167,7 @@ __device__ __noinline__ void seq_solve(const Agent a) {
         L.t[c] = s;
       }
       wsync();
-      const gdbl* Ai = a.fac(k);
+      const wdbl* Ai = a.fac(k);
       for (int i = lane; i < NB; i += WAVE) {
         double u = a.sol(k)[i];
         for (int c = 0; c < NX; ++c) u -= Ai[i * LDB + NV + c] * L.t[c];
@@ -1200,7 +1230,7 @@ __device__ __forceinline__ int lblk(int i, int kind) {
 template <int GG, bool COMPACT>
 __device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd* F, const KKTDiag kd,
                                                unsigned long long fm) {
-  const gdbl* ws = a.base();
+  const wdbl* ws = a.base();
   for (int i = g; i < NLOC; i += GG) {
     const int ki = lkind(i);
     const bool prim = (ki == 0 || ki == 3);
@@ -1222,7 +1252,7 @@ __device__ __forceinline__ void local_diagonal(const Agent a, int k, int g, ldsd
 // derivative arrays (least-squares multiplier system; diagonal terms added afterwards)
 __device__ __forceinline__ double generic_entry(const Agent a, int k, int i, int j, unsigned long long fm,
                                                 const KKTDiag kd) {
-  const gdbl* ws = a.base();
+  const wdbl* ws = a.base();
   const int ki = lkind(i), kj = lkind(j);
   const bool pi = (ki == 0 || ki == 2 || ki == 3), pj = (kj == 0 || kj == 2 || kj == 3);
   const bool fi = pi && ((fm >> i) & 1ull), fj = pj && ((fm >> j) & 1ull);
@@ -1282,9 +1312,9 @@ template <int GG, bool DENSE>
 __device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F, const KKTDiag kd) {
   constexpr int EPC = (NCPT + GG - 1) / GG;  // compact entries per lane
   const unsigned long long fm = gL.fixm[k];
-  const gdbl* src = a.lp(k);
-  const gdbl* dg = a.dg(k);
-  const gdbl* rb = a.rhs(k);
+  const wdbl* src = a.lp(k);
+  const wdbl* dg = a.dg(k);
+  const wdbl* rb = a.rhs(k);
   if constexpr (DENSE) {
     for (int t = g; t < PKB; t += GG) F[t] = 0.0;
     wsync();
@@ -1884,7 +1914,7 @@ __device__ __noinline__ void solve(const Agent a) {
 #pragma unroll 1
   for (int q = lane; q < N * NI; q += WAVE) {
     const int k = q % N, p = q / N;  // stage fastest: the stage-minor operator reads coalesce
-    const gdbl* t = a.tr(k) + (long)p * N;
+    const wdbl* t = a.tr(k) + (long)p * N;
     double u = t[(long)(NX + NC) * NI * N];
 #pragma unroll
     for (int c = 0; c < NX; ++c) u -= ((k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0) * t[(long)c * NI * N];
@@ -3361,7 +3391,9 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   const int lane = lane_now();
   if (lane == 0) {
     gL.kp_bits = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+#ifndef MPCX_WS_LDS
     gL.ws_bits = (unsigned long long)((gdbl*)args.ws + (long)agent * args.ws_stride);
+#endif
   }
   wsync();
   KState& K = gL.ks;
@@ -3549,5 +3581,10 @@ extern "C" __global__ void mpcx_query(long* out) {
     out[1] = N; out[2] = NX; out[3] = NV; out[4] = NG; out[5] = NPS; out[6] = NPG;
     out[7] = MPCX_KERNEL_ABI;  // one definition (mpcx_internal.h), checked by mpcx_problem_create
     out[8] = sizeof(Lds);
+#ifdef MPCX_WS_LDS
+    out[9] = 1;  // workspace in LDS: one agent per CU (small fleets)
+#else
+    out[9] = 0;
+#endif
   }
 }

@@ -9,6 +9,7 @@
  *                            (optimization_backends/casadi_/core/discretization.py:156-162,
  *                             data_structures/casadi_utils.py:282-300): load the generated
  *                             code object of one transcribed NLP structure.
+ *   mpcx_problem_small_fleet <- the same call (a small-fleet specialisation, workspace in LDS)
  *   mpcx_batch_solve      <- self._optimizer(**nlp_inputs)
  *                            (optimization_backends/casadi_/core/discretization.py:203), i.e.
  *                            ca.nlpsol("mpc", "ipopt", ...)(p, x0, lbx, ubx, lbg, ubg),
@@ -47,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 5
+#define MPCX_API_VERSION 6
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -142,6 +143,15 @@ int mpcx_set_options(mpcx_handle* h, const mpcx_options* opts);
 int mpcx_reserve(mpcx_handle* h, int32_t n_agents);
 /* Workspace bytes per agent (for capacity planning on 288 GB HBM). */
 int64_t mpcx_workspace_bytes_per_agent(const mpcx_handle* h);
+/* Small-fleet specialisation of the same structure (replaces the same reference call as
+ * mpcx_problem_create, for a handful of agents -- the reference's usual one MPC agent per
+ * process, core/discretization.py:203): a second code object built with the agent's
+ * workspace in LDS (MPCX_WS_LDS, one agent per CU), so that every operand round trip of the
+ * IPM is an LDS access instead of an L2 / HBM one.  code_object_path NULL keeps the loaded
+ * one.  mpcx_batch_solve launches it for batches of at most max_agents agents
+ * (max_agents < 0: the device's CU count, one generation; 0: never).  Returns
+ * MPCX_ERR_MODULE if the code object is not such a variant of this structure. */
+int mpcx_problem_small_fleet(mpcx_handle* h, const char* code_object_path, int32_t max_agents);
 
 /* Batched solve.  Shapes (agent-major, fp64, device):
  *   active [n_agents] int32 or NULL  agents with active[a] == 0 are skipped (their outputs

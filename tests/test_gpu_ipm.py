@@ -289,3 +289,36 @@ def test_gpu_c3_fleet_matches_c_oracle():
     np.testing.assert_allclose([s["obj"] for s, o in zip(gs, ok) if o], [s["obj"] for s, o in zip(cs, ok) if o],
                                rtol=RTOL_OBJ)
     np.testing.assert_allclose(gw[ok], cw[ok], rtol=RTOL_TRAJ, atol=1e-7 * 300.0)
+
+
+def test_gpu_small_fleet_build_matches_hbm_build():
+    """The small-fleet build (workspace in LDS, one agent per CU; ``mpcx_problem_small_fleet``,
+    used for batches of at most one agent per CU) against the HBM-workspace build on the same
+    200 C3 agents at the reference's settings: same status and iteration count per agent, same
+    solutions (the arithmetic is the same; only the memory the workspace lives in differs)."""
+    import bench
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+
+    n = 200
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261015 + 2))
+    native = be._native()
+    assert native.small_fleet_path is not None, "one_room's workspace fits LDS: the small-fleet build must load"
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    out = {}
+    for mode, max_agents in (("lds", -1), ("hbm", 0)):
+        native.set_small_fleet_max(max_agents)
+        tw = T(w0)
+        st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device="cuda")
+        native.solve(T(p), T(lbw), T(ubw), tw, stats=st)
+        torch.cuda.synchronize()
+        out[mode] = (tw.cpu().numpy(), stats_to_dicts(st.cpu().numpy().tobytes()))
+    native.set_small_fleet_max(-1)
+    (wl, sl), (wh, sh) = out["lds"], out["hbm"]
+    assert [s["status"] for s in sl] == [s["status"] for s in sh]
+    assert [s["iter_count"] for s in sl] == [s["iter_count"] for s in sh]
+    assert np.mean([s["status"] in (0, 1) for s in sl]) > 0.99
+    np.testing.assert_allclose(wl, wh, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose([s["obj"] for s in sl], [s["obj"] for s in sh], rtol=1e-12)

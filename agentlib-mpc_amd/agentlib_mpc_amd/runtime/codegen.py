@@ -506,8 +506,13 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
         "#define MPCX_ELIM_FENCE __builtin_amdgcn_sched_barrier(0)",
         "#endif",
         "typedef __attribute__((address_space(3))) double mpcx_elim_ld;",
+        "#ifdef MPCX_WS_LDS  // small-fleet build: the workspace (operators, pivot order) is in LDS",
+        "typedef __attribute__((address_space(3))) double mpcx_elim_gd;",
+        "typedef __attribute__((address_space(3))) int mpcx_elim_gi;",
+        "#else",
         "typedef __attribute__((address_space(1))) double mpcx_elim_gd;",
         "typedef __attribute__((address_space(1))) int mpcx_elim_gi;",
+        "#endif",
         "__device__ __forceinline__ int gen_stage_elim(mpcx_elim_ld* __restrict__ F, mpcx_elim_ld* __restrict__ S, mpcx_elim_ld* __restrict__ ZX, mpcx_elim_gd* __restrict__ TR, mpcx_elim_gi* __restrict__ PRM, int* __restrict__ inert) {",
         "  int bad = 0, pos = 0, neg = 0;",
         *elim_lines,

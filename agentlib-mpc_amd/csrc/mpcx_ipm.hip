@@ -1745,6 +1745,9 @@ __device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* F) {
   mpcx_elim_ld* const ZX = (mpcx_elim_ld*)LDSP(gL.zx + k * (NX + NC));
   int bad;
 #ifdef MPCX_STATIC_ELIM0
+  // the generated body addresses the workspace with its own pointer types: they must be the
+  // workspace's (an HBM-typed pointer into the LDS workspace would be a wild address)
+  static_assert(__is_same(mpcx_elim_gd, wdbl) && __is_same(mpcx_elim_gi, wint), "workspace pointer types");
   if constexpr (STAGE0) bad = gen_stage_elim0((mpcx_elim_ld*)F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
   else
 #endif

@@ -4,12 +4,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "agentlib-mpc_amd")]
 import numpy as np
 
-def build_profile_hsaco(gen):
+def build_profile_hsaco(gen, wslds=False):
     from agentlib_mpc_amd.runtime import native
-    src = native.KERNEL_DIR / f"prof_{gen.key}.hip"
+    src = native.KERNEL_DIR / f"prof_{gen.key}{'_wslds' if wslds else ''}.hip"
     out = src.with_suffix(".hsaco")
     src.parent.mkdir(parents=True, exist_ok=True)
-    src.write_text("#define MPCX_PROFILE 1\n" + gen.source)
+    src.write_text("#define MPCX_PROFILE 1\n" + ("#define MPCX_WS_LDS 1\n" if wslds else "") + gen.source)
     subprocess.run([native._hipcc(), "--genco", "--offload-arch=gfx950", "-O3", "-std=c++17",
                     f"-I{native.INCLUDE}", f"-I{native.CSRC}", str(src), "-o", str(out)], check=True)
     return out
@@ -25,8 +25,11 @@ def main():
     kopts = ipopt_options_to_kernel(sopts)
     be, cv = {**bm.BUILDERS, "mhe_room": bm.mhe_room, "rng_room_mpc": bm.rng_room_mpc}[model](solver_options=sopts)
     path = build_profile_hsaco(be.problem.gen)
+    # WSLDS=1: the small-fleet build (workspace in LDS) for batches of <= one agent per CU
+    wslds = os.environ.get("WSLDS", "0") == "1"
+    lpath = build_profile_hsaco(be.problem.gen, wslds=True) if wslds else None
     if len(sys.argv) > 1 and sys.argv[1] == "build":
-        print(path); return
+        print(path, lpath); return
     import torch
     n = int(os.environ.get("AGENTS", "4096"))
     if model == "one_room":
@@ -38,6 +41,8 @@ def main():
     nat = NativeProblem(be.problem.gen, hsaco=path)
     nat.set_options(**kopts)
     nat.reserve(n)
+    if lpath is not None:
+        assert nat.lib.mpcx_problem_small_fleet(nat.handle, str(lpath).encode(), -1) == 0
     d = torch.device("cuda")
     T = lambda a: torch.as_tensor(a, device=d).contiguous()
     tp, tl, tu, tw = T(p), T(lbw), T(ubw), T(w0)

@@ -39,6 +39,10 @@ import numpy as np
 
 from agentlib_mpc_amd.optimization_backends.problem import BatchMarshal
 
+#: batches of at most this many agents update their inputs on the host and upload them in
+#: one copy; larger ones scatter the changed columns on the device
+SMALL_BATCH = 64
+
 
 def _values(vs, attr, n):
     """(n,) float array of one attribute over the agents, or None if not all numbers
@@ -128,8 +132,29 @@ class ResidentBatch:
         p, lbw, ubw, w0, (ls, us) = m.inputs(batch_vars, now, None, return_sampled_bounds=True)
         self.base_p, self.base_ls, self.base_us = p[0].copy(), ls[0].copy(), us[0].copy()
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(device)  # noqa: E731
-        self.P, self.L, self.U, self.W = T(p), T(lbw), T(ubw), T(w0)
+        # P, L, U, W: contiguous blocks of ONE device buffer, so that a small batch uploads all
+        # of its inputs with one copy
+        sizes = [p.size, lbw.size, ubw.size, w0.size]
+        self.BUF = torch.empty(sum(sizes), dtype=torch.float64, device=device)
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        views = [self.BUF[offs[i]:offs[i + 1]].view(a.shape) for i, a in enumerate((p, lbw, ubw, w0))]
+        self.P, self.L, self.U, self.W = views
+        self.BUF.copy_(torch.from_numpy(np.concatenate([a.ravel() for a in (p, lbw, ubw, w0)])))
         self.LS, self.US = T(ls), T(us)  # sampled bounds (before the parameter overrides)
+        # small batches (the reference's one agent per process): the inputs are kept on the
+        # host too and updated there (numpy), then uploaded in one copy -- a handful of device
+        # scatters costs ~20 us of launch overhead each, more than uploading a few KB
+        self.small = n <= SMALL_BATCH
+        if self.small:
+            pin = device.type == "cuda"
+            self.hbuf_t = torch.empty(sum(sizes), dtype=torch.float64, pin_memory=pin)
+            self.hbuf = self.hbuf_t.numpy()
+            self._h2d = None  # event after the last upload (the host mirrors are its source)
+            self.hP, self.hL, self.hU, self.hW = [self.hbuf[offs[i]:offs[i + 1]].reshape(a.shape)
+                                                  for i, a in enumerate((p, lbw, ubw, w0))]
+            self.hbuf[:] = self.BUF.cpu().numpy()
+            self.hLS, self.hUS = ls.copy(), us.copy()
+            self.over_h = {k: (c, q) for k, (c, q) in m.over.items() if c.size}
         self.idx = {}
         for key, cols in self.targets.items():
             for _, c, _ in cols:
@@ -215,6 +240,8 @@ class ResidentBatch:
         bounds and guesses; returns the snapshot of the values read."""
         torch = self.torch
         cur = self.read(batch_vars, now)
+        if self.small:
+            return self._update_host(batch_vars, now, cur)
         dst = {"p": self.P, "ls": self.LS, "us": self.US}
         changed = False
         for key, val in cur.items():
@@ -256,6 +283,49 @@ class ResidentBatch:
         self.last = cur
         return cur
 
+    def _update_host(self, batch_vars, now, cur):
+        """:meth:`update` of a small batch: the same scatters on the host mirrors, one upload."""
+        if self._h2d is not None:
+            self._h2d.synchronize()  # the last upload has read the mirrors
+        dst = {"p": self.hP, "ls": self.hLS, "us": self.hUS}
+        changed = False
+        for key, val in cur.items():
+            old = self.last.get(key)
+            same = (isinstance(val, np.ndarray) and isinstance(old, np.ndarray) and val.shape == old.shape
+                    and np.array_equal(val, old)) or (
+                isinstance(val, dict) and isinstance(old, dict) and val.keys() == old.keys()
+                and all(np.array_equal(val[g], old[g]) for g in val))
+            if same:
+                cur[key] = old
+                continue
+            changed = True
+            for arr_key, c, g in self.targets.get(key, []):
+                if isinstance(val, np.ndarray):
+                    dst[arr_key][:, c] = val[:, None]
+                else:
+                    dst[arr_key][:, c] = val[g][:, :c.size]
+        if changed:
+            self.hL[:] = self.hLS
+            self.hU[:] = self.hUS
+            for k, arr in (("lb", self.hL), ("ub", self.hU)):
+                if k in self.over_h:
+                    c, q = self.over_h[k]
+                    arr[:, c] = self.hP[:, q]
+        if "guess" in self.over_h:
+            c, q = self.over_h["guess"]
+            self.hW[:, c] = self.hP[:, q]
+        if self.cold_rows is not None and self.cold_rows.size:
+            rows = [batch_vars[i] for i in self.cold_rows]
+            _, _, _, w0 = self.marshal.inputs(rows, now, None)
+            self.hW[self.cold_rows] = w0
+            self.cold_rows = None
+        self.BUF.copy_(self.hbuf_t, non_blocking=True)
+        if self.dev.type == "cuda":
+            self._h2d = self.torch.cuda.Event()
+            self._h2d.record()
+        self.last = cur
+        return cur
+
     def restart_cold(self):
         """Every agent's next guess is the cold-start guess (no remembered optimum)."""
         self.cold_rows = np.arange(self.n)
@@ -269,6 +339,8 @@ class ResidentBatch:
         w.copy_(self.W, non_blocking=True)
         raw = self.ST.cpu().numpy()  # synchronises (w is complete too: same stream)
         w = w.numpy()
+        if self.small:
+            self.hW[:] = w  # the next call's warm start (uploaded with the inputs)
         with np.errstate(invalid="ignore"):
             bad = np.flatnonzero(np.isnan(w.sum(axis=1)))
         self.cold_rows = bad if bad.size else None

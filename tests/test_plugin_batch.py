@@ -38,7 +38,12 @@ def _check(rb, m, agents, now, w_prev):
     return p, ls, us
 
 
-def test_resident_inputs_equal_full_marshalling():
+@pytest.mark.parametrize("small", [True, False])
+def test_resident_inputs_equal_full_marshalling(small, monkeypatch):
+    """Both update paths: host mirrors + one upload (small batches) and device scatters."""
+    from agentlib_mpc_amd.optimization_backends import plugin_batch
+
+    monkeypatch.setattr(plugin_batch, "SMALL_BATCH", 64 if small else 0)
     be, cv = bm.one_room(solver_options=bm.REFERENCE)
     m = be.problem.marshal
     agents = _agents(cv, 16, 3)
@@ -50,6 +55,8 @@ def test_resident_inputs_equal_full_marshalling():
     w_prev = rb.W.numpy().copy()
     w_prev[:, 5:9] += 0.25          # stands in for the solution the kernel would write in place
     rb.W.copy_(torch.from_numpy(w_prev))
+    if rb.small:
+        rb.hW[:] = w_prev  # what solve() does with the solution it reads back
     for i, c in enumerate(agents):
         c["T"].value += 0.1 * (i + 1)
     grid = len(be.problem.nlp.par_groups["d"].grid)
@@ -127,12 +134,17 @@ def test_native_reader_equals_python_reader():
 
 
 @pytest.mark.gpu
-def test_gpu_resident_plugin_path_matches_host_marshalling():
+@pytest.mark.parametrize("small", [True, False])
+def test_gpu_resident_plugin_path_matches_host_marshalling(small, monkeypatch):
     """Three closed-loop steps through ``solve_batch`` (resident inputs, warm start in HBM)
     against the host path (full re-marshalling with the previous optimum as guess,
-    ``solve_arrays``): identical solutions, statuses and per-agent Results."""
+    ``solve_arrays``): identical solutions, statuses and per-agent Results -- with the
+    small-batch update (host mirrors, one upload) and with the device scatters."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    from agentlib_mpc_amd.optimization_backends import plugin_batch
+
+    monkeypatch.setattr(plugin_batch, "SMALL_BATCH", 64 if small else 0)
     be, cv = bm.one_room(solver_options=bm.REFERENCE)
     twin = bm.one_room(solver_options=bm.REFERENCE)[0]
     agents = _agents(cv, 24, 11)

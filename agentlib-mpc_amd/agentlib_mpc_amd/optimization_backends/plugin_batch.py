@@ -315,9 +315,7 @@ class ResidentBatch:
             c, q = self.over_h["guess"]
             self.hW[:, c] = self.hP[:, q]
         if self.cold_rows is not None and self.cold_rows.size:
-            rows = [batch_vars[i] for i in self.cold_rows]
-            _, _, _, w0 = self.marshal.inputs(rows, now, None)
-            self.hW[self.cold_rows] = w0
+            self.hW[self.cold_rows] = self._cold_guess(self.cold_rows)
             self.cold_rows = None
         self.BUF.copy_(self.hbuf_t, non_blocking=True)
         if self.dev.type == "cuda":
@@ -325,6 +323,29 @@ class ResidentBatch:
             self._h2d.record()
         self.last = cur
         return cur
+
+    def _cold_guess(self, rows) -> np.ndarray:
+        """The cold-start guess of some agents (``BatchMarshal.assemble`` with no previous
+        optimum, `core/discretization.py:212-245`) from the host mirrors: states tiled from
+        their measured initial value, other variables at the midpoint of their sampled bounds
+        (infinite -> 0), then the guesses taken from parameters."""
+        m = self.marshal
+        P, LS, US = self.hP[rows], self.hLS[rows], self.hUS[rows]
+        g = np.zeros((len(rows), self.hW.shape[1]))
+        for name, grid, _, index in m.vars:
+            if index is None:
+                continue
+            flat = index.ravel()
+            if name in m.initial:
+                meas = P[:, m.initial[name][:, -1]]                      # [r, dim]
+                g[:, flat] = np.repeat(meas[:, :, None], len(grid), axis=2).reshape(len(rows), -1)
+            else:
+                with np.errstate(invalid="ignore"):
+                    g[:, flat] = np.nan_to_num(0.5 * (LS[:, flat] + US[:, flat]), posinf=0, neginf=-0)
+        if "guess" in self.over_h:
+            c, q = self.over_h["guess"]
+            g[:, c] = P[:, q]
+        return np.nan_to_num(g)
 
     def restart_cold(self):
         """Every agent's next guess is the cold-start guess (no remembered optimum)."""

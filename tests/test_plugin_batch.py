@@ -166,3 +166,27 @@ def test_gpu_resident_plugin_path_matches_host_marshalling(small, monkeypatch):
         np.testing.assert_allclose(res.w, ref.w, rtol=1e-13, atol=1e-13)
         for i in (0, 7, 23):
             np.testing.assert_allclose(res[i].matrix, ref[i].matrix, rtol=1e-13, atol=1e-13, equal_nan=True)
+
+
+@pytest.mark.parametrize("small", [True, False])
+def test_cold_restart_guess_equals_full_marshalling(small, monkeypatch):
+    """``restart_cold`` (a backend's first solve, `core/discretization.py:212-245`): the next
+    update's guess equals the full marshalling's cold guess -- small batches build it from
+    the host mirrors, large ones re-marshal the rows."""
+    from agentlib_mpc_amd.optimization_backends import plugin_batch
+
+    monkeypatch.setattr(plugin_batch, "SMALL_BATCH", 64 if small else 0)
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    m = be.problem.marshal
+    agents = _agents(cv, 6, 4)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    rb.W.fill_(1.5)
+    if rb.small:
+        rb.hW[:] = 1.5
+    for i, c in enumerate(agents):
+        c["T"].value += 0.3 * i
+    agents[2]["mDot"] = copy.deepcopy(agents[2]["mDot"])
+    agents[2]["mDot"].ub = 0.03
+    rb.restart_cold()
+    rb.update(agents, 600.0)
+    _check(rb, m, agents, 600.0, None)

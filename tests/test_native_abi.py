@@ -54,6 +54,42 @@ def test_generated_kernel_compiles(tmp_path, monkeypatch):
     be, _ = bm.exchange_supply()
     path = be.problem.compile()
     assert path.exists() and path.stat().st_size > 0
+    # the small-fleet build (workspace hot part in LDS) of the same structure
+    sp = native.compile_model(be.problem.gen, variant=native.SMALL_FLEET)
+    assert sp is not None and sp.exists() and sp != path
+
+
+def test_small_fleet_build_keeps_hbm_addressing_off_the_lds_workspace():
+    """In the small-fleet build the only global-memory stores are the kernel's outputs and the
+    workspace's cold part: the phases that run every iteration (evaluators, elimination,
+    line search, iteration head) address the LDS workspace with LDS instructions (a pointer
+    cast from the LDS workspace to an HBM type was a wild address on the GPU)."""
+    import re
+    import subprocess
+
+    from agentlib_mpc_amd import benchmarks as bm
+
+    be, _ = bm.one_room()
+    src = native.KERNEL_DIR / "test_wslds_isa.hip"
+    src.parent.mkdir(parents=True, exist_ok=True)
+    src.write_text(be.problem.gen.source)
+    out = src.with_suffix(".s")
+    subprocess.run([native._hipcc(), "--cuda-device-only", "-S", f"--offload-arch={native.OFFLOAD_ARCH}", "-O3",
+                    "-std=c++17", f"-I{native.INCLUDE}", f"-I{native.CSRC}", "-DMPCX_WS_LDS", str(src), "-o", str(out)],
+                   check=True, capture_output=True)
+    fn, stores = None, {}
+    for line in out.read_text().splitlines():
+        m = re.match(r"^(_Z\S+|mpcx_ipm_solve):", line)
+        if m:
+            fn = m.group(1)
+        elif "global_store" in line or "flat_store" in line:
+            stores[fn] = stores.get(fn, 0) + 1
+    src.unlink()
+    out.unlink()
+    hot = ("line_search", "recover_step", "accept_step", "local_assemble", "chain_factor", "eval_fg")
+    bad = {f: c for f, c in stores.items() if f and any(h in f for h in hot) and "resto" not in f}
+    assert not bad, bad
+    assert stores.get("mpcx_ipm_solve", 0) <= 40, stores.get("mpcx_ipm_solve")
 
 
 def test_product_path_has_no_cpu_fallback(monkeypatch):

@@ -59,7 +59,7 @@ def test_generated_kernel_compiles(tmp_path, monkeypatch):
     assert sp is not None and sp.exists() and sp != path
 
 
-def test_small_fleet_build_keeps_hbm_addressing_off_the_lds_workspace():
+def test_small_fleet_build_keeps_hbm_addressing_off_the_lds_workspace(tmp_path):
     """In the small-fleet build the only global-memory stores are the kernel's outputs and the
     workspace's cold part: the phases that run every iteration (evaluators, elimination,
     line search, iteration head) address the LDS workspace with LDS instructions (a pointer
@@ -70,8 +70,7 @@ def test_small_fleet_build_keeps_hbm_addressing_off_the_lds_workspace():
     from agentlib_mpc_amd import benchmarks as bm
 
     be, _ = bm.one_room()
-    src = native.KERNEL_DIR / "test_wslds_isa.hip"
-    src.parent.mkdir(parents=True, exist_ok=True)
+    src = tmp_path / "wslds_isa.hip"
     src.write_text(be.problem.gen.source)
     out = src.with_suffix(".s")
     subprocess.run([native._hipcc(), "--cuda-device-only", "-S", f"--offload-arch={native.OFFLOAD_ARCH}", "-O3",
@@ -84,8 +83,6 @@ def test_small_fleet_build_keeps_hbm_addressing_off_the_lds_workspace():
             fn = m.group(1)
         elif "global_store" in line or "flat_store" in line:
             stores[fn] = stores.get(fn, 0) + 1
-    src.unlink()
-    out.unlink()
     hot = ("line_search", "recover_step", "accept_step", "local_assemble", "chain_factor", "eval_fg")
     bad = {f: c for f, c in stores.items() if f and any(h in f for h in hot) and "resto" not in f}
     assert not bad, bad

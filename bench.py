@@ -693,7 +693,9 @@ def c1_latency(args, dev):
         ks.append(e0.elapsed_time(e1))
     out = {"workload": "C1: examples/one_room_mpc/physical/simple_mpc.py, one agent, cold start",
            "ms_end_to_end": float(np.median(e2e) * 1e3), "ms_kernel": float(np.median(ks)),
-           "iter_count": int(r.stats["iter_count"]), "return_status": r.stats["return_status"]}
+           "iter_count": int(r.stats["iter_count"]), "return_status": r.stats["return_status"],
+           "build": ("small-fleet (workspace hot part in LDS, DESIGN 2.4)" if native.small_fleet_path is not None
+                     else "HBM workspace")}
     try:
         from oracle import cbuild
 

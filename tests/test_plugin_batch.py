@@ -190,3 +190,31 @@ def test_cold_restart_guess_equals_full_marshalling(small, monkeypatch):
     rb.restart_cold()
     rb.update(agents, 600.0)
     _check(rb, m, agents, 600.0, None)
+
+
+def test_native_reader_takes_any_mapping():
+    """Agents' variable sets given as mappings that are not dicts (the native reader's
+    ``PyObject_GetItem`` path) read the same as dicts."""
+    from collections.abc import Mapping
+
+    class Vars(Mapping):
+        def __init__(self, d):
+            self.d = d
+
+        def __getitem__(self, k):
+            return self.d[k]
+
+        def __iter__(self):
+            return iter(self.d)
+
+        def __len__(self):
+            return len(self.d)
+
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    agents = _agents(cv, 5, 9)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    want = rb.read(agents, 0.0)
+    got = rb.read([Vars(a) for a in agents], 0.0)
+    assert got.keys() == want.keys()
+    for k in want:
+        np.testing.assert_array_equal(got[k], want[k])

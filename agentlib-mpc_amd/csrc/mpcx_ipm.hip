@@ -81,6 +81,8 @@ typedef ldsi wint;
 typedef gdbl wdbl;
 typedef gint wint;
 #endif
+typedef gdbl cdbl;  // the workspace's cold part (HBM in both builds)
+typedef gint cint;
 
 // stage-local system [V_k, lambda_rest | x_k | mu_k, x_{k+1} | rhs].  mu_k: the NMU
 // continuity rows of the stage (the rows through x_{k+1}) when they are kept in the border
@@ -132,23 +134,27 @@ constexpr long O_X = 0, O_S = O_X + NW, O_LAM = O_S + M, O_ZL = O_LAM + M, O_ZU 
 constexpr long O_VL = O_ZU + NW, O_VU = O_VL + M, O_XL = O_VU + M, O_XU = O_XL + NW;
 constexpr long O_SL = O_XU + NW, O_SU = O_SL + M, O_GS = O_SU + M, O_GV = O_GS + M;
 constexpr long O_DX = O_GV + M, O_DS = O_DX + NW, O_DL = O_DS + M, O_LB = O_DL + M, O_UB = O_LB + M;
+// hot part first (every iteration reads / writes it), then the cold part (scaling at init,
+// the block-chain and dense fallbacks, the restoration phase): the small-fleet build keeps
+// only the hot part in LDS
 constexpr long O_SDG = O_UB + M;                 // [NL][N]      stage cost gradient
 constexpr long O_JTL = O_SDG + (long)NL * N;     // [NL][N]      stage (gs*J)^T lambda
-constexpr long O_SDJ = O_JTL + (long)NL * N;     // [NG*NL][N]   stage jacobian (scaling, block chain)
-constexpr long O_SDH = O_SDJ + (long)NG * NL * N;// [NL*NL][N]   stage hessian
-constexpr long O_RHS = O_SDH + (long)NL * NL * N;// [N][NB]      KKT right-hand side
+constexpr long O_RHS = O_JTL + (long)NL * N;     // [N][NB]      KKT right-hand side
 constexpr long O_TR = O_RHS + (long)N * NB;      // [N][NTR][NI] back-substitution operators
-constexpr long O_PRM = O_TR + (long)N * NI * NTR;// [N][NI] ints interior pivot order (dense stages)
+constexpr long O_LP = O_TR + (long)N * NI * NTR;   // [NCPT][N] compact local systems (evaluators; stage-minor)
+constexpr long O_DG = O_LP + (long)NCPT * N;       // [N][NLOC] diagonal terms (rhs phases; Newton mode)
+constexpr long WS_HOT = O_DG + (long)N * NLOC;     // end of the hot part
+constexpr long O_SDJ = WS_HOT;                   // [NG*NL][N]   stage jacobian (scaling, block chain)
+constexpr long O_SDH = O_SDJ + (long)NG * NL * N;// [NL*NL][N]   stage hessian (block chain)
+constexpr long O_PRM = O_SDH + (long)NL * NL * N;// [N][NI] ints interior pivot order (dense stages)
 constexpr long O_KX = O_PRM + (long)N * NI;      // [N*NP] primal KKT diagonal   (block chain)
 constexpr long O_KD = O_KX + (long)N * NP;       // [M] dual KKT diagonal        (block chain)
 constexpr long O_SOL = O_KD + M;                 // [N][NB] solution             (block chain)
 constexpr long O_FAC = O_SOL + (long)N * NB;     // [N][NB*LDB] block inverses   (block chain)
 constexpr long O_CPL = O_FAC + (long)N * NB * LDB;  // [N][NB*NX] couplings      (block chain)
-constexpr long O_LP = O_CPL + (long)N * NB * NXP;  // [NCPT][N] compact local systems (evaluators; stage-minor)
-constexpr long O_DG = O_LP + (long)NCPT * N;       // [N][NLOC] diagonal terms (rhs phases; Newton mode)
 constexpr int SQ = NX > 0 ? NB : 1;   // the block-chain fallback exists only when stages are coupled
 constexpr int SQL = NX > 0 ? LDB : 1;
-constexpr long O_SQW = O_DG + (long)N * NLOC;  // [2][SQ*SQL] block-chain inverse scratch W, Y
+constexpr long O_SQW = O_CPL + (long)N * NB * NXP;  // [2][SQ*SQL] block-chain inverse scratch W, Y
 // feasibility restoration phase and soft restoration step (touched only on those paths)
 constexpr long O_RP = O_SQW + (NX > 0 ? 2L * SQ * SQL : 0L);  // [M] restoration p (c~ - p + n)
 constexpr long O_RN = O_RP + M;          // [M] restoration n
@@ -436,7 +442,7 @@ constexpr int REST_BYTES = (int)sizeof(LdsRest);
 constexpr int UFIX_BYTES = cmax((int)sizeof(SeqLds), cmax(8 * N * NB, (int)sizeof(TrialLds)));
 constexpr int LDS_CU_ALL = 163840, LDS_SLACK = 256;
 #ifdef MPCX_WS_LDS
-constexpr int WS_LDS_BYTES = (int)(8 * WS_DOUBLES);
+constexpr int WS_LDS_BYTES = (int)(8 * WS_HOT);
 #else
 constexpr int WS_LDS_BYTES = 0;
 #endif
@@ -505,11 +511,13 @@ static_assert(sizeof(Lds) + LDS_SLACK <= LDS_CU / APC, "LDS share per agent exce
 __shared__ Lds gL;  // one agent per workgroup: the agent's LDS scratch
 __device__ __forceinline__ KArgs* kargs() { return (KArgs*)uni64(gL.kp_bits); }
 #ifdef MPCX_WS_LDS
-__shared__ double gWS[WS_DOUBLES];
+__shared__ double gWS[WS_HOT];
 __device__ __forceinline__ wdbl* ws_base() { return (wdbl*)gWS; }
 #else
 __device__ __forceinline__ wdbl* ws_base() { return (wdbl*)uni64(gL.ws_bits); }
 #endif
+// the cold part: offsets >= WS_HOT of the agent's HBM slab (both builds)
+__device__ __forceinline__ cdbl* cold_base() { return (cdbl*)uni64(gL.ws_bits); }
 #define LDSP(x) ((ldsd*)(x))
 #define LDSI(x) ((ldsi*)(x))
 #ifdef MPCX_PROFILE
@@ -554,6 +562,7 @@ __device__ __forceinline__ wdbl* ws_base() { return (wdbl*)uni64(gL.ws_bits); }
 struct Agent {
   // the agent's workspace slab, wave-uniform (SGPRs): nothing of the view is passed in VGPRs
   __device__ __forceinline__ wdbl* base() const { return ws_base(); }
+  __device__ __forceinline__ cdbl* cold() const { return cold_base(); }
 #define ws base()
   __device__ wdbl* x() const { return ws + O_X; }
   __device__ wdbl* s() const { return ws + O_S; }
@@ -575,34 +584,34 @@ struct Agent {
   __device__ wdbl* ub() const { return ws + O_UB; }
   __device__ wdbl* sdg() const { return ws + O_SDG; }
   __device__ wdbl* jtl() const { return ws + O_JTL; }
-  __device__ wdbl* sdj() const { return ws + O_SDJ; }
-  __device__ wdbl* sdh() const { return ws + O_SDH; }
+  __device__ cdbl* sdj() const { return cold_base() + O_SDJ; }
+  __device__ cdbl* sdh() const { return cold_base() + O_SDH; }
   __device__ wdbl* rhs(int k) const { return ws + O_RHS + (long)k * NB; }
   __device__ wdbl* tr(int k) const { return ws + O_TR + k; }  // [NTR][NI][N]: W_k[t][p] at tr(k)[(t NI + p) N]
-  __device__ wint* prm(int k) const { return reinterpret_cast<wint*>(ws + O_PRM) + (long)k * NI; }
-  __device__ wdbl* kx() const { return ws + O_KX; }
-  __device__ wdbl* kd() const { return ws + O_KD; }
-  __device__ wdbl* sol(int k) const { return ws + O_SOL + (long)k * NB; }
-  __device__ wdbl* fac(int k) const { return ws + O_FAC + (long)k * NB * LDB; }
-  __device__ wdbl* cpl(int k) const { return ws + O_CPL + (long)k * NB * NXP; }
+  __device__ cint* prm(int k) const { return reinterpret_cast<cint*>(cold_base() + O_PRM) + (long)k * NI; }
+  __device__ cdbl* kx() const { return cold_base() + O_KX; }
+  __device__ cdbl* kd() const { return cold_base() + O_KD; }
+  __device__ cdbl* sol(int k) const { return cold_base() + O_SOL + (long)k * NB; }
+  __device__ cdbl* fac(int k) const { return cold_base() + O_FAC + (long)k * NB * LDB; }
+  __device__ cdbl* cpl(int k) const { return cold_base() + O_CPL + (long)k * NB * NXP; }
   __device__ wdbl* lp(int k) const { return ws + O_LP + k; }  // entry c of stage k at lp(k)[c * N]
   __device__ wdbl* dg(int k) const { return ws + O_DG + (long)k * NLOC; }
-  __device__ wdbl* sqw() const { return ws + O_SQW; }
-  __device__ wdbl* rp() const { return ws + O_RP; }
-  __device__ wdbl* rn() const { return ws + O_RN; }
-  __device__ wdbl* rzp() const { return ws + O_RZP; }
-  __device__ wdbl* rzn() const { return ws + O_RZN; }
-  __device__ wdbl* rdp() const { return ws + O_RDP; }
-  __device__ wdbl* rdn() const { return ws + O_RDN; }
-  __device__ wdbl* xr() const { return ws + O_XR; }
-  __device__ wdbl* sr() const { return ws + O_SR; }
-  __device__ wdbl* lr() const { return ws + O_LR; }
-  __device__ wdbl* gvr() const { return ws + O_GVR; }
-  __device__ wdbl* zl0() const { return ws + O_ZL0; }
-  __device__ wdbl* zu0() const { return ws + O_ZU0; }
-  __device__ wdbl* vl0() const { return ws + O_VL0; }
-  __device__ wdbl* vu0() const { return ws + O_VU0; }
-  __device__ wdbl* flt0() const { return ws + O_FLT0; }
+  __device__ cdbl* sqw() const { return cold_base() + O_SQW; }
+  __device__ cdbl* rp() const { return cold_base() + O_RP; }
+  __device__ cdbl* rn() const { return cold_base() + O_RN; }
+  __device__ cdbl* rzp() const { return cold_base() + O_RZP; }
+  __device__ cdbl* rzn() const { return cold_base() + O_RZN; }
+  __device__ cdbl* rdp() const { return cold_base() + O_RDP; }
+  __device__ cdbl* rdn() const { return cold_base() + O_RDN; }
+  __device__ cdbl* xr() const { return cold_base() + O_XR; }
+  __device__ cdbl* sr() const { return cold_base() + O_SR; }
+  __device__ cdbl* lr() const { return cold_base() + O_LR; }
+  __device__ cdbl* gvr() const { return cold_base() + O_GVR; }
+  __device__ cdbl* zl0() const { return cold_base() + O_ZL0; }
+  __device__ cdbl* zu0() const { return cold_base() + O_ZU0; }
+  __device__ cdbl* vl0() const { return cold_base() + O_VL0; }
+  __device__ cdbl* vu0() const { return cold_base() + O_VU0; }
+  __device__ cdbl* flt0() const { return cold_base() + O_FLT0; }
 #undef ws
 };
 
@@ -1148,7 +1157,7 @@ __device__ __noinline__ void seq_solve(const Agent a) {
         L.v[i] = v;
       }
       wsync();
-      const wdbl* Ai = a.fac(k);
+      const cdbl* Ai = a.fac(k);
       for (int i = lane; i < NB; i += WAVE) {
         double acc = 0.0;
         for (int j = 0; j < NB; ++j) acc += Ai[i * LDB + j] * L.v[j];
@@ -1167,7 +1176,7 @@ __device__ __noinline__ void seq_solve(const Agent a) {
         L.t[c] = s;
       }
       wsync();
-      const wdbl* Ai = a.fac(k);
+      const cdbl* Ai = a.fac(k);
       for (int i = lane; i < NB; i += WAVE) {
         double u = a.sol(k)[i];
         for (int c = 0; c < NX; ++c) u -= Ai[i * LDB + NV + c] * L.t[c];
@@ -1269,7 +1278,7 @@ __device__ __forceinline__ double generic_entry(const Agent a, int k, int i, int
   } else if (bd) {
     off = O_RHS + (long)k * NB + lblk(j, kj);
   }
-  const double d = ws[off];
+  const double d = (pp || dp) ? a.cold()[off] : ws[off];  // SDH / SDJ: cold part
   const double gsv = ws[goff];
   double v = 0.0;
   if (pp) v = (fi || fj) ? ((i == j && ki == 0) ? 1.0 : 0.0) : (kd.mode == LSQ ? 0.0 : d);
@@ -1966,7 +1975,8 @@ __device__ __noinline__ Scal init_agent(const Agent a, int agent) {
   const gdbl* wio = (const gdbl*)args.w + (long)agent * NW;
   const gdbl* pin = (const gdbl*)args.p + (long)agent * NPAR;
   for (int t = lane; t < NPAR; t += WAVE) gL.par[t] = pin[t];
-  for (long t = lane; t < (long)(2 * NL + NG * NL + NL * NL) * N; t += WAVE) a.base()[O_SDG + t] = 0.0;
+  for (long t = lane; t < (long)(2 * NL) * N; t += WAVE) a.base()[O_SDG + t] = 0.0;           // SDG, JTL
+  for (long t = lane; t < (long)(NG * NL + NL * NL) * N; t += WAVE) a.cold()[O_SDJ + t] = 0.0;  // SDJ, SDH
   for (long t = lane; t < (long)NCPT * N; t += WAVE) a.base()[O_LP + t] = 0.0;  // structural zeros stay zero
   for (int i = lane; i < NW; i += WAVE) {
     double lo = lbw[i], hi = ubw[i];
@@ -3394,9 +3404,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   const int lane = lane_now();
   if (lane == 0) {
     gL.kp_bits = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
-#ifndef MPCX_WS_LDS
     gL.ws_bits = (unsigned long long)((gdbl*)args.ws + (long)agent * args.ws_stride);
-#endif
   }
   wsync();
   KState& K = gL.ks;

@@ -43,7 +43,7 @@ from typing import Dict, List, Optional, Sequence, Union
 import numpy as np
 
 from agentlib_mpc_amd.data_structures import admm_datatypes as adt
-from agentlib_mpc_amd.runtime.native import ADMM_TOTALS, STATS_BYTES
+from agentlib_mpc_amd.runtime.native import ADMM_TOTALS, STATS_BYTES, admm_reduce_count
 
 CONSENSUS = "consensus"
 EXCHANGE = "exchange"
@@ -399,7 +399,8 @@ class ADMMFleet:
         self.MOM = t.zeros(self.ops.moments_size(max(G, 1), nb, T), dtype=f64, device=dev)
         self.totals_off = self.n_global * self.S
         # all-reduce range: global groups' moments + the totals of the blocks spanning ranks
-        self.reduce_len = self.n_global * self.S + ADMM_TOTALS * self.n_global_blocks
+        # (numbered first), as the C ABI defines it (include/mpcx.h mpcx_admm_reduce_count)
+        self.reduce_len = admm_reduce_count(self.n_global, self.n_global_blocks, T) if self.world > 1 else 0
         # per-block coordinator state on the device: penalty, group freeze mask
         self.BLOCK_G = t.as_tensor(self.block_of_group if G else np.zeros(1, np.int32), dtype=i32, device=dev)
         self.RHO_B = t.zeros((nb, 1), dtype=f64, device=dev)

@@ -82,7 +82,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
     "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_problem_small_fleet",
     "mpcx_batch_solve",
-    "mpcx_admm_moments_size", "mpcx_admm_moments", "mpcx_admm_finalize",
+    "mpcx_admm_moments_size", "mpcx_admm_reduce_count", "mpcx_admm_moments", "mpcx_admm_finalize",
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
@@ -186,6 +186,8 @@ def load_library():
         i64 = ctypes.c_int64
         lib.mpcx_admm_moments_size.argtypes = [i32, i32, i32]
         lib.mpcx_admm_moments_size.restype = i64
+        lib.mpcx_admm_reduce_count.argtypes = [i32, i32, i32]
+        lib.mpcx_admm_reduce_count.restype = i64
         lib.mpcx_admm_moments.argtypes = [i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp]
         lib.mpcx_admm_finalize.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, f64, vp, vp, vp, vp, vp, vp,
                                            vp]
@@ -204,6 +206,15 @@ def load_library():
             getattr(lib, name)  # raises AttributeError if a symbol is missing
         _lib = lib
         return lib
+
+
+def admm_reduce_count(n_global: int, n_global_blocks: int, T: int) -> int:
+    """Doubles of the ADMM moments buffer that are all-reduced over the ranks
+    (``mpcx_admm_reduce_count``, host arithmetic of the C ABI: no GPU call)."""
+    n = int(load_library().mpcx_admm_reduce_count(int(n_global), int(n_global_blocks), int(T)))
+    if n < 0:
+        raise NativeError(f"mpcx_admm_reduce_count({n_global}, {n_global_blocks}, {T}) failed ({n})")
+    return n
 
 
 def default_options() -> Options:

@@ -300,6 +300,14 @@ extern "C" int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t n_blocks, in
   return (int64_t)n_groups * (NMOM * (int64_t)T + 1) + (int64_t)MPCX_ADMM_TOTALS * n_blocks;
 }
 
+// Length of the all-reduced prefix of the moments buffer: the global groups' moments, then
+// the totals of the blocks that span ranks (numbered first, identically on every rank; the
+// rank-local blocks' totals follow them and stay local).
+extern "C" int64_t mpcx_admm_reduce_count(int32_t n_global, int32_t n_global_blocks, int32_t T) {
+  if (n_global < 0 || n_global_blocks < 0 || T <= 0) return MPCX_ERR_ARG;
+  return (int64_t)n_global * (NMOM * (int64_t)T + 1) + (int64_t)MPCX_ADMM_TOTALS * n_global_blocks;
+}
+
 extern "C" int mpcx_admm_moments_masked(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
                                         const int32_t* gstart, int32_t max_group_rows,
                                         const double* locals, const double* multipliers,

@@ -184,14 +184,27 @@ int mpcx_batch_solve(mpcx_handle* h, int32_t n_agents, const double* p, const do
  * (NULL: the scalar rho for all) and groups with active_g[g] == 0 (NULL: all active) are
  * frozen — the blocks that already met their stopping rule.  One ADMM iteration of the
  * reference coordinator (admm_coordinator.py:288-304) is
- *   moments -> [all-reduce of the first mpcx_admm_reduce_count doubles] -> finalize
+ *   moments -> [all-reduce (sum) of the first mpcx_admm_reduce_count(...) doubles] -> finalize
  *   -> consensus_multipliers / exchange_update -> scatter into the NLP parameters.
+ *
+ * Block numbering with several ranks: the blocks that contain a global group (participants on
+ * more than one rank) are numbered FIRST, 0 .. n_global_blocks-1, identically on every rank;
+ * each rank numbers its rank-local blocks after them (n_global_blocks .. n_blocks-1, so the
+ * same number means different blocks on different ranks).  Only the first n_global_blocks
+ * blocks' totals are summed over the ranks; summing a rank-local block's totals would add
+ * unrelated blocks' residuals.
  */
 #define MPCX_ADMM_TOTALS 8
 /* doubles in a moments buffer (zero it before mpcx_admm_moments):
- *   [n_global x (5T+1) global-group moments][n_blocks x MPCX_ADMM_TOTALS totals][local groups];
- * the all-reduce range is the first n_global*(5T+1) + n_blocks*MPCX_ADMM_TOTALS doubles. */
+ *   [n_global x (5T+1) global-group moments][n_blocks x MPCX_ADMM_TOTALS totals][local groups]
+ *   <- the per-alias sums of ADMMCoordinator._check_convergence (admm_coordinator.py:354-435) */
 int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t n_blocks, int32_t T);
+/* Length of the all-reduced prefix of that buffer:
+ *   n_global*(5T+1) + n_global_blocks*MPCX_ADMM_TOTALS doubles
+ * (global-group moments, then the totals of the rank-spanning blocks, which are numbered
+ * first).  Single rank: nothing to reduce.  <- the one exchange per ADMM iteration of
+ * admm_coordinator.py:288-304 when the agents sit on several GPUs. */
+int64_t mpcx_admm_reduce_count(int32_t n_global, int32_t n_global_blocks, int32_t T);
 
 /* Per (group, t) moments of the locals about center = the current mean [n_groups][T]:
  * sum(x-c), sum(x-c)^2 and, if multipliers != NULL (consensus rows), sum lam, sum lam^2,

@@ -17,6 +17,7 @@ import torch.multiprocessing as mp
 
 from agentlib_mpc_amd import benchmarks as bm
 from agentlib_mpc_amd.admm.fleet import ADMMFleet
+from agentlib_mpc_amd.runtime import native
 from oracle import admm as oadmm
 from oracle import nlps
 from tests.admm_cases import C2Oracle, C4Oracle, participation_rounds
@@ -416,7 +417,7 @@ def test_consensus_multipliers_of_an_alias_sum_to_zero():
         np.testing.assert_allclose(rows.sum(0), 0.0, atol=1e-12 * np.abs(lam).max())
 
 
-def _mixed_worker(rank, world, init_file, out_file):
+def _mixed_worker(rank, world, init_file, out_file, tols=(1e-12, 1e-12), iter_max=2):
     """One coordinated fleet holding a C4 exchange alias that spans the ranks (one global
     block) and C2 consensus blocks that are rank-local: world 1 holds everything, rank r of
     world 2 its share of the C4 agents and C2 block r."""
@@ -433,10 +434,14 @@ def _mixed_worker(rank, world, init_file, out_file):
         fl = ADMMFleet(c2 + c4, device="cpu", ops=ops, comm="default" if world > 1 else None)
         assert fl.n_global_blocks == (1 if world > 1 else 0)
         if world > 1:   # the exchange group's moments + ONE block's totals, whatever the C2 count
+            # the length the C ABI defines (ctypes call of mpcx_admm_reduce_count, no GPU) is
+            # the layout the fleet fills: global moments first, then the spanning block's totals
+            assert fl.reduce_len == native.admm_reduce_count(fl.n_global, 1, fl.T)
             assert fl.reduce_len == fl.n_global * fl.S + 8
-        out = fl.run_coordinated(1.0, admm_iter_max=2, use_relative_tolerances=False, primal_tol=1e-12,
-                                 dual_tol=1e-12)
+        out = fl.run_coordinated(1.0, admm_iter_max=iter_max, use_relative_tolerances=False, primal_tol=tols[0],
+                                 dual_tol=tols[1])
         xb = fl.block_index("mDot_coupling")
+        np.savez(f"{out_file}.{rank}.iters.npz", iters=out["block_iterations"][[xb] + c2b_of(fl, world, rank)])
         c2b = [fl.block_index(f"mDot1_coupling_b{b}") for b in ((0, 1) if world == 1 else (rank,))]
         rec = {"x": np.array([[r.primal_residual, r.dual_residual] for r in out["block_records"][xb]])}
         for b, blk in zip((0, 1) if world == 1 else (rank,), c2b):
@@ -448,16 +453,34 @@ def _mixed_worker(rank, world, init_file, out_file):
             dist.destroy_process_group()
 
 
-def test_mixed_global_and_local_blocks_world2_matches_world1(tmp_path):
+def c2b_of(fl, world, rank):
+    return [fl.block_index(f"mDot1_coupling_b{b}") for b in ((0, 1) if world == 1 else (rank,))]
+
+
+@pytest.mark.parametrize("tols,iter_max,want_iters", [
+    ((1e-12, 1e-12), 2, None),
+    # the spanning exchange block meets its rule at iteration 2 (primal 0.041 < 0.05, dual 2e-5 <
+    # 1e-3) while the C2 blocks keep going to the cap: from then on the ranks skip the
+    # all-reduce (no active spanning block) and iterate their local blocks on their own
+    ((0.05, 1e-3), 5, (2, 5)),
+])
+def test_mixed_global_and_local_blocks_world2_matches_world1(tmp_path, tols, iter_max, want_iters):
     """Blocks spanning ranks and rank-local blocks in one coordinated fleet: the
     spanning block's totals travel in the one all-reduce, the local blocks' do not, and two
-    ranks reproduce the one-rank histories block by block."""
+    ranks reproduce the one-rank histories block by block -- also once the spanning block has
+    stopped and the ranks no longer reduce."""
     init, out = str(tmp_path / "init"), str(tmp_path / "out")
-    _mixed_worker(0, 1, init, out + "1")
+    _mixed_worker(0, 1, init, out + "1", tols, iter_max)
     one = dict(np.load(f"{out}1.0.npz"))
-    mp.spawn(_mixed_worker, args=(2, init, out + "2"), nprocs=2, join=True)
+    if want_iters is not None:
+        it1 = np.load(f"{out}1.0.iters.npz")["iters"]
+        assert it1[0] == want_iters[0] and (it1[1:] == want_iters[1]).all(), it1
+    mp.spawn(_mixed_worker, args=(2, init, out + "2", tols, iter_max), nprocs=2, join=True)
     for r in range(2):
         two = dict(np.load(f"{out}2.{r}.npz"))
         assert f"b{r}" in two
         for k, v in two.items():
             np.testing.assert_allclose(v, one[k], rtol=1e-9, atol=1e-12, err_msg=k)
+        if want_iters is not None:
+            it2 = np.load(f"{out}2.{r}.iters.npz")["iters"]
+            assert it2[0] == want_iters[0] and (it2[1:] == want_iters[1]).all(), it2

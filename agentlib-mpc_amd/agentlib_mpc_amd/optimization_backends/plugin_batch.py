@@ -74,6 +74,13 @@ class RowSource:
         return p, ls, us
 
 
+def _has_nan(val) -> bool:
+    """NaN in a read column (an (n,) array, or {grid: samples})."""
+    if isinstance(val, np.ndarray):
+        return bool(np.isnan(val).any()) if val.dtype.kind == "f" else False
+    return any(np.isnan(np.asarray(a, dtype=np.float64)).any() for a in val.values())
+
+
 class ResidentBatch:
     """Resident NLP inputs of one batch size of one backend (reference layout == kernel
     layout)."""
@@ -243,7 +250,7 @@ class ResidentBatch:
         if self.small:
             return self._update_host(batch_vars, now, cur)
         dst = {"p": self.P, "ls": self.LS, "us": self.US}
-        changed = False
+        changed = nan_in = False
         for key, val in cur.items():
             old = self.last.get(key)
             same = (isinstance(val, np.ndarray) and isinstance(old, np.ndarray) and val.shape == old.shape
@@ -254,6 +261,7 @@ class ResidentBatch:
                 cur[key] = old  # keep the array already referenced by earlier snapshots
                 continue
             changed = True
+            nan_in |= _has_nan(val)
             if isinstance(val, np.ndarray):
                 dv = torch.from_numpy(val).to(self.dev, non_blocking=True)
             else:
@@ -272,6 +280,8 @@ class ResidentBatch:
                 if k in self.over:
                     c, q = self.over[k]
                     arr[:, c] = self.P[:, q]
+        if nan_in and bool(torch.isnan(self.P).any() | torch.isnan(self.L).any() | torch.isnan(self.U).any()):
+            self._reject_nan()
         if "guess" in self.over:
             c, q = self.over["guess"]
             self.W[:, c] = self.P[:, q]
@@ -288,7 +298,7 @@ class ResidentBatch:
         if self._h2d is not None:
             self._h2d.synchronize()  # the last upload has read the mirrors
         dst = {"p": self.hP, "ls": self.hLS, "us": self.hUS}
-        changed = False
+        changed = nan_in = False
         for key, val in cur.items():
             old = self.last.get(key)
             same = (isinstance(val, np.ndarray) and isinstance(old, np.ndarray) and val.shape == old.shape
@@ -299,6 +309,7 @@ class ResidentBatch:
                 cur[key] = old
                 continue
             changed = True
+            nan_in |= _has_nan(val)
             for arr_key, c, g in self.targets.get(key, []):
                 if isinstance(val, np.ndarray):
                     dst[arr_key][:, c] = val[:, None]
@@ -311,6 +322,8 @@ class ResidentBatch:
                 if k in self.over_h:
                     c, q = self.over_h[k]
                     arr[:, c] = self.hP[:, q]
+        if nan_in and (np.isnan(self.hP).any() or np.isnan(self.hL).any() or np.isnan(self.hU).any()):
+            self._reject_nan()
         if "guess" in self.over_h:
             c, q = self.over_h["guess"]
             self.hW[:, c] = self.hP[:, q]
@@ -323,6 +336,14 @@ class ResidentBatch:
             self._h2d.record()
         self.last = cur
         return cur
+
+    def _reject_nan(self):
+        """A NaN reached the parameters or the bounds: the host path's error
+        (``BatchMarshal.assemble``: 'incomplete NLP inputs'), and nothing is launched.  The
+        snapshot is dropped so that the next call re-applies every column (the NaN values
+        are already scattered into the resident arrays)."""
+        self.last = {}
+        raise ValueError("incomplete NLP inputs (NaN in parameters or bounds)")
 
     def _cold_guess(self, rows) -> np.ndarray:
         """The cold-start guess of some agents (``BatchMarshal.assemble`` with no previous

@@ -15,6 +15,7 @@ import pathlib
 import shutil
 import subprocess
 import threading
+import warnings
 from typing import List, Dict, Optional
 
 PKG_DIR = pathlib.Path(__file__).resolve().parents[1]          # agentlib_mpc_amd/
@@ -270,8 +271,14 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
            f"-I{INCLUDE}", f"-I{CSRC}", *[f"-D{d}" for d in defs], str(src), "-o", str(tmp)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        if variant is not None and "workspace does not fit LDS" in res.stderr:
-            nofit.write_text("")
+        if variant is not None:
+            # an optional build (the small-fleet variant): any failure -- its workspace does
+            # not fit LDS, or the per-agent LDS share is exceeded -- means "no such build";
+            # the main code object serves every batch size.  The marker keeps the reason.
+            if "workspace does not fit LDS" not in res.stderr:
+                warnings.warn(f"small-fleet build of {gen.key} failed; the HBM build serves every batch:\n"
+                              f"{res.stderr[-800:]}")
+            nofit.write_text(res.stderr[-4000:])
             return None
         raise NativeError(f"compiling {src} failed:\n{res.stderr[-4000:]}")
     if verbose and res.stderr:
@@ -304,9 +311,10 @@ class NativeProblem:
             sp = compile_model(gen, variant=SMALL_FLEET)
             if sp is not None:
                 rc = self.lib.mpcx_problem_small_fleet(handle, str(sp).encode(), -1)
-                if rc != 0:
-                    raise NativeError(f"mpcx_problem_small_fleet failed ({rc}) for {sp}")
-                self.small_fleet_path = sp
+                if rc != 0:  # optional: the HBM build (loaded above) serves every batch size
+                    warnings.warn(f"mpcx_problem_small_fleet failed ({rc}) for {sp}; using the HBM build")
+                else:
+                    self.small_fleet_path = sp
         self.options = default_options()
         self.nw = d["NX"] + d["N"] * (d["NV"] + d["NX"])
         self.ng_total = d["N"] * d["NG"]

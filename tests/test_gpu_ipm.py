@@ -23,15 +23,38 @@ RTOL_TRAJ = 1e-5
 UNDETERMINED = {"mhe_room": {"algebraics"}, "mhe_room_u": {"algebraics"}}
 
 
-def _oracle(case):
+_ORACLE_CACHE = {}
+
+
+def _oracle(case, opts=None, key=None):
+    """Oracle IPM solve of a case (tight options by default), cached per (case, options) so
+    that both kernel builds compare against one oracle run."""
+    opts = opts or ipm.IPMOptions(tol=1e-10, max_iter=500, acceptable_iter=0)
+    ck = None if key is None else (key, repr(opts))
+    if ck is not None and ck in _ORACLE_CACHE:
+        return _ORACLE_CACHE[ck]
     p, lbw, ubw, w0 = case.oracle_inputs
-    return ipm.solve(case.oracle.functions(p), w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p),
-                     ipm.IPMOptions(tol=1e-10, max_iter=500, acceptable_iter=0))
+    ref = ipm.solve(case.oracle.functions(p), w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), opts)
+    if ck is not None:
+        _ORACLE_CACHE[ck] = ref
+    return ref
 
 
-def _gpu_solve(case, n_copies=1):
-    res = case.backend.solve_batch(0.0, [case.current_vars] * n_copies)
-    return res
+#: the two builds of every structure: the small-fleet build (workspace in LDS, what a batch
+#: of at most one agent per CU runs) and the HBM-workspace build (every larger fleet and
+#: every bench leg).  The parity cases below run both (ADVICE r03).
+BUILDS = ["lds", "hbm"]
+
+
+def _gpu_solve(case, n_copies=1, build="lds"):
+    native = case.backend._native()
+    if build == "lds" and native.small_fleet_path is None:
+        pytest.skip("no small-fleet build for this structure")
+    native.set_small_fleet_max(-1 if build == "lds" else 0)
+    try:
+        return case.backend.solve_batch(0.0, [case.current_vars] * n_copies)
+    finally:
+        native.set_small_fleet_max(-1)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -81,11 +104,12 @@ def _cuda():
     ("fixture_mpc", {}),
     ("fixture_mpc", {"T0": 285.0, "disturbance": 300.0}),
 ])
-def test_gpu_matches_oracle(name, kw):
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_matches_oracle(name, kw, build):
     case = configs.CASES[name](**kw)
-    ref = _oracle(case)
+    ref = _oracle(case, key=(name, repr(kw)))
     assert ref.success, ref.status
-    res = _gpu_solve(case, n_copies=3)
+    res = _gpu_solve(case, n_copies=3, build=build)
     nlp = case.backend.problem.nlp
     for r in res:
         assert r.stats["success"], r.stats
@@ -124,18 +148,17 @@ REFERENCE_OPTS = dict(tol=1e-4, max_iter=100, acceptable_tol=0.1, acceptable_ite
     ("tz_cca", {}),                                    # C5 CCA, N=24
     ("fixture_mpc", {}),                               # reference test-suite model
 ])
-def test_gpu_matches_oracle_at_reference_defaults(name, kw):
+@pytest.mark.parametrize("build", BUILDS)
+def test_gpu_matches_oracle_at_reference_defaults(name, kw, build):
     """Drop-in configs left at the reference's default solver options: the kernel and the
     oracle stop by the same rule (Solve_Succeeded or Solved_To_Acceptable_Level) after the
     same number of iterations, at the same point."""
     from agentlib_mpc_amd import benchmarks as bm
 
     case = configs.CASES[name](solver_options=bm.REFERENCE, **kw)
-    p, lbw, ubw, w0 = case.oracle_inputs
-    ref = ipm.solve(case.oracle.functions(p), w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p),
-                    ipm.IPMOptions(**REFERENCE_OPTS))
+    ref = _oracle(case, ipm.IPMOptions(**REFERENCE_OPTS), key=(name, repr(kw)))
     assert ref.success, ref.status
-    res = _gpu_solve(case, n_copies=2)
+    res = _gpu_solve(case, n_copies=2, build=build)
     nlp = case.backend.problem.nlp
     for r in res:
         assert r.stats["return_status"] == ref.status, (r.stats, ref.status)
@@ -171,19 +194,19 @@ RESTO_CASES = [
 ]
 
 
+@pytest.mark.parametrize("build", BUILDS)
 @pytest.mark.parametrize("name,kw,setting", RESTO_CASES)
-def test_gpu_restoration_phase_matches_oracle(name, kw, setting):
+def test_gpu_restoration_phase_matches_oracle(name, kw, setting, build):
     """Line-search failures: same status, iteration count, number of soft restoration steps,
     restoration phases and restoration iterations as the oracle, at the same point."""
     from agentlib_mpc_amd import benchmarks as bm
 
     tight = setting == "tight"
     case = configs.CASES[name](solver_options=bm.TIGHT if tight else bm.REFERENCE, **kw)
-    p, lbw, ubw, w0 = case.oracle_inputs
     opts = ipm.IPMOptions(tol=1e-10, max_iter=500, acceptable_iter=0) if tight else ipm.IPMOptions(**REFERENCE_OPTS)
-    ref = ipm.solve(case.oracle.functions(p), w0, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), opts)
+    ref = _oracle(case, opts, key=(name, repr(kw)))
     assert ref.n_resto > 0
-    res = _gpu_solve(case, n_copies=2)
+    res = _gpu_solve(case, n_copies=2, build=build)
     for r in res:
         st = r.stats
         got = (st["return_status"], st["iter_count"], st["n_soft_restorations"], st["n_restorations"],

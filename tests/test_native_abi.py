@@ -106,3 +106,21 @@ def test_kernel_abi_versions_agree():
     text = (native.CSRC / "mpcx_internal.h").read_text()
     abi = int(re.search(r"#define MPCX_KERNEL_ABI (\d+)", text).group(1))
     assert native.KERNEL_ABI == abi == codegen.KERNEL_ABI_VERSION
+
+
+def test_small_fleet_variant_failure_is_not_fatal(tmp_path, monkeypatch):
+    """The small-fleet build is optional: ANY failure of its compile means "no
+    small-fleet build" (warning + .nofit marker, the HBM build serves every batch), while a
+    failure of the main code object stays fatal."""
+    from agentlib_mpc_amd import benchmarks as bm
+
+    be, _ = bm.one_room()
+    gen = be.problem.gen
+    monkeypatch.setattr(native, "KERNEL_DIR", tmp_path)
+    monkeypatch.setattr(native, "_hipcc", lambda: "/bin/false")
+    with pytest.warns(UserWarning, match="small-fleet build"):
+        assert native.compile_model(gen, variant=native.SMALL_FLEET) is None
+    assert native.code_object_path(gen.key, native.SMALL_FLEET).with_suffix(".nofit").exists()
+    assert native.compile_model(gen, variant=native.SMALL_FLEET) is None  # marker: no retry
+    with pytest.raises(native.NativeError):
+        native.compile_model(gen)

@@ -218,3 +218,28 @@ def test_native_reader_takes_any_mapping():
     assert got.keys() == want.keys()
     for k in want:
         np.testing.assert_array_equal(got[k], want[k])
+
+
+@pytest.mark.parametrize("small", [True, False])
+def test_nan_input_after_the_first_call_raises_like_the_host_path(small, monkeypatch):
+    """A NaN measurement or bound arriving at a later call is rejected before any launch with
+    the host path's error (`BatchMarshal.assemble`: 'incomplete NLP inputs'), and the next
+    valid call re-applies every column."""
+    from agentlib_mpc_amd.optimization_backends import plugin_batch
+
+    monkeypatch.setattr(plugin_batch, "SMALL_BATCH", 64 if small else 0)
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    m = be.problem.marshal
+    agents = _agents(cv, 6, 11)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    for field, attr in (("T", "value"), ("mDot", "ub")):
+        bad = [copy.deepcopy(a) for a in agents]
+        setattr(bad[2][field], attr, float("nan"))
+        with pytest.raises(ValueError, match="incomplete NLP inputs"):
+            m.inputs(bad, 300.0, None)                 # the host path
+        with pytest.raises(ValueError, match="incomplete NLP inputs"):
+            rb.update(bad, 300.0)                      # the resident plugin path
+    # the agents' valid values again: every column re-applied, no NaN left behind
+    rb.update(agents, 300.0)
+    w_prev = rb.W.numpy().copy()
+    _check(rb, m, agents, 300.0, w_prev)

@@ -112,6 +112,7 @@ class MI355XBackend(OptimizationBackend):
         self.system = None
         self._remembered: Optional[np.ndarray] = None  # [n, nw] last optimum per batch slot (host path)
         self._resident = None  # device-resident inputs + warm start of the plugin batch (plugin_batch.py)
+        self._slot_ids: Optional[list] = None  # agent key of each batch slot (solve_batch agent_ids)
         name = getattr(self.config.solver.name, "value", self.config.solver.name)
         if name not in KERNEL_SOLVERS:
             raise ValueError(f"solver {name!r} is not available on the MI355X backend "
@@ -135,6 +136,7 @@ class MI355XBackend(OptimizationBackend):
         """Forget the remembered optima: the next solve starts cold (a new backend's first
         solve, `core/discretization.py:212-245`)."""
         self._remembered = None
+        self._slot_ids = None
         if getattr(self, "_resident", None) is not None:
             self._resident.restart_cold()  # keep the device buffers, forget the optima
 
@@ -147,25 +149,46 @@ class MI355XBackend(OptimizationBackend):
     def solve(self, now: float, current_vars: dict) -> Results:
         return self.solve_batch(now, [current_vars])[0]
 
-    def solve_batch(self, now, batch_vars: Sequence[dict]):
+    def solve_batch(self, now, batch_vars: Sequence[dict], agent_ids: Optional[Sequence] = None):
         """Solve one NLP per entry of ``batch_vars`` (same structure) in one launch.
 
         Entry ``i`` is one agent: its warm start is ITS previous optimum (the reference
         keeps one remembered solution per backend instance, `core/discretization.py:
-        221-223`, `247-251`), kept here per batch slot while the batch size is unchanged.
+        221-223`, `247-251`).  ``agent_ids`` (one hashable key per entry, unique) names the
+        agents: each one is warm-started from the optimum of the entry with the same key at
+        the previous call, wherever it sat in that batch and whatever that batch's size was;
+        a key not seen at the previous call starts cold.  Without keys the optima are kept
+        per batch slot while the batch size is unchanged (entry i <- entry i).
         Marshalling is vectorised over the agents (:class:`BatchMarshal`); the returned
         :class:`FleetResults` builds each agent's ``Results`` on access."""
         if self.problem is None:
             raise RuntimeError("setup_optimization() must be called before solve()")
         prob = self.problem
         n = len(batch_vars)
+        src = None  # per entry: the previous call's slot of its agent (-1: cold), or None (by slot)
+        if agent_ids is not None:
+            ids = list(agent_ids)
+            if len(ids) != n or len(set(ids)) != n:
+                raise ValueError("agent_ids: one unique key per batch entry")
+            old = {k: i for i, k in enumerate(self._slot_ids or [])}
+            src = np.array([old.get(k, -1) for k in ids], np.int64)
+            self._slot_ids = ids
+        else:
+            self._slot_ids = None
         if prob.nlp.lift is None:
-            res = self._solve_resident(now, batch_vars)
+            res = self._solve_resident(now, batch_vars, src)
             if self.config.save_results:
                 for i in range(n):
                     self.save_result_df(res[i], now)
             return res
-        w_prev = self._remembered if self._remembered is not None and self._remembered.shape[0] == n else None
+        if src is not None:
+            w_prev = None
+            if self._remembered is not None:
+                w_prev = np.full((n, self._remembered.shape[1]), np.nan)
+                hit = src >= 0
+                w_prev[hit] = self._remembered[src[hit]]
+        else:
+            w_prev = self._remembered if self._remembered is not None and self._remembered.shape[0] == n else None
         p, lbw, ubw, w0, sampled = prob.marshal.inputs(batch_vars, now, w_prev, return_sampled_bounds=True)
         res = self.solve_arrays(p, lbw, ubw, w0, result_bounds=sampled)
         self._remembered = res.w.copy()
@@ -174,9 +197,10 @@ class MI355XBackend(OptimizationBackend):
                 self.save_result_df(res[i], now)
         return res
 
-    def _solve_resident(self, now, batch_vars):
+    def _solve_resident(self, now, batch_vars, src=None):
         """Plugin batch on device-resident inputs (:mod:`.plugin_batch`): only the inputs
-        that changed since the last call cross PCIe, the warm start stays in HBM."""
+        that changed since the last call cross PCIe, the warm start stays in HBM.  ``src``:
+        the previous slot of each entry's agent (-1 cold), None to keep the optima by slot."""
         import torch
 
         from agentlib_mpc_amd.optimization_backends.plugin_batch import ResidentBatch, RowSource
@@ -188,10 +212,15 @@ class MI355XBackend(OptimizationBackend):
         rb = self._resident
         if rb is None or rb.n != len(batch_vars):
             self._remembered = None
+            old = rb
             rb = self._resident = ResidentBatch(prob, self._native(), batch_vars, now, torch.device("cuda"))
+            if old is not None and src is not None:
+                rb.adopt_warm_starts(old, src)  # known agents keep their optima across sizes
             snap = rb.last
         else:
             self._native()  # options of this backend (set_options is per handle)
+            if src is not None:
+                rb.permute_warm_starts(src)
             snap = rb.update(batch_vars, now)
         w, raw = rb.solve()
         stats = StatsView(stats_array(raw), {"t_wall_total": time.perf_counter() - t0})

@@ -368,6 +368,43 @@ class ResidentBatch:
             g[:, c] = P[:, q]
         return np.nan_to_num(g)
 
+    # -- warm starts keyed by agent (MI355XBackend.solve_batch agent_ids) ---------------
+    def permute_warm_starts(self, src: np.ndarray):
+        """Entry i takes the warm start of the previous call's slot src[i] (-1: cold start,
+        applied by the next update).  Same batch size; the inputs are re-read by update()
+        (a column whose per-entry values moved differs from the snapshot and is re-applied)."""
+        src = np.asarray(src, np.int64)
+        if np.array_equal(src, np.arange(self.n)):
+            return
+        hit = np.flatnonzero(src >= 0)
+        cold = np.flatnonzero(src < 0)
+        if hit.size:
+            rows = self.torch.as_tensor(src[hit], device=self.dev)
+            dst = self.torch.as_tensor(hit, device=self.dev)
+            self.W[dst] = self.W[rows].clone()
+            if self.small:
+                if self._h2d is not None:
+                    self._h2d.synchronize()
+                self.hW[hit] = self.hW[src[hit]].copy()
+        self._mark_cold(cold)
+
+    def adopt_warm_starts(self, old: "ResidentBatch", src: np.ndarray):
+        """A new batch (new size): entry i takes the warm start of slot src[i] of the old
+        batch (-1: keeps its cold-start guess)."""
+        src = np.asarray(src, np.int64)
+        hit = np.flatnonzero(src >= 0)
+        if not hit.size:
+            return
+        rows = self.torch.as_tensor(src[hit], device=self.dev)
+        self.W[self.torch.as_tensor(hit, device=self.dev)] = old.W[rows].to(self.dev)
+        if self.small:
+            self.hW[hit] = old.W[rows].cpu().numpy()
+
+    def _mark_cold(self, rows: np.ndarray):
+        if rows.size:
+            prev = self.cold_rows if self.cold_rows is not None else np.zeros(0, np.int64)
+            self.cold_rows = np.union1d(prev, rows).astype(np.int64)
+
     def restart_cold(self):
         """Every agent's next guess is the cold-start guess (no remembered optimum)."""
         self.cold_rows = np.arange(self.n)

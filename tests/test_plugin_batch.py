@@ -243,3 +243,72 @@ def test_nan_input_after_the_first_call_raises_like_the_host_path(small, monkeyp
     rb.update(agents, 300.0)
     w_prev = rb.W.numpy().copy()
     _check(rb, m, agents, 300.0, w_prev)
+
+
+@pytest.mark.parametrize("small", [True, False])
+def test_warm_starts_follow_the_agent_keys(small, monkeypatch):
+    """``solve_batch(..., agent_ids)`` plumbing: after a permutation of
+    the batch every agent keeps ITS previous optimum (the reference's one remembered solution
+    per backend, `core/discretization.py:221-223`), a new key starts cold, and the inputs
+    equal a full re-marshalling of the permuted agents with those warm starts."""
+    from agentlib_mpc_amd.optimization_backends import plugin_batch
+
+    monkeypatch.setattr(plugin_batch, "SMALL_BATCH", 64 if small else 0)
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    m = be.problem.marshal
+    agents = _agents(cv, 5, 21)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    sol = rb.W.numpy().copy() + np.arange(5)[:, None] * 0.01 + 0.3   # stands in for the solutions
+    rb.W.copy_(torch.from_numpy(sol))
+    if rb.small:
+        rb.hW[:] = sol
+    src = np.array([2, 0, -1, 1, 4])          # entry 2 is a new agent
+    newcomer = copy.deepcopy(cv)
+    newcomer["T"].value = 299.5
+    perm = [agents[2], agents[0], newcomer, agents[1], agents[4]]
+    rb.permute_warm_starts(src)
+    rb.update(perm, 300.0)
+    w_prev = np.full_like(sol, np.nan)
+    w_prev[src >= 0] = sol[src[src >= 0]]
+    _check(rb, m, perm, 300.0, w_prev)
+    # a new batch size: known agents carry their optima over, the others start cold
+    rb2 = ResidentBatch(be.problem, None, perm[:3], 300.0, torch.device("cpu"))
+    rb2.adopt_warm_starts(rb, np.array([4, -1, 0]))
+    want = m.inputs(perm[:3], 300.0, None)[3]
+    want[0], want[2] = rb.W.numpy()[4], rb.W.numpy()[0]
+    np.testing.assert_array_equal(rb2.W.numpy(), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("small", [True, False])
+def test_gpu_permuted_batch_keeps_each_agents_warm_start(small, monkeypatch):
+    """a batch permuted between two calls (``agent_ids``) equals two
+    unpermuted calls agent by agent -- same statuses, iteration counts and solutions -- and
+    a batch of another size carries the known agents' optima over."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from agentlib_mpc_amd.optimization_backends import plugin_batch
+
+    monkeypatch.setattr(plugin_batch, "SMALL_BATCH", 64 if small else 0)
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    twin = bm.one_room(solver_options=bm.REFERENCE)[0]
+    agents = _agents(cv, 12, 5)
+    ids = [f"room{i}" for i in range(12)]
+    be.solve_batch(0.0, agents, agent_ids=ids)
+    twin.solve_batch(0.0, agents, agent_ids=ids)
+    for c in agents:
+        c["T"].value += 0.2
+    perm = np.random.default_rng(4).permutation(12)
+    got = be.solve_batch(300.0, [agents[i] for i in perm], agent_ids=[ids[i] for i in perm])
+    want = twin.solve_batch(300.0, agents, agent_ids=ids)
+    np.testing.assert_array_equal(got.stats.array["iter_count"], want.stats.array["iter_count"][perm])
+    np.testing.assert_array_equal(got.stats.array["status"], want.stats.array["status"][perm])
+    np.testing.assert_allclose(got.w, want.w[perm], rtol=1e-13, atol=1e-13)
+    # a smaller batch of known agents in another order: the same warm starts again
+    sub = perm[:5]
+    for c in agents:
+        c["T"].value += 0.2
+    got = be.solve_batch(600.0, [agents[i] for i in sub], agent_ids=[ids[i] for i in sub])
+    want = twin.solve_batch(600.0, agents, agent_ids=ids)
+    np.testing.assert_array_equal(got.stats.array["iter_count"], want.stats.array["iter_count"][sub])
+    np.testing.assert_allclose(got.w, want.w[sub], rtol=1e-13, atol=1e-13)

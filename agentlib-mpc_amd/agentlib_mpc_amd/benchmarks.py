@@ -502,7 +502,27 @@ def compile_all(verbose: bool = False):
                 paths[name] = path
             if verbose:
                 print(f"[mpcx] {name}{' small-fleet' if v else ''}: {path.name if path else 'workspace does not fit LDS'}")
+    # test build: the filter capped at FILTER_CAP_TEST entries (overflow parity with the oracle,
+    # tests/test_gpu_ipm.py::test_gpu_filter_overflow_matches_oracle); MPCX_DEFINES names it
+    saved = os.environ.get("MPCX_DEFINES")
+    os.environ["MPCX_DEFINES"] = FILTER_CAP_DEFINES
+    try:
+        gen = cubic_room()[0].problem.gen
+        for v in (None, native.SMALL_FLEET):
+            path = native.compile_model(gen, False, v)
+            if verbose:
+                print(f"[mpcx] cubic_room {FILTER_CAP_DEFINES}{' small-fleet' if v else ''}: {path.name if path else '-'}")
+    finally:
+        if saved is None:
+            os.environ.pop("MPCX_DEFINES", None)
+        else:
+            os.environ["MPCX_DEFINES"] = saved
     return paths
+
+
+#: the filter cap of the overflow-parity test build (MPCX_DEFINES, csrc/mpcx_ipm.hip MPCX_MAXF)
+FILTER_CAP_TEST = 8
+FILTER_CAP_DEFINES = f"MPCX_MAXF={FILTER_CAP_TEST}"
 
 
 # ---------------------------------------------------------------------------

@@ -70,7 +70,8 @@ class Options(ctypes.Structure):
 
 
 _STATS_INTS = ("iter_count", "status", "n_inertia_corrections", "n_restorations", "n_factorizations", "n_trials",
-               "n_block_chain", "n_dense_stages", "n_soft_restorations", "n_restoration_iters")
+               "n_block_chain", "n_dense_stages", "n_soft_restorations", "n_restoration_iters",
+               "n_filter_overflows", "n_refinement_steps")
 
 
 class Stats(ctypes.Structure):
@@ -89,7 +90,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
 ]
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
-KERNEL_ABI = 6  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
+KERNEL_ABI = 7  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
 
 _lib = None
 _lib_lock = threading.Lock()

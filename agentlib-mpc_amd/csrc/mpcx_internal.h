@@ -5,7 +5,7 @@
 
 #include "mpcx.h"
 
-#define MPCX_KERNEL_ABI 6
+#define MPCX_KERNEL_ABI 7
 
 typedef struct mpcx_kernel_args {
   const double* p;

@@ -52,8 +52,15 @@ constexpr int LDB = (NB % 2 == 0) ? NB + 1 : NB;
 constexpr int WAVE = 64;
 constexpr int VS = (NW + WAVE - 1) / WAVE;  // variable slots per lane
 constexpr int CS = (M + WAVE - 1) / WAVE;   // constraint slots per lane
-constexpr int MAXF = 32;           // filter entries kept in LDS
-static_assert(MAXF <= 64, "the filter test reads one entry per lane");
+// filter entries kept in LDS (IPOPT's filter list is unbounded; entries a new one dominates are
+// removed on insertion, Filter::AddEntry): one cap shared with oracle/ipm.py (max_filter) and
+// oracle/c/ipm_oracle.c; an insertion into a full filter drops the oldest entry (counted)
+// (MPCX_MAXF: a smaller cap for the overflow-parity test build, tests/test_gpu_ipm.py)
+#ifndef MPCX_MAXF
+#define MPCX_MAXF 64
+#endif
+constexpr int MAXF = MPCX_MAXF;
+static_assert(MAXF >= 1 && MAXF <= 64, "the filter test reads one entry per lane");
 constexpr double INF_BOUND = 1e19;
 constexpr double TS = MPCX_TS;
 #ifdef MPCX_WS_LDS  // small-fleet variant: one agent per CU, its workspace in LDS
@@ -171,13 +178,23 @@ constexpr long O_ZU0 = O_ZL0 + NW;
 constexpr long O_VL0 = O_ZU0 + NW;       // [M]
 constexpr long O_VU0 = O_VL0 + M;
 constexpr long O_FLT0 = O_VU0 + M;       // [2][MAXF] the original filter while restoring
-constexpr long WS_DOUBLES = O_FLT0 + 2L * MAXF;
+// iterative refinement of the restoration steps (resto_refine)
+constexpr long O_RRHS = O_FLT0 + 2L * MAXF;      // [N][NB] the step's right-hand side
+constexpr long O_RSOL = O_RRHS + (long)N * NB;   // [N][NB] the step so far
+constexpr long O_RU = O_RSOL + (long)N * NB;     // [N][NLOC] local step vectors
+constexpr long O_RY = O_RU + (long)N * NLOC;     // [N][NLOC] local KKT products
+constexpr long WS_DOUBLES = O_RY + (long)N * NLOC;
 // IPOPT restoration constants (its defaults; not exposed as options)
 constexpr double RESTO_RHO = 1000.0;          // resto_penalty_parameter
 constexpr double RESTO_KAPPA = 0.9;           // required_infeasibility_reduction
 constexpr double SOFT_PD_FACTOR = 0.9999;     // soft_resto_pderror_reduction_factor
 constexpr int MAX_SOFT_ITERS = 10;            // max_soft_resto_iters
 constexpr double BOUND_MULT_RESET = 1000.0;   // bound_mult_reset_threshold
+// PDFullSpaceSolver iterative refinement (IPOPT defaults)
+constexpr int MIN_REFINE = 1;                 // min_refinement_steps
+constexpr int MAX_REFINE = 10;                // max_refinement_steps
+constexpr double RESID_RATIO_MAX = 1e-10;     // residual_ratio_max
+constexpr double RESID_IMPROVE = 1.0;         // residual_improvement_factor
 
 using Args = mpcx_kernel_args;
 // kernel arguments read in place from the kernarg segment (address space 4: scalar
@@ -371,6 +388,8 @@ struct KState {
   Acceptable acc0;
   double fo, zeta, prox, mu0, tau0, dw_last0, theta_max0, theta_min0, theta_start;
   int resto, soft, soft_count, lsmode, nfilt0, square_r, n_soft, n_resto_it;
+  int n_filt_over, n_refine;  // filter insertions that dropped the oldest entry; refinement steps
+  double rnrm;                // refinement: max-norm of the step's full right-hand side
 };
 
 #ifndef MPCX_NETX
@@ -612,6 +631,10 @@ struct Agent {
   __device__ cdbl* vl0() const { return cold_base() + O_VL0; }
   __device__ cdbl* vu0() const { return cold_base() + O_VU0; }
   __device__ cdbl* flt0() const { return cold_base() + O_FLT0; }
+  __device__ cdbl* rrhs() const { return cold_base() + O_RRHS; }
+  __device__ cdbl* rsol() const { return cold_base() + O_RSOL; }
+  __device__ cdbl* ru() const { return cold_base() + O_RU; }
+  __device__ cdbl* ry() const { return cold_base() + O_RY; }
 #undef ws
 };
 
@@ -1014,18 +1037,20 @@ __device__ __forceinline__ double dual_diag_v(int cl, double sig, const KKTDiag 
 // ---------------------------------------------------------------------------
 // sequential block chain (fallback when a stage interior is singular)
 // ---------------------------------------------------------------------------
-// per-variable / per-constraint diagonal terms (workspace; NaN in kx marks a fixed variable)
+__device__ __forceinline__ int crow(int r);
+// per-variable / per-constraint diagonal terms (workspace; NaN in kx marks a fixed variable).
+// Newton mode: the terms the rhs phases wrote (dg: barrier Sigma, the restoration's proximity
+// weight and its eliminated p, n terms), + delta_w on the primal side
 __device__ __noinline__ void kkt_diagonals(const Agent a, const KKTDiag kd) {
   for (int q = lane_now(); q < N * NP; q += WAVE) {
-    const int i = NX + q;
+    const int i = NX + q, b = q / NP, off = q % NP;
     const double lo = a.xL()[i], hi = a.xU()[i];
-    a.kx()[q] = (lo == hi) ? NAN
-                           : (kd.mode == LSQ ? 1.0 : sigma_x_v(a.x()[i], lo, hi, a.zL()[i], a.zU()[i]) + kd.dw);
+    a.kx()[q] = (lo == hi) ? NAN : (kd.mode == LSQ ? 1.0 : a.dg(b)[off < NV ? off : LX1 + off - NV] + kd.dw);
   }
   for (int c = lane_now(); c < M; c += WAVE) {
     const double sl = a.sL()[c], su = a.sU()[c];
     const int cl = cls_of(a.lb()[c], a.ub()[c], sl, su);
-    a.kd()[c] = dual_diag_v(cl, sigma_s_v(a.s()[c], sl, su, a.vL()[c], a.vU()[c]), kd);
+    a.kd()[c] = kd.mode == LSQ ? dual_diag_v(cl, 0.0, kd) : -a.dg(c / NG)[crow(c % NG)];
   }
   sync();
 }
@@ -2752,6 +2777,30 @@ __device__ __noinline__ int soft_try(const Agent a) {
   return 0;
 }
 
+// IPOPT Filter::AddEntry of (th, ph): the entries the new one dominates (th <= theta_j and
+// ph <= phi_j) are removed, order kept, then it is appended; a full filter drops its oldest
+// entry (counted: IPOPT's list is unbounded).  One entry per lane: a ballot compacts the kept
+// entries in one LDS read and write.
+__device__ __forceinline__ void filter_insert(double th, double ph) {
+  KState& K = gL.ks;
+  const int j = lane_now();
+  const int nf = K.nfilt;
+  const double ej = gL.fth[j < MAXF ? j : 0], pj = gL.fph[j < MAXF ? j : 0];
+  const bool keep = j < nf && !(th <= ej && ph <= pj);
+  const unsigned long long km = __ballot(keep);
+  int nk = __popcll(km);
+  int pos = __popcll(km & ((1ull << j) - 1ull));
+  const int drop = nk >= MAXF ? 1 : 0;  // still full: the oldest kept entry goes
+  pos -= drop;
+  nk -= drop;
+  wsync();
+  if (keep && pos >= 0) { gL.fth[pos] = ej; gL.fph[pos] = pj; }
+  if (j == 0) { gL.fth[nk] = th; gL.fph[nk] = ph; }
+  wsync();
+  K.nfilt = nk + 1;
+  K.n_filt_over += drop;
+}
+
 // ---- restoration phase ----------------------------------------------------------------
 
 // start: called at the iterate whose line search (and soft step) failed, with K.st of it
@@ -2762,15 +2811,8 @@ __device__ __noinline__ void resto_start(const Agent a) {
   const int lane = lane_now();
   {  // FilterLSAcceptor::PrepareRestoPhaseStart: the current point enters the original filter
     const double theta = K.st.theta, phi = K.fx - K.mu * K.st.barrier;
-    int nfilt = K.nfilt;
-    if (nfilt == MAXF) {
-      if (lane == 0)
-        for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
-      nfilt--;
-    }
-    if (lane == 0) { gL.fth[nfilt] = (1.0 - ka.opt.gamma_theta) * theta; gL.fph[nfilt] = phi - ka.opt.gamma_phi * theta; }
-    nfilt++;
-    wsync();
+    filter_insert((1.0 - ka.opt.gamma_theta) * theta, phi - ka.opt.gamma_phi * theta);
+    const int nfilt = K.nfilt;
     for (int j = lane; j < nfilt; j += WAVE) { a.flt0()[j] = gL.fth[j]; a.flt0()[MAXF + j] = gL.fph[j]; }
     K.nfilt0 = nfilt;
     K.theta_start = theta;
@@ -3080,6 +3122,121 @@ __device__ __noinline__ void rhs_dual_resto(const Agent a, double mu, double dw,
   sync();
 }
 
+// ---- iterative refinement of the restoration step (IPOPT PDFullSpaceSolver::Solve) -------
+// The restoration KKT system is solved with p and n eliminated (their diagonal terms folded
+// into the constraint rows, as IPOPT's AugRestoSystemSolver does); IPOPT then refines the
+// step on the FULL system, p and n explicit.  Where a row stays violated Sigma_p = z_p / p is
+// tiny and dp = (dlam - r_p) / (Sigma_p + dw) amplifies the rounding of dlam, so the
+// eliminated step alone misses the linearised constraints by far more than the direct solve
+// of the full system does (profiles/r03/s2/resto_trace_case4_*.txt).  resto_resid forms the
+// residual of the full system at the current step (gL.u.sol; dp, dn recovered from dlam) from
+// the compact stage images and the diagonal terms, writes it as the next right-hand side and
+// returns IPOPT's residual ratio; the kernel body re-factors (same matrix) and adds the
+// correction, at least MIN_REFINE times and until the ratio is <= RESID_RATIO_MAX.
+
+// local step vector of stage k at local index i (the step in block order, LDS)
+__device__ __forceinline__ double loc_step(int k, int i) {
+  const int ki = lkind(i);
+  if (ki == 0) return gL.u.sol[k * NB + i];
+  if (kdual(ki)) return gL.u.sol[k * NB + NP + lrow(i)];
+  if (ki == 3) return gL.u.sol[k * NB + NV + (i - LX1)];
+  if (ki == 2) return k > 0 ? gL.u.sol[(k - 1) * NB + NV + (i - NI)] : 0.0;
+  return 0.0;
+}
+
+__device__ __noinline__ double resto_resid(const Agent a, int first) {
+  KState& K = gL.ks;
+  const double mu = K.mu, dw = K.dw, dc = K.dc;
+  const int lane = lane_now();
+  cdbl* const RU = a.ru();
+  cdbl* const RY = a.ry();
+  cdbl* const RR = a.rrhs();
+  if (first)
+    for (int t = lane; t < N * NB; t += WAVE) RR[t] = a.rhs(t / NB)[t % NB];
+  // stage-local products y_k = A_k u_k of the off-diagonal entries and the primal diagonal
+  // (lane k, stage k); the dual diagonal is applied below with p, n explicit
+  for (int k = lane; k < N; k += WAVE) {
+    const unsigned long long fm = gL.fixm[k];
+    for (int i = 0; i < NLOC; ++i) { RU[k * NLOC + i] = loc_step(k, i); RY[k * NLOC + i] = 0.0; }
+    const wdbl* src = a.lp(k);
+    const wdbl* dg = a.dg(k);
+#pragma unroll 1
+    for (int t = 0; t < NCPT; ++t) {
+      if (t >= CB && t < CB + NLOC) continue;  // border (rhs) entries
+      const int ij = kCIJ[t], i = ij & 255, j = ij >> 8;
+      if (i >= NLOC || j >= NLOC || (((fm >> i) | (fm >> j)) & 1ull)) continue;
+      double v = src[t * N];
+      if (i == j) {
+        const int ki = lkind(i);
+        if (kdual(ki)) continue;
+        if (ki == 0 || ki == 3) v += dg[i] + dw;
+        RY[k * NLOC + i] += v * RU[k * NLOC + i];
+      } else {
+        RY[k * NLOC + i] += v * RU[k * NLOC + j];
+        RY[k * NLOC + j] += v * RU[k * NLOC + i];
+      }
+    }
+  }
+  sync();
+  double nres = 0.0, nsol = 0.0, nrhs = 0.0;
+  for (int i = NX + lane; i < NW; i += WAVE) {
+    const int b = (i - NX) / NP, off = (i - NX) % NP;
+    double y;
+    if (off < NV) {
+      y = RY[b * NLOC + off];
+    } else {
+      const int c = off - NV;
+      y = RY[b * NLOC + LX1 + c] + (b + 1 < N ? RY[(b + 1) * NLOC + NI + c] : 0.0);
+    }
+    const double r0 = RR[b * NB + off];
+    const double res = (a.xL()[i] == a.xU()[i]) ? 0.0 : r0 - y;
+    a.rhs(b)[off] = res;
+    nres = fmax(nres, fabs(res));
+    nrhs = fmax(nrhs, fabs(r0));
+    nsol = fmax(nsol, fabs(gL.u.sol[b * NB + off]));
+  }
+  for (int c = lane; c < M; c += WAVE) {
+    const int b = c / NG, r = c % NG;
+    const double lbv = a.lb()[c], ubv = a.ub()[c], slo = a.sL()[c], sup = a.sU()[c];
+    const double gvv = a.gv()[c], gsc = a.gs()[c], sv = a.s()[c], lm = a.lam()[c];
+    const double pv = a.rp()[c], nv = a.rn()[c], sgp = a.rzp()[c] / pv + dw, sgn = a.rzn()[c] / nv + dw;
+    const int cl = cls_of(lbv, ubv, slo, sup);
+    const double sg = sigma_s_v(sv, slo, sup, a.vL()[c], a.vU()[c]);
+    double rl = -((cl == 0 ? gvv - gsc * lbv : gvv - sv) - pv + nv);
+    if (cl == 1) {
+      double gphis = 0.0;
+      if (isfin(slo)) gphis -= mu / (sv - slo);
+      if (isfin(sup)) gphis += mu / (sup - sv);
+      rl -= (gphis - lm) / (sg + dw);
+    }
+    const double rpv = resto_r(-lm, mu / pv), rnv = resto_r(lm, mu / nv);
+    const double dl = gL.u.sol[b * NB + NP + r];
+    const double dp = (dl - rpv) / sgp, dn = (-dl - rnv) / sgn;
+    const double dd = dual_diag_v(cl, sg, KKTDiag{dw, dc, NEWTON});
+    const double res = rl - (RY[b * NLOC + crow(r)] - dp + dn - dd * dl);
+    a.rhs(b)[NP + r] = res;
+    nres = fmax(nres, fabs(res));
+    nrhs = fmax(nrhs, fmax(fabs(rl), fmax(fabs(rpv), fabs(rnv))));
+    nsol = fmax(nsol, fmax(fabs(dl), fmax(fabs(dp), fabs(dn))));
+  }
+  nres = wmax(nres);
+  nsol = wmax(nsol);
+  if (first) K.rnrm = wmax(nrhs);
+  const double nr = K.rnrm;
+  sync();
+  return (nr + nsol == 0.0) ? nres : nres / (fmin(nsol, 1e6 * nr) + nr);
+}
+
+// the step so far <-> the workspace (the factorisation reuses the step's LDS)
+__device__ __noinline__ void resto_step_io(const Agent a, int add) {
+  const int lane = lane_now();
+  for (int t = lane; t < N * NB; t += WAVE) {
+    if (add) gL.u.sol[t] += a.rsol()[t];
+    else a.rsol()[t] = gL.u.sol[t];
+  }
+  sync();
+}
+
 // restoration step from the Newton solution: x, s, lambda as in recover_step, p and n
 // eliminated (dp = (dlam - r_p)/(Sigma_p + dw), dn = (-dlam - r_n)/(Sigma_n + dw))
 __device__ __noinline__ StepInfo recover_step_resto(const Agent a, double mu, double tau, double dw) {
@@ -3306,14 +3463,7 @@ __device__ __forceinline__ void filter_augment(KArgs* argp) {
   KState& K = gL.ks;
   const double gt = (*argp).opt.gamma_theta, gp = (*argp).opt.gamma_phi;
   const double theta = K.st.theta, phi = K.fx - K.mu * K.st.barrier;
-  int nfilt = K.nfilt;
-  if (nfilt == MAXF) {
-    if (lane_now() == 0)
-      for (int j = 1; j < MAXF; ++j) { gL.fth[j - 1] = gL.fth[j]; gL.fph[j - 1] = gL.fph[j]; }
-    nfilt--;
-  }
-  if (lane_now() == 0) { gL.fth[nfilt] = (1.0 - gt) * theta; gL.fph[nfilt] = phi - gp * theta; }
-  K.nfilt = nfilt + 1;
+  filter_insert((1.0 - gt) * theta, phi - gp * theta);
 }
 
 // rest of a restoration iteration after the step: line search, filter, accept.  1: stop
@@ -3448,6 +3598,7 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
   K.it = 0;
   K.acc = Acceptable{-1e50, -1e50, -1, 0};
   K.resto = 0; K.soft = 0; K.soft_count = 0; K.lsmode = 0; K.n_soft = 0; K.n_resto_it = 0;
+  K.n_filt_over = 0; K.n_refine = 0;
 #define KARGP ((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())
 #pragma unroll 1
   for (;;) {
@@ -3460,23 +3611,44 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     PROF(2);
     eval_hess(a, K.resto ? 0.0 : K.obj_scale);  // restoration: the constraints' curvature only
     PROF(3);
-    // factorisation with inertia correction (IPOPT Algorithm IC)
+    // factorisation with inertia correction (IPOPT Algorithm IC); in the restoration phase the
+    // same loop then re-factors for the iterative-refinement corrections (one factor() call
+    // site: it is inlined into the kernel body)
     K.dw = 0.0;
     K.dc = 0.0;
-    int ok = 0;
+    int ok = 0, refining = 0, steps = 0;
+    double old_ratio = 0.0;
 #pragma unroll 1
-    for (int attempt = 0; attempt < 60; ++attempt) {
-      if (attempt > 0) {  // attempt 0: the iteration head wrote the rhs
+    for (int attempt = 0; attempt < 60 + MAX_REFINE + 2; ++attempt) {
+      if (!refining && attempt >= 60) break;
+      if (attempt > 0 && !refining) {  // attempt 0: the iteration head wrote the rhs
         if (K.resto) rhs_dual_resto(a, K.mu, K.dw, K.dc);
         else rhs_dual(a, K.mu, K.dw, K.dc);
       }
       const Inertia in = factor(a, KKTDiag{K.dw, K.dc, NEWTON});
+      if (refining) {  // correction for the residual in the rhs: add it, re-test
+        solve(a);
+        resto_step_io(a, 1);
+        steps += 1;
+        const double ratio = resto_resid(a, 0);
+        if (ratio <= RESID_RATIO_MAX && steps >= MIN_REFINE) break;
+        if (steps > MIN_REFINE && (steps > MAX_REFINE || ratio > RESID_IMPROVE * old_ratio)) break;
+        old_ratio = ratio;
+        resto_step_io(a, 0);
+        continue;
+      }
       K.n_fact += 1;
       K.n_chain += gL.seq;
       if (in.pos == N * NP && in.neg == M && in.zero == 0) {
         if (attempt > 0) K.dw_last = K.dw;
         ok = 1;
-        break;
+        if (!K.resto) break;
+        solve(a);
+        old_ratio = resto_resid(a, 1);
+        if (MIN_REFINE == 0 && old_ratio <= RESID_RATIO_MAX) break;
+        refining = 1;
+        resto_step_io(a, 0);
+        continue;
       }
       K.n_ic += 1;
       const double dw = K.dw, dw_last = K.dw_last;
@@ -3490,7 +3662,8 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     }
     PROF(5);
     if (!ok) { K.status = MPCX_ERROR_IN_STEP; break; }
-    solve(a);
+    if (refining) K.n_refine += steps;
+    else solve(a);
     PROF(6);
     if (K.resto) {
       const StepInfo st = recover_step_resto(a, K.mu, K.tau, K.dw);
@@ -3578,6 +3751,8 @@ extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(
     st.n_restorations = K.n_fallback;
     st.n_soft_restorations = K.n_soft;
     st.n_restoration_iters = K.n_resto_it;
+    st.n_filter_overflows = K.n_filt_over;
+    st.n_refinement_steps = K.n_refine;
     st.n_factorizations = K.n_fact;
     st.n_trials = K.n_trials;
     st.n_block_chain = K.n_chain;

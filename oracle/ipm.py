@@ -86,7 +86,17 @@ class IPMOptions:
     gamma_phi: float = 1e-8
     gamma_theta: float = 1e-5
     alpha_min_frac: float = 0.05
+    #: filter entries kept (IPOPT's list is unbounded; the kernel keeps one entry per lane of a
+    #: wavefront): one cap for the kernel (MAXF, csrc/mpcx_ipm.hip), oracle/c/ipm_oracle.c and
+    #: this file; an insertion into a full filter drops the oldest entry and is counted
     max_filter: int = 64
+    # iterative refinement of the restoration-phase Newton steps on the full system (IPOPT
+    # PDFullSpaceSolver: min_refinement_steps, max_refinement_steps, residual_ratio_max,
+    # residual_improvement_factor)
+    min_refinement_steps: int = 1
+    max_refinement_steps: int = 10
+    residual_ratio_max: float = 1e-10
+    residual_improvement_factor: float = 1.0
     # soft restoration and the feasibility restoration phase (IPOPT defaults)
     soft_resto_pderror_reduction_factor: float = 0.9999
     max_soft_resto_iters: int = 10
@@ -123,6 +133,9 @@ class IPMResult:
     n_soft_resto: int = 0               # line-search failures resolved by a soft restoration step
     n_resto: int = 0                    # calls of the feasibility restoration phase
     resto_iterations: int = 0           # iterations spent in it (counted in ``iterations``)
+    filter_overflows: int = 0           # insertions into a full filter (oldest entry dropped)
+    max_filter_size: int = 0            # largest filter held
+    refine_steps: int = 0               # iterative-refinement corrections (restoration phase)
 
 
 def _relax(b, lower: bool, factor: float):
@@ -408,7 +421,7 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
     history = []
     status = "Maximum_Iterations_Exceeded"
     it = 0
-    counts = dict(soft=0, resto=0, resto_iters=0)
+    counts = dict(soft=0, resto=0, resto_iters=0, filter_overflows=0, max_filter=0)
     in_soft, soft_count = False, 0
     # IPOPT MonotoneMuUpdate::CalcNewMuAndTau: mu >= min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
     mu_floor = max(min(o.tol, o.compl_inf_tol) / (o.kappa_eps + 1.0), o.mu_min)
@@ -417,9 +430,15 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
         return th <= theta_max and not any(th >= a and ph >= b for a, b in filt)
 
     def augment(theta, phi):
-        filt.append(((1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta))
-        if len(filt) > o.max_filter:
+        """IPOPT Filter::AddEntry: the entries the new one dominates are removed (in order),
+        then it is appended; a full filter (max_filter) drops its oldest entry."""
+        nt, nph = (1 - o.gamma_theta) * theta, phi - o.gamma_phi * theta
+        filt[:] = [(a, b) for a, b in filt if not (nt <= a and nph <= b)]
+        if len(filt) >= o.max_filter:
             filt.pop(0)
+            counts["filter_overflows"] += 1
+        filt.append((nt, nph))
+        counts["max_filter"] = max(counts["max_filter"], len(filt))
 
     while True:
         if inner is not None and inner.check(x, s):
@@ -493,8 +512,18 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
             npos = int(np.sum(ev > 0))
             nneg = int(np.sum(ev < 0))
             nzero = len(ev) - npos - nneg
-            sol = np.linalg.solve(K, np.concatenate([rhs_x, rhs_l])) if nzero == 0 else None
+            sol = None
+            if nzero == 0:
+                rhs = np.concatenate([rhs_x, rhs_l])
+                if inner is None:
+                    sol = np.linalg.solve(K, rhs)
+                else:  # restoration phase: refined on the full system once the inertia is right
+                    lu = scipy.linalg.lu_factor(K)
+                    sol = scipy.linalg.lu_solve(lu, rhs)
+                    last_sys[:] = [K, lu, rhs]
             return npos, nneg, nzero, sol
+
+        last_sys = []
 
         dw, dc = 0.0, 0.0
         npos, nneg, nzero, sol = factor_solve(dw, dc)
@@ -510,6 +539,10 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
                 dw = o.kappa_w_plus_bar * dw if delta_w_last == 0 else o.kappa_w_plus * dw
                 if dw > o.delta_w_max:
                     raise RuntimeError("inertia correction failed")
+        if inner is not None:
+            # IPOPT PDFullSpaceSolver: iterative refinement of the step on the full system (here
+            # the restoration NLP's, p and n explicit)
+            sol = _refine(*last_sys, sol, o, counts)
         dx = sol[:n]
         dlam = sol[n:]
         dx[fixed] = 0.0
@@ -663,6 +696,9 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
             o_r = dataclasses.replace(o, max_iter=o.max_iter - it)
             r = _solve(sub, x_r0, lbx_r, ubx_r, lbg_r, ubg_r, o_r, False, inner=inner_r)
             counts["resto_iters"] += r.iterations
+            counts["filter_overflows"] += r.filter_overflows
+            counts["max_filter"] = max(counts["max_filter"], r.max_filter_size)
+            counts["refine"] = counts.get("refine", 0) + r.refine_steps
             it += r.iterations
             if r.status != "Resto_Return":
                 status = {"Solve_Succeeded": "Infeasible_Problem_Detected",
@@ -728,7 +764,34 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
     return IPMResult(x=x, lam_g=lam_g, lam_x=lam_x, f=fx / obj_scale, iterations=it,
                      status=status, success=status in ("Solve_Succeeded", "Solved_To_Acceptable_Level"),
                      history=history, s=s, n_soft_resto=counts["soft"], n_resto=counts["resto"],
-                     resto_iterations=counts["resto_iters"])
+                     resto_iterations=counts["resto_iters"], filter_overflows=counts["filter_overflows"],
+                     max_filter_size=counts["max_filter"], refine_steps=counts.get("refine", 0))
+
+
+def _refine(K, lu, rhs, sol, o: IPMOptions, counts: dict):
+    """IPOPT PDFullSpaceSolver::Solve's iterative refinement on the full system K sol = rhs:
+    at least ``min_refinement_steps`` corrections, more while the residual ratio
+    ||r||_inf / (min(||sol||_inf, 1e6 ||rhs||_inf) + ||rhs||_inf) exceeds
+    ``residual_ratio_max``, at most ``max_refinement_steps``, stopping early when a step does
+    not improve the ratio (``residual_improvement_factor``)."""
+
+    def ratio(res, x):
+        nr, nx = np.max(np.abs(rhs), initial=0.0), np.max(np.abs(x), initial=0.0)
+        return np.max(np.abs(res), initial=0.0) / (min(nx, 1e6 * nr) + nr) if nr + nx > 0 else 0.0
+
+    res = rhs - K @ sol
+    rr = ratio(res, sol)
+    steps = 0
+    while steps < o.min_refinement_steps or rr > o.residual_ratio_max:
+        sol = sol + scipy.linalg.lu_solve(lu, res)
+        res = rhs - K @ sol
+        old, rr = rr, ratio(res, sol)
+        steps += 1
+        if rr > o.residual_ratio_max and steps > o.min_refinement_steps and (
+                steps > o.max_refinement_steps or rr > o.residual_improvement_factor * old):
+            break
+    counts["refine"] = counts.get("refine", 0) + steps
+    return sol
 
 
 def _block_eigs(D: np.ndarray) -> np.ndarray:

@@ -28,13 +28,13 @@ def test_library_builds_loads_and_exports_all_symbols():
     lib = ctypes.CDLL(str(path))
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.mpcx_version() == 6
+    assert lib.mpcx_version() == 7
 
 
 def test_struct_sizes_match_header():
-    # mpcx_options: 40 doubles + 4 int32; mpcx_stats: 6 doubles + 8 int32
+    # mpcx_options: 40 doubles + 4 int32; mpcx_stats: 6 doubles + 12 int32
     assert ctypes.sizeof(native.Options) == 40 * 8 + 4 * 4
-    assert ctypes.sizeof(native.Stats) == 6 * 8 + 10 * 4
+    assert ctypes.sizeof(native.Stats) == 6 * 8 + 12 * 4
     assert ctypes.sizeof(native.ProblemDesc) == 8 * 4
 
 

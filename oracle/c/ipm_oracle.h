@@ -31,9 +31,13 @@ typedef struct {
   int max_iter, acceptable_iter;
 } opts_t;
 
+/* status: 0 Solve_Succeeded, 1 Solved_To_Acceptable_Level, -1 Maximum_Iterations_Exceeded,
+   -2 Restoration_Failed, -3 Error_In_Step_Computation, -4 Invalid_Number_Detected,
+   -5 Infeasible_Problem_Detected (the mpcx_status codes) */
 typedef struct {
   double obj;
   int iter, status, n_fact, n_trials;
+  int n_soft, n_resto, n_resto_iters, n_filter_over, n_refine;
 } ostats_t;
 
 /* Solve n_agents NLPs of one stage model (agent-major p/lbw/ubw/w_io, kernel layout);

@@ -46,8 +46,16 @@ def options(**kw) -> OOpts:
     return OOpts(**{n: getattr(d, n) for n, _ in OOpts._fields_})
 
 
+_OSTATS_INTS = ("iter", "status", "n_fact", "n_trials", "n_soft", "n_resto", "n_resto_iters", "n_filter_over",
+                "n_refine")
+
+
 class OStats(ctypes.Structure):
-    _fields_ = [("obj", ctypes.c_double)] + [(n, ctypes.c_int) for n in ("iter", "status", "n_fact", "n_trials")]
+    _fields_ = [("obj", ctypes.c_double)] + [(n, ctypes.c_int) for n in _OSTATS_INTS]
+
+
+def _stats_dicts(st):
+    return [dict(obj=s.obj, **{n: getattr(s, n) for n in _OSTATS_INTS}) for s in st]
 
 
 HDR = HERE / "c" / "ipm_oracle.h"
@@ -113,8 +121,7 @@ def solve_room_fleet(p, lbw, ubw, w0, N=15, d=2, tol=1e-8, max_iter=500, threads
     st = (OStats * n)()
     ok = lib().oracle_room_solve_fleet(ctypes.byref(m), n, p.ctypes.data, lbw.ctypes.data, ubw.ctypes.data,
                                        w.ctypes.data, st, ctypes.byref(opts), threads)
-    stats = [{"obj": s.obj, "iter": s.iter, "status": s.status, "n_fact": s.n_fact, "n_trials": s.n_trials}
-             for s in st]
+    stats = _stats_dicts(st)
     return w, stats, ok
 
 
@@ -183,6 +190,5 @@ def solve_generated_fleet(gen, p, lbw, ubw, w0, threads=0, tol=1e-8, max_iter=50
     opts = options(tol=tol, max_iter=max_iter, **ipopt)
     ok = _gen_lib(gen).oracle_gen_solve_fleet(n, p.ctypes.data, lbw.ctypes.data, ubw.ctypes.data, w.ctypes.data,
                                               st, ctypes.byref(opts), threads)
-    stats = [{"obj": s.obj, "iter": s.iter, "status": s.status, "n_fact": s.n_fact, "n_trials": s.n_trials}
-             for s in st]
+    stats = _stats_dicts(st)
     return w, stats, ok

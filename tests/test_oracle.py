@@ -193,3 +193,47 @@ def test_restoration_phase_on_a_stage_nlp():
     assert r.status == "Solve_Succeeded" and r.n_resto == 2
     z = r.x[[i for i, n in enumerate(case.oracle.w_names) if n.startswith("z@")]]
     np.testing.assert_allclose(z, 2.279018786, rtol=1e-7)
+
+
+_C_STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", -1: "Maximum_Iterations_Exceeded",
+             -2: "Restoration_Failed", -3: "Error_In_Step_Computation", -4: "Invalid_Number_Detected",
+             -5: "Infeasible_Problem_Detected"}
+
+
+def _resto_case_inputs(name, kw, setting):
+    from agentlib_mpc_amd import benchmarks as bm
+    from tests import configs
+
+    case = configs.CASES[name](solver_options=bm.TIGHT if setting == "tight" else bm.REFERENCE, **kw)
+    prob = case.backend.problem
+    mi = prob.mpc_inputs(case.current_vars, 0.0)
+    mi.update(prob.initial_guess(mi))
+    kin = prob.to_kernel(*[a[None] for a in prob.nlp_inputs(mi)])
+    base = dict(tol=1e-10, max_iter=500, acceptable_iter=0) if setting == "tight" else dict(REFERENCE_OPTS)
+    return case, prob, kin, base
+
+
+@pytest.mark.parametrize("name,kw,setting", [
+    ("cubic_room", {}, "tight"),
+    ("cubic_room", {}, "reference"),
+    ("fixture_mpc", {"T_lb": 245.0, "T_ub": 302.0, "disturbance": 260.0}, "reference"),
+])
+def test_c_oracle_restoration_phase_matches_numpy_oracle(name, kw, setting):
+    """The C restatement (CPU baselines) runs IPOPT's soft restoration step and feasibility
+    restoration phase as oracle/ipm.py does (the restoration NLP with p, n explicit as a stage
+    model, every step refined on the full system): same status, iteration, soft-step,
+    restoration-phase and restoration-iteration counts, refinement steps and objective."""
+    case, prob, (p, lbw, ubw, w0), base = _resto_case_inputs(name, kw, setting)
+    o = dict(base)
+    tol, mi_ = o.pop("tol"), o.pop("max_iter")
+    w, st, ok = cbuild.solve_generated_fleet(prob.gen, p, lbw, ubw, w0, threads=1, tol=tol, max_iter=mi_, **o)
+    op, olb, oub, ow = case.oracle_inputs
+    ref = ipm.solve(case.oracle.functions(op), ow, olb, oub, case.oracle.lbg(op), case.oracle.ubg(op),
+                    ipm.IPMOptions(**base))
+    s = st[0]
+    assert ref.n_resto > 0
+    got = (_C_STATUS[s["status"]], s["iter"], s["n_soft"], s["n_resto"], s["n_resto_iters"], s["n_refine"],
+           s["n_filter_over"])
+    assert got == (ref.status, ref.iterations, ref.n_soft_resto, ref.n_resto, ref.resto_iterations,
+                   ref.refine_steps, ref.filter_overflows), got
+    np.testing.assert_allclose(s["obj"], ref.f, rtol=1e-9)

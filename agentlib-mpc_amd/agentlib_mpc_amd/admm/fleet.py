@@ -565,6 +565,8 @@ class ADMMFleet:
         self._blk_key = None
         if participating is None:
             self._part, self.ROW_ON = None, None
+            for c in self.classes:
+                c.PART = None
             return
         part = []
         on = np.ones(self.X.shape[0], np.int32)
@@ -579,6 +581,8 @@ class ADMMFleet:
                 c.dev_slots[si]["rows_part"] = t.as_tensor(np.where(m, rows, self.X.shape[0] - 1).astype(np.int32),
                                                            device=self.device)
         self._part = part
+        for c, m in zip(self.classes, part):
+            c.PART = t.as_tensor(m.astype(np.int32), device=self.device)
         self.ROW_ON = t.as_tensor(on, device=self.device)
 
     def register(self, class_name: str, agent: Optional[int]):
@@ -617,82 +621,102 @@ class ADMMFleet:
     def run_coordinated(self, penalty_factor: float, admm_iter_max: int = 20, primal_tol: float = 1e-3,
                         dual_tol: float = 1e-3, use_relative_tolerances: bool = True, abs_tol: float = 1e-3,
                         rel_tol: float = 1e-3, penalty_change_threshold: float = -1.0,
-                        penalty_change_factor: float = 2.0) -> dict:
+                        penalty_change_factor: float = 2.0, check_every: int = 4) -> dict:
         """One control step of the coordinator (`admm_coordinator.py:259-321`), run by every
         block independently: its own residual test, penalty variation and iteration count;
         a converged block is frozen (no solves, no updates) while the others go on.
+
+        The stopping test runs on the device (``mpcx_admm_block_stop``, one thread per block,
+        after each iteration's residual totals): the block penalties, freeze masks, records and
+        iteration counts stay in HBM, so an iteration issues launches only.  The host reads the
+        number of blocks still active every ``check_every`` iterations (one small all-reduce of
+        it across ranks first) and the records once, after the round; iterations run past the
+        last block's stop before that check are no-ops (every agent and group frozen) and are
+        not counted.  Per-iteration wall times are device-clock stamps of the end of each
+        iteration relative to the round's first stamp.
 
         Returns ``iterations`` (the last iteration any block ran), ``converged`` (all blocks),
         ``block_iterations`` / ``block_converged`` / ``block_records`` per block and
         ``records`` (block 0's history when there is one block, else the per-iteration
         norms over the blocks still running)."""
-        nb = self.n_blocks
+        t = self.torch
+        ops, nb = self.ops, self.n_blocks
+        dev, i32 = self.device, t.int32
         t0 = time.perf_counter()  # _performance_counter, set at the start of the round (:270)
-        rho_b = np.full(nb, float(penalty_factor))
-        active = np.ones(nb, bool)
-        self._set_blocks(rho_b, None)
-        self._update_means(float(penalty_factor), apply_multipliers=False, per_block=True)
+        rho0 = float(penalty_factor)
+        n_it = max(int(admm_iter_max), 0)
+        ACTIVE_B = t.ones(nb, dtype=i32, device=dev)
+        ITERS_B = t.full((nb,), n_it, dtype=i32, device=dev)
+        REC = t.zeros(max(n_it, 1) * nb * 4, dtype=t.float64, device=dev)
+        NACT = t.zeros(n_it + 1, dtype=i32, device=dev)
+        CLOCK = t.zeros(n_it + 1, dtype=t.int64, device=dev)
+        self.RHO_B.fill_(rho0)
+        self._expand_blocks(ACTIVE_B)
+        self._blk_key = None
+        self._masked = True
+        crit = (1 if use_relative_tolerances else 0, abs_tol, rel_tol, primal_tol, dual_tol,
+                penalty_change_threshold, penalty_change_factor)
+        self._update_means(rho0, apply_multipliers=False, per_block=True)
         shift = int(len(self.classes[0].coupling_grid) / self.classes[0].horizon)
         self._shift_all(shift)
-        iters = np.full(nb, admm_iter_max, np.int64)
-        conv_b = np.zeros(nb, bool)
-        block_records = _BlockRecords(nb)
-        records = []
         self._ok_count.zero_()
         self._fb_count.zero_()
-        it = 0
-        gblk = self.block_is_global
-        for it in range(1, admm_iter_max + 1):
-            self._solve_all(float(penalty_factor))
-            # a block spanning ranks stops on the same (reduced) totals everywhere, so this
-            # decision agrees over the ranks; rank-local blocks need no collective at all
-            reduce = bool(active[gblk].any())
-            tot = self._update_means(float(penalty_factor), apply_multipliers=True, per_block=True,
-                                     reduce=reduce).cpu().numpy()
-            now_t = time.perf_counter() - t0
-            prim = np.sqrt(np.maximum(tot[:, 0], 0.0))
-            dual = np.sqrt(np.maximum(tot[:, 1], 0.0))
-            if use_relative_tolerances:
-                scale_p = np.maximum(np.sqrt(np.maximum(tot[:, 2], 0.0)), np.sqrt(np.maximum(tot[:, 3], 0.0)))
-                eps_pri = np.sqrt(tot[:, 6]) * abs_tol + rel_tol * scale_p
-                eps_dual = np.sqrt(tot[:, 5]) * abs_tol + rel_tol * np.sqrt(np.maximum(tot[:, 4], 0.0))
-                conv = (prim < eps_pri) & (dual < eps_dual)
-            else:
-                conv = (prim < primal_tol) & (dual < dual_tol)
-            # _check_convergence: vary the penalty, THEN record it (admm_coordinator.py:396-402)
-            if penalty_change_threshold > 1:
-                up = active & (prim > penalty_change_threshold * dual)
-                down = active & ~up & (dual > penalty_change_threshold * prim)
-                rho_b = np.where(up, rho_b * penalty_change_factor, np.where(down, rho_b / penalty_change_factor, rho_b))
-            block_records.append(prim, dual, rho_b, active, now_t)
-            a = active
-            records.append(IterationRecord(float(np.sqrt(tot[a, 0].clip(0).sum())),
-                                           float(np.sqrt(tot[a, 1].clip(0).sum())),
-                                           float(rho_b[a][0]) if nb == 1 else float(np.mean(rho_b[a])),
-                                           wall_time=now_t))
-            done = active & conv
-            if done.any():
-                iters[done] = it
-                conv_b |= done
-                active = active & ~done
-            if not active.any():
-                break
-            self._set_blocks(rho_b, active)
+        tot = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
+        ops.block_stop(0, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK)  # the round's first stamp
+        ran = 0
+        for it in range(1, n_it + 1):
+            self._solve_all(rho0)
+            # ranks iterate in lockstep (the loop exit below is agreed on), so every rank takes
+            # part in every iteration's all-reduce; frozen groups' moments travel but are not used
+            tot = self._update_means(rho0, apply_multipliers=True, per_block=True, reduce=True)
+            ops.block_stop(it, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK)
+            self._expand_blocks(ACTIVE_B)
+            ran = it
+            if it % max(int(check_every), 1) == 0 or it == n_it:
+                left = NACT[it:it + 1].to(t.float64)
+                if self.world > 1:
+                    self.dist.all_reduce(left, group=self.group)
+                if float(left.item()) == 0.0:
+                    break
         self._sync()
-        # the next round starts from full penalties and no freeze mask: drop the upload
-        # cache with the mask, or a round that converged at its first iteration (cache key
-        # still the start-of-round one) would leave the participation mask unapplied
+        # the next round starts from full penalties and no freeze mask
         self._masked = False
         self._blk_key = None
         wall = time.perf_counter() - t0
+        iters = ITERS_B.cpu().numpy().astype(np.int64)
+        conv_b = ACTIVE_B.cpu().numpy() == 0
+        last = int(iters.max()) if nb else 0
+        rec = REC.cpu().numpy().reshape(max(n_it, 1), nb, 4)[:ran]
+        clk = CLOCK.cpu().numpy()
+        hz = ops.clock_hz()
+        block_records = _BlockRecords(nb)
+        records = []
+        for j in range(min(last, ran)):
+            r = rec[j]
+            a = r[:, 3] != 0
+            now_t = float(clk[j + 1] - clk[0]) / hz
+            block_records.append(r[:, 0], r[:, 1], r[:, 2], a, now_t)
+            if nb == 1:
+                continue
+            records.append(IterationRecord(float(np.sqrt((r[a, 0] ** 2).sum())), float(np.sqrt((r[a, 1] ** 2).sum())),
+                                           float(np.mean(r[a, 2])), wall_time=now_t))
         if nb == 1:
             records = block_records[0]
         self.history.extend(records)
         self.rounds += 1
-        return {"iterations": it, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
+        return {"iterations": last, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
                 "converged_solves": int(self._ok_count.item()), "block_iterations": iters,
-                "block_converged": conv_b, "block_records": block_records, "block_is_global": gblk.copy(),
-                "restorations": int(self._fb_count.item())}
+                "block_converged": conv_b, "block_records": block_records, "block_is_global": self.block_is_global.copy(),
+                "restorations": int(self._fb_count.item()), "loop_iterations": ran}
+
+    def _expand_blocks(self, active_b):
+        """Per-block penalties and freeze masks (device) to the groups and the agents (with the
+        participation mask) -- what the solves, means and multiplier updates read."""
+        ops = self.ops
+        if self.G:
+            ops.block_expand(self.BLOCK_G, active_b, self.RHO_B, None, self.ACTIVE_G, self.RHO_G)
+        for c in self.classes:
+            ops.block_expand(c.BLOCK, active_b, None, getattr(c, "PART", None), c.ACTIVE, None)
 
     def save_stats(self, path, start_time: float, records: Sequence[IterationRecord], first_iteration: int = 0):
         """Append one round's residual history to the coordinator's ``solve_stats_file``

@@ -92,5 +92,25 @@ class NativeADMMOps:
                                                             _p(rho_g), _p(active_g), _p(row_on), self.stream),
                   "mpcx_admm_exchange_update_masked")
 
+    # -- the coordinators' stopping test (include/mpcx.h mpcx_admm_block_stop / _expand) ----
+    def block_stop(self, it, totals, crit, rho_b, active_b, iters_b, record, n_active, clock):
+        """``crit`` = (use_relative, abs_tol, rel_tol, primal_tol, dual_tol, change_threshold,
+        change_factor); device state tensors updated in place."""
+        nb = active_b.shape[0]
+        self._chk(self.lib.mpcx_admm_block_stop(nb, it, _p(totals), int(crit[0]), *[float(v) for v in crit[1:]],
+                                                _p(rho_b), _p(active_b), _p(iters_b), _p(record), _p(n_active),
+                                                _p(clock), self.stream), "mpcx_admm_block_stop")
+
+    def block_expand(self, idx, active_b, rho_b, part, out_active, out_rho):
+        self._chk(self.lib.mpcx_admm_block_expand(idx.shape[0], _p(idx), _p(active_b), _p(rho_b), _p(part),
+                                                  _p(out_active), _p(out_rho), self.stream),
+                  "mpcx_admm_block_expand")
+
+    def clock_hz(self) -> float:
+        khz = int(self.lib.mpcx_device_clock_khz())
+        if khz <= 0:
+            raise native.NativeError(f"mpcx_device_clock_khz failed ({khz})")
+        return 1e3 * khz
+
     def shift(self, T, shift, x):
         self._chk(self.lib.mpcx_admm_shift(x.shape[0], T, shift, _p(x), self.stream), "mpcx_admm_shift")

@@ -88,6 +88,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
+    "mpcx_admm_block_stop", "mpcx_admm_block_expand", "mpcx_device_clock_khz",
 ]
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
 KERNEL_ABI = 7  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
@@ -204,6 +205,10 @@ def load_library():
         lib.mpcx_gather_rows.argtypes = [i32, i32, vp, i64, vp, vp, vp, vp]
         lib.mpcx_scatter_rows.argtypes = [i32, i32, vp, vp, vp, i64, vp, vp]
         lib.mpcx_fill_column.argtypes = [i32, vp, i64, i32, f64, vp]
+        lib.mpcx_admm_block_stop.argtypes = [i32, i32, vp, i32, f64, f64, f64, f64, f64, f64, vp, vp, vp, vp, vp,
+                                             vp, vp]
+        lib.mpcx_admm_block_expand.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp]
+        lib.mpcx_device_clock_khz.restype = i64
         for name in EXPORTED_SYMBOLS:
             getattr(lib, name)  # raises AttributeError if a symbol is missing
         _lib = lib

@@ -414,3 +414,84 @@ extern "C" int mpcx_admm_shift(int32_t n_rows, int32_t T, int32_t shift, double*
   LAUNCH_CHECK();
   return MPCX_OK;
 }
+
+// --- the coordinators' stopping test on the device ------------------------------------------
+// One thread per block (one reference ADMMCoordinator each): ADMMCoordinator._check_convergence
+// (admm_coordinator.py:354-435) on the block's residual totals of this iteration, the penalty
+// variation (:467-479, recorded after it, :396-402), and the loop's freeze of a converged block
+// (:288-304) -- so that a fleet iteration needs no host round trip: the host reads the number
+// of active blocks only every few iterations and the records once per round.
+namespace {
+__global__ void k_block_stop(int nb, int it, const double* __restrict__ totals, int use_rel, double abs_tol,
+                             double rel_tol, double primal_tol, double dual_tol, double thr, double fac,
+                             double* __restrict__ rho_b, int* __restrict__ active_b, int* __restrict__ iters_b,
+                             double* __restrict__ record, int* __restrict__ n_active, long long* __restrict__ clock) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b == 0 && clock) clock[it] = (long long)wall_clock64();
+  if (it == 0 || b >= nb) return;
+  const double* t = totals + (long)b * MPCX_ADMM_TOTALS;
+  const double prim = sqrt(fmax(t[0], 0.0)), dual = sqrt(fmax(t[1], 0.0));
+  bool conv;
+  if (use_rel) {
+    const double scale_p = fmax(sqrt(fmax(t[2], 0.0)), sqrt(fmax(t[3], 0.0)));
+    const double eps_pri = sqrt(t[6]) * abs_tol + rel_tol * scale_p;
+    const double eps_dual = sqrt(t[5]) * abs_tol + rel_tol * sqrt(fmax(t[4], 0.0));
+    conv = prim < eps_pri && dual < eps_dual;
+  } else {
+    conv = prim < primal_tol && dual < dual_tol;
+  }
+  const bool act = active_b[b] != 0;
+  double rho = rho_b[b];
+  if (thr > 1.0 && act) {
+    if (prim > thr * dual) rho = rho * fac;
+    else if (dual > thr * prim) rho = rho / fac;
+    rho_b[b] = rho;
+  }
+  double* r = record + ((long)(it - 1) * nb + b) * 4;
+  r[0] = prim; r[1] = dual; r[2] = rho; r[3] = act ? 1.0 : 0.0;
+  const bool still = act && !conv;
+  if (act && conv) { active_b[b] = 0; iters_b[b] = it; }
+  if (n_active && still) atomicAdd(n_active + it, 1);
+}
+
+__global__ void k_block_expand(int n, const int* __restrict__ idx, const int* __restrict__ active_b,
+                               const double* __restrict__ rho_b, const int* __restrict__ part,
+                               int* __restrict__ out_active, double* __restrict__ out_rho) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int b = idx[i];
+  if (out_active) out_active[i] = (active_b[b] != 0 && (part == nullptr || part[i] != 0)) ? 1 : 0;
+  if (out_rho) out_rho[i] = rho_b[b];
+}
+}  // namespace
+
+extern "C" int mpcx_admm_block_stop(int32_t n_blocks, int32_t it, const double* totals, int32_t use_relative,
+                                    double abs_tol, double rel_tol, double primal_tol, double dual_tol,
+                                    double change_threshold, double change_factor, double* rho_b,
+                                    int32_t* active_b, int32_t* iters_b, double* record, int32_t* n_active,
+                                    int64_t* clock, void* stream) {
+  if (n_blocks < 1 || it < 0 || (it > 0 && (!totals || !rho_b || !active_b || !iters_b || !record)))
+    return MPCX_ERR_ARG;
+  hipLaunchKernelGGL(k_block_stop, dim3(blocks_for(n_blocks, 256)), dim3(256), 0, (hipStream_t)stream,
+                     n_blocks, it, totals, use_relative, abs_tol, rel_tol, primal_tol, dual_tol, change_threshold,
+                     change_factor, rho_b, active_b, iters_b, record, n_active, (long long*)clock);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int mpcx_admm_block_expand(int32_t n, const int32_t* idx, const int32_t* active_b, const double* rho_b,
+                                      const int32_t* part, int32_t* out_active, double* out_rho, void* stream) {
+  if (n < 0 || (n > 0 && !idx) || (out_active && !active_b) || (out_rho && !rho_b)) return MPCX_ERR_ARG;
+  if (n == 0 || (!out_active && !out_rho)) return MPCX_OK;
+  hipLaunchKernelGGL(k_block_expand, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, idx,
+                     active_b, rho_b, part, out_active, out_rho);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int64_t mpcx_device_clock_khz(void) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return MPCX_ERR_HIP;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return MPCX_ERR_HIP;
+  return khz;
+}

@@ -275,6 +275,28 @@ int mpcx_admm_exchange_update_masked(int32_t n_groups, int32_t T, const int32_t*
  *      326-331), ADMM._shift (admm.py:329-342) */
 int mpcx_admm_shift(int32_t n_rows, int32_t T, int32_t shift, double* x, void* stream);
 
+/* ---- the coordinators' stopping test on the device -------------------------------------
+ * After mpcx_admm_finalize of ADMM iteration `it` (1-based), one thread per block applies
+ * ADMMCoordinator._check_convergence (admm_coordinator.py:354-435) to the block's totals:
+ * prim = sqrt(t0), dual = sqrt(t1); use_relative: prim < sqrt(t6)*abs_tol + rel_tol*max(sqrt(t2),
+ * sqrt(t3)) and dual < sqrt(t5)*abs_tol + rel_tol*sqrt(t4), else prim < primal_tol and
+ * dual < dual_tol.  Active blocks vary their penalty (change_threshold > 1: rho*factor if
+ * prim > threshold*dual, rho/factor if dual > threshold*prim; admm_coordinator.py:467-479) and
+ * record[it-1][b] = {prim, dual, rho after variation, active} (:396-402); a block meeting its
+ * rule is frozen (active_b[b] = 0, iters_b[b] = it, the loop of :288-304).  n_active[it] (zero
+ * it first) receives the number of blocks still active, clock[it] the device wall clock
+ * (mpcx_device_clock_khz ticks; it = 0 only stamps the clock).  n_active / clock may be NULL. */
+int mpcx_admm_block_stop(int32_t n_blocks, int32_t it, const double* totals, int32_t use_relative,
+                         double abs_tol, double rel_tol, double primal_tol, double dual_tol,
+                         double change_threshold, double change_factor, double* rho_b, int32_t* active_b,
+                         int32_t* iters_b, double* record, int32_t* n_active, int64_t* clock, void* stream);
+/* Block state to groups / agents: out_active[i] = active_b[idx[i]] (and part[i] != 0 when
+ * part != NULL: the participation mask), out_rho[i] = rho_b[idx[i]]; either output may be NULL. */
+int mpcx_admm_block_expand(int32_t n, const int32_t* idx, const int32_t* active_b, const double* rho_b,
+                           const int32_t* part, int32_t* out_active, double* out_rho, void* stream);
+/* Rate of the device wall clock the stopping test stamps (kHz). */
+int64_t mpcx_device_clock_khz(void);
+
 /* ---- NLP vector <-> trajectory moves (no host round trip) ----------------------------
  * dst[dst_rows[a]][t] <- src[a*src_ld + cols[t]]: the coupling trajectories out of the
  * solutions w  <- Results[coupling.name] in CoordinatedADMM.optimize

@@ -149,3 +149,48 @@ class CpuFleetOps:
         a = x.numpy()
         if shift:
             a[:, :T - shift] = a[:, shift:].copy()
+
+    # -- the coordinators' stopping test (restates admm_kernels.hip k_block_stop / _expand) ----
+    def block_stop(self, it, totals, crit, rho_b, active_b, iters_b, record, n_active, clock):
+        import time
+
+        if clock is not None:
+            clock.numpy()[it] = int(time.perf_counter() * 1e9)
+        if it == 0:
+            return
+        use_rel, abs_tol, rel_tol, primal_tol, dual_tol, thr, fac = crit
+        t = totals.numpy().reshape(-1, TOTALS)
+        prim = np.sqrt(np.maximum(t[:, 0], 0.0))
+        dual = np.sqrt(np.maximum(t[:, 1], 0.0))
+        if use_rel:
+            scale_p = np.maximum(np.sqrt(np.maximum(t[:, 2], 0.0)), np.sqrt(np.maximum(t[:, 3], 0.0)))
+            conv = (prim < np.sqrt(t[:, 6]) * abs_tol + rel_tol * scale_p) & \
+                   (dual < np.sqrt(t[:, 5]) * abs_tol + rel_tol * np.sqrt(np.maximum(t[:, 4], 0.0)))
+        else:
+            conv = (prim < primal_tol) & (dual < dual_tol)
+        act = active_b.numpy() != 0
+        rho = rho_b.numpy().reshape(-1)
+        if thr > 1.0:
+            up = act & (prim > thr * dual)
+            down = act & ~up & (dual > thr * prim)
+            rho[:] = np.where(up, rho * fac, np.where(down, rho / fac, rho))
+        rec = record.numpy().reshape(-1, t.shape[0], 4)
+        rec[it - 1] = np.stack([prim, dual, rho, act.astype(float)], axis=1)
+        done = act & conv
+        active_b.numpy()[done] = 0
+        iters_b.numpy()[done] = it
+        if n_active is not None:
+            n_active.numpy()[it] += int((act & ~conv).sum())
+
+    def block_expand(self, idx, active_b, rho_b, part, out_active, out_rho):
+        i = idx.numpy()
+        if out_active is not None:
+            a = active_b.numpy()[i] != 0
+            if part is not None:
+                a &= part.numpy() != 0
+            out_active.numpy()[:] = a.astype(np.int32)
+        if out_rho is not None:
+            out_rho.numpy().reshape(-1)[:] = rho_b.numpy().reshape(-1)[i]
+
+    def clock_hz(self) -> float:
+        return 1e9

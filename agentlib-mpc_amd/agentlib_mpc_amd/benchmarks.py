@@ -561,6 +561,7 @@ def c2_fleet_classes(n_blocks=1, N=10, rho=0.4, seed=None, block_offset=0, solve
     nr = 4 * n_blocks
     rooms = FleetClass("room", be_r, _class_inputs(be_r, cv_r, {"T": T0, "d": d}, nr),
                        aliases={"mDot": aliases}, initial={"mDot": 0.02})
+    rooms.plant = (cv_r, {"T": list(T0), "d": list(d)}, ("T",))  # closed-loop measurement update
     be_a, cv_a = admm_ahu(N=N, rho=rho, solver_options=solver_options)
     blocks = range(block_offset, block_offset + n_blocks)
     ahu = FleetClass("ahu", be_a, _class_inputs(be_a, cv_a, {}, n_blocks),
@@ -568,6 +569,38 @@ def c2_fleet_classes(n_blocks=1, N=10, rho=0.4, seed=None, block_offset=0, solve
                               for i in range(4)},
                      initial={f"mDot_out_{i + 1}": 0.01 for i in range(4)})
     return [rooms, ahu]
+
+
+def value_at(problem, w: np.ndarray, var: str, t: float) -> np.ndarray:
+    """Every agent's value of variable ``var`` at grid time ``t`` from reference-layout
+    solutions ``w`` [n, nw] (the predicted state one control interval ahead: the measurement
+    of a synthetic plant that follows the model)."""
+    for _, grid, rows, index in problem.marshal.vars:
+        if index is None:
+            continue
+        for row in rows:
+            if row[1] == var:
+                j = next(k for k, g in enumerate(grid) if abs(float(g) - t) <= 1e-9 * max(1.0, abs(t)))
+                return w[:, index[row[0]][j]]
+    raise KeyError(var)
+
+
+def advance_plant(fleet, t: float):
+    """Closed loop of a coordinated fleet (the reference's agents re-measuring before the next
+    control step): every class built with a ``plant`` (template variables, measured values,
+    state names) takes its states' predicted values at ``t`` as the next measurements and
+    uploads the new NLP inputs (``ADMMFleet.set_inputs``); the warm starts, means and
+    multipliers stay resident (the coordinator shifts the latter at the start of the round)."""
+    for c in fleet.classes:
+        plant = getattr(c, "plant", None)
+        if plant is None:
+            continue
+        cv, vals, states = plant
+        w = fleet.solutions(c.name)
+        for name in states:
+            vals[name] = list(value_at(c.backend.problem, w, name, t))
+        p, lbw, ubw, _ = _class_inputs(c.backend, cv, vals, c.n)
+        fleet.set_inputs(c.name, p, lbw, ubw)
 
 
 def split_range(total: int, rank: int, world: int):
@@ -641,6 +674,7 @@ def c5_fleet_classes(n_blocks=1, N=24, rho=1.0, seed=None, block_offset=0, solve
                        aliases={"T_v": zone_alias("T_coupling"), "T_ahu": zone_alias("T_coupling_ahu"),
                                 "T_CCA_out": zone_alias("T_rucklauf"), "T_air_out": zone_alias("T_airin")},
                        initial={"T_v": 294.15, "T_ahu": 295.0, "T_CCA_out": 294.15, "T_air_out": 294.0})
+    rooms.plant = (cv_r, {k: list(v) for k, v in vals.items()}, ("T_air",))
     be_a, cv_a = tz_ahu(N=N, rho=rho, solver_options=solver_options)
     ahu_al = {}
     for i in range(3):

@@ -383,16 +383,9 @@ def c2_admm_bench(args, world, rank, dev):
     fleet = ADMMFleet(classes, device=dev, comm="default" if world > 1 else None)
     for c in classes:
         c.native.reserve(c.n)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    out = fleet.run_coordinated(0.4, admm_iter_max=40, use_relative_tolerances=False,
-                                primal_tol=0.002, dual_tol=0.1)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
+    loop = _closed_loop(fleet, lambda: fleet.run_coordinated(0.4, admm_iter_max=40, use_relative_tolerances=False,
+                                                              primal_tol=0.002, dual_tol=0.1),
+                        args.admm_steps, 60.0, 5, world, dev)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         sample = bm.c2_fleet_classes(n_blocks=nb, N=10, seed=20261015 + 1, solver_options={"ipopt": {}})
@@ -407,9 +400,58 @@ def c2_admm_bench(args, world, rank, dev):
         "scaling": "strong", "blocks_total": nb, "rooms_total": 4 * nb, "agents_total": 5 * nb,
         "blocks_rank0": hi - lo if rank == 0 else None,
         "allreduce_doubles": fleet.reduce_len if world > 1 else 0,
-        **_block_summary(out, wall, 5, world, dev),
-        **_restorations(out["restorations"], world, dev),
+        **loop,
         "cpu_baseline": cpu,
+    }
+
+
+def _closed_loop(fleet, run, steps, ts, agents_per_block, world, dev):
+    """``steps`` control steps of a coordinated fleet, as the reference's coordinator runs
+    them (`admm_coordinator.py:259-321`): each step shifts means and multipliers by one
+    interval and iterates every block to its own stopping rule (or the iteration cap) from
+    the agents' resident warm starts; between the steps the synthetic plant moves every
+    zone to its predicted state at ``ts`` (``benchmarks.advance_plant``: new measurements,
+    untimed).  Each step is timed on its own (barrier + synchronize on both sides); the leg
+    reports the per-step figures and the median ADMM iterations/s over the steps."""
+    import torch
+    import torch.distributed as dist
+    from agentlib_mpc_amd import benchmarks as bm
+
+    per = []
+    rest = 0
+    for step in range(max(int(steps), 1)):
+        if step:
+            bm.advance_plant(fleet, ts)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        out = run()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        summ = _block_summary(out, wall, agents_per_block, world, dev)
+        summ["loop_iterations"] = out.get("loop_iterations")
+        per.append(summ)
+        rest += out["restorations"]
+    ips = [p["admm_iters_per_s"] for p in per]
+    return {
+        "control_steps": len(per),
+        "admm_iters_per_s": float(np.median(ips)),
+        "admm_iters_per_s_steps": ips,
+        "admm_iterations_steps": [p["admm_iterations"] for p in per],
+        "converged_block_fraction_steps": [p["converged_block_fraction"] for p in per],
+        "block_iterations_p50_max_steps": [p["block_iterations_p50_max"] for p in per],
+        "wall_s_steps": [p["wall_s"] for p in per],
+        "loop_iterations_steps": [p["loop_iterations"] for p in per],
+        "agent_solves_per_s": float(np.median([p["agent_solves_per_s"] for p in per])),
+        "converged_solve_fraction_steps": [p["converged_solve_fraction"] for p in per],
+        # the first step (cold start of every agent) in the fields the single-round leg reported
+        "admm_iterations": per[0]["admm_iterations"], "converged": per[0]["converged"],
+        "converged_block_fraction": per[0]["converged_block_fraction"],
+        "block_iterations_p50_max": per[0]["block_iterations_p50_max"],
+        **_restorations(rest, world, dev),
     }
 
 
@@ -498,16 +540,10 @@ def c5_admm_bench(args, world, rank, dev):
     fleet = ADMMFleet(classes, device=dev, comm="default" if world > 1 else None)
     for c in classes:
         c.native.reserve(c.n)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    out = fleet.run_coordinated(1.0, admm_iter_max=args.c5_iters, use_relative_tolerances=False,
-                                primal_tol=0.04, dual_tol=0.04)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
+    loop = _closed_loop(fleet, lambda: fleet.run_coordinated(1.0, admm_iter_max=args.c5_iters,
+                                                              use_relative_tolerances=False, primal_tol=0.04,
+                                                              dual_tol=0.04),
+                        args.admm_steps, 1800.0, 5, world, dev)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         sample = bm.c5_fleet_classes(n_blocks=nb, N=24, seed=20261015 + 5, solver_options=opts)
@@ -520,8 +556,7 @@ def c5_admm_bench(args, world, rank, dev):
                     "consensus, rho=1, N=24 ts=1800, abs tol 0.04/0.04, per-block stopping",
         "scaling": "strong", "blocks_total": nb, "zones_total": 3 * nb, "agents_total": 5 * nb,
         "blocks_rank0": hi - lo if rank == 0 else None,
-        **_block_summary(out, wall, 5, world, dev),
-        **_restorations(out["restorations"], world, dev),
+        **loop,
         "solver": "reference IPOPT defaults (casadi_utils.py:197-206)",
         "cpu_baseline": cpu,
     }
@@ -734,6 +769,8 @@ def main():
     ap.add_argument("--mhe-agents", type=int, default=4096, help="MHE estimators per GPU (0: skip)")
     ap.add_argument("--c2-blocks", type=int, default=1024,
                     help="C2 4-room+AHU blocks in total (1024 = the 4096-room fleet), split over the GPUs (0: skip)")
+    ap.add_argument("--admm-steps", type=int, default=5,
+                    help="closed-loop control steps of the coordinated legs (C2, C5), each to the stopping rule")
     ap.add_argument("--no-e2e", action="store_true", help="skip the plugin-API end-to-end leg and C1 latency")
     args = ap.parse_args()
 

@@ -484,3 +484,50 @@ def test_mixed_global_and_local_blocks_world2_matches_world1(tmp_path, tols, ite
         if want_iters is not None:
             it2 = np.load(f"{out}2.{r}.iters.npz")["iters"]
             assert it2[0] == want_iters[0] and (it2[1:] == want_iters[1]).all(), it2
+
+
+def test_device_stopping_test_reproduces_the_c2_coordinator_fixture_on_cpu():
+    """The coordinators' stopping test as the fleet runs it now -- on the device state
+    (``mpcx_admm_block_stop`` restated in numpy, `oracle/cpu_fleet.py`), the host reading the
+    active-block count every few iterations -- against the oracle coordinator's host loop
+    (`tests/golden/c2_admm_N10.json`: examples/4_Room_ADMM_Coordinator at its settings, N=10,
+    run to its stopping rule): same stopping iteration, residual and penalty history, means.
+    Local solves: the C IPM restatement at the fixture's settings."""
+    import json
+    from oracle.cpu_fleet import CpuFleetOps
+
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c2_admm_N10.json")))
+    for check_every in (1, 4, 7):
+        fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=gold["N"]), device="cpu",
+                       ops=CpuFleetOps(gold["solver"], threads=2))
+        out = fl.run_coordinated(gold["rho"], admm_iter_max=gold["admm_iter_max"], check_every=check_every,
+                                 **gold["criterion"])
+        assert out["iterations"] == gold["iterations"] and out["converged"] == gold["converged"]
+        assert out["loop_iterations"] - out["iterations"] < check_every
+        got = np.array([[r.primal_residual, r.dual_residual, r.penalty] for r in out["records"]])
+        np.testing.assert_allclose(got, np.array(gold["history"]), rtol=1e-5, atol=1e-9)
+        traj = fl.trajectories()
+        for al, mean in gold["means"].items():
+            np.testing.assert_allclose(traj[al], mean, rtol=1e-5, atol=1e-9)
+
+
+def test_closed_loop_plant_update_takes_the_predicted_state():
+    """``benchmarks.advance_plant`` (the coordinated bench legs' closed loop): after a round,
+    each room's next measurement is its predicted temperature one interval ahead, and the
+    uploaded NLP inputs equal a fresh marshalling of the rooms at those measurements."""
+    N = 2
+    classes = bm.c2_fleet_classes(n_blocks=1, N=N)
+    fl = ADMMFleet(classes, device="cpu", ops=_c2_ops(N))
+    fl.run_coordinated(0.4, admm_iter_max=2, use_relative_tolerances=False, primal_tol=1e-9, dual_tol=1e-9)
+    room = classes[0]
+    ts = room.backend.config.discretization_options.time_step
+    w = fl.solutions("room")
+    want_T = bm.value_at(room.backend.problem, w, "T", ts)
+    assert np.all(np.abs(want_T - np.array([t for _, t in bm.C2_ROOMS])) > 0)
+    bm.advance_plant(fl, ts)
+    cv, vals, _ = room.plant
+    np.testing.assert_array_equal(vals["T"], want_T)
+    p, lbw, ubw, _ = bm._class_inputs(room.backend, cv, {"T": want_T, "d": [d for d, _ in bm.C2_ROOMS]}, 4)
+    kp, kl, ku = room.to_kernel(p, lbw, ubw)
+    np.testing.assert_array_equal(room.P.numpy(), kp)
+    np.testing.assert_array_equal(room.LB.numpy(), kl)

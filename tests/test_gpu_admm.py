@@ -448,3 +448,47 @@ def test_gpu_c5_full_size_fleet_blocks_equal_their_own_runs():
             for i in range(3):
                 al = f"{pre}{i + 1}_b{b}"
                 np.testing.assert_allclose(tb[al], to[al], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("crit", [(0, 1e-3, 1e-3, 0.3, 0.2, -1.0, 2.0), (1, 0.05, 0.02, 1e-3, 1e-3, 1.5, 1.3)])
+def test_gpu_block_stop_matches_restatement(crit):
+    """``mpcx_admm_block_stop`` / ``mpcx_admm_block_expand`` against their numpy restatement
+    (`oracle/cpu_fleet.py`, the host coordinator's rule) on random residual totals of 700
+    blocks over 6 iterations: same freeze decisions and iteration counts, penalties, records
+    and active counts (absolute criterion; relative criterion with penalty variation)."""
+    from oracle.cpu_fleet import CpuFleetOps
+
+    rng = np.random.default_rng(3)
+    nb, its = 700, 6
+    ops_g, ops_c = NativeADMMOps(), CpuFleetOps()
+    state = {}
+    for name, dev in (("gpu", "cuda"), ("cpu", "cpu")):
+        f = lambda *a, **k: torch.zeros(*a, **k, device=dev)  # noqa: E731
+        state[name] = dict(rho=torch.full((nb, 1), 0.4, dtype=torch.float64, device=dev),
+                           act=torch.ones(nb, dtype=torch.int32, device=dev),
+                           it=torch.full((nb,), its, dtype=torch.int32, device=dev),
+                           rec=f(its * nb * 4, dtype=torch.float64), nact=f(its + 1, dtype=torch.int32),
+                           clk=f(its + 1, dtype=torch.int64))
+    idx = rng.integers(0, nb, 1500).astype(np.int32)
+    part = (rng.random(1500) < 0.9).astype(np.int32)
+    for it in range(1, its + 1):
+        tot = np.abs(rng.normal(size=(nb, 8))) * np.array([1e-5, 1e-2, 1, 1, 1, 30, 30, 1]) * rng.random((nb, 1))
+        for name, ops in (("gpu", ops_g), ("cpu", ops_c)):
+            s = state[name]
+            dev = "cuda" if name == "gpu" else "cpu"
+            ops.block_stop(it, torch.as_tensor(tot.ravel(), device=dev), crit, s["rho"], s["act"], s["it"], s["rec"],
+                           s["nact"], s["clk"])
+            out_a = torch.zeros(1500, dtype=torch.int32, device=dev)
+            out_r = torch.zeros(1500, dtype=torch.float64, device=dev)
+            ops.block_expand(torch.as_tensor(idx, device=dev), s["act"], s["rho"], torch.as_tensor(part, device=dev),
+                             out_a, out_r)
+            s["exp"] = (out_a.cpu().numpy(), out_r.cpu().numpy())
+        g, c = state["gpu"], state["cpu"]
+        for k in ("act", "it", "nact"):
+            np.testing.assert_array_equal(g[k].cpu().numpy(), c[k].cpu().numpy(), err_msg=k)
+        np.testing.assert_allclose(g["rho"].cpu().numpy(), c["rho"].numpy(), rtol=1e-15)
+        np.testing.assert_allclose(g["rec"].cpu().numpy(), c["rec"].numpy(), rtol=1e-14)
+        np.testing.assert_array_equal(g["exp"][0], c["exp"][0])
+        np.testing.assert_allclose(g["exp"][1], c["exp"][1], rtol=1e-15)
+    assert 0 < int(state["cpu"]["nact"][its]) < nb          # some blocks stopped, some did not
+    assert (state["gpu"]["clk"].cpu().numpy()[1:] >= state["gpu"]["clk"].cpu().numpy()[:-1]).all()

@@ -63,13 +63,6 @@ constexpr int MAXF = MPCX_MAXF;
 static_assert(MAXF >= 1 && MAXF <= 64, "the filter test reads one entry per lane");
 constexpr double INF_BOUND = 1e19;
 constexpr double TS = MPCX_TS;
-#ifdef MPCX_WS_LDS  // small-fleet variant: one agent per CU, its workspace in LDS
-#undef MPCX_MIN_WAVES
-#define MPCX_MIN_WAVES 1
-#endif
-#ifndef MPCX_MIN_WAVES
-#define MPCX_MIN_WAVES 4
-#endif
 
 // address-space qualified pointers: global_* / ds_* addressing inside the
 // noinline phases (generic pointers compile to flat_*, which drain both
@@ -525,6 +518,15 @@ struct Lds : LdsRest {
 };
 #ifndef MPCX_LDS_TARGET_OVERRIDE
 static_assert(sizeof(Lds) + LDS_SLACK <= LDS_CU / APC, "LDS share per agent exceeded");
+#endif
+// Waves per SIMD the LDS share allows (APC agents = APC one-wave workgroups per CU, 4 SIMDs):
+// the register budget of the kernel and of every phase it calls follows it -- 128 VGPRs at
+// 16 agents per CU, 512 at 4 (MHE: 480 -> 48 B/lane of call-frame scratch).  A tighter budget
+// than the occupancy needs only spills (MPCX_MIN_WAVES overrides, scripts/variants.py).
+#ifdef MPCX_MIN_WAVES
+constexpr int MIN_WAVES = MPCX_MIN_WAVES;
+#else
+constexpr int MIN_WAVES = (APC + 3) / 4;
 #endif
 
 __shared__ Lds gL;  // one agent per workgroup: the agent's LDS scratch
@@ -3543,7 +3545,7 @@ using namespace mpcx_kernel;
 // ---------------------------------------------------------------------------
 #define KOPT (((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())->opt)
 #define OPT(f) (*(volatile const __attribute__((address_space(4))) decltype(mpcx_options::f)*)&KOPT.f)
-extern "C" __global__ void __launch_bounds__(64, MPCX_MIN_WAVES) mpcx_ipm_solve(Args args) {
+extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args args) {
   const int agent = blockIdx.x;
   if (agent >= args.n_agents) return;
   if (args.active != nullptr && args.active[agent] == 0) return;  // frozen (converged ADMM block)

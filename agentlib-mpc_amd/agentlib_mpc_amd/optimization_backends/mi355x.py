@@ -141,8 +141,14 @@ class MI355XBackend(OptimizationBackend):
             self._resident.restart_cold()  # keep the device buffers, forget the optima
 
     def _native(self):
+        """The structure's native handle with this backend's solver options (uploaded to the
+        handle only when they differ from what it holds: a handle may serve several backends
+        of one structure, and re-setting every option costs ~30 us of ctypes calls)."""
         prob = self.problem.native
-        prob.set_options(**{k: v for k, v in self.solver_options.items()})
+        key = tuple(sorted(self.solver_options.items()))
+        if getattr(prob, "options_key", None) != key:
+            prob.set_options(**dict(self.solver_options))
+            prob.options_key = key
         return prob
 
     # -- solve (`core/casadi_backend.py:133-139`) --------------------------------

@@ -174,6 +174,11 @@ class ResidentBatch:
         from agentlib_mpc_amd.runtime.native import STATS_BYTES
 
         self.ST = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=device)
+        self._launch = None
+        if self.small and device.type == "cuda":
+            self._pin_w = torch.empty((n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)
+            self._pin_st = torch.empty(n * STATS_BYTES, dtype=torch.uint8, pin_memory=True)
+            self._d2h = torch.cuda.Event()
 
     # -- reading the agents' variables ---------------------------------------------------
     def read(self, batch_vars: Sequence[dict], now: float) -> Dict[tuple, object]:
@@ -413,13 +418,24 @@ class ResidentBatch:
         """Launch on the resident arrays (the solution replaces the guess in place); returns
         (w, raw stats) on the host."""
         torch = self.torch
-        self.native.solve(self.P, self.L, self.U, self.W, lam_g=self.lam_g, stats=self.ST)
-        w = torch.empty((self.n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)
-        w.copy_(self.W, non_blocking=True)
-        raw = self.ST.cpu().numpy()  # synchronises (w is complete too: same stream)
-        w = w.numpy()
+        if self._launch is None:  # the buffers are resident: checked once, pointers pre-bound
+            self._launch = self.native.bind(self.P, self.L, self.U, self.W, lam_g=self.lam_g, stats=self.ST)
+        self._launch()
         if self.small:
+            # persistent pinned buffers: both copies queued, one wait (a fresh pinned buffer and a
+            # blocking stats copy cost ~40 us per call, a tenth of a single agent's solve)
+            self._pin_w.copy_(self.W, non_blocking=True)
+            self._pin_st.copy_(self.ST, non_blocking=True)
+            self._d2h.record()
+            self._d2h.synchronize()
+            w = self._pin_w.numpy().copy()
+            raw = self._pin_st.numpy().copy()
             self.hW[:] = w  # the next call's warm start (uploaded with the inputs)
+        else:
+            w = torch.empty((self.n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)
+            w.copy_(self.W, non_blocking=True)
+            raw = self.ST.cpu().numpy()  # synchronises (w is complete too: same stream)
+            w = w.numpy()
         with np.errstate(invalid="ignore"):
             bad = np.flatnonzero(np.isnan(w.sum(axis=1)))
         self.cold_rows = bad if bad.size else None

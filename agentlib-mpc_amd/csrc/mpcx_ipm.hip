@@ -64,6 +64,16 @@ static_assert(MAXF >= 1 && MAXF <= 64, "the filter test reads one entry per lane
 constexpr double INF_BOUND = 1e19;
 constexpr double TS = MPCX_TS;
 
+// The phases of an IPM iteration are out-of-line calls in the fleet build (at 16 agents per CU
+// a phase inlined into the loop keeps its operands live across the others: spills); the
+// small-fleet build (one agent per CU, 512 VGPRs) inlines them into the kernel body, which
+// removes the call overhead and the callee-saved register traffic from the single wave's chain
+#ifdef MPCX_WS_LDS
+#define MPCX_HOT __attribute__((always_inline))
+#else
+#define MPCX_HOT __noinline__
+#endif
+
 // address-space qualified pointers: global_* / ds_* addressing inside the
 // noinline phases (generic pointers compile to flat_*, which drain both
 // counters and block load/store reordering)
@@ -678,7 +688,7 @@ __device__ __forceinline__ const double* par_global() { return (const double*)gL
 #endif
 
 // f and unscaled g at the trial point in LDS (xt -> gt); returns wave-summed f
-__device__ __noinline__ double eval_fg_lds(const Agent a) {
+__device__ MPCX_HOT double eval_fg_lds(const Agent a) {
   NET_PREP(gL.u.t.xt, fg);
   double f = 0.0;
   for (int k = lane_now(); k < N; k += WAVE) {
@@ -727,7 +737,7 @@ __device__ __attribute__((always_inline)) void eval_gj_lds(const Agent a) {
 // Hessian of sigma*f + sum lam_i * gs_i * g_i (scaled Lagrangian) into the packed
 // stage systems; the strided full Hessians (read only by the block-chain fallback)
 // are written when that path is in use, or on demand (eval_hess_full)
-__device__ __noinline__ void eval_hess_impl(const Agent a, double sigma, int full) {
+__device__ MPCX_HOT void eval_hess_impl(const Agent a, double sigma, int full) {
   NET_PREP(a.x(), hess);
   for (int k = lane_now(); k < N; k += WAVE) {
     double lk[NG > 0 ? NG : 1];
@@ -1345,7 +1355,7 @@ __device__ __noinline__ void local_assemble_generic(const Agent a, int k, int g,
 // + delta_w here; dual diagonal) are applied on the way.  DENSE: scattered into a zeroed
 // dense packed image (Bunch-Kaufman path), else the compact image itself (static path).
 template <int GG, bool DENSE>
-__device__ __noinline__ void local_assemble(const Agent a, int k, int g, ldsd* F, const KKTDiag kd) {
+__device__ MPCX_HOT void local_assemble(const Agent a, int k, int g, ldsd* F, const KKTDiag kd) {
   constexpr int EPC = (NCPT + GG - 1) / GG;  // compact entries per lane
   const unsigned long long fm = gL.fixm[k];
   const wdbl* src = a.lp(k);
@@ -1601,7 +1611,7 @@ __device__ __forceinline__ const double* s00(int k) { return (const double*)(gL.
 __device__ __forceinline__ const double* s11(int k) { return (const double*)(gL.S + k * SOFF + NXX); }
 __device__ __forceinline__ const double* s10(int k) { return (const double*)(gL.S + k * SOFF + NXX + NCC); }
 
-__device__ __noinline__ Inertia chain_factor(const Agent a) {
+__device__ MPCX_HOT Inertia chain_factor(const Agent a) {
   Lds& L = gL;
   Inertia in{0, 0, 0};
   const int lane = lane_now();
@@ -1666,7 +1676,7 @@ __device__ __noinline__ Inertia chain_factor(const Agent a) {
   return in;
 }
 
-__device__ __noinline__ void chain_solve(const Agent a) {
+__device__ MPCX_HOT void chain_solve(const Agent a) {
   Lds& L = gL;
   const int lane = lane_now();
   constexpr int ZS = NX + NC;  // zx stride per stage: [x_k | c_k]
@@ -1941,7 +1951,7 @@ __device__ __forceinline__ bool stage_was_dense(int k) {
 }
 
 // Newton step into gL.u.sol (block order per stage) from the last factorisation.
-__device__ __noinline__ void solve(const Agent a) {
+__device__ MPCX_HOT void solve(const Agent a) {
   Lds& L = gL;
   if (L.seq) { seq_solve(a); return; }
   SPROF_DECL
@@ -2187,7 +2197,7 @@ __device__ __noinline__ void ls_mult_finish(const Agent a, const double constr_m
 
 // full step from the Newton solution (LDS) + fraction-to-the-boundary step
 // sizes + constraint violation and barrier at the current point
-__device__ __noinline__ StepInfo recover_step(const Agent a, double mu, double tau, double dw, double obj_scale) {
+__device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, double dw, double obj_scale) {
   const int lane = lane_now();
   double amax = 1.0, az = 1.0, gphid = 0.0, theta = 0.0, bar = 0.0;
 #pragma unroll
@@ -2275,15 +2285,15 @@ struct LSOpt {  // line-search options by value (registers, not kernarg loads)
 
 // pow / log out of line: inlined into a loop that also calls a phase function, their
 // polynomial constants are hoisted into VGPRs that live across the call (scratch spills)
-__device__ __noinline__ double pow_ool(double x, double y) { return pow(x, y); }
-__device__ __noinline__ double log_ool(double x) { return log(x); }
+__device__ MPCX_HOT double pow_ool(double x, double y) { return pow(x, y); }
+__device__ MPCX_HOT double log_ool(double x) { return log(x); }
 
 // filter line search from the recovered step (gL.ks.st) into gL.ks.ls; trial points live
 // in LDS (xt, scaled gt).  The search state is kept in LDS too and nothing vector-sized
 // stays in registers across the evaluation call (a non-leaf function saves every
 // callee-saved VGPR it uses to scratch): the x-part of the barrier is summed while the
 // trial point is written, the constraint part is re-read after the call.
-__device__ __noinline__ void line_search(const Agent a) {
+__device__ MPCX_HOT void line_search(const Agent a) {
   KArgs* const argp = kargs();
   KState& K = gL.ks;
   {
@@ -2391,7 +2401,7 @@ __device__ __noinline__ void line_search(const Agent a) {
 }
 
 // take the last trial point (xt, gt in LDS) and the multiplier steps
-__device__ __noinline__ void accept_step(const Agent a, const double kappa_sigma, double mu, double alpha, double az) {
+__device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, double mu, double alpha, double az) {
   const int lane = lane_now();
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
@@ -3492,7 +3502,7 @@ __device__ __noinline__ int resto_tail(const Agent a) {
 // the step of an original-problem iteration: 0 line-search step, 1 soft step accepted by
 // the filter (taken like a line-search step), 2 soft step accepted by the error test
 // (already the iterate), -1 restoration phase started, -2 stop at an acceptable point
-__device__ __noinline__ int search_step(const Agent a) {
+__device__ MPCX_HOT int search_step(const Agent a) {
   KArgs* const argp = kargs();
   KState& K = gL.ks;
   int mode;

@@ -43,6 +43,17 @@ VARIANTS = {
     "o2": (["-O2"], None),
     # the kernel source of the last commit (A/B against the working tree)
     "head": ([], "HEAD"),
+    # the round-3 record kernel (b34f043) against the working tree (same headers)
+    "r03": ([], "REV:b34f043"),
+    # r04: the filter cap of round 3 (LDS share 512 B smaller)
+    "maxf32": (["-DMPCX_MAXF=32"], None),
+    # r04: the hot phases inlined into the fleet build too
+    "hot_inline": ([], ("#define MPCX_HOT __noinline__", "#define MPCX_HOT __attribute__((always_inline))")),
+    # small-fleet (workspace-in-LDS) builds, loaded through mpcx_problem_small_fleet (AGENTS <= CUs):
+    # r04 default (hot phases inlined) and with the phases out of line as in r03
+    "lds_base": (["-DMPCX_WS_LDS"], None),
+    "lds_noinl": (["-DMPCX_WS_LDS"], ("#define MPCX_HOT __attribute__((always_inline))", "#define MPCX_HOT __noinline__")),
+    "lds_r03": (["-DMPCX_WS_LDS"], "REV:b34f043"),
     # wave reductions as the __shfl_xor (ds_bpermute) butterfly instead of DPP + readlane
     "shfl": (["-DMPCX_SHFL_REDUCE=1"], None),
     # leaf phases inlined into the kernel body: no callee-saved VGPR saves per call
@@ -68,8 +79,9 @@ def build(names):
         kern = native.CSRC / "mpcx_ipm.hip"
         src_text = gen.source
         if tr is not None:
-            if tr == "HEAD":
-                ktxt = subprocess.run(["git", "-C", str(ROOT), "show", "HEAD:agentlib-mpc_amd/csrc/mpcx_ipm.hip"],
+            if isinstance(tr, str):
+                rev = "HEAD" if tr == "HEAD" else tr.split(":", 1)[1]
+                ktxt = subprocess.run(["git", "-C", str(ROOT), "show", f"{rev}:agentlib-mpc_amd/csrc/mpcx_ipm.hip"],
                                       capture_output=True, text=True, check=True).stdout
             else:
                 ktxt = kern.read_text()
@@ -114,7 +126,12 @@ def run(names):
     ref = None
     res = {}
     for name in names:
-        nat = NativeProblem(be.problem.gen, hsaco=vdir() / f"{name}.hsaco")
+        if name.startswith("lds"):  # a small-fleet build: loaded beside the default code object
+            nat = NativeProblem(be.problem.gen)
+            rc = nat.lib.mpcx_problem_small_fleet(nat.handle, str(vdir() / f"{name}.hsaco").encode(), -1)
+            assert rc == 0, (name, rc)
+        else:
+            nat = NativeProblem(be.problem.gen, hsaco=vdir() / f"{name}.hsaco")
         nat.set_options(tol=1e-8, max_iter=500)
         nat.reserve(n)
         tw = tw0.clone()

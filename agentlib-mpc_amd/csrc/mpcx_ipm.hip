@@ -68,10 +68,12 @@ constexpr double TS = MPCX_TS;
 // a phase inlined into the loop keeps its operands live across the others: spills); the
 // small-fleet build (one agent per CU, 512 VGPRs) inlines them into the kernel body, which
 // removes the call overhead and the callee-saved register traffic from the single wave's chain
+#ifndef MPCX_HOT  // (tests/test_native_abi.py compiles the phases out of line to inspect them)
 #ifdef MPCX_WS_LDS
 #define MPCX_HOT __attribute__((always_inline))
 #else
 #define MPCX_HOT __noinline__
+#endif
 #endif
 
 // address-space qualified pointers: global_* / ds_* addressing inside the

@@ -63,7 +63,9 @@ def test_small_fleet_build_keeps_hbm_addressing_off_the_lds_workspace(tmp_path):
     """In the small-fleet build the only global-memory stores are the kernel's outputs and the
     workspace's cold part: the phases that run every iteration (evaluators, elimination,
     line search, iteration head) address the LDS workspace with LDS instructions (a pointer
-    cast from the LDS workspace to an HBM type was a wild address on the GPU)."""
+    cast from the LDS workspace to an HBM type was a wild address on the GPU).  The build inlines
+    those phases into the kernel body; compiled out of line here (MPCX_HOT) they can be told
+    apart by function."""
     import re
     import subprocess
 
@@ -74,7 +76,8 @@ def test_small_fleet_build_keeps_hbm_addressing_off_the_lds_workspace(tmp_path):
     src.write_text(be.problem.gen.source)
     out = src.with_suffix(".s")
     subprocess.run([native._hipcc(), "--cuda-device-only", "-S", f"--offload-arch={native.OFFLOAD_ARCH}", "-O3",
-                    "-std=c++17", f"-I{native.INCLUDE}", f"-I{native.CSRC}", "-DMPCX_WS_LDS", str(src), "-o", str(out)],
+                    "-std=c++17", f"-I{native.INCLUDE}", f"-I{native.CSRC}", "-DMPCX_WS_LDS", "-DMPCX_HOT=__noinline__",
+                    str(src), "-o", str(out)],
                    check=True, capture_output=True)
     fn, stores = None, {}
     for line in out.read_text().splitlines():

@@ -480,14 +480,19 @@ class BatchMarshal:
 
     def result_matrices(self, p, lbw, ubw, w) -> np.ndarray:
         """[n, len(full grid), n_columns] result matrices from the NLP vectors (``lbw`` /
-        ``ubw``: the sampled bounds, see :meth:`inputs`)."""
+        ``ubw``: the sampled bounds, see :meth:`inputs`).  One gather from [p | w | lbw | ubw]
+        (the cell -> vector-entry map is built once; empty cells read a NaN entry)."""
         n = p.shape[0]
-        src = {"p": p, "w": w, "lbw": lbw, "ubw": ubw}
-        mat = np.full((n, self.n_rows, self.n_cols), np.nan)
-        for col, dim, rows, cols, key, index in self.blocks:
-            vals = src[key][:, index]                      # [n, dim, G]
-            mat[:, rows, col:col + dim] = np.transpose(vals[:, :, cols], (0, 2, 1))
-        return mat
+        if getattr(self, "_gather", None) is None or self._gather[0] != (p.shape[1], w.shape[1]):
+            npar, nw = p.shape[1], w.shape[1]
+            base = {"p": 0, "w": npar, "lbw": npar + nw, "ubw": npar + 2 * nw}
+            nan_at = npar + 3 * nw
+            idx = np.full((self.n_rows, self.n_cols), nan_at, np.int64)
+            for col, dim, rows, cols, key, index in self.blocks:
+                idx[rows, col:col + dim] = (base[key] + np.asarray(index)[:, cols]).T
+            self._gather = ((npar, nw), idx.ravel())
+        src = np.concatenate([p, w, lbw, ubw, np.full((n, 1), np.nan)], axis=1)
+        return src[:, self._gather[1]].reshape(n, self.n_rows, self.n_cols)
 
 
 class FleetResults(Sequence):

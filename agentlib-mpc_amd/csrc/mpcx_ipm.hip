@@ -1786,20 +1786,31 @@ __device__ __noinline__ void stage_tail(const Agent a, int k, int g, ldsd* F, co
 // in the slot's LDS image; returns 1 on a (numerically) singular static pivot, before
 // writing any output: the slot is then re-assembled and factored densely.
 template <bool STAGE0 = false>
-__device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* F) {
+__device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* Fl) {
   int in[3];
   asm volatile(";; STATIC_BEGIN");
   mpcx_elim_ld* const S = (mpcx_elim_ld*)LDSP(gL.S + k * SOFF);
   mpcx_elim_ld* const ZX = (mpcx_elim_ld*)LDSP(gL.zx + k * (NX + NC));
+#ifdef MPCX_ELIM_REG
+  // small-fleet build: the eliminating lane holds its stage image in registers (NCPT doubles;
+  // one wave per SIMD, 512 VGPRs), so the dependent pivot chain runs on registers instead of
+  // LDS round trips; the image is scratch (the outputs go to S, ZX and the operators)
+  double Fr[NCPT];
+#pragma unroll
+  for (int t = 0; t < NCPT; ++t) Fr[t] = Fl[t];
+  mpcx_elim_fd* const F = Fr;
+#else
+  mpcx_elim_fd* const F = (mpcx_elim_fd*)Fl;
+#endif
   int bad;
 #ifdef MPCX_STATIC_ELIM0
   // the generated body addresses the workspace with its own pointer types: they must be the
   // workspace's (an HBM-typed pointer into the LDS workspace would be a wild address)
   static_assert(__is_same(mpcx_elim_gd, wdbl) && __is_same(mpcx_elim_gi, wint), "workspace pointer types");
-  if constexpr (STAGE0) bad = gen_stage_elim0((mpcx_elim_ld*)F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
+  if constexpr (STAGE0) bad = gen_stage_elim0(F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
   else
 #endif
-    bad = gen_stage_elim((mpcx_elim_ld*)F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
+    bad = gen_stage_elim(F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
   asm volatile(";; STATIC_END");
   if (!bad) { atomicAdd(&gL.fin[0], in[0]); atomicAdd(&gL.fin[1], in[1]); }
   return bad;

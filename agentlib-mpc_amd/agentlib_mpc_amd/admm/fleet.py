@@ -48,6 +48,7 @@ from agentlib_mpc_amd.runtime.native import ADMM_TOTALS, STATS_BYTES, admm_reduc
 CONSENSUS = "consensus"
 EXCHANGE = "exchange"
 NMOM = 5
+_ITER_WORD = 12  # int32 index of mpcx_stats.iter_count
 _STATUS_WORD = 13  # int32 index of mpcx_stats.status (6 doubles + iter_count)
 _RESTO_WORD = 15  # int32 index of mpcx_stats.n_restorations
 
@@ -435,6 +436,10 @@ class ADMMFleet:
         self.X[:R].copy_(t.as_tensor(x0, device=dev))
         self._ok_count = t.zeros(1, dtype=t.int64, device=dev)
         self._fb_count = t.zeros(1, dtype=t.int64, device=dev)  # restoration-phase calls of the solves
+        #: a list to record every iteration's local-solve (iter_count, status) per class (device
+        #: copies, [n, 2] int32) -- the per-agent counterpart of the reference's per-solve stats;
+        #: None (the default) records nothing
+        self.solve_trace = None
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
@@ -496,6 +501,8 @@ class ADMMFleet:
                 # agents not participating keep their local (their rows map to the scratch row)
                 ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
             words = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)
+            if self.solve_trace is not None:
+                self.solve_trace.append((c.name, words[:, _ITER_WORD:_STATUS_WORD + 1].clone()))
             st = words[:, _STATUS_WORD]
             ok = (st == 0) | (st == 1)
             fb = words[:, _RESTO_WORD]

@@ -139,14 +139,20 @@ class ResidentBatch:
         p, lbw, ubw, w0, (ls, us) = m.inputs(batch_vars, now, None, return_sampled_bounds=True)
         self.base_p, self.base_ls, self.base_us = p[0].copy(), ls[0].copy(), us[0].copy()
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(device)  # noqa: E731
-        # P, L, U, W: contiguous blocks of ONE device buffer, so that a small batch uploads all
-        # of its inputs with one copy
-        sizes = [p.size, lbw.size, ubw.size, w0.size]
-        self.BUF = torch.empty(sum(sizes), dtype=torch.float64, device=device)
+        from agentlib_mpc_amd.runtime.native import STATS_BYTES
+
+        # P, L, U, W, stats: contiguous blocks of ONE device buffer, so that a small batch uploads
+        # all of its inputs with one copy and reads the solution and the stats back with one
+        st_words = -(-n * STATS_BYTES // 8)
+        sizes = [p.size, lbw.size, ubw.size, w0.size, st_words]
+        self.BUF = torch.zeros(sum(sizes), dtype=torch.float64, device=device)
         offs = np.concatenate([[0], np.cumsum(sizes)])
         views = [self.BUF[offs[i]:offs[i + 1]].view(a.shape) for i, a in enumerate((p, lbw, ubw, w0))]
         self.P, self.L, self.U, self.W = views
-        self.BUF.copy_(torch.from_numpy(np.concatenate([a.ravel() for a in (p, lbw, ubw, w0)])))
+        self.ST = self.BUF[offs[4]:].view(torch.uint8)[:n * STATS_BYTES]
+        self._out_off = int(offs[3])  # W and the stats: the tail the solve writes
+        self._buf_in = self.BUF[:offs[4]]  # what an upload writes
+        self._buf_in.copy_(torch.from_numpy(np.concatenate([a.ravel() for a in (p, lbw, ubw, w0)])))
         self.LS, self.US = T(ls), T(us)  # sampled bounds (before the parameter overrides)
         # small batches (the reference's one agent per process): the inputs are kept on the
         # host too and updated there (numpy), then uploaded in one copy -- a handful of device
@@ -160,6 +166,7 @@ class ResidentBatch:
             self.hP, self.hL, self.hU, self.hW = [self.hbuf[offs[i]:offs[i + 1]].reshape(a.shape)
                                                   for i, a in enumerate((p, lbw, ubw, w0))]
             self.hbuf[:] = self.BUF.cpu().numpy()
+            self._hbuf_in = self.hbuf_t[:offs[4]]
             self.hLS, self.hUS = ls.copy(), us.copy()
             self.over_h = {k: (c, q) for k, (c, q) in m.over.items() if c.size}
         self.idx = {}
@@ -173,13 +180,9 @@ class ResidentBatch:
         self.last: Dict[tuple, object] = self.read(batch_vars, now)
         self.cold_rows: Optional[np.ndarray] = None
         self.lam_g = torch.empty((n, prob.nlp.kernel_ng), dtype=torch.float64, device=device)
-        from agentlib_mpc_amd.runtime.native import STATS_BYTES
-
-        self.ST = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device=device)
         self._launch = None
         if self.small and device.type == "cuda":
-            self._pin_w = torch.empty((n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)
-            self._pin_st = torch.empty(n * STATS_BYTES, dtype=torch.uint8, pin_memory=True)
+            self._pin_out = torch.empty(self.BUF.numel() - self._out_off, dtype=torch.float64, pin_memory=True)
             self._d2h = torch.cuda.Event()
 
     # -- reading the agents' variables ---------------------------------------------------
@@ -351,7 +354,7 @@ class ResidentBatch:
         if self.cold_rows is not None and self.cold_rows.size:
             self.hW[self.cold_rows] = self._cold_guess(self.cold_rows)
             self.cold_rows = None
-        self.BUF.copy_(self.hbuf_t, non_blocking=True)
+        self._buf_in.copy_(self._hbuf_in, non_blocking=True)
         if self.dev.type == "cuda":
             self._h2d = self.torch.cuda.Event()
             self._h2d.record()
@@ -438,14 +441,15 @@ class ResidentBatch:
             self._launch = self.native.bind(self.P, self.L, self.U, self.W, lam_g=self.lam_g, stats=self.ST)
         self._launch()
         if self.small:
-            # persistent pinned buffers: both copies queued, one wait (a fresh pinned buffer and a
-            # blocking stats copy cost ~40 us per call, a tenth of a single agent's solve)
-            self._pin_w.copy_(self.W, non_blocking=True)
-            self._pin_st.copy_(self.ST, non_blocking=True)
+            # a persistent pinned buffer: solution and stats in one copy, one wait (a fresh pinned
+            # buffer and a blocking stats copy cost ~40 us per call, a tenth of a single agent's solve)
+            self._pin_out.copy_(self.BUF[self._out_off:], non_blocking=True)
             self._d2h.record()
             self._d2h.synchronize()
-            w = self._pin_w.numpy().copy()
-            raw = self._pin_st.numpy().copy()
+            out = self._pin_out.numpy()
+            nw = self.hW.size
+            w = out[:nw].reshape(self.hW.shape).copy()
+            raw = out[nw:].view(np.uint8)[:self.ST.numel()].copy()
             self.hW[:] = w  # the next call's warm start (uploaded with the inputs)
         else:
             w = torch.empty((self.n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)

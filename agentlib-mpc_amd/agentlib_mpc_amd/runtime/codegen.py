@@ -506,16 +506,8 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
         "#define MPCX_ELIM_FENCE __builtin_amdgcn_sched_barrier(0)",
         "#endif",
         "typedef __attribute__((address_space(3))) double mpcx_elim_ld;",
-        "// the stage image the elimination works on: LDS, or (small-fleet build, one wave per SIMD with",
-        "// 512 registers) a register array the eliminating lane loads it into (mpcx_ipm.hip static_stage).",
-        "// Above 96 stage entries the image no longer fits beside the kernel's live state: the r04 gfx950",
-        "// builds spill 12-97 VGPRs at NCPT 106..202 with it and none at NCPT 67, so large stages stay in LDS.",
-        "#if defined(MPCX_WS_LDS) && !defined(MPCX_ELIM_NOREG) && MPCX_NCPT <= 96",
-        "#define MPCX_ELIM_REG 1",
-        "typedef double mpcx_elim_fd;",
-        "#else",
-        "typedef __attribute__((address_space(3))) double mpcx_elim_fd;",
-        "#endif",
+        "// F: the stage image the elimination works on -- LDS, or a register array the eliminating lane\n"
+        "// loads it into (mpcx_ipm.hip static_stage, ELIM_REG)",
         "#ifdef MPCX_WS_LDS  // small-fleet build: the workspace (operators, pivot order) is in LDS",
         "typedef __attribute__((address_space(3))) double mpcx_elim_gd;",
         "typedef __attribute__((address_space(3))) int mpcx_elim_gi;",
@@ -523,7 +515,7 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
         "typedef __attribute__((address_space(1))) double mpcx_elim_gd;",
         "typedef __attribute__((address_space(1))) int mpcx_elim_gi;",
         "#endif",
-        "__device__ __forceinline__ int gen_stage_elim(mpcx_elim_fd* __restrict__ F, mpcx_elim_ld* __restrict__ S, mpcx_elim_ld* __restrict__ ZX, mpcx_elim_gd* __restrict__ TR, mpcx_elim_gi* __restrict__ PRM, int* __restrict__ inert) {",
+        "template <typename FD> __device__ __forceinline__ int gen_stage_elim(FD* __restrict__ F, mpcx_elim_ld* __restrict__ S, mpcx_elim_ld* __restrict__ ZX, mpcx_elim_gd* __restrict__ TR, mpcx_elim_gi* __restrict__ PRM, int* __restrict__ inert) {",
         "  int bad = 0, pos = 0, neg = 0;",
         *elim_lines,
         "  inert[0] = pos; inert[1] = neg; inert[2] = 0;",
@@ -532,7 +524,7 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
         *([f"// stage 0: {len(elim0_plan.blocks)} pivot blocks, {elim0_plan.n_update} interior updates "
            f"(rows open at k = 0 are 1x1 pivots)",
            "#define MPCX_STATIC_ELIM0 1",
-           "__device__ __forceinline__ int gen_stage_elim0(mpcx_elim_fd* __restrict__ F, mpcx_elim_ld* __restrict__ S, mpcx_elim_ld* __restrict__ ZX, mpcx_elim_gd* __restrict__ TR, mpcx_elim_gi* __restrict__ PRM, int* __restrict__ inert) {",
+           "template <typename FD> __device__ __forceinline__ int gen_stage_elim0(FD* __restrict__ F, mpcx_elim_ld* __restrict__ S, mpcx_elim_ld* __restrict__ ZX, mpcx_elim_gd* __restrict__ TR, mpcx_elim_gi* __restrict__ PRM, int* __restrict__ inert) {",
            "  int bad = 0, pos = 0, neg = 0;",
            *elim0_lines,
            "  inert[0] = pos; inert[1] = neg; inert[2] = 0;",

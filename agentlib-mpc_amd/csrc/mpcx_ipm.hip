@@ -1785,32 +1785,49 @@ __device__ __noinline__ void stage_tail(const Agent a, int k, int g, ldsd* F, co
 // back-substitution operators that interior_bk + stage_tail would.  Eliminates in place
 // in the slot's LDS image; returns 1 on a (numerically) singular static pivot, before
 // writing any output: the slot is then re-assembled and factored densely.
+// The eliminating lane works on a register image of the stage (NCPT doubles) where the register
+// budget holds it, so the dependent pivot chain runs on registers instead of LDS round trips (the
+// image is scratch: the outputs go to S, ZX and the operators).  Measured on gfx950 (r04,
+// profiles/r04/s3): small-fleet builds (one wave per SIMD) spill 12-97 VGPRs with it at NCPT
+// 106..202 and none at 67 -> NCPT <= 96 there; fleet builds at one wave per SIMD (MHE, 4 agents
+// per CU) 9.74 -> 9.38 ms with scratch 48 -> 128 B/lane; at 4 waves per SIMD (C3, 128 VGPRs) it
+// spills 540 B/lane, 2.02 -> 2.43 ms, so those keep the LDS image.
+#if defined(MPCX_ELIM_NOREG)
+constexpr bool ELIM_REG = false;
+#elif defined(MPCX_ELIM_FORCE_REG)
+constexpr bool ELIM_REG = true;
+#elif defined(MPCX_WS_LDS)
+constexpr bool ELIM_REG = NCPT <= 96;
+#else
+constexpr bool ELIM_REG = MIN_WAVES == 1;
+#endif
+
+template <bool STAGE0, typename FD>
+__device__ __forceinline__ int static_body(const Agent a, int k, FD* F, mpcx_elim_ld* S, mpcx_elim_ld* ZX, int* in) {
+#ifdef MPCX_STATIC_ELIM0
+  // the generated body addresses the workspace with its own pointer types: they must be the
+  // workspace's (an HBM-typed pointer into the LDS workspace would be a wild address)
+  static_assert(__is_same(mpcx_elim_gd, wdbl) && __is_same(mpcx_elim_gi, wint), "workspace pointer types");
+  if constexpr (STAGE0) return gen_stage_elim0(F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
+#endif
+  return gen_stage_elim(F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
+}
+
 template <bool STAGE0 = false>
 __device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* Fl) {
   int in[3];
   asm volatile(";; STATIC_BEGIN");
   mpcx_elim_ld* const S = (mpcx_elim_ld*)LDSP(gL.S + k * SOFF);
   mpcx_elim_ld* const ZX = (mpcx_elim_ld*)LDSP(gL.zx + k * (NX + NC));
-#ifdef MPCX_ELIM_REG
-  // small-fleet build: the eliminating lane holds its stage image in registers (NCPT doubles;
-  // one wave per SIMD, 512 VGPRs), so the dependent pivot chain runs on registers instead of
-  // LDS round trips; the image is scratch (the outputs go to S, ZX and the operators)
-  double Fr[NCPT];
-#pragma unroll
-  for (int t = 0; t < NCPT; ++t) Fr[t] = Fl[t];
-  mpcx_elim_fd* const F = Fr;
-#else
-  mpcx_elim_fd* const F = (mpcx_elim_fd*)Fl;
-#endif
   int bad;
-#ifdef MPCX_STATIC_ELIM0
-  // the generated body addresses the workspace with its own pointer types: they must be the
-  // workspace's (an HBM-typed pointer into the LDS workspace would be a wild address)
-  static_assert(__is_same(mpcx_elim_gd, wdbl) && __is_same(mpcx_elim_gi, wint), "workspace pointer types");
-  if constexpr (STAGE0) bad = gen_stage_elim0(F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
-  else
-#endif
-    bad = gen_stage_elim(F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
+  if constexpr (ELIM_REG) {
+    double Fr[NCPT];
+#pragma unroll
+    for (int t = 0; t < NCPT; ++t) Fr[t] = Fl[t];
+    bad = static_body<STAGE0>(a, k, Fr, S, ZX, in);
+  } else {
+    bad = static_body<STAGE0>(a, k, (mpcx_elim_ld*)Fl, S, ZX, in);
+  }
   asm volatile(";; STATIC_END");
   if (!bad) { atomicAdd(&gL.fin[0], in[0]); atomicAdd(&gL.fin[1], in[1]); }
   return bad;

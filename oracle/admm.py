@@ -158,7 +158,7 @@ class _Exchange:
 def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max, primal_tol=1e-3,
                       dual_tol=1e-3, use_relative_tolerances=True, abs_tol=1e-3, rel_tol=1e-3,
                       penalty_change_threshold=-1.0, penalty_change_factor=2.0, T=None, state=None,
-                      solve_batch=None, active=None):
+                      solve_batch=None, active=None, trace=None):
     """One round of ``ADMMCoordinator._fast_process`` (`admm_coordinator.py:259-321`).
 
     participation: {agent: {alias: "consensus"|"exchange"}}; initial: {agent: {alias: value}}
@@ -168,6 +168,7 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
     active (optional): the agents with status ``ready`` this round (`admm_coordinator.py:
     323-353`); only they are solved and enter means, multiplier updates and the residual
     scalings (``sources=active_agents``); None: every registered agent.
+    trace (optional list): gets {alias: mean} after every iteration's mean update.
     Returns (state, history [(primal, dual, rho after the variation)], iterations, converged).
     """
     if state is None:  # registration (`admm_coordinator.py:528-560`)
@@ -208,6 +209,8 @@ def coordinated_round(participation, initial, solve, rho, horizon, admm_iter_max
             v.update_mean(active)
         for v in vars_.values():
             v.update_multipliers(rho, active)
+        if trace is not None:
+            trace.append({al: [float(x) for x in v.mean] for al, v in vars_.items()})
         prim, dual, flat_locals, flat_means, flat_mult = [], [], [], [], []
         for v in vars_.values():
             prim.extend(v.primal_residual.flatten())

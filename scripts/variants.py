@@ -59,6 +59,10 @@ VARIANTS = {
     # leaf phases inlined into the kernel body: no callee-saved VGPR saves per call
     "inl_gj": ([], ("__device__ __noinline__ void eval_gj_lds(", "__device__ __attribute__((always_inline)) void eval_gj_lds(")),
     "inl_head": ([], ("__device__ __noinline__ int iter_head(const Agent a)", "__device__ __attribute__((always_inline)) int iter_head(const Agent a)")),
+    # r04: the static elimination on a register image of the stage in the fleet build too
+    "elimreg": (["-DMPCX_ELIM_FORCE_REG"], None),
+    "elimreg_w1": (["-DMPCX_ELIM_FORCE_REG", "-DMPCX_MIN_WAVES=1"], None),
+    "lds_noreg": (["-DMPCX_WS_LDS", "-DMPCX_ELIM_NOREG"], None),
 }
 
 

@@ -23,6 +23,7 @@ class _Solver:
     def __init__(self):
         self.last = {}
         self.failed = 0
+        self.log = []  # (agent, status, iterations) of every local solve, in call order
 
     def _run(self, key, prob, p, lbw, ubw, w0):
         guess = self.last.get(key)
@@ -39,6 +40,7 @@ class _Solver:
         if not self.allow_failed:
             assert r.success, (key, r.status)
         self.failed += 0 if r.success else 1
+        self.log.append((key, r.status, int(r.iterations)))
         self.last[key] = r.x
         return r.x
 

@@ -3,9 +3,9 @@
 * ``c2_admm_N10.json`` — examples/4_Room_ADMM_Coordinator (4 rooms + air handler, collocation
   d=3, N=10, ts=60, rho=0.4, absolute criterion 0.002 / 0.1, admm_iter_max 40;
   `configs/coordinator.json:7-18`) run to its stopping rule;
-* ``c5_admm_N24.json`` — examples/three_zone_datadriven_admm (3 NARX zones + AHU + CCA,
-  N=24, ts=1800, rho=1, absolute criterion 0.04 / 0.04, admm_iter_max 50;
-  `configs/coordinator.json:5-20`) at the config horizon;
+* ``c5_admm_N8.json`` / ``c5_admm_N24.json`` — examples/three_zone_datadriven_admm (3 NARX zones + AHU + CCA,
+  N=8 and the config horizon N=24, ts=1800, rho=1, absolute criterion 0.04 / 0.04, admm_iter_max 50;
+  `configs/coordinator.json:5-20`);
 * ``c2_admm_N10_b3.json`` — block 3 of the bench's scaled C2 fleet (synthetic rooms drawn as
   ``benchmarks.c2_fleet_classes(seed=20261015 + 1)`` draws them), same coordinator settings,
   local solves at the reference's IPOPT settings (tol 1e-4, acceptable level 0.1 over 5
@@ -17,7 +17,7 @@ coordinator-loop restatement ``oracle.admm.coordinated_round``.  The agents of o
 iteration are solved in parallel, one worker process per agent (each keeps its own warm
 start, as the reference backend does).  Minutes of CPU, hence committed fixtures.
 
-Run from the repository root: ``python tests/golden/make_admm_goldens.py [c2] [c5] [c2b3]``.
+Run from the repository root: ``python tests/golden/make_admm_goldens.py [c2] [c5n8] [c5] [c2b3]``.
 """
 import json
 import multiprocessing as mp
@@ -77,7 +77,8 @@ def _worker(kind, N, conn, block=None):
             conn.send(orc.failed)  # local solves that stopped unsuccessfully
             break
         ag, inp, rho = msg
-        conn.send(orc(ag, inp, rho))
+        out = orc(ag, inp, rho)
+        conn.send((out, orc.log[-1][1:]))
 
 
 def run(kind, N, rho, iters, block=None, **crit):
@@ -92,17 +93,22 @@ def run(kind, N, rho, iters, block=None, **crit):
         pipes[ag] = a
         procs.append(p)
 
+    solves = []  # per ADMM iteration: {agent: [status, IPM iterations]}
+
     def solve_batch(reqs, rho_):
         for ag, inp in reqs:
             pipes[ag].send((ag, inp, rho_))
-        return [pipes[ag].recv() for ag, _ in reqs]
+        got = [pipes[ag].recv() for ag, _ in reqs]
+        solves.append({ag: list(r[1]) for (ag, _), r in zip(reqs, got)})
+        return [r[0] for r in got]
 
     from oracle import admm as oadmm
 
     t0 = time.time()
     T = 3 * N if kind == "c2" else N
+    trace = []
     state, hist, it, conv = oadmm.coordinated_round(orc.participation, orc.initial, None, rho, N, iters,
-                                                    T=T, solve_batch=solve_batch, **crit)
+                                                    T=T, solve_batch=solve_batch, trace=trace, **crit)
     failed = {}
     for ag in agents:
         pipes[ag].send(None)
@@ -113,12 +119,14 @@ def run(kind, N, rho, iters, block=None, **crit):
            "solver": dict(orc.options) if orc.options else {"tol": orc.tol, "acceptable_iter": 0, "max_iter": 500},
            "failed_local_solves": failed,
            "history": [[float(a), float(b), float(c)] for a, b, c in hist],
-           "means": {al: list(map(float, v.mean)) for al, v in state["vars"].items()}}
+           "means": {al: list(map(float, v.mean)) for al, v in state["vars"].items()},
+           # per iteration: every agent's local solve (status, IPM iterations) and the means after it
+           "local_solves": solves, "mean_history": trace}
     if block is not None:
         out["block"], out["seed"] = block, C2_FLEET_SEED
     path = os.path.join(HERE, f"{kind}_admm_N{N}" + (f"_b{block}" if block is not None else "") + ".json")
     with open(path, "w") as f:
-        json.dump(out, f, indent=1)
+        json.dump(out, f, separators=(",", ":"))
     print(path, f"{it} iterations, converged={conv}, {time.time() - t0:.0f}s", flush=True)
 
 
@@ -128,5 +136,7 @@ if __name__ == "__main__":
         run("c2", 10, 0.4, 40, primal_tol=0.002, dual_tol=0.1, use_relative_tolerances=False)
     if "c2b3" in which:  # a block of the bench's scaled fleet that stalls above the primal tolerance
         run("c2", 10, 0.4, 40, block=3, primal_tol=0.002, dual_tol=0.1, use_relative_tolerances=False)
+    if "c5n8" in which:
+        run("c5", 8, 1.0, 50, primal_tol=0.04, dual_tol=0.04, use_relative_tolerances=False)
     if "c5" in which:
         run("c5", 24, 1.0, 50, primal_tol=0.04, dual_tol=0.04, use_relative_tolerances=False)

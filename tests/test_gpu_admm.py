@@ -176,40 +176,75 @@ def test_gpu_participation_and_registration_match_oracle():
                                        state["vars"][al].mult["ahu"], rtol=RTOL, atol=1e-8)
 
 
+def _fleet_local_iterations(fl, n_iter):
+    """Per ADMM iteration: every agent's local-solve IPM iteration count ({agent: n}) from the
+    fleet's ``solve_trace`` (agent names as the oracle's C5 participation: zone0-2, ahu, cca)."""
+    k = len(fl.classes)
+    out = []
+    for it in range(n_iter):
+        row = {}
+        for name, w in fl.solve_trace[it * k:(it + 1) * k]:
+            w = w.cpu().numpy()
+            for i in range(w.shape[0]):
+                row[f"{name}{i}" if name == "zone" else name] = int(w[i, 0])
+        out.append(row)
+    return out
+
+
 @pytest.mark.parametrize("N", [8, 24])
 def test_gpu_three_zone_narx_fleet_matches_oracle_fixture(N):
     """examples/three_zone_datadriven_admm: 3 NARX zones + AHU + CCA (networks trained as
     the example trains them, `models/data/`), coordinated ADMM, rho=1, absolute criterion
     0.04/0.04, to the example's stopping rule (admm_iter_max 50), at N=8 and at the
     example's horizon N=24, against the oracle's round (`tests/golden/c5_admm_N{8,24}.json`,
-    `tests/golden/make_c5_admm_golden.py`: hand-restated NLPs, oracle IPM and coordinator;
-    both at tol 1e-8): residual history to the stopping iteration and the final means."""
+    `tests/golden/make_admm_goldens.py`: hand-restated NLPs, oracle IPM and coordinator;
+    both at tol 1e-8).
+
+    The supply agents' costs are nearly non-smooth (sqrt(W^2 + 0.02) at objective scale ~1e6):
+    their local solves end at the fp64 noise floor of tol 1e-8, so their IPM iteration counts
+    differ between the two sides from the first iterations on while the solutions agree to
+    ~1e-10 (scripts/c5_counts.py, profiles/r04/s3/c5_counts_n8.txt), and at some iteration one of
+    them stops at a nearby point and the consensus paths part; which iteration depends on
+    rounding.  That iteration is found from the data -- the first whose residuals differ from
+    the oracle's by more than 1e-6 relative -- and must not come before iteration 10; up to it
+    the zones' local IPM iteration counts (deterministic) equal the oracle's.  After it: the
+    stopping outcome, the residual levels of the last ten iterations (within 3x), and the final
+    consensus means inside a band sized from the oracle's own sensitivity (how far its means
+    still move after the divergence iteration)."""
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", f"c5_admm_N{N}.json")))
     opts = {"ipopt": {"tol": 1e-8, "max_iter": 500, "acceptable_iter": 0}}
     fl = ADMMFleet(bm.c5_fleet_classes(n_blocks=1, N=gold["N"], solver_options=opts))
+    fl.solve_trace = []
     out = fl.run_coordinated(gold["rho"], admm_iter_max=gold.get("admm_iter_max", 50),
-                             use_relative_tolerances=False, primal_tol=0.04, dual_tol=0.04)
+                             use_relative_tolerances=False, primal_tol=0.04, dual_tol=0.04, check_every=1)
     assert out["iterations"] == gold["iterations"] and out["converged"] == gold["converged"]
     got = np.array([[r.primal_residual, r.dual_residual] for r in out["records"]])
     want = np.array(gold["history"])[:, :2]
     rel = np.max(np.abs(got - want) / np.maximum(np.abs(want), 1e-3), axis=1)
-    print("C5 N=%d per-iteration relative residual difference:" % N, np.array2string(rel, precision=2))
-    # the runs agree to ~1e-10 until one local solve of the supply agents -- nearly non-smooth
-    # costs, sqrt(W^2 + 0.02) at objective scale ~1e6 -- takes another line-search path (a soft
-    # or full restoration on one side, scripts/c5_diverge.py, profiles/r03/s3/c5_diverge_*.txt)
-    # and stops at a nearby point; which iteration that is depends on rounding (12 in one
-    # build, 44 in the next).  From there the consensus paths differ by up to ~50 % on the
-    # small primal residuals while the outcome stays: the prefix is compared tightly, the rest
-    # by the stopping outcome and the level of the dual residual that blocks convergence.
-    tight = min(len(want), 11)
-    np.testing.assert_allclose(got[:tight], want[:tight], rtol=RTOL, atol=1e-8)
-    if len(want) > tight:
-        ratio = got[tight:, 1] / want[tight:, 1]
-        assert np.all((ratio > 1 / 3) & (ratio < 3)), ratio
-    if len(want) == gold["admm_iter_max"] and tight == len(want):
-        traj = fl.trajectories()
+    div = int(np.argmax(rel > 1e-6)) if np.any(rel > 1e-6) else len(want)
+    print(f"C5 N={N}: residual histories part at iteration {div + 1} of {len(want)}")
+    print("per-iteration relative residual difference:", np.array2string(rel, precision=2))
+    assert div >= 10, (div, rel[:div + 1])
+    kits = _fleet_local_iterations(fl, div)
+    for k in range(div):
+        zones = {ag: n for ag, n in kits[k].items() if ag.startswith("zone")}
+        assert zones == {ag: gold["local_solves"][k][ag][1] for ag in zones}, (k, zones, gold["local_solves"][k])
+    traj = fl.trajectories()
+    if div == len(want):
         for al, mean in gold["means"].items():
             np.testing.assert_allclose(traj[al], mean, rtol=RTOL, atol=1e-6)
+        return
+    tail = slice(max(div, len(want) - 10), len(want))
+    for col in (0, 1):
+        ratio = np.median(got[tail, col]) / np.median(want[tail, col])
+        assert 1 / 3 < ratio < 3, (col, ratio)
+    hist = gold["mean_history"]
+    for al, mean in gold["means"].items():
+        mean = np.asarray(mean)
+        drift = max(np.max(np.abs(np.asarray(h[al]) - mean)) for h in hist[div:])
+        dev = np.max(np.abs(traj[al] - mean))
+        print(f"  {al}: |gpu - oracle| {dev:.3g}, oracle drift after iteration {div + 1}: {drift:.3g}")
+        assert dev <= 3 * drift + 1e-6, (al, dev, drift)
 
 
 def test_gpu_fleet_blocks_are_independent():

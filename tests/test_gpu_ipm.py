@@ -398,7 +398,9 @@ def test_gpu_small_fleet_build_matches_hbm_build():
     """The small-fleet build (workspace in LDS, one agent per CU; ``mpcx_problem_small_fleet``,
     used for batches of at most one agent per CU) against the HBM-workspace build on the same
     200 C3 agents at the reference's settings: same status and iteration count per agent, same
-    solutions (the arithmetic is the same; only the memory the workspace lives in differs)."""
+    solutions (the operations are the same; the memory the workspace lives in differs, and small
+    stages are eliminated on a register image of the stage, where the compiler
+    contracts some products into FMAs differently: objectives agree to 1e-10)."""
     import bench
     from agentlib_mpc_amd import benchmarks as bm
     from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
@@ -424,4 +426,4 @@ def test_gpu_small_fleet_build_matches_hbm_build():
     assert [s["iter_count"] for s in sl] == [s["iter_count"] for s in sh]
     assert np.mean([s["status"] in (0, 1) for s in sl]) > 0.99
     np.testing.assert_allclose(wl, wh, rtol=1e-12, atol=1e-12)
-    np.testing.assert_allclose([s["obj"] for s in sl], [s["obj"] for s in sh], rtol=1e-12)
+    np.testing.assert_allclose([s["obj"] for s in sl], [s["obj"] for s in sh], rtol=1e-10)

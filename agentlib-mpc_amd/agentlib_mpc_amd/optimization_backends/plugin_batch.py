@@ -176,6 +176,7 @@ class ResidentBatch:
         self.over = {k: (torch.as_tensor(c, device=device), torch.as_tensor(q, device=device))
                      for k, (c, q) in m.over.items() if c.size}
         self._prev_buf = None
+        self._cold_plan = None
         self._unchanged = set()
         self.last: Dict[tuple, object] = self.read(batch_vars, now)
         self.cold_rows: Optional[np.ndarray] = None
@@ -373,24 +374,39 @@ class ResidentBatch:
         """The cold-start guess of some agents (``BatchMarshal.assemble`` with no previous
         optimum, `core/discretization.py:212-245`) from the host mirrors: states tiled from
         their measured initial value, other variables at the midpoint of their sampled bounds
-        (infinite -> 0), then the guesses taken from parameters."""
-        m = self.marshal
-        P, LS, US = self.hP[rows], self.hLS[rows], self.hUS[rows]
+        (infinite -> 0), then the guesses taken from parameters.  The column maps are built once
+        (three gathers per call: the per-variable loop cost ~0.1 ms, a fifth of a single agent's
+        solve)."""
+        if self._cold_plan is None:
+            m = self.marshal
+            dst_a, src_a, mid = [], [], []
+            for name, grid, _, index in m.vars:
+                if index is None:
+                    continue
+                flat = index.ravel()
+                if name in m.initial:
+                    cols = m.initial[name][:, -1]
+                    dst_a.append(flat)
+                    src_a.append(np.repeat(cols[:, None], len(grid), axis=1).reshape(-1))
+                else:
+                    mid.append(flat)
+            cat = lambda parts: np.concatenate(parts).astype(np.int64) if parts else np.zeros(0, np.int64)  # noqa
+            self._cold_plan = (cat(dst_a), cat(src_a), cat(mid))
+        dst_a, src_a, mid = self._cold_plan
+        P = self.hP[rows]
         g = np.zeros((len(rows), self.hW.shape[1]))
-        for name, grid, _, index in m.vars:
-            if index is None:
-                continue
-            flat = index.ravel()
-            if name in m.initial:
-                meas = P[:, m.initial[name][:, -1]]                      # [r, dim]
-                g[:, flat] = np.repeat(meas[:, :, None], len(grid), axis=2).reshape(len(rows), -1)
-            else:
-                with np.errstate(invalid="ignore"):
-                    g[:, flat] = np.nan_to_num(0.5 * (LS[:, flat] + US[:, flat]), posinf=0, neginf=-0)
+        g[:, dst_a] = P[:, src_a]
+        ix = np.ix_(rows, mid)
+        with np.errstate(invalid="ignore"):
+            v = 0.5 * (self.hLS[ix] + self.hUS[ix])
+        bad = ~np.isfinite(v)
+        if bad.any():  # nan_to_num(posinf=0, neginf=-0)
+            v[bad] = np.where(v[bad] < 0, -0.0, 0.0)
+        g[:, mid] = v
         if "guess" in self.over_h:
             c, q = self.over_h["guess"]
             g[:, c] = P[:, q]
-        return np.nan_to_num(g)
+        return g if np.isfinite(g).all() else np.nan_to_num(g)
 
     # -- warm starts keyed by agent (MI355XBackend.solve_batch agent_ids) ---------------
     def permute_warm_starts(self, src: np.ndarray):

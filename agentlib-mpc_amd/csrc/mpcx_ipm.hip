@@ -1788,10 +1788,10 @@ __device__ __noinline__ void stage_tail(const Agent a, int k, int g, ldsd* F, co
 // The eliminating lane works on a register image of the stage (NCPT doubles) where the register
 // budget holds it, so the dependent pivot chain runs on registers instead of LDS round trips (the
 // image is scratch: the outputs go to S, ZX and the operators).  Measured on gfx950 (r04,
-// profiles/r04/s3): small-fleet builds (one wave per SIMD) spill 12-97 VGPRs with it at NCPT
+// profiles/r04/s3, s5): small-fleet builds (one wave per SIMD) spill 12-97 VGPRs with it at NCPT
 // 106..202 and none at 67 -> NCPT <= 96 there; fleet builds at one wave per SIMD (MHE, 4 agents
-// per CU) 9.74 -> 9.38 ms with scratch 48 -> 128 B/lane; at 4 waves per SIMD (C3, 128 VGPRs) it
-// spills 540 B/lane, 2.02 -> 2.43 ms, so those keep the LDS image.
+// per CU) 9.76 -> 8.91 ms with the image assembled in registers (scratch 48 -> 176 B/lane); at
+// 4 waves per SIMD (C3, 128 VGPRs) it spills 540 B/lane, 2.02 -> 2.43 ms: LDS image there.
 #if defined(MPCX_ELIM_NOREG)
 constexpr bool ELIM_REG = false;
 #elif defined(MPCX_ELIM_FORCE_REG)
@@ -1800,6 +1800,13 @@ constexpr bool ELIM_REG = true;
 constexpr bool ELIM_REG = NCPT <= 96;
 #else
 constexpr bool ELIM_REG = MIN_WAVES == 1;
+#endif
+
+// ... and assembles the Newton systems itself (assemble_reg) unless MPCX_ASM_NOREG (A/B builds)
+#ifdef MPCX_ASM_NOREG
+constexpr bool ASM_REG = false;
+#else
+constexpr bool ASM_REG = ELIM_REG;
 #endif
 
 template <bool STAGE0, typename FD>
@@ -1813,8 +1820,41 @@ __device__ __forceinline__ int static_body(const Agent a, int k, FD* F, mpcx_eli
   return gen_stage_elim(F, S, ZX, (mpcx_elim_gd*)a.tr(k), (mpcx_elim_gi*)a.prm(k), in);
 }
 
+// Stage k's compact image assembled by the eliminating lane itself, straight into its registers:
+// local_assemble<1, false>'s arithmetic entry by entry (same operations, same order), with no LDS
+// image and no wave barrier between assembly and elimination.  The loads are independent (the
+// stage-minor image coalesces across the lanes of the round's stages).
+__device__ __forceinline__ void assemble_reg(const Agent a, int k, const KKTDiag& kd, double* Fr) {
+  const unsigned long long fm = gL.fixm[k];
+  const wdbl* src = a.lp(k);
+  const wdbl* dg = a.dg(k);
+  const wdbl* rb = a.rhs(k);
+#pragma unroll
+  for (int t = 0; t < NCPT; ++t) {
+    // border (rhs) entries from the rhs the rhs phases wrote in block order; x_k has none
+    const bool bd = t >= CB && t < CB + NLOC && lkind(t - CB) != 2;
+    Fr[t] = bd ? rb[lblk(t - CB, lkind(t - CB))] : src[t * N];
+  }
+  if (fm != 0ull) {
+#pragma unroll
+    for (int t = 0; t < NCPT; ++t) {
+      const int ij = kCIJ[t], i = ij & 255, j = ij >> 8;
+      if ((((fm >> i) | (fm >> j)) & 1ull) != 0ull) Fr[t] = (i == j && lkind(i) == 0) ? 1.0 : 0.0;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < (NLOC < NCPT ? NLOC : NCPT); ++t) {  // diagonal (t, t)
+    const int ki = lkind(t);
+    const bool fix = ((fm >> t) & 1ull) != 0ull;
+    if ((ki == 0 || ki == 3) && !fix) Fr[t] += dg[t] + kd.dw;
+    if (kdual(ki)) Fr[t] = dg[t];
+  }
+}
+
+// kdr: the KKT diagonal terms when the eliminating lane assembles the image itself (ELIM_REG,
+// Newton systems), nullptr when the image was assembled into Fl (least-squares system, LDS image)
 template <bool STAGE0 = false>
-__device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* Fl) {
+__device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* Fl, const KKTDiag* kdr = nullptr) {
   int in[3];
   asm volatile(";; STATIC_BEGIN");
   mpcx_elim_ld* const S = (mpcx_elim_ld*)LDSP(gL.S + k * SOFF);
@@ -1822,8 +1862,12 @@ __device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* Fl) {
   int bad;
   if constexpr (ELIM_REG) {
     double Fr[NCPT];
+    if (kdr != nullptr) {
+      assemble_reg(a, k, *kdr, Fr);
+    } else {
 #pragma unroll
-    for (int t = 0; t < NCPT; ++t) Fr[t] = Fl[t];
+      for (int t = 0; t < NCPT; ++t) Fr[t] = Fl[t];
+    }
     bad = static_body<STAGE0>(a, k, Fr, S, ZX, in);
   } else {
     bad = static_body<STAGE0>(a, k, (mpcx_elim_ld*)Fl, S, ZX, in);
@@ -1866,9 +1910,11 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   }
 #endif
 #ifdef MPCX_STATIC_ELIM
+  // register-image builds assemble the Newton systems in the eliminating lane (assemble_reg)
+  const bool reg_asm = ASM_REG && kd.mode != LSQ;
 #pragma unroll 1
   for (int r = 0; r < CROUNDS; ++r) {
-    {
+    if (!reg_asm) {
       // stage fastest across the lanes: the stage-minor image reads coalesce over the round
       const int slot = lane_now() % SRC, g = lane_now() / SRC, k = K0 + r * SRC + slot;
       if (g < GC && k < N) {
@@ -1876,12 +1922,12 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
         if (kd.mode == LSQ) local_assemble_generic<GC, true>(a, k, g, F, kd);
         else local_assemble<GC, false>(a, k, g, F, kd);
       }
+      wsync();
     }
-    wsync();
     SPROF(0);
     {
       const int slot = lane_now(), k = K0 + r * SRC + slot;  // one lane per stage
-      if (slot < SRC && k < N && static_stage(a, k, LDSP(L.u.c.F + slot * NCS))) {
+      if (slot < SRC && k < N && static_stage(a, k, LDSP(L.u.c.F + slot * NCS), reg_asm ? &kd : nullptr)) {
         atomicOr(&L.dmask[k >> 5], 1u << (k & 31));
         atomicAdd(&L.ks.n_dense, 1);
       }
@@ -1892,12 +1938,14 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
 #ifdef MPCX_STATIC_ELIM0
   {  // stage 0 with its own plan (GC lanes assemble into slot 0, one lane eliminates)
     ldsd* F = LDSP(L.u.c.F);
-    if (lane_now() < GC) {
-      if (kd.mode == LSQ) local_assemble_generic<GC, true>(a, 0, lane_now(), F, kd);
-      else local_assemble<GC, false>(a, 0, lane_now(), F, kd);
+    if (!reg_asm) {
+      if (lane_now() < GC) {
+        if (kd.mode == LSQ) local_assemble_generic<GC, true>(a, 0, lane_now(), F, kd);
+        else local_assemble<GC, false>(a, 0, lane_now(), F, kd);
+      }
+      wsync();
     }
-    wsync();
-    if (lane_now() == 0 && static_stage<true>(a, 0, F)) {
+    if (lane_now() == 0 && static_stage<true>(a, 0, F, reg_asm ? &kd : nullptr)) {
       atomicOr(&L.dmask[0], 1u);
       atomicAdd(&L.ks.n_dense, 1);
     }

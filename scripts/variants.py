@@ -63,6 +63,10 @@ VARIANTS = {
     "elimreg": (["-DMPCX_ELIM_FORCE_REG"], None),
     "elimreg_w1": (["-DMPCX_ELIM_FORCE_REG", "-DMPCX_MIN_WAVES=1"], None),
     "lds_noreg": (["-DMPCX_WS_LDS", "-DMPCX_ELIM_NOREG"], None),
+    # r04: the register image loaded from the LDS image the GC lanes assembled (no assemble_reg)
+    "asm_noreg": (["-DMPCX_ASM_NOREG"], None),
+    "noreg": (["-DMPCX_ELIM_NOREG"], None),
+    "lds_asm_noreg": (["-DMPCX_WS_LDS", "-DMPCX_ASM_NOREG"], None),
 }
 
 

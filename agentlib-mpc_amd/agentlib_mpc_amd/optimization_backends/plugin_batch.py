@@ -184,7 +184,7 @@ class ResidentBatch:
         self._launch = None
         if self.small and device.type == "cuda":
             self._pin_out = torch.empty(self.BUF.numel() - self._out_off, dtype=torch.float64, pin_memory=True)
-            self._d2h = torch.cuda.Event()
+        self._roundtrip = None
 
     # -- reading the agents' variables ---------------------------------------------------
     def read(self, batch_vars: Sequence[dict], now: float) -> Dict[tuple, object]:
@@ -355,10 +355,8 @@ class ResidentBatch:
         if self.cold_rows is not None and self.cold_rows.size:
             self.hW[self.cold_rows] = self._cold_guess(self.cold_rows)
             self.cold_rows = None
-        self._buf_in.copy_(self._hbuf_in, non_blocking=True)
-        if self.dev.type == "cuda":
-            self._h2d = self.torch.cuda.Event()
-            self._h2d.record()
+        if self.dev.type != "cuda":
+            self._buf_in.copy_(self._hbuf_in)  # on the GPU, solve() stages the upload
         self.last = cur
         return cur
 
@@ -453,21 +451,24 @@ class ResidentBatch:
         """Launch on the resident arrays (the solution replaces the guess in place); returns
         (w, raw stats) on the host."""
         torch = self.torch
-        if self._launch is None:  # the buffers are resident: checked once, pointers pre-bound
-            self._launch = self.native.bind(self.P, self.L, self.U, self.W, lam_g=self.lam_g, stats=self.ST)
-        self._launch()
         if self.small:
-            # a persistent pinned buffer: solution and stats in one copy, one wait (a fresh pinned
-            # buffer and a blocking stats copy cost ~40 us per call, a tenth of a single agent's solve)
-            self._pin_out.copy_(self.BUF[self._out_off:], non_blocking=True)
-            self._d2h.record()
-            self._d2h.synchronize()
+            # ONE native call: the host mirrors uploaded from pinned memory, the solve, solution and
+            # stats read back into a persistent pinned buffer, the wait (as separate torch copies,
+            # events and a launch: ~25 us more per call, a twentieth of a single agent's solve)
+            if self._roundtrip is None:
+                self._roundtrip = self.native.bind_staged(self.P, self.L, self.U, self.W, self.lam_g, self.ST,
+                                                          self._hbuf_in, self._buf_in, self._pin_out,
+                                                          self.BUF[self._out_off:])
+            self._roundtrip()
             out = self._pin_out.numpy()
             nw = self.hW.size
             w = out[:nw].reshape(self.hW.shape).copy()
             raw = out[nw:].view(np.uint8)[:self.ST.numel()].copy()
             self.hW[:] = w  # the next call's warm start (uploaded with the inputs)
         else:
+            if self._launch is None:  # the buffers are resident: checked once, pointers pre-bound
+                self._launch = self.native.bind(self.P, self.L, self.U, self.W, lam_g=self.lam_g, stats=self.ST)
+            self._launch()
             w = torch.empty((self.n, self.W.shape[1]), dtype=torch.float64, pin_memory=True)
             w.copy_(self.W, non_blocking=True)
             raw = self.ST.cpu().numpy()  # synchronises (w is complete too: same stream)

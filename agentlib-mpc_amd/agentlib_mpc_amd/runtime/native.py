@@ -83,7 +83,7 @@ STATS_BYTES = ctypes.sizeof(Stats)
 EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
     "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_problem_small_fleet",
-    "mpcx_batch_solve",
+    "mpcx_batch_solve", "mpcx_batch_solve_staged",
     "mpcx_admm_moments_size", "mpcx_admm_reduce_count", "mpcx_admm_moments", "mpcx_admm_finalize",
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
@@ -187,6 +187,7 @@ def load_library():
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
         lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp, vp]
         i64 = ctypes.c_int64
+        lib.mpcx_batch_solve_staged.argtypes = [vp, i32, vp, vp, i64, vp, vp, i64] + [vp] * 6 + [vp]
         lib.mpcx_admm_moments_size.argtypes = [i32, i32, i32]
         lib.mpcx_admm_moments_size.restype = i64
         lib.mpcx_admm_reduce_count.argtypes = [i32, i32, i32]
@@ -423,6 +424,34 @@ class NativeProblem:
             if rc != 0:
                 raise NativeError(f"mpcx_batch_solve failed ({rc})")
         return launch
+
+    def bind_staged(self, p, lbw, ubw, w, lam_g, stats, host_in, dev_in, host_out, dev_out):
+        """:meth:`bind` for the small-batch host round trip (``mpcx_batch_solve_staged``): the
+        returned call uploads ``host_in`` (pinned) into ``dev_in``, solves, reads ``dev_out``
+        back into ``host_out`` (pinned) and returns when both are done -- one native call."""
+        import torch
+
+        self.bind(p, lbw, ubw, w, lam_g=lam_g, stats=stats)  # the same argument checks
+        for name, t, dev in (("host_in", host_in, False), ("dev_in", dev_in, True),
+                             ("host_out", host_out, False), ("dev_out", dev_out, True)):
+            if not t.is_contiguous() or t.is_cuda != dev or (not dev and not t.is_pinned()):
+                raise ValueError(f"{name}: contiguous {'device' if dev else 'pinned host'} tensor expected")
+        nin, nout = host_in.numel() * host_in.element_size(), host_out.numel() * host_out.element_size()
+        if dev_in.numel() * dev_in.element_size() != nin or dev_out.numel() * dev_out.element_size() != nout:
+            raise ValueError("staged buffers: host and device sizes differ")
+        vp = ctypes.c_void_p
+        args = (self.handle, int(p.shape[0]), vp(host_in.data_ptr()), vp(dev_in.data_ptr()), nin,
+                vp(host_out.data_ptr()), vp(dev_out.data_ptr()), nout, vp(p.data_ptr()), vp(lbw.data_ptr()),
+                vp(ubw.data_ptr()), vp(w.data_ptr()), None if lam_g is None else vp(lam_g.data_ptr()),
+                None if stats is None else vp(stats.data_ptr()))
+        fn = self.lib.mpcx_batch_solve_staged
+
+        def roundtrip(stream=None):
+            s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+            rc = fn(*args, vp(s))
+            if rc != 0:
+                raise NativeError(f"mpcx_batch_solve_staged failed ({rc})")
+        return roundtrip
 
 
 _STATS_DOUBLES = ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")

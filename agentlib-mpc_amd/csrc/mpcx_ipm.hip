@@ -1018,6 +1018,108 @@ __device__ __noinline__ Inertia bk_sweep(ldsd* A, OutT* out, int lane) {
   return in;
 }
 
+// Two independent blocks swept at once (the twisted chain's forward and backward pivots, r04):
+// bk_sweep's arithmetic and pivot choices for each block -- lanes 0-7 search block A's pivot
+// candidates and lanes 8-15 block B's, each octet with its own DPP reduction, and every owning
+// lane updates its entry of both blocks -- so one pass costs the dependent latency of one.
+// In place (each block receives its own inverse); twob false sweeps A alone.
+template <int NN, int LD>
+__device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane) {
+  static_assert(NN * NN <= WAVE && NN <= 8, "one lane per entry; pivot candidates in one lane octet");
+  constexpr unsigned FULL = (1u << NN) - 1u;
+  Inertia in{0, 0, 0};
+  const int ti = lane / NN, tj = lane % NN;
+  const bool own = lane < NN * NN;
+  const int oc = lane >> 3, ol = lane & 7;  // octet 0 searches A, octet 1 searches B
+  ldsd* const M = oc == 0 ? A : B;
+  unsigned dA = 0u, zA = 0u, dB = twob ? 0u : FULL, zB = 0u;
+#pragma unroll 1
+  while (dA != FULL || dB != FULL) {
+    const bool goA = dA != FULL, goB = dB != FULL;
+    const int kA = goA ? __builtin_ctz(~dA) : 0, kB = goB ? __builtin_ctz(~dB) : 0;
+    const int k = oc == 0 ? kA : kB;
+    const bool cand = oc < 2 && ol < NN && (oc == 0 ? goA : goB) && !(((oc == 0 ? dA : dB) >> ol) & 1u);
+    double lam = -1.0;
+    int r = -1;
+    if (cand && ol != k) { lam = fabs(M[ol * LD + k]); r = ol; }
+    gargmax<8>(lam, r);
+    double lamA = rl_f64(lam, 0), lamB = rl_f64(lam, 8);
+    const int rA = __builtin_amdgcn_readlane(r, 0), rB = __builtin_amdgcn_readlane(r, 8);
+    if (rA < 0) lamA = 0.0;
+    if (rB < 0) lamB = 0.0;
+    const double akkA = fabs(A[kA * LD + kA]), akkB = fabs(B[kB * LD + kB]);
+    const bool needA = goA && !(fmax(akkA, lamA) == 0.0 || akkA >= BK_ALPHA * lamA);
+    const bool needB = goB && !(fmax(akkB, lamB) == 0.0 || akkB >= BK_ALPHA * lamB);
+    int pA = kA, qA = -1, pB = kB, qB = -1;
+    if (needA || needB) {
+      const int ro = oc == 0 ? rA : rB;
+      double sg = 0.0;
+      if (cand && ol != ro && (oc == 0 ? needA : needB)) sg = fabs(M[ro * LD + ol]);
+      const double g8 = gmax<8>(sg);
+      const double sigA = rl_f64(g8, 0), sigB = rl_f64(g8, 8);
+      if (needA) {
+        if (akkA * sigA >= BK_ALPHA * lamA * lamA) pA = kA;
+        else if (fabs(A[rA * LD + rA]) >= BK_ALPHA * sigA) pA = rA;
+        else qA = rA;
+      }
+      if (needB) {
+        if (akkB * sigB >= BK_ALPHA * lamB * lamB) pB = kB;
+        else if (fabs(B[rB * LD + rB]) >= BK_ALPHA * sigB) pB = rB;
+        else qB = rB;
+      }
+    }
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+      if (blk == 0 ? !goA : !goB) continue;
+      ldsd* const X = blk == 0 ? A : B;
+      unsigned& done = blk == 0 ? dA : dB;
+      unsigned& zero = blk == 0 ? zA : zB;
+      const int kk = blk == 0 ? kA : kB, p = blk == 0 ? pA : pB, q = blk == 0 ? qA : qB;
+      if (q < 0) {
+        const double d = X[p * LD + p];
+        done |= 1u << p;
+        if (fabs(d) <= ZERO_PIVOT) { in.zero++; zero |= 1u << p; continue; }
+        if (d > 0) in.pos++; else in.neg++;
+        const double rd = 1.0 / d;
+        if (own) {
+          const double aip = X[ti * LD + p], apj = X[p * LD + tj], aij = X[ti * LD + tj];
+          X[ti * LD + tj] = (ti == p) ? ((tj == p) ? -rd : apj * rd) : (tj == p) ? aip * rd : aij - aip * apj * rd;
+        }
+      } else {
+        const double a11 = X[kk * LD + kk], a21 = X[q * LD + kk], a22 = X[q * LD + q];
+        const double det = a11 * a22 - a21 * a21;
+        done |= (1u << kk) | (1u << q);
+        if (fabs(det) <= ZERO_PIVOT * ZERO_PIVOT) { in.zero += 2; zero |= (1u << kk) | (1u << q); continue; }
+        if (det < 0) { in.pos++; in.neg++; }
+        else if (a11 + a22 > 0) in.pos += 2;
+        else in.neg += 2;
+        const double rdet = 1.0 / det;
+        const double p11 = a22 * rdet, p12 = -a21 * rdet, p22 = a11 * rdet;
+        if (own) {
+          const double aik = X[ti * LD + kk], aiq = X[ti * LD + q], akj = X[kk * LD + tj], aqj = X[q * LD + tj];
+          const double aij = X[ti * LD + tj];
+          const double xk = aik * p11 + aiq * p12, xq = aik * p12 + aiq * p22;
+          const double yk = p11 * akj + p12 * aqj, yq = p12 * akj + p22 * aqj;
+          const bool ip = ti == kk || ti == q, jp = tj == kk || tj == q;
+          double v;
+          if (ip && jp) v = -((ti == kk) ? ((tj == kk) ? p11 : p12) : ((tj == kk) ? p12 : p22));
+          else if (ip) v = (ti == kk) ? yk : yq;
+          else if (jp) v = (tj == kk) ? xk : xq;
+          else v = aij - (xk * akj + xq * aqj);
+          X[ti * LD + tj] = v;
+        }
+      }
+    }
+    wsync();
+  }
+  if (own) {
+    A[ti * LD + tj] = (((zA >> ti) | (zA >> tj)) & 1u) ? 0.0 : -A[ti * LD + tj];
+    if (twob) B[ti * LD + tj] = (((zB >> ti) | (zB >> tj)) & 1u) ? 0.0 : -B[ti * LD + tj];
+  }
+  wsync();
+  return in;
+}
+
 // ---------------------------------------------------------------------------
 // KKT entries
 // ---------------------------------------------------------------------------
@@ -1745,6 +1847,167 @@ __device__ MPCX_HOT void chain_solve(const Agent a) {
   wsync();
 }
 
+// Twisted chain (r04): the block-tridiagonal chain eliminated from BOTH ends at once -- forward
+// pivots D_j = C_j - S10(j) [D_{j-1}^-1]_xx S10(j)^T for j < CMID, backward pivots
+// E_j = C_j - E S10(j+1)^T E_{j+1}^-1 S10(j+1) E^T for j > CMID (E embeds the states), one
+// forward and one backward pivot per step swept together (bk_sweep2), and the middle pivot
+// M = C_CMID minus both neighbours' contributions last: ceil(N/2) + 1 sequential sweeps instead
+// of N.  Another symmetric elimination order of the same matrix, so the same inertia (sum of
+// the swept pivots' inertias, Sylvester) and the same solution up to rounding.  Each pivot's
+// inverse is swept in place in its Dinv slot.  MPCX_CHAIN_SEQ keeps the one-sided chain (A/B).
+#if !defined(MPCX_CHAIN_SEQ) && !defined(MPCX_CHAIN_BK)
+constexpr bool CHAIN_TW = NC > 0 && !(NX == 1 && NMU == 0) && NC * NC <= WAVE;
+#else
+constexpr bool CHAIN_TW = false;
+#endif
+constexpr int CMID = N / 2;                                        // the middle pivot
+constexpr int CSTEPS = CMID > N - 1 - CMID ? CMID : N - 1 - CMID;  // steps before it
+
+__device__ MPCX_HOT Inertia chain_factor_tw(const Agent a) {
+  Lds& L = gL;
+  Inertia in{0, 0, 0};
+  const int lane = lane_now();
+  constexpr int XO = NMU;
+  constexpr int NCX = NC * NX;
+#pragma unroll 1
+  for (int s = 0; s <= CSTEPS; ++s) {
+    const bool mid = s == CSTEPS;
+    const int jf = mid ? CMID : s, jb = N - 1 - s;
+    const bool hf = mid || s < CMID;   // a forward pivot (or the middle one) this step
+    const bool hb = !mid && jb > CMID;  // a backward pivot this step
+    const int jt = mid ? CMID : jb;     // the pivot that takes a backward contribution
+    const bool bw = mid ? CMID + 1 < N : hb && jb + 1 < N;
+    // CW = S10(jf) [D_{jf-1}^-1]_xx  and  CY = E_{jt+1}^-1 S10(jt+1)   (NC x NX each)
+    for (int e = lane; e < 2 * NCX; e += WAVE) {
+      const bool sec = e >= NCX;
+      const int ee = sec ? e - NCX : e, r = ee / NX, c = ee % NX;
+      double sacc = 0.0;
+      if (!sec) {
+        if (hf && jf > 0)
+          for (int m = 0; m < NX; ++m) sacc += s10(jf)[r * NX + m] * L.Dinv[(jf - 1) * NCC + (XO + m) * NC + XO + c];
+        L.CW[ee] = sacc;
+      } else {
+        if (bw)
+          for (int m = 0; m < NC; ++m) sacc += L.Dinv[(jt + 1) * NCC + r * NC + m] * s10(jt + 1)[m * NX + c];
+        L.CY[ee] = sacc;
+      }
+    }
+    wsync();
+    // the pivots, assembled in their Dinv slots
+    for (int e = lane; e < 2 * NC * NC; e += WAVE) {
+      const bool sec = e >= NC * NC;
+      if (sec ? !hb : !hf) continue;
+      const int ee = sec ? e - NC * NC : e, r = ee / NC, c = ee % NC;
+      const int j = sec ? jb : jf;
+      double v = s11(j)[ee];
+      if (j + 1 < N && r >= XO && c >= XO) v += s00(j + 1)[(r - XO) * NX + (c - XO)];
+      if (!sec && jf > 0)
+        for (int m = 0; m < NX; ++m) v -= L.CW[r * NX + m] * s10(jf)[c * NX + m];
+      if ((sec || mid) && bw && r >= XO && c >= XO)
+        for (int m = 0; m < NC; ++m) v -= s10(jt + 1)[m * NX + (r - XO)] * L.CY[m * NX + (c - XO)];
+      const bool fr = r >= XO && ((L.fixm[j] >> (LX1 + r - XO)) & 1ull);
+      const bool fc = c >= XO && ((L.fixm[j] >> (LX1 + c - XO)) & 1ull);
+      if (fr || fc) v = (r == c) ? 1.0 : 0.0;
+      L.Dinv[j * NCC + ee] = v;
+    }
+    wsync();
+    const Inertia bi = bk_sweep2<NC, NC>(LDSP(L.Dinv + jf * NCC), LDSP(L.Dinv + jb * NCC), hb, lane);
+    in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;
+  }
+  wsync();
+  return in;
+}
+
+// The twisted chain's solve: the rhs eliminated from both ends towards the middle (y_j for
+// j < CMID, z_j for j > CMID), the middle block solved, then the back-substitution outwards in
+// both directions.  xs holds y / z, then the solution.
+__device__ MPCX_HOT void chain_solve_tw(const Agent a) {
+  Lds& L = gL;
+  const int lane = lane_now();
+  constexpr int XO = NMU;
+  constexpr int ZS = NX + NC;  // zx stride per stage: [x_k | c_k]
+  // rhs of c_j: z[c_j] + E z[x_{j+1}]
+  auto rhs = [&](int j, int r) -> double {
+    return L.zx[j * ZS + NX + r] + (j + 1 < N && r >= XO ? L.zx[(j + 1) * ZS + (r - XO)] : 0.0);
+  };
+  for (int e = lane; e < 2 * NC; e += WAVE) {
+    const bool sec = e >= NC;
+    const int r = sec ? e - NC : e, j = sec ? N - 1 : 0;
+    if (sec ? N - 1 > CMID : (CMID > 0 || CSTEPS == 0)) L.xs[j * NC + r] = rhs(j, r);
+  }
+  wsync();
+  // towards the middle: y_j = rhs_j - S10(j) [D_{j-1}^-1 y_{j-1}]_x,
+  //                     z_j = rhs_j - E S10(j+1)^T E_{j+1}^-1 z_{j+1}
+#pragma unroll 1
+  for (int s = 1; s <= CSTEPS; ++s) {
+    const bool mid = s == CSTEPS;
+    const int jf = mid ? CMID : s, jb = mid ? CMID : N - 1 - s;
+    const bool hf = (mid || jf < CMID) && jf > 0, hb = (mid || jb > CMID) && jb + 1 < N;
+    for (int e = lane; e < NX + NC; e += WAVE) {
+      double sacc = 0.0;
+      if (e < NX) {  // CY = [D_{jf-1}^-1 y_{jf-1}]_x
+        if (hf)
+          for (int m = 0; m < NC; ++m) sacc += L.Dinv[(jf - 1) * NCC + (XO + e) * NC + m] * L.xs[(jf - 1) * NC + m];
+        L.CY[e] = sacc;
+      } else {  // CW = E_{jb+1}^-1 z_{jb+1}
+        const int r = e - NX;
+        if (hb)
+          for (int m = 0; m < NC; ++m) sacc += L.Dinv[(jb + 1) * NCC + r * NC + m] * L.xs[(jb + 1) * NC + m];
+        L.CW[r] = sacc;
+      }
+    }
+    wsync();
+    for (int e = lane; e < 2 * NC; e += WAVE) {
+      const bool sec = e >= NC;
+      const int r = sec ? e - NC : e;
+      if (mid && sec) continue;  // the middle block: one update with both terms
+      const int j = sec ? jb : jf;
+      if (!mid && (sec ? !(jb > CMID) : !(jf < CMID))) continue;
+      double v = rhs(j, r);
+      if ((!sec || mid) && hf)
+        for (int m = 0; m < NX; ++m) v -= s10(jf)[r * NX + m] * L.CY[m];
+      if ((sec || mid) && hb && r >= XO)
+        for (int m = 0; m < NC; ++m) v -= s10(jb + 1)[m * NX + (r - XO)] * L.CW[m];
+      L.xs[j * NC + r] = v;
+    }
+    wsync();
+  }
+  // the middle block, then outwards: c_j = D_j^-1 (y_j - E S10(j+1)^T c_{j+1}) for j < CMID,
+  //                                  c_j = E_j^-1 (z_j - S10(j) [c_{j-1}]_x)   for j > CMID
+#pragma unroll 1
+  for (int s = 0; s <= CSTEPS; ++s) {
+    const int jf = CMID - s, jb = CMID + s;
+    const bool hf = jf >= 0, hb = s > 0 && jb < N;
+    for (int e = lane; e < 2 * NC; e += WAVE) {
+      const bool sec = e >= NC;
+      const int r = sec ? e - NC : e;
+      if (sec ? !hb : !hf) continue;
+      if (!sec) {
+        double v = L.xs[jf * NC + r];
+        if (s > 0 && r >= XO)
+          for (int m = 0; m < NC; ++m) v -= s10(jf + 1)[m * NX + (r - XO)] * L.xs[(jf + 1) * NC + m];
+        L.CY[r] = v;
+      } else {
+        double v = L.xs[jb * NC + r];
+        for (int m = 0; m < NX; ++m) v -= s10(jb)[r * NX + m] * L.xs[(jb - 1) * NC + XO + m];
+        L.CW[r] = v;
+      }
+    }
+    wsync();
+    for (int e = lane; e < 2 * NC; e += WAVE) {
+      const bool sec = e >= NC;
+      const int r = sec ? e - NC : e;
+      if (sec ? !hb : !hf) continue;
+      const int j = sec ? jb : jf;
+      const double* src = sec ? (const double*)L.CW : (const double*)L.CY;
+      double sacc = 0.0;
+      for (int m = 0; m < NC; ++m) sacc += L.Dinv[j * NCC + r * NC + m] * src[m];
+      L.xs[j * NC + r] = sacc;
+    }
+    wsync();
+  }
+}
+
 // After the interior elimination of stage k (slot lanes g): store its local Schur blocks
 // and eliminated rhs (chain input), back-substitute the trailing rows and store the
 // back-substitution operators.  A leaf, so factor() keeps almost nothing live across calls.
@@ -2012,7 +2275,7 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   Inertia in{L.fin[0], L.fin[1], L.fin[2]};
   if (lane_now() == 0) L.seq = 0;
   if (NC > 0) {
-    const Inertia ci = chain_factor(a);
+    const Inertia ci = CHAIN_TW ? chain_factor_tw(a) : chain_factor(a);
     in.pos += ci.pos; in.neg += ci.neg; in.zero += ci.zero;
   }
   SPROF(3);
@@ -2034,7 +2297,7 @@ __device__ MPCX_HOT void solve(const Agent a) {
   if (L.seq) { seq_solve(a); return; }
   SPROF_DECL
   const int lane = lane_now();
-  if (NC > 0) chain_solve(a);
+  if (NC > 0) { if constexpr (CHAIN_TW) chain_solve_tw(a); else chain_solve(a); }
   SPROF(4);
   // u = W [x_k, c_k, 1] per stage interior (operators column-major per stage); the lanes
   // run over all (stage, interior row) pairs

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 7
+#define MPCX_API_VERSION 8
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -172,6 +172,19 @@ int mpcx_batch_solve(mpcx_handle* h, int32_t n_agents, const double* p, const do
                      const double* ubw, const double* lbg, const double* ubg, double* w_io,
                      double* lam_g, double* lam_w, mpcx_stats* stats, const int32_t* active,
                      void* stream);
+
+/* Host round trip of a small batch in ONE call (C ABI v8): the reference's usual deployment
+ * is one MPC agent per process whose do_step blocks on its solve (modules/mpc/mpc.py:322-340 ->
+ * core/discretization.py:203).  Copies in_bytes from host_in to dev_in (pinned host memory
+ * makes it asynchronous), runs mpcx_batch_solve on the device buffers (p, lbw, ubw, w_io,
+ * lam_g, stats: typically views into dev_in / dev_out), copies out_bytes from dev_out back to
+ * host_out and waits for the stream: on return the solution and stats are on the host.  One
+ * call instead of an upload, a launch, a read-back and a wait (each a host API call).  in_bytes
+ * or out_bytes 0 skips that copy. */
+int mpcx_batch_solve_staged(mpcx_handle* h, int32_t n_agents, const void* host_in, void* dev_in,
+                            int64_t in_bytes, void* host_out, const void* dev_out, int64_t out_bytes,
+                            const double* p, const double* lbw, const double* ubw, double* w_io,
+                            double* lam_g, mpcx_stats* stats, void* stream);
 
 /* ---- ADMM kernels (agent-batched) --------------------------------------------------
  * Local trajectories are rows of `locals` [n_rows][T] (fp64, device).  The participants

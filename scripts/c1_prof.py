@@ -35,12 +35,13 @@ def main():
         print(f"{label}: median {np.median(ts) * 1e3:.3f} ms  p10 {np.percentile(ts, 10) * 1e3:.3f}  "
               f"iters {r.stats['iter_count']}", flush=True)
     rb = be._resident
+    launch = rb.native.bind(rb.P, rb.L, rb.U, rb.W, lam_g=rb.lam_g, stats=rb.ST)
     s = torch.cuda.current_stream()
     ks = []
     for _ in range(50):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        rb._launch()
+        launch()
         e1.record(s)
         torch.cuda.synchronize()
         ks.append(e0.elapsed_time(e1))

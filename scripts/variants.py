@@ -66,6 +66,8 @@ VARIANTS = {
     # r04: the register image loaded from the LDS image the GC lanes assembled (no assemble_reg)
     "asm_noreg": (["-DMPCX_ASM_NOREG"], None),
     "noreg": (["-DMPCX_ELIM_NOREG"], None),
+    # r04: the one-sided state chain instead of the twisted one
+    "chain_seq": (["-DMPCX_CHAIN_SEQ"], None),
     "lds_asm_noreg": (["-DMPCX_WS_LDS", "-DMPCX_ASM_NOREG"], None),
 }
 

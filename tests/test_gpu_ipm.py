@@ -427,3 +427,41 @@ def test_gpu_small_fleet_build_matches_hbm_build():
     assert np.mean([s["status"] in (0, 1) for s in sl]) > 0.99
     np.testing.assert_allclose(wl, wh, rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose([s["obj"] for s in sl], [s["obj"] for s in sh], rtol=1e-10)
+
+
+def test_gpu_staged_round_trip_equals_separate_calls():
+    """``mpcx_batch_solve_staged`` (C ABI v8: upload from pinned host memory, solve, read-back,
+    wait in one call) against the same solve as separate steps (device copy, ``mpcx_batch_solve``,
+    read-back): identical solutions and stats, bit for bit, on three C1-type agents."""
+    import bench
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES
+
+    n = 3
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261015 + 5))
+    p, lbw, ubw, w0 = be.problem.to_kernel(p, lbw, ubw, w0)
+    native = be._native()
+    host = np.concatenate([np.ascontiguousarray(a, np.float64).ravel() for a in (p, lbw, ubw, w0)])
+    st_words = -(-n * STATS_BYTES // 8)
+    out = {}
+    for mode in ("separate", "staged"):
+        buf = torch.zeros(host.size + st_words, dtype=torch.float64, device="cuda")
+        offs = np.cumsum([0, p.size, lbw.size, ubw.size, w0.size])
+        P, L, U, W = (buf[offs[i]:offs[i + 1]].view(a.shape) for i, a in enumerate((p, lbw, ubw, w0)))
+        ST = buf[offs[4]:].view(torch.uint8)[:n * STATS_BYTES]
+        lam = torch.empty((n, be.problem.nlp.kernel_ng), dtype=torch.float64, device="cuda")
+        hin = torch.from_numpy(host).pin_memory()
+        hout = torch.empty(buf.numel() - int(offs[3]), dtype=torch.float64).pin_memory()
+        if mode == "separate":
+            buf[:offs[4]].copy_(hin)
+            native.bind(P, L, U, W, lam_g=lam, stats=ST)()
+            hout.copy_(buf[offs[3]:])
+            torch.cuda.synchronize()
+        else:
+            native.bind_staged(P, L, U, W, lam, ST, hin, buf[:offs[4]], hout, buf[offs[3]:])()
+        out[mode] = hout.numpy().copy()
+    np.testing.assert_array_equal(out["staged"], out["separate"])
+    w = out["staged"][:w0.size].reshape(w0.shape)
+    assert np.isfinite(w).all() and not np.array_equal(w, w0)

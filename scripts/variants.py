@@ -68,6 +68,7 @@ VARIANTS = {
     "noreg": (["-DMPCX_ELIM_NOREG"], None),
     # r04: the one-sided state chain instead of the twisted one
     "chain_seq": (["-DMPCX_CHAIN_SEQ"], None),
+    "lds_nofence": (["-DMPCX_WS_LDS", "-DMPCX_ELIM_FENCE=(void)0"], None),
     "lds_asm_noreg": (["-DMPCX_WS_LDS", "-DMPCX_ASM_NOREG"], None),
 }
 

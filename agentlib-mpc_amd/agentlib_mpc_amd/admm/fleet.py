@@ -35,8 +35,10 @@ path.
 
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import math
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Union
 
@@ -440,6 +442,12 @@ class ADMMFleet:
         #: copies, [n, 2] int32) -- the per-agent counterpart of the reference's per-solve stats;
         #: None (the default) records nothing
         self.solve_trace = None
+        #: the classes' solves of an iteration on one HIP stream each (see _solve_all);
+        #: MPCX_FLEET_STREAMS=0 keeps them on the caller's stream, one after the other
+        self.concurrent_classes = (dev.type == "cuda" and len(self.classes) > 1
+                                   and os.environ.get("MPCX_FLEET_STREAMS", "1") != "0")
+        self._class_streams = [t.cuda.Stream(device=dev) for _ in self.classes] if self.concurrent_classes else None
+        self._ev_solve = t.cuda.Event() if self.concurrent_classes else None
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
@@ -483,24 +491,40 @@ class ADMMFleet:
 
     def _solve_all(self, rho: float):
         """Inject mean/diff, multipliers and the block's rho into every agent's p; solve
-        (agents of frozen blocks are skipped); gather locals."""
-        ops, T = self.ops, self.T
+        (agents of frozen blocks are skipped); gather locals.
+
+        The classes' solves are independent within an iteration (each agent reads the means and
+        multipliers of the previous one), so with several classes each runs on a HIP stream of
+        its own (``concurrent_classes``): a class's launch fills the CUs the other's leaves idle
+        (its last, partial generation of agents), instead of starting after it."""
+        ops, T, t = self.ops, self.T, self.torch
+        streams = self._class_streams if self.concurrent_classes else None
+        if streams:
+            main = t.cuda.current_stream(self.device)
+            self._ev_solve.record(main)
         for ci, c in enumerate(self.classes):
-            for si, s in enumerate(c.slots):
-                d = c.dev_slots[si]
-                if s.kind == CONSENSUS:
-                    ops.scatter_rows(T, self.MEAN, d["groups"], c.P, d["mean_cols"])
-                    ops.scatter_rows(T, self.LAMR, d["rows"], c.P, d["mult_cols"])
-                else:
-                    ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
-                    ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
-            ops.scatter_rows(1, self.RHO_B, c.BLOCK, c.P, c.RHO_COL)  # the block's penalty
-            ops.solve(c, c.ACTIVE if self._masked else None)
-            for si, s in enumerate(c.slots):
-                d = c.dev_slots[si]
-                # agents not participating keep their local (their rows map to the scratch row)
-                ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
-            words = c.ST.view(self.torch.int32).view(c.n, STATS_BYTES // 4)
+            with (t.cuda.stream(streams[ci]) if streams else contextlib.nullcontext()):
+                if streams:
+                    streams[ci].wait_event(self._ev_solve)
+                for si, s in enumerate(c.slots):
+                    d = c.dev_slots[si]
+                    if s.kind == CONSENSUS:
+                        ops.scatter_rows(T, self.MEAN, d["groups"], c.P, d["mean_cols"])
+                        ops.scatter_rows(T, self.LAMR, d["rows"], c.P, d["mult_cols"])
+                    else:
+                        ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
+                        ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
+                ops.scatter_rows(1, self.RHO_B, c.BLOCK, c.P, c.RHO_COL)  # the block's penalty
+                ops.solve(c, c.ACTIVE if self._masked else None)
+                for si, s in enumerate(c.slots):
+                    d = c.dev_slots[si]
+                    # agents not participating keep their local (their rows map to the scratch row)
+                    ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
+        if streams:
+            for st_ in streams:
+                main.wait_stream(st_)
+        for c in self.classes:
+            words = c.ST.view(t.int32).view(c.n, STATS_BYTES // 4)
             if self.solve_trace is not None:
                 self.solve_trace.append((c.name, words[:, _ITER_WORD:_STATUS_WORD + 1].clone()))
             st = words[:, _STATUS_WORD]

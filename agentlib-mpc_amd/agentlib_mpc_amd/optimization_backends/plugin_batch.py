@@ -32,6 +32,7 @@ MHE stage forms re-marshal on the host).
 
 from __future__ import annotations
 
+import itertools
 import operator
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -177,6 +178,7 @@ class ResidentBatch:
                      for k, (c, q) in m.over.items() if c.size}
         self._prev_buf = None
         self._cold_plan = None
+        self._mid_cache = None  # (sampled bounds of the midpoint columns, their cold guess)
         self._unchanged = set()
         self.last: Dict[tuple, object] = self.read(batch_vars, now)
         self.cold_rows: Optional[np.ndarray] = None
@@ -199,6 +201,7 @@ class ResidentBatch:
         if self.specs is None:
             self.specs = [(ref, tuple(attrs), "value" in attrs) for ref, attrs in self.refs.items()]
             self.n_cols = sum(len(a) for _, a, _ in self.specs)
+            self._col_keys = [(ref, attr) for ref, attrs, _ in self.specs for attr in attrs]
         if not isinstance(batch_vars, list):
             batch_vars = list(batch_vars)
         buf = np.empty((self.n_cols, n), dtype=np.float64)
@@ -206,6 +209,16 @@ class ResidentBatch:
             status, bad = self.pyread.read_columns(batch_vars, self.specs, buf)
         except KeyError:  # a variable missing: the Python path raises it in the reference's order
             return self._read_python(batch_vars, now, self.refs)
+        prev = self._prev_buf
+        if bad < 0 and not status.strip(b"\x00"):
+            # every column numeric (the usual case): the column keys in one zip, the unchanged
+            # columns from one vectorised comparison
+            self._prev_buf = buf
+            if prev is not None and prev.shape == buf.shape:
+                self._unchanged = set(itertools.compress(self._col_keys, ~np.any(buf != prev, axis=1)))
+            else:
+                self._unchanged = set()
+            return dict(zip(self._col_keys, buf))
         out = {}
         c = 0
         slow = {}
@@ -222,7 +235,6 @@ class ResidentBatch:
                 c += 1
         # numeric columns unchanged since the last read, in one vectorised comparison (the
         # per-column comparisons were a sixth of a single agent's host time)
-        prev = self._prev_buf
         self._unchanged = set()
         if prev is not None and prev.shape == buf.shape:
             same = ~np.any(buf != prev, axis=1)
@@ -328,9 +340,10 @@ class ResidentBatch:
             self._h2d.synchronize()  # the last upload has read the mirrors
         dst = {"p": self.hP, "ls": self.hLS, "us": self.hUS}
         changed = nan_in = False
+        last, unch = self.last, self._unchanged
         for key, val in cur.items():
-            old = self.last.get(key)
-            if self._same(key, val, old):
+            old = last.get(key)
+            if (key in unch and isinstance(old, np.ndarray)) or self._same(key, val, old):
                 cur[key] = old
                 continue
             changed = True
@@ -391,15 +404,23 @@ class ResidentBatch:
             cat = lambda parts: np.concatenate(parts).astype(np.int64) if parts else np.zeros(0, np.int64)  # noqa
             self._cold_plan = (cat(dst_a), cat(src_a), cat(mid))
         dst_a, src_a, mid = self._cold_plan
-        P = self.hP[rows]
+        if len(rows) == self.n:  # every agent (a cold restart): no row gathers
+            P, LS, US = self.hP, self.hLS, self.hUS
+        else:
+            P, LS, US = self.hP[rows], self.hLS[rows], self.hUS[rows]
         g = np.zeros((len(rows), self.hW.shape[1]))
         g[:, dst_a] = P[:, src_a]
-        ix = np.ix_(rows, mid)
-        with np.errstate(invalid="ignore"):
-            v = 0.5 * (self.hLS[ix] + self.hUS[ix])
-        bad = ~np.isfinite(v)
-        if bad.any():  # nan_to_num(posinf=0, neginf=-0)
-            v[bad] = np.where(v[bad] < 0, -0.0, 0.0)
+        lo, hi = LS[:, mid], US[:, mid]
+        key = (lo.tobytes(), hi.tobytes())
+        if self._mid_cache is not None and self._mid_cache[0] == key:
+            v = self._mid_cache[1]  # the same sampled bounds as at the last cold start
+        else:
+            with np.errstate(invalid="ignore"):
+                v = 0.5 * (lo + hi)
+            bad = ~np.isfinite(v)
+            if bad.any():  # nan_to_num(posinf=0, neginf=-0)
+                v[bad] = np.where(v[bad] < 0, -0.0, 0.0)
+            self._mid_cache = (key, v)
         g[:, mid] = v
         if "guess" in self.over_h:
             c, q = self.over_h["guess"]

@@ -763,7 +763,11 @@ def main():
                     help="C4 agents in total, split over the GPUs (0: skip)")
     ap.add_argument("--admm-iters", type=int, default=15)
     ap.add_argument("--nn-zones", type=int, default=1024, help="C5 NARX zones per GPU (0: skip)")
-    ap.add_argument("--c5-blocks", type=int, default=342,
+    # 341 blocks = 1023 zones, the block count closest to BASELINE configs[4]'s 1024 zones (342
+    # would be 1026); 1024 zones are one generation of the zone kernel (4 per CU x 256 CUs), and
+    # two zones past it wait for a second one: 2.53 -> 4.83 ms per zone launch, 347 -> 298 ADMM
+    # it/s on the leg (profiles/r04/s11)
+    ap.add_argument("--c5-blocks", type=int, default=341,
                     help="C5 ADMM blocks (3 zones+AHU+CCA) in total, split over the GPUs (0: skip)")
     ap.add_argument("--c5-iters", type=int, default=50)
     ap.add_argument("--mhe-agents", type=int, default=4096, help="MHE estimators per GPU (0: skip)")

@@ -493,25 +493,28 @@ def compile_all(verbose: bool = False):
 
     probs = {name: fn()[0].problem for name, fn in variants.items()}
     jobs = int(os.environ.get("MPCX_BUILD_JOBS", "4"))
+    label = {None: "", native.SMALL_FLEET: " small-fleet", native.MID_FLEET: " one-wave-per-SIMD"}
     with ThreadPoolExecutor(max_workers=jobs) as ex:  # hipcc processes: one per code object
-        futs = {(name, v): ex.submit(native.compile_model, pr.gen, False, v)
-                for name, pr in probs.items() for v in (None, native.SMALL_FLEET)}
-        for (name, v), fut in futs.items():
-            path = fut.result()
-            if v is None:
-                paths[name] = path
-            if verbose:
-                print(f"[mpcx] {name}{' small-fleet' if v else ''}: {path.name if path else 'workspace does not fit LDS'}")
+        # the one-wave-per-SIMD builds after the main ones (they read the main build's occupancy)
+        for group in ((None, native.SMALL_FLEET), (native.MID_FLEET,)):
+            futs = {(name, v): ex.submit(native.compile_model, pr.gen, False, v)
+                    for name, pr in probs.items() for v in group}
+            for (name, v), fut in futs.items():
+                path = fut.result()
+                if v is None:
+                    paths[name] = path
+                if verbose:
+                    print(f"[mpcx] {name}{label[v]}: {path.name if path else '-'}")
     # test build: the filter capped at FILTER_CAP_TEST entries (overflow parity with the oracle,
     # tests/test_gpu_ipm.py::test_gpu_filter_overflow_matches_oracle); MPCX_DEFINES names it
     saved = os.environ.get("MPCX_DEFINES")
     os.environ["MPCX_DEFINES"] = FILTER_CAP_DEFINES
     try:
         gen = cubic_room()[0].problem.gen
-        for v in (None, native.SMALL_FLEET):
+        for v in (None, native.SMALL_FLEET, native.MID_FLEET):
             path = native.compile_model(gen, False, v)
             if verbose:
-                print(f"[mpcx] cubic_room {FILTER_CAP_DEFINES}{' small-fleet' if v else ''}: {path.name if path else '-'}")
+                print(f"[mpcx] cubic_room {FILTER_CAP_DEFINES}{label[v]}: {path.name if path else '-'}")
     finally:
         if saved is None:
             os.environ.pop("MPCX_DEFINES", None)

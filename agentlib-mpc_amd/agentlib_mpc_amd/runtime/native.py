@@ -12,6 +12,7 @@ import ctypes
 import hashlib
 import os
 import pathlib
+import re
 import shutil
 import subprocess
 import threading
@@ -83,6 +84,7 @@ STATS_BYTES = ctypes.sizeof(Stats)
 EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
     "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_problem_small_fleet",
+    "mpcx_problem_mid_fleet",
     "mpcx_batch_solve", "mpcx_batch_solve_staged",
     "mpcx_admm_moments_size", "mpcx_admm_reduce_count", "mpcx_admm_moments", "mpcx_admm_finalize",
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
@@ -184,6 +186,7 @@ def load_library():
         lib.mpcx_reserve.argtypes = [vp, i32]
         lib.mpcx_workspace_bytes_per_agent.argtypes = [vp]
         lib.mpcx_problem_small_fleet.argtypes = [vp, ctypes.c_char_p, i32]
+        lib.mpcx_problem_mid_fleet.argtypes = [vp, ctypes.c_char_p, i32]
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
         lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp, vp]
         i64 = ctypes.c_int64
@@ -249,7 +252,9 @@ def _extra_defines() -> List[str]:
 
 #: small-fleet variant (workspace in LDS, one agent per CU; ``mpcx_problem_small_fleet``)
 SMALL_FLEET = "wslds"
-_VARIANT_DEFINES = {None: [], SMALL_FLEET: ["MPCX_WS_LDS"]}
+#: mid-fleet variant (one wave per SIMD, up to 512 registers; ``mpcx_problem_mid_fleet``)
+MID_FLEET = "w1"
+_VARIANT_DEFINES = {None: [], SMALL_FLEET: ["MPCX_WS_LDS"], MID_FLEET: ["MPCX_MIN_WAVES=1"]}
 
 
 def code_object_path(gen_key: str, variant: Optional[str] = None) -> pathlib.Path:
@@ -270,12 +275,20 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
     nofit = out.with_suffix(".nofit")
     if variant is not None and nofit.exists():
         return None
+    if variant == MID_FLEET:
+        # only where the main build's register budget is tighter than one wave per SIMD
+        base = compile_model(gen, verbose)
+        occ = base.with_suffix(".occ")
+        if not occ.exists() or int(occ.read_text() or "1") <= 1:
+            nofit.write_text("the main build already runs one wave per SIMD")
+            return None
     src = out.with_suffix(".hip")
     src.write_text(gen.source)
     tmp = out.with_suffix(".tmp")
     defs = _extra_defines() + _VARIANT_DEFINES[variant]
     cmd = [_hipcc(), "--genco", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17",
-           f"-I{INCLUDE}", f"-I{CSRC}", *[f"-D{d}" for d in defs], str(src), "-o", str(tmp)]
+           f"-I{INCLUDE}", f"-I{CSRC}", *[f"-D{d}" for d in defs], str(src), "-o", str(tmp),
+           "-Rpass-analysis=kernel-resource-usage"]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         if variant is not None:
@@ -283,13 +296,17 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
             # not fit LDS, or the per-agent LDS share is exceeded -- means "no such build";
             # the main code object serves every batch size.  The marker keeps the reason.
             if "workspace does not fit LDS" not in res.stderr:
-                warnings.warn(f"small-fleet build of {gen.key} failed; the HBM build serves every batch:\n"
+                name = {SMALL_FLEET: "small-fleet", MID_FLEET: "one-wave-per-SIMD"}.get(variant, variant)
+                warnings.warn(f"{name} build of {gen.key} failed; the main build serves every batch:\n"
                               f"{res.stderr[-800:]}")
             nofit.write_text(res.stderr[-4000:])
             return None
         raise NativeError(f"compiling {src} failed:\n{res.stderr[-4000:]}")
     if verbose and res.stderr:
         print(res.stderr)
+    if variant is None:  # the register budget's occupancy (mpcx_ipm_solve), for the w1 decision
+        occ = re.search(r"Function Name: mpcx_ipm_solve.*?Occupancy \[waves/SIMD\]: (\d+)", res.stderr, re.S)
+        out.with_suffix(".occ").write_text(occ.group(1) if occ else "1")
     os.replace(tmp, out)
     return out
 
@@ -322,6 +339,16 @@ class NativeProblem:
                     warnings.warn(f"mpcx_problem_small_fleet failed ({rc}) for {sp}; using the HBM build")
                 else:
                     self.small_fleet_path = sp
+        self.mid_fleet_path = None
+        if hsaco is None and os.environ.get("MPCX_MID_FLEET", "1") != "0":
+            # fleets of at most one agent per SIMD run the build with that register budget
+            mp = compile_model(gen, variant=MID_FLEET)
+            if mp is not None:
+                rc = self.lib.mpcx_problem_mid_fleet(handle, str(mp).encode(), -1)
+                if rc != 0:  # optional, as the small-fleet build
+                    warnings.warn(f"mpcx_problem_mid_fleet failed ({rc}) for {mp}; using the main build")
+                else:
+                    self.mid_fleet_path = mp
         self.options = default_options()
         self.nw = d["NX"] + d["N"] * (d["NV"] + d["NX"])
         self.ng_total = d["N"] * d["NG"]
@@ -352,6 +379,12 @@ class NativeProblem:
         rc = self.lib.mpcx_problem_small_fleet(self.handle, None, int(max_agents))
         if rc != 0:
             raise NativeError(f"mpcx_problem_small_fleet failed ({rc})")
+
+    def set_mid_fleet_max(self, max_agents: int):
+        """Largest batch launched on the one-wave-per-SIMD build: -1 four per CU (default), 0 never."""
+        rc = self.lib.mpcx_problem_mid_fleet(self.handle, None, int(max_agents))
+        if rc != 0:
+            raise NativeError(f"mpcx_problem_mid_fleet failed ({rc})")
 
     def workspace_bytes_per_agent(self) -> int:
         return int(self.lib.mpcx_workspace_bytes_per_agent(self.handle))

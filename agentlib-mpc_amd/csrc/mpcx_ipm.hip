@@ -487,6 +487,8 @@ constexpr int APC_TWO = apc_for(REST_BYTES + cmax(UFIX_BYTES, cmax(SLOT_BYTES, c
 #ifdef MPCX_WS_LDS
 static_assert(WS_LDS_BYTES + REST_BYTES + UFIX_BYTES + LDS_SLACK <= LDS_CU_ALL, "MPCX_WS_LDS: workspace does not fit LDS");
 constexpr int APC = 1;
+#elif defined(MPCX_APC)  // agents per CU chosen by the build (more than 16: 5-8 waves per SIMD)
+constexpr int APC = MPCX_APC;
 #else
 constexpr int APC = (APC_TWO >= 16 || APC_ONE < 4) ? APC_TWO : APC_ONE;
 #endif
@@ -4125,5 +4127,7 @@ extern "C" __global__ void mpcx_query(long* out) {
 #else
     out[9] = 0;
 #endif
+    out[10] = MIN_WAVES;  // waves per SIMD the register budget is compiled for
+    out[11] = APC;        // agents per CU the LDS share allows
   }
 }

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 8
+#define MPCX_API_VERSION 9
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -155,6 +155,14 @@ int64_t mpcx_workspace_bytes_per_agent(const mpcx_handle* h);
  * (max_agents < 0: the device's CU count, one generation; 0: never).  Returns
  * MPCX_ERR_MODULE if the code object is not such a variant of this structure. */
 int mpcx_problem_small_fleet(mpcx_handle* h, const char* code_object_path, int32_t max_agents);
+
+/* Optional (C ABI v9): the same structure compiled for one wave per SIMD (MPCX_MIN_WAVES=1: up
+ * to 512 registers per lane, where the main build's budget follows its LDS-limited occupancy,
+ * e.g. 128 at 16 agents per CU, and spills).  mpcx_batch_solve launches it for batches of at
+ * most max_agents agents that the small-fleet build does not take (max_agents < 0: four per CU,
+ * one generation at one wave per SIMD; 0: never).  Ignored (max 0) when the main build already
+ * runs one wave per SIMD.  Returns MPCX_ERR_MODULE if the code object is not such a variant. */
+int mpcx_problem_mid_fleet(mpcx_handle* h, const char* code_object_path, int32_t max_agents);
 
 /* Batched solve.  Shapes (agent-major, fp64, device):
  *   active [n_agents] int32 or NULL  agents with active[a] == 0 are skipped (their outputs

@@ -26,6 +26,7 @@ VARIANTS = {
     "lds14k_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=14000", "-DMPCX_MIN_WAVES=2"], None),
     "lds24k": (["-DMPCX_LDS_TARGET_OVERRIDE=24000"], None),
     "w2": (["-DMPCX_MIN_WAVES=2"], None),
+    "w3": (["-DMPCX_MIN_WAVES=3"], None),
     # 8 agents per CU: LDS share 160 KB / 8 and at most 256 VGPRs (2 waves per SIMD)
     "apc8_w2": (["-DMPCX_LDS_TARGET_OVERRIDE=20224", "-DMPCX_MIN_WAVES=2"], None),
     # 5 / 6 agents per CU with <= 256 registers: some SIMDs hold two waves
@@ -69,6 +70,10 @@ VARIANTS = {
     # r04: the one-sided state chain instead of the twisted one
     "chain_seq": (["-DMPCX_CHAIN_SEQ"], None),
     "lds_nofence": (["-DMPCX_WS_LDS", "-DMPCX_ELIM_FENCE=(void)0"], None),
+    # r04: more than 16 agents per CU for structures with a small LDS share and register need
+    "apc20": (["-DMPCX_APC=20"], None),
+    "apc24": (["-DMPCX_APC=24"], None),
+    "apc32": (["-DMPCX_APC=32"], None),
     "lds_asm_noreg": (["-DMPCX_WS_LDS", "-DMPCX_ASM_NOREG"], None),
 }
 

@@ -413,6 +413,7 @@ def test_gpu_small_fleet_build_matches_hbm_build():
     assert native.small_fleet_path is not None, "one_room's workspace fits LDS: the small-fleet build must load"
     T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
     out = {}
+    native.set_mid_fleet_max(0)  # the main build, not the one-wave-per-SIMD one, for "hbm"
     for mode, max_agents in (("lds", -1), ("hbm", 0)):
         native.set_small_fleet_max(max_agents)
         tw = T(w0)
@@ -421,6 +422,7 @@ def test_gpu_small_fleet_build_matches_hbm_build():
         torch.cuda.synchronize()
         out[mode] = (tw.cpu().numpy(), stats_to_dicts(st.cpu().numpy().tobytes()))
     native.set_small_fleet_max(-1)
+    native.set_mid_fleet_max(-1)
     (wl, sl), (wh, sh) = out["lds"], out["hbm"]
     assert [s["status"] for s in sl] == [s["status"] for s in sh]
     assert [s["iter_count"] for s in sl] == [s["iter_count"] for s in sh]
@@ -465,3 +467,37 @@ def test_gpu_staged_round_trip_equals_separate_calls():
     np.testing.assert_array_equal(out["staged"], out["separate"])
     w = out["staged"][:w0.size].reshape(w0.shape)
     assert np.isfinite(w).all() and not np.array_equal(w, w0)
+
+
+def test_gpu_mid_fleet_build_matches_main_build():
+    """The one-wave-per-SIMD build (``mpcx_problem_mid_fleet``, C ABI v9: the same structure
+    compiled for up to 512 registers per lane, launched for batches of at most four agents per
+    CU) against the main build on the same 600 C3 agents at the reference's settings: same
+    statuses and iteration counts, solutions to 1e-9 (same operations; the register budget --
+    and with it the spills and the instruction schedule -- differs, and the compiler contracts a
+    few products into FMAs differently: 10 of 72600 entries differ at ~1e-11, r04/s15)."""
+    import bench
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+
+    n = 600
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261015 + 7))
+    native = be._native()
+    assert native.mid_fleet_path is not None, "one_room's main build runs 4 waves per SIMD: the w1 build must load"
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    out = {}
+    for mode, max_agents in (("mid", -1), ("main", 0)):
+        native.set_mid_fleet_max(max_agents)
+        tw = T(w0)
+        st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device="cuda")
+        native.solve(T(p), T(lbw), T(ubw), tw, stats=st)
+        torch.cuda.synchronize()
+        out[mode] = (tw.cpu().numpy(), stats_to_dicts(st.cpu().numpy().tobytes()))
+    native.set_mid_fleet_max(-1)
+    (wm, sm), (wb, sb) = out["mid"], out["main"]
+    assert [s["status"] for s in sm] == [s["status"] for s in sb]
+    assert [s["iter_count"] for s in sm] == [s["iter_count"] for s in sb]
+    assert np.mean([s["status"] in (0, 1) for s in sm]) > 0.99
+    np.testing.assert_allclose(wm, wb, rtol=1e-9, atol=1e-10)

@@ -127,3 +127,18 @@ def test_small_fleet_variant_failure_is_not_fatal(tmp_path, monkeypatch):
     assert native.compile_model(gen, variant=native.SMALL_FLEET) is None  # marker: no retry
     with pytest.raises(native.NativeError):
         native.compile_model(gen)
+
+
+def test_one_wave_per_simd_build_only_where_the_main_build_is_tighter():
+    """The mid-fleet variant (``mpcx_problem_mid_fleet``, C ABI v9) is compiled only when the main
+    build's register budget allows more than one wave per SIMD (read from the compiler's resource
+    report into the ``.occ`` file next to the main code object): one_room (16 agents per CU, 4
+    waves per SIMD) gets it, the MHE (4 agents per CU, already one wave per SIMD) does not."""
+    from agentlib_mpc_amd import benchmarks as bm
+
+    gen = bm.one_room()[0].problem.gen
+    assert native.compile_model(gen, variant=native.MID_FLEET) is not None
+    assert int(native.code_object_path(gen.key).with_suffix(".occ").read_text()) == 4
+    gen = bm.mhe_room()[0].problem.gen
+    assert native.compile_model(gen, variant=native.MID_FLEET) is None
+    assert int(native.code_object_path(gen.key).with_suffix(".occ").read_text()) == 1

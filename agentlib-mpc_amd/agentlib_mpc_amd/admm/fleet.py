@@ -52,7 +52,6 @@ EXCHANGE = "exchange"
 NMOM = 5
 _ITER_WORD = 12  # int32 index of mpcx_stats.iter_count
 _STATUS_WORD = 13  # int32 index of mpcx_stats.status (6 doubles + iter_count)
-_RESTO_WORD = 15  # int32 index of mpcx_stats.n_restorations
 
 
 @dataclasses.dataclass
@@ -436,8 +435,8 @@ class ADMMFleet:
             for si, s in enumerate(c.slots):
                 x0[self.slot_rows[(ci, si)]] = s.initial[:, None]
         self.X[:R].copy_(t.as_tensor(x0, device=dev))
-        self._ok_count = t.zeros(1, dtype=t.int64, device=dev)
-        self._fb_count = t.zeros(1, dtype=t.int64, device=dev)  # restoration-phase calls of the solves
+        # [converged solves, restoration-phase calls] of the round's batched solves
+        self._counts = t.zeros(2, dtype=t.int64, device=dev)
         #: a list to record every iteration's local-solve (iter_count, status) per class (device
         #: copies, [n, 2] int32) -- the per-agent counterpart of the reference's per-solve stats;
         #: None (the default) records nothing
@@ -524,17 +523,11 @@ class ADMMFleet:
             for st_ in streams:
                 main.wait_stream(st_)
         for c in self.classes:
-            words = c.ST.view(t.int32).view(c.n, STATS_BYTES // 4)
             if self.solve_trace is not None:
+                words = c.ST.view(t.int32).view(c.n, STATS_BYTES // 4)
                 self.solve_trace.append((c.name, words[:, _ITER_WORD:_STATUS_WORD + 1].clone()))
-            st = words[:, _STATUS_WORD]
-            ok = (st == 0) | (st == 1)
-            fb = words[:, _RESTO_WORD]
-            if self._masked:
-                ok &= c.ACTIVE != 0
-                fb = fb * (c.ACTIVE != 0)
-            self._ok_count += ok.sum()
-            self._fb_count += fb.sum()
+            # converged solves and restoration calls: one launch per class (mpcx_stats_count)
+            ops.stats_count(c.n, c.ST, c.ACTIVE if self._masked else None, self._counts)
 
     def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False, reduce: bool = True):
         """Mean (+ exchange diffs) from the current locals; with ``apply_multipliers``
@@ -690,8 +683,7 @@ class ADMMFleet:
         self._update_means(rho0, apply_multipliers=False, per_block=True)
         shift = int(len(self.classes[0].coupling_grid) / self.classes[0].horizon)
         self._shift_all(shift)
-        self._ok_count.zero_()
-        self._fb_count.zero_()
+        self._counts.zero_()
         tot = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
         ops.block_stop(0, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK)  # the round's first stamp
         ran = 0
@@ -736,9 +728,9 @@ class ADMMFleet:
         self.history.extend(records)
         self.rounds += 1
         return {"iterations": last, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
-                "converged_solves": int(self._ok_count.item()), "block_iterations": iters,
+                "converged_solves": int(self._counts[0].item()), "block_iterations": iters,
                 "block_converged": conv_b, "block_records": block_records, "block_is_global": self.block_is_global.copy(),
-                "restorations": int(self._fb_count.item()), "loop_iterations": ran}
+                "restorations": int(self._counts[1].item()), "loop_iterations": ran}
 
     def _expand_blocks(self, active_b):
         """Per-block penalties and freeze masks (device) to the groups and the agents (with the
@@ -781,8 +773,7 @@ class ADMMFleet:
         hist = self.torch.zeros((max(max_iterations, 1), ADMM_TOTALS), dtype=self.torch.float64,
                                 device=self.device)
         t0 = time.perf_counter()
-        self._ok_count.zero_()
-        self._fb_count.zero_()
+        self._counts.zero_()
         for it in range(max_iterations):
             self._solve_all(rho)
             tot = self._update_means(rho, apply_multipliers=True)
@@ -795,8 +786,8 @@ class ADMMFleet:
         self.history.extend(records)
         self.rounds += 1
         return {"iterations": max_iterations, "converged": None, "records": records, "wall_s": wall,
-                "converged_solves": int(self._ok_count.item()),
-                "restorations": int(self._fb_count.item())}
+                "converged_solves": int(self._counts[0].item()),
+                "restorations": int(self._counts[1].item())}
 
     # ------------------------------------------------------------------ outputs
     def solutions(self, class_name: str) -> np.ndarray:

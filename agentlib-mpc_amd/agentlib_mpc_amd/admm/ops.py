@@ -106,6 +106,10 @@ class NativeADMMOps:
                                                   _p(out_active), _p(out_rho), self.stream),
                   "mpcx_admm_block_expand")
 
+    def stats_count(self, n, stats, active, counts):
+        """counts[0] += converged agents, counts[1] += their restoration calls (one launch)."""
+        self._chk(self.lib.mpcx_stats_count(n, _p(stats), _p(active), _p(counts), self.stream), "mpcx_stats_count")
+
     def clock_hz(self) -> float:
         khz = int(self.lib.mpcx_device_clock_khz())
         if khz <= 0:

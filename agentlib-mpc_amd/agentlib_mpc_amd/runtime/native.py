@@ -90,7 +90,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
-    "mpcx_admm_block_stop", "mpcx_admm_block_expand", "mpcx_device_clock_khz",
+    "mpcx_admm_block_stop", "mpcx_admm_block_expand", "mpcx_device_clock_khz", "mpcx_stats_count",
 ]
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
 KERNEL_ABI = 7  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
@@ -213,6 +213,7 @@ def load_library():
                                              vp, vp]
         lib.mpcx_admm_block_expand.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp]
         lib.mpcx_device_clock_khz.restype = i64
+        lib.mpcx_stats_count.argtypes = [i32, vp, vp, vp, vp]
         for name in EXPORTED_SYMBOLS:
             getattr(lib, name)  # raises AttributeError if a symbol is missing
         _lib = lib

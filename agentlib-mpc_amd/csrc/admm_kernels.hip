@@ -463,7 +463,40 @@ __global__ void k_block_expand(int n, const int* __restrict__ idx, const int* __
   if (out_active) out_active[i] = (active_b[b] != 0 && (part == nullptr || part[i] != 0)) ? 1 : 0;
   if (out_rho) out_rho[i] = rho_b[b];
 }
+
+// a class's batched solve, counted for the fleet's bookkeeping: counts[0] += agents whose status
+// is Solve_Succeeded / Solved_To_Acceptable_Level, counts[1] += their restoration-phase calls;
+// agents with active[i] == 0 (frozen blocks, not solved) are skipped.  One atomic per wave.
+__global__ void k_stats_count(int n, const mpcx_stats* __restrict__ st, const int* __restrict__ active,
+                              unsigned long long* __restrict__ counts) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int ok = 0, fb = 0;
+  if (i < n && (active == nullptr || active[i] != 0)) {
+    const int s = st[i].status;
+    ok = (s == 0 || s == 1) ? 1 : 0;
+    fb = st[i].n_restorations;
+  }
+#pragma unroll
+  for (int o = WAVE / 2; o > 0; o >>= 1) {
+    ok += __shfl_xor(ok, o, WAVE);
+    fb += __shfl_xor(fb, o, WAVE);
+  }
+  if ((threadIdx.x & (WAVE - 1)) == 0) {
+    if (ok) atomicAdd(counts, (unsigned long long)ok);
+    if (fb) atomicAdd(counts + 1, (unsigned long long)fb);
+  }
+}
 }  // namespace
+
+extern "C" int mpcx_stats_count(int32_t n, const mpcx_stats* stats, const int32_t* active, int64_t* counts,
+                                void* stream) {
+  if (n < 0 || (n > 0 && (!stats || !counts))) return MPCX_ERR_ARG;
+  if (n == 0) return MPCX_OK;
+  hipLaunchKernelGGL(k_stats_count, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, stats, active,
+                     (unsigned long long*)counts);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
 
 extern "C" int mpcx_admm_block_stop(int32_t n_blocks, int32_t it, const double* totals, int32_t use_relative,
                                     double abs_tol, double rel_tol, double primal_tol, double dual_tol,

@@ -318,6 +318,13 @@ int mpcx_admm_block_expand(int32_t n, const int32_t* idx, const int32_t* active_
 /* Rate of the device wall clock the stopping test stamps (kHz). */
 int64_t mpcx_device_clock_khz(void);
 
+/* Fleet bookkeeping of one batched solve (C ABI v9): counts[0] += agents whose status is
+ * MPCX_SOLVE_SUCCEEDED or MPCX_SOLVED_TO_ACCEPTABLE, counts[1] += their restoration-phase calls
+ * (mpcx_stats.n_restorations); agents with active[i] == 0 are skipped (active NULL: all).
+ * counts: device int64[2], accumulated across calls (the converged-solve count the reference's
+ * modules log per solve, `mpc.py:397-400`, summed over a round). */
+int mpcx_stats_count(int32_t n, const mpcx_stats* stats, const int32_t* active, int64_t* counts, void* stream);
+
 /* ---- NLP vector <-> trajectory moves (no host round trip) ----------------------------
  * dst[dst_rows[a]][t] <- src[a*src_ld + cols[t]]: the coupling trajectories out of the
  * solutions w  <- Results[coupling.name] in CoordinatedADMM.optimize

@@ -192,5 +192,16 @@ class CpuFleetOps:
         if out_rho is not None:
             out_rho.numpy().reshape(-1)[:] = rho_b.numpy().reshape(-1)[i]
 
+    def stats_count(self, n, stats, active, counts):
+        """numpy restatement of ``mpcx_stats_count`` (admm_kernels.hip k_stats_count)."""
+        from agentlib_mpc_amd.runtime.native import STATS_BYTES
+
+        w = stats.numpy().view(np.int32).reshape(n, STATS_BYTES // 4)
+        on = np.ones(n, bool) if active is None else active.numpy() != 0
+        st = w[:, 13]
+        c = counts.numpy()
+        c[0] += int((((st == 0) | (st == 1)) & on).sum())
+        c[1] += int(w[:, 15][on].sum())
+
     def clock_hz(self) -> float:
         return 1e9

@@ -529,3 +529,31 @@ def test_gpu_block_stop_matches_restatement(crit):
         np.testing.assert_allclose(g["exp"][1], c["exp"][1], rtol=1e-15)
     assert 0 < int(state["cpu"]["nact"][1]) < nb          # some blocks stopped, some did not
     assert (state["gpu"]["clk"].cpu().numpy()[1:] >= state["gpu"]["clk"].cpu().numpy()[:-1]).all()
+
+
+def test_gpu_stats_count_matches_restatement():
+    """``mpcx_stats_count`` (C ABI v9, one launch per class and ADMM iteration instead of a chain of
+    tensor ops) against its numpy restatement (`oracle/cpu_fleet.py`) on random stats records of
+    5000 agents (statuses -4..3, restoration counts 0..3), with and without an active mask,
+    accumulated over two calls."""
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES
+    from oracle.cpu_fleet import CpuFleetOps
+
+    rng = np.random.default_rng(11)
+    n = 5000
+    words = np.zeros((n, STATS_BYTES // 4), np.int32)
+    words[:, 13] = rng.integers(-4, 4, n)  # status
+    words[:, 15] = rng.integers(0, 4, n)   # n_restorations
+    raw = words.view(np.uint8).ravel()
+    act = (rng.random(n) < 0.7).astype(np.int32)
+    got, want = {}, {}
+    for name, ops, dev in (("gpu", NativeADMMOps(), "cuda"), ("cpu", CpuFleetOps(), "cpu")):
+        st = torch.as_tensor(raw, device=dev)
+        counts = torch.zeros(2, dtype=torch.int64, device=dev)
+        ops.stats_count(n, st, None, counts)
+        ops.stats_count(n, st, torch.as_tensor(act, device=dev), counts)
+        (got if name == "gpu" else want)["c"] = counts.cpu().numpy()
+    ok = (words[:, 13] == 0) | (words[:, 13] == 1)
+    expect = [ok.sum() + (ok & (act != 0)).sum(), words[:, 15].sum() + words[:, 15][act != 0].sum()]
+    np.testing.assert_array_equal(want["c"], expect)
+    np.testing.assert_array_equal(got["c"], expect)

@@ -553,12 +553,14 @@ class ADMMFleet:
             self.dist.all_reduce(self.MOM[:self.reduce_len], group=self.group)
         ops.finalize(0, self.n_global, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
                      self.MEAN, self.DMEAN, totals)
-        if apply_multipliers:
+        # consensus rows of exchange groups are never read; exchange rows of consensus groups neither
+        # (so a fleet of one kind launches only its own update)
+        if apply_multipliers and not self.exchange_flags.all():
             ops.consensus_multipliers(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, rho, rho_g, act_g,
                                       self.LAMR, row_on=self.ROW_ON)
-        # consensus rows of exchange groups are never read; exchange rows of consensus groups neither
-        ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT,
-                            apply_multipliers, rho, rho_g, act_g, row_on=self.ROW_ON)
+        if exch is not None:
+            ops.exchange_update(G, T, self.GSTART, self.max_rows, self.X, self.MEAN, self.DIFF, self.GMULT,
+                                apply_multipliers, rho, rho_g, act_g, row_on=self.ROW_ON)
         return totals.view(nb, ADMM_TOTALS)
 
     def _shift_all(self, shift: int):

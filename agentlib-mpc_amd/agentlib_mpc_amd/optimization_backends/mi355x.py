@@ -209,7 +209,7 @@ class MI355XBackend(OptimizationBackend):
         the previous slot of each entry's agent (-1 cold), None to keep the optima by slot."""
         import torch
 
-        from agentlib_mpc_amd.optimization_backends.plugin_batch import ResidentBatch, RowSource
+        from agentlib_mpc_amd.optimization_backends.plugin_batch import ResidentBatch
         from agentlib_mpc_amd.optimization_backends.problem import FleetResults
         from agentlib_mpc_amd.runtime.native import StatsView, stats_array
 
@@ -230,7 +230,7 @@ class MI355XBackend(OptimizationBackend):
             snap = rb.update(batch_vars, now)
         w, raw = rb.solve()
         stats = StatsView(stats_array(raw), {"t_wall_total": time.perf_counter() - t0})
-        return FleetResults(prob, prob.marshal, None, None, None, w, stats, rows=RowSource(rb, snap))
+        return FleetResults(prob, prob.marshal, None, None, None, w, stats, rows=rb.row_source(snap))
 
     def solve_arrays(self, p, lbw, ubw, w0, lbg=None, ubg=None, result_bounds=None):
         """Batched solve of reference-layout NLP inputs [n, .] (host arrays): device

@@ -75,6 +75,18 @@ class RowSource:
         return p, ls, us
 
 
+class MirrorRows:
+    """:class:`RowSource` of a small batch: the host mirrors already hold every agent's
+    reference-layout p and sampled bounds after :meth:`ResidentBatch.update` (the same values
+    RowSource rebuilds from the read columns), copied at solve time."""
+
+    def __init__(self, p: np.ndarray, ls: np.ndarray, us: np.ndarray):
+        self.p, self.ls, self.us = p, ls, us
+
+    def rows(self, i: int) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        return self.p[i].copy(), self.ls[i].copy(), self.us[i].copy()
+
+
 def _has_nan(val) -> bool:
     """NaN in a read column (an (n,) array, or {grid: samples})."""
     if isinstance(val, np.ndarray):
@@ -463,6 +475,13 @@ class ResidentBatch:
         if rows.size:
             prev = self.cold_rows if self.cold_rows is not None else np.zeros(0, np.int64)
             self.cold_rows = np.union1d(prev, rows).astype(np.int64)
+
+    def row_source(self, snapshot):
+        """What :class:`~.problem.FleetResults` rebuilds each agent's reference-layout rows
+        from: the host mirrors of a small batch (copied now), else the call's read columns."""
+        if self.small:
+            return MirrorRows(self.hP.copy(), self.hLS.copy(), self.hUS.copy())
+        return RowSource(self, snapshot)
 
     def restart_cold(self):
         """Every agent's next guess is the cold-start guess (no remembered optimum)."""

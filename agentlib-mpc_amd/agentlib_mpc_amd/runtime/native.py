@@ -491,13 +491,22 @@ class NativeProblem:
 _STATS_DOUBLES = ("obj", "primal_inf", "dual_inf", "compl_inf", "mu", "obj_scale")
 
 
+_STATS_DTYPE = None
+
+
 def stats_array(raw_bytes):
-    """``mpcx_stats`` records as a numpy structured array (no per-agent objects)."""
+    """``mpcx_stats`` records as a numpy structured array (no per-agent objects); a contiguous
+    uint8 array is viewed in place, anything else copied."""
     import numpy as np
 
-    dt = np.dtype([(n, "<f8") for n in _STATS_DOUBLES] + [(n, "<i4") for n in _STATS_INTS])
-    assert dt.itemsize == STATS_BYTES
-    return np.frombuffer(bytes(raw_bytes), dtype=dt)
+    global _STATS_DTYPE
+    if _STATS_DTYPE is None:
+        _STATS_DTYPE = np.dtype([(n, "<f8") for n in _STATS_DOUBLES] + [(n, "<i4") for n in _STATS_INTS])
+        assert _STATS_DTYPE.itemsize == STATS_BYTES
+    if isinstance(raw_bytes, np.ndarray) and raw_bytes.dtype == np.uint8 and raw_bytes.ndim == 1 \
+            and raw_bytes.flags.c_contiguous and raw_bytes.size % STATS_BYTES == 0:
+        return raw_bytes.view(_STATS_DTYPE)
+    return np.frombuffer(bytes(raw_bytes), dtype=_STATS_DTYPE)
 
 
 class StatsView:
@@ -517,14 +526,17 @@ class StatsView:
     def __getitem__(self, i):
         if isinstance(i, slice):
             return [self[k] for k in range(*i.indices(len(self)))]
-        s = self.array[i]
-        st = int(s["status"])
-        d = {"obj": float(s["obj"]), "primal_inf": float(s["primal_inf"]), "dual_inf": float(s["dual_inf"]),
-             "compl_inf": float(s["compl_inf"]), "mu": float(s["mu"]), "obj_scale": float(s["obj_scale"]),
-             "status": st, "return_status": STATUS_NAMES.get(st, str(st)), "success": st in (0, 1)}
+        # one conversion of the record to Python numbers (float / int per field), keys in the
+        # order of the result files' stats columns
+        v = dict(zip(self.array.dtype.names, self.array[i].tolist()))
+        st = v["status"]
+        d = {k: v[k] for k in _STATS_DOUBLES}
+        d["status"] = st
+        d["return_status"] = STATUS_NAMES.get(st, str(st))
+        d["success"] = st in (0, 1)
         for k in _STATS_INTS:
             if k != "status":
-                d[k] = int(s[k])
+                d[k] = v[k]
         d.update(self.extra)
         return d
 

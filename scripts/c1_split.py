@@ -16,7 +16,7 @@ def main():
     import torch
 
     from agentlib_mpc_amd import benchmarks as bm
-    from agentlib_mpc_amd.optimization_backends.plugin_batch import RowSource
+    from agentlib_mpc_amd.optimization_backends.plugin_batch import RowSource  # noqa: F401
     from agentlib_mpc_amd.optimization_backends.problem import FleetResults
     from agentlib_mpc_amd.runtime.native import StatsView, stats_array
 

@@ -551,8 +551,9 @@ class ADMMFleet:
                      self.MEAN, self.DMEAN, totals)
         if self.world > 1 and reduce and self.reduce_len:
             self.dist.all_reduce(self.MOM[:self.reduce_len], group=self.group)
-        ops.finalize(0, self.n_global, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
-                     self.MEAN, self.DMEAN, totals)
+        if self.n_global:  # the groups spanning ranks, after their moments were summed
+            ops.finalize(0, self.n_global, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
+                         self.MEAN, self.DMEAN, totals)
         # consensus rows of exchange groups are never read; exchange rows of consensus groups neither
         # (so a fleet of one kind launches only its own update)
         if apply_multipliers and not self.exchange_flags.all():

@@ -234,6 +234,13 @@ step_s20() {
   echo "exit $?"
 }
 
+step_s21() {
+  # MHE per-phase cycles after the register-image elimination and the twisted chain
+  mkdir -p gpurun_out/s21
+  MODEL=mhe_room timeout -k 10 600 python -u scripts/prof_phases.py > gpurun_out/s21/phases_mhe.txt 2>&1
+  echo "exit $?"
+}
+
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }
 "$fn"

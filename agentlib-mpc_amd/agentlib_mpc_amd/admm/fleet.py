@@ -27,10 +27,10 @@ own ``ADMMCoordinator`` would stop (`admm_coordinator.py:284-309`).
 
 Multi-GPU: one process per GPU, each holding a contiguous slice of every
 class's agents.  Aliases whose participants live on several ranks are "global
-groups"; their per-(group, t) moments (and the residual partial sums of the
-rank-local groups) travel in ONE ``all_reduce(SUM)`` per ADMM iteration
-(`include/mpcx.h`, ``mpcx_admm_moments``).  No other collective is on the data
-path.
+groups"; their per-(group, t) moments, the residual totals of the blocks spanning ranks and
+the coordinated loop's count of blocks still active (one control double) travel in ONE
+``all_reduce(SUM)`` per ADMM iteration (`include/mpcx.h`, ``mpcx_admm_reduce_count``).  No
+other collective is on the data path.
 """
 
 from __future__ import annotations
@@ -45,7 +45,7 @@ from typing import Dict, List, Optional, Sequence, Union
 import numpy as np
 
 from agentlib_mpc_amd.data_structures import admm_datatypes as adt
-from agentlib_mpc_amd.runtime.native import ADMM_TOTALS, STATS_BYTES, admm_reduce_count
+from agentlib_mpc_amd.runtime.native import ADMM_CONTROL, ADMM_TOTALS, STATS_BYTES, admm_reduce_count
 
 CONSENSUS = "consensus"
 EXCHANGE = "exchange"
@@ -398,11 +398,17 @@ class ADMMFleet:
         self.GSTART = t.as_tensor(self.gstart, dtype=i32, device=dev)
         self.S = NMOM * T + 1
         nb = self.n_blocks
-        self.MOM = t.zeros(self.ops.moments_size(max(G, 1), nb, T), dtype=f64, device=dev)
+        # [control][moments buffer]: the all-reduce range starts at the control double (the
+        # coordinated loop's count of blocks still active), then the global groups' moments and
+        # the totals of the blocks spanning ranks (numbered first), as the C ABI defines it
+        # (include/mpcx.h mpcx_admm_reduce_count, v10); the kernels get the moments buffer
+        self.MOMBUF = t.zeros(ADMM_CONTROL + self.ops.moments_size(max(G, 1), nb, T), dtype=f64, device=dev)
+        self.CONTROL = self.MOMBUF[:ADMM_CONTROL]
+        self.MOM = self.MOMBUF[ADMM_CONTROL:]
         self.totals_off = self.n_global * self.S
-        # all-reduce range: global groups' moments + the totals of the blocks spanning ranks
-        # (numbered first), as the C ABI defines it (include/mpcx.h mpcx_admm_reduce_count)
         self.reduce_len = admm_reduce_count(self.n_global, self.n_global_blocks, T) if self.world > 1 else 0
+        #: all-reduces issued (the one collective per ADMM iteration; tests count them)
+        self.n_collectives = 0
         # per-block coordinator state on the device: penalty, group freeze mask
         self.BLOCK_G = t.as_tensor(self.block_of_group if G else np.zeros(1, np.int32), dtype=i32, device=dev)
         self.RHO_B = t.zeros((nb, 1), dtype=f64, device=dev)
@@ -529,28 +535,32 @@ class ADMMFleet:
             # converged solves and restoration calls: one launch per class (mpcx_stats_count)
             ops.stats_count(c.n, c.ST, c.ACTIVE if self._masked else None, self._counts)
 
-    def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False, reduce: bool = True):
+    def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False):
         """Mean (+ exchange diffs) from the current locals; with ``apply_multipliers``
         also the multiplier update.  Returns the residual totals [n_blocks][8] (device).
-        ``per_block``: per-group penalties and freeze masks of the coordinated run.
-        ``reduce``: take part in the all-reduce (every rank must pass the same value; False
-        only once every block spanning ranks is frozen)."""
+        ``per_block``: per-group penalties and freeze masks of the coordinated run.  With
+        several ranks every call is the iteration's one all-reduce (every rank calls it the
+        same number of times: the ranks iterate in lockstep)."""
         ops, T, G, nb = self.ops, self.T, self.G, self.n_blocks
-        if G == 0:
+        if G == 0 and self.world == 1:
             return None
         rho_g = self.RHO_G if per_block else None
         act_g = self.ACTIVE_G if per_block and self._masked else None
         blk = self.BLOCK_G if nb > 1 else None
-        self.MOM.zero_()
-        ops.moments(G, self.n_global, nb, T, self.GSTART, self.max_rows, self.X, self.LAMR, self.MEAN, self.MOM,
-                    row_on=self.ROW_ON)
+        self.MOM.zero_()  # the moments buffer only: the control double keeps its value
         totals = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
         exch = self.EXCH if self.exchange_flags.any() else None
         gm = self.GMULT if exch is not None else None
-        ops.finalize(self.n_global, G, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
-                     self.MEAN, self.DMEAN, totals)
-        if self.world > 1 and reduce and self.reduce_len:
-            self.dist.all_reduce(self.MOM[:self.reduce_len], group=self.group)
+        if G:
+            ops.moments(G, self.n_global, nb, T, self.GSTART, self.max_rows, self.X, self.LAMR, self.MEAN,
+                        self.MOM, row_on=self.ROW_ON)
+            ops.finalize(self.n_global, G, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
+                         self.MEAN, self.DMEAN, totals)
+        if self.world > 1:
+            self.dist.all_reduce(self.MOMBUF[:self.reduce_len], group=self.group)
+            self.n_collectives += 1
+        if G == 0:
+            return None
         if self.n_global:  # the groups spanning ranks, after their moments were summed
             ops.finalize(0, self.n_global, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
                          self.MEAN, self.DMEAN, totals)
@@ -656,11 +666,13 @@ class ADMMFleet:
         The stopping test runs on the device (``mpcx_admm_block_stop``, one thread per block,
         after each iteration's residual totals): the block penalties, freeze masks, records and
         iteration counts stay in HBM, so an iteration issues launches only.  The host reads the
-        number of blocks still active every ``check_every`` iterations (one small all-reduce of
-        it across ranks first) and the records once, after the round; iterations run past the
-        last block's stop before that check are no-ops (every agent and group frozen) and are
-        not counted.  Per-iteration wall times are device-clock stamps of the end of each
-        iteration relative to the round's first stamp.
+        number of blocks still active every ``check_every`` iterations and the records once,
+        after the round; iterations run past the last block's stop before that check are no-ops
+        (every agent and group frozen) and are not counted.  With several ranks the count
+        travels in the control double of the iteration's one all-reduce (C ABI v10): after the
+        reduce it is the count over all ranks after the PREVIOUS iteration, so every rank leaves
+        the loop at the same iteration without a second collective.  Per-iteration wall times
+        are device-clock stamps of the end of each iteration relative to the round's first stamp.
 
         Returns ``iterations`` (the last iteration any block ran), ``converged`` (all blocks),
         ``block_iterations`` / ``block_converged`` / ``block_records`` per block and
@@ -683,27 +695,31 @@ class ADMMFleet:
         self._masked = True
         crit = (1 if use_relative_tolerances else 0, abs_tol, rel_tol, primal_tol, dual_tol,
                 penalty_change_threshold, penalty_change_factor)
+        coll0 = self.n_collectives
         self._update_means(rho0, apply_multipliers=False, per_block=True)
         shift = int(len(self.classes[0].coupling_grid) / self.classes[0].horizon)
         self._shift_all(shift)
         self._counts.zero_()
         tot = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
-        ops.block_stop(0, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK)  # the round's first stamp
-        ran = 0
+        multi = self.world > 1
+        ctrl = self.CONTROL if multi else None
+        # the round's first stamp (and, with several ranks, the starting count into the control)
+        ops.block_stop(0, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK, ctrl)
+        ran = executed = 0
+        every = max(int(check_every), 1)
         for it in range(1, n_it + 1):
             self._solve_all(rho0)
             # ranks iterate in lockstep (the loop exit below is agreed on), so every rank takes
             # part in every iteration's all-reduce; frozen groups' moments travel but are not used
-            tot = self._update_means(rho0, apply_multipliers=True, per_block=True, reduce=True)
-            ops.block_stop(it, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK)
+            tot = self._update_means(rho0, apply_multipliers=True, per_block=True)
+            executed = it
+            if multi and it > 1 and (it - 1) % every == 0 and float(self.CONTROL.item()) == 0.0:
+                break  # every block on every rank had stopped by iteration it - 1: this one was a no-op
+            ops.block_stop(it, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK, ctrl)
             self._expand_blocks(ACTIVE_B)
             ran = it
-            if it % max(int(check_every), 1) == 0 or it == n_it:
-                left = NACT[it:it + 1].to(t.float64)
-                if self.world > 1:
-                    self.dist.all_reduce(left, group=self.group)
-                if float(left.item()) == 0.0:
-                    break
+            if not multi and (it % every == 0 or it == n_it) and int(NACT[it].item()) == 0:
+                break
         self._sync()
         # the next round starts from full penalties and no freeze mask
         self._masked = False
@@ -733,7 +749,8 @@ class ADMMFleet:
         return {"iterations": last, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
                 "converged_solves": int(self._counts[0].item()), "block_iterations": iters,
                 "block_converged": conv_b, "block_records": block_records, "block_is_global": self.block_is_global.copy(),
-                "restorations": int(self._counts[1].item()), "loop_iterations": ran}
+                "restorations": int(self._counts[1].item()), "loop_iterations": ran,
+                "iterations_executed": executed, "collectives": self.n_collectives - coll0}
 
     def _expand_blocks(self, active_b):
         """Per-block penalties and freeze masks (device) to the groups and the agents (with the

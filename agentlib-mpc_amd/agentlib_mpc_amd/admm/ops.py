@@ -93,13 +93,14 @@ class NativeADMMOps:
                   "mpcx_admm_exchange_update_masked")
 
     # -- the coordinators' stopping test (include/mpcx.h mpcx_admm_block_stop / _expand) ----
-    def block_stop(self, it, totals, crit, rho_b, active_b, iters_b, record, n_active, clock):
+    def block_stop(self, it, totals, crit, rho_b, active_b, iters_b, record, n_active, clock, control=None):
         """``crit`` = (use_relative, abs_tol, rel_tol, primal_tol, dual_tol, change_threshold,
-        change_factor); device state tensors updated in place."""
+        change_factor); device state tensors updated in place.  ``control``: the all-reduce's
+        control slot (float64 [1]), receives n_active[it] (C ABI v10)."""
         nb = active_b.shape[0]
         self._chk(self.lib.mpcx_admm_block_stop(nb, it, _p(totals), int(crit[0]), *[float(v) for v in crit[1:]],
                                                 _p(rho_b), _p(active_b), _p(iters_b), _p(record), _p(n_active),
-                                                _p(clock), self.stream), "mpcx_admm_block_stop")
+                                                _p(clock), _p(control), self.stream), "mpcx_admm_block_stop")
 
     def block_expand(self, idx, active_b, rho_b, part, out_active, out_rho):
         self._chk(self.lib.mpcx_admm_block_expand(idx.shape[0], _p(idx), _p(active_b), _p(rho_b), _p(part),

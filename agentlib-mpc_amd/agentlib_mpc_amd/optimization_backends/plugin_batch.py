@@ -443,12 +443,17 @@ class ResidentBatch:
     def permute_warm_starts(self, src: np.ndarray):
         """Entry i takes the warm start of the previous call's slot src[i] (-1: cold start,
         applied by the next update).  Same batch size; the inputs are re-read by update()
-        (a column whose per-entry values moved differs from the snapshot and is re-applied)."""
+        (a column whose per-entry values moved differs from the snapshot and is re-applied).
+        Pending cold starts (slots whose last solve came back NaN, in the OLD numbering) move
+        with their agents: entry i is cold when src[i] < 0 or src[i] was cold."""
         src = np.asarray(src, np.int64)
         if np.array_equal(src, np.arange(self.n)):
             return
-        hit = np.flatnonzero(src >= 0)
-        cold = np.flatnonzero(src < 0)
+        was_cold = self.cold_rows if self.cold_rows is not None else np.zeros(0, np.int64)
+        self.cold_rows = None
+        cold_src = np.isin(src, was_cold)
+        hit = np.flatnonzero((src >= 0) & ~cold_src)
+        cold = np.flatnonzero((src < 0) | cold_src)
         if hit.size:
             rows = self.torch.as_tensor(src[hit], device=self.dev)
             dst = self.torch.as_tensor(hit, device=self.dev)
@@ -461,8 +466,10 @@ class ResidentBatch:
 
     def adopt_warm_starts(self, old: "ResidentBatch", src: np.ndarray):
         """A new batch (new size): entry i takes the warm start of slot src[i] of the old
-        batch (-1: keeps its cold-start guess)."""
+        batch (-1, or an old slot whose last solve came back NaN: keeps its cold-start guess)."""
         src = np.asarray(src, np.int64)
+        if old.cold_rows is not None and old.cold_rows.size:
+            src = np.where(np.isin(src, old.cold_rows), -1, src)
         hit = np.flatnonzero(src >= 0)
         if not hit.size:
             return

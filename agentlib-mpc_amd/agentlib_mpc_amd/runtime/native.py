@@ -93,6 +93,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_admm_block_stop", "mpcx_admm_block_expand", "mpcx_device_clock_khz", "mpcx_stats_count",
 ]
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
+ADMM_CONTROL = 1  # MPCX_ADMM_CONTROL: control doubles before the moments buffer (C ABI v10)
 KERNEL_ABI = 7  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
 
 _lib = None
@@ -210,7 +211,7 @@ def load_library():
         lib.mpcx_scatter_rows.argtypes = [i32, i32, vp, vp, vp, i64, vp, vp]
         lib.mpcx_fill_column.argtypes = [i32, vp, i64, i32, f64, vp]
         lib.mpcx_admm_block_stop.argtypes = [i32, i32, vp, i32, f64, f64, f64, f64, f64, f64, vp, vp, vp, vp, vp,
-                                             vp, vp]
+                                             vp, vp, vp]
         lib.mpcx_admm_block_expand.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp]
         lib.mpcx_device_clock_khz.restype = i64
         lib.mpcx_stats_count.argtypes = [i32, vp, vp, vp, vp]
@@ -221,8 +222,8 @@ def load_library():
 
 
 def admm_reduce_count(n_global: int, n_global_blocks: int, T: int) -> int:
-    """Doubles of the ADMM moments buffer that are all-reduced over the ranks
-    (``mpcx_admm_reduce_count``, host arithmetic of the C ABI: no GPU call)."""
+    """Doubles all-reduced over the ranks per ADMM iteration, from the control slot before the
+    moments buffer on (``mpcx_admm_reduce_count``, host arithmetic of the C ABI: no GPU call)."""
     n = int(load_library().mpcx_admm_reduce_count(int(n_global), int(n_global_blocks), int(T)))
     if n < 0:
         raise NativeError(f"mpcx_admm_reduce_count({n_global}, {n_global_blocks}, {T}) failed ({n})")
@@ -255,6 +256,9 @@ def _extra_defines() -> List[str]:
 SMALL_FLEET = "wslds"
 #: mid-fleet variant (one wave per SIMD, up to 512 registers; ``mpcx_problem_mid_fleet``)
 MID_FLEET = "w1"
+#: compiler messages of the kernel's own static_asserts that mean "this structure does not fit
+#: the variant" (permanent for the code object's source hash)
+_NOFIT_MESSAGES = ("workspace does not fit LDS", "LDS share per agent exceeded")
 _VARIANT_DEFINES = {None: [], SMALL_FLEET: ["MPCX_WS_LDS"], MID_FLEET: ["MPCX_MIN_WAVES=1"]}
 
 
@@ -280,7 +284,12 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
         # only where the main build's register budget is tighter than one wave per SIMD
         base = compile_model(gen, verbose)
         occ = base.with_suffix(".occ")
-        if not occ.exists() or int(occ.read_text() or "1") <= 1:
+        if not occ.exists():
+            # the main build's occupancy is unknown (its resource remark was not found): no
+            # marker, so the decision is taken again once the occupancy is known
+            warnings.warn(f"occupancy of {base.name} unknown; no one-wave-per-SIMD build this time")
+            return None
+        if int(occ.read_text() or "1") <= 1:
             nofit.write_text("the main build already runs one wave per SIMD")
             return None
     src = out.with_suffix(".hip")
@@ -293,21 +302,27 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         if variant is not None:
-            # an optional build (the small-fleet variant): any failure -- its workspace does
-            # not fit LDS, or the per-agent LDS share is exceeded -- means "no such build";
-            # the main code object serves every batch size.  The marker keeps the reason.
-            if "workspace does not fit LDS" not in res.stderr:
+            # an optional build: any failure means "no such build this time", the main code
+            # object serves every batch size.  Only a structural misfit (a static_assert of the
+            # LDS / register budgets) is recorded as permanent (.nofit); a transient failure
+            # (hipcc killed, out of memory, interrupted) is retried by the next process.
+            if any(m in res.stderr for m in _NOFIT_MESSAGES):
+                nofit.write_text(res.stderr[-4000:])
+            else:
                 name = {SMALL_FLEET: "small-fleet", MID_FLEET: "one-wave-per-SIMD"}.get(variant, variant)
                 warnings.warn(f"{name} build of {gen.key} failed; the main build serves every batch:\n"
                               f"{res.stderr[-800:]}")
-            nofit.write_text(res.stderr[-4000:])
+            tmp.unlink(missing_ok=True)
             return None
         raise NativeError(f"compiling {src} failed:\n{res.stderr[-4000:]}")
     if verbose and res.stderr:
         print(res.stderr)
     if variant is None:  # the register budget's occupancy (mpcx_ipm_solve), for the w1 decision
         occ = re.search(r"Function Name: mpcx_ipm_solve.*?Occupancy \[waves/SIMD\]: (\d+)", res.stderr, re.S)
-        out.with_suffix(".occ").write_text(occ.group(1) if occ else "1")
+        if occ:
+            out.with_suffix(".occ").write_text(occ.group(1))
+        else:  # remark format changed: leave the decision open rather than never building w1
+            warnings.warn(f"no occupancy remark for mpcx_ipm_solve in the build of {out.name}")
     os.replace(tmp, out)
     return out
 

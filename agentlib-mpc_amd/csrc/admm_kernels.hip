@@ -300,12 +300,14 @@ extern "C" int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t n_blocks, in
   return (int64_t)n_groups * (NMOM * (int64_t)T + 1) + (int64_t)MPCX_ADMM_TOTALS * n_blocks;
 }
 
-// Length of the all-reduced prefix of the moments buffer: the global groups' moments, then
-// the totals of the blocks that span ranks (numbered first, identically on every rank; the
-// rank-local blocks' totals follow them and stay local).
+// Length of the all-reduced range (C ABI v10): the control doubles right before the moments
+// buffer (the coordinated loop's count of blocks still active), the global groups' moments,
+// then the totals of the blocks that span ranks (numbered first, identically on every rank;
+// the rank-local blocks' totals follow them and stay local).
 extern "C" int64_t mpcx_admm_reduce_count(int32_t n_global, int32_t n_global_blocks, int32_t T) {
   if (n_global < 0 || n_global_blocks < 0 || T <= 0) return MPCX_ERR_ARG;
-  return (int64_t)n_global * (NMOM * (int64_t)T + 1) + (int64_t)MPCX_ADMM_TOTALS * n_global_blocks;
+  return (int64_t)MPCX_ADMM_CONTROL + (int64_t)n_global * (NMOM * (int64_t)T + 1) +
+         (int64_t)MPCX_ADMM_TOTALS * n_global_blocks;
 }
 
 extern "C" int mpcx_admm_moments_masked(int32_t n_groups, int32_t n_global, int32_t n_blocks, int32_t T,
@@ -428,7 +430,11 @@ __global__ void k_block_stop(int nb, int it, const double* __restrict__ totals, 
                              double* __restrict__ record, int* __restrict__ n_active, long long* __restrict__ clock) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b == 0 && clock) clock[it] = (long long)wall_clock64();
-  if (it == 0 || b >= nb) return;
+  if (b >= nb) return;
+  if (it == 0) {  // the round's start: stamp the clock, count the blocks that will iterate
+    if (n_active && active_b && active_b[b] != 0) atomicAdd(n_active, 1);
+    return;
+  }
   const double* t = totals + (long)b * MPCX_ADMM_TOTALS;
   const double prim = sqrt(fmax(t[0], 0.0)), dual = sqrt(fmax(t[1], 0.0));
   bool conv;
@@ -452,6 +458,12 @@ __global__ void k_block_stop(int nb, int it, const double* __restrict__ totals, 
   const bool still = act && !conv;
   if (act && conv) { active_b[b] = 0; iters_b[b] = it; }
   if (n_active && still) atomicAdd(n_active + it, 1);
+}
+
+// the count of blocks still active as a double in the caller's control slot (the first double
+// of the all-reduced range, C ABI v10): one plain store after k_block_stop's atomics have landed
+__global__ void k_control_store(const int* __restrict__ n_active, double* __restrict__ control) {
+  if (threadIdx.x == 0) control[0] = (double)n_active[0];
 }
 
 __global__ void k_block_expand(int n, const int* __restrict__ idx, const int* __restrict__ active_b,
@@ -502,13 +514,18 @@ extern "C" int mpcx_admm_block_stop(int32_t n_blocks, int32_t it, const double* 
                                     double abs_tol, double rel_tol, double primal_tol, double dual_tol,
                                     double change_threshold, double change_factor, double* rho_b,
                                     int32_t* active_b, int32_t* iters_b, double* record, int32_t* n_active,
-                                    int64_t* clock, void* stream) {
+                                    int64_t* clock, double* control, void* stream) {
   if (n_blocks < 1 || it < 0 || (it > 0 && (!totals || !rho_b || !active_b || !iters_b || !record)))
     return MPCX_ERR_ARG;
+  if (control && !n_active) return MPCX_ERR_ARG;
   hipLaunchKernelGGL(k_block_stop, dim3(blocks_for(n_blocks, 256)), dim3(256), 0, (hipStream_t)stream,
                      n_blocks, it, totals, use_relative, abs_tol, rel_tol, primal_tol, dual_tol, change_threshold,
                      change_factor, rho_b, active_b, iters_b, record, n_active, (long long*)clock);
   LAUNCH_CHECK();
+  if (control) {
+    hipLaunchKernelGGL(k_control_store, dim3(1), dim3(WAVE), 0, (hipStream_t)stream, n_active + it, control);
+    LAUNCH_CHECK();
+  }
   return MPCX_OK;
 }
 

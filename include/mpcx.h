@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 9
+#define MPCX_API_VERSION 10
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -223,11 +223,18 @@ int mpcx_batch_solve_staged(mpcx_handle* h, int32_t n_agents, const void* host_i
  *   [n_global x (5T+1) global-group moments][n_blocks x MPCX_ADMM_TOTALS totals][local groups]
  *   <- the per-alias sums of ADMMCoordinator._check_convergence (admm_coordinator.py:354-435) */
 int64_t mpcx_admm_moments_size(int32_t n_groups, int32_t n_blocks, int32_t T);
-/* Length of the all-reduced prefix of that buffer:
- *   n_global*(5T+1) + n_global_blocks*MPCX_ADMM_TOTALS doubles
- * (global-group moments, then the totals of the rank-spanning blocks, which are numbered
- * first).  Single rank: nothing to reduce.  <- the one exchange per ADMM iteration of
- * admm_coordinator.py:288-304 when the agents sit on several GPUs. */
+/* The ONE collective per ADMM iteration (C ABI v10).  The caller keeps MPCX_ADMM_CONTROL control
+ * doubles immediately BEFORE the moments buffer ([control][moments buffer], one allocation; the
+ * kernels get the moments buffer, zero only it before mpcx_admm_moments) and all-reduces (sum)
+ *   mpcx_admm_reduce_count(...) = MPCX_ADMM_CONTROL + n_global*(5T+1) + n_global_blocks*MPCX_ADMM_TOTALS
+ * doubles starting at the control: the coordinated loop's number of blocks still active
+ * (written by mpcx_admm_block_stop's `control` output), the global-group moments, then the
+ * totals of the rank-spanning blocks, which are numbered first.  After the reduce the control
+ * holds the count over all ranks after the PREVIOUS iteration: every rank reads the same value
+ * and leaves the loop at the same iteration, with no second collective.  Single rank: nothing
+ * to reduce.  <- the one exchange per ADMM iteration of admm_coordinator.py:288-304 when the
+ * agents sit on several GPUs. */
+#define MPCX_ADMM_CONTROL 1
 int64_t mpcx_admm_reduce_count(int32_t n_global, int32_t n_global_blocks, int32_t T);
 
 /* Per (group, t) moments of the locals about center = the current mean [n_groups][T]:
@@ -306,11 +313,15 @@ int mpcx_admm_shift(int32_t n_rows, int32_t T, int32_t shift, double* x, void* s
  * record[it-1][b] = {prim, dual, rho after variation, active} (:396-402); a block meeting its
  * rule is frozen (active_b[b] = 0, iters_b[b] = it, the loop of :288-304).  n_active[it] (zero
  * it first) receives the number of blocks still active, clock[it] the device wall clock
- * (mpcx_device_clock_khz ticks; it = 0 only stamps the clock).  n_active / clock may be NULL. */
+ * (mpcx_device_clock_khz ticks; it = 0 stamps the clock and counts the blocks with
+ * active_b != 0 into n_active[0]).  n_active / clock may be NULL.  control (C ABI v10, may be
+ * NULL; needs n_active): receives n_active[it] as a double -- the control slot of the next
+ * iteration's all-reduce (mpcx_admm_reduce_count). */
 int mpcx_admm_block_stop(int32_t n_blocks, int32_t it, const double* totals, int32_t use_relative,
                          double abs_tol, double rel_tol, double primal_tol, double dual_tol,
                          double change_threshold, double change_factor, double* rho_b, int32_t* active_b,
-                         int32_t* iters_b, double* record, int32_t* n_active, int64_t* clock, void* stream);
+                         int32_t* iters_b, double* record, int32_t* n_active, int64_t* clock, double* control,
+                         void* stream);
 /* Block state to groups / agents: out_active[i] = active_b[idx[i]] (and part[i] != 0 when
  * part != NULL: the participation mask), out_rho[i] = rho_b[idx[i]]; either output may be NULL. */
 int mpcx_admm_block_expand(int32_t n, const int32_t* idx, const int32_t* active_b, const double* rho_b,

@@ -151,12 +151,16 @@ class CpuFleetOps:
             a[:, :T - shift] = a[:, shift:].copy()
 
     # -- the coordinators' stopping test (restates admm_kernels.hip k_block_stop / _expand) ----
-    def block_stop(self, it, totals, crit, rho_b, active_b, iters_b, record, n_active, clock):
+    def block_stop(self, it, totals, crit, rho_b, active_b, iters_b, record, n_active, clock, control=None):
         import time
 
         if clock is not None:
             clock.numpy()[it] = int(time.perf_counter() * 1e9)
         if it == 0:
+            if n_active is not None and active_b is not None:
+                n_active.numpy()[0] += int((active_b.numpy() != 0).sum())
+            if control is not None:
+                control.numpy()[0] = float(n_active.numpy()[0])
             return
         use_rel, abs_tol, rel_tol, primal_tol, dual_tol, thr, fac = crit
         t = totals.numpy().reshape(-1, TOTALS)
@@ -181,6 +185,8 @@ class CpuFleetOps:
         iters_b.numpy()[done] = it
         if n_active is not None:
             n_active.numpy()[it] += int((act & ~conv).sum())
+        if control is not None:  # the control slot of the next all-reduce (C ABI v10)
+            control.numpy()[0] = float(n_active.numpy()[it])
 
     def block_expand(self, idx, active_b, rho_b, part, out_active, out_rho):
         i = idx.numpy()

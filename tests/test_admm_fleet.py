@@ -307,8 +307,9 @@ def _part_worker(rank, world, init_file, N, out_file):
         out = fl.run_coordinated(0.4, **kw)
         traj = fl.trajectories()
         # per-block histories: world 1 holds blocks 0 and 1, rank r of world 2 block r (its
-        # only, rank-local block); the all-reduce carries nothing for rank-local blocks
-        assert fl.n_global_blocks == 0 and fl.reduce_len == 0 or world == 1
+        # only, rank-local block); the all-reduce carries nothing for rank-local blocks but the
+        # control double (the count of blocks still active that agrees the loop exit)
+        assert fl.n_global_blocks == 0 and fl.reduce_len == 1 or world == 1
         rec = {f"rec{b if world == 1 else rank}": np.array(
             [[r.primal_residual, r.dual_residual] for r in first["block_records"][b] + out["block_records"][b]])
             for b in range(fl.n_blocks)}
@@ -417,7 +418,7 @@ def test_consensus_multipliers_of_an_alias_sum_to_zero():
         np.testing.assert_allclose(rows.sum(0), 0.0, atol=1e-12 * np.abs(lam).max())
 
 
-def _mixed_worker(rank, world, init_file, out_file, tols=(1e-12, 1e-12), iter_max=2):
+def _mixed_worker(rank, world, init_file, out_file, tols=(1e-12, 1e-12), iter_max=2, check_every=4):
     """One coordinated fleet holding a C4 exchange alias that spans the ranks (one global
     block) and C2 consensus blocks that are rank-local: world 1 holds everything, rank r of
     world 2 its share of the C4 agents and C2 block r."""
@@ -437,9 +438,22 @@ def _mixed_worker(rank, world, init_file, out_file, tols=(1e-12, 1e-12), iter_ma
             # the length the C ABI defines (ctypes call of mpcx_admm_reduce_count, no GPU) is
             # the layout the fleet fills: global moments first, then the spanning block's totals
             assert fl.reduce_len == native.admm_reduce_count(fl.n_global, 1, fl.T)
-            assert fl.reduce_len == fl.n_global * fl.S + 8
-        out = fl.run_coordinated(1.0, admm_iter_max=iter_max, use_relative_tolerances=False, primal_tol=tols[0],
-                                 dual_tol=tols[1])
+            assert fl.reduce_len == 1 + fl.n_global * fl.S + 8   # control + moments + one block's totals
+        calls = []
+        real = dist.all_reduce
+        if world > 1:   # count every collective the round issues
+            dist.all_reduce = lambda *a, **k: (calls.append(a[0].numel()), real(*a, **k))[1]
+        try:
+            out = fl.run_coordinated(1.0, admm_iter_max=iter_max, use_relative_tolerances=False,
+                                     primal_tol=tols[0], dual_tol=tols[1], check_every=check_every)
+        finally:
+            dist.all_reduce = real
+        if world > 1:
+            # ONE all-reduce per ADMM iteration executed (plus the round's initial mean update),
+            # each of the same length: no second collective for the loop exit
+            assert len(calls) == out["collectives"] == 1 + out["iterations_executed"], (calls, out)
+            assert set(calls) == {fl.reduce_len}, calls
+            assert out["iterations_executed"] - out["loop_iterations"] <= 1
         xb = fl.block_index("mDot_coupling")
         np.savez(f"{out_file}.{rank}.iters.npz", iters=out["block_iterations"][[xb] + c2b_of(fl, world, rank)])
         c2b = [fl.block_index(f"mDot1_coupling_b{b}") for b in ((0, 1) if world == 1 else (rank,))]
@@ -457,25 +471,29 @@ def c2b_of(fl, world, rank):
     return [fl.block_index(f"mDot1_coupling_b{b}") for b in ((0, 1) if world == 1 else (rank,))]
 
 
-@pytest.mark.parametrize("tols,iter_max,want_iters", [
-    ((1e-12, 1e-12), 2, None),
+@pytest.mark.parametrize("tols,iter_max,want_iters,check_every", [
+    ((1e-12, 1e-12), 2, None, 4),
     # the spanning exchange block meets its rule at iteration 2 (primal 0.041 < 0.05, dual 2e-5 <
-    # 1e-3) while the C2 blocks keep going to the cap: from then on the ranks skip the
-    # all-reduce (no active spanning block) and iterate their local blocks on their own
-    ((0.05, 1e-3), 5, (2, 5)),
+    # 1e-3) while the C2 blocks keep going to the cap: the ranks go on in lockstep (one all-reduce
+    # per iteration, the stopped spanning block's moments travel but are not used)
+    ((0.05, 1e-3), 5, (2, 5), 4),
+    # every block stops early (loose rule): the loop exit is read from the control double of the
+    # iteration's all-reduce, one iteration late at most, and both ranks leave together
+    ((10.0, 10.0), 8, (1, 1), 1),
 ])
-def test_mixed_global_and_local_blocks_world2_matches_world1(tmp_path, tols, iter_max, want_iters):
+def test_mixed_global_and_local_blocks_world2_matches_world1(tmp_path, tols, iter_max, want_iters, check_every):
     """Blocks spanning ranks and rank-local blocks in one coordinated fleet: the
     spanning block's totals travel in the one all-reduce, the local blocks' do not, and two
     ranks reproduce the one-rank histories block by block -- also once the spanning block has
-    stopped and the ranks no longer reduce."""
+    stopped.  Exactly one all-reduce per ADMM iteration (patched ``dist.all_reduce``): the count
+    of blocks still active rides in its control double."""
     init, out = str(tmp_path / "init"), str(tmp_path / "out")
-    _mixed_worker(0, 1, init, out + "1", tols, iter_max)
+    _mixed_worker(0, 1, init, out + "1", tols, iter_max, check_every)
     one = dict(np.load(f"{out}1.0.npz"))
     if want_iters is not None:
         it1 = np.load(f"{out}1.0.iters.npz")["iters"]
         assert it1[0] == want_iters[0] and (it1[1:] == want_iters[1]).all(), it1
-    mp.spawn(_mixed_worker, args=(2, init, out + "2", tols, iter_max), nprocs=2, join=True)
+    mp.spawn(_mixed_worker, args=(2, init, out + "2", tols, iter_max, check_every), nprocs=2, join=True)
     for r in range(2):
         two = dict(np.load(f"{out}2.{r}.npz"))
         assert f"b{r}" in two

@@ -335,6 +335,39 @@ def test_gpu_every_block_stops_like_its_own_coordinator():
             np.testing.assert_allclose(tb[al], to[al], rtol=1e-9, atol=1e-12)
 
 
+def test_gpu_c2_bench_fleet_blocks_stop_like_their_own_coordinators():
+    """The C2 leg's own fleet (`bench.py` c2_admm: 1024 blocks = the 4096-room fleet, seed
+    20261015 + 1, the reference's IPOPT settings, the example coordinator's stopping rule): at
+    4096 rooms the room class runs the MAIN code object (more than four agents per CU), which a
+    single-block run (small-fleet build) never touches.  The first block, the blocks that stop
+    first and last, and a middle one each end at the iteration, with the residual history and
+    coupling means, of a single-block run of that block alone."""
+    N, kw = 10, dict(admm_iter_max=40, use_relative_tolerances=False, primal_tol=0.002, dual_tol=0.1)
+    opts = {"ipopt": {}}
+    big = ADMMFleet(bm.c2_fleet_classes(n_blocks=1024, N=N, seed=20261015 + 1, solver_options=opts))
+    rooms = big.classes[0]
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert rooms.n == 4096 and rooms.n > 4 * cus, "the room class must run the main build at this size"
+    out = big.run_coordinated(0.4, **kw)
+    its = np.asarray(out["block_iterations"])
+    assert len(set(its.tolist())) > 1, its
+    tb = big.trajectories()
+    seed_block = {big.block_index(f"mDot1_coupling_b{b}"): b for b in range(1024)}
+    for k in sorted({big.block_index("mDot1_coupling_b0"), int(np.argmin(its)), int(np.argmax(its)),
+                     big.block_index("mDot1_coupling_b511")}):
+        b = seed_block[k]
+        one = ADMMFleet(bm.c2_fleet_classes(n_blocks=1, N=N, seed=20261015 + 1, block_offset=b, solver_options=opts))
+        o1 = one.run_coordinated(0.4, **kw)
+        assert its[k] == o1["iterations"], (b, its[k], o1["iterations"])
+        got = np.array([[r.primal_residual, r.dual_residual] for r in out["block_records"][k]])
+        want = np.array([[r.primal_residual, r.dual_residual] for r in o1["records"]])
+        np.testing.assert_allclose(got, want, rtol=1e-7, atol=1e-12)
+        to = one.trajectories()
+        for i in range(4):
+            al = f"mDot{i + 1}_coupling_b{b}"
+            np.testing.assert_allclose(tb[al], to[al], rtol=1e-7, atol=1e-10)
+
+
 def test_gpu_admm_golden_through_native_kernels():
     """The reference's own ConsensusVariable / ExchangeVariable outputs
     (`tests/golden/admm_golden.json`, produced by executing `admm_datatypes.py` itself,

@@ -40,21 +40,38 @@ def _oracle(case, opts=None, key=None):
     return ref
 
 
-#: the two builds of every structure: the small-fleet build (workspace in LDS, what a batch
-#: of at most one agent per CU runs) and the HBM-workspace build (every larger fleet and
-#: every bench leg).  The parity cases below run both.
-BUILDS = ["lds", "hbm"]
+#: the three code objects of every structure, by the batch size that selects them
+#: (`mpcx_runtime.cpp` mpcx_batch_solve): "lds" the small-fleet build (workspace in LDS, at most
+#: one agent per CU), "mid" the one-wave-per-SIMD build (at most four agents per CU, only where
+#: the main build runs more waves), "main" the LDS-limited-occupancy build (every larger fleet:
+#: the C3 bench fleet, the C2 / C4 room classes).  Every parity case below runs on each build that
+#: exists for its structure: the limits of BOTH optional builds are set, so
+#: the build named is the one that runs whatever the batch size.
+BUILDS = ["lds", "mid", "main"]
+
+
+def select_build(native, build):
+    """Route every batch size of ``native`` to one code object (skip when it does not exist)."""
+    if build == "lds" and native.small_fleet_path is None:
+        pytest.skip("no small-fleet build for this structure")
+    if build == "mid" and native.mid_fleet_path is None:
+        pytest.skip("no one-wave-per-SIMD build for this structure (its main build runs one wave per SIMD)")
+    native.set_small_fleet_max(1 << 30 if build == "lds" else 0)
+    native.set_mid_fleet_max(1 << 30 if build == "mid" else 0)
+
+
+def reset_builds(native):
+    native.set_small_fleet_max(-1)
+    native.set_mid_fleet_max(-1)
 
 
 def _gpu_solve(case, n_copies=1, build="lds"):
     native = case.backend._native()
-    if build == "lds" and native.small_fleet_path is None:
-        pytest.skip("no small-fleet build for this structure")
-    native.set_small_fleet_max(-1 if build == "lds" else 0)
+    select_build(native, build)
     try:
         return case.backend.solve_batch(0.0, [case.current_vars] * n_copies)
     finally:
-        native.set_small_fleet_max(-1)
+        reset_builds(native)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -358,27 +375,32 @@ def test_batch_of_distinct_agents_matches_individual_solves():
         np.testing.assert_allclose(r.stats["obj"], single.stats["obj"], rtol=1e-12)
 
 
-def test_gpu_c3_fleet_matches_c_oracle():
-    """Bench-shaped parity: 512 agents of the C3 fleet (bench.py inputs, the reference's
-    default solver settings: tol 1e-4, acceptable_tol 0.1 over 5 iterations, ...) solved by
-    the kernel and by the C restatement of the oracle IPM (`oracle/c/ipm_oracle.c`): same
-    return status and iteration count per agent; objectives rel 1e-6 and solutions rel 1e-5
-    where both succeed."""
+@pytest.mark.parametrize("n,build", [(256, "lds"), (512, "mid"), (4096, "main")])
+def test_gpu_c3_fleet_matches_c_oracle(n, build):
+    """Bench-shaped parity: the C3 fleet (bench.py inputs, the reference's default solver
+    settings: tol 1e-4, acceptable_tol 0.1 over 5 iterations, ...) solved by the kernel and by
+    the C restatement of the oracle IPM (`oracle/c/ipm_oracle.c`): same return status and
+    iteration count per agent; objectives rel 1e-6 and solutions rel 1e-5 where both succeed.
+    Each code object at a batch size that selects it: 4096 agents is the bench's own launch
+    (`bench.py` value) on the main build."""
     import bench
     from agentlib_mpc_amd import benchmarks as bm
     from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
     from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
     from oracle import cbuild
 
-    n = 512
     be, cv = bm.one_room(solver_options=bm.REFERENCE)
     p, lbw, ubw, w0 = fleet_nlp_inputs(be.problem, cv, bench.fleet_values(n, 20261015 + 2))
     native = be._native()
+    select_build(native, build)
     T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
     tw = T(w0)
     st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device="cuda")
-    native.solve(T(p), T(lbw), T(ubw), tw, stats=st)
-    torch.cuda.synchronize()
+    try:
+        native.solve(T(p), T(lbw), T(ubw), tw, stats=st)
+        torch.cuda.synchronize()
+    finally:
+        reset_builds(native)
     gw = tw.cpu().numpy()
     gs = stats_to_dicts(st.cpu().numpy().tobytes())
     cbuild.build()

@@ -279,6 +279,45 @@ def test_warm_starts_follow_the_agent_keys(small, monkeypatch):
     np.testing.assert_array_equal(rb2.W.numpy(), want)
 
 
+@pytest.mark.parametrize("small", [True, False])
+def test_failed_agent_restarts_cold_after_permutation(small, monkeypatch):
+    """an agent whose last solve came back NaN (``cold_rows``, old slot numbering)
+    restarts cold wherever the next call puts it -- after a permutation of the batch and after
+    a change of batch size -- and the agent now sitting in its old slot keeps its own warm start."""
+    from agentlib_mpc_amd.optimization_backends import plugin_batch
+
+    monkeypatch.setattr(plugin_batch, "SMALL_BATCH", 64 if small else 0)
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)
+    m = be.problem.marshal
+    agents = _agents(cv, 5, 23)
+    rb = ResidentBatch(be.problem, None, agents, 0.0, torch.device("cpu"))
+    sol = rb.W.numpy().copy() + np.arange(5)[:, None] * 0.01 + 0.3
+    sol[1] = np.nan                            # agent 1's solve failed (what solve() records)
+    rb.W.copy_(torch.from_numpy(sol))
+    if rb.small:
+        rb.hW[:] = sol
+    rb.cold_rows = np.array([1])
+    src = np.array([1, 3, 4, 0, 2])            # agent 1 moves to slot 0; agent 3 into its old slot
+    perm = [agents[i] for i in src]
+    rb.permute_warm_starts(src)
+    rb.update(perm, 300.0)
+    w_prev = sol[src].copy()                   # NaN row = cold start in the host marshalling
+    _check(rb, m, perm, 300.0, w_prev)
+    assert np.isfinite(rb.W.numpy()).all()
+    # a failure, then a batch-size change: the failed agent keeps the cold guess
+    sol2 = rb.W.numpy().copy() + 0.1
+    sol2[2] = np.nan
+    rb.W.copy_(torch.from_numpy(sol2))
+    if rb.small:
+        rb.hW[:] = sol2
+    rb.cold_rows = np.array([2])
+    rb2 = ResidentBatch(be.problem, None, [perm[2], perm[4]], 600.0, torch.device("cpu"))
+    rb2.adopt_warm_starts(rb, np.array([2, 4]))
+    want = m.inputs([perm[2], perm[4]], 600.0, None)[3]
+    want[1] = sol2[4]
+    np.testing.assert_array_equal(rb2.W.numpy(), want)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("small", [True, False])
 def test_gpu_permuted_batch_keeps_each_agents_warm_start(small, monkeypatch):

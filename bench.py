@@ -388,11 +388,13 @@ def c2_admm_bench(args, world, rank, dev):
                         args.admm_steps, 60.0, 5, world, dev)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
+        # the GPU leg's fleet and closed loop (a few x 40 ADMM iterations of 5120 C IPM solves:
+        # ~30 s on 16 host cores)
         sample = bm.c2_fleet_classes(n_blocks=nb, N=10, seed=20261015 + 1, solver_options={"ipopt": {}})
-        cpu = admm_cpu_baseline(sample, lambda fl: fl.run_coordinated(0.4, admm_iter_max=40,
-                                                                      use_relative_tolerances=False,
-                                                                      primal_tol=0.002, dual_tol=0.1),
-                                5 * nb, "C2 coordinated, to each block's stopping rule")
+        cpu = admm_cpu_baseline_closed_loop(
+            sample, lambda fl: fl.run_coordinated(0.4, admm_iter_max=40, use_relative_tolerances=False,
+                                                  primal_tol=0.002, dual_tol=0.1),
+            5 * nb, "C2 coordinated, to each block's stopping rule", args.admm_steps, 60.0)
     return {
         "workload": "C2 scaled: 4-room + air-handler blocks (casadi_admm collocation d=3, N=10, ts=60), "
                     "coordinated consensus, rho=0.4, abs tol 0.002/0.1, iter max 40, per-block stopping; "
@@ -411,23 +413,31 @@ def _closed_loop(fleet, run, steps, ts, agents_per_block, world, dev):
     interval and iterates every block to its own stopping rule (or the iteration cap) from
     the agents' resident warm starts; between the steps the synthetic plant moves every
     zone to its predicted state at ``ts`` (``benchmarks.advance_plant``: new measurements,
-    untimed).  Each step is timed on its own (barrier + synchronize on both sides); the leg
-    reports the per-step figures and the median ADMM iterations/s over the steps."""
+    untimed).  Each step is timed on its own (barrier + synchronize on both sides).  The leg
+    reports the per-step figures and, over the whole sequence, ADMM iterations/s = all steps'
+    fleet-loop iterations / all steps' wall time (r05: the median over the steps sat between
+    the slow cold steps and the fast warm ones and moved by 40 % between boxes) and block
+    iterations/s = all blocks' own iterations / the same wall time (the fleet-loop rate rises
+    as blocks freeze; the block rate counts the work each coordinator did).  ``dev`` "cpu": the
+    same loop on the host fleet (the CPU baseline runs the identical step sequence)."""
     import torch
     import torch.distributed as dist
     from agentlib_mpc_amd import benchmarks as bm
 
+    cuda = torch.device(dev).type == "cuda"
     per = []
     rest = 0
     for step in range(max(int(steps), 1)):
         if step:
             bm.advance_plant(fleet, ts)
-        torch.cuda.synchronize(dev)
+        if cuda:
+            torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         out = run()
-        torch.cuda.synchronize(dev)
+        if cuda:
+            torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         wall = time.perf_counter() - t0
@@ -436,10 +446,15 @@ def _closed_loop(fleet, run, steps, ts, agents_per_block, world, dev):
         per.append(summ)
         rest += out["restorations"]
     ips = [p["admm_iters_per_s"] for p in per]
+    wall_tot = float(sum(p["wall_s"] for p in per))
     return {
         "control_steps": len(per),
-        "admm_iters_per_s": float(np.median(ips)),
+        "admm_iters_per_s": float(sum(p["admm_iterations"] for p in per)) / wall_tot,
+        "block_admm_iters_per_s": float(sum(p["block_iterations_sum"] for p in per)) / wall_tot,
+        "admm_iters_per_s_median": float(np.median(ips)),
         "admm_iters_per_s_steps": ips,
+        "admm_iters_per_s_spread": [float(min(ips)), float(max(ips))],
+        "block_admm_iters_per_s_steps": [p["block_admm_iters_per_s"] for p in per],
         "admm_iterations_steps": [p["admm_iterations"] for p in per],
         "converged_block_fraction_steps": [p["converged_block_fraction"] for p in per],
         "block_iterations_p50_max_steps": [p["block_iterations_p50_max"] for p in per],
@@ -497,6 +512,7 @@ def _block_summary(out, wall, agents_per_block, world=1, dev=None):
         "block_iterations_p50_max": [float(np.percentile(it, 50)), int(it.max())],
         "admm_iters_per_s": iters / wall,
         "block_admm_iters_per_s": float(it.sum()) / wall,
+        "block_iterations_sum": int(it.sum()),
         "wall_s": wall,
         "agent_solves_per_s": ok / wall,
         "converged_solve_fraction": ok / max(1, solves),
@@ -546,11 +562,13 @@ def c5_admm_bench(args, world, rank, dev):
                         args.admm_steps, 1800.0, 5, world, dev)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        sample = bm.c5_fleet_classes(n_blocks=nb, N=24, seed=20261015 + 5, solver_options=opts)
-        cpu = admm_cpu_baseline(sample, lambda fl: fl.run_coordinated(1.0, admm_iter_max=args.c5_iters,
-                                                                      use_relative_tolerances=False,
-                                                                      primal_tol=0.04, dual_tol=0.04),
-                                5 * nb, "C5 coordinated")
+        # the first third of the GPU leg's blocks over its closed loop (5 x 50 ADMM iterations of the
+        # whole fleet would take ~50 s on 16 host cores), projected by the agent ratio
+        sample = bm.c5_fleet_classes(n_blocks=max(1, nb // 3), N=24, seed=20261015 + 5, solver_options=opts)
+        cpu = admm_cpu_baseline_closed_loop(
+            sample, lambda fl: fl.run_coordinated(1.0, admm_iter_max=args.c5_iters, use_relative_tolerances=False,
+                                                  primal_tol=0.04, dual_tol=0.04),
+            5 * nb, "C5 coordinated", args.admm_steps, 1800.0)
     return {
         "workload": "C5: three-zone data-driven ADMM (3 NARX zones + AHU + CCA per block), coordinated "
                     "consensus, rho=1, N=24 ts=1800, abs tol 0.04/0.04, per-block stopping",
@@ -562,12 +580,42 @@ def c5_admm_bench(args, world, rank, dev):
     }
 
 
+def admm_cpu_baseline_closed_loop(classes, run, full_agents, label, steps, ts):
+    """CPU baseline of a coordinated leg over the SAME closed loop as the GPU leg (VERDICT r04
+    item 5): ``steps`` control steps with the synthetic plant advanced between them
+    (:func:`_closed_loop` on the host fleet: `admm/fleet.py` with `oracle/cpu_fleet.py`, every
+    class's agents solved by the C IPM restatement over the class's host-compiled generated
+    model, OpenMP over the host cores).  ``classes`` may be a sample of the GPU leg's fleet
+    (fewer blocks): its rates are scaled to the full fleet by the agent ratio ("projected")."""
+    from agentlib_mpc_amd.admm.fleet import ADMMFleet
+    from oracle.cpu_fleet import CpuFleetOps
+
+    ops = CpuFleetOps(ipopt=dict(solver_settings_ns.oracle))
+    fleet = ADMMFleet(classes, device="cpu", ops=ops)
+    n_sample = sum(c.n for c in classes)
+    t0 = time.perf_counter()
+    loop = _closed_loop(fleet, lambda: run(fleet), steps, ts, 5, 1, "cpu")
+    dt = time.perf_counter() - t0
+    scale = n_sample / full_agents
+    unit = "ADMM iters/s" if n_sample == full_agents else "ADMM iters/s (GPU leg's fleet, projected)"
+    return {"value": loop["admm_iters_per_s"] * scale, "unit": unit,
+            "block_admm_iters_per_s": loop["block_admm_iters_per_s"] * scale,
+            "admm_iters_per_s_steps": [v * scale for v in loop["admm_iters_per_s_steps"]],
+            "admm_iterations_steps": loop["admm_iterations_steps"],
+            "cores": ops.threads, "kind": "port",
+            "sample": f"{label}: the GPU leg's closed loop ({loop['control_steps']} control steps, plant advanced "
+                      f"between them), {sum(loop['admm_iterations_steps'])} ADMM iterations over a {n_sample}-agent "
+                      f"sample fleet in {dt:.1f} s, x {n_sample}/{full_agents} agents; solves by "
+                      f"oracle/c/ipm_oracle.c on host-compiled generated models, same IPOPT settings"}
+
+
 def admm_cpu_baseline(classes, run, full_agents, label, min_seconds=8.0):
     """The same ADMM driver (`admm/fleet.py`) on the host: every class's agents solved by
     the C IPM restatement over the class's generated model compiled for the host
     (`oracle/c/gen_model.cpp`, OpenMP over the host cores), the ADMM arithmetic in numpy
     (`oracle/cpu_fleet.py`).  Run on the GPU leg's whole fleet (``classes``; a smaller
-    sample is scaled to it by the agent ratio and labelled "projected")."""
+    sample is scaled to it by the agent ratio and labelled "projected").  The C4 leg (LocalADMM,
+    one round of a fixed iteration count, no stopping rule)."""
     from agentlib_mpc_amd.admm.fleet import ADMMFleet
     from oracle.cpu_fleet import CpuFleetOps
 

@@ -453,6 +453,15 @@ class ADMMFleet:
                                    and os.environ.get("MPCX_FLEET_STREAMS", "1") != "0")
         self._class_streams = [t.cuda.Stream(device=dev) for _ in self.classes] if self.concurrent_classes else None
         self._ev_solve = t.cuda.Event() if self.concurrent_classes else None
+        #: coordinated rounds launch only the agents still active (mpcx_active_map +
+        #: mpcx_batch_solve_mapped): each class's solve is ``bound`` workgroups over the compacted
+        #: agent map, the bound being the class's active count at the last stopping check (the
+        #: active set only shrinks within a round); MPCX_FLEET_MAP=0 launches every agent
+        self.map_launch = os.environ.get("MPCX_FLEET_MAP", "1") != "0" and hasattr(self.ops, "active_map")
+        self._mapped = False
+        for c in self.classes:
+            c.MAP = t.zeros(c.n, dtype=i32, device=dev)
+            c.bound = c.n
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
@@ -520,7 +529,11 @@ class ADMMFleet:
                         ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
                         ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
                 ops.scatter_rows(1, self.RHO_B, c.BLOCK, c.P, c.RHO_COL)  # the block's penalty
-                ops.solve(c, c.ACTIVE if self._masked else None)
+                if self._mapped:  # only the agents still active, compacted (mpcx_active_map)
+                    ops.active_map(c.n, c.ACTIVE, c.MAP, self._map_counts[ci:ci + 1])
+                    ops.solve(c, c.ACTIVE, c.MAP, c.bound)
+                else:
+                    ops.solve(c, c.ACTIVE if self._masked else None)
                 for si, s in enumerate(c.slots):
                     d = c.dev_slots[si]
                     # agents not participating keep their local (their rows map to the scratch row)
@@ -687,7 +700,14 @@ class ADMMFleet:
         ACTIVE_B = t.ones(nb, dtype=i32, device=dev)
         ITERS_B = t.full((nb,), n_it, dtype=i32, device=dev)
         REC = t.zeros(max(n_it, 1) * nb * 4, dtype=t.float64, device=dev)
-        NACT = t.zeros(n_it + 1, dtype=i32, device=dev)
+        # [n_active per iteration | each class's active-agent count of the last compaction]: what
+        # a stopping check reads, in one copy
+        CHK = t.zeros(n_it + 1 + len(self.classes), dtype=i32, device=dev)
+        NACT = CHK[:n_it + 1]
+        self._map_counts = CHK[n_it + 1:]
+        self._mapped = self.map_launch
+        for c in self.classes:
+            c.bound = c.n
         CLOCK = t.zeros(n_it + 1, dtype=t.int64, device=dev)
         self.RHO_B.fill_(rho0)
         self._expand_blocks(ACTIVE_B)
@@ -713,16 +733,21 @@ class ADMMFleet:
             # part in every iteration's all-reduce; frozen groups' moments travel but are not used
             tot = self._update_means(rho0, apply_multipliers=True, per_block=True)
             executed = it
-            if multi and it > 1 and (it - 1) % every == 0 and float(self.CONTROL.item()) == 0.0:
-                break  # every block on every rank had stopped by iteration it - 1: this one was a no-op
+            if multi and it > 1 and (it - 1) % every == 0:
+                left = float(self.CONTROL.item())  # the count over all ranks after iteration it - 1
+                self._take_bounds(CHK)
+                if left == 0.0:
+                    break  # every block on every rank had stopped by iteration it - 1: this one was a no-op
             ops.block_stop(it, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK, ctrl)
             self._expand_blocks(ACTIVE_B)
             ran = it
-            if not multi and (it % every == 0 or it == n_it) and int(NACT[it].item()) == 0:
-                break
+            if not multi and (it % every == 0 or it == n_it):
+                if self._take_bounds(CHK)[it] == 0:
+                    break
         self._sync()
         # the next round starts from full penalties and no freeze mask
         self._masked = False
+        self._mapped = False
         self._blk_key = None
         wall = time.perf_counter() - t0
         iters = ITERS_B.cpu().numpy().astype(np.int64)
@@ -751,6 +776,15 @@ class ADMMFleet:
                 "block_converged": conv_b, "block_records": block_records, "block_is_global": self.block_is_global.copy(),
                 "restorations": int(self._counts[1].item()), "loop_iterations": ran,
                 "iterations_executed": executed, "collectives": self.n_collectives - coll0}
+
+    def _take_bounds(self, chk) -> np.ndarray:
+        """Read a stopping check's counters (one copy) and take each class's active-agent count
+        of the last compaction as its launch size for the rest of the round."""
+        h = chk.cpu().numpy()
+        if self._mapped:
+            for c, n in zip(self.classes, h[len(h) - len(self.classes):]):
+                c.bound = int(n)
+        return h
 
     def _expand_blocks(self, active_b):
         """Per-block penalties and freeze masks (device) to the groups and the agents (with the

@@ -39,11 +39,16 @@ class NativeADMMOps:
             raise native.NativeError(f"{name} failed ({rc})")
 
     # -- NLP solves ---------------------------------------------------------------------
-    def solve(self, cls, active=None) -> None:
+    def solve(self, cls, active=None, agent_map=None, n_launch=None) -> None:
         """Batched solve of one class; ``active`` (int32 [n] device tensor or None) skips the
-        agents of converged blocks."""
+        agents of converged blocks; ``agent_map`` + ``n_launch`` (mpcx_active_map's output and a
+        bound on its count) launch only that many workgroups (``mpcx_batch_solve_mapped``)."""
         cls.native.solve(cls.P, cls.LB, cls.UB, cls.W, lam_g=cls.LAMG, stats=cls.ST, active=active,
-                         stream=self.stream.value)
+                         stream=self.stream.value, agent_map=agent_map, n_launch=n_launch)
+
+    def active_map(self, n, active, amap, count):
+        """``mpcx_active_map``: the active agents' indices first (increasing), then -1; count[0]."""
+        self._chk(self.lib.mpcx_active_map(n, _p(active), _p(amap), _p(count), self.stream), "mpcx_active_map")
 
     # -- moves ---------------------------------------------------------------------------
     def gather_rows(self, T, src, cols, dst, dst_rows):

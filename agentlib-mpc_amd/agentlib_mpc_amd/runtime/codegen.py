@@ -34,7 +34,7 @@ from agentlib_mpc_amd import symbolic as sx
 from agentlib_mpc_amd.runtime import stage_elim
 from agentlib_mpc_amd.optimization_backends.discretization import StageNLP
 
-KERNEL_ABI_VERSION = 7  # must equal MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
+KERNEL_ABI_VERSION = 8  # must equal MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
 
 
 @dataclasses.dataclass

@@ -85,7 +85,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
     "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_problem_small_fleet",
     "mpcx_problem_mid_fleet",
-    "mpcx_batch_solve", "mpcx_batch_solve_staged",
+    "mpcx_batch_solve", "mpcx_batch_solve_staged", "mpcx_batch_solve_mapped", "mpcx_active_map",
     "mpcx_admm_moments_size", "mpcx_admm_reduce_count", "mpcx_admm_moments", "mpcx_admm_finalize",
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
@@ -94,7 +94,7 @@ EXPORTED_SYMBOLS = [
 ]
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
 ADMM_CONTROL = 1  # MPCX_ADMM_CONTROL: control doubles before the moments buffer (C ABI v10)
-KERNEL_ABI = 7  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
+KERNEL_ABI = 8  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -190,6 +190,8 @@ def load_library():
         lib.mpcx_problem_mid_fleet.argtypes = [vp, ctypes.c_char_p, i32]
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
         lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp, vp]
+        lib.mpcx_batch_solve_mapped.argtypes = [vp, i32, i32, vp] + [vp] * 9 + [vp, vp]
+        lib.mpcx_active_map.argtypes = [i32, vp, vp, vp, vp]
         i64 = ctypes.c_int64
         lib.mpcx_batch_solve_staged.argtypes = [vp, i32, vp, vp, i64, vp, vp, i64] + [vp] * 6 + [vp]
         lib.mpcx_admm_moments_size.argtypes = [i32, i32, i32]
@@ -411,8 +413,12 @@ class NativeProblem:
             raise NativeError(f"mpcx_reserve failed ({rc})")
 
     def solve(self, p, lbw, ubw, w, lbg=None, ubg=None, lam_g=None, lam_w=None, stats=None,
-              active=None, stream=None):
+              active=None, stream=None, agent_map=None, n_launch=None):
         """Launch the batched solve on device tensors (stream-ordered, async).
+
+        ``agent_map`` (int32 [n] device tensor, with ``n_launch``): launch ``n_launch``
+        workgroups, workgroup i solving agent ``agent_map[i]`` (-1: none) --
+        ``mpcx_batch_solve_mapped``, the code object chosen by ``n_launch``.
 
         Every buffer the kernel reads or writes is checked here (dtype, device, contiguity,
         size): an undersized or host buffer would otherwise become an out-of-bounds device
@@ -442,6 +448,17 @@ class NativeProblem:
         if stream is None:
             stream = torch.cuda.current_stream().cuda_stream
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        if agent_map is not None:
+            check("agent_map", agent_map, (n,), torch.int32)
+            n_launch = int(n_launch)
+            if not 0 <= n_launch <= n:
+                raise ValueError(f"n_launch {n_launch} outside [0, {n}]")
+            rc = self.lib.mpcx_batch_solve_mapped(self.handle, n, n_launch, ptr(agent_map), ptr(p), ptr(lbw),
+                                                  ptr(ubw), ptr(lbg), ptr(ubg), ptr(w), ptr(lam_g), ptr(lam_w),
+                                                  ptr(stats), ptr(active), ctypes.c_void_p(stream))
+            if rc != 0:
+                raise NativeError(f"mpcx_batch_solve_mapped failed ({rc})")
+            return
         rc = self.lib.mpcx_batch_solve(self.handle, n, ptr(p), ptr(lbw), ptr(ubw), ptr(lbg), ptr(ubg),
                                        ptr(w), ptr(lam_g), ptr(lam_w), ptr(stats), ptr(active),
                                        ctypes.c_void_p(stream))

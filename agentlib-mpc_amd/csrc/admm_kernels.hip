@@ -476,6 +476,38 @@ __global__ void k_block_expand(int n, const int* __restrict__ idx, const int* __
   if (out_rho) out_rho[i] = rho_b[b];
 }
 
+// compaction of an active mask into an agent map (one workgroup, chunks of THREADS entries:
+// ballot + popcount prefix per wave, wave offsets through LDS, a running base across chunks)
+__global__ void __launch_bounds__(THREADS) k_active_map(int n, const int* __restrict__ active,
+                                                        int* __restrict__ map, int* __restrict__ count) {
+  __shared__ int wave_cnt[THREADS / WAVE];
+  __shared__ int base_s;
+  const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+  if (t == 0) base_s = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += THREADS) {
+    const int i = c0 + t;
+    const bool on = i < n && active[i] != 0;
+    const unsigned long long bal = __ballot(on);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[w] = __popcll(bal);
+    __syncthreads();
+    int off = base_s;
+    for (int q = 0; q < w; ++q) off += wave_cnt[q];
+    if (on) map[off + before] = i;
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int q = 0; q < THREADS / WAVE; ++q) tot += wave_cnt[q];
+      base_s += tot;
+    }
+    __syncthreads();
+  }
+  const int m = base_s;
+  for (int i = m + t; i < n; i += THREADS) map[i] = -1;
+  if (t == 0) count[0] = m;
+}
+
 // a class's batched solve, counted for the fleet's bookkeeping: counts[0] += agents whose status
 // is Solve_Succeeded / Solved_To_Acceptable_Level, counts[1] += their restoration-phase calls;
 // agents with active[i] == 0 (frozen blocks, not solved) are skipped.  One atomic per wave.
@@ -506,6 +538,13 @@ extern "C" int mpcx_stats_count(int32_t n, const mpcx_stats* stats, const int32_
   if (n == 0) return MPCX_OK;
   hipLaunchKernelGGL(k_stats_count, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, stats, active,
                      (unsigned long long*)counts);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int mpcx_active_map(int32_t n, const int32_t* active, int32_t* map, int32_t* count, void* stream) {
+  if (n < 0 || (n > 0 && (!active || !map)) || !count) return MPCX_ERR_ARG;
+  hipLaunchKernelGGL(k_active_map, dim3(1), dim3(THREADS), 0, (hipStream_t)stream, n, active, map, count);
   LAUNCH_CHECK();
   return MPCX_OK;
 }

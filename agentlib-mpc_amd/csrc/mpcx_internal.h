@@ -5,7 +5,7 @@
 
 #include "mpcx.h"
 
-#define MPCX_KERNEL_ABI 7
+#define MPCX_KERNEL_ABI 8
 
 typedef struct mpcx_kernel_args {
   const double* p;
@@ -18,6 +18,7 @@ typedef struct mpcx_kernel_args {
   double* lam_w;
   mpcx_stats* stats;
   const int* active;
+  const int* agent_map;  // workgroup -> agent (mpcx_batch_solve_mapped; -1: no agent), or NULL
   double* ws;
   long ws_stride;
   int n_agents;

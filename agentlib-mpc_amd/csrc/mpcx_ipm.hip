@@ -3899,8 +3899,10 @@ using namespace mpcx_kernel;
 #define KOPT (((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())->opt)
 #define OPT(f) (*(volatile const __attribute__((address_space(4))) decltype(mpcx_options::f)*)&KOPT.f)
 extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args args) {
-  const int agent = blockIdx.x;
-  if (agent >= args.n_agents) return;
+  // workgroup -> agent: the identity, or the compacted list of the agents still active
+  // (mpcx_batch_solve_mapped: a coordinated fleet launches only its unfrozen agents)
+  const int agent = args.agent_map != nullptr ? args.agent_map[blockIdx.x] : (int)blockIdx.x;
+  if (agent < 0 || agent >= args.n_agents) return;
   if (args.active != nullptr && args.active[agent] == 0) return;  // frozen (converged ADMM block)
   // Loop state lives in LDS (KState, written identically by every lane) and the options are
   // re-read from the kernarg segment where they are used (volatile scalar loads): held in

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 10
+#define MPCX_API_VERSION 11
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -180,6 +180,19 @@ int mpcx_batch_solve(mpcx_handle* h, int32_t n_agents, const double* p, const do
                      const double* ubw, const double* lbg, const double* ubg, double* w_io,
                      double* lam_g, double* lam_w, mpcx_stats* stats, const int32_t* active,
                      void* stream);
+
+/* Mapped launch (C ABI v11): n_launch workgroups, workgroup i solving agent agent_map[i] of the
+ * n_agents-agent arrays above (agent_map[i] < 0: no agent; device int32 [n_launch]).  The code
+ * object is chosen by n_launch, not n_agents: a coordinated fleet whose blocks have mostly met
+ * their stopping rule launches only the agents still active (mpcx_active_map compacts them) and
+ * runs them on the small-fleet build however large the class is -- the straggling blocks of
+ * ADMMCoordinator (admm_coordinator.py:284-309), each waiting on its agents' solves
+ * (modules/dmpc/admm/admm_coordinated.py:133-193).  agent_map NULL: n_launch must equal
+ * n_agents (= mpcx_batch_solve). */
+int mpcx_batch_solve_mapped(mpcx_handle* h, int32_t n_agents, int32_t n_launch, const int32_t* agent_map,
+                            const double* p, const double* lbw, const double* ubw, const double* lbg,
+                            const double* ubg, double* w_io, double* lam_g, double* lam_w, mpcx_stats* stats,
+                            const int32_t* active, void* stream);
 
 /* Host round trip of a small batch in ONE call (C ABI v8): the reference's usual deployment
  * is one MPC agent per process whose do_step blocks on its solve (modules/mpc/mpc.py:322-340 ->
@@ -326,6 +339,11 @@ int mpcx_admm_block_stop(int32_t n_blocks, int32_t it, const double* totals, int
  * part != NULL: the participation mask), out_rho[i] = rho_b[idx[i]]; either output may be NULL. */
 int mpcx_admm_block_expand(int32_t n, const int32_t* idx, const int32_t* active_b, const double* rho_b,
                            const int32_t* part, int32_t* out_active, double* out_rho, void* stream);
+/* Compaction of an active mask (C ABI v11): map[0 .. count-1] <- the indices i with active[i] != 0
+ * in increasing order, map[count .. n-1] <- -1, count[0] <- count (device int32).  The agent map
+ * of mpcx_batch_solve_mapped; the host reads count with the stopping test's n_active, so the
+ * launch size of the next iterations is known without an extra synchronisation. */
+int mpcx_active_map(int32_t n, const int32_t* active, int32_t* map, int32_t* count, void* stream);
 /* Rate of the device wall clock the stopping test stamps (kHz). */
 int64_t mpcx_device_clock_khz(void);
 

@@ -28,12 +28,25 @@ class CpuFleetOps:
         self.ipopt = dict(ipopt or {"tol": 1e-8, "max_iter": 500, "acceptable_iter": 0})
         self.threads = threads or int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
 
-    def solve(self, cls, active=None):
+    def active_map(self, n, active, amap, count):
+        """numpy restatement of ``mpcx_active_map`` (admm_kernels.hip k_active_map)."""
+        idx = np.flatnonzero(active.numpy()[:n] != 0)
+        m = amap.numpy()
+        m[:idx.size] = idx
+        m[idx.size:n] = -1
+        count.numpy()[0] = idx.size
+
+    def solve(self, cls, active=None, agent_map=None, n_launch=None):
         from oracle import cbuild
 
         P, LB, UB, W = (t.numpy() for t in (cls.P, cls.LB, cls.UB, cls.W))
         st = cls.ST.view(torch.int32).view(cls.n, -1).numpy()
         act = np.ones(cls.n, bool) if active is None else active.numpy() != 0
+        if agent_map is not None:  # the mapped launch: only the first n_launch map entries run
+            m = agent_map.numpy()[:int(n_launch)]
+            sel = np.zeros(cls.n, bool)
+            sel[m[m >= 0]] = True
+            act &= sel
         idx = np.flatnonzero(act)
         if idx.size == 0:
             return

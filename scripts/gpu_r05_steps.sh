@@ -13,7 +13,8 @@ step_s1() {
   [ $rc -ne 0 ] && [ $rc -ne 1 ] && { echo "tests exit $rc"; exit $rc; }
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s1/smoke.txt 2>&1 || exit $?
   # kernel time of each code object over fleet sizes (the build choice by agents per CU)
-  timeout -k 10 300 python -u scripts/build_scan.py > gpurun_out/s1/build_scan_c3.txt 2>&1
+  timeout -k 10 300 python -u scripts/build_scan.py > gpurun_out/s1/build_scan_c3.txt 2>&1 || exit $?
+  MODEL=admm_room SIZES=1,64,256,512,1024,4096 timeout -k 10 300 python -u scripts/build_scan.py > gpurun_out/s1/build_scan_c2room.txt 2>&1
   echo "tests exit $rc, scan exit $?"
 }
 

@@ -22,11 +22,16 @@ class CpuADMMOps(CpuFleetOps):
         self.oracle_problems = oracle_problems  # class name -> oracle.nlps.OracleProblem
         self.tol = tol
 
-    def solve(self, cls, active=None):
+    def solve(self, cls, active=None, agent_map=None, n_launch=None):
         prob = self.oracle_problems[cls.name]
         P, LB, UB, W = (t.numpy() for t in (cls.P, cls.LB, cls.UB, cls.W))
         st = cls.ST.view(torch.int32).view(cls.n, -1).numpy()
         act = np.ones(cls.n, bool) if active is None else active.numpy() != 0
+        if agent_map is not None:  # the mapped launch: only the first n_launch map entries run
+            m = agent_map.numpy()[:int(n_launch)]
+            sel = np.zeros(cls.n, bool)
+            sel[m[m >= 0]] = True
+            act &= sel
         for a in np.flatnonzero(act):
             p = P[a]
             r = ipm.solve(prob.functions(p), W[a].copy(), LB[a], UB[a], prob.lbg(p), prob.ubg(p),

@@ -590,3 +590,55 @@ def test_gpu_stats_count_matches_restatement():
     expect = [ok.sum() + (ok & (act != 0)).sum(), words[:, 15].sum() + words[:, 15][act != 0].sum()]
     np.testing.assert_array_equal(want["c"], expect)
     np.testing.assert_array_equal(got["c"], expect)
+
+
+@pytest.mark.parametrize("n", [0, 1, 700, 5000, 16384])
+def test_gpu_active_map_matches_restatement(n):
+    """``mpcx_active_map`` (C ABI v11) against its numpy restatement (`oracle/cpu_fleet.py`): the
+    active indices in increasing order, then -1, and the count."""
+    from oracle.cpu_fleet import CpuFleetOps
+
+    rng = np.random.default_rng(n)
+    act = (rng.random(n) < 0.3).astype(np.int32)
+    out = {}
+    for name, ops, dev in (("gpu", NativeADMMOps(), "cuda"), ("cpu", CpuFleetOps(), "cpu")):
+        amap = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        ops.active_map(n, torch.as_tensor(act, device=dev), amap, cnt)
+        out[name] = (amap.cpu().numpy(), int(cnt.item()))
+    np.testing.assert_array_equal(out["gpu"][0], out["cpu"][0])
+    assert out["gpu"][1] == out["cpu"][1] == int(act.sum())
+    np.testing.assert_array_equal(out["gpu"][0][:int(act.sum())], np.flatnonzero(act))
+
+
+def test_gpu_mapped_launch_matches_full_launch(monkeypatch):
+    """Coordinated rounds launch only the agents still active (``mpcx_active_map`` +
+    ``mpcx_batch_solve_mapped``, C ABI v11; the code object chosen by the launch size, so the
+    stragglers of a mostly converged fleet run the small-fleet build): a 256-block C2 fleet at
+    the reference's settings over two closed-loop steps gives every block the stopping iteration,
+    residual history and means of the same fleet launched whole (one launch of every agent, the
+    converged ones skipped in the kernel).  The builds differ in FMA contraction (1e-12)."""
+    N, kw = 10, dict(admm_iter_max=40, use_relative_tolerances=False, primal_tol=0.002, dual_tol=0.1)
+    runs = {}
+    for mapped in (True, False):
+        monkeypatch.setenv("MPCX_FLEET_MAP", "1" if mapped else "0")
+        fl = ADMMFleet(bm.c2_fleet_classes(n_blocks=256, N=N, seed=20261015 + 1, solver_options={"ipopt": {}}))
+        assert fl.map_launch == mapped
+        outs = []
+        for step in range(2):
+            if step:
+                bm.advance_plant(fl, 60.0)
+            outs.append(fl.run_coordinated(0.4, **kw))
+        bounds = [c.bound for c in fl.classes]
+        runs[mapped] = (outs, fl.trajectories(), bounds)
+    (om, tm, bm_), (of, tf, _) = runs[True], runs[False]
+    assert any(b < c.n for b, c in zip(bm_, fl.classes)), bm_   # the mapped fleet did shrink its launches
+    for a, b in zip(om, of):
+        np.testing.assert_array_equal(a["block_iterations"], b["block_iterations"])
+        assert a["converged_solves"] == b["converged_solves"]
+        for k in range(0, 256, 17):
+            ga = np.array([[r.primal_residual, r.dual_residual] for r in a["block_records"][k]])
+            gb = np.array([[r.primal_residual, r.dual_residual] for r in b["block_records"][k]])
+            np.testing.assert_allclose(ga, gb, rtol=1e-8, atol=1e-12)
+    for al in tm:
+        np.testing.assert_allclose(tm[al], tf[al], rtol=1e-8, atol=1e-11)

@@ -75,6 +75,16 @@ VARIANTS = {
     "apc24": (["-DMPCX_APC=24"], None),
     "apc32": (["-DMPCX_APC=32"], None),
     "lds_asm_noreg": (["-DMPCX_WS_LDS", "-DMPCX_ASM_NOREG"], None),
+    # r05: the kernel source of any revision (REV=<sha>) against the working tree, fleet and
+    # small-fleet builds
+    "rev": ([], "REV:" + os.environ.get("REV", "HEAD")),
+    "lds_rev": (["-DMPCX_WS_LDS"], "REV:" + os.environ.get("REV", "HEAD")),
+    # r05: IEEE divisions instead of the refined reciprocals (MPCX_RCP) in the generated elimination,
+    # alone and with a revision's kernel
+    "ieee": (["-DMPCX_IEEE_DIV"], None),
+    "rev_ieee": (["-DMPCX_IEEE_DIV"], "REV:" + os.environ.get("REV", "HEAD")),
+    "lds_ieee": (["-DMPCX_WS_LDS", "-DMPCX_IEEE_DIV"], None),
+    "lds_rev_ieee": (["-DMPCX_WS_LDS", "-DMPCX_IEEE_DIV"], "REV:" + os.environ.get("REV", "HEAD")),
 }
 
 

@@ -502,6 +502,24 @@ def generate(nlp: StageNLP, ts: float = None, _bordered=None) -> GeneratedModel:
         "#ifndef MPCX_ELIM_GROWTH  // threshold-pivoting bound on the static multipliers (runtime/stage_elim.py)",
         "#define MPCX_ELIM_GROWTH 1e8",
         "#endif",
+        "// reciprocals of pivots and slacks (mpcx_ipm.hip): v_rcp_f64 (2^-23 relative) refined by two",
+        "// Newton steps to within an ulp -- five dependent instructions instead of the eleven of an",
+        "// IEEE division (scaling, fixup); MPCX_IEEE_DIV keeps the division (A/B builds)",
+        "#ifndef MPCX_RCP",
+        "#ifdef MPCX_IEEE_DIV",
+        "__device__ __forceinline__ double mpcx_frcp(double x) { return 1.0 / x; }",
+        "#else",
+        "__device__ __forceinline__ double mpcx_frcp(double x) {",
+        "  const double r0 = __builtin_amdgcn_rcp(x);",
+        "  double r = fma(fma(-x, r0, 1.0), r0, r0);",
+        "  r = fma(fma(-x, r, 1.0), r, r);",
+        "  // 0, +-inf, NaN (x = +-inf, +-0, NaN or overflowing): v_rcp_f64's IEEE value, which the",
+        "  // Newton steps would turn into NaN (-0 * inf)",
+        "  return __builtin_amdgcn_class(r0, 0x267) ? r0 : r;  // classes snan | qnan | -inf | -0 | +0 | +inf",
+        "}",
+        "#endif",
+        "#define MPCX_RCP(x) mpcx_frcp(x)",
+        "#endif",
         "#ifndef MPCX_ELIM_FENCE  // scheduling fence between pivot blocks (register pressure)",
         "#define MPCX_ELIM_FENCE __builtin_amdgcn_sched_barrier(0)",
         "#endif",

@@ -57,7 +57,7 @@ class _Singular(Exception):
 def run(code, F: np.ndarray, ni: int, ntr: int, ns: int, nzx: int):
     env = {"_Singular": _Singular, "F": F, "fma": _fma, "abs": abs, "math": math, "bad": False, "pos": 0, "neg": 0,
            "TR": np.full(ni * ntr, np.nan), "S": np.full(max(ns, 1), np.nan), "ZX": np.full(max(nzx, 1), np.nan),
-           "PRM": np.full(ni, -1), "MPCX_N": 1, "MPCX_ELIM_GROWTH": 1e8}
+           "PRM": np.full(ni, -1), "MPCX_N": 1, "MPCX_ELIM_GROWTH": 1e8, "MPCX_RCP": lambda x: 1.0 / x}
     try:
         exec(code, env)
     except _Singular:

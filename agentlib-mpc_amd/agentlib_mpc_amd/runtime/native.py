@@ -392,8 +392,9 @@ class NativeProblem:
             raise NativeError(f"mpcx_set_options failed ({rc})")
 
     def set_small_fleet_max(self, max_agents: int):
-        """Largest batch launched on the small-fleet (workspace-in-LDS) build: -1 the
-        device's CU count (default), 0 never."""
+        """Largest batch launched on the small-fleet (workspace-in-LDS) build: -1 one generation
+        (the CU count times the agents a CU's LDS holds of that build, at most four; default),
+        0 never."""
         rc = self.lib.mpcx_problem_small_fleet(self.handle, None, int(max_agents))
         if rc != 0:
             raise NativeError(f"mpcx_problem_small_fleet failed ({rc})")

@@ -203,7 +203,7 @@ def emit(P: Sequence[Sequence[bool]], ni: int, nv: int, nx: int, nc: int,
             p = b[0]
             d = new(fac, f"F[{pk(p, p)}]")
             fac.append(f"  bad |= !(fabs({d}) > {ZERO_PIVOT}); pos += {d} > 0.0; neg += {d} < 0.0;")
-            r = new(fac, f"1.0 / {d}")
+            r = new(fac, f"MPCX_RCP({d})")
             u = {i: new(fac, f"F[{pk(i, p)}]") for i in col}
             lm = {i: (new(fac, f"{u[i]} * {r}"),) for i in col}
             if col:
@@ -221,7 +221,7 @@ def emit(P: Sequence[Sequence[bool]], ni: int, nv: int, nx: int, nc: int,
             fac.append(f"  bad |= !(fabs({det}) > {ZERO_PIVOT} * {ZERO_PIVOT});")
             fac.append(f"  if ({det} < 0.0) {{ pos += 1; neg += 1; }} else if ({a11} + {a22} > 0.0) pos += 2; "
                        f"else neg += 2;")
-            rd = new(fac, f"1.0 / {det}")
+            rd = new(fac, f"MPCX_RCP({det})")
             u1 = {i: new(fac, f"F[{pk(i, p)}]") for i in col}
             u2 = {i: new(fac, f"F[{pk(i, q)}]") for i in col}
             lm = {i: (new(fac, f"({u1[i]} * {a22} - {u2[i]} * {a21}) * {rd}"),

@@ -797,6 +797,14 @@ class CodeGen:
         names: Dict[int, str] = {}
         lines: List[str] = []
         n_groups = 0
+        # denominators divided by more than once: ONE reciprocal, then products (r05: the MHE
+        # Hessian divided by the same capacity term ten times per stage; a division is eleven
+        # dependent instructions on the GPU).  The products agree with the quotients to an ulp.
+        den_uses: Dict[int, int] = {}
+        for n in order:
+            if n.op == "div":
+                den_uses[n.args[1].uid] = den_uses.get(n.args[1].uid, 0) + 1
+        recips: Dict[int, str] = {}
         for n in order:
             if n.uid in names:
                 continue
@@ -825,7 +833,14 @@ class CodeGen:
                 lines += _emit_network(nid, a, members, gp, names, indent)
                 self.networks.add(nid)
                 continue
-            expr = _c_op(n.op, a)
+            if n.op == "div" and den_uses.get(n.args[1].uid, 0) > 1:
+                du = n.args[1].uid
+                if du not in recips:
+                    recips[du] = f"{self.prefix}{len(lines)}"
+                    lines.append(f"{indent}const double {recips[du]} = 1.0 / {a[1]};")
+                expr = f"{a[0]} * {recips[du]}"
+            else:
+                expr = _c_op(n.op, a)
             # temporaries are numbered in emission order (not by node uid), so the
             # generated source -- and the code-object cache key -- is independent of
             # what else the process has traced before

@@ -372,6 +372,7 @@ struct Trial {
 struct LSResult {
   Trial tr;
   double alpha;
+  double bar;  // barrier sum (sum of log slacks) at the last trial point
   int accepted, ftype, trials;
 };
 
@@ -395,6 +396,10 @@ struct KState {
   int resto, soft, soft_count, lsmode, nfilt0, square_r, n_soft, n_resto_it;
   int n_filt_over, n_refine;  // filter insertions that dropped the oldest entry; refinement steps
   double rnrm;                // refinement: max-norm of the step's full right-hand side
+  // the barrier sum at the current iterate when it is the last accepted line-search trial point
+  // (bar_ok): recover_step then takes it instead of recomputing every log of the slacks
+  double bar_val;
+  int bar_ok;
 };
 
 #ifndef MPCX_NETX
@@ -845,7 +850,7 @@ __device__ __noinline__ Inertia bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int la
         for (int i = k + 1 + lane; i < NN; i += WAVE) A[i * LD + k] = 0.0;
       } else {
         if (d > 0) in.pos++; else in.neg++;
-        const double rd = 1.0 / d;
+        const double rd = MPCX_RCP(d);
         for (int t = lane; t < NN2; t += WAVE) {
           const int i = t / NN, j = t % NN;
           if (i > k && j > k) A[i * LD + j] -= A[i * LD + k] * A[j * LD + k] * rd;
@@ -864,7 +869,7 @@ __device__ __noinline__ Inertia bk_factor(ldsd* A, ldsi* perm, ldsi* piv, int la
         else if (a11 + a22 > 0) in.pos += 2;
         else in.neg += 2;
       }
-      const double rdet = 1.0 / det;
+      const double rdet = MPCX_RCP(det);
       for (int t = lane; t < NN2; t += WAVE) {
         const int i = t / NN, j = t % NN;
         if (i > k + 1 && j > k + 1) {
@@ -983,7 +988,7 @@ __device__ __noinline__ Inertia bk_sweep(ldsd* A, OutT* out, int lane) {
       done |= 1u << p;
       if (fabs(d) <= ZERO_PIVOT) { in.zero++; zero |= 1u << p; continue; }
       if (d > 0) in.pos++; else in.neg++;
-      const double rd = 1.0 / d;
+      const double rd = MPCX_RCP(d);
       if (own) {
         const double aip = A[ti * LD + p], apj = A[p * LD + tj], aij = A[ti * LD + tj];
         A[ti * LD + tj] = (ti == p) ? ((tj == p) ? -rd : apj * rd) : (tj == p) ? aip * rd : aij - aip * apj * rd;
@@ -996,7 +1001,7 @@ __device__ __noinline__ Inertia bk_sweep(ldsd* A, OutT* out, int lane) {
       if (det < 0) { in.pos++; in.neg++; }
       else if (a11 + a22 > 0) in.pos += 2;
       else in.neg += 2;
-      const double rdet = 1.0 / det;
+      const double rdet = MPCX_RCP(det);
       const double p11 = a22 * rdet, p12 = -a21 * rdet, p22 = a11 * rdet;  // pivot-block inverse
       if (own) {
         const double aik = A[ti * LD + k], aiq = A[ti * LD + q], akj = A[k * LD + tj], aqj = A[q * LD + tj];
@@ -1082,7 +1087,7 @@ __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane)
         done |= 1u << p;
         if (fabs(d) <= ZERO_PIVOT) { in.zero++; zero |= 1u << p; continue; }
         if (d > 0) in.pos++; else in.neg++;
-        const double rd = 1.0 / d;
+        const double rd = MPCX_RCP(d);
         if (own) {
           const double aip = X[ti * LD + p], apj = X[p * LD + tj], aij = X[ti * LD + tj];
           X[ti * LD + tj] = (ti == p) ? ((tj == p) ? -rd : apj * rd) : (tj == p) ? aip * rd : aij - aip * apj * rd;
@@ -1095,7 +1100,7 @@ __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane)
         if (det < 0) { in.pos++; in.neg++; }
         else if (a11 + a22 > 0) in.pos += 2;
         else in.neg += 2;
-        const double rdet = 1.0 / det;
+        const double rdet = MPCX_RCP(det);
         const double p11 = a22 * rdet, p12 = -a21 * rdet, p22 = a11 * rdet;
         if (own) {
           const double aik = X[ti * LD + kk], aiq = X[ti * LD + q], akj = X[kk * LD + tj], aqj = X[q * LD + tj];
@@ -1151,6 +1156,14 @@ __device__ __forceinline__ double dual_diag_v(int cl, double sig, const KKTDiag 
   if (cl == 2) return 1.0;
   return 1.0 / (sig + kd.dw) + kd.dc;
 }
+// The per-iteration vector phases (iteration head, inertia-correction rhs, step recovery,
+// accept) take ONE reciprocal per slack, 1 / (x - lo) and 1 / (hi - x), and multiply, where the
+// formulas divide several numerators by the same slack (mu / s, z / s, Sigma = z / s, ...); the
+// reciprocal is MPCX_RCP (v_rcp_f64 + two Newton steps, generated preamble).  The quotients agree
+// with the divisions to an ulp or two; the oracle's decisions (statuses, iteration counts) are
+// unchanged on every parity case (tests/test_gpu_ipm.py).  r05: a division is eleven dependent
+// VALU instructions, and these phases held ~120 of them per iteration.
+__device__ __forceinline__ double rcp_or0(bool fin, double s) { return fin ? MPCX_RCP(s) : 0.0; }
 
 // ---------------------------------------------------------------------------
 // sequential block chain (fallback when a stage interior is singular)
@@ -1731,14 +1744,58 @@ __device__ MPCX_HOT Inertia chain_factor(const Agent a) {
       aj = fx ? 1.0 : s11(lane)[0] + (lane + 1 < N ? s00(lane + 1)[0] : 0.0);
       if (!fx && lane > 0) { const double t = s10(lane)[0]; bj = t * t; }
     }
-    double dprev = 0.0, mine = 0.0;
+    // The pivots d_j = a_j - b_j / d_{j-1} are ratios p_j / p_{j-1} of the three-term recurrence
+    // p_j = a_j p_{j-1} - b_j p_{j-2} (leading minors of the chain): lane j forms the prefix
+    // product of M_j = [[a_j, -b_j], [1, 0]] by a Hillis-Steele scan inside its row of 16 lanes
+    // (DPP row shifts, log2 N steps, each partial product rescaled by a power of two: the ratio
+    // of its first column is scale-free), then d_j = P_j[0][0] / P_j[1][0] -- one division per
+    // lane instead of N dependent ones.  Near a zero pivot (or on overflow) the serial recurrence
+    // runs instead, with its zero-pivot rule (a zero pivot restarts the chain).
+    bool serial = true;
+    double mine = 0.0;
+#ifdef MPCX_CHAIN_SERIAL  // diagnostics (A/B): the serial recurrence only
+    if constexpr (false) {
+#else
+    if constexpr (N <= 16) {
+#endif
+      double p00 = aj, p01 = -bj, p10 = 1.0, p11 = 0.0;  // lane j: M_j, then M_j ... M_0
+      if (lane >= N) { p00 = 1.0; p01 = 0.0; p10 = 0.0; p11 = 1.0; }
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const double a = rl_f64(aj, j), b = rl_f64(bj, j);
-      const double d = a - b * dprev;
-      if (fabs(d) <= ZERO_PIVOT) { in.zero++; dprev = 0.0; }
-      else { if (d > 0) in.pos++; else in.neg++; dprev = 1.0 / d; }
-      if (lane == j) mine = dprev;
+      for (int sh = 1; sh < N; sh <<= 1) {
+        // the partial product ending sh lanes below (row_shr:sh), identity below the row start
+        double q00, q01, q10, q11;
+        if (sh == 1) { q00 = dpp_f64<0x111>(p00); q01 = dpp_f64<0x111>(p01); q10 = dpp_f64<0x111>(p10); q11 = dpp_f64<0x111>(p11); }
+        else if (sh == 2) { q00 = dpp_f64<0x112>(p00); q01 = dpp_f64<0x112>(p01); q10 = dpp_f64<0x112>(p10); q11 = dpp_f64<0x112>(p11); }
+        else if (sh == 4) { q00 = dpp_f64<0x114>(p00); q01 = dpp_f64<0x114>(p01); q10 = dpp_f64<0x114>(p10); q11 = dpp_f64<0x114>(p11); }
+        else { q00 = dpp_f64<0x118>(p00); q01 = dpp_f64<0x118>(p01); q10 = dpp_f64<0x118>(p10); q11 = dpp_f64<0x118>(p11); }
+        if ((lane & 15) >= sh) {
+          const double r00 = p00 * q00 + p01 * q10, r01 = p00 * q01 + p01 * q11;
+          const double r10 = p10 * q00 + p11 * q10, r11 = p10 * q01 + p11 * q11;
+          const double mx = fmax(fmax(fabs(r00), fabs(r01)), fmax(fabs(r10), fabs(r11)));
+          const int e = mx > 0.0 && mx < INFINITY ? ilogb(mx) : 0;
+          p00 = ldexp(r00, -e); p01 = ldexp(r01, -e); p10 = ldexp(r10, -e); p11 = ldexp(r11, -e);
+        }
+      }
+      const double d = p00 / p10;
+      const bool ok = lane >= N || (isfin(d) && fabs(d) > 1e-8 * fmax(fabs(aj), 1e-300) && fabs(d) > ZERO_PIVOT);
+      serial = !__all(ok);
+      if (!serial) {
+        mine = MPCX_RCP(d);
+        const unsigned long long pos = __ballot(lane < N && d > 0.0);
+        in.pos = __popcll(pos);
+        in.neg = N - in.pos;
+      }
+    }
+    if (serial) {
+      double dprev = 0.0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const double a = rl_f64(aj, j), b = rl_f64(bj, j);
+        const double d = a - b * dprev;
+        if (fabs(d) <= ZERO_PIVOT) { in.zero++; dprev = 0.0; }
+        else { if (d > 0) in.pos++; else in.neg++; dprev = MPCX_RCP(d); }
+        if (lane == j) mine = dprev;
+      }
     }
     if (lane < N) L.Dinv[lane] = mine;
   } else if constexpr (NC > 0) {
@@ -2489,19 +2546,21 @@ __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, doubl
     if (on) {
       const int cl = cls_of(lbv, ubv, slo, sup);
       double rr;
+      const double rsl = rcp_or0(cl == 1 && isfin(slo), sv - slo), rsu = rcp_or0(cl == 1 && isfin(sup), sup - sv);
+      const double rsd = rcp_or0(cl == 1, vl * rsl + vu * rsu + dw);  // 1 / (Sigma_s + delta_w)
       if (cl == 0) {
         rr = -(gvv - gsc * lbv);
       } else {
         rr = -(gvv - sv);
         if (cl == 1) {
           double gphis = 0.0;
-          if (isfin(slo)) gphis -= mu / (sv - slo);
-          if (isfin(sup)) gphis += mu / (sup - sv);
-          rr -= (gphis - lm) / (sigma_s_v(sv, slo, sup, vl, vu) + dw);
+          if (isfin(slo)) gphis -= mu * rsl;
+          if (isfin(sup)) gphis += mu * rsu;
+          rr -= (gphis - lm) * rsd;
         }
       }
       a.rhs(c / NG)[NP + c % NG] = rr;
-      a.dg(c / NG)[crow(c % NG)] = -dual_diag_v(cl, sigma_s_v(sv, slo, sup, vl, vu), KKTDiag{dw, dc, NEWTON});
+      a.dg(c / NG)[crow(c % NG)] = (cl == 0) ? -dc : (cl == 2) ? -1.0 : -(rsd + dc);
     }
   }
   sync();
@@ -2540,9 +2599,34 @@ __device__ __noinline__ void ls_mult_finish(const Agent a, const double constr_m
 
 // full step from the Newton solution (LDS) + fraction-to-the-boundary step
 // sizes + constraint violation and barrier at the current point
-__device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, double dw, double obj_scale) {
+// running minimum of step-size ratios num / den (num >= 0, den > 0) kept as the pair: one
+// division per lane at the end instead of one per candidate; the quotient taken is the one the
+// per-candidate division gives for the minimising candidate (rounding is monotone)
+#ifndef MPCX_RATIO_FMIN
+struct RatioMin {
+  double n = 1.0, d = 1.0;  // the default step size 1
+  __device__ __forceinline__ void take(double num, double den) {
+    if (num * d < n * den) { n = num; d = den; }
+  }
+  __device__ __forceinline__ double value() const { return n / d; }
+};
+#else  // diagnostics (A/B): one division per candidate
+struct RatioMin {
+  double v = 1.0;
+  __device__ __forceinline__ void take(double num, double den) { v = fmin(v, num / den); }
+  __device__ __forceinline__ double value() const { return v; }
+};
+#endif
+
+// full step from the Newton solution (LDS) + fraction-to-the-boundary step sizes + constraint
+// violation at the current point; the barrier sum too unless the caller passes the cached one
+// (bar_cached: the current point is the last accepted trial point, whose logs the line search
+// summed -- the logs were a fifth of this phase's instructions)
+__device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, double dw, double obj_scale,
+                                          int bar_cached) {
   const int lane = lane_now();
-  double amax = 1.0, az = 1.0, gphid = 0.0, theta = 0.0, bar = 0.0;
+  RatioMin ra, rz;
+  double gphid = 0.0, theta = 0.0, bar = 0.0;
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
@@ -2558,20 +2642,20 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
     if (!free_) continue;
     double gphi = obj_scale * gr;
     if (isfin(lo)) {
-      const double s_l = xv - lo;
-      gphi -= mu / s_l;
-      if (d < 0) amax = fmin(amax, -tau * s_l / d);
-      const double dz = mu / s_l - zl - (zl / s_l) * d;
-      if (dz < 0) az = fmin(az, -tau * zl / dz);
-      bar += log(s_l);
+      const double s_l = xv - lo, rl = MPCX_RCP(s_l);
+      gphi -= mu * rl;
+      if (d < 0) ra.take(tau * s_l, -d);
+      const double dz = mu * rl - zl - (zl * rl) * d;
+      if (dz < 0) rz.take(tau * zl, -dz);
+      if (!bar_cached) bar += log(s_l);
     }
     if (isfin(hi)) {
-      const double s_u = hi - xv;
-      gphi += mu / s_u;
-      if (d > 0) amax = fmin(amax, tau * s_u / d);
-      const double dz = mu / s_u - zu + (zu / s_u) * d;
-      if (dz < 0) az = fmin(az, -tau * zu / dz);
-      bar += log(s_u);
+      const double s_u = hi - xv, ru = MPCX_RCP(s_u);
+      gphi += mu * ru;
+      if (d > 0) ra.take(tau * s_u, d);
+      const double dz = mu * ru - zu + (zu * ru) * d;
+      if (dz < 0) rz.take(tau * zu, -dz);
+      if (!bar_cached) bar += log(s_u);
     }
     gphid += gphi * d;
   }
@@ -2590,35 +2674,36 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
     theta += fabs((cl == 0) ? gvv - gsc * lbv : gvv - sv);
     double dsv = 0.0;
     if (cl == 1) {
+      const double rsl = rcp_or0(isfin(slo), sv - slo), rsu = rcp_or0(isfin(sup), sup - sv);
       double gphis = 0.0;
-      if (isfin(slo)) gphis -= mu / (sv - slo);
-      if (isfin(sup)) gphis += mu / (sup - sv);
+      if (isfin(slo)) gphis -= mu * rsl;
+      if (isfin(sup)) gphis += mu * rsu;
       const double rs = gphis - lm;
-      dsv = (dlam - rs) / (sigma_s_v(sv, slo, sup, vl, vu) + dw);
+      dsv = (dlam - rs) * MPCX_RCP(vl * rsl + vu * rsu + dw);
       gphid += (rs + lm) * dsv;
       if (isfin(slo)) {
         const double s_l = sv - slo;
-        if (dsv < 0) amax = fmin(amax, -tau * s_l / dsv);
-        const double dv = mu / s_l - vl - (vl / s_l) * dsv;
-        if (dv < 0) az = fmin(az, -tau * vl / dv);
-        bar += log(s_l);
+        if (dsv < 0) ra.take(tau * s_l, -dsv);
+        const double dv = mu * rsl - vl - (vl * rsl) * dsv;
+        if (dv < 0) rz.take(tau * vl, -dv);
+        if (!bar_cached) bar += log(s_l);
       }
       if (isfin(sup)) {
         const double s_u = sup - sv;
-        if (dsv > 0) amax = fmin(amax, tau * s_u / dsv);
-        const double dv = mu / s_u - vu + (vu / s_u) * dsv;
-        if (dv < 0) az = fmin(az, -tau * vu / dv);
-        bar += log(s_u);
+        if (dsv > 0) ra.take(tau * s_u, dsv);
+        const double dv = mu * rsu - vu + (vu * rsu) * dsv;
+        if (dv < 0) rz.take(tau * vu, -dv);
+        if (!bar_cached) bar += log(s_u);
       }
     }
     a.ds()[c] = dsv;
   }
   StepInfo st;
-  st.amax = wmin(amax);
-  st.az = wmin(az);
+  st.amax = wmin(ra.value());
+  st.az = wmin(rz.value());
   st.gphid = wsum(gphid);
   st.theta = wsum(theta);
-  st.barrier = wsum(bar);
+  st.barrier = bar_cached ? gL.ks.bar_val : wsum(bar);
   return st;
 }
 
@@ -2658,7 +2743,9 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     K.ls.accepted = 0;
     K.ls.ftype = 0;
     K.ls.trials = 0;
-    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};    TRACE_LS_HEAD(argp);
+    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};
+    K.ls.bar = 0.0;
+    TRACE_LS_HEAD(argp);
   }
 #pragma unroll 1
   for (int ls = 0; ls < 64; ++ls) {
@@ -2711,8 +2798,10 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     const double phi = K.fx - mu * K.st.barrier;
     Trial tr = K.ls.tr;
     tr.theta = wsum(th);
-    tr.phi = tr.f - mu * (K.barx + wsum(bar));
+    const double trial_bar = K.barx + wsum(bar);
+    tr.phi = tr.f - mu * trial_bar;
     K.ls.tr = tr;
+    K.ls.bar = trial_bar;
     K.ls.trials += 1;
     bool okt = (tr.theta <= K.theta_max) && (tr.phi == tr.phi);
     {  // filter test, one entry per lane (MAXF <= 64): one LDS read instead of nfilt in sequence
@@ -2746,6 +2835,7 @@ __device__ MPCX_HOT void line_search(const Agent a) {
 // take the last trial point (xt, gt in LDS) and the multiplier steps
 __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, double mu, double alpha, double az) {
   const int lane = lane_now();
+  const double ksm = kappa_sigma * mu, mks = mu * MPCX_RCP(kappa_sigma);  // the kappa_sigma safeguard's bounds x s
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
@@ -2757,16 +2847,16 @@ __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, do
     if (!on || lo == hi) continue;
     a.x()[i] = xn;
     if (isfin(lo)) {
-      const double sl0 = xold - lo;
-      const double dz = mu / sl0 - zl - (zl / sl0) * d;
-      const double zn = zl + az * dz, s_l = xn - lo;
-      a.zL()[i] = fmax(fmin(zn, kappa_sigma * mu / s_l), mu / (kappa_sigma * s_l));
+      const double r0 = MPCX_RCP(xold - lo);
+      const double dz = mu * r0 - zl - (zl * r0) * d;
+      const double zn = zl + az * dz, rn = MPCX_RCP(xn - lo);
+      a.zL()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
     }
     if (isfin(hi)) {
-      const double su0 = hi - xold;
-      const double dz = mu / su0 - zu + (zu / su0) * d;
-      const double zn = zu + az * dz, s_u = hi - xn;
-      a.zU()[i] = fmax(fmin(zn, kappa_sigma * mu / s_u), mu / (kappa_sigma * s_u));
+      const double r0 = MPCX_RCP(hi - xold);
+      const double dz = mu * r0 - zu + (zu * r0) * d;
+      const double zn = zu + az * dz, rn = MPCX_RCP(hi - xn);
+      a.zU()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
     }
   }
 #pragma unroll
@@ -2785,16 +2875,16 @@ __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, do
     a.s()[c] = sn;
     if (cls_of(lbv, ubv, slo, sup) != 1) continue;
     if (isfin(slo)) {
-      const double sl0 = sold - slo;
-      const double dv = mu / sl0 - vl - (vl / sl0) * dsv;
-      const double vn = vl + az * dv, s_l = sn - slo;
-      a.vL()[c] = fmax(fmin(vn, kappa_sigma * mu / s_l), mu / (kappa_sigma * s_l));
+      const double r0 = MPCX_RCP(sold - slo);
+      const double dv = mu * r0 - vl - (vl * r0) * dsv;
+      const double vn = vl + az * dv, rn = MPCX_RCP(sn - slo);
+      a.vL()[c] = fmax(fmin(vn, ksm * rn), mks * rn);
     }
     if (isfin(sup)) {
-      const double su0 = sup - sold;
-      const double dv = mu / su0 - vu + (vu / su0) * dsv;
-      const double vn = vu + az * dv, s_u = sup - sn;
-      a.vU()[c] = fmax(fmin(vn, kappa_sigma * mu / s_u), mu / (kappa_sigma * s_u));
+      const double r0 = MPCX_RCP(sup - sold);
+      const double dv = mu * r0 - vu + (vu * r0) * dsv;
+      const double vn = vu + az * dv, rn = MPCX_RCP(sup - sn);
+      a.vU()[c] = fmax(fmin(vn, ksm * rn), mks * rn);
     }
   }
 }
@@ -2846,9 +2936,10 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
       double xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
       const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
       const bool on = i >= NX && i < NW && lo != hi;
+      const double rl = rcp_or0(isfin(lo) && lo != hi, xv - lo), ru = rcp_or0(isfin(hi) && lo != hi, hi - xv);
       pr0[sl] = on ? -(obj_scale * gr + jt) : 0.0;
-      pr1[sl] = on ? (isfin(lo) ? 1.0 / (xv - lo) : 0.0) - (isfin(hi) ? 1.0 / (hi - xv) : 0.0) : 0.0;
-      psx[sl] = sigma_x_v(xv, lo, hi, zl, zu);
+      pr1[sl] = on ? rl - ru : 0.0;
+      psx[sl] = (lo == hi) ? 0.0 : zl * rl + zu * ru;  // sigma_x_v
       if (on) {
         const double rd = obj_scale * gr + jt - zl + zu;
         dmax = fmax(dmax, fabs(rd));
@@ -2866,11 +2957,13 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
       double gvv = a.gv()[cc], sv = a.s()[cc], vl = a.vL()[cc], vu = a.vU()[cc];
       const int cl = cls_of(lbv, ubv, slo, sup);
       {
-        const double sg = sigma_s_v(sv, slo, sup, vl, vu);
+        const double rsl = rcp_or0(cl == 1 && isfin(slo), sv - slo), rsu = rcp_or0(cl == 1 && isfin(sup), sup - sv);
+        const double sg = vl * rsl + vu * rsu;  // sigma_s_v
+        const double rsg = rcp_or0(cl == 1, sg);
         const double r = (cl == 0) ? -(gvv - gsc * lbv) : -(gvv - sv);
-        dq0[sl] = (cl == 1) ? r + lm / sg : r;
-        dq1[sl] = (cl == 1) ? ((isfin(sup) ? 1.0 / (sup - sv) : 0.0) - (isfin(slo) ? 1.0 / (sv - slo) : 0.0)) / sg : 0.0;
-        ddg[sl] = -dual_diag_v(cl, sg, KKTDiag{0.0, 0.0, NEWTON});
+        dq0[sl] = (cl == 1) ? r + lm * rsg : r;
+        dq1[sl] = (cl == 1) ? (rsu - rsl) * rsg : 0.0;
+        ddg[sl] = (cl == 0) ? -0.0 : (cl == 2) ? -1.0 : -rsg;  // -dual_diag_v at delta_w = delta_c = 0
       }
       if (c < M) {
         double cv, vv = 0.0;
@@ -3703,7 +3796,9 @@ __device__ __noinline__ void line_search_resto(const Agent a) {
     K.ls.accepted = 0;
     K.ls.ftype = 0;
     K.ls.trials = 0;
-    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};    TRACE_LS_HEAD(argp);
+    K.ls.tr = Trial{0.0, 0.0, 0.0, 0.0};
+    K.ls.bar = 0.0;
+    TRACE_LS_HEAD(argp);
   }
 #pragma unroll 1
   for (int ls = 0; ls < 64; ++ls) {
@@ -3956,6 +4051,7 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
   K.acc = Acceptable{-1e50, -1e50, -1, 0};
   K.resto = 0; K.soft = 0; K.soft_count = 0; K.lsmode = 0; K.n_soft = 0; K.n_resto_it = 0;
   K.n_filt_over = 0; K.n_refine = 0;
+  K.bar_ok = 0; K.bar_val = 0.0;
 #define KARGP ((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())
 #pragma unroll 1
   for (;;) {
@@ -4026,7 +4122,11 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
       const StepInfo st = recover_step_resto(a, K.mu, K.tau, K.dw);
       K.st = st;
     } else {
-      const StepInfo st = recover_step(a, K.mu, K.tau, K.dw, K.obj_scale);
+#ifndef MPCX_NO_BARCACHE
+      const StepInfo st = recover_step(a, K.mu, K.tau, K.dw, K.obj_scale, K.bar_ok);
+#else  // diagnostics (A/B): the barrier recomputed at every iterate
+      const StepInfo st = recover_step(a, K.mu, K.tau, K.dw, K.obj_scale, 0);
+#endif
       K.st = st;
     }
     PROF(7);
@@ -4037,6 +4137,7 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
     // filter line search; on failure the soft restoration step, then the restoration phase
     // (IPOPT BacktrackingLineSearch::FindAcceptableTrialPoint)
     const int mode = search_step(a);
+    K.bar_ok = 0;                // the iterate changes below; only an accepted trial re-validates it
     if (mode == -2) break;       // acceptable point, status set
     if (mode == -1) continue;    // restoration phase started
     if (mode == 2) {  // the soft trial is already the iterate
@@ -4050,6 +4151,8 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
     wsync();
     PROF(8);
     accept_step(a, OPT(kappa_sigma), K.mu, K.ls.alpha, mode == 1 ? K.ls.alpha : K.st.az);
+    K.bar_val = K.ls.bar;        // the new iterate IS the last trial point: its barrier sum holds
+    K.bar_ok = 1;
     sync();  // accepted multipliers visible to the stage lanes
     eval_gj_lds(a);
     sync();

@@ -152,7 +152,8 @@ int64_t mpcx_workspace_bytes_per_agent(const mpcx_handle* h);
  * workspace in LDS (MPCX_WS_LDS, one agent per CU), so that every operand round trip of the
  * IPM is an LDS access instead of an L2 / HBM one.  code_object_path NULL keeps the loaded
  * one.  mpcx_batch_solve launches it for batches of at most max_agents agents
- * (max_agents < 0: the device's CU count, one generation; 0: never).  Returns
+ * (max_agents < 0: one generation -- the CU count times the agents a CU's LDS holds of this
+ * build, at most four; 0: never).  Returns
  * MPCX_ERR_MODULE if the code object is not such a variant of this structure. */
 int mpcx_problem_small_fleet(mpcx_handle* h, const char* code_object_path, int32_t max_agents);
 

@@ -33,6 +33,55 @@ step_s2() {
   echo "tests exit $rc, scan exit $?"
 }
 
+step_s3() {
+  # r05/s3: the long restoration cases with the refined reciprocals (now IEEE on 0 / inf / NaN)
+  # and with IEEE divisions (MPCX_IEEE_DIV builds), the tol 1e-8 C3 A/B with iteration counts,
+  # then the GPU parity suite
+  mkdir -p gpurun_out/s3
+  K="long_restoration"
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_ipm.py -m gpu -q -s -rfE --timeout 300 --timeout-method thread -k "$K" > gpurun_out/s3/long_resto_rcp.txt 2>&1
+  rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+  MPCX_DEFINES=MPCX_IEEE_DIV timeout -k 10 600 python -u -m pytest tests/test_gpu_ipm.py -m gpu -q -s -rfE --timeout 300 --timeout-method thread -k "$K" > gpurun_out/s3/long_resto_ieee.txt 2>&1
+  rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+  timeout -k 10 300 python -u scripts/variants.py run base ieee rev_ieee base ieee > gpurun_out/s3/var_c3_tight.txt 2>&1 || exit $?
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s3/gpu_tests.txt 2>&1
+  echo "tests exit $?"
+}
+
+step_s4() {
+  # r05/s4: which of the r05 kernel changes moves the rounding-chaotic restoration case kw1 (10
+  # restoration phases at the reference settings): each diagnostic toggle alone, all of them, all
+  # with IEEE divisions (main build only); then the default build
+  mkdir -p gpurun_out/s4
+  K="long_restoration and kw1 and main"
+  for D in "" MPCX_NO_BARCACHE MPCX_RATIO_FMIN MPCX_CHAIN_SERIAL MPCX_NO_BARCACHE,MPCX_RATIO_FMIN,MPCX_CHAIN_SERIAL MPCX_IEEE_DIV,MPCX_NO_BARCACHE,MPCX_RATIO_FMIN,MPCX_CHAIN_SERIAL; do
+    echo "== MPCX_DEFINES=$D" >> gpurun_out/s4/kw1.txt
+    MPCX_DEFINES=$D MPCX_SMALL_FLEET=0 MPCX_MID_FLEET=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_ipm.py -m gpu -q -s --timeout 240 --timeout-method thread -k "$K" >> gpurun_out/s4/kw1.txt 2>&1
+    rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+  done
+  echo "s4 exit 0"
+}
+
+step_rec() {
+  # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
+  # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,
+  # the 2-rank gloo rehearsal; TESTS=1 runs the GPU parity suite first
+  OUT=${OUT:-profiles/r05/rec}
+  mkdir -p gpurun_out/rec "$OUT"
+  if [ "${TESTS:-0}" = 1 ]; then
+    timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/rec/gpu_tests.txt 2>&1 || exit $?
+    timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/rec/smoke.txt 2>&1 || exit $?
+  fi
+  PMC_OUT=$OUT bash scripts/gpu_pmc.sh || exit $?
+  mkdir -p gpurun_out/rec/pmc && cp $OUT/* gpurun_out/rec/pmc/
+  timeout -k 10 900 python -u bench.py > gpurun_out/rec/bench.json 2> gpurun_out/rec/bench.err || exit $?
+  rm -rf gpurun_out/rec/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rec/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --admm-agents 0 --c2-blocks 0 --c5-blocks 0 > gpurun_out/rec/prof_bench.json 2> gpurun_out/rec/prof.err || exit $?
+  python scripts/trace_summary.py gpurun_out/rec/prof gpurun_out/rec/kernel_trace_summary.txt > /dev/null
+  bash scripts/gpu_mgpu_rehearsal.sh > gpurun_out/rec/mgpu.txt 2>&1
+  echo "rec exit $?"
+}
+
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }
 "$fn"

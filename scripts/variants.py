@@ -182,7 +182,12 @@ def run(names):
         if ref is None:
             ref = w
         dev_max = float(np.max(np.abs(w - ref) / (1 + np.abs(ref))))
-        res[name] = {"ms": ms, "solves_per_s": ok / ms * 1e3, "ok": ok, "maxdev_vs_first": dev_max}
+        its = [x["iter_count"] for x in stats]
+        res[name] = {"ms": ms, "solves_per_s": ok / ms * 1e3, "ok": ok, "maxdev_vs_first": dev_max,
+                     "iters_mean_max": [float(np.mean(its)), int(np.max(its))],
+                     "statuses": sorted({x["status"] for x in stats}),
+                     "restorations": int(sum(x["n_restorations"] for x in stats)),
+                     "dense_stages": int(sum(x["n_dense_stages"] for x in stats))}
         print(name, json.dumps(res[name]), flush=True)
         del nat
     return res

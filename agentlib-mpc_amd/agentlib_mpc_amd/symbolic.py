@@ -800,9 +800,10 @@ class CodeGen:
         # denominators divided by more than once: ONE reciprocal, then products (r05: the MHE
         # Hessian divided by the same capacity term ten times per stage; a division is eleven
         # dependent instructions on the GPU).  The products agree with the quotients to an ulp.
+        # (constant denominators keep their divisions: x / 10.0 is not x * 0.1)
         den_uses: Dict[int, int] = {}
         for n in order:
-            if n.op == "div":
+            if n.op == "div" and n.args[1].op != "const":
                 den_uses[n.args[1].uid] = den_uses.get(n.args[1].uid, 0) + 1
         recips: Dict[int, str] = {}
         for n in order:

@@ -1777,10 +1777,17 @@ __device__ MPCX_HOT Inertia chain_factor(const Agent a) {
         }
       }
       const double d = p00 / p10;
-      const bool ok = lane >= N || (isfin(d) && fabs(d) > 1e-8 * fmax(fabs(aj), 1e-300) && fabs(d) > ZERO_PIVOT);
+      const double r = MPCX_RCP(d);
+      // a posteriori: every pivot must satisfy the recurrence with its neighbour's pivot to the
+      // rounding of its terms (the minors' products cancel where the chain is nearly singular --
+      // restoration phases -- and their errors compound along the scan, unlike the recurrence's)
+      const double rprev = dpp_f64<0x111>(r);  // 1 / d_{j-1} (row_shr:1; lane 0 has b_0 = 0)
+      const double rec = aj - bj * ((lane & 15) > 0 ? rprev : 0.0);
+      const bool ok = lane >= N || (isfin(d) && fabs(d) > 1e-8 * fmax(fabs(aj), 1e-300) && fabs(d) > ZERO_PIVOT &&
+                                    fabs(d - rec) <= 1e-12 * (fabs(aj) + fabs(bj * rprev)));
       serial = !__all(ok);
       if (!serial) {
-        mine = MPCX_RCP(d);
+        mine = r;
         const unsigned long long pos = __ballot(lane < N && d > 0.0);
         in.pos = __popcll(pos);
         in.neg = N - in.pos;

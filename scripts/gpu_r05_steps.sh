@@ -59,7 +59,11 @@ step_s4() {
     MPCX_DEFINES=$D MPCX_SMALL_FLEET=0 MPCX_MID_FLEET=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_ipm.py -m gpu -q -s --timeout 240 --timeout-method thread -k "$K" >> gpurun_out/s4/kw1.txt 2>&1
     rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
   done
-  echo "s4 exit 0"
+  # per-phase cycles of the r05 kernel: C1 (small-fleet build) and the C3 fleet
+  WSLDS=1 AGENTS=1 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s4/phases_c1_lds.txt 2>&1 || exit $?
+  AGENTS=4096 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s4/phases_c3.txt 2>&1 || exit $?
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s4/gpu_tests.txt 2>&1
+  echo "s4 exit $?"
 }
 
 step_rec() {

@@ -68,3 +68,34 @@ def test_scan_survives_the_range_of_a_restoration_chain():
     a = np.full(n, 3e20)
     b = np.concatenate([[0.0], np.full(n - 1, 1e40)])
     np.testing.assert_allclose(scan(a, b), serial(a, b), rtol=1e-12)
+
+
+def accepted(a, b, d):
+    """The kernel's acceptance of a scanned chain (else it runs the serial recurrence): finite
+    pivots away from zero relative to their diagonals, each satisfying the recurrence with its
+    neighbour's pivot to the rounding of its terms."""
+    r = 1.0 / d
+    rprev = np.concatenate([[0.0], r[:-1]])
+    rec = a - b * rprev
+    return bool(np.all(np.isfinite(d)) and np.all(np.abs(d) > 1e-8 * np.abs(a)) and np.all(np.abs(d) > 1e-20)
+                and np.all(np.abs(d - rec) <= 1e-12 * (np.abs(a) + np.abs(b * rprev))))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_accepted_scans_agree_with_the_recurrence_on_near_singular_chains(seed):
+    """Chains with strong cancellation (each pivot 1e-3..1e-7 of its diagonal, indefinite signs: the
+    restoration phase's chains): whenever the kernel's checks accept the scan, its pivots agree with
+    the serial recurrence; rejected chains take the recurrence itself."""
+    rng = np.random.default_rng(100 + seed)
+    n = 15
+    a = 10.0 ** rng.uniform(-2, 6, n) * rng.choice([-1.0, 1.0], n)
+    b = np.zeros(n)
+    d = np.zeros(n)
+    d[0] = a[0]
+    for j in range(1, n):   # b_j chosen so that d_j = a_j - b_j / d_{j-1} is a tiny fraction of a_j
+        target = a[j] * 10.0 ** rng.uniform(-7, -3)
+        b[j] = abs((a[j] - target) * d[j - 1])
+        d[j] = a[j] - b[j] / d[j - 1]
+    ds, dq = serial(a, b), scan(a, b)
+    if accepted(a, b, dq):
+        np.testing.assert_allclose(dq, ds, rtol=1e-6)

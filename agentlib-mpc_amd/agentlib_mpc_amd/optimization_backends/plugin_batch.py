@@ -13,7 +13,9 @@ call costs an order of magnitude more than the kernel at fleet sizes.
 * reads every (variable, attribute) the marshalling needs in ONE native pass over the
   agents (``csrc/mpcx_pyread.c``: dict lookup, attribute lookup, float unpack into one
   buffer; Python iterators cost ~90 ns per read, 3-6 ms per 4096-agent call, more than
-  the kernel); lists, series and other trajectories take the sampling path of
+  the kernel); a variable whose instance dict has not changed since the last call (the
+  dict's version tag) costs no lookups at all; lists, series and other trajectories take
+  the sampling path of
   :class:`~agentlib_mpc_amd.optimization_backends.problem.BatchMarshal`, with the same
   errors for empty values and non-``MPCVariable`` inputs);
 * uploads only the columns whose values changed since the last call and scatters them
@@ -147,6 +149,9 @@ class ResidentBatch:
         from agentlib_mpc_amd.runtime.native import load_pyread
 
         self.pyread = load_pyread()
+        # the reader's numbers of the last call, per (agent, variable), reused while the agent's
+        # mapping and the variable's instance dict are unchanged (csrc/mpcx_pyread.c)
+        self._read_cache = self.pyread.new_cache()
         self.specs = None
         # full marshal once: device arrays, template rows, the values of this call
         p, lbw, ubw, w0, (ls, us) = m.inputs(batch_vars, now, None, return_sampled_bounds=True)
@@ -218,7 +223,7 @@ class ResidentBatch:
             batch_vars = list(batch_vars)
         buf = np.empty((self.n_cols, n), dtype=np.float64)
         try:
-            status, bad = self.pyread.read_columns(batch_vars, self.specs, buf)
+            status, bad = self.pyread.read_columns(batch_vars, self.specs, buf, self._read_cache)
         except KeyError:  # a variable missing: the Python path raises it in the reference's order
             return self._read_python(batch_vars, now, self.refs)
         prev = self._prev_buf

@@ -80,6 +80,27 @@ def _cuda():
         pytest.skip("no GPU")
 
 
+#: cases whose NLP has several local minima among which the interior-point path is chosen by
+#: rounding: one_room_switch at the tight options (bilinear dynamics, switched objective) -- the
+#: oracle itself ends at 5714.008, 5714.924 or 5715.828 when w0 is perturbed by 1e-12 relative
+#: (12 seeded perturbations, r05), and the kernel builds at 5714.008 or 5714.604.  A kernel result
+#: off the oracle's minimum must then be a local minimum of the same NLP (below).
+MULTI_MINIMA = {("one_room_switch", "{}")}
+
+
+def _assert_oracle_local_minimum(case, r):
+    """The oracle warm-started at the kernel's point (mu 1e-9, bound push 1e-9: IPOPT's warm
+    start) converges there within a few iterations, to the kernel's objective and point."""
+    p, lbw, ubw, _ = case.oracle_inputs
+    w = _w_of(case, r)
+    opts = ipm.IPMOptions(tol=1e-10, max_iter=50, acceptable_iter=0, mu_init=1e-9, bound_push=1e-9,
+                          bound_frac=1e-9)
+    chk = ipm.solve(case.oracle.functions(p), w, lbw, ubw, case.oracle.lbg(p), case.oracle.ubg(p), opts)
+    assert chk.success and chk.iterations <= 10, (chk.status, chk.iterations)
+    np.testing.assert_allclose(chk.f, r.stats["obj"], rtol=RTOL_OBJ, atol=1e-9)
+    np.testing.assert_allclose(chk.x, w, rtol=RTOL_TRAJ, atol=1e-7 * max(1.0, np.abs(w).max()))
+
+
 @pytest.mark.parametrize("name,kw", [
     ("one_room", {}),
     ("one_room", {"T0": 292.0, "load": 250.0, "T_upper": 294.15}),
@@ -131,6 +152,9 @@ def test_gpu_matches_oracle(name, kw, build):
     for r in res:
         assert r.stats["success"], r.stats
         assert r.stats["iter_count"] > 0
+        if (name, repr(kw)) in MULTI_MINIMA and not np.isclose(r.stats["obj"], ref.f, rtol=RTOL_OBJ, atol=1e-9):
+            _assert_oracle_local_minimum(case, r)
+            continue
         np.testing.assert_allclose(r.stats["obj"], ref.f, rtol=RTOL_OBJ, atol=1e-9)
         # every variable group on its grid, against the oracle's vector
         for gname, lay in nlp.var_groups.items():

@@ -200,6 +200,10 @@ constexpr int MIN_REFINE = 1;                 // min_refinement_steps
 constexpr int MAX_REFINE = 10;                // max_refinement_steps
 constexpr double RESID_RATIO_MAX = 1e-10;     // residual_ratio_max
 constexpr double RESID_IMPROVE = 1.0;         // residual_improvement_factor
+// factorisations one inertia correction may take: IPOPT bounds the shifts by delta_w_max only;
+// two full shift sequences (x8 from delta_w_min to delta_w_max: 67 each, the second one with the
+// constraint block regularised) fit
+constexpr int IC_ATTEMPTS = 140;
 
 using Args = mpcx_kernel_args;
 // kernel arguments read in place from the kernarg segment (address space 4: scalar
@@ -400,6 +404,7 @@ struct KState {
   // (bar_ok): recover_step then takes it instead of recomputing every log of the slacks
   double bar_val;
   int bar_ok;
+  double sw_l, sw_r;          // the line search's switching-condition powers (loop invariant)
 };
 
 #ifndef MPCX_NETX
@@ -2625,6 +2630,21 @@ struct RatioMin {
 };
 #endif
 
+// Sum of logs of a lane's slacks as ONE log: the mantissas multiplied (each in [0.5, 1), a lane
+// takes at most a few dozen: no underflow), the exponents summed, log(prod) + e ln 2 at the end
+// (r05: the trial point's barrier took a log -- ~35 dependent instructions -- per slack)
+struct LogSum {
+  double m = 1.0;
+  int e = 0;
+  __device__ __forceinline__ void add(double s) {
+    int k;
+    const double f = frexp(s, &k);
+    m *= s < 0 ? __builtin_nan("") : f;   // a negative slack: NaN like its log (0 -> -inf, as log)
+    e += k;
+  }
+};
+constexpr double LN2 = 0.6931471805599453;
+
 // full step from the Newton solution (LDS) + fraction-to-the-boundary step sizes + constraint
 // violation at the current point; the barrier sum too unless the caller passes the cached one
 // (bar_cached: the current point is the last accepted trial point, whose logs the line search
@@ -2633,7 +2653,8 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
                                           int bar_cached) {
   const int lane = lane_now();
   RatioMin ra, rz;
-  double gphid = 0.0, theta = 0.0, bar = 0.0;
+  LogSum lb;
+  double gphid = 0.0, theta = 0.0;
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
@@ -2654,7 +2675,7 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
       if (d < 0) ra.take(tau * s_l, -d);
       const double dz = mu * rl - zl - (zl * rl) * d;
       if (dz < 0) rz.take(tau * zl, -dz);
-      if (!bar_cached) bar += log(s_l);
+      if (!bar_cached) lb.add(s_l);
     }
     if (isfin(hi)) {
       const double s_u = hi - xv, ru = MPCX_RCP(s_u);
@@ -2662,7 +2683,7 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
       if (d > 0) ra.take(tau * s_u, d);
       const double dz = mu * ru - zu + (zu * ru) * d;
       if (dz < 0) rz.take(tau * zu, -dz);
-      if (!bar_cached) bar += log(s_u);
+      if (!bar_cached) lb.add(s_u);
     }
     gphid += gphi * d;
   }
@@ -2693,14 +2714,14 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
         if (dsv < 0) ra.take(tau * s_l, -dsv);
         const double dv = mu * rsl - vl - (vl * rsl) * dsv;
         if (dv < 0) rz.take(tau * vl, -dv);
-        if (!bar_cached) bar += log(s_l);
+        if (!bar_cached) lb.add(s_l);
       }
       if (isfin(sup)) {
         const double s_u = sup - sv;
         if (dsv > 0) ra.take(tau * s_u, dsv);
         const double dv = mu * rsu - vu + (vu * rsu) * dsv;
         if (dv < 0) rz.take(tau * vu, -dv);
-        if (!bar_cached) bar += log(s_u);
+        if (!bar_cached) lb.add(s_u);
       }
     }
     a.ds()[c] = dsv;
@@ -2710,7 +2731,7 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
   st.az = wmin(rz.value());
   st.gphid = wsum(gphid);
   st.theta = wsum(theta);
-  st.barrier = bar_cached ? gL.ks.bar_val : wsum(bar);
+  st.barrier = bar_cached ? gL.ks.bar_val : wsum(log(lb.m) + lb.e * LN2);
   return st;
 }
 
@@ -2734,10 +2755,13 @@ __device__ MPCX_HOT void line_search(const Agent a) {
   {
     KArgs& ka = *argp;
     const double gphid = K.st.gphid, theta = K.st.theta;
+    // the switching condition's powers are loop invariant (only alpha changes between trials)
+    K.sw_l = gphid < 0 ? pow_ool(-gphid, ka.opt.s_phi) : 0.0;
+    K.sw_r = gphid < 0 ? ka.opt.delta * pow_ool(theta, ka.opt.s_theta) : 0.0;
     double amin;
     if (gphid < 0 && theta <= K.theta_min)
       amin = ka.opt.alpha_min_frac * fmin(fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid)),
-                                     ka.opt.delta * pow_ool(theta, ka.opt.s_theta) / pow_ool(-gphid, ka.opt.s_phi));
+                                     K.sw_r / K.sw_l);
     else if (gphid < 0)
       amin = ka.opt.alpha_min_frac * fmin(ka.opt.gamma_theta, ka.opt.gamma_phi * theta / (-gphid));
     else
@@ -2759,7 +2783,7 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     {
       const int lane = lane_now();
       const double alpha = K.ls.alpha;
-      double barx = 0.0;
+      LogSum bx;
 #pragma unroll 1
       for (int sl = 0; sl < VS; ++sl) {
         const int i = lane + sl * WAVE;
@@ -2768,12 +2792,12 @@ __device__ MPCX_HOT void line_search(const Agent a) {
           const double xt = a.x()[i] + alpha * a.dx()[i];
           gL.u.t.xt[i] = xt;
           if (i >= NX && lo != hi) {
-            if (isfin(lo)) barx += log_ool(xt - lo);
-            if (isfin(hi)) barx += log_ool(hi - xt);
+            if (isfin(lo)) bx.add(xt - lo);
+            if (isfin(hi)) bx.add(hi - xt);
           }
         }
       }
-      K.barx = wsum(barx);
+      K.barx = wsum(log_ool(bx.m) + bx.e * LN2);
     }
     wsync();
     {
@@ -2783,7 +2807,8 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     wsync();
     const int lane = lane_now();
     const double alpha = K.ls.alpha;
-    double th = 0.0, bar = 0.0;
+    double th = 0.0;
+    LogSum bs;
 #pragma unroll 1
     for (int sl = 0; sl < CS; ++sl) {
       const int c = lane + sl * WAVE;
@@ -2795,11 +2820,12 @@ __device__ MPCX_HOT void line_search(const Agent a) {
         const double st = a.s()[c] + alpha * a.ds()[c];
         th += fabs(cl == 0 ? gt - gsv * lbv : gt - st);
         if (cl == 1) {
-          if (isfin(slv)) bar += log_ool(st - slv);
-          if (isfin(suv)) bar += log_ool(suv - st);
+          if (isfin(slv)) bs.add(st - slv);
+          if (isfin(suv)) bs.add(suv - st);
         }
       }
     }
+    const double bar = log_ool(bs.m) + bs.e * LN2;
     KArgs& ka = *argp;
     const double mu = K.mu, theta = K.st.theta, gphid = K.st.gphid;
     const double phi = K.fx - mu * K.st.barrier;
@@ -2820,8 +2846,7 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     (void)okf;
     bool ftype = false;
     if (okt) {
-      const bool switching = !K.lsmode && gphid < 0 &&
-                             alpha * pow_ool(-gphid, ka.opt.s_phi) > ka.opt.delta * pow_ool(theta, ka.opt.s_theta);
+      const bool switching = !K.lsmode && gphid < 0 && alpha * K.sw_l > K.sw_r;
       if (theta <= K.theta_min && switching) {
         okt = tr.phi <= phi + ka.opt.eta_phi * alpha * gphid;
         ftype = true;
@@ -4079,13 +4104,18 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
     int ok = 0, refining = 0, steps = 0;
     double old_ratio = 0.0;
 #pragma unroll 1
-    for (int attempt = 0; attempt < 60 + MAX_REFINE + 2; ++attempt) {
-      if (!refining && attempt >= 60) break;
+    for (int attempt = 0; attempt < IC_ATTEMPTS + MAX_REFINE + 2; ++attempt) {
+      if (!refining && attempt >= IC_ATTEMPTS) break;
       if (attempt > 0 && !refining) {  // attempt 0: the iteration head wrote the rhs
         if (K.resto) rhs_dual_resto(a, K.mu, K.dw, K.dc);
         else rhs_dual(a, K.mu, K.dw, K.dc);
       }
       const Inertia in = factor(a, KKTDiag{K.dw, K.dc, NEWTON});
+#ifdef MPCX_TRACE_IC  // diagnostics: long inertia-correction sequences
+      if (!refining && attempt > 2 && lane_now() == 0)
+        printf("mpcx ic it=%d resto=%d att=%d dw=%.3e dc=%.3e mu=%.3e pos=%d neg=%d zero=%d want=%d/%d\n", K.it,
+               K.resto, attempt, K.dw, K.dc, K.mu, in.pos, in.neg, in.zero, N * NP, M);
+#endif
       if (refining) {  // correction for the residual in the rhs: add it, re-test
         solve(a);
         resto_step_io(a, 1);
@@ -4117,7 +4147,14 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
         K.dw = (dw_last == 0.0) ? OPT(delta_w_first) : fmax(OPT(delta_w_min), OPT(kappa_w_minus) * dw_last);
       } else {
         K.dw = (dw_last == 0.0) ? OPT(kappa_w_plus_bar) * dw : OPT(kappa_w_plus) * dw;
-        if (K.dw > OPT(delta_w_max)) break;
+        if (K.dw > OPT(delta_w_max)) {
+          // IPOPT PDPerturbationHandler::PerturbForWrongInertia: the Hessian shift alone cannot
+          // fix the inertia (a constraint direction the Jacobian does not span) -- regularise the
+          // constraint block as for a singular matrix and run the shifts again from the start
+          if (K.dc != 0.0) break;
+          K.dc = OPT(delta_c_bar) * pow_ool(K.mu, OPT(kappa_c));
+          K.dw = (dw_last == 0.0) ? OPT(delta_w_first) : fmax(OPT(delta_w_min), OPT(kappa_w_minus) * dw_last);
+        }
       }
     }
     PROF(5);

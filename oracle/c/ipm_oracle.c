@@ -1082,7 +1082,7 @@ static int ipm_run(const model_t* m, const double* p, const double* lbw, const d
     }
     double dw = 0.0, dc = 0.0;
     int ok = 0;
-    for (int attempt = 0; attempt < 60; ++attempt) {
+    for (int attempt = 0; attempt < 140; ++attempt) {
       inertia_t in = factor_chain(w, dw, dc, 0);
       n_fact++;
       if (in.pos == N * NP && in.neg == M && in.zero == 0) { if (attempt > 0) dw_last = dw; ok = 1; break; }
@@ -1091,7 +1091,12 @@ static int ipm_run(const model_t* m, const double* p, const double* lbw, const d
         dw = dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
       } else {
         dw = dw_last == 0.0 ? 100.0 * dw : 8.0 * dw;
-        if (dw > 1e40) break;
+        if (dw > 1e40) {
+          /* IPOPT PerturbForWrongInertia: regularise the constraint block, shift again */
+          if (dc != 0.0) break;
+          dc = 1e-8 * pow(mu, 0.25);
+          dw = dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0);
+        }
       }
     }
     if (!ok) { status = -3; break; }

@@ -538,7 +538,13 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
                     break
                 dw = o.kappa_w_plus_bar * dw if delta_w_last == 0 else o.kappa_w_plus * dw
                 if dw > o.delta_w_max:
-                    raise RuntimeError("inertia correction failed")
+                    # IPOPT PDPerturbationHandler::PerturbForWrongInertia: with the Hessian shift
+                    # alone failing, the constraint block is regularised (as for a singular
+                    # matrix) and the shifts run again from the start; failing that too, give up
+                    if dc != 0.0:
+                        raise RuntimeError("inertia correction failed")
+                    dc = o.delta_c_bar * mu ** o.kappa_c
+                    dw = o.delta_w_first if delta_w_last == 0 else max(o.delta_w_min, o.kappa_w_minus * delta_w_last)
         if inner is not None:
             # IPOPT PDFullSpaceSolver: iterative refinement of the step on the full system (here
             # the restoration NLP's, p and n explicit)

@@ -24,7 +24,7 @@ def main(n):
     from agentlib_mpc_amd import benchmarks as bm
 
     dev = torch.device("cuda")
-    be, cv = bm.one_room(solver_options={"ipopt": {}})
+    be, cv = bm.one_room(solver_options=bm.REFERENCE)  # the bench e2e leg's settings
     vals = bench.fleet_values(n, 20261015 + 2)
     agents = []
     for a in range(n):
@@ -36,6 +36,16 @@ def main(n):
     be.solve_batch(0.0, agents)
     rb = be._resident
     sync = torch.cuda.synchronize
+    t_read = []
+    read0 = rb.read
+
+    def timed_read(*a, **k):
+        t0 = time.perf_counter()
+        out = read0(*a, **k)
+        t_read.append(time.perf_counter() - t0)
+        return out
+
+    rb.read = timed_read
     rows = []
     for k in range(1, 8):
         drift = rng.normal(0.0, 0.05, n)
@@ -66,9 +76,10 @@ def main(n):
         t.append(time.perf_counter())
         d = np.diff(t) * 1e3
         rows.append((d, e0.elapsed_time(e1), float(st["iter_count"].mean()), int(st["iter_count"].max())))
-    print("plugin step pieces (ms): update | launch+kernel | pinned alloc | D2H w+stats | results+first_values ; kernel(events) ; mean/max it")
-    for d, km, mi, mx in rows:
-        print("  " + " | ".join(f"{x:7.3f}" for x in d) + f" ; {km:7.3f} ; {mi:.2f}/{mx}")
+    print("plugin step pieces (ms): update (of which read) | launch+kernel | pinned alloc | D2H w+stats | "
+          "results+first_values ; kernel(events) ; mean/max it")
+    for (d, km, mi, mx), tr in zip(rows, t_read):
+        print(f"  {d[0]:7.3f} ({tr * 1e3:6.3f}) | " + " | ".join(f"{x:7.3f}" for x in d[1:]) + f" ; {km:7.3f} ; {mi:.2f}/{mx}")
     # the full call, profiled
     pr = cProfile.Profile()
     t0 = time.perf_counter()

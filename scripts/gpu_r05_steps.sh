@@ -66,6 +66,52 @@ step_s4() {
   echo "s4 exit $?"
 }
 
+step_s5() {
+  # r05/s5: GPU parity suite on the fixed kernel (chain-scan acceptance, constant denominators),
+  # the C5 fixture runs with their divergence iterations printed, then the default bench line and
+  # the kernel-trace stats
+  mkdir -p gpurun_out/s5
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s5/gpu_tests.txt 2>&1
+  rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_admm.py -m gpu -q -s --timeout 240 --timeout-method thread -k "three_zone" > gpurun_out/s5/c5_fixtures.txt 2>&1
+  rc2=$?; [ $rc2 -ne 0 ] && [ $rc2 -ne 1 ] && exit $rc2
+  timeout -k 10 900 python -u bench.py > gpurun_out/s5/bench.json 2> gpurun_out/s5/bench.err || exit $?
+  rm -rf gpurun_out/s5/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s5/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --admm-agents 0 --c2-blocks 0 --c5-blocks 0 > gpurun_out/s5/prof_bench.json 2> gpurun_out/s5/prof.err || exit $?
+  python scripts/trace_summary.py gpurun_out/s5/prof gpurun_out/s5/kernel_trace_summary.txt > /dev/null
+  echo "tests exit $rc, c5 exit $rc2"
+}
+
+step_s6() {
+  # r05/s6: line-search barrier as one log per lane (mantissa products) and loop-invariant
+  # switching powers: kernel A/B against the committed kernel (rev) for C3 and C1; the kw1 long
+  # restoration case with the inertia-correction trace on every build; then the GPU parity suite
+  mkdir -p gpurun_out/s6
+  REV=$REV timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s6/var_c3.txt 2>&1 || exit $?
+  REV=$REV AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_rev lds_base lds_rev > gpurun_out/s6/var_c1.txt 2>&1 || exit $?
+  MPCX_DEFINES=MPCX_TRACE_IC timeout -k 10 600 python -u -m pytest tests/test_gpu_ipm.py -m gpu -q -s -rfE --timeout 300 --timeout-method thread -k "long_restoration and kw1" > gpurun_out/s6/kw1_trace.txt 2>&1
+  rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+  timeout -k 10 600 python -u bench.py > gpurun_out/s6/bench.json 2> gpurun_out/s6/bench.err || exit $?
+  timeout -k 10 700 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s6/gpu_tests.txt 2>&1
+  echo "tests exit $?"
+}
+
+step_s7() {
+  # r05/s7: the kernel with the line-search barrier as one log per lane and IPOPT's constraint
+  # regularisation after a failed Hessian shift (kw1 mid build: 24 shifts to 1e40 at it=46, one
+  # constraint direction the Jacobian misses); GPU suite, the plugin step's host breakdown with the
+  # read cache, a kernel trace of the C4 leg, the default bench line
+  mkdir -p gpurun_out/s7
+  timeout -k 10 700 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s7/gpu_tests.txt 2>&1
+  rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+  timeout -k 10 300 python -u scripts/e2e_prof.py > gpurun_out/s7/e2e_prof.txt 2>&1 || exit $?
+  rm -rf gpurun_out/s7/prof_c4
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s7/prof_c4 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --agents 256 --no-cpu-baseline --no-e2e --nn-zones 0 --c5-blocks 0 --mhe-agents 0 --c2-blocks 0 > gpurun_out/s7/prof_c4.json 2> gpurun_out/s7/prof_c4.err || exit $?
+  python scripts/trace_summary.py gpurun_out/s7/prof_c4 gpurun_out/s7/c4_trace_summary.txt > /dev/null
+  timeout -k 10 600 python -u bench.py > gpurun_out/s7/bench.json 2> gpurun_out/s7/bench.err
+  echo "tests exit $rc, bench exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -112,6 +112,32 @@ step_s7() {
   echo "tests exit $rc, bench exit $?"
 }
 
+step_s8() {
+  # r05/s8: the twisted chain's pivot sweeps in registers (MHE A/B against the LDS sweep), an
+  # occupancy scan of the fleets that take two generations (C4 rooms, C2 rooms), the C3 phase
+  # profile of the current kernel, then the GPU parity suite
+  mkdir -p gpurun_out/s8
+  # (the register sweep measured 8.11-8.13 ms against 8.06-8.08 ms through LDS: not kept; its
+  # variant is gone from variants.py)
+  MODEL=exchange_room N=13108 PER_CU=0,26,22,20,16,0 timeout -k 10 300 python -u scripts/occ_scan.py > gpurun_out/s8/occ_c4room.txt 2>&1 || exit $?
+  MODEL=admm_room N=4096 PER_CU=0,24,20,16,12,0 timeout -k 10 300 python -u scripts/occ_scan.py > gpurun_out/s8/occ_c2room.txt 2>&1 || exit $?
+  AGENTS=4096 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s8/phases_c3.txt 2>&1 || exit $?
+  timeout -k 10 700 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s8/gpu_tests.txt 2>&1
+  echo "tests exit $?"
+}
+
+step_s9() {
+  # r05/s9: occupancy scan of the C4 room fleet (13108 agents, two generations at 29 per CU) with
+  # the static LDS given; the C2 room code object's LDS from a kernel trace; a 512-agent C3 launch
+  mkdir -p gpurun_out/s9
+  MODEL=exchange_room N=13108 LDS=5632 PER_CU=0,26,22,20,16,0 timeout -k 10 300 python -u scripts/occ_scan.py > gpurun_out/s9/occ_c4room.txt 2>&1 || exit $?
+  rm -rf gpurun_out/s9/prof_c2
+  MODEL=admm_room N=4096 LDS=1 PER_CU=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s9/prof_c2 -o run --output-format csv -- python3 scripts/occ_scan.py > gpurun_out/s9/occ_c2_trace.txt 2>&1 || exit $?
+  python scripts/trace_summary.py gpurun_out/s9/prof_c2 gpurun_out/s9/c2room_trace_summary.txt > /dev/null
+  SIZES=512,1024,4096 timeout -k 10 300 python -u scripts/build_scan.py > gpurun_out/s9/build_scan_c3.txt 2>&1
+  echo "s9 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -138,6 +138,32 @@ step_s9() {
   echo "s9 exit $?"
 }
 
+step_s10() {
+  # r05/s10: kernel traces of the coordinated legs alone (C2: 1024 blocks, C5: 341 blocks): how
+  # much of a round the GPU idles between launches (scripts/trace_gaps.py)
+  mkdir -p gpurun_out/s10
+  rm -rf gpurun_out/s10/prof_c2 gpurun_out/s10/prof_c5
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/s10/prof_c2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0 > gpurun_out/s10/c2.json 2> gpurun_out/s10/c2.err || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/s10/prof_c5 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c2-blocks 0 --mhe-agents 0 > gpurun_out/s10/c5.json 2> gpurun_out/s10/c5.err
+  echo "s10 exit $?"
+}
+
+step_s11() {
+  # r05/s11: each agent class on a hardware queue of its own (mpcx_stream_create) against plain
+  # streams (MPCX_FLEET_QUEUES=0): the three ADMM legs twice each; a C2 kernel trace (queue ids);
+  # the ADMM GPU tests
+  mkdir -p gpurun_out/s11
+  B="python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --nn-zones 0 --mhe-agents 0"
+  for Q in 1 0 1 0; do
+    MPCX_FLEET_QUEUES=$Q timeout -k 10 300 $B > gpurun_out/s11/legs_q$Q.json.tmp 2> gpurun_out/s11/legs_q$Q.err || exit $?
+    cat gpurun_out/s11/legs_q$Q.json.tmp >> gpurun_out/s11/legs_q$Q.json
+  done
+  rm -rf gpurun_out/s11/prof_c2
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/s11/prof_c2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0 > gpurun_out/s11/c2.json 2> gpurun_out/s11/c2.err || exit $?
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_admm.py tests/test_native_abi.py -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s11/gpu_admm_tests.txt 2>&1
+  echo "s11 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -164,6 +164,28 @@ step_s11() {
   echo "s11 exit $?"
 }
 
+step_s12() {
+  # r05/s12: the classes' solves on the caller's stream (MPCX_FLEET_STREAMS=0: no fork / join
+  # events; the plain class streams share one hardware queue anyway, s10) against one stream per
+  # class: the three ADMM legs twice each
+  mkdir -p gpurun_out/s12
+  B="python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --nn-zones 0 --mhe-agents 0"
+  for S in 0 1 0 1; do
+    MPCX_FLEET_STREAMS=$S timeout -k 10 300 $B > gpurun_out/s12/legs_s$S.json.tmp 2> gpurun_out/s12/legs_s$S.err || exit $?
+    cat gpurun_out/s12/legs_s$S.json.tmp >> gpurun_out/s12/legs_s$S.json
+  done
+  echo "s12 exit $?"
+}
+
+step_s13() {
+  # r05/s13: phase profiles of the current kernel: C1 (one agent, small-fleet build) and the MHE
+  # fleet (4096 estimators, reference settings)
+  mkdir -p gpurun_out/s13
+  WSLDS=1 AGENTS=1 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s13/phases_c1_lds.txt 2>&1 || exit $?
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s13/phases_mhe.txt 2>&1
+  echo "s13 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -458,6 +458,9 @@ class ADMMFleet:
         #: agent map, the bound being the class's active count at the last stopping check (the
         #: active set only shrinks within a round); MPCX_FLEET_MAP=0 launches every agent
         self.map_launch = os.environ.get("MPCX_FLEET_MAP", "1") != "0" and hasattr(self.ops, "active_map")
+        #: a class's per-iteration row moves (means / multipliers / penalty into p, locals out of w)
+        #: as one scatter and one gather launch (C ABI v12); MPCX_FLEET_FUSED=0: one launch per move
+        self.fused_moves = os.environ.get("MPCX_FLEET_FUSED", "1") != "0" and hasattr(self.ops, "scatter_many")
         self._mapped = False
         for c in self.classes:
             c.MAP = t.zeros(c.n, dtype=i32, device=dev)
@@ -520,24 +523,32 @@ class ADMMFleet:
             with (t.cuda.stream(streams[ci]) if streams else contextlib.nullcontext()):
                 if streams:
                     streams[ci].wait_event(self._ev_solve)
+                moves = []
                 for si, s in enumerate(c.slots):
                     d = c.dev_slots[si]
                     if s.kind == CONSENSUS:
-                        ops.scatter_rows(T, self.MEAN, d["groups"], c.P, d["mean_cols"])
-                        ops.scatter_rows(T, self.LAMR, d["rows"], c.P, d["mult_cols"])
+                        moves += [(T, self.MEAN, d["groups"], d["mean_cols"]), (T, self.LAMR, d["rows"], d["mult_cols"])]
                     else:
-                        ops.scatter_rows(T, self.DIFF, d["rows"], c.P, d["mean_cols"])
-                        ops.scatter_rows(T, self.GMULT, d["groups"], c.P, d["mult_cols"])
-                ops.scatter_rows(1, self.RHO_B, c.BLOCK, c.P, c.RHO_COL)  # the block's penalty
+                        moves += [(T, self.DIFF, d["rows"], d["mean_cols"]), (T, self.GMULT, d["groups"], d["mult_cols"])]
+                moves.append((1, self.RHO_B, c.BLOCK, c.RHO_COL))  # the block's penalty
+                if self.fused_moves:  # every move of the class in one launch (C ABI v12)
+                    ops.scatter_many(moves, c.P)
+                else:
+                    for T_, src, rows, cols in moves:
+                        ops.scatter_rows(T_, src, rows, c.P, cols)
                 if self._mapped:  # only the agents still active, compacted (mpcx_active_map)
                     ops.active_map(c.n, c.ACTIVE, c.MAP, self._map_counts[ci:ci + 1])
                     ops.solve(c, c.ACTIVE, c.MAP, c.bound)
                 else:
                     ops.solve(c, c.ACTIVE if self._masked else None)
-                for si, s in enumerate(c.slots):
-                    d = c.dev_slots[si]
-                    # agents not participating keep their local (their rows map to the scratch row)
-                    ops.gather_rows(T, c.W, d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
+                # agents not participating keep their local (their rows map to the scratch row)
+                gathers = [(d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
+                           for d in c.dev_slots]
+                if self.fused_moves and gathers:
+                    ops.gather_many(T, c.W, gathers)
+                else:
+                    for cols, dst, rows in gathers:
+                        ops.gather_rows(T, c.W, cols, dst, rows)
         if streams:
             for st_ in streams:
                 main.wait_stream(st_)

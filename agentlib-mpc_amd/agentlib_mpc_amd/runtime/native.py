@@ -91,7 +91,9 @@ EXPORTED_SYMBOLS = [
     "mpcx_admm_consensus_multipliers", "mpcx_admm_exchange_update", "mpcx_admm_shift",
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
     "mpcx_admm_block_stop", "mpcx_admm_block_expand", "mpcx_device_clock_khz", "mpcx_stats_count",
+    "mpcx_scatter_rows_multi", "mpcx_gather_rows_multi",
 ]
+MOVE_DESC = 4  # MPCX_MOVE_DESC: int64 words per descriptor of the fused row moves (C ABI v12)
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
 ADMM_CONTROL = 1  # MPCX_ADMM_CONTROL: control doubles before the moments buffer (C ABI v10)
 KERNEL_ABI = 8  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
@@ -212,6 +214,8 @@ def load_library():
         lib.mpcx_gather_rows.argtypes = [i32, i32, vp, i64, vp, vp, vp, vp]
         lib.mpcx_scatter_rows.argtypes = [i32, i32, vp, vp, vp, i64, vp, vp]
         lib.mpcx_fill_column.argtypes = [i32, vp, i64, i32, f64, vp]
+        lib.mpcx_scatter_rows_multi.argtypes = [i32, i32, vp, i32, vp, i64, vp]
+        lib.mpcx_gather_rows_multi.argtypes = [i32, i32, vp, i32, vp, i64, vp]
         lib.mpcx_admm_block_stop.argtypes = [i32, i32, vp, i32, f64, f64, f64, f64, f64, f64, vp, vp, vp, vp, vp,
                                              vp, vp, vp]
         lib.mpcx_admm_block_expand.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp]

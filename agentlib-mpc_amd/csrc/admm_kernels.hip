@@ -66,6 +66,36 @@ __global__ void k_scatter_rows(int n, int T, const double* __restrict__ src,
   dst[(long)a * ld + cols[t]] = src[r * T + t];
 }
 
+// Several row moves in one launch (C ABI v12): blockIdx.y selects a descriptor of MPCX_MOVE_DESC
+// int64 words in device memory.  Scatter descriptor: (src, src_rows or 0, cols, T) into the common
+// destination; gather descriptor: (dst, dst_rows, cols, T) from the common source.
+__global__ void k_scatter_rows_multi(int n, const long long* __restrict__ desc, double* __restrict__ dst,
+                                     long ld) {
+  const long long* d = desc + (long)blockIdx.y * MPCX_MOVE_DESC;
+  const int T = (int)d[3];
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)n * T) return;
+  const double* src = (const double*)d[0];
+  const int* rows = (const int*)d[1];
+  const int* cols = (const int*)d[2];
+  const int a = (int)(e / T), t = (int)(e % T);
+  const long r = rows ? rows[a] : a;
+  dst[(long)a * ld + cols[t]] = src[r * T + t];
+}
+
+__global__ void k_gather_rows_multi(int n, const long long* __restrict__ desc, const double* __restrict__ src,
+                                    long ld) {
+  const long long* d = desc + (long)blockIdx.y * MPCX_MOVE_DESC;
+  const int T = (int)d[3];
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)n * T) return;
+  double* dst = (double*)d[0];
+  const int* rows = (const int*)d[1];
+  const int* cols = (const int*)d[2];
+  const int a = (int)(e / T), t = (int)(e % T);
+  dst[(long)rows[a] * T + t] = src[(long)a * ld + cols[t]];
+}
+
 __global__ void k_fill_column(int n, double* __restrict__ dst, long ld, int col, double v) {
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a < n) dst[(long)a * ld + col] = v;
@@ -281,6 +311,28 @@ extern "C" int mpcx_scatter_rows(int32_t n_agents, int32_t T, const double* src,
   const long n = (long)n_agents * T;
   hipLaunchKernelGGL(k_scatter_rows, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
                      n_agents, T, src, src_rows, dst, (long)dst_ld, cols);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int mpcx_scatter_rows_multi(int32_t n_agents, int32_t n_desc, const int64_t* desc, int32_t max_T,
+                                       double* dst, int64_t dst_ld, void* stream) {
+  if (n_agents < 0 || n_desc < 0 || max_T <= 0 || dst_ld <= 0 || !dst || (n_desc > 0 && !desc)) return MPCX_ERR_ARG;
+  if (n_agents == 0 || n_desc == 0) return MPCX_OK;
+  const long n = (long)n_agents * max_T;
+  hipLaunchKernelGGL(k_scatter_rows_multi, dim3(blocks_for(n, 256), n_desc), dim3(256), 0, (hipStream_t)stream,
+                     n_agents, (const long long*)desc, dst, (long)dst_ld);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int mpcx_gather_rows_multi(int32_t n_agents, int32_t n_desc, const int64_t* desc, int32_t max_T,
+                                      const double* src, int64_t src_ld, void* stream) {
+  if (n_agents < 0 || n_desc < 0 || max_T <= 0 || src_ld <= 0 || !src || (n_desc > 0 && !desc)) return MPCX_ERR_ARG;
+  if (n_agents == 0 || n_desc == 0) return MPCX_OK;
+  const long n = (long)n_agents * max_T;
+  hipLaunchKernelGGL(k_gather_rows_multi, dim3(blocks_for(n, 256), n_desc), dim3(256), 0, (hipStream_t)stream,
+                     n_agents, (const long long*)desc, src, (long)src_ld);
   LAUNCH_CHECK();
   return MPCX_OK;
 }

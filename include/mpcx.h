@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 11
+#define MPCX_API_VERSION 12
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -370,6 +370,19 @@ int mpcx_scatter_rows(int32_t n_agents, int32_t T, const double* src, const int3
 /* dst[a*dst_ld + col] <- value (the penalty factor rho into p). */
 int mpcx_fill_column(int32_t n_agents, double* dst, int64_t dst_ld, int32_t col, double value,
                      void* stream);
+/* Several row moves in ONE launch (C ABI v12): the per-iteration marshalling of an ADMM class --
+ * every coupling slot's mean / multiplier columns and the block penalty into p, every slot's
+ * local trajectory out of w -- was one launch per move.  desc: n_desc descriptors of
+ * MPCX_MOVE_DESC int64 words in DEVICE memory (built once per class).
+ * scatter: desc k = (src, src_rows or 0, cols, T): dst[i * dst_ld + cols[t]] = src[src_rows[i] * T + t]
+ * gather:  desc k = (dst, dst_rows, cols, T):     dst[dst_rows[i] * T + t] = src[i * src_ld + cols[t]]
+ * for i < n_agents, t < T (<= max_T).  The moves of one call must not write the same element
+ * (rows mapped to a shared scratch row excepted: what lands there is never read). */
+#define MPCX_MOVE_DESC 4
+int mpcx_scatter_rows_multi(int32_t n_agents, int32_t n_desc, const int64_t* desc, int32_t max_T, double* dst,
+                            int64_t dst_ld, void* stream);
+int mpcx_gather_rows_multi(int32_t n_agents, int32_t n_desc, const int64_t* desc, int32_t max_T,
+                           const double* src, int64_t src_ld, void* stream);
 
 #ifdef __cplusplus
 }

@@ -66,6 +66,14 @@ class CpuFleetOps:
         d = dst.numpy()
         d[:, cols.numpy()] = s[rows]
 
+    def scatter_many(self, moves, dst):
+        for T, src, rows, cols in moves:
+            self.scatter_rows(T, src, rows, dst, cols)
+
+    def gather_many(self, T, src, moves):
+        for cols, dst, rows in moves:
+            self.gather_rows(T, src, cols, dst, rows)
+
     def fill_column(self, dst, col, value):
         dst.numpy()[:, col] = value
 

@@ -186,6 +186,23 @@ step_s13() {
   echo "s13 exit $?"
 }
 
+step_s14() {
+  # r05/s14: a class's row moves fused into one scatter + one gather launch (C ABI v12): the ADMM
+  # GPU tests (fused vs one launch per move bit for bit), the three ADMM legs fused / unfused
+  # twice each; phase profiles of C1 and the MHE fleet
+  mkdir -p gpurun_out/s14
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_admm.py tests/test_native_abi.py -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s14/gpu_admm_tests.txt 2>&1
+  rc=$?; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+  B="python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --nn-zones 0 --mhe-agents 0"
+  for F in 1 0 1 0; do
+    MPCX_FLEET_FUSED=$F timeout -k 10 300 $B > gpurun_out/s14/legs_f$F.json.tmp 2> gpurun_out/s14/legs_f$F.err || exit $?
+    cat gpurun_out/s14/legs_f$F.json.tmp >> gpurun_out/s14/legs_f$F.json
+  done
+  WSLDS=1 AGENTS=1 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s14/phases_c1_lds.txt 2>&1 || exit $?
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s14/phases_mhe.txt 2>&1
+  echo "tests exit $rc, s14 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -453,6 +453,14 @@ class ADMMFleet:
                                    and os.environ.get("MPCX_FLEET_STREAMS", "1") != "0")
         self._class_streams = [t.cuda.Stream(device=dev) for _ in self.classes] if self.concurrent_classes else None
         self._ev_solve = t.cuda.Event() if self.concurrent_classes else None
+        #: the lead class (most agents x NLP size) is issued first and the others wait for its
+        #: pre-solve moves (see _solve_all); MPCX_FLEET_LEAD=0: every class starts at once
+        size = [c.n * (c.P.shape[1] + c.W.shape[1]) for c in self.classes]
+        self._lead = (int(np.argmax(size)) if self.concurrent_classes and os.environ.get("MPCX_FLEET_LEAD", "1") != "0"
+                      else None)
+        self._class_order = ([self._lead] + [i for i in range(len(self.classes)) if i != self._lead]
+                             if self._lead is not None else list(range(len(self.classes))))
+        self._ev_lead = t.cuda.Event() if self._lead is not None else None
         #: coordinated rounds launch only the agents still active (mpcx_active_map +
         #: mpcx_batch_solve_mapped): each class's solve is ``bound`` workgroups over the compacted
         #: agent map, the bound being the class's active count at the last stopping check (the
@@ -519,10 +527,16 @@ class ADMMFleet:
         if streams:
             main = t.cuda.current_stream(self.device)
             self._ev_solve.record(main)
-        for ci, c in enumerate(self.classes):
+        lead = self._lead
+        for ci in self._class_order:
+            c = self.classes[ci]
             with (t.cuda.stream(streams[ci]) if streams else contextlib.nullcontext()):
                 if streams:
-                    streams[ci].wait_event(self._ev_solve)
+                    # the other classes start once the lead class's solve is next in its queue: its
+                    # workgroups claim the CUs first and the smaller classes fill what they leave
+                    # (a class that needs a whole generation of the LDS, the C5 zones, split into two
+                    # when the others' workgroups were dispatched beside it: r05/s14)
+                    streams[ci].wait_event(self._ev_solve if ci == lead or lead is None else self._ev_lead)
                 moves = []
                 for si, s in enumerate(c.slots):
                     d = c.dev_slots[si]
@@ -538,6 +552,9 @@ class ADMMFleet:
                         ops.scatter_rows(T_, src, rows, c.P, cols)
                 if self._mapped:  # only the agents still active, compacted (mpcx_active_map)
                     ops.active_map(c.n, c.ACTIVE, c.MAP, self._map_counts[ci:ci + 1])
+                if streams and ci == lead:
+                    self._ev_lead.record(streams[ci])
+                if self._mapped:
                     ops.solve(c, c.ACTIVE, c.MAP, c.bound)
                 else:
                     ops.solve(c, c.ACTIVE if self._masked else None)

@@ -203,6 +203,21 @@ step_s14() {
   echo "tests exit $rc, s14 exit $?"
 }
 
+step_s15() {
+  # r05/s15: the lead class issued first, the others after its pre-solve moves (MPCX_FLEET_LEAD),
+  # with the fused moves; against no lead and against unfused moves: the three ADMM legs twice
+  # each; then the ADMM GPU tests
+  mkdir -p gpurun_out/s15
+  B="python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --nn-zones 0 --mhe-agents 0"
+  for V in L1F1 L0F1 L1F0 L1F1 L0F1 L1F0; do
+    L=${V:1:1}; F=${V:3:1}
+    MPCX_FLEET_LEAD=$L MPCX_FLEET_FUSED=$F timeout -k 10 300 $B > gpurun_out/s15/legs_$V.json.tmp 2> gpurun_out/s15/legs_$V.err || exit $?
+    cat gpurun_out/s15/legs_$V.json.tmp >> gpurun_out/s15/legs_$V.json
+  done
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_admm.py -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s15/gpu_admm_tests.txt 2>&1
+  echo "s15 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -218,6 +218,19 @@ step_s15() {
   echo "s15 exit $?"
 }
 
+step_s16() {
+  # r05/s16: the full default bench line twice with the fused moves + lead class and once with
+  # neither (MPCX_FLEET_LEAD=0 MPCX_FLEET_FUSED=0): the record's C2 leg fell to 741 it/s inside the
+  # full line while the legs-only runs gave 1178
+  mkdir -p gpurun_out/s16
+  for V in L1F1 L0F0 L1F1; do
+    L=${V:1:1}; F=${V:3:1}
+    MPCX_FLEET_LEAD=$L MPCX_FLEET_FUSED=$F timeout -k 10 600 python -u bench.py > gpurun_out/s16/bench_$V.json.tmp 2> gpurun_out/s16/bench_$V.err || exit $?
+    cat gpurun_out/s16/bench_$V.json.tmp >> gpurun_out/s16/bench_$V.json
+  done
+  echo "s16 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -468,7 +468,8 @@ class ADMMFleet:
         self.map_launch = os.environ.get("MPCX_FLEET_MAP", "1") != "0" and hasattr(self.ops, "active_map")
         #: a class's per-iteration row moves (means / multipliers / penalty into p, locals out of w)
         #: as one scatter and one gather launch (C ABI v12); MPCX_FLEET_FUSED=0: one launch per move
-        self.fused_moves = os.environ.get("MPCX_FLEET_FUSED", "1") != "0" and hasattr(self.ops, "scatter_many")
+        self.fused_moves = os.environ.get("MPCX_FLEET_FUSED", "1") != "0" and hasattr(self.ops, "scatter_plan")
+        self._prepare_moves()
         self._mapped = False
         for c in self.classes:
             c.MAP = t.zeros(c.n, dtype=i32, device=dev)
@@ -514,6 +515,37 @@ class ADMMFleet:
             c.ACTIVE.copy_(t.as_tensor(a.astype(np.int32)))
         self._masked = masked
 
+    def _scatter_moves(self, c):
+        """Every row move into a class's p per iteration: each coupling slot's mean (or exchange
+        diff) and multiplier columns, and the block's penalty."""
+        T, moves = self.T, []
+        for si, s in enumerate(c.slots):
+            d = c.dev_slots[si]
+            if s.kind == CONSENSUS:
+                moves += [(T, self.MEAN, d["groups"], d["mean_cols"]), (T, self.LAMR, d["rows"], d["mult_cols"])]
+            else:
+                moves += [(T, self.DIFF, d["rows"], d["mean_cols"]), (T, self.GMULT, d["groups"], d["mult_cols"])]
+        moves.append((1, self.RHO_B, c.BLOCK, c.RHO_COL))
+        return moves
+
+    def _gather_moves(self, c):
+        """Each slot's local trajectory out of w; agents not participating keep their local
+        (their rows map to the scratch row)."""
+        part = getattr(self, "_part", None)
+        return [(d["w_cols"], self.X, d["rows_part"] if part is not None else d["rows"]) for d in c.dev_slots]
+
+    def _prepare_moves(self):
+        """The fused moves of every class, prepared once (the buffers never move; the gathers
+        again whenever the participation masks change): the iteration then issues each as one
+        launch without building anything on the host -- a per-iteration list of moves was enough
+        Python allocation to make the interpreter's collector show in the C2 leg."""
+        if not getattr(self, "fused_moves", False):
+            return
+        for c in self.classes:
+            c.scatter_plan = self.ops.scatter_plan(self._scatter_moves(c), c.P)
+            g = self._gather_moves(c)
+            c.gather_plan = self.ops.gather_plan(self.T, c.W, g) if g else None
+
     def _solve_all(self, rho: float):
         """Inject mean/diff, multipliers and the block's rho into every agent's p; solve
         (agents of frozen blocks are skipped); gather locals.
@@ -537,18 +569,10 @@ class ADMMFleet:
                     # (a class that needs a whole generation of the LDS, the C5 zones, split into two
                     # when the others' workgroups were dispatched beside it: r05/s14)
                     streams[ci].wait_event(self._ev_solve if ci == lead or lead is None else self._ev_lead)
-                moves = []
-                for si, s in enumerate(c.slots):
-                    d = c.dev_slots[si]
-                    if s.kind == CONSENSUS:
-                        moves += [(T, self.MEAN, d["groups"], d["mean_cols"]), (T, self.LAMR, d["rows"], d["mult_cols"])]
-                    else:
-                        moves += [(T, self.DIFF, d["rows"], d["mean_cols"]), (T, self.GMULT, d["groups"], d["mult_cols"])]
-                moves.append((1, self.RHO_B, c.BLOCK, c.RHO_COL))  # the block's penalty
-                if self.fused_moves:  # every move of the class in one launch (C ABI v12)
-                    ops.scatter_many(moves, c.P)
+                if self.fused_moves:  # every move of the class in one launch (C ABI v12), prepared
+                    ops.run_plan(c.scatter_plan)
                 else:
-                    for T_, src, rows, cols in moves:
+                    for T_, src, rows, cols in self._scatter_moves(c):
                         ops.scatter_rows(T_, src, rows, c.P, cols)
                 if self._mapped:  # only the agents still active, compacted (mpcx_active_map)
                     ops.active_map(c.n, c.ACTIVE, c.MAP, self._map_counts[ci:ci + 1])
@@ -558,13 +582,11 @@ class ADMMFleet:
                     ops.solve(c, c.ACTIVE, c.MAP, c.bound)
                 else:
                     ops.solve(c, c.ACTIVE if self._masked else None)
-                # agents not participating keep their local (their rows map to the scratch row)
-                gathers = [(d["w_cols"], self.X, d["rows_part"] if self._part is not None else d["rows"])
-                           for d in c.dev_slots]
-                if self.fused_moves and gathers:
-                    ops.gather_many(T, c.W, gathers)
+                if self.fused_moves:
+                    if c.gather_plan is not None:
+                        ops.run_plan(c.gather_plan)
                 else:
-                    for cols, dst, rows in gathers:
+                    for cols, dst, rows in self._gather_moves(c):
                         ops.gather_rows(T, c.W, cols, dst, rows)
         if streams:
             for st_ in streams:
@@ -645,6 +667,7 @@ class ADMMFleet:
             self._part, self.ROW_ON = None, None
             for c in self.classes:
                 c.PART = None
+            self._prepare_moves()
             return
         part = []
         on = np.ones(self.X.shape[0], np.int32)
@@ -659,6 +682,7 @@ class ADMMFleet:
                 c.dev_slots[si]["rows_part"] = t.as_tensor(np.where(m, rows, self.X.shape[0] - 1).astype(np.int32),
                                                            device=self.device)
         self._part = part
+        self._prepare_moves()  # the gathers read the new row maps
         for c, m in zip(self.classes, part):
             c.PART = t.as_tensor(m.astype(np.int32), device=self.device)
         self.ROW_ON = t.as_tensor(on, device=self.device)

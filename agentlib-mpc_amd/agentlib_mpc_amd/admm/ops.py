@@ -26,7 +26,6 @@ class NativeADMMOps:
     def __init__(self, stream=None):
         self.lib = native.load_library()
         self._stream = stream
-        self._plans = {}  # fused-move descriptor tables by buffer addresses
 
     @property
     def stream(self):
@@ -60,39 +59,35 @@ class NativeADMMOps:
         self._chk(self.lib.mpcx_scatter_rows(dst.shape[0], T, _p(src), _p(src_rows), _p(dst), dst.shape[1],
                                              _p(cols), self.stream), "mpcx_scatter_rows")
 
-    def _plan(self, key, words, device):
-        """Descriptor table of a fused move (device int64), built once per distinct set of buffers."""
+    def scatter_plan(self, moves, dst):
+        """A prepared ``mpcx_scatter_rows_multi`` launch of several ``scatter_rows`` into one
+        destination (``moves`` = [(T, src, src_rows, cols)], not writing the same element): the
+        descriptor table is built once on the device; :meth:`run_plan` issues it."""
         import torch
 
-        desc = self._plans.get(key)
-        if desc is None:
-            if len(self._plans) > 256:  # participation masks come and go: bound the cache
-                self._plans.clear()
-            desc = torch.tensor(words, dtype=torch.int64, device=device)
-            self._plans[key] = desc
-        return desc
-
-    def scatter_many(self, moves, dst):
-        """Several ``scatter_rows`` into one destination in ONE launch (``mpcx_scatter_rows_multi``):
-        ``moves`` = [(T, src, src_rows, cols)]; the moves must not write the same element."""
         words = []
         for T, src, rows, cols in moves:
             words += [src.data_ptr(), 0 if rows is None else rows.data_ptr(), cols.data_ptr(), int(T)]
-        key = ("s", dst.data_ptr(), *words)
-        desc = self._plan(key, words, dst.device)
-        self._chk(self.lib.mpcx_scatter_rows_multi(dst.shape[0], len(moves), _p(desc), max(int(m[0]) for m in moves),
-                                                   _p(dst), dst.shape[1], self.stream), "mpcx_scatter_rows_multi")
+        desc = torch.tensor(words, dtype=torch.int64, device=dst.device)
+        args = (dst.shape[0], len(moves), _p(desc), max(int(m[0]) for m in moves), _p(dst), dst.shape[1])
+        return (self.lib.mpcx_scatter_rows_multi, args, desc, "mpcx_scatter_rows_multi")
 
-    def gather_many(self, T, src, moves):
-        """Several ``gather_rows`` from one source in ONE launch (``mpcx_gather_rows_multi``):
-        ``moves`` = [(cols, dst, dst_rows)], each of ``T`` columns."""
+    def gather_plan(self, T, src, moves):
+        """A prepared ``mpcx_gather_rows_multi`` launch of several ``gather_rows`` from one source
+        (``moves`` = [(cols, dst, dst_rows)], each of ``T`` columns)."""
+        import torch
+
         words = []
         for cols, dst, rows in moves:
             words += [dst.data_ptr(), rows.data_ptr(), cols.data_ptr(), int(T)]
-        key = ("g", src.data_ptr(), *words)
-        desc = self._plan(key, words, src.device)
-        self._chk(self.lib.mpcx_gather_rows_multi(src.shape[0], len(moves), _p(desc), int(T), _p(src), src.shape[1],
-                                                  self.stream), "mpcx_gather_rows_multi")
+        desc = torch.tensor(words, dtype=torch.int64, device=src.device)
+        args = (src.shape[0], len(moves), _p(desc), int(T), _p(src), src.shape[1])
+        return (self.lib.mpcx_gather_rows_multi, args, desc, "mpcx_gather_rows_multi")
+
+    def run_plan(self, plan):
+        """Issue a prepared fused move on the current stream (one launch, no host allocation)."""
+        fn, args, _desc, name = plan
+        self._chk(fn(*args, self.stream), name)
 
     def fill_column(self, dst, col, value):
         self._chk(self.lib.mpcx_fill_column(dst.shape[0], _p(dst), dst.shape[1], col, float(value),

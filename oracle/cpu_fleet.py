@@ -66,13 +66,20 @@ class CpuFleetOps:
         d = dst.numpy()
         d[:, cols.numpy()] = s[rows]
 
-    def scatter_many(self, moves, dst):
-        for T, src, rows, cols in moves:
-            self.scatter_rows(T, src, rows, dst, cols)
+    def scatter_plan(self, moves, dst):
+        return ("s", list(moves), dst)
 
-    def gather_many(self, T, src, moves):
-        for cols, dst, rows in moves:
-            self.gather_rows(T, src, cols, dst, rows)
+    def gather_plan(self, T, src, moves):
+        return ("g", T, src, list(moves))
+
+    def run_plan(self, plan):
+        if plan[0] == "s":
+            for T, src, rows, cols in plan[1]:
+                self.scatter_rows(T, src, rows, plan[2], cols)
+        else:
+            _, T, src, moves = plan
+            for cols, dst, rows in moves:
+                self.gather_rows(T, src, cols, dst, rows)
 
     def fill_column(self, dst, col, value):
         dst.numpy()[:, col] = value

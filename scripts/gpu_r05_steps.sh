@@ -223,12 +223,26 @@ step_s16() {
   # neither (MPCX_FLEET_LEAD=0 MPCX_FLEET_FUSED=0): the record's C2 leg fell to 741 it/s inside the
   # full line while the legs-only runs gave 1178
   mkdir -p gpurun_out/s16
+  # the ADMM legs alone but WITH their CPU baselines (does the host work between legs matter?)
+  timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 --agents 64 --no-e2e --nn-zones 0 --mhe-agents 0 > gpurun_out/s16/legs_cpu.json 2> gpurun_out/s16/legs_cpu.err || exit $?
   for V in L1F1 L0F0 L1F1; do
     L=${V:1:1}; F=${V:3:1}
     MPCX_FLEET_LEAD=$L MPCX_FLEET_FUSED=$F timeout -k 10 600 python -u bench.py > gpurun_out/s16/bench_$V.json.tmp 2> gpurun_out/s16/bench_$V.err || exit $?
     cat gpurun_out/s16/bench_$V.json.tmp >> gpurun_out/s16/bench_$V.json
   done
   echo "s16 exit $?"
+}
+
+step_s17() {
+  # r05/s17: fused moves prepared once per fleet (no per-iteration host allocation); the full
+  # default bench line normally and with the interpreter's cyclic collector off (diagnostics: is
+  # the C2 leg's slowdown inside the full line the collector scanning the earlier legs' objects?);
+  # the ADMM GPU tests
+  mkdir -p gpurun_out/s17
+  timeout -k 10 600 python -u bench.py > gpurun_out/s17/bench.json 2> gpurun_out/s17/bench.err || exit $?
+  timeout -k 10 600 python -u -c "import gc, runpy, sys; gc.disable(); sys.argv = ['bench.py']; runpy.run_path('bench.py', run_name='__main__')" > gpurun_out/s17/bench_nogc.json 2> gpurun_out/s17/bench_nogc.err || exit $?
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_admm.py -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s17/gpu_admm_tests.txt 2>&1
+  echo "s17 exit $?"
 }
 
 step_rec() {

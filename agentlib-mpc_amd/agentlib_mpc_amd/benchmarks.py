@@ -505,16 +505,17 @@ def compile_all(verbose: bool = False):
                     paths[name] = path
                 if verbose:
                     print(f"[mpcx] {name}{label[v]}: {path.name if path else '-'}")
-    # test build: the filter capped at FILTER_CAP_TEST entries (overflow parity with the oracle,
-    # tests/test_gpu_ipm.py::test_gpu_filter_overflow_matches_oracle); MPCX_DEFINES names it
+    # test builds of the filter (tests/test_gpu_ipm.py::test_gpu_filter_matches_oracle): a small LDS
+    # part, so that the cubic_room case spills, and a small total capacity, so that it overflows
     saved = os.environ.get("MPCX_DEFINES")
-    os.environ["MPCX_DEFINES"] = FILTER_CAP_DEFINES
     try:
         gen = cubic_room()[0].problem.gen
-        for v in (None, native.SMALL_FLEET, native.MID_FLEET):
-            path = native.compile_model(gen, False, v)
-            if verbose:
-                print(f"[mpcx] cubic_room {FILTER_CAP_DEFINES}{label[v]}: {path.name if path else '-'}")
+        for defines, _cap in FILTER_TEST_BUILDS.values():
+            os.environ["MPCX_DEFINES"] = defines
+            for v in (None, native.SMALL_FLEET, native.MID_FLEET):
+                path = native.compile_model(gen, False, v)
+                if verbose:
+                    print(f"[mpcx] cubic_room {defines}{label[v]}: {path.name if path else '-'}")
     finally:
         if saved is None:
             os.environ.pop("MPCX_DEFINES", None)
@@ -523,9 +524,11 @@ def compile_all(verbose: bool = False):
     return paths
 
 
-#: the filter cap of the overflow-parity test build (MPCX_DEFINES, csrc/mpcx_ipm.hip MPCX_MAXF)
-FILTER_CAP_TEST = 8
-FILTER_CAP_DEFINES = f"MPCX_MAXF={FILTER_CAP_TEST}"
+#: the filter's capacity (csrc/mpcx_ipm.hip MAXF + FSPILL; oracle/ipm.py max_filter)
+FILTER_CAPACITY = 1024
+#: filter test builds (MPCX_DEFINES) and the oracle cap each matches: "spill" keeps 8 entries in LDS
+#: and the rest in the spill list (capacity unchanged), "capped" holds 12 in all (8 + 4)
+FILTER_TEST_BUILDS = {"spill": ("MPCX_MAXF=8", FILTER_CAPACITY), "capped": ("MPCX_MAXF=8,MPCX_FSPILL=4", 12)}
 
 
 # ---------------------------------------------------------------------------

@@ -52,15 +52,23 @@ constexpr int LDB = (NB % 2 == 0) ? NB + 1 : NB;
 constexpr int WAVE = 64;
 constexpr int VS = (NW + WAVE - 1) / WAVE;  // variable slots per lane
 constexpr int CS = (M + WAVE - 1) / WAVE;   // constraint slots per lane
-// filter entries kept in LDS (IPOPT's filter list is unbounded; entries a new one dominates are
-// removed on insertion, Filter::AddEntry): one cap shared with oracle/ipm.py (max_filter) and
-// oracle/c/ipm_oracle.c; an insertion into a full filter drops the oldest entry (counted)
-// (MPCX_MAXF: a smaller cap for the overflow-parity test build, tests/test_gpu_ipm.py)
+// The filter (IPOPT Filter: entries a new one dominates are removed on insertion, AddEntry; the
+// list is unbounded).  Its newest MAXF entries live in LDS, one per lane for the filter test; older
+// ones move, in insertion order, to a spill list in the agent's HBM workspace (FSPILL entries,
+// scanned only while it holds any -- no benchmark case ever fills the LDS part).  Together
+// MAXF + FSPILL = 1024 entries, the cap shared with oracle/ipm.py (max_filter) and
+// oracle/c/ipm_oracle.c; an insertion into a full filter drops the oldest entry (counted).
+// MPCX_MAXF / MPCX_FSPILL: smaller parts for the parity test builds (tests/test_gpu_ipm.py).
 #ifndef MPCX_MAXF
 #define MPCX_MAXF 64
 #endif
 constexpr int MAXF = MPCX_MAXF;
 static_assert(MAXF >= 1 && MAXF <= 64, "the filter test reads one entry per lane");
+#ifndef MPCX_FSPILL
+#define MPCX_FSPILL (1024 - MPCX_MAXF)
+#endif
+constexpr int FSPILL = MPCX_FSPILL;
+static_assert(FSPILL >= 0, "spill list size");
 constexpr double INF_BOUND = 1e19;
 constexpr double TS = MPCX_TS;
 
@@ -188,7 +196,10 @@ constexpr long O_RRHS = O_FLT0 + 2L * MAXF;      // [N][NB] the step's right-han
 constexpr long O_RSOL = O_RRHS + (long)N * NB;   // [N][NB] the step so far
 constexpr long O_RU = O_RSOL + (long)N * NB;     // [N][NLOC] local step vectors
 constexpr long O_RY = O_RU + (long)N * NLOC;     // [N][NLOC] local KKT products
-constexpr long WS_DOUBLES = O_RY + (long)N * NLOC;
+// filter spill lists: [tier][theta | phi][FSPILL], tier 0 the problem's filter (kept while a
+// restoration phase runs), tier 1 the restoration phase's own
+constexpr long O_FSP = O_RY + (long)N * NLOC;
+constexpr long WS_DOUBLES = O_FSP + 4L * FSPILL;
 // IPOPT restoration constants (its defaults; not exposed as options)
 constexpr double RESTO_RHO = 1000.0;          // resto_penalty_parameter
 constexpr double RESTO_KAPPA = 0.9;           // required_infeasibility_reduction
@@ -399,6 +410,7 @@ struct KState {
   double fo, zeta, prox, mu0, tau0, dw_last0, theta_max0, theta_min0, theta_start;
   int resto, soft, soft_count, lsmode, nfilt0, square_r, n_soft, n_resto_it;
   int n_filt_over, n_refine;  // filter insertions that dropped the oldest entry; refinement steps
+  int nsp[2];                 // entries in the filter spill lists (tier 0: the problem's, 1: restoration's)
   double rnrm;                // refinement: max-norm of the step's full right-hand side
   // the barrier sum at the current iterate when it is the last accepted line-search trial point
   // (bar_ok): recover_step then takes it instead of recomputing every log of the slacks
@@ -657,6 +669,7 @@ struct Agent {
   __device__ cdbl* vl0() const { return cold_base() + O_VL0; }
   __device__ cdbl* vu0() const { return cold_base() + O_VU0; }
   __device__ cdbl* flt0() const { return cold_base() + O_FLT0; }
+  __device__ cdbl* fsp(int tier) const { return cold_base() + O_FSP + 2L * FSPILL * tier; }
   __device__ cdbl* rrhs() const { return cold_base() + O_RRHS; }
   __device__ cdbl* rsol() const { return cold_base() + O_RSOL; }
   __device__ cdbl* ru() const { return cold_base() + O_RU; }
@@ -2735,6 +2748,8 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
   return st;
 }
 
+__device__ __noinline__ bool spill_dominates(double th, double ph);  // the filter's spill list (below)
+
 struct LSOpt {  // line-search options by value (registers, not kernarg loads)
   double alpha_min_frac, gamma_theta, gamma_phi, delta, s_theta, s_phi, eta_phi;
 };
@@ -2841,6 +2856,7 @@ __device__ MPCX_HOT void line_search(const Agent a) {
       const int j = lane_now();
       const bool dom = j < K.nfilt && tr.theta >= gL.fth[j < MAXF ? j : 0] && tr.phi >= gL.fph[j < MAXF ? j : 0];
       if (__any(dom)) okt = false;
+      if (okt && K.nsp[K.resto] > 0 && spill_dominates(tr.theta, tr.phi)) okt = false;  // older entries
     }
     const bool okf = okt;
     (void)okf;
@@ -3067,6 +3083,7 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
     K.mu = new_mu;
     K.tau = fmax(ka.opt.tau_min, 1.0 - new_mu);
     K.nfilt = 0;
+    K.nsp[0] = 0;  // the filter is reset with mu (both parts)
   }
   SPROF(8);  // termination tests, barrier update
   const double mu = K.mu;
@@ -3257,28 +3274,96 @@ __device__ __noinline__ int soft_try(const Agent a) {
   return 0;
 }
 
+// The current filter's spill list (tier = K.resto): its entries older than the MAXF in LDS.
+__device__ __forceinline__ cdbl* fsp_tier(int tier) { return cold_base() + O_FSP + 2L * FSPILL * tier; }
+
+// a trial (th, ph) dominated by an entry of the current filter's spill list (wave-uniform)
+__device__ __noinline__ bool spill_dominates(double th, double ph) {
+  KState& K = gL.ks;
+  const int t = K.resto, ns = K.nsp[t];
+  cdbl* sp = fsp_tier(t);
+  const int lane = lane_now();
+  bool dom = false;
+  for (int b = 0; b < ns; b += WAVE) {
+    const int j = b + lane;
+    if (j < ns && th >= sp[j] && ph >= sp[FSPILL + j]) dom = true;
+  }
+  return __any(dom);
+}
+
+// remove the spill entries (th, ph) dominates, order kept; returns the new count.  Each lane
+// writes at or below the index it read, after the whole chunk was read.
+__device__ __noinline__ int spill_prune(double th, double ph, int t, int ns) {
+  cdbl* sp = fsp_tier(t);
+  const int lane = lane_now();
+  int out = 0;
+  for (int b = 0; b < ns; b += WAVE) {
+    const int j = b + lane;
+    double e = 0.0, p = 0.0;
+    if (j < ns) { e = sp[j]; p = sp[FSPILL + j]; }
+    const bool keep = j < ns && !(th <= e && ph <= p);
+    const unsigned long long km = __ballot(keep);
+    const int pos = out + __popcll(km & ((1ull << lane) - 1ull));
+    wsync();
+    if (keep) { sp[pos] = e; sp[FSPILL + pos] = p; }
+    wsync();
+    out += __popcll(km);
+  }
+  return out;
+}
+
+// drop the oldest spill entry (a full filter), order kept
+__device__ __noinline__ void spill_shift(int t, int ns) {
+  cdbl* sp = fsp_tier(t);
+  const int lane = lane_now();
+  for (int b = 1; b < ns; b += WAVE) {
+    const int j = b + lane;
+    double e = 0.0, p = 0.0;
+    if (j < ns) { e = sp[j]; p = sp[FSPILL + j]; }
+    wsync();
+    if (j < ns) { sp[j - 1] = e; sp[FSPILL + j - 1] = p; }
+    wsync();
+  }
+}
+
 // IPOPT Filter::AddEntry of (th, ph): the entries the new one dominates (th <= theta_j and
-// ph <= phi_j) are removed, order kept, then it is appended; a full filter drops its oldest
-// entry (counted: IPOPT's list is unbounded).  One entry per lane: a ballot compacts the kept
-// entries in one LDS read and write.
+// ph <= phi_j) are removed from both parts, order kept, then it is appended to the LDS part; when
+// the LDS part is still full its oldest entry moves to the end of the spill list, and a full spill
+// list first drops its own oldest entry (counted: IPOPT's list is unbounded).  One LDS entry per
+// lane: a ballot compacts the kept entries in one LDS read and write.
 __device__ __forceinline__ void filter_insert(double th, double ph) {
   KState& K = gL.ks;
   const int j = lane_now();
+  const int t = K.resto;
+  int ns = K.nsp[t];
+  if (ns > 0) ns = spill_prune(th, ph, t, ns);
   const int nf = K.nfilt;
   const double ej = gL.fth[j < MAXF ? j : 0], pj = gL.fph[j < MAXF ? j : 0];
   const bool keep = j < nf && !(th <= ej && ph <= pj);
   const unsigned long long km = __ballot(keep);
   int nk = __popcll(km);
   int pos = __popcll(km & ((1ull << j) - 1ull));
-  const int drop = nk >= MAXF ? 1 : 0;  // still full: the oldest kept entry goes
-  pos -= drop;
-  nk -= drop;
+  const int full = nk >= MAXF ? 1 : 0;  // the oldest kept entry leaves the LDS part
+  if (full) {
+    const int first = __builtin_ctzll(km);
+    const double e0 = rl_f64(ej, first), p0 = rl_f64(pj, first);
+    if (FSPILL == 0) {
+      K.n_filt_over += 1;
+    } else {
+      if (ns >= FSPILL) { spill_shift(t, ns); ns -= 1; K.n_filt_over += 1; }
+      cdbl* sp = fsp_tier(t);
+      if (j == 0) { sp[ns] = e0; sp[FSPILL + ns] = p0; }
+      ns += 1;
+    }
+  }
+  pos -= full;
+  nk -= full;
   wsync();
   if (keep && pos >= 0) { gL.fth[pos] = ej; gL.fph[pos] = pj; }
   if (j == 0) { gL.fth[nk] = th; gL.fph[nk] = ph; }
   wsync();
   K.nfilt = nk + 1;
-  K.n_filt_over += drop;
+  K.nsp[t] = ns;
 }
 
 // ---- restoration phase ----------------------------------------------------------------
@@ -3348,6 +3433,7 @@ __device__ __noinline__ void resto_start(const Agent a) {
   K.theta_max = ka.opt.theta_max_fact * fmax(1.0, th);
   K.theta_min = ka.opt.theta_min_fact * fmax(1.0, th);
   K.nfilt = 0;
+  K.nsp[1] = 0;  // the restoration phase's own filter; the problem's (LDS part saved, spill kept) returns with it
   K.dw_last = 0.0;
   K.acc = Acceptable{-1e50, -1e50, -1, 0};
   K.resto = 1;
@@ -3504,6 +3590,9 @@ __device__ __noinline__ int iter_head_resto(const Agent a) {
       const int nf = K.nfilt0;
       for (int j = 0; j < nf && ret; ++j)
         if (tho >= a.flt0()[j] && phio >= a.flt0()[MAXF + j]) ret = false;
+      const int ns0 = K.nsp[0];  // the original filter's older entries (its spill list, untouched)
+      for (int j = 0; j < ns0 && ret; ++j)
+        if (tho >= a.fsp(0)[j] && phio >= a.fsp(0)[FSPILL + j]) ret = false;
     }
     if (ret) return 2;
   }
@@ -3555,6 +3644,7 @@ __device__ __noinline__ int iter_head_resto(const Agent a) {
     K.mu = new_mu;
     K.tau = fmax(ka.opt.tau_min, 1.0 - new_mu);
     K.nfilt = 0;
+    K.nsp[1] = 0;
     K.zeta = sqrt(new_mu);
     K.fx = RESTO_RHO * spn + 0.5 * K.zeta * sd;
     e.dual = dual_x(K.zeta);
@@ -3898,6 +3988,7 @@ __device__ __noinline__ void line_search_resto(const Agent a) {
       const int j = lane_now();
       const bool dom = j < K.nfilt && tr.theta >= gL.fth[j < MAXF ? j : 0] && tr.phi >= gL.fph[j < MAXF ? j : 0];
       if (__any(dom)) okt = false;
+      if (okt && K.nsp[K.resto] > 0 && spill_dominates(tr.theta, tr.phi)) okt = false;  // older entries
     }
     const bool okf = okt;
     (void)okf;
@@ -4078,6 +4169,7 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
     K.theta_min = OPT(theta_min_fact) * fmax(1.0, theta0);
   }
   K.nfilt = 0;
+  K.nsp[0] = 0; K.nsp[1] = 0;
   K.status = MPCX_MAX_ITER_EXCEEDED;
   K.it = 0;
   K.acc = Acceptable{-1e50, -1e50, -1, 0};

@@ -601,8 +601,8 @@ static double push_into(double v, double lo, double hi) {
   return fmin(fmax(v, lop), hip);
 }
 
-/* ---- filter (IPOPT Filter): one cap shared with the kernel (MAXF) and oracle/ipm.py ---- */
-#define MAXF 64
+/* ---- filter (IPOPT Filter): one cap shared with the kernel (MAXF + FSPILL) and oracle/ipm.py ---- */
+#define MAXF 1024
 typedef struct { double th[MAXF], ph[MAXF]; int n, over, maxn; } filter_t;
 static int filter_accepts(const filter_t* f, double th, double ph) {
   for (int j = 0; j < f->n; ++j)

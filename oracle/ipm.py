@@ -86,10 +86,11 @@ class IPMOptions:
     gamma_phi: float = 1e-8
     gamma_theta: float = 1e-5
     alpha_min_frac: float = 0.05
-    #: filter entries kept (IPOPT's list is unbounded; the kernel keeps one entry per lane of a
-    #: wavefront): one cap for the kernel (MAXF, csrc/mpcx_ipm.hip), oracle/c/ipm_oracle.c and
-    #: this file; an insertion into a full filter drops the oldest entry and is counted
-    max_filter: int = 64
+    #: filter entries kept (IPOPT's list is unbounded; the kernel keeps its newest 64 in LDS and
+    #: the older ones in a spill list in HBM, MAXF + FSPILL = 1024 in all, csrc/mpcx_ipm.hip): one
+    #: cap for the kernel, oracle/c/ipm_oracle.c and this file; an insertion into a full filter
+    #: drops the oldest entry and is counted
+    max_filter: int = 1024
     # iterative refinement of the restoration-phase Newton steps on the full system (IPOPT
     # PDFullSpaceSolver: min_refinement_steps, max_refinement_steps, residual_ratio_max,
     # residual_improvement_factor)

@@ -313,22 +313,24 @@ def test_gpu_long_restoration_run_follows_the_oracle(name, kw, setting, prefix, 
 
 
 @pytest.mark.parametrize("build", BUILDS)
-@pytest.mark.parametrize("capped", [False, True])
-def test_gpu_filter_overflow_matches_oracle(capped, build, monkeypatch):
-    """The filter (IPOPT Filter::AddEntry: dominated entries removed on insertion) with one cap
-    for kernel and oracle: at the shipped cap (64) the cubic_room restoration case holds up to
-    22 entries and never overflows; a test build capped at 8 entries (MPCX_MAXF, prebuilt by
-    build()) overflows 14 times -- the oldest entry dropped, counted -- exactly as the oracle
-    with max_filter = 8 does, on the same path."""
+@pytest.mark.parametrize("mode", ["shipped", "spill", "capped"])
+def test_gpu_filter_matches_oracle(mode, build, monkeypatch):
+    """The filter (IPOPT Filter::AddEntry: dominated entries removed on insertion; IPOPT's list is
+    unbounded) against the oracle's on the cubic_room restoration case, which holds up to 22
+    entries: the shipped build (64 in LDS + 960 in the spill list) never spills; a test build with
+    8 entries in LDS moves the older ones to the spill list and must follow the oracle's unbounded
+    (1024) filter exactly -- same path, no overflow; a test build holding 12 in all (8 + 4)
+    overflows, dropping the oldest entry, exactly as the oracle with max_filter = 12 does."""
     from agentlib_mpc_amd import benchmarks as bm
 
-    cap = bm.FILTER_CAP_TEST if capped else 64
-    if capped:
-        monkeypatch.setenv("MPCX_DEFINES", bm.FILTER_CAP_DEFINES)
+    cap = bm.FILTER_CAPACITY
+    if mode != "shipped":
+        defines, cap = bm.FILTER_TEST_BUILDS[mode]
+        monkeypatch.setenv("MPCX_DEFINES", defines)
     case = configs.CASES["cubic_room"](solver_options=bm.TIGHT)
     ref = _oracle(case, ipm.IPMOptions(tol=1e-10, max_iter=500, acceptable_iter=0, max_filter=cap),
                   key=("cubic_room", "filter"))
-    assert ref.max_filter_size == (cap if capped else 22) and (ref.filter_overflows > 0) == capped
+    assert ref.max_filter_size == min(cap, 22) and (ref.filter_overflows > 0) == (mode == "capped")
     for r in _gpu_solve(case, n_copies=2, build=build):
         st = r.stats
         got = (st["return_status"], st["iter_count"], st["n_soft_restorations"], st["n_restorations"],

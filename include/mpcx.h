@@ -127,8 +127,9 @@ typedef struct mpcx_stats {
   int32_t n_dense_stages; /* stage factorisations redone densely (static sparse pivot rejected) */
   int32_t n_soft_restorations; /* line-search failures resolved by a soft restoration step */
   int32_t n_restoration_iters; /* iterations spent in the restoration phase (in iter_count) */
-  int32_t n_filter_overflows;  /* filter insertions that dropped the oldest entry (cap 64; IPOPT's
-                                  filter is unbounded, so 0 means the run is IPOPT's) */
+  int32_t n_filter_overflows;  /* filter insertions that dropped the oldest entry (cap 1024: 64 in
+                                  LDS, the older ones in HBM; IPOPT's filter is unbounded, so 0
+                                  means the run is IPOPT's) */
   int32_t n_refinement_steps;  /* iterative-refinement corrections of restoration-phase steps */
 } mpcx_stats;
 

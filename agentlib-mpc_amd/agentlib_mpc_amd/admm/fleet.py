@@ -39,6 +39,7 @@ import contextlib
 import dataclasses
 import math
 import os
+import sys
 import time
 from typing import Dict, List, Optional, Sequence, Union
 
@@ -199,6 +200,9 @@ class _BlockRecords(Sequence):
             raise IndexError(b)
         return [IterationRecord(float(p[b]), float(d[b]), float(r[b]), wall_time=t)
                 for p, d, r, a, t in self._rows if a[b]]
+
+
+_DEBUG = os.environ.get("MPCX_FLEET_DEBUG", "0") == "1"
 
 
 class ADMMFleet:
@@ -836,6 +840,9 @@ class ADMMFleet:
         if self._mapped:
             for c, n in zip(self.classes, h[len(h) - len(self.classes):]):
                 c.bound = int(n)
+        if _DEBUG:  # diagnostics: the launch sizes a round takes
+            print(f"[fleet] mapped={self._mapped} bounds={[c.bound for c in self.classes]} "
+                  f"t={time.perf_counter():.4f}", file=sys.stderr, flush=True)
         return h
 
     def _expand_blocks(self, active_b):

@@ -245,6 +245,16 @@ step_s17() {
   echo "s17 exit $?"
 }
 
+step_s18() {
+  # r05/s18: which earlier leg slows the C2 leg's late steps inside the full line: the full line,
+  # without the C5-zone leg, with a 64-agent C3 leg; launch sizes logged (MPCX_FLEET_DEBUG)
+  mkdir -p gpurun_out/s18
+  MPCX_FLEET_DEBUG=1 timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e > gpurun_out/s18/full.json 2> gpurun_out/s18/full.err || exit $?
+  MPCX_FLEET_DEBUG=1 timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e --nn-zones 0 > gpurun_out/s18/nonn.json 2> gpurun_out/s18/nonn.err || exit $?
+  MPCX_FLEET_DEBUG=1 timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e --agents 64 > gpurun_out/s18/c3small.json 2> gpurun_out/s18/c3small.err
+  echo "s18 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -205,6 +205,9 @@ class _BlockRecords(Sequence):
 _DEBUG = os.environ.get("MPCX_FLEET_DEBUG", "0") == "1"
 
 
+_DEBUG = os.environ.get("MPCX_FLEET_DEBUG", "0") == "1"
+
+
 class ADMMFleet:
     """Device-resident ADMM over fleets of agents (one or more classes).
 
@@ -647,11 +650,16 @@ class ADMMFleet:
         exchange alias is NOT shifted."""
         ops, T = self.ops, self.T
         if self.G:
-            ex = self.torch.as_tensor(self.exchange_flags, device=self.device) != 0
-            keep = self.MEAN[:self.G][ex].clone() if bool(ex.any()) else None
+            # the exchange aliases' rows, a device index built once: a mask built from the host
+            # flags here was a pageable host-to-device copy and two synchronisations per round,
+            # which took 14-27 ms in some processes (r05/s20) against a 30 ms round
+            if getattr(self, "_ex_rows", None) is None:
+                self._ex_rows = self.torch.as_tensor(np.flatnonzero(np.asarray(self.exchange_flags)[:self.G]),
+                                                     dtype=self.torch.int64, device=self.device)
+            keep = self.MEAN.index_select(0, self._ex_rows) if self._ex_rows.numel() else None
             ops.shift(T, shift, self.MEAN)
             if keep is not None:
-                self.MEAN[:self.G][ex] = keep
+                self.MEAN.index_copy_(0, self._ex_rows, keep)
         ops.shift(T, shift, self.LAMR)
         ops.shift(T, shift, self.DIFF)
         ops.shift(T, shift, self.GMULT)
@@ -751,6 +759,7 @@ class ADMMFleet:
         ops, nb = self.ops, self.n_blocks
         dev, i32 = self.device, t.int32
         t0 = time.perf_counter()  # _performance_counter, set at the start of the round (:270)
+        marks = [("entry", t0)] if _DEBUG else None
         rho0 = float(penalty_factor)
         n_it = max(int(admm_iter_max), 0)
         ACTIVE_B = t.ones(nb, dtype=i32, device=dev)
@@ -772,15 +781,24 @@ class ADMMFleet:
         crit = (1 if use_relative_tolerances else 0, abs_tol, rel_tol, primal_tol, dual_tol,
                 penalty_change_threshold, penalty_change_factor)
         coll0 = self.n_collectives
+        if marks is not None:
+            marks.append(("alloc", time.perf_counter()))
         self._update_means(rho0, apply_multipliers=False, per_block=True)
+        if marks is not None:
+            marks.append(("means", time.perf_counter()))
         shift = int(len(self.classes[0].coupling_grid) / self.classes[0].horizon)
         self._shift_all(shift)
+        if marks is not None:
+            marks.append(("shift", time.perf_counter()))
         self._counts.zero_()
         tot = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
         multi = self.world > 1
         ctrl = self.CONTROL if multi else None
         # the round's first stamp (and, with several ranks, the starting count into the control)
         ops.block_stop(0, tot, crit, self.RHO_B, ACTIVE_B, ITERS_B, REC, NACT, CLOCK, ctrl)
+        if marks is not None:
+            self._sync()
+            marks.append(("prologue", time.perf_counter()))
         ran = executed = 0
         every = max(int(check_every), 1)
         for it in range(1, n_it + 1):
@@ -801,6 +819,8 @@ class ADMMFleet:
                 if self._take_bounds(CHK)[it] == 0:
                     break
         self._sync()
+        if marks is not None:
+            marks.append(("loop", time.perf_counter()))
         # the next round starts from full penalties and no freeze mask
         self._masked = False
         self._mapped = False
@@ -827,6 +847,10 @@ class ADMMFleet:
             records = block_records[0]
         self.history.extend(records)
         self.rounds += 1
+        if marks is not None and self.device.type == "cuda":
+            marks.append(("records", time.perf_counter()))
+            print("[fleet] round " + " ".join(f"{n}={(t - t0) * 1e3:.2f}" for n, t in marks[1:]) + f" it={ran}",
+                  file=sys.stderr, flush=True)
         return {"iterations": last, "converged": bool(conv_b.all()), "records": records, "wall_s": wall,
                 "converged_solves": int(self._counts[0].item()), "block_iterations": iters,
                 "block_converged": conv_b, "block_records": block_records, "block_is_global": self.block_is_global.copy(),

@@ -255,6 +255,30 @@ step_s18() {
   echo "s18 exit $?"
 }
 
+step_s19() {
+  # r05/s19: the lead class's stream at high priority (its own hardware queue): three line runs
+  # (no MHE / e2e legs) against two with plain streams (MPCX_FLEET_PRIO=0); launch sizes logged
+  mkdir -p gpurun_out/s19
+  for V in p1 p0 p1 p0 p1; do
+    P=${V:1:1}
+    MPCX_FLEET_PRIO=$P timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e > gpurun_out/s19/line_$V.json.tmp 2> gpurun_out/s19/line_$V.err || exit $?
+    cat gpurun_out/s19/line_$V.json.tmp >> gpurun_out/s19/line_$V.json
+  done
+  rm -rf gpurun_out/s19/prof_c2
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/s19/prof_c2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0 > gpurun_out/s19/c2.json 2> gpurun_out/s19/c2.err
+  echo "s19 exit $?"
+}
+
+step_s20() {
+  # r05/s20: where a slow C2 step's extra ~16 ms go (round prologue / loop / records, logged by
+  # MPCX_FLEET_DEBUG): three line runs without the MHE / e2e legs
+  mkdir -p gpurun_out/s20
+  for V in a b c; do
+    MPCX_FLEET_DEBUG=1 timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e > gpurun_out/s20/line_$V.json 2> gpurun_out/s20/line_$V.err || exit $?
+  done
+  echo "s20 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -279,6 +279,15 @@ step_s20() {
   echo "s20 exit $?"
 }
 
+step_s21() {
+  # r05/s21: kernel trace of the line (no MHE / e2e legs) with the round phase log: what the GPU
+  # does in a slow C2 round's prologue
+  mkdir -p gpurun_out/s21
+  rm -rf gpurun_out/s21/prof
+  MPCX_FLEET_DEBUG=1 timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/s21/prof -o run --output-format csv -- python3 bench.py --mhe-agents 0 --no-e2e --no-cpu-baseline > gpurun_out/s21/line.json 2> gpurun_out/s21/line.err
+  echo "s21 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -430,6 +430,10 @@ def _closed_loop(fleet, run, steps, ts, agents_per_block, world, dev):
     for step in range(max(int(steps), 1)):
         if step:
             bm.advance_plant(fleet, ts)
+        if cuda and os.environ.get("MPCX_BENCH_WAKE") == "1":
+            # diagnostics only: one trivial launch after the idle plant step,
+            # outside the timed region -- does the slow first GPU work of a step go away?
+            torch.ones(1, device=dev).add_(1.0)
         if cuda:
             torch.cuda.synchronize(dev)
         if world > 1:

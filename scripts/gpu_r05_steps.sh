@@ -288,6 +288,26 @@ step_s21() {
   echo "s21 exit $?"
 }
 
+step_s22() {
+  # r05/s22: diagnostics -- one trivial launch after each untimed plant step (MPCX_BENCH_WAKE=1)
+  # in three line runs: if the C2 leg is then always fast, the slow first GPU work of a step is
+  # the GPU waking from idle
+  mkdir -p gpurun_out/s22
+  for V in a b c; do
+    MPCX_BENCH_WAKE=1 MPCX_FLEET_DEBUG=1 timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e --no-cpu-baseline > gpurun_out/s22/line_$V.json 2> gpurun_out/s22/line_$V.err || exit $?
+  done
+  echo "s22 exit $?"
+}
+
+step_s23() {
+  # r05/s23: control for s22 -- the line without CPU baselines and without the wake-up launch
+  mkdir -p gpurun_out/s23
+  for V in a b c; do
+    MPCX_FLEET_DEBUG=1 timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e --no-cpu-baseline > gpurun_out/s23/line_$V.json 2> gpurun_out/s23/line_$V.err || exit $?
+  done
+  echo "s23 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -308,6 +308,14 @@ step_s23() {
   echo "s23 exit $?"
 }
 
+step_s24() {
+  # r05/s24: agents per CU of the C4 room build (MPCX_APC: 12 / 16 = default / 20 / 24 / 32, the
+  # register budget following) on the 13108-room fleet
+  mkdir -p gpurun_out/s24
+  MODEL=exchange_room AGENTS=13108 timeout -k 10 600 python -u scripts/variants.py run base apc12 apc20 apc24 apc32 base apc20 apc24 apc32 > gpurun_out/s24/var_c4room.txt 2>&1
+  echo "s24 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -71,6 +71,8 @@ VARIANTS = {
     "chain_seq": (["-DMPCX_CHAIN_SEQ"], None),
     "lds_nofence": (["-DMPCX_WS_LDS", "-DMPCX_ELIM_FENCE=(void)0"], None),
     # r04: more than 16 agents per CU for structures with a small LDS share and register need
+    "apc12": (["-DMPCX_APC=12"], None),
+    "apc16": (["-DMPCX_APC=16"], None),
     "apc20": (["-DMPCX_APC=20"], None),
     "apc24": (["-DMPCX_APC=24"], None),
     "apc32": (["-DMPCX_APC=32"], None),
@@ -85,6 +87,8 @@ VARIANTS = {
     "rev_ieee": (["-DMPCX_IEEE_DIV"], "REV:" + os.environ.get("REV", "HEAD")),
     "lds_ieee": (["-DMPCX_WS_LDS", "-DMPCX_IEEE_DIV"], None),
     "lds_rev_ieee": (["-DMPCX_WS_LDS", "-DMPCX_IEEE_DIV"], "REV:" + os.environ.get("REV", "HEAD")),
+    # r05: interprocedural register allocation on the current kernel, fleet and small-fleet builds
+    "lds_ipra": (["-DMPCX_WS_LDS", "-mllvm", "-enable-ipra"], None),
 }
 
 

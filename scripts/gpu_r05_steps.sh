@@ -316,6 +316,14 @@ step_s24() {
   echo "s24 exit $?"
 }
 
+step_s25() {
+  # r05/s25: compile-flag variants of the small-fleet build on C1 (one agent): -O2, no loop
+  # unrolling, a scheduler metric bias, interprocedural register allocation
+  mkdir -p gpurun_out/s25
+  AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_nounroll lds_o2 lds_maxnsa lds_ipra lds_base lds_nounroll lds_o2 lds_maxnsa lds_ipra > gpurun_out/s25/var_c1.txt 2>&1
+  echo "s25 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -89,6 +89,9 @@ VARIANTS = {
     "lds_rev_ieee": (["-DMPCX_WS_LDS", "-DMPCX_IEEE_DIV"], "REV:" + os.environ.get("REV", "HEAD")),
     # r05: interprocedural register allocation on the current kernel, fleet and small-fleet builds
     "lds_ipra": (["-DMPCX_WS_LDS", "-mllvm", "-enable-ipra"], None),
+    "lds_nounroll": (["-DMPCX_WS_LDS", "-fno-unroll-loops"], None),
+    "lds_o2": (["-DMPCX_WS_LDS", "-O2"], None),
+    "lds_maxnsa": (["-DMPCX_WS_LDS", "-mllvm", "-amdgpu-schedule-metric-bias=100"], None),
 }
 
 

@@ -324,6 +324,17 @@ step_s25() {
   echo "s25 exit $?"
 }
 
+step_s26() {
+  # r05/s26: the least-squares multiplier system assembled in the eliminating lane's registers
+  # (assemble_reg_lsq, the default now) against the LDS-image assembly (lsq_noreg): MHE fleet and
+  # C1 (one agent, small-fleet build); then the GPU parity suite on the default build
+  mkdir -p gpurun_out/s26
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base lsq_noreg base lsq_noreg > gpurun_out/s26/var_mhe.txt 2>&1 || exit $?
+  AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_lsq_noreg lds_base lds_lsq_noreg > gpurun_out/s26/var_c1.txt 2>&1 || exit $?
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s26/gpu_tests.txt 2>&1
+  echo "s26 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

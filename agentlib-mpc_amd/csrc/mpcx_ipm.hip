@@ -2198,39 +2198,8 @@ __device__ __forceinline__ void assemble_reg(const Agent a, int k, const KKTDiag
   }
 }
 
-// The least-squares multiplier system assembled the same way: generic_entry + local_diagonal's
-// values entry by entry, the Jacobian entries taken from the evaluators' compact image (gs * J,
-// the product generic_entry forms from the cold strided copy) instead of the strided arrays
-__device__ __forceinline__ void assemble_reg_lsq(const Agent a, int k, const KKTDiag& kd, double* Fr) {
-  const unsigned long long fm = gL.fixm[k];
-  const wdbl* src = a.lp(k);
-  const wdbl* rb = a.rhs(k);
-  const wdbl* ws = a.base();
-#pragma unroll
-  for (int t = 0; t < NCPT; ++t) {
-    const int ij = kCIJ[t], i = ij & 255, j = ij >> 8;
-    const int ki = lkind(i), kj = lkind(j);
-    const bool pi = (ki == 0 || ki == 2 || ki == 3), pj = (kj == 0 || kj == 2 || kj == 3);
-    const bool fix = (pi && ((fm >> i) & 1ull)) || (pj && ((fm >> j) & 1ull));
-    double v = 0.0;
-    if (pi && pj) v = (fix && i == j && ki == 0) ? 1.0 : 0.0;
-    else if ((kdual(ki) && pj) || (kdual(kj) && pi)) v = fix ? 0.0 : src[t * N];
-    else if (ki == 4 && kj != 2 && kj != 4) v = rb[lblk(j, kj)];
-    Fr[t] = v;
-  }
-#pragma unroll
-  for (int t = 0; t < (NLOC < NCPT ? NLOC : NCPT); ++t) {  // diagonal (t, t)
-    const int ki = lkind(t);
-    if ((ki == 0 || ki == 3) && ((fm >> t) & 1ull) == 0ull) Fr[t] += 1.0;
-    if (kdual(ki)) {
-      const int c = k * NG + lrow(t);
-      Fr[t] = -dual_diag_v(cls_of(ws[O_LB + c], ws[O_UB + c], ws[O_SL + c], ws[O_SU + c]), 0.0, kd);
-    }
-  }
-}
-
-// kdr: the KKT diagonal terms when the eliminating lane assembles the image itself (ELIM_REG),
-// nullptr when the image was assembled into Fl (LDS image)
+// kdr: the KKT diagonal terms when the eliminating lane assembles the image itself (ELIM_REG,
+// Newton systems), nullptr when the image was assembled into Fl (least-squares system, LDS image)
 template <bool STAGE0 = false>
 __device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* Fl, const KKTDiag* kdr = nullptr) {
   int in[3];
@@ -2241,8 +2210,7 @@ __device__ __forceinline__ int static_stage(const Agent a, int k, ldsd* Fl, cons
   if constexpr (ELIM_REG) {
     double Fr[NCPT];
     if (kdr != nullptr) {
-      if (kdr->mode == LSQ) assemble_reg_lsq(a, k, *kdr, Fr);
-      else assemble_reg(a, k, *kdr, Fr);
+      assemble_reg(a, k, *kdr, Fr);
     } else {
 #pragma unroll
       for (int t = 0; t < NCPT; ++t) Fr[t] = Fl[t];
@@ -2289,13 +2257,8 @@ __device__ __forceinline__ Inertia factor(const Agent a, const KKTDiag kd) {
   }
 #endif
 #ifdef MPCX_STATIC_ELIM
-  // register-image builds assemble the systems in the eliminating lane (assemble_reg,
-  // assemble_reg_lsq; MPCX_LSQ_NOREG: the least-squares system through the LDS image, A/B builds)
-#ifdef MPCX_LSQ_NOREG
+  // register-image builds assemble the Newton systems in the eliminating lane (assemble_reg)
   const bool reg_asm = ASM_REG && kd.mode != LSQ;
-#else
-  const bool reg_asm = ASM_REG;
-#endif
 #pragma unroll 1
   for (int r = 0; r < CROUNDS; ++r) {
     if (!reg_asm) {

@@ -327,7 +327,8 @@ step_s25() {
 step_s26() {
   # r05/s26: the least-squares multiplier system assembled in the eliminating lane's registers
   # (assemble_reg_lsq, the default now) against the LDS-image assembly (lsq_noreg): MHE fleet and
-  # C1 (one agent, small-fleet build); then the GPU parity suite on the default build
+  # C1 (one agent, small-fleet build); then the GPU parity suite on the default build.  Run at
+  # 9a47260 (base = that kernel); the kernel was reverted after it (MHE 10 % slower: 1776 B scratch)
   mkdir -p gpurun_out/s26
   MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base lsq_noreg base lsq_noreg > gpurun_out/s26/var_mhe.txt 2>&1 || exit $?
   AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_lsq_noreg lds_base lds_lsq_noreg > gpurun_out/s26/var_c1.txt 2>&1 || exit $?

@@ -92,9 +92,10 @@ VARIANTS = {
     "lds_nounroll": (["-DMPCX_WS_LDS", "-fno-unroll-loops"], None),
     "lds_o2": (["-DMPCX_WS_LDS", "-O2"], None),
     "lds_maxnsa": (["-DMPCX_WS_LDS", "-mllvm", "-amdgpu-schedule-metric-bias=100"], None),
-    # r05: the least-squares multiplier system through the LDS image (before assemble_reg_lsq)
-    "lsq_noreg": (["-DMPCX_LSQ_NOREG"], None),
-    "lds_lsq_noreg": (["-DMPCX_WS_LDS", "-DMPCX_LSQ_NOREG"], None),
+    # r05/s26: the least-squares multiplier system through the LDS image (MPCX_LSQ_NOREG) in the
+    # kernel of 9a47260 (assemble_reg_lsq; not kept: MHE 8.97 ms against 8.12, scratch 1776 B)
+    "lsq_noreg": (["-DMPCX_LSQ_NOREG"], "REV:9a47260"),
+    "lds_lsq_noreg": (["-DMPCX_WS_LDS", "-DMPCX_LSQ_NOREG"], "REV:9a47260"),
 }
 
 

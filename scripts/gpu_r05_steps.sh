@@ -336,6 +336,14 @@ step_s26() {
   echo "s26 exit $?"
 }
 
+step_s27() {
+  # r05/s27: the MHE twisted chain's phases (CW/CY products, pivot assembly, the swept pivots;
+  # scripts/prof_phases.py CHAIN_PROF=1 on a patched copy of the kernel)
+  mkdir -p gpurun_out/s27
+  CHAIN_PROF=1 MODEL=mhe_room AGENTS=4096 timeout -k 10 400 python -u scripts/prof_phases.py > gpurun_out/s27/phases_mhe_chain.txt 2>&1
+  echo "s27 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -4,12 +4,38 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "agentlib-mpc_amd")]
 import numpy as np
 
+CHAIN_PATCH = [
+    ("SPROF(6);  // loads and the per-element terms", "(void)0;"),
+    ("SPROF(7);  // reductions", "(void)0;"),
+    ("SPROF(8);  // termination tests, barrier update", "(void)0;"),
+    ("SPROF(9);  // rhs / diagonal stores and the barrier", "(void)0;"),
+    ("  constexpr int NCX = NC * NX;\n#pragma unroll 1\n  for (int s = 0; s <= CSTEPS; ++s) {",
+     "  constexpr int NCX = NC * NX;\n  SPROF_DECL\n#pragma unroll 1\n  for (int s = 0; s <= CSTEPS; ++s) {"),
+    ("    wsync();\n    // the pivots, assembled in their Dinv slots", "    wsync();\n    SPROF(6);\n    // the pivots, assembled in their Dinv slots"),
+    ("      L.Dinv[j * NCC + ee] = v;\n    }\n    wsync();\n", "      L.Dinv[j * NCC + ee] = v;\n    }\n    wsync();\n    SPROF(7);\n"),
+    ("    in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;\n  }\n  wsync();\n  return in;\n}\n\n// The twisted chain's solve",
+     "    in.pos += bi.pos; in.neg += bi.neg; in.zero += bi.zero;\n    SPROF(8);\n  }\n  wsync();\n  return in;\n}\n\n// The twisted chain's solve"),
+]
+
+
 def build_profile_hsaco(gen, wslds=False):
     from agentlib_mpc_amd.runtime import native
     src = native.KERNEL_DIR / f"prof_{gen.key}{'_wslds' if wslds else ''}.hip"
     out = src.with_suffix(".hsaco")
     src.parent.mkdir(parents=True, exist_ok=True)
-    src.write_text("#define MPCX_PROFILE 1\n" + ("#define MPCX_WS_LDS 1\n" if wslds else "") + gen.source)
+    text = gen.source
+    if os.environ.get("CHAIN_PROF", "0") == "1":
+        # the twisted chain's three phases in the iteration head's profile slots (6-8), on a
+        # patched copy of the kernel source (the shipped source stays as it is)
+        k = (native.CSRC / "mpcx_ipm.hip").read_text()
+        for a, b in CHAIN_PATCH:
+            assert k.count(a) == 1, a
+            k = k.replace(a, b)
+        kp = src.with_name(src.stem + "_chainprof_ipm.hip")
+        kp.write_text(k)
+        text = text.replace('#include "mpcx_ipm.hip"', f'#include "{kp}"')
+        assert str(kp) in text
+    src.write_text("#define MPCX_PROFILE 1\n" + ("#define MPCX_WS_LDS 1\n" if wslds else "") + text)
     subprocess.run([native._hipcc(), "--genco", "--offload-arch=gfx950", "-O3", "-std=c++17",
                     f"-I{native.INCLUDE}", f"-I{native.CSRC}", str(src), "-o", str(out)], check=True)
     return out
@@ -78,7 +104,9 @@ def main():
     print("total kcycles/agent", tot / 1e3)
     if prof.shape[1] >= 22:
         head = lw[:, 18:22].cpu().numpy().mean(axis=0)
-        for k, v in zip(["h:loads+terms", "h:reductions", "h:tests+mu", "h:stores+sync"], head):
+        labels = (["c:cw+cy", "c:assemble", "c:sweep", "-"] if os.environ.get("CHAIN_PROF", "0") == "1"
+                  else ["h:loads+terms", "h:reductions", "h:tests+mu", "h:stores+sync"])
+        for k, v in zip(labels, head):
             print(f"{k:14s} {v/1e3:10.1f} kcyc")
     seen = lw[:, 16].cpu().numpy().astype(np.int64) | (lw[:, 17].cpu().numpy().astype(np.int64) << 32)
     hist = [int(((seen >> k) & 1).sum()) for k in range(be.problem.gen.dims["N"])]

@@ -344,6 +344,15 @@ step_s27() {
   echo "s27 exit $?"
 }
 
+step_s28() {
+  # r05/s28: the twisted chain's pivot blocks swept on register images (bk_sweep2, readlane
+  # broadcasts) against the LDS sweep (sweep_lds) on the MHE fleet; then the GPU parity suite
+  mkdir -p gpurun_out/s28
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base sweep_lds base sweep_lds > gpurun_out/s28/var_mhe.txt 2>&1 || exit $?
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s28/gpu_tests.txt 2>&1
+  echo "s28 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

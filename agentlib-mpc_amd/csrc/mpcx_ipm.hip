@@ -1048,8 +1048,6 @@ __device__ __noinline__ Inertia bk_sweep(ldsd* A, OutT* out, int lane) {
 // candidates and lanes 8-15 block B's, each octet with its own DPP reduction, and every owning
 // lane updates its entry of both blocks -- so one pass costs the dependent latency of one.
 // In place (each block receives its own inverse); twob false sweeps A alone.
-// MPCX_SWEEP_LDS (A/B builds): this LDS sweep; by default the register sweep below.
-#ifdef MPCX_SWEEP_LDS
 template <int NN, int LD>
 __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane) {
   static_assert(NN * NN <= WAVE && NN <= 8, "one lane per entry; pivot candidates in one lane octet");
@@ -1146,114 +1144,6 @@ __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane)
   wsync();
   return in;
 }
-#else
-// r05: the same sweep on register images.  Lane (i, j) holds entry (i, j) of each block in a VGPR;
-// the pivot indices are wave-uniform, so the column / row entries a pivot step reads are
-// broadcast with v_readlane (the LDS sweep's dependent LDS round trip and wave barrier per pivot
-// step go away) and each lane picks its own from them.  Same arithmetic, same pivot choices
-// (candidates scanned in index order with gargmax's rule: the largest, the smallest index on a
-// tie), so the same inverse bit for bit; the blocks are read from / written back to LDS once.
-template <int NN>
-__device__ __forceinline__ double pick_nn(const double (&v)[NN], int i) {
-  double r = v[0];
-#pragma unroll
-  for (int m = 1; m < NN; ++m) r = (i == m) ? v[m] : r;
-  return r;
-}
-template <int NN>
-__device__ __forceinline__ void sweep_step(double& x, unsigned& done, unsigned& zero, Inertia& in, int ti, int tj,
-                                           bool own) {
-  constexpr int NA = NN > 0 ? NN : 1;  // (NN = 0: instantiated by structures without a state chain)
-  const int k = __builtin_ctz(~done);
-  double lam = -1.0;
-  int r = -1;
-#pragma unroll
-  for (int m = 0; m < NN; ++m) {
-    const double c = fabs(rl_f64(x, m * NN + k));  // X[m][k]
-    if (!((done >> m) & 1u) && m != k) amax_merge(lam, r, c, m);
-  }
-  if (r < 0) lam = 0.0;
-  const double akk = fabs(rl_f64(x, k * NN + k));
-  int p = k, q = -1;  // 1x1 pivot p, or 2x2 pivot {k, q}
-  if (!(fmax(akk, lam) == 0.0 || akk >= BK_ALPHA * lam)) {
-    double sigma = 0.0;
-#pragma unroll
-    for (int m = 0; m < NN; ++m) {
-      const double c = fabs(rl_f64(x, r * NN + m));  // X[r][m]
-      if (!((done >> m) & 1u) && m != r) sigma = fmax(sigma, c);
-    }
-    if (akk * sigma >= BK_ALPHA * lam * lam) p = k;
-    else if (fabs(rl_f64(x, r * NN + r)) >= BK_ALPHA * sigma) p = r;
-    else q = r;
-  }
-  if (q < 0) {
-    const double d = rl_f64(x, p * NN + p);
-    done |= 1u << p;
-    if (fabs(d) <= ZERO_PIVOT) { in.zero++; zero |= 1u << p; return; }
-    if (d > 0) in.pos++; else in.neg++;
-    const double rd = MPCX_RCP(d);
-    double cp[NA], rp[NA];
-#pragma unroll
-    for (int m = 0; m < NN; ++m) { cp[m] = rl_f64(x, m * NN + p); rp[m] = rl_f64(x, p * NN + m); }
-    if (own) {
-      const double aip = pick_nn<NA>(cp, ti), apj = pick_nn<NA>(rp, tj), aij = x;
-      x = (ti == p) ? ((tj == p) ? -rd : apj * rd) : (tj == p) ? aip * rd : aij - aip * apj * rd;
-    }
-  } else {
-    const double a11 = rl_f64(x, k * NN + k), a21 = rl_f64(x, q * NN + k), a22 = rl_f64(x, q * NN + q);
-    const double det = a11 * a22 - a21 * a21;
-    done |= (1u << k) | (1u << q);
-    if (fabs(det) <= ZERO_PIVOT * ZERO_PIVOT) { in.zero += 2; zero |= (1u << k) | (1u << q); return; }
-    if (det < 0) { in.pos++; in.neg++; }
-    else if (a11 + a22 > 0) in.pos += 2;
-    else in.neg += 2;
-    const double rdet = MPCX_RCP(det);
-    const double p11 = a22 * rdet, p12 = -a21 * rdet, p22 = a11 * rdet;
-    double ck[NA], cq[NA], rk[NA], rq[NA];
-#pragma unroll
-    for (int m = 0; m < NN; ++m) {
-      ck[m] = rl_f64(x, m * NN + k); cq[m] = rl_f64(x, m * NN + q);
-      rk[m] = rl_f64(x, k * NN + m); rq[m] = rl_f64(x, q * NN + m);
-    }
-    if (own) {
-      const double aik = pick_nn<NA>(ck, ti), aiq = pick_nn<NA>(cq, ti), akj = pick_nn<NA>(rk, tj),
-                   aqj = pick_nn<NA>(rq, tj);
-      const double aij = x;
-      const double xk = aik * p11 + aiq * p12, xq = aik * p12 + aiq * p22;
-      const double yk = p11 * akj + p12 * aqj, yq = p12 * akj + p22 * aqj;
-      const bool ip = ti == k || ti == q, jp = tj == k || tj == q;
-      double v;
-      if (ip && jp) v = -((ti == k) ? ((tj == k) ? p11 : p12) : ((tj == k) ? p12 : p22));
-      else if (ip) v = (ti == k) ? yk : yq;
-      else if (jp) v = (tj == k) ? xk : xq;
-      else v = aij - (xk * akj + xq * aqj);
-      x = v;
-    }
-  }
-}
-template <int NN, int LD>
-__device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane) {
-  static_assert(NN * NN <= WAVE && NN <= 8, "one lane per entry");
-  constexpr unsigned FULL = (1u << NN) - 1u;
-  Inertia in{0, 0, 0};
-  const int ti = lane / NN, tj = lane % NN;
-  const bool own = lane < NN * NN;
-  double xa = own ? (double)A[ti * LD + tj] : 0.0;
-  double xb = (own && twob) ? (double)B[ti * LD + tj] : 0.0;
-  unsigned dA = 0u, zA = 0u, dB = twob ? 0u : FULL, zB = 0u;
-#pragma unroll 1
-  while (dA != FULL || dB != FULL) {
-    if (dA != FULL) sweep_step<NN>(xa, dA, zA, in, ti, tj, own);
-    if (dB != FULL) sweep_step<NN>(xb, dB, zB, in, ti, tj, own);
-  }
-  if (own) {
-    A[ti * LD + tj] = (((zA >> ti) | (zA >> tj)) & 1u) ? 0.0 : -xa;
-    if (twob) B[ti * LD + tj] = (((zB >> ti) | (zB >> tj)) & 1u) ? 0.0 : -xb;
-  }
-  wsync();
-  return in;
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // KKT entries

@@ -346,7 +346,8 @@ step_s27() {
 
 step_s28() {
   # r05/s28: the twisted chain's pivot blocks swept on register images (bk_sweep2, readlane
-  # broadcasts) against the LDS sweep (sweep_lds) on the MHE fleet; then the GPU parity suite
+  # broadcasts) against the LDS sweep (sweep_lds) on the MHE fleet; then the GPU parity suite.  Run
+  # at 1bfd8f5 (base = that kernel); reverted after it (bit-identical but 29 % slower)
   mkdir -p gpurun_out/s28
   MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base sweep_lds base sweep_lds > gpurun_out/s28/var_mhe.txt 2>&1 || exit $?
   timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s28/gpu_tests.txt 2>&1

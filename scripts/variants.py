@@ -95,9 +95,10 @@ VARIANTS = {
     # r05/s26: the least-squares multiplier system through the LDS image (MPCX_LSQ_NOREG) in the
     # kernel of 9a47260 (assemble_reg_lsq; not kept: MHE 8.97 ms against 8.12, scratch 1776 B)
     "lsq_noreg": (["-DMPCX_LSQ_NOREG"], "REV:9a47260"),
-    # r05/s28: the twisted chain's pivot blocks swept in LDS (before the register sweep)
-    "sweep_lds": (["-DMPCX_SWEEP_LDS"], None),
-    "lds_sweep_lds": (["-DMPCX_WS_LDS", "-DMPCX_SWEEP_LDS"], None),
+    # r05/s28: the LDS pivot sweep (MPCX_SWEEP_LDS) in the kernel of 1bfd8f5, whose default swept the
+    # twisted chain's pivots on register images (not kept: MHE 10.44 ms against 8.09 ms)
+    "sweep_lds": (["-DMPCX_SWEEP_LDS"], "REV:1bfd8f5"),
+    "sweep_reg": ([], "REV:1bfd8f5"),
     "lds_lsq_noreg": (["-DMPCX_WS_LDS", "-DMPCX_LSQ_NOREG"], "REV:9a47260"),
 }
 

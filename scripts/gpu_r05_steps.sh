@@ -354,6 +354,14 @@ step_s28() {
   echo "s28 exit $?"
 }
 
+step_s29() {
+  # r05/s29: the LDS pivot sweep with its pivot values read into SGPRs (uni_f64) against f641ef4's
+  # sweep (rev) on the MHE fleet
+  mkdir -p gpurun_out/s29
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s29/var_mhe.txt 2>&1
+  echo "s29 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -227,13 +227,6 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
   return ((unsigned long long)hi << 32) | lo;
 }
-// wave-uniform double (an LDS value every lane read from one address) into SGPRs: the
-// branches that test it become scalar branches instead of exec-mask regions
-__device__ __forceinline__ double uni_f64(double v) {
-  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
-  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
-  return __hiloint2double(hi, lo);
-}
 
 // ---------------------------------------------------------------------------
 // wave and lane-group helpers
@@ -1079,7 +1072,7 @@ __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane)
     const int rA = __builtin_amdgcn_readlane(r, 0), rB = __builtin_amdgcn_readlane(r, 8);
     if (rA < 0) lamA = 0.0;
     if (rB < 0) lamB = 0.0;
-    const double akkA = fabs(uni_f64(A[kA * LD + kA])), akkB = fabs(uni_f64(B[kB * LD + kB]));
+    const double akkA = fabs(A[kA * LD + kA]), akkB = fabs(B[kB * LD + kB]);
     const bool needA = goA && !(fmax(akkA, lamA) == 0.0 || akkA >= BK_ALPHA * lamA);
     const bool needB = goB && !(fmax(akkB, lamB) == 0.0 || akkB >= BK_ALPHA * lamB);
     int pA = kA, qA = -1, pB = kB, qB = -1;
@@ -1091,12 +1084,12 @@ __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane)
       const double sigA = rl_f64(g8, 0), sigB = rl_f64(g8, 8);
       if (needA) {
         if (akkA * sigA >= BK_ALPHA * lamA * lamA) pA = kA;
-        else if (fabs(uni_f64(A[rA * LD + rA])) >= BK_ALPHA * sigA) pA = rA;
+        else if (fabs(A[rA * LD + rA]) >= BK_ALPHA * sigA) pA = rA;
         else qA = rA;
       }
       if (needB) {
         if (akkB * sigB >= BK_ALPHA * lamB * lamB) pB = kB;
-        else if (fabs(uni_f64(B[rB * LD + rB])) >= BK_ALPHA * sigB) pB = rB;
+        else if (fabs(B[rB * LD + rB]) >= BK_ALPHA * sigB) pB = rB;
         else qB = rB;
       }
     }
@@ -1108,7 +1101,7 @@ __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane)
       unsigned& zero = blk == 0 ? zA : zB;
       const int kk = blk == 0 ? kA : kB, p = blk == 0 ? pA : pB, q = blk == 0 ? qA : qB;
       if (q < 0) {
-        const double d = uni_f64(X[p * LD + p]);
+        const double d = X[p * LD + p];
         done |= 1u << p;
         if (fabs(d) <= ZERO_PIVOT) { in.zero++; zero |= 1u << p; continue; }
         if (d > 0) in.pos++; else in.neg++;
@@ -1118,7 +1111,7 @@ __device__ __noinline__ Inertia bk_sweep2(ldsd* A, ldsd* B, bool twob, int lane)
           X[ti * LD + tj] = (ti == p) ? ((tj == p) ? -rd : apj * rd) : (tj == p) ? aip * rd : aij - aip * apj * rd;
         }
       } else {
-        const double a11 = uni_f64(X[kk * LD + kk]), a21 = uni_f64(X[q * LD + kk]), a22 = uni_f64(X[q * LD + q]);
+        const double a11 = X[kk * LD + kk], a21 = X[q * LD + kk], a22 = X[q * LD + q];
         const double det = a11 * a22 - a21 * a21;
         done |= (1u << kk) | (1u << q);
         if (fabs(det) <= ZERO_PIVOT * ZERO_PIVOT) { in.zero += 2; zero |= (1u << kk) | (1u << q); continue; }

@@ -356,7 +356,7 @@ step_s28() {
 
 step_s29() {
   # r05/s29: the LDS pivot sweep with its pivot values read into SGPRs (uni_f64) against f641ef4's
-  # sweep (rev) on the MHE fleet
+  # sweep (rev) on the MHE fleet.  Run at the next commit after f641ef4; reverted (2 % slower)
   mkdir -p gpurun_out/s29
   MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s29/var_mhe.txt 2>&1
   echo "s29 exit $?"

@@ -493,10 +493,12 @@ def compile_all(verbose: bool = False):
 
     probs = {name: fn()[0].problem for name, fn in variants.items()}
     jobs = int(os.environ.get("MPCX_BUILD_JOBS", "4"))
-    label = {None: "", native.SMALL_FLEET: " small-fleet", native.MID_FLEET: " one-wave-per-SIMD"}
+    label = {None: "", native.SMALL_FLEET: " small-fleet", native.MID_FLEET: " one-wave-per-SIMD",
+             native.WIDE_FLEET: " 20-agents-per-CU"}
     with ThreadPoolExecutor(max_workers=jobs) as ex:  # hipcc processes: one per code object
-        # the one-wave-per-SIMD builds after the main ones (they read the main build's occupancy)
-        for group in ((None, native.SMALL_FLEET), (native.MID_FLEET,)):
+        # the one-wave-per-SIMD and 20-agents-per-CU builds after the main ones (they read the main
+        # build's occupancy)
+        for group in ((None, native.SMALL_FLEET), (native.MID_FLEET, native.WIDE_FLEET)):
             futs = {(name, v): ex.submit(native.compile_model, pr.gen, False, v)
                     for name, pr in probs.items() for v in group}
             for (name, v), fut in futs.items():
@@ -512,7 +514,7 @@ def compile_all(verbose: bool = False):
         gen = cubic_room()[0].problem.gen
         for defines, _cap in FILTER_TEST_BUILDS.values():
             os.environ["MPCX_DEFINES"] = defines
-            for v in (None, native.SMALL_FLEET, native.MID_FLEET):
+            for v in (None, native.SMALL_FLEET, native.MID_FLEET, native.WIDE_FLEET):
                 path = native.compile_model(gen, False, v)
                 if verbose:
                     print(f"[mpcx] cubic_room {defines}{label[v]}: {path.name if path else '-'}")

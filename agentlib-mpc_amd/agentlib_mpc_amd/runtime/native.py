@@ -84,7 +84,7 @@ STATS_BYTES = ctypes.sizeof(Stats)
 EXPORTED_SYMBOLS = [
     "mpcx_version", "mpcx_default_options", "mpcx_problem_create", "mpcx_problem_destroy",
     "mpcx_set_options", "mpcx_reserve", "mpcx_workspace_bytes_per_agent", "mpcx_problem_small_fleet",
-    "mpcx_problem_mid_fleet",
+    "mpcx_problem_mid_fleet", "mpcx_problem_wide_fleet",
     "mpcx_batch_solve", "mpcx_batch_solve_staged", "mpcx_batch_solve_mapped", "mpcx_active_map",
     "mpcx_admm_moments_size", "mpcx_admm_reduce_count", "mpcx_admm_moments", "mpcx_admm_finalize",
     "mpcx_admm_moments_masked", "mpcx_admm_consensus_multipliers_masked", "mpcx_admm_exchange_update_masked",
@@ -190,6 +190,7 @@ def load_library():
         lib.mpcx_workspace_bytes_per_agent.argtypes = [vp]
         lib.mpcx_problem_small_fleet.argtypes = [vp, ctypes.c_char_p, i32]
         lib.mpcx_problem_mid_fleet.argtypes = [vp, ctypes.c_char_p, i32]
+        lib.mpcx_problem_wide_fleet.argtypes = [vp, ctypes.c_char_p, i32]
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
         lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp, vp]
         lib.mpcx_batch_solve_mapped.argtypes = [vp, i32, i32, vp] + [vp] * 9 + [vp, vp]
@@ -262,10 +263,17 @@ def _extra_defines() -> List[str]:
 SMALL_FLEET = "wslds"
 #: mid-fleet variant (one wave per SIMD, up to 512 registers; ``mpcx_problem_mid_fleet``)
 MID_FLEET = "w1"
+#: wide-fleet variant (20 agents per CU where the main build holds 16; ``mpcx_problem_wide_fleet``)
+WIDE_FLEET = "apc20"
+#: largest call-frame scratch (B/lane) a wide build may have: its register budget (96) spills more
+#: than the main build's, and a structure whose stage code needs the registers loses more than
+#: the extra agents per CU give (C4 room 92 B: 4 % faster at 13108 agents; C2 room 740 B)
+WIDE_SCRATCH_MAX = 128
 #: compiler messages of the kernel's own static_asserts that mean "this structure does not fit
 #: the variant" (permanent for the code object's source hash)
 _NOFIT_MESSAGES = ("workspace does not fit LDS", "LDS share per agent exceeded")
-_VARIANT_DEFINES = {None: [], SMALL_FLEET: ["MPCX_WS_LDS"], MID_FLEET: ["MPCX_MIN_WAVES=1"]}
+_VARIANT_DEFINES = {None: [], SMALL_FLEET: ["MPCX_WS_LDS"], MID_FLEET: ["MPCX_MIN_WAVES=1"],
+                    WIDE_FLEET: ["MPCX_APC=20"]}
 
 
 def code_object_path(gen_key: str, variant: Optional[str] = None) -> pathlib.Path:
@@ -286,8 +294,9 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
     nofit = out.with_suffix(".nofit")
     if variant is not None and nofit.exists():
         return None
-    if variant == MID_FLEET:
-        # only where the main build's register budget is tighter than one wave per SIMD
+    if variant in (MID_FLEET, WIDE_FLEET):
+        # MID_FLEET only where the main build's register budget is tighter than one wave per SIMD,
+        # WIDE_FLEET only where the main build holds 16 agents per CU (four waves per SIMD)
         base = compile_model(gen, verbose)
         occ = base.with_suffix(".occ")
         if not occ.exists():
@@ -295,8 +304,11 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
             # marker, so the decision is taken again once the occupancy is known
             warnings.warn(f"occupancy of {base.name} unknown; no one-wave-per-SIMD build this time")
             return None
-        if int(occ.read_text() or "1") <= 1:
+        if variant == MID_FLEET and int(occ.read_text() or "1") <= 1:
             nofit.write_text("the main build already runs one wave per SIMD")
+            return None
+        if variant == WIDE_FLEET and int(occ.read_text() or "0") != 4:
+            nofit.write_text("the main build does not hold 16 agents per CU")
             return None
     src = out.with_suffix(".hip")
     src.write_text(gen.source)
@@ -315,7 +327,8 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
             if any(m in res.stderr for m in _NOFIT_MESSAGES):
                 nofit.write_text(res.stderr[-4000:])
             else:
-                name = {SMALL_FLEET: "small-fleet", MID_FLEET: "one-wave-per-SIMD"}.get(variant, variant)
+                name = {SMALL_FLEET: "small-fleet", MID_FLEET: "one-wave-per-SIMD",
+                        WIDE_FLEET: "20-agents-per-CU"}.get(variant, variant)
                 warnings.warn(f"{name} build of {gen.key} failed; the main build serves every batch:\n"
                               f"{res.stderr[-800:]}")
             tmp.unlink(missing_ok=True)
@@ -329,6 +342,16 @@ def compile_model(gen, verbose: bool = False, variant: Optional[str] = None) -> 
             out.with_suffix(".occ").write_text(occ.group(1))
         else:  # remark format changed: leave the decision open rather than never building w1
             warnings.warn(f"no occupancy remark for mpcx_ipm_solve in the build of {out.name}")
+    if variant == WIDE_FLEET:
+        scr = re.search(r"Function Name: mpcx_ipm_solve.*?ScratchSize \[bytes/lane\]: (\d+)", res.stderr, re.S)
+        if scr is None or int(scr.group(1)) > WIDE_SCRATCH_MAX:
+            # permanent for this source hash when measured; an unreadable remark is retried
+            if scr is not None:
+                nofit.write_text(f"scratch {scr.group(1)} B/lane > {WIDE_SCRATCH_MAX}")
+            else:
+                warnings.warn(f"no scratch remark for mpcx_ipm_solve in the build of {out.name}")
+            tmp.unlink(missing_ok=True)
+            return None
     os.replace(tmp, out)
     return out
 
@@ -371,6 +394,17 @@ class NativeProblem:
                     warnings.warn(f"mpcx_problem_mid_fleet failed ({rc}) for {mp}; using the main build")
                 else:
                     self.mid_fleet_path = mp
+        self.wide_fleet_path = None
+        if hsaco is None and os.environ.get("MPCX_WIDE_FLEET", "1") != "0":
+            # fleets of more than two generations of a 16-agents-per-CU main build run the
+            # 20-agents-per-CU build where its spills stay small
+            wp = compile_model(gen, variant=WIDE_FLEET)
+            if wp is not None:
+                rc = self.lib.mpcx_problem_wide_fleet(handle, str(wp).encode(), -1)
+                if rc != 0:  # optional, as the other builds
+                    warnings.warn(f"mpcx_problem_wide_fleet failed ({rc}) for {wp}; using the main build")
+                else:
+                    self.wide_fleet_path = wp
         self.options = default_options()
         self.nw = d["NX"] + d["N"] * (d["NV"] + d["NX"])
         self.ng_total = d["N"] * d["NG"]
@@ -408,6 +442,13 @@ class NativeProblem:
         rc = self.lib.mpcx_problem_mid_fleet(self.handle, None, int(max_agents))
         if rc != 0:
             raise NativeError(f"mpcx_problem_mid_fleet failed ({rc})")
+
+    def set_wide_fleet_min(self, min_agents: int):
+        """Smallest batch launched on the 20-agents-per-CU build: -1 more than two generations of
+        the main build (default), 0 never."""
+        rc = self.lib.mpcx_problem_wide_fleet(self.handle, None, int(min_agents))
+        if rc != 0:
+            raise NativeError(f"mpcx_problem_wide_fleet failed ({rc})")
 
     def workspace_bytes_per_agent(self) -> int:
         return int(self.lib.mpcx_workspace_bytes_per_agent(self.handle))

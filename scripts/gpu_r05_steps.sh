@@ -362,6 +362,25 @@ step_s29() {
   echo "s29 exit $?"
 }
 
+step_s30() {
+  # r05/s30: the 20-agents-per-CU build of the C4 room against the default (16 per CU) over fleet
+  # sizes from 1 to 6 generations of the default build on 256 CUs
+  mkdir -p gpurun_out/s30
+  for n in 4096 6144 8192 9216 10240 12288 13108 16384 20480 24576; do
+    echo "AGENTS $n" >> gpurun_out/s30/var_c4room_sizes.txt
+    MODEL=exchange_room AGENTS=$n timeout -k 10 200 python -u scripts/variants.py run base apc20 base apc20 >> gpurun_out/s30/var_c4room_sizes.txt 2>&1 || exit $?
+  done
+  echo "s30 exit $?"
+}
+
+step_s31() {
+  # r05/s31: the GPU parity suite and smoke with the 20-agents-per-CU build (C ABI v13)
+  mkdir -p gpurun_out/s31
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s31/gpu_tests.txt 2>&1 || exit $?
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s31/smoke.txt 2>&1
+  echo "s31 exit $?"
+}
+
 step_rec() {
   # r05 record on the current tree ($OUT, default profiles/r05/rec): PMC passes of the C3 leg, the
   # default bench line (every leg + CPU baselines), kernel-trace stats of the C3 / MHE / NARX legs,

@@ -40,14 +40,16 @@ def _oracle(case, opts=None, key=None):
     return ref
 
 
-#: the three code objects of every structure, by the batch size that selects them
+#: the code objects of every structure, by the batch size that selects them
 #: (`mpcx_runtime.cpp` mpcx_batch_solve): "lds" the small-fleet build (workspace in LDS, at most
 #: one agent per CU), "mid" the one-wave-per-SIMD build (at most four agents per CU, only where
 #: the main build runs more waves), "main" the LDS-limited-occupancy build (every larger fleet:
-#: the C3 bench fleet, the C2 / C4 room classes).  Every parity case below runs on each build that
-#: exists for its structure: the limits of BOTH optional builds are set, so
-#: the build named is the one that runs whatever the batch size.
-BUILDS = ["lds", "mid", "main"]
+#: the C3 bench fleet, the C2 / C4 room classes), "wide" the 20-agents-per-CU build (fleets of more
+#: than two generations of a 16-per-CU main build, where its spills stay small: the C4 rooms).
+#: Every parity case below runs on each build that exists for its structure:
+#: the limits of ALL optional builds are set, so the build named is the one that runs whatever
+#: the batch size.
+BUILDS = ["lds", "mid", "main", "wide"]
 
 
 def select_build(native, build):
@@ -56,13 +58,17 @@ def select_build(native, build):
         pytest.skip("no small-fleet build for this structure")
     if build == "mid" and native.mid_fleet_path is None:
         pytest.skip("no one-wave-per-SIMD build for this structure (its main build runs one wave per SIMD)")
+    if build == "wide" and native.wide_fleet_path is None:
+        pytest.skip("no 20-agents-per-CU build for this structure")
     native.set_small_fleet_max(1 << 30 if build == "lds" else 0)
     native.set_mid_fleet_max(1 << 30 if build == "mid" else 0)
+    native.set_wide_fleet_min(1 if build == "wide" else 0)
 
 
 def reset_builds(native):
     native.set_small_fleet_max(-1)
     native.set_mid_fleet_max(-1)
+    native.set_wide_fleet_min(-1)
 
 
 def _gpu_solve(case, n_copies=1, build="lds"):
@@ -440,6 +446,51 @@ def test_gpu_c3_fleet_matches_c_oracle(n, build):
     np.testing.assert_allclose([s["obj"] for s, o in zip(gs, ok) if o], [s["obj"] for s, o in zip(cs, ok) if o],
                                rtol=RTOL_OBJ)
     np.testing.assert_allclose(gw[ok], cw[ok], rtol=RTOL_TRAJ, atol=1e-7 * 300.0)
+
+
+def test_gpu_wide_build_takes_large_c4_room_fleets():
+    """The 20-agents-per-CU build (``mpcx_problem_wide_fleet``, C ABI v13) on a C4 room fleet one
+    agent past two generations of the main build (2 x 16 x CUs + 1; the bench's C4 classes are
+    13108 rooms): the default routing launches it (bit-identical to the run forced onto it), and
+    against the main build every agent has the same status and iteration count and the same
+    solution (same operations; the tighter register budget only moves values through scratch, the
+    compiler may contract a few products into FMAs differently)."""
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+
+    be, cv = bm.exchange_room(solver_options=bm.REFERENCE)
+    native = be._native()
+    if native.wide_fleet_path is None:
+        pytest.fail("exchange_room's main build holds 16 agents per CU: the 20-per-CU build must load")
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 2 * 16 * cus + 1
+    rng = np.random.default_rng(20261018)
+    vals = {"T": cv["T"].value + rng.uniform(-2.0, 3.0, n),
+            "admm_exchange_lambda_mDot_out": rng.uniform(-20.0, 20.0, n)}
+    p, lbw, ubw, w0 = be.problem.to_kernel(*fleet_nlp_inputs(be.problem, cv, vals))
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    tp, tl, tu = T(p), T(lbw), T(ubw)
+    out = {}
+    for mode in ("default", "wide", "main"):
+        if mode != "default":
+            select_build(native, mode)
+        tw = T(w0)
+        st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device="cuda")
+        try:
+            native.solve(tp, tl, tu, tw, stats=st)
+            torch.cuda.synchronize()
+        finally:
+            reset_builds(native)
+        out[mode] = (tw.cpu().numpy(), stats_to_dicts(st.cpu().numpy().tobytes()))
+    (wd, sd), (ww, sw), (wm, sm) = out["default"], out["wide"], out["main"]
+    np.testing.assert_array_equal(wd, ww)
+    assert [s["iter_count"] for s in sd] == [s["iter_count"] for s in sw]
+    assert [s["status"] for s in sw] == [s["status"] for s in sm]
+    assert [s["iter_count"] for s in sw] == [s["iter_count"] for s in sm]
+    assert np.mean([s["success"] for s in sw]) > 0.99
+    np.testing.assert_allclose([s["obj"] for s in sw], [s["obj"] for s in sm], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(ww, wm, rtol=1e-8, atol=1e-10)
 
 
 def test_gpu_small_fleet_build_matches_hbm_build():

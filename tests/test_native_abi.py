@@ -28,7 +28,7 @@ def test_library_builds_loads_and_exports_all_symbols():
     lib = ctypes.CDLL(str(path))
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.mpcx_version() == 12
+    assert lib.mpcx_version() == 13
 
 
 def test_struct_sizes_match_header():

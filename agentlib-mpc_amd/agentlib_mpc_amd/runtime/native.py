@@ -396,7 +396,7 @@ class NativeProblem:
                     self.mid_fleet_path = mp
         self.wide_fleet_path = None
         if hsaco is None and os.environ.get("MPCX_WIDE_FLEET", "1") != "0":
-            # fleets of more than two generations of a 16-agents-per-CU main build run the
+            # fleets of more than one generation of a 16-agents-per-CU main build run the
             # 20-agents-per-CU build where its spills stay small
             wp = compile_model(gen, variant=WIDE_FLEET)
             if wp is not None:
@@ -444,7 +444,7 @@ class NativeProblem:
             raise NativeError(f"mpcx_problem_mid_fleet failed ({rc})")
 
     def set_wide_fleet_min(self, min_agents: int):
-        """Smallest batch launched on the 20-agents-per-CU build: -1 more than two generations of
+        """Smallest batch launched on the 20-agents-per-CU build: -1 more than one generation of
         the main build (default), 0 never."""
         rc = self.lib.mpcx_problem_wide_fleet(self.handle, None, int(min_agents))
         if rc != 0:

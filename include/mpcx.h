@@ -169,8 +169,8 @@ int mpcx_problem_mid_fleet(mpcx_handle* h, const char* code_object_path, int32_t
 /* Optional (C ABI v13): the same structure compiled for more agents per CU than the main build
  * holds (MPCX_APC=20 where the main build holds 16: a smaller LDS share and register budget per
  * agent).  mpcx_batch_solve launches it for batches of at least min_agents agents that neither
- * the small-fleet nor the one-wave-per-SIMD build takes (min_agents < 0: more than two
- * generations of the main build, 2 x its agents per CU x the CU count; 0: never).  Returns
+ * the small-fleet nor the one-wave-per-SIMD build takes (min_agents < 0: more than one
+ * generation of the main build, its agents per CU x the CU count; 0: never).  Returns
  * MPCX_ERR_MODULE if the code object is not such a variant (HBM workspace, same workspace, more
  * agents per CU than the main build). */
 int mpcx_problem_wide_fleet(mpcx_handle* h, const char* code_object_path, int32_t min_agents);

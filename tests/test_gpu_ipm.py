@@ -45,7 +45,7 @@ def _oracle(case, opts=None, key=None):
 #: one agent per CU), "mid" the one-wave-per-SIMD build (at most four agents per CU, only where
 #: the main build runs more waves), "main" the LDS-limited-occupancy build (every larger fleet:
 #: the C3 bench fleet, the C2 / C4 room classes), "wide" the 20-agents-per-CU build (fleets of more
-#: than two generations of a 16-per-CU main build, where its spills stay small: the C4 rooms).
+#: than one generation of a 16-per-CU main build, where its spills stay small: the C4 rooms).
 #: Every parity case below runs on each build that exists for its structure:
 #: the limits of ALL optional builds are set, so the build named is the one that runs whatever
 #: the batch size.
@@ -449,8 +449,8 @@ def test_gpu_c3_fleet_matches_c_oracle(n, build):
 
 
 def test_gpu_wide_build_takes_large_c4_room_fleets():
-    """The 20-agents-per-CU build (``mpcx_problem_wide_fleet``, C ABI v13) on a C4 room fleet one
-    agent past two generations of the main build (2 x 16 x CUs + 1; the bench's C4 classes are
+    """The 20-agents-per-CU build (``mpcx_problem_wide_fleet``, C ABI v13) on a C4 room fleet of
+    two generations of the main build plus one agent (2 x 16 x CUs + 1; the bench's C4 classes are
     13108 rooms): the default routing launches it (bit-identical to the run forced onto it), and
     against the main build every agent has the same status and iteration count and the same
     solution (same operations; the tighter register budget only moves values through scratch, the

@@ -205,9 +205,6 @@ class _BlockRecords(Sequence):
 _DEBUG = os.environ.get("MPCX_FLEET_DEBUG", "0") == "1"
 
 
-_DEBUG = os.environ.get("MPCX_FLEET_DEBUG", "0") == "1"
-
-
 class ADMMFleet:
     """Device-resident ADMM over fleets of agents (one or more classes).
 
@@ -228,12 +225,18 @@ class ADMMFleet:
         self.ops = ops
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.dist = None
+        self.collective = None
         if comm is not None:
             import torch.distributed as dist
 
             self.dist = dist
             self.group = None if comm == "default" else comm
             self.world = dist.get_world_size(self.group)
+            if self.world > 1:
+                # the iteration's one all-reduce goes through the C ABI (mpcx_admm_allreduce, v14)
+                from agentlib_mpc_amd.runtime.collective import Collective
+
+                self.collective = Collective(dist, self.group, self.device)
         else:
             self.world = 1
         T = {c.T for c in self.classes}
@@ -414,6 +417,8 @@ class ADMMFleet:
         self.MOM = self.MOMBUF[ADMM_CONTROL:]
         self.totals_off = self.n_global * self.S
         self.reduce_len = admm_reduce_count(self.n_global, self.n_global_blocks, T) if self.world > 1 else 0
+        if self.collective is not None:
+            self.collective.bind(self.MOMBUF)
         #: all-reduces issued (the one collective per ADMM iteration; tests count them)
         self.n_collectives = 0
         # per-block coordinator state on the device: penalty, group freeze mask
@@ -605,19 +610,25 @@ class ADMMFleet:
             # converged solves and restoration calls: one launch per class (mpcx_stats_count)
             ops.stats_count(c.n, c.ST, c.ACTIVE if self._masked else None, self._counts)
 
-    def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False):
+    def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False,
+                      keep_control: bool = False):
         """Mean (+ exchange diffs) from the current locals; with ``apply_multipliers``
         also the multiplier update.  Returns the residual totals [n_blocks][8] (device).
         ``per_block``: per-group penalties and freeze masks of the coordinated run.  With
         several ranks every call is the iteration's one all-reduce (every rank calls it the
-        same number of times: the ranks iterate in lockstep)."""
+        same number of times: the ranks iterate in lockstep).  ``keep_control``: the control
+        double holds this rank's count of active blocks (written by the stopping test of the
+        coordinated loop) and is summed with the moments; otherwise it is zeroed with them, so
+        a reduce outside that loop never sums a stale count (it would grow by a factor of the
+        world size per call)."""
         ops, T, G, nb = self.ops, self.T, self.G, self.n_blocks
         if G == 0 and self.world == 1:
             return None
         rho_g = self.RHO_G if per_block else None
         act_g = self.ACTIVE_G if per_block and self._masked else None
         blk = self.BLOCK_G if nb > 1 else None
-        self.MOM.zero_()  # the moments buffer only: the control double keeps its value
+        # the moments buffer, and the control double unless the stopping test just wrote it
+        (self.MOM if keep_control else self.MOMBUF).zero_()
         totals = self.MOM[self.totals_off:self.totals_off + ADMM_TOTALS * nb]
         exch = self.EXCH if self.exchange_flags.any() else None
         gm = self.GMULT if exch is not None else None
@@ -626,8 +637,8 @@ class ADMMFleet:
                         self.MOM, row_on=self.ROW_ON)
             ops.finalize(self.n_global, G, self.n_global, nb, T, self.MOM, exch, gm, rho, rho_g, act_g, blk,
                          self.MEAN, self.DMEAN, totals)
-        if self.world > 1:
-            self.dist.all_reduce(self.MOMBUF[:self.reduce_len], group=self.group)
+        if self.world > 1:  # the one collective, issued by the library (mpcx_admm_allreduce)
+            self.collective.allreduce(self.reduce_len)
             self.n_collectives += 1
         if G == 0:
             return None
@@ -805,7 +816,7 @@ class ADMMFleet:
             self._solve_all(rho0)
             # ranks iterate in lockstep (the loop exit below is agreed on), so every rank takes
             # part in every iteration's all-reduce; frozen groups' moments travel but are not used
-            tot = self._update_means(rho0, apply_multipliers=True, per_block=True)
+            tot = self._update_means(rho0, apply_multipliers=True, per_block=True, keep_control=multi)
             executed = it
             if multi and it > 1 and (it - 1) % every == 0:
                 left = float(self.CONTROL.item())  # the count over all ranks after iteration it - 1

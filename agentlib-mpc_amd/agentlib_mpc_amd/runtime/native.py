@@ -92,10 +92,18 @@ EXPORTED_SYMBOLS = [
     "mpcx_gather_rows", "mpcx_scatter_rows", "mpcx_fill_column",
     "mpcx_admm_block_stop", "mpcx_admm_block_expand", "mpcx_device_clock_khz", "mpcx_stats_count",
     "mpcx_scatter_rows_multi", "mpcx_gather_rows_multi",
+    "mpcx_allreduce_register", "mpcx_allreduce_register_fn", "mpcx_allreduce_unregister", "mpcx_allreduce_kind",
+    "mpcx_admm_allreduce", "mpcx_allreduce_calls", "mpcx_rccl_unique_id", "mpcx_rccl_comm_init",
+    "mpcx_rccl_comm_init_file", "mpcx_rccl_comm_destroy",
 ]
 MOVE_DESC = 4  # MPCX_MOVE_DESC: int64 words per descriptor of the fused row moves (C ABI v12)
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
 ADMM_CONTROL = 1  # MPCX_ADMM_CONTROL: control doubles before the moments buffer (C ABI v10)
+RCCL_ID_BYTES = 128  # MPCX_RCCL_ID_BYTES
+COLLECTIVE_NONE, COLLECTIVE_RCCL, COLLECTIVE_FN = 0, 1, 2  # mpcx_allreduce_kind
+ERR_ARG, ERR_COMM = -1, -6  # MPCX_ERR_ARG, MPCX_ERR_COMM
+#: mpcx_allreduce_fn: int (*)(void* ctx, double* buf, int64_t count, void* stream)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 KERNEL_ABI = 8  # MPCX_KERNEL_ABI (csrc/mpcx_internal.h)
 
 _lib = None
@@ -112,7 +120,7 @@ def _hipcc() -> str:
 def build_library(force: bool = False) -> pathlib.Path:
     """Compile libmpcx.so (host runtime + ADMM kernels) for gfx950, in-tree."""
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
-    srcs = [CSRC / "mpcx_runtime.cpp", CSRC / "admm_kernels.hip"]
+    srcs = [CSRC / "mpcx_runtime.cpp", CSRC / "admm_kernels.hip", CSRC / "mpcx_collective.cpp"]
     deps = srcs + [INCLUDE / "mpcx.h", CSRC / "mpcx_internal.h"]
     if LIB_PATH.exists() and not force:
         if LIB_PATH.stat().st_mtime >= max(p.stat().st_mtime for p in deps):
@@ -120,7 +128,7 @@ def build_library(force: bool = False) -> pathlib.Path:
     tmp = LIB_PATH.with_suffix(".so.tmp")
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}", "-O3", "-std=c++17",
            "-Wno-unused-result", "-Wno-unused-value", f"-I{INCLUDE}", f"-I{CSRC}",
-           *map(str, srcs), "-o", str(tmp)]
+           *map(str, srcs), "-ldl", "-o", str(tmp)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise NativeError(f"building libmpcx.so failed:\n{res.stderr[-4000:]}")
@@ -222,6 +230,15 @@ def load_library():
         lib.mpcx_admm_block_expand.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp]
         lib.mpcx_device_clock_khz.restype = i64
         lib.mpcx_stats_count.argtypes = [i32, vp, vp, vp, vp]
+        # the collective of an ADMM iteration (C ABI v14, runtime/collective.py)
+        lib.mpcx_allreduce_register.argtypes = [vp, ctypes.c_char_p]
+        lib.mpcx_allreduce_register_fn.argtypes = [ALLREDUCE_FN, vp]
+        lib.mpcx_admm_allreduce.argtypes = [vp, i64, vp]
+        lib.mpcx_allreduce_calls.restype = i64
+        lib.mpcx_rccl_unique_id.argtypes = [ctypes.c_char_p, vp]
+        lib.mpcx_rccl_comm_init.argtypes = [ctypes.c_char_p, i32, i32, vp, ctypes.POINTER(vp)]
+        lib.mpcx_rccl_comm_init_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i32, i32, i32, ctypes.POINTER(vp)]
+        lib.mpcx_rccl_comm_destroy.argtypes = [ctypes.c_char_p, vp]
         for name in EXPORTED_SYMBOLS:
             getattr(lib, name)  # raises AttributeError if a symbol is missing
         _lib = lib

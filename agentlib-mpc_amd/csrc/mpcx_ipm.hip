@@ -454,6 +454,9 @@ struct LdsRest {
   // convention passes in VGPRs, callee-saved -- spilled to scratch -- when live across a call
   // (the kernarg segment pointer itself is not an implicit input of called functions)
   unsigned long long kp_bits, ws_bits;
+#ifdef MPCX_TRACE_LS
+  int trace_agent;         // the agent this workgroup solves (mapped launches: not blockIdx.x)
+#endif
 #ifdef MPCX_PROFILE
   double sprof[10];  // 0-3 factor, 4-5 solve, 6-9 iteration head (profile build)
   unsigned int dense_seen[2];  // stages ever rejected by the static plan (profile build)
@@ -592,7 +595,7 @@ __device__ __forceinline__ cdbl* cold_base() { return (cdbl*)uni64(gL.ws_bits); 
 #define TRACE_LS_HEAD(argp)                                                                      \
   do {                                                                                           \
     if (lane_now() == 0 && (*argp).lam_w != nullptr) {                                           \
-      gdbl* h = (gdbl*)(*argp).lam_w + (long)blockIdx.x * NW;                                    \
+      gdbl* h = (gdbl*)(*argp).lam_w + (long)gL.trace_agent * NW;                                \
       const double hv[8] = {K.st.theta, K.fx - K.mu * K.st.barrier, K.st.gphid, K.amin,          \
                             K.theta_min, K.theta_max, K.mu, (double)K.nfilt};                    \
       for (int q = 0; q < 8 && q < NW; ++q) h[q] = hv[q];                                        \
@@ -604,7 +607,7 @@ __device__ __forceinline__ cdbl* cold_base() { return (cdbl*)uni64(gL.ws_bits); 
   do {                                                                                           \
     const int t_ = K.ls.trials - 1;                                                              \
     if (lane_now() == 0 && (*argp).lam_g != nullptr && 6 * t_ + 5 < M) {                         \
-      gdbl* g = (gdbl*)(*argp).lam_g + (long)blockIdx.x * M + 6 * t_;                            \
+      gdbl* g = (gdbl*)(*argp).lam_g + (long)gL.trace_agent * M + 6 * t_;                        \
       g[0] = (alpha); g[1] = (tr).theta; g[2] = (tr).phi; g[3] = (okf); g[4] = (okt); g[5] = (ft); \
     }                                                                                            \
   } while (0)
@@ -2631,7 +2634,20 @@ __device__ __noinline__ void ls_mult_finish(const Agent a, const double constr_m
 struct RatioMin {
   double n = 1.0, d = 1.0;  // the default step size 1
   __device__ __forceinline__ void take(double num, double den) {
-    if (num * d < n * den) { n = num; d = den; }
+    const double l = num * d, r = n * den;
+    // the cross products leave the normal range only for extreme slacks / step components (the
+    // ill-conditioned restoration cases): there the quotients are compared, as fmin(num / den) did
+    // (a branch of its own, kept from being if-converted by the empty volatile asm: the divisions
+    // run only when a lane needs them)
+    const bool exact = __builtin_isnormal(l) && __builtin_isnormal(r);  // v_cmp_class each
+    bool lt;
+    if (__builtin_expect(exact, 1)) {
+      lt = l < r;
+    } else {
+      asm volatile("");
+      lt = num / den < n / d;
+    }
+    if (lt) { n = num; d = den; }
   }
   __device__ __forceinline__ double value() const { return n / d; }
 };
@@ -4130,6 +4146,9 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
   if (lane == 0) {
     gL.kp_bits = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
     gL.ws_bits = (unsigned long long)((gdbl*)args.ws + (long)agent * args.ws_stride);
+#ifdef MPCX_TRACE_LS
+    gL.trace_agent = agent;
+#endif
   }
   wsync();
   KState& K = gL.ks;

@@ -29,6 +29,10 @@
  *                         <- ExchangeVariable.update_diff_trajectories / update_multiplier
  *                            (admm_datatypes.py:292-324), admm.py:550-570, 635-655
  *   mpcx_admm_shift       <- shift_values_by_one (admm_datatypes.py:275-282, 326-331)
+ *   mpcx_admm_allreduce (+ mpcx_allreduce_register)
+ *                         <- the coordinator's gather of the locals and broadcast of the means
+ *                            (modules/dmpc/admm/admm_coordinator.py:284-314) across GPUs: ONE
+ *                            RCCL all-reduce per ADMM iteration, issued by the library (v14)
  *   mpcx_gather_rows / mpcx_scatter_rows / mpcx_fill_column
  *                         <- moving coupling trajectories between Results and the
  *                            coordinator messages (modules/dmpc/admm/admm_coordinated.py:133-193)
@@ -48,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 13
+#define MPCX_API_VERSION 14
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -393,6 +397,44 @@ int mpcx_scatter_rows_multi(int32_t n_agents, int32_t n_desc, const int64_t* des
                             int64_t dst_ld, void* stream);
 int mpcx_gather_rows_multi(int32_t n_agents, int32_t n_desc, const int64_t* desc, int32_t max_T,
                            const double* src, int64_t src_ld, void* stream);
+
+/* ---- the collective of an ADMM iteration, issued by the library (C ABI v14) -----------------
+ * SURVEY §8b `mpcx_allreduce_register(comm)`: the one all-reduce per ADMM iteration (sum, fp64, in
+ * place, mpcx_admm_reduce_count doubles from the control on; see MPCX_ADMM_CONTROL) goes through
+ * mpcx_admm_allreduce, which issues it on the registered transport.  It replaces the exchange of
+ * the reference coordinator's round (modules/dmpc/admm/admm_coordinator.py:284-314: every agent's
+ * locals gathered, the means sent back) when the fleet's agents sit on several GPUs.  One transport
+ * per process (one process per GPU), registered before the loop:
+ *   mpcx_allreduce_register(comm, rccl_library): an RCCL communicator (ncclComm_t).  RCCL is loaded
+ *     with dlopen (an already loaded copy first: a communicator must be used with the library that
+ *     created it; NULL = "librccl.so.1") and ncclAllReduce runs on the `stream` of each call.
+ *   mpcx_allreduce_register_fn(fn, ctx): any other transport; fn(ctx, buf, count, stream) sums
+ *     `count` doubles at `buf` over the ranks in place and returns 0.
+ * mpcx_rccl_comm_init (unique id from mpcx_rccl_unique_id on rank 0, passed to every rank by the
+ * caller) or mpcx_rccl_comm_init_file (rank 0 writes the id to `id_path` -- a path no earlier run
+ * left behind --, the other ranks read it, waiting up to timeout_ms) make the communicator, so a C
+ * caller needs no collective library of its own. */
+#define MPCX_ERR_COMM (-6)
+#define MPCX_RCCL_ID_BYTES 128
+#define MPCX_COLLECTIVE_NONE 0
+#define MPCX_COLLECTIVE_RCCL 1
+#define MPCX_COLLECTIVE_FN 2
+typedef int (*mpcx_allreduce_fn)(void* ctx, double* buf, int64_t count, void* stream);
+int mpcx_allreduce_register(void* comm, const char* rccl_library);
+int mpcx_allreduce_register_fn(mpcx_allreduce_fn fn, void* ctx);
+int mpcx_allreduce_unregister(void);
+/* the registered transport: MPCX_COLLECTIVE_NONE / _RCCL / _FN */
+int mpcx_allreduce_kind(void);
+/* sum `count` doubles at `buf` over the ranks, in place, stream-ordered (MPCX_ERR_COMM when no
+ * transport is registered or it failed) */
+int mpcx_admm_allreduce(double* buf, int64_t count, void* stream);
+/* collectives issued through mpcx_admm_allreduce since the library was loaded */
+int64_t mpcx_allreduce_calls(void);
+int mpcx_rccl_unique_id(const char* rccl_library, void* id /* MPCX_RCCL_ID_BYTES */);
+int mpcx_rccl_comm_init(const char* rccl_library, int32_t nranks, int32_t rank, const void* id, void** comm);
+int mpcx_rccl_comm_init_file(const char* rccl_library, const char* id_path, int32_t nranks, int32_t rank,
+                             int32_t timeout_ms, void** comm);
+int mpcx_rccl_comm_destroy(const char* rccl_library, void* comm);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,31 @@
+# Round-6 measurement steps, one function per step (the profiles/r06/<step> directories name them).
+# Each step runs its GPU commands under their own time limits and stops at the first failure.
+# usage (on the GPU box, via gpurun):  bash scripts/gpu_r06_steps.sh <step>   e.g. s1
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+
+pmc_calib() {  # $1 = output dir: FETCH_SIZE / WRITE_SIZE of the known-bytes kernels (scripts/fetch_calib.hip)
+  local o=$1
+  timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d $o/calib_fetch -o run --output-format csv -- ./scripts/bin/fetch_calib 2 > $o/calib_fetch.out 2>&1 || return $?
+  timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d $o/calib_write -o run --output-format csv -- ./scripts/bin/fetch_calib 2 > $o/calib_write.out 2>&1 || return $?
+  timeout -s KILL 60 rocprofv3 --kernel-trace --stats -d $o/calib_trace -o run --output-format csv -- ./scripts/bin/fetch_calib 2 > $o/calib_trace.out 2>&1
+}
+
+step_s1() {
+  # r06/s1: the RatioMin overflow fallback A/B (C3 4096 agents, tol 1e-8 runs: working tree vs HEAD);
+  # the GPU suite with the collective through the C ABI (RCCL one-rank test), the wide build's
+  # bench-size oracle test; smoke; FETCH_SIZE calibration; the default bench line
+  mkdir -p gpurun_out/s1
+  REV=HEAD timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s1/var_c3.txt 2>&1 || exit $?
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s1/gpu_tests.txt 2>&1
+  rc=$?
+  [ $rc -ne 0 ] && [ $rc -ne 1 ] && { echo "tests exit $rc"; exit $rc; }
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s1/smoke.txt 2>&1 || exit $?
+  pmc_calib gpurun_out/s1 || exit $?
+  timeout -k 10 900 python -u bench.py > gpurun_out/s1/bench.json 2> gpurun_out/s1/bench.err
+  echo "tests exit $rc, bench exit $?"
+}
+
+fn="step_$1"
+declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }
+"$fn"

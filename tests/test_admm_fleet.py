@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 
 from agentlib_mpc_amd import benchmarks as bm
 from agentlib_mpc_amd.admm.fleet import ADMMFleet
-from agentlib_mpc_amd.runtime import native
+from agentlib_mpc_amd.runtime import collective, native
 from oracle import admm as oadmm
 from oracle import nlps
 from tests.admm_cases import C2Oracle, C4Oracle, participation_rounds
@@ -443,6 +443,10 @@ def _mixed_worker(rank, world, init_file, out_file, tols=(1e-12, 1e-12), iter_ma
         real = dist.all_reduce
         if world > 1:   # count every collective the round issues
             dist.all_reduce = lambda *a, **k: (calls.append(a[0].numel()), real(*a, **k))[1]
+            # the collective goes through the C ABI (mpcx_admm_allreduce, v14): the library's own
+            # count of the collectives it issued, its transport the registered function (gloo)
+            lib0 = collective.calls()
+            assert collective.kind() == native.COLLECTIVE_FN
         try:
             out = fl.run_coordinated(1.0, admm_iter_max=iter_max, use_relative_tolerances=False,
                                      primal_tol=tols[0], dual_tol=tols[1], check_every=check_every)
@@ -452,6 +456,7 @@ def _mixed_worker(rank, world, init_file, out_file, tols=(1e-12, 1e-12), iter_ma
             # ONE all-reduce per ADMM iteration executed (plus the round's initial mean update),
             # each of the same length: no second collective for the loop exit
             assert len(calls) == out["collectives"] == 1 + out["iterations_executed"], (calls, out)
+            assert collective.calls() - lib0 == len(calls), (collective.calls() - lib0, calls)
             assert set(calls) == {fl.reduce_len}, calls
             assert out["iterations_executed"] - out["loop_iterations"] <= 1
         xb = fl.block_index("mDot_coupling")

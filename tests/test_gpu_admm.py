@@ -679,3 +679,50 @@ def test_gpu_fused_moves_match_one_launch_per_move(monkeypatch):
         np.testing.assert_array_equal(tf[al], tu[al])
     for al in etf:
         np.testing.assert_array_equal(etf[al], etu[al])
+
+
+def test_gpu_collective_rccl_transport_one_rank(tmp_path):
+    """C ABI v14 on the GPU: the ADMM iteration's all-reduce issued by the library on an
+    RCCL communicator.  One rank (the box has one GPU; a communicator's ranks must sit on distinct
+    GPUs): (1) the fleet driver's path -- a one-rank ``nccl`` process group, the library's own
+    communicator made from PyTorch's loaded RCCL (``runtime/collective.py``), the sum over one rank
+    leaves the buffer as it is and the library counts the call; (2) a C caller's path --
+    ``mpcx_rccl_comm_init_file`` (shared-file bootstrap of the unique id), ``mpcx_allreduce_register``,
+    ``mpcx_admm_allreduce`` on a HIP stream, ``mpcx_rccl_comm_destroy``."""
+    import ctypes
+    import torch.distributed as dist
+
+    from agentlib_mpc_amd.runtime import collective, native
+
+    lib = native.load_library()
+    dist.init_process_group("nccl", init_method=f"file://{tmp_path / 'pg'}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        coll = collective.Collective(dist, None, torch.device("cuda"))
+        assert coll.kind == "rccl" and collective.kind() == native.COLLECTIVE_RCCL
+        buf = torch.arange(1.0, 41.0, dtype=torch.float64, device="cuda")
+        coll.bind(buf)
+        c0 = collective.calls()
+        for _ in range(5):
+            coll.allreduce(33)
+        torch.cuda.synchronize()
+        assert collective.calls() - c0 == 5
+        np.testing.assert_array_equal(buf.cpu().numpy(), np.arange(1.0, 41.0))
+    finally:
+        lib.mpcx_allreduce_unregister()
+        dist.destroy_process_group()
+    path = collective.loaded_rccl_path()
+    cpath = path.encode() if path else None
+    comm = ctypes.c_void_p()
+    assert lib.mpcx_rccl_comm_init_file(cpath, str(tmp_path / "rccl_id").encode(), 1, 0, 10000, ctypes.byref(comm)) == 0
+    try:
+        assert lib.mpcx_allreduce_register(comm, cpath) == 0
+        x = torch.full((17,), 2.5, dtype=torch.float64, device="cuda")
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            assert lib.mpcx_admm_allreduce(ctypes.c_void_p(x.data_ptr()), 17, ctypes.c_void_p(s.cuda_stream)) == 0
+        s.synchronize()
+        np.testing.assert_array_equal(x.cpu().numpy(), np.full(17, 2.5))
+    finally:
+        assert lib.mpcx_rccl_comm_destroy(cpath, comm) == 0
+    assert lib.mpcx_allreduce_kind() == native.COLLECTIVE_NONE

@@ -493,6 +493,49 @@ def test_gpu_wide_build_takes_large_c4_room_fleets():
     np.testing.assert_allclose(ww, wm, rtol=1e-8, atol=1e-10)
 
 
+def test_gpu_wide_build_c4_room_fleet_matches_c_oracle():
+    """Bench-size parity of the 20-agents-per-CU build: a C4 room fleet of
+    two generations of the main build plus one agent (2 x 16 x CUs + 1 = 8193 rooms on 256 CUs;
+    the bench's C4 class holds 13108), launched by the default routing -- the wide build -- and
+    solved by the C restatement of the oracle IPM over the same generated model
+    (`oracle/c/ipm_oracle.c` + the host-compiled stage functions, `cbuild.solve_generated_fleet`),
+    the reference's solver settings: same return status and iteration count per agent, objectives
+    rel 1e-6 and solutions rel 1e-5 where both succeed.  Mirrors the 4096-agent C3 main-build test."""
+    from agentlib_mpc_amd import benchmarks as bm
+    from agentlib_mpc_amd.optimization_backends.problem import fleet_nlp_inputs
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES, stats_to_dicts
+    from oracle import cbuild
+
+    be, cv = bm.exchange_room(solver_options=bm.REFERENCE)
+    native = be._native()
+    if native.wide_fleet_path is None:
+        pytest.fail("exchange_room's main build holds 16 agents per CU: the 20-per-CU build must load")
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 2 * 16 * cus + 1
+    assert n >= 8193 or cus < 256
+    rng = np.random.default_rng(20261019)
+    vals = {"T": cv["T"].value + rng.uniform(-2.0, 3.0, n),
+            "admm_exchange_lambda_mDot_out": rng.uniform(-20.0, 20.0, n)}
+    p, lbw, ubw, w0 = be.problem.to_kernel(*fleet_nlp_inputs(be.problem, cv, vals))
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    tw = T(w0)
+    st = torch.zeros(n * STATS_BYTES, dtype=torch.uint8, device="cuda")
+    native.solve(T(p), T(lbw), T(ubw), tw, stats=st)   # default routing: n >= wide_min
+    torch.cuda.synchronize()
+    gw = tw.cpu().numpy()
+    gs = stats_to_dicts(st.cpu().numpy().tobytes())
+    ref = dict(REFERENCE_OPTS)
+    cw, cs, _ = cbuild.solve_generated_fleet(be.problem.gen, p, lbw, ubw, w0, threads=16, tol=ref.pop("tol"),
+                                             max_iter=ref.pop("max_iter"), **ref)
+    assert [s["status"] for s in gs] == [s["status"] for s in cs]
+    assert [s["iter_count"] for s in gs] == [s["iter"] for s in cs]
+    ok = np.array([s["status"] in (0, 1) for s in gs])
+    assert ok.mean() > 0.99
+    np.testing.assert_allclose([s["obj"] for s, o in zip(gs, ok) if o], [s["obj"] for s, o in zip(cs, ok) if o],
+                               rtol=RTOL_OBJ, atol=1e-9)
+    np.testing.assert_allclose(gw[ok], cw[ok], rtol=RTOL_TRAJ, atol=1e-7 * max(1.0, np.abs(cw[ok]).max()))
+
+
 def test_gpu_small_fleet_build_matches_hbm_build():
     """The small-fleet build (workspace in LDS, one agent per CU; ``mpcx_problem_small_fleet``,
     used for batches of at most one agent per CU) against the HBM-workspace build on the same

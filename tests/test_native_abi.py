@@ -28,7 +28,47 @@ def test_library_builds_loads_and_exports_all_symbols():
     lib = ctypes.CDLL(str(path))
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.mpcx_version() == 13
+    assert lib.mpcx_version() == 14
+
+
+def test_collective_goes_through_the_registered_transport():
+    """C ABI v14: mpcx_admm_allreduce issues the ADMM iteration's one all-reduce on the
+    transport registered with the library.  A stub transport (a C-callable function that "sums" over
+    two identical ranks by doubling) through the ABI: every call reaches it once with the buffer and
+    length, the library counts the calls, and without a transport the call fails (MPCX_ERR_COMM).
+    No GPU: host buffers, null stream."""
+    import numpy as np
+
+    lib = native.load_library()
+    seen = []
+
+    def stub(ctx, buf, count, stream):
+        a = np.ctypeslib.as_array((ctypes.c_double * count).from_address(buf))
+        a *= 2.0  # two ranks holding the same values
+        seen.append((buf, count, ctx))
+        return 0
+
+    fn = native.ALLREDUCE_FN(stub)
+    x = np.arange(1.0, 8.0)
+    ptr = ctypes.c_void_p(x.ctypes.data)
+    try:
+        assert lib.mpcx_allreduce_register_fn(fn, ctypes.c_void_p(1234)) == 0
+        assert lib.mpcx_allreduce_kind() == native.COLLECTIVE_FN
+        c0 = lib.mpcx_allreduce_calls()
+        for _ in range(3):
+            assert lib.mpcx_admm_allreduce(ptr, 5, None) == 0
+        assert lib.mpcx_allreduce_calls() - c0 == 3
+        assert seen == [(x.ctypes.data, 5, 1234)] * 3
+        np.testing.assert_array_equal(x, np.r_[8.0 * np.arange(1.0, 6.0), 6.0, 7.0])
+        assert lib.mpcx_admm_allreduce(ptr, -1, None) == native.ERR_ARG
+    finally:
+        lib.mpcx_allreduce_unregister()
+    assert lib.mpcx_allreduce_kind() == native.COLLECTIVE_NONE
+    assert lib.mpcx_admm_allreduce(ptr, 5, None) == native.ERR_COMM
+    # the RCCL transport's argument checks (no communicator is made here)
+    assert lib.mpcx_allreduce_register(None, None) == native.ERR_ARG
+    comm = ctypes.c_void_p()
+    assert lib.mpcx_rccl_comm_init(None, 2, 2, ctypes.create_string_buffer(128), ctypes.byref(comm)) == native.ERR_ARG
 
 
 def test_struct_sizes_match_header():

@@ -486,6 +486,9 @@ class ADMMFleet:
         for c in self.classes:
             c.MAP = t.zeros(c.n, dtype=i32, device=dev)
             c.bound = c.n
+        #: page-locked host twins of the buffers set_inputs / solutions move (see _pinned)
+        self._host = {}
+        self._host_ev = t.cuda.Event() if dev.type == "cuda" else None
 
     def set_inputs(self, class_name: str, p: np.ndarray, lbw: Optional[np.ndarray] = None,
                    ubw: Optional[np.ndarray] = None):
@@ -493,11 +496,41 @@ class ADMMFleet:
         reference-layout arrays (lifted classes need all three)."""
         c = next(c for c in self.classes if c.name == class_name)
         p, lbw, ubw = c.to_kernel(p, lbw, ubw)
-        c.P.copy_(self.torch.as_tensor(p))
-        if lbw is not None:
-            c.LB.copy_(self.torch.as_tensor(lbw))
-        if ubw is not None:
-            c.UB.copy_(self.torch.as_tensor(ubw))
+        for dst, src in ((c.P, p), (c.LB, lbw), (c.UB, ubw)):
+            if src is not None:
+                self._upload(dst, src)
+
+    def _pinned(self, dev_t):
+        """The page-locked host twin of a device buffer (made once): the fleet's host <-> device
+        moves go through it.  A copy from pageable memory makes the HIP runtime lock the pages
+        for the transfer and release them after it -- on a fresh numpy array every control step
+        -- and the GPU work after such a step started 14-27 ms late in some processes (the C2
+        leg's slow mode, r05/s20-s23)."""
+        key = dev_t.data_ptr()
+        buf = self._host.get(key)
+        if buf is None or buf.shape != dev_t.shape:
+            buf = self.torch.empty(dev_t.shape, dtype=dev_t.dtype, pin_memory=True)
+            self._host[key] = buf
+        return buf
+
+    def _upload(self, dst, src):
+        if self.device.type != "cuda":
+            dst.copy_(self.torch.as_tensor(src))
+            return
+        h = self._pinned(dst)
+        self._host_ev.synchronize()  # the previous upload out of this buffer is done
+        np.copyto(h.numpy(), np.asarray(src, dtype=np.float64).reshape(h.shape))
+        dst.copy_(h, non_blocking=True)
+        self._host_ev.record()
+
+    def _download(self, src) -> np.ndarray:
+        if self.device.type != "cuda":
+            return src.cpu().numpy()
+        h = self._pinned(src)
+        self._host_ev.synchronize()
+        h.copy_(src, non_blocking=True)
+        self.torch.cuda.current_stream(self.device).synchronize()
+        return h.numpy().copy()
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -941,7 +974,7 @@ class ADMMFleet:
     def solutions(self, class_name: str) -> np.ndarray:
         """Reference-layout NLP solution vectors [n, nw] of one class."""
         c = next(c for c in self.classes if c.name == class_name)
-        return c.backend.problem.from_kernel(c.W.cpu().numpy(), c.lbw_ref)
+        return c.backend.problem.from_kernel(self._download(c.W), c.lbw_ref)
 
     def stats(self, class_name: str) -> list:
         from agentlib_mpc_amd.runtime.native import stats_to_dicts

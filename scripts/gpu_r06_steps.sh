@@ -26,6 +26,24 @@ step_s1() {
   echo "tests exit $rc, bench exit $?"
 }
 
+step_s2() {
+  # r06/s2: the C2 leg's slow mode with the fleet's host moves through page-locked buffers: three
+  # line runs without the CPU baselines and the MHE / e2e legs (as r05/s23), round phases logged;
+  # then what PC sampling this box offers, and a host-trap PC-sample histogram of the C3 leg
+  mkdir -p gpurun_out/s2
+  for V in a b c; do
+    MPCX_FLEET_DEBUG=1 timeout -k 10 600 python -u bench.py --mhe-agents 0 --no-e2e --no-cpu-baseline > gpurun_out/s2/line_$V.json 2> gpurun_out/s2/line_$V.err || exit $?
+  done
+  timeout -s KILL 60 rocprofv3 -L > gpurun_out/s2/rocprof_list.txt 2>&1
+  echo "list exit $?"
+  grep -i -A12 "pc.sampl\|host_trap\|stochastic" gpurun_out/s2/rocprof_list.txt > gpurun_out/s2/pcs_configs.txt 2>&1
+  if grep -qi "host_trap" gpurun_out/s2/rocprof_list.txt; then
+    rm -rf gpurun_out/s2/pcs
+    timeout -s KILL 240 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time --pc-sampling-interval 1 -d gpurun_out/s2/pcs -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --admm-agents 0 --c2-blocks 0 --c5-blocks 0 --nn-zones 0 --mhe-agents 0 > gpurun_out/s2/pcs.out 2>&1
+    echo "pcs exit $?"
+  fi
+}
+
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }
 "$fn"

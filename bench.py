@@ -18,11 +18,11 @@ fleet slice (``--agents`` per GPU, weak scaling, no data-path collective);
 barrier + synchronize bracket the timed steps and the max time over ranks is
 reported.
 
-Extra JSON fields: ``roofline`` for the dominant kernel (mpcx_ipm_solve, FP64
-vector-bound: algorithmic flops from the generated code's op counts and the
-kernel's per-agent iteration counters / kernel time measured with HIP events
-on the launch stream) and ``cpu_baseline`` (oracle timed on host cores on a
-bounded sample, rank 0, N=1 only).
+Extra JSON fields: ``roofline`` for the dominant kernel (mpcx_ipm_solve; kernel time measured
+with HIP events on the launch stream; ``roofline_block``: bound "hbm" -- the counters show the
+memory side as the limit -- with the algorithmic bytes as ``achieved``, the counted bytes as
+``traffic`` / ``memory_side`` and the algorithmic FP64 flops beside them) and ``cpu_baseline``
+(oracle timed on host cores on a bounded sample, rank 0, N=1 only).
 """
 
 from __future__ import annotations
@@ -43,6 +43,7 @@ import numpy as np  # noqa: E402
 METRIC = "converged MPC solves/sec (whole node) at N agents; ADMM iters/sec to consensus"
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector peak (spec)
 PEAK_HBM_GBS = 8000.0
+MEASURED_HBM_GBS = 6300.0  # MI355X_MICROARCH.md: ~6.3 TB/s achievable
 
 
 def fleet_values(n, seed):
@@ -142,6 +143,48 @@ def pmc_fp64(code_object: str, n_agents: int, kernel_ms: float):
                     "fp64_share_of_valu_insts": d["fp64_share_of_valu_insts"],
                     "wave_cycle_split": d.get("wave_cycle_split"), "source": os.path.relpath(path, ROOT)}
     return None
+
+
+def roofline_block(kernel_ms, io_bytes, flops, traffic, traffic_src, fp64_pmc):
+    """``roofline`` of the C3 launch (the label follows the counters).
+
+    bound "hbm": the rocprofv3 counters put the kernel on the memory side -- FETCH_SIZE + WRITE_SIZE
+    bytes per launch at ~60 % of the 8 TB/s spec (FETCH_SIZE doubled: calibrated on known byte counts
+    at 4, 8 and 16 B per lane, profiles/r06/s1/fetch_calib.json), waves parked on memory half their
+    cycles, VALU issue ~17 % (profiles/r05/final2/pmc_fp64_c3.json).  ``achieved`` / ``frac``: the
+    ALGORITHMIC bytes of a launch (its inputs and outputs) over the kernel time -- tiny,
+    because the traffic is the solver's per-agent workspace (97 KB, re-streamed every IPM iteration,
+    DESIGN §3) and not the problem's data; ``memory_side``: the counted bytes over the same time;
+    ``fp64``: the algorithmic flops (generated-code op counts x per-agent counters) over that time."""
+    ks = kernel_ms * 1e-3
+    achieved = io_bytes / ks / 1e9
+    mem = None
+    if traffic:
+        gbs = traffic / ks / 1e9
+        mem = {"bytes_per_launch": traffic, "achieved": gbs, "unit": "GB/s", "frac_of_peak": gbs / PEAK_HBM_GBS,
+               "frac_of_measured_max": gbs / MEASURED_HBM_GBS, "traffic_over_algorithmic": traffic / io_bytes,
+               "fetch_size_factor": 2.0, "calibration": "profiles/r06/s1/fetch_calib.json", "source": traffic_src}
+    fp = flops / ks / 1e12
+    return {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": PEAK_HBM_GBS,
+        "unit": "GB/s",
+        "frac": achieved / PEAK_HBM_GBS,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "memory_side": mem,
+        "fp64": {"achieved": fp, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": fp / PEAK_FP64_TFLOPS,
+                 "flops_per_launch": flops, "pmc": fp64_pmc},
+        "algorithmic_io_bytes": io_bytes,
+        "kernel": "mpcx_ipm_solve",
+        "kernel_ms": kernel_ms,
+        "note": "algorithmic bytes = the launch's NLP inputs and outputs (p, bounds, guess, solution, multipliers, "
+                "stats); the counted traffic is the per-agent workspace every IPM iteration streams (its vectors, "
+                "stage derivatives, compact stage images, back-substitution operators), which 16 agents per CU "
+                "cannot keep in LDS (DESIGN §3, §5); FP64 work: generated-code op counts of the stage "
+                "evaluations, the sparse static stage elimination, dense fallback stages and the state chain",
+    }
 
 
 def pmc_traffic(code_object: str, n_agents: int):
@@ -919,7 +962,6 @@ def main():
     total_ok = float(ok_t.item())
     value = total_ok * args.steps / wall
     if rank == 0:
-        achieved = flops / (kernel_ms * 1e-3) / 1e12
         from agentlib_mpc_amd.runtime.native import code_object_path
         traffic, traffic_src = pmc_traffic(code_object_path(prob.gen.key).name, n)
         io_bytes = n * 8 * (prob.nlp.npar + 3 * prob.nlp.nw + prob.nlp.ng_total) + n * STATS_BYTES
@@ -952,25 +994,8 @@ def main():
                 "ipm_iterations_p50_p99_max": [float(np.percentile(arr["iter"], q)) for q in (50, 99, 100)],
                 "parallelism": f"agent-partitioned dp{world}",
             },
-            "roofline": {
-                "bound": "fp64-valu",  # FP64 vector ALU; latency-bound in practice
-                "achieved": achieved,
-                "peak": PEAK_FP64_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved / PEAK_FP64_TFLOPS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "fp64_pmc": pmc_fp64(code_object_path(prob.gen.key).name, n, kernel_ms),
-                "algorithmic_io_bytes": io_bytes,
-                "kernel": "mpcx_ipm_solve",
-                "kernel_ms": kernel_ms,
-                "flops_per_launch": flops,
-                "note": "FP64 vector pipe (the C3 model has no network; the C5 NARX networks run on the FP64 "
-                        "matrix cores, DESIGN 2.1b); algorithmic flops = generated-code op "
-                        "counts (stage evaluations, sparse static stage elimination, dense fallback stages, "
-                        "state chain) x per-agent iteration/factorisation/trial counters; the kernel is bound "
-                        "by dependent LDS/L2 round trips, not by FP64 issue (DESIGN §5)",
-            },
+            "roofline": roofline_block(kernel_ms, io_bytes, flops, traffic, traffic_src,
+                                       pmc_fp64(code_object_path(prob.gen.key).name, n, kernel_ms)),
         }
         if c3s is not None:
             out["c3_strong"] = c3s

@@ -44,6 +44,20 @@ step_s2() {
   fi
 }
 
+step_s3() {
+  # r06/s3: PMC passes of the C3 leg on the current code object (traffic, FP64 mix, wave split);
+  # a kernel trace of the C2 leg alone (per-iteration spans of its rounds: scripts/iter_trace.py);
+  # phase profiles of C1 (one agent, small-fleet build) and the C3 fleet
+  mkdir -p gpurun_out/s3/pmc
+  PMC_OUT=gpurun_out/s3/pmc bash scripts/gpu_pmc.sh || exit $?
+  rm -rf gpurun_out/s3/prof_c2
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/s3/prof_c2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0 > gpurun_out/s3/c2.json 2> gpurun_out/s3/c2.err || exit $?
+  python scripts/iter_trace.py gpurun_out/s3/prof_c2 5 > gpurun_out/s3/c2_iterations.txt 2>&1
+  WSLDS=1 AGENTS=1 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s3/phases_c1_lds.txt 2>&1 || exit $?
+  AGENTS=4096 timeout -k 10 300 python -u scripts/prof_phases.py > gpurun_out/s3/phases_c3.txt 2>&1
+  echo "s3 exit $?"
+}
+
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }
 "$fn"

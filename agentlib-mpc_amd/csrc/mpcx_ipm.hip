@@ -59,8 +59,10 @@ constexpr int CS = (M + WAVE - 1) / WAVE;   // constraint slots per lane
 // MAXF + FSPILL = 1024 entries, the cap shared with oracle/ipm.py (max_filter) and
 // oracle/c/ipm_oracle.c; an insertion into a full filter drops the oldest entry (counted).
 // MPCX_MAXF / MPCX_FSPILL: smaller parts for the parity test builds (tests/test_gpu_ipm.py).
+// r06: 48 in LDS (was 64): the 256 bytes pay for the per-lane element-class word (ecls) so that no
+// structure's LDS share, agents per CU or stage rounds change; no parity case holds more than 22.
 #ifndef MPCX_MAXF
-#define MPCX_MAXF 64
+#define MPCX_MAXF 48
 #endif
 constexpr int MAXF = MPCX_MAXF;
 static_assert(MAXF >= 1 && MAXF <= 64, "the filter test reads one entry per lane");
@@ -434,6 +436,8 @@ struct LdsRest {
   double CW[NCC];
   double CY[NCC];
   unsigned long long fixm[N];  // per stage: local primal indices that are fixed variables
+  unsigned int ecls[WAVE];     // per lane: its rows' classes (2 bits per slot) and its variables' free /
+                               // finite-bound bits (3 bits per slot, after them): cls_word, vcls_word
   int cperm[NCP];
   int cpiv[NCP];
   int fin[4];              // factor(): summed interior inertia (pos, neg, zero) and singular flag
@@ -686,6 +690,20 @@ __device__ __forceinline__ int cls_of(double lo, double hi, double sl, double su
   if (!isfin(sl) && !isfin(su)) return 2;
   return 1;
 }
+// The classes of a lane's rows (slot sl: row lane + 64 sl), computed once by init_agent (the bounds
+// never change): the hot phases read one LDS word instead of loading ub to classify each row, and
+// no row's class waits for its bound loads (r06: the iteration head classified a slot's rows from
+// lb / ub before loading its other operands -- one more memory round trip per slot)
+static_assert(2 * CS + 3 * VS <= 32, "element classes: 2 bits per constraint slot, 3 per variable slot, one word");
+__device__ __forceinline__ unsigned cls_word() { return gL.ecls[lane_now()]; }
+__device__ __forceinline__ int cls_slot(unsigned w, int sl) { return (int)((w >> (2 * sl)) & 3u); }
+// The same for the variables (slot sl: variable lane + 64 sl): VFREE (NX <= i < NW, lo != hi),
+// VLO / VHI (finite lower / upper bound), 3 bits per slot -- the hot phases' branches on a variable's
+// bounds then do not wait for the bound loads (the compiler issued a slot's other loads only after
+// testing lo == hi: two memory round trips per slot)
+constexpr unsigned VFREE = 1u, VLO = 2u, VHI = 4u;
+__device__ __forceinline__ unsigned vcls_word() { return gL.ecls[lane_now()] >> (2 * CS); }
+__device__ __forceinline__ unsigned vcls_slot(unsigned w, int sl) { return (w >> (3 * sl)) & 7u; }
 
 // ---------------------------------------------------------------------------
 // evaluation (lane k evaluates stage k; parameters from LDS)
@@ -782,19 +800,24 @@ __device__ __forceinline__ void eval_hess(const Agent a, double sigma) { eval_he
 
 // gradient of the (unscaled) objective w.r.t. w[i], i >= NX (stage derivatives of
 // stage b and, for a state, the X0 part of stage b+1)
-__device__ __forceinline__ double acc_grad(const Agent a, int i) {
+// Both loads are unconditional (the second from a valid address either way, its value selected
+// away where unused): a load under a divergent branch is waited for inside the branch, and the
+// wait drains every older load of the phase (vmcnt counts in issue order) -- r06: four such drains
+// per iteration head, one memory round trip each
+__device__ __forceinline__ double stage_pair_sum(const wdbl* arr, int i) {
   const int b = (i - NX) / NP, off = (i - NX) % NP;
-  double v = a.sdg()[(NX + off) * N + b];
-  if (NX > 0 && off >= NV && b + 1 < N) v += a.sdg()[(off - NV) * N + b + 1];
+  const int i0 = (NX + off) * N + b;
+  const double v = arr[i0];
+  if constexpr (NX > 0) {
+    const bool two = off >= NV && b + 1 < N;
+    const double w = arr[two ? (off - NV) * N + b + 1 : i0];
+    return two ? v + w : v;
+  }
   return v;
 }
+__device__ __forceinline__ double acc_grad(const Agent a, int i) { return stage_pair_sum(a.sdg(), i); }
 // (J~^T lam)[i] with J~ = gs*J, from the per-stage products the evaluators wrote
-__device__ __forceinline__ double acc_jtl(const Agent a, int i) {
-  const int b = (i - NX) / NP, off = (i - NX) % NP;
-  double v = a.jtl()[(NX + off) * N + b];
-  if (NX > 0 && off >= NV && b + 1 < N) v += a.jtl()[(off - NV) * N + b + 1];
-  return v;
-}
+__device__ __forceinline__ double acc_jtl(const Agent a, int i) { return stage_pair_sum(a.jtl(), i); }
 
 // ---------------------------------------------------------------------------
 // dense Bunch-Kaufman LDL^T in LDS (full symmetric storage, wave-wide):
@@ -1506,9 +1529,11 @@ __device__ MPCX_HOT void local_assemble(const Agent a, int k, int g, ldsd* F, co
     wsync();
   }
   constexpr int CH = EPC < 12 ? EPC : 12;  // entries per lane in flight (loads before the first use)
+  const bool anyfix = __ballot(fm != 0ull) != 0ull;  // wave-uniform: some stage of the round has fixed entries
 #pragma unroll 1
   for (int e0 = 0; e0 < EPC; e0 += CH) {
     double v[CH], dv[CH];
+    int ijv[CH];
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
       const int t = g + (e0 + e) * GG;
@@ -1516,6 +1541,10 @@ __device__ MPCX_HOT void local_assemble(const Agent a, int k, int g, ldsd* F, co
       const bool bd = t >= CB && t < CB + NLOC && lkind(t - CB) != 2;
       v[e] = bd ? rb[lblk(t - CB, lkind(t - CB))] : src[(t < NCPT ? t : 0) * N];
       dv[e] = dg[t < NLOC ? t : 0];
+      // the entry's (row, column) with the image loads, not under the fixed-entry branch below:
+      // kCIJ is a global-memory table, and a load waited for inside a divergent branch drains
+      // every older load (r06: one memory round trip per entry of a round holding stage 0)
+      ijv[e] = anyfix ? (int)kCIJ[t < NCPT ? t : 0] : 0;
     }
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
@@ -1524,7 +1553,7 @@ __device__ MPCX_HOT void local_assemble(const Agent a, int k, int g, ldsd* F, co
       double x = v[e];
       bool fix = false;
       if (fm != 0ull) {
-        const int ij = kCIJ[t], i = ij & 255, j = ij >> 8;
+        const int ij = ijv[e], i = ij & 255, j = ij >> 8;
         fix = (((fm >> i) | (fm >> j)) & 1ull) != 0ull;
         if (fix) x = (i == j && lkind(i) == 0) ? 1.0 : 0.0;
       }
@@ -2505,6 +2534,18 @@ __device__ __noinline__ Scal init_agent(const Agent a, int agent) {
       a.zU()[i] = 0.0;
     }
   }
+  {  // the variables' bound classes for the hot phases (this lane wrote them above)
+    unsigned w = 0u;
+    for (int sl = 0; sl < VS; ++sl) {
+      const int i = lane + sl * WAVE;
+      if (i < NW) {
+        const double lo = a.xL()[i], hi = a.xU()[i];
+        const unsigned b = ((i >= NX && lo != hi) ? VFREE : 0u) | (isfin(lo) ? VLO : 0u) | (isfin(hi) ? VHI : 0u);
+        w |= b << (3 * sl);
+      }
+    }
+    gL.ecls[lane] = w << (2 * CS);  // the rows' classes are added below, once their bounds are final
+  }
   sync();
   // fixed-variable masks of the stage-local systems (bounds never change fixedness)
   for (int k = lane; k < N; k += WAVE) {
@@ -2542,6 +2583,14 @@ __device__ __noinline__ Scal init_agent(const Agent a, int agent) {
     }
     a.lam()[c] = 0.0;
   }
+  {  // the rows' classes for the hot phases (this lane wrote its rows' bounds above)
+    unsigned w = 0u;
+    for (int sl = 0; sl < CS; ++sl) {
+      const int c = lane + sl * WAVE;
+      if (c < M) w |= (unsigned)cls_of(a.lb()[c], a.ub()[c], a.sL()[c], a.sU()[c]) << (2 * sl);
+    }
+    gL.ecls[lane] |= w;
+  }
   sync();
   eval_gj_ws(a, a.x(), 1);
   sync();
@@ -2563,16 +2612,17 @@ __device__ __noinline__ double theta_now(const Agent a) {
 // the whole rhs to the factorisation lanes
 __device__ __noinline__ void rhs_dual(const Agent a, double mu, double dw, double dc) {
   const int lane = lane_now();
+  const unsigned cw = cls_word();
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
     const int c = lane + sl * WAVE;
     const bool on = c < M;
     const int cc = on ? c : 0;
-    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double lbv = a.lb()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
     const double gvv = a.gv()[cc], gsc = a.gs()[cc], sv = a.s()[cc], lm = a.lam()[cc];
     const double vl = a.vL()[cc], vu = a.vU()[cc];
     if (on) {
-      const int cl = cls_of(lbv, ubv, slo, sup);
+      const int cl = cls_slot(cw, sl);
       double rr;
       const double rsl = rcp_or0(cl == 1 && isfin(slo), sv - slo), rsu = rcp_or0(cl == 1 && isfin(sup), sup - sv);
       const double rsd = rcp_or0(cl == 1, vl * rsl + vu * rsu + dw);  // 1 / (Sigma_s + delta_w)
@@ -2684,21 +2734,23 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
   RatioMin ra, rz;
   LogSum lb;
   double gphid = 0.0, theta = 0.0;
+  const unsigned vw = vcls_word();
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
     const bool on = i < NW;
     const int ii = (i >= NX && on) ? i : NX;
+    const unsigned vb = vcls_slot(vw, sl);
     const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
     const double gr = acc_grad(a, ii);
     const double sv = gL.u.sol[((ii - NX) / NP) * NB + (ii - NX) % NP];
     if (!on) continue;
-    const bool free_ = i >= NX && lo != hi;
+    const bool free_ = (vb & VFREE) != 0u;
     const double d = free_ ? sv : 0.0;
     a.dx()[i] = d;
     if (!free_) continue;
     double gphi = obj_scale * gr;
-    if (isfin(lo)) {
+    if (vb & VLO) {
       const double s_l = xv - lo, rl = MPCX_RCP(s_l);
       gphi -= mu * rl;
       if (d < 0) ra.take(tau * s_l, -d);
@@ -2706,7 +2758,7 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
       if (dz < 0) rz.take(tau * zl, -dz);
       if (!bar_cached) lb.add(s_l);
     }
-    if (isfin(hi)) {
+    if (vb & VHI) {
       const double s_u = hi - xv, ru = MPCX_RCP(s_u);
       gphi += mu * ru;
       if (d > 0) ra.take(tau * s_u, d);
@@ -2716,18 +2768,19 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
     }
     gphid += gphi * d;
   }
+  const unsigned cw = cls_word();
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
     const int c = lane + sl * WAVE;
     const bool on = c < M;
     const int cc = on ? c : 0;
-    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double lbv = a.lb()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
     const double sv = a.s()[cc], lm = a.lam()[cc], vl = a.vL()[cc], vu = a.vU()[cc];
     const double gvv = a.gv()[cc], gsc = a.gs()[cc];
     const double dlam = gL.u.sol[(cc / NG) * NB + NP + cc % NG];
     if (!on) continue;
     a.dl()[c] = dlam;
-    const int cl = cls_of(lbv, ubv, slo, sup);
+    const int cl = cls_slot(cw, sl);
     theta += fabs((cl == 0) ? gvv - gsc * lbv : gvv - sv);
     double dsv = 0.0;
     if (cl == 1) {
@@ -2815,16 +2868,18 @@ __device__ MPCX_HOT void line_search(const Agent a) {
       const int lane = lane_now();
       const double alpha = K.ls.alpha;
       LogSum bx;
+      const unsigned vw = vcls_word();
 #pragma unroll 1
       for (int sl = 0; sl < VS; ++sl) {
         const int i = lane + sl * WAVE;
         if (i < NW) {
+          const unsigned vb = vcls_slot(vw, sl);
           const double lo = a.xL()[i], hi = a.xU()[i];
           const double xt = a.x()[i] + alpha * a.dx()[i];
           gL.u.t.xt[i] = xt;
-          if (i >= NX && lo != hi) {
-            if (isfin(lo)) bx.add(xt - lo);
-            if (isfin(hi)) bx.add(hi - xt);
+          if (vb & VFREE) {
+            if (vb & VLO) bx.add(xt - lo);
+            if (vb & VHI) bx.add(hi - xt);
           }
         }
       }
@@ -2840,12 +2895,13 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     const double alpha = K.ls.alpha;
     double th = 0.0;
     LogSum bs;
+    const unsigned cw = cls_word();
 #pragma unroll 1
     for (int sl = 0; sl < CS; ++sl) {
       const int c = lane + sl * WAVE;
       if (c < M) {
         const double gsv = a.gs()[c], lbv = a.lb()[c], slv = a.sL()[c], suv = a.sU()[c];
-        const int cl = cls_of(lbv, a.ub()[c], slv, suv);
+        const int cl = cls_slot(cw, sl);
         const double gt = gL.u.t.gt[c] * gsv;
         gL.u.t.gt[c] = gt;
         const double st = a.s()[c] + alpha * a.ds()[c];
@@ -2900,35 +2956,38 @@ __device__ MPCX_HOT void line_search(const Agent a) {
 __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, double mu, double alpha, double az) {
   const int lane = lane_now();
   const double ksm = kappa_sigma * mu, mks = mu * MPCX_RCP(kappa_sigma);  // the kappa_sigma safeguard's bounds x s
+  const unsigned vw = vcls_word();
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
     const bool on = i >= NX && i < NW;
     const int ii = on ? i : NX;
+    const unsigned vb = vcls_slot(vw, sl);
     const double lo = a.xL()[ii], hi = a.xU()[ii], xold = a.x()[ii], d = a.dx()[ii];
     const double zl = a.zL()[ii], zu = a.zU()[ii];
     const double xn = gL.u.t.xt[ii];
-    if (!on || lo == hi) continue;
+    if (!(vb & VFREE)) continue;  // VFREE: NX <= i < NW, lo != hi
     a.x()[i] = xn;
-    if (isfin(lo)) {
+    if (vb & VLO) {
       const double r0 = MPCX_RCP(xold - lo);
       const double dz = mu * r0 - zl - (zl * r0) * d;
       const double zn = zl + az * dz, rn = MPCX_RCP(xn - lo);
       a.zL()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
     }
-    if (isfin(hi)) {
+    if (vb & VHI) {
       const double r0 = MPCX_RCP(hi - xold);
       const double dz = mu * r0 - zu + (zu * r0) * d;
       const double zn = zu + az * dz, rn = MPCX_RCP(hi - xn);
       a.zU()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
     }
   }
+  const unsigned cw = cls_word();
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
     const int c = lane + sl * WAVE;
     const bool on = c < M;
     const int cc = on ? c : 0;
-    const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+    const double slo = a.sL()[cc], sup = a.sU()[cc];
     const double lm = a.lam()[cc], dl = a.dl()[cc], sold = a.s()[cc], dsv = a.ds()[cc];
     const double vl = a.vL()[cc], vu = a.vU()[cc];
     const double gt = gL.u.t.gt[cc];
@@ -2937,7 +2996,7 @@ __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, do
     a.gv()[c] = gt;
     const double sn = sold + alpha * dsv;
     a.s()[c] = sn;
-    if (cls_of(lbv, ubv, slo, sup) != 1) continue;
+    if (cls_slot(cw, sl) != 1) continue;
     if (isfin(slo)) {
       const double r0 = MPCX_RCP(sold - slo);
       const double dv = mu * r0 - vl - (vl * r0) * dsv;
@@ -2992,34 +3051,39 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
     double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, vmax_u = 0.0, pmx = -INFINITY, pmn = INFINITY;
     double lsum = 0.0, zsum = 0.0;
     int nz = 0;
+    const unsigned vw = vcls_word();
 #pragma unroll
     for (int sl = 0; sl < VS; ++sl) {
       const int i = lane + sl * WAVE;
       const int ii = (i >= NX && i < NW) ? i : NX;
+      const unsigned vb = vcls_slot(vw, sl);
       const double lo = a.xL()[ii], hi = a.xU()[ii];
       double xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
       const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
-      const bool on = i >= NX && i < NW && lo != hi;
-      const double rl = rcp_or0(isfin(lo) && lo != hi, xv - lo), ru = rcp_or0(isfin(hi) && lo != hi, hi - xv);
+      // on: NX <= i < NW and lo != hi; a fixed variable (lo == hi: every x_0 entry) has no barrier
+      // terms (its psx is stored as 0)
+      const bool on = (vb & VFREE) != 0u;
+      const double rl = rcp_or0(on && (vb & VLO), xv - lo), ru = rcp_or0(on && (vb & VHI), hi - xv);
       pr0[sl] = on ? -(obj_scale * gr + jt) : 0.0;
       pr1[sl] = on ? rl - ru : 0.0;
-      psx[sl] = (lo == hi) ? 0.0 : zl * rl + zu * ru;  // sigma_x_v
+      psx[sl] = on ? zl * rl + zu * ru : 0.0;  // sigma_x_v
       if (on) {
         const double rd = obj_scale * gr + jt - zl + zu;
         dmax = fmax(dmax, fabs(rd));
         dmax_u = fmax(dmax_u, fabs(rd) / obj_scale);
-        if (isfin(lo)) { const double pr = (xv - lo) * zl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zl); nz++; }
-        if (isfin(hi)) { const double pr = (hi - xv) * zu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zu); nz++; }
+        if (vb & VLO) { const double pr = (xv - lo) * zl; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zl); nz++; }
+        if (vb & VHI) { const double pr = (hi - xv) * zu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zu); nz++; }
       }
     }
+    const unsigned cw = cls_word();
 #pragma unroll
     for (int sl = 0; sl < CS; ++sl) {
       const int c = lane + sl * WAVE;
       const int cc = c < M ? c : 0;
-      const double lbv = a.lb()[cc], ubv = a.ub()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
+      const double lbv = a.lb()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
       const double gsc = a.gs()[cc], lm = a.lam()[cc];
       double gvv = a.gv()[cc], sv = a.s()[cc], vl = a.vL()[cc], vu = a.vU()[cc];
-      const int cl = cls_of(lbv, ubv, slo, sup);
+      const int cl = cls_slot(cw, sl);
       {
         const double rsl = rcp_or0(cl == 1 && isfin(slo), sv - slo), rsu = rcp_or0(cl == 1 && isfin(sup), sup - sv);
         const double sg = vl * rsl + vu * rsu;  // sigma_s_v

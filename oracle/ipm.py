@@ -86,7 +86,7 @@ class IPMOptions:
     gamma_phi: float = 1e-8
     gamma_theta: float = 1e-5
     alpha_min_frac: float = 0.05
-    #: filter entries kept (IPOPT's list is unbounded; the kernel keeps its newest 64 in LDS and
+    #: filter entries kept (IPOPT's list is unbounded; the kernel keeps its newest 48 in LDS and
     #: the older ones in a spill list in HBM, MAXF + FSPILL = 1024 in all, csrc/mpcx_ipm.hip): one
     #: cap for the kernel, oracle/c/ipm_oracle.c and this file; an insertion into a full filter
     #: drops the oldest entry and is counted

@@ -64,11 +64,11 @@ step_s4() {
   # the C3 fleet, C1 (small-fleet build), the C4 room fleet (13108), MHE (4096) and the C2 air handler
   # (1024); then the GPU suite, smoke and the default bench line
   mkdir -p gpurun_out/s4
-  REV=HEAD timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_c3.txt 2>&1 || exit $?
-  REV=HEAD AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_rev lds_base lds_rev > gpurun_out/s4/var_c1.txt 2>&1 || exit $?
-  MODEL=exchange_room AGENTS=13108 REV=HEAD timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_c4room.txt 2>&1 || exit $?
-  MODEL=mhe_room AGENTS=4096 REV=HEAD timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_mhe.txt 2>&1 || exit $?
-  MODEL=admm_ahu AGENTS=1024 REV=HEAD timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_ahu.txt 2>&1 || exit $?
+  REV=$REV timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_c3.txt 2>&1 || exit $?
+  REV=$REV AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_rev48 lds_base lds_rev48 > gpurun_out/s4/var_c1.txt 2>&1 || exit $?
+  MODEL=exchange_room AGENTS=13108 REV=$REV timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_c4room.txt 2>&1 || exit $?
+  MODEL=mhe_room AGENTS=4096 REV=$REV timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_mhe.txt 2>&1 || exit $?
+  MODEL=admm_ahu AGENTS=1024 REV=$REV timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s4/var_ahu.txt 2>&1 || exit $?
   timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s4/gpu_tests.txt 2>&1
   rc=$?
   [ $rc -ne 0 ] && [ $rc -ne 1 ] && { echo "tests exit $rc"; exit $rc; }

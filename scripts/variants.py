@@ -100,6 +100,9 @@ VARIANTS = {
     "sweep_lds": (["-DMPCX_SWEEP_LDS"], "REV:1bfd8f5"),
     "sweep_reg": ([], "REV:1bfd8f5"),
     "lds_lsq_noreg": (["-DMPCX_WS_LDS", "-DMPCX_LSQ_NOREG"], "REV:9a47260"),
+    # r06: a revision's small-fleet build with the working tree's filter size (48 in LDS), so that its
+    # workspace matches the main build it is loaded beside (mpcx_problem_small_fleet checks it)
+    "lds_rev48": (["-DMPCX_WS_LDS", "-DMPCX_MAXF=48"], "REV:" + os.environ.get("REV", "HEAD")),
 }
 
 

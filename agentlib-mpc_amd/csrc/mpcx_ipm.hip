@@ -334,6 +334,16 @@ __device__ __forceinline__ int lane_now() {
   return l;
 }
 
+// Pin a loaded operand: the empty asm "uses" it here, so the compiler issues the load before this
+// point instead of sinking it into the branch that uses it -- a load waited for inside a branch
+// drains every older load (vmcnt counts in issue order), one memory round trip per such load.  A
+// phase loads all its operands, pins them, then computes: one round trip for the batch.
+#ifndef MPCX_NO_PIN
+#define MPCX_PIN(x) asm volatile("" ::"v"(x))
+#else  // diagnostics (A/B): the compiler places the loads
+#define MPCX_PIN(x) (void)0
+#endif
+
 template <int GG>
 __device__ __forceinline__ double gmax(double v) {
   if constexpr (GG >= 2) v = fmax(v, dpp_f64<0xB1>(v));
@@ -2416,18 +2426,38 @@ __device__ MPCX_HOT void solve(const Agent a) {
   if (NC > 0) { if constexpr (CHAIN_TW) chain_solve_tw(a); else chain_solve(a); }
   SPROF(4);
   // u = W [x_k, c_k, 1] per stage interior (operators column-major per stage); the lanes
-  // run over all (stage, interior row) pairs
+  // run over all (stage, interior row) pairs, QB rounds of them per batch of operator loads (loaded
+  // first, MPCX_PIN: one memory round trip per batch instead of one per round)
+  constexpr int QR = (N * NI + WAVE - 1) / WAVE;   // rounds of 64 (stage, row) pairs
+  constexpr int QB = cmax(1, cmin(QR, 24 / NTR));  // rounds per batch (<= 24 operator entries per lane)
 #pragma unroll 1
-  for (int q = lane; q < N * NI; q += WAVE) {
-    const int k = q % N, p = q / N;  // stage fastest: the stage-minor operator reads coalesce
-    const wdbl* t = a.tr(k) + (long)p * N;
-    double u = t[(long)(NX + NC) * NI * N];
+  for (int r0 = 0; r0 < QR; r0 += QB) {
+    double tv[QB][NTR];
 #pragma unroll
-    for (int c = 0; c < NX; ++c) u -= ((k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0) * t[(long)c * NI * N];
+    for (int r = 0; r < QB; ++r) {
+      const int q = lane + (r0 + r) * WAVE, qq = q < N * NI ? q : 0;
+      const int k = qq % N, p = qq / N;  // stage fastest: the stage-minor operator reads coalesce
+      const wdbl* t = a.tr(k) + (long)p * N;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) u -= L.xs[k * NC + c] * t[(long)(NX + c) * NI * N];
-    const int o = stage_was_dense(k) ? a.prm(k)[p] : p;  // static stages: identity order
-    L.u.sol[k * NB + lblk(o, lkind(o))] = u;
+      for (int c = 0; c < NTR; ++c) tv[r][c] = t[(long)c * NI * N];
+    }
+#pragma unroll
+    for (int r = 0; r < QB; ++r)
+#pragma unroll
+      for (int c = 0; c < NTR; ++c) MPCX_PIN(tv[r][c]);
+#pragma unroll
+    for (int r = 0; r < QB; ++r) {
+      const int q = lane + (r0 + r) * WAVE;
+      if (r0 + r >= QR || q >= N * NI) continue;
+      const int k = q % N, p = q / N;
+      double u = tv[r][NX + NC];
+#pragma unroll
+      for (int c = 0; c < NX; ++c) u -= ((k > 0) ? L.xs[(k - 1) * NC + NMU + c] : 0.0) * tv[r][c];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) u -= L.xs[k * NC + c] * tv[r][NX + c];
+      const int o = stage_was_dense(k) ? a.prm(k)[p] : p;  // static stages: identity order
+      L.u.sol[k * NB + lblk(o, lkind(o))] = u;
+    }
   }
   for (int q = lane; q < N * NC; q += WAVE) {
     const int k = q / NC, li = LMU + q % NC;
@@ -2734,75 +2764,89 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
   RatioMin ra, rz;
   LogSum lb;
   double gphid = 0.0, theta = 0.0;
-  const unsigned vw = vcls_word();
+  const unsigned vw = vcls_word(), cw = cls_word();
+  // every operand of the phase loaded first, in one batch (MPCX_PIN: one memory round trip)
+  double lo[VS], hi[VS], xv[VS], zl[VS], zu[VS], gr[VS], sx[VS];
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
-    const bool on = i < NW;
-    const int ii = (i >= NX && on) ? i : NX;
+    const int ii = (i >= NX && i < NW) ? i : NX;
+    lo[sl] = a.xL()[ii]; hi[sl] = a.xU()[ii]; xv[sl] = a.x()[ii]; zl[sl] = a.zL()[ii]; zu[sl] = a.zU()[ii];
+    gr[sl] = acc_grad(a, ii);
+    sx[sl] = gL.u.sol[((ii - NX) / NP) * NB + (ii - NX) % NP];
+  }
+  double lbv[CS], slo[CS], sup[CS], sv[CS], lm[CS], vl[CS], vu[CS], gvv[CS], gsc[CS], dlam[CS];
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const int cc = c < M ? c : 0;
+    lbv[sl] = a.lb()[cc]; slo[sl] = a.sL()[cc]; sup[sl] = a.sU()[cc]; sv[sl] = a.s()[cc]; lm[sl] = a.lam()[cc];
+    vl[sl] = a.vL()[cc]; vu[sl] = a.vU()[cc]; gvv[sl] = a.gv()[cc]; gsc[sl] = a.gs()[cc];
+    dlam[sl] = gL.u.sol[(cc / NG) * NB + NP + cc % NG];
+  }
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) { MPCX_PIN(lo[sl]); MPCX_PIN(hi[sl]); MPCX_PIN(xv[sl]); MPCX_PIN(zl[sl]); MPCX_PIN(zu[sl]); MPCX_PIN(gr[sl]); }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    MPCX_PIN(lbv[sl]); MPCX_PIN(slo[sl]); MPCX_PIN(sup[sl]); MPCX_PIN(sv[sl]); MPCX_PIN(lm[sl]);
+    MPCX_PIN(vl[sl]); MPCX_PIN(vu[sl]); MPCX_PIN(gvv[sl]); MPCX_PIN(gsc[sl]);
+  }
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    if (i >= NW) continue;
     const unsigned vb = vcls_slot(vw, sl);
-    const double lo = a.xL()[ii], hi = a.xU()[ii], xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
-    const double gr = acc_grad(a, ii);
-    const double sv = gL.u.sol[((ii - NX) / NP) * NB + (ii - NX) % NP];
-    if (!on) continue;
     const bool free_ = (vb & VFREE) != 0u;
-    const double d = free_ ? sv : 0.0;
+    const double d = free_ ? sx[sl] : 0.0;
     a.dx()[i] = d;
     if (!free_) continue;
-    double gphi = obj_scale * gr;
+    double gphi = obj_scale * gr[sl];
     if (vb & VLO) {
-      const double s_l = xv - lo, rl = MPCX_RCP(s_l);
+      const double s_l = xv[sl] - lo[sl], rl = MPCX_RCP(s_l);
       gphi -= mu * rl;
       if (d < 0) ra.take(tau * s_l, -d);
-      const double dz = mu * rl - zl - (zl * rl) * d;
-      if (dz < 0) rz.take(tau * zl, -dz);
+      const double dz = mu * rl - zl[sl] - (zl[sl] * rl) * d;
+      if (dz < 0) rz.take(tau * zl[sl], -dz);
       if (!bar_cached) lb.add(s_l);
     }
     if (vb & VHI) {
-      const double s_u = hi - xv, ru = MPCX_RCP(s_u);
+      const double s_u = hi[sl] - xv[sl], ru = MPCX_RCP(s_u);
       gphi += mu * ru;
       if (d > 0) ra.take(tau * s_u, d);
-      const double dz = mu * ru - zu + (zu * ru) * d;
-      if (dz < 0) rz.take(tau * zu, -dz);
+      const double dz = mu * ru - zu[sl] + (zu[sl] * ru) * d;
+      if (dz < 0) rz.take(tau * zu[sl], -dz);
       if (!bar_cached) lb.add(s_u);
     }
     gphid += gphi * d;
   }
-  const unsigned cw = cls_word();
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
     const int c = lane + sl * WAVE;
-    const bool on = c < M;
-    const int cc = on ? c : 0;
-    const double lbv = a.lb()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
-    const double sv = a.s()[cc], lm = a.lam()[cc], vl = a.vL()[cc], vu = a.vU()[cc];
-    const double gvv = a.gv()[cc], gsc = a.gs()[cc];
-    const double dlam = gL.u.sol[(cc / NG) * NB + NP + cc % NG];
-    if (!on) continue;
-    a.dl()[c] = dlam;
+    if (c >= M) continue;
+    a.dl()[c] = dlam[sl];
     const int cl = cls_slot(cw, sl);
-    theta += fabs((cl == 0) ? gvv - gsc * lbv : gvv - sv);
+    theta += fabs((cl == 0) ? gvv[sl] - gsc[sl] * lbv[sl] : gvv[sl] - sv[sl]);
     double dsv = 0.0;
     if (cl == 1) {
-      const double rsl = rcp_or0(isfin(slo), sv - slo), rsu = rcp_or0(isfin(sup), sup - sv);
+      const double rsl = rcp_or0(isfin(slo[sl]), sv[sl] - slo[sl]), rsu = rcp_or0(isfin(sup[sl]), sup[sl] - sv[sl]);
       double gphis = 0.0;
-      if (isfin(slo)) gphis -= mu * rsl;
-      if (isfin(sup)) gphis += mu * rsu;
-      const double rs = gphis - lm;
-      dsv = (dlam - rs) * MPCX_RCP(vl * rsl + vu * rsu + dw);
-      gphid += (rs + lm) * dsv;
-      if (isfin(slo)) {
-        const double s_l = sv - slo;
+      if (isfin(slo[sl])) gphis -= mu * rsl;
+      if (isfin(sup[sl])) gphis += mu * rsu;
+      const double rs = gphis - lm[sl];
+      dsv = (dlam[sl] - rs) * MPCX_RCP(vl[sl] * rsl + vu[sl] * rsu + dw);
+      gphid += (rs + lm[sl]) * dsv;
+      if (isfin(slo[sl])) {
+        const double s_l = sv[sl] - slo[sl];
         if (dsv < 0) ra.take(tau * s_l, -dsv);
-        const double dv = mu * rsl - vl - (vl * rsl) * dsv;
-        if (dv < 0) rz.take(tau * vl, -dv);
+        const double dv = mu * rsl - vl[sl] - (vl[sl] * rsl) * dsv;
+        if (dv < 0) rz.take(tau * vl[sl], -dv);
         if (!bar_cached) lb.add(s_l);
       }
-      if (isfin(sup)) {
-        const double s_u = sup - sv;
+      if (isfin(sup[sl])) {
+        const double s_u = sup[sl] - sv[sl];
         if (dsv > 0) ra.take(tau * s_u, dsv);
-        const double dv = mu * rsu - vu + (vu * rsu) * dsv;
-        if (dv < 0) rz.take(tau * vu, -dv);
+        const double dv = mu * rsu - vu[sl] + (vu[sl] * rsu) * dsv;
+        if (dv < 0) rz.take(tau * vu[sl], -dv);
         if (!bar_cached) lb.add(s_u);
       }
     }
@@ -2869,17 +2913,24 @@ __device__ MPCX_HOT void line_search(const Agent a) {
       const double alpha = K.ls.alpha;
       LogSum bx;
       const unsigned vw = vcls_word();
-#pragma unroll 1
+      double lo[VS], hi[VS], xv[VS], dx[VS];  // loaded first, one batch (MPCX_PIN)
+#pragma unroll
+      for (int sl = 0; sl < VS; ++sl) {
+        const int i = lane + sl * WAVE, ii = i < NW ? i : 0;
+        lo[sl] = a.xL()[ii]; hi[sl] = a.xU()[ii]; xv[sl] = a.x()[ii]; dx[sl] = a.dx()[ii];
+      }
+#pragma unroll
+      for (int sl = 0; sl < VS; ++sl) { MPCX_PIN(lo[sl]); MPCX_PIN(hi[sl]); MPCX_PIN(xv[sl]); MPCX_PIN(dx[sl]); }
+#pragma unroll
       for (int sl = 0; sl < VS; ++sl) {
         const int i = lane + sl * WAVE;
         if (i < NW) {
           const unsigned vb = vcls_slot(vw, sl);
-          const double lo = a.xL()[i], hi = a.xU()[i];
-          const double xt = a.x()[i] + alpha * a.dx()[i];
+          const double xt = xv[sl] + alpha * dx[sl];
           gL.u.t.xt[i] = xt;
           if (vb & VFREE) {
-            if (vb & VLO) bx.add(xt - lo);
-            if (vb & VHI) bx.add(hi - xt);
+            if (vb & VLO) bx.add(xt - lo[sl]);
+            if (vb & VHI) bx.add(hi[sl] - xt);
           }
         }
       }
@@ -2896,19 +2947,29 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     double th = 0.0;
     LogSum bs;
     const unsigned cw = cls_word();
-#pragma unroll 1
+    double gsv[CS], lbv[CS], slv[CS], suv[CS], sv[CS], dsv[CS];  // loaded first, one batch (MPCX_PIN)
+#pragma unroll
+    for (int sl = 0; sl < CS; ++sl) {
+      const int c = lane + sl * WAVE, cc = c < M ? c : 0;
+      gsv[sl] = a.gs()[cc]; lbv[sl] = a.lb()[cc]; slv[sl] = a.sL()[cc]; suv[sl] = a.sU()[cc];
+      sv[sl] = a.s()[cc]; dsv[sl] = a.ds()[cc];
+    }
+#pragma unroll
+    for (int sl = 0; sl < CS; ++sl) {
+      MPCX_PIN(gsv[sl]); MPCX_PIN(lbv[sl]); MPCX_PIN(slv[sl]); MPCX_PIN(suv[sl]); MPCX_PIN(sv[sl]); MPCX_PIN(dsv[sl]);
+    }
+#pragma unroll
     for (int sl = 0; sl < CS; ++sl) {
       const int c = lane + sl * WAVE;
       if (c < M) {
-        const double gsv = a.gs()[c], lbv = a.lb()[c], slv = a.sL()[c], suv = a.sU()[c];
         const int cl = cls_slot(cw, sl);
-        const double gt = gL.u.t.gt[c] * gsv;
+        const double gt = gL.u.t.gt[c] * gsv[sl];
         gL.u.t.gt[c] = gt;
-        const double st = a.s()[c] + alpha * a.ds()[c];
-        th += fabs(cl == 0 ? gt - gsv * lbv : gt - st);
+        const double st = sv[sl] + alpha * dsv[sl];
+        th += fabs(cl == 0 ? gt - gsv[sl] * lbv[sl] : gt - st);
         if (cl == 1) {
-          if (isfin(slv)) bs.add(st - slv);
-          if (isfin(suv)) bs.add(suv - st);
+          if (isfin(slv[sl])) bs.add(st - slv[sl]);
+          if (isfin(suv[sl])) bs.add(suv[sl] - st);
         }
       }
     }
@@ -2956,57 +3017,73 @@ __device__ MPCX_HOT void line_search(const Agent a) {
 __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, double mu, double alpha, double az) {
   const int lane = lane_now();
   const double ksm = kappa_sigma * mu, mks = mu * MPCX_RCP(kappa_sigma);  // the kappa_sigma safeguard's bounds x s
-  const unsigned vw = vcls_word();
+  const unsigned vw = vcls_word(), cw = cls_word();
+  // every operand loaded first, one batch (MPCX_PIN), then the updates and stores
+  double lo[VS], hi[VS], xold[VS], dx[VS], zl[VS], zu[VS], xn[VS];
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
-    const bool on = i >= NX && i < NW;
-    const int ii = on ? i : NX;
-    const unsigned vb = vcls_slot(vw, sl);
-    const double lo = a.xL()[ii], hi = a.xU()[ii], xold = a.x()[ii], d = a.dx()[ii];
-    const double zl = a.zL()[ii], zu = a.zU()[ii];
-    const double xn = gL.u.t.xt[ii];
-    if (!(vb & VFREE)) continue;  // VFREE: NX <= i < NW, lo != hi
-    a.x()[i] = xn;
-    if (vb & VLO) {
-      const double r0 = MPCX_RCP(xold - lo);
-      const double dz = mu * r0 - zl - (zl * r0) * d;
-      const double zn = zl + az * dz, rn = MPCX_RCP(xn - lo);
-      a.zL()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
-    }
-    if (vb & VHI) {
-      const double r0 = MPCX_RCP(hi - xold);
-      const double dz = mu * r0 - zu + (zu * r0) * d;
-      const double zn = zu + az * dz, rn = MPCX_RCP(hi - xn);
-      a.zU()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
-    }
+    const int ii = (i >= NX && i < NW) ? i : NX;
+    lo[sl] = a.xL()[ii]; hi[sl] = a.xU()[ii]; xold[sl] = a.x()[ii]; dx[sl] = a.dx()[ii];
+    zl[sl] = a.zL()[ii]; zu[sl] = a.zU()[ii];
+    xn[sl] = gL.u.t.xt[ii];
   }
-  const unsigned cw = cls_word();
+  double slo[CS], sup[CS], lm[CS], dl[CS], sold[CS], dsv[CS], vl[CS], vu[CS], gt[CS];
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
     const int c = lane + sl * WAVE;
-    const bool on = c < M;
-    const int cc = on ? c : 0;
-    const double slo = a.sL()[cc], sup = a.sU()[cc];
-    const double lm = a.lam()[cc], dl = a.dl()[cc], sold = a.s()[cc], dsv = a.ds()[cc];
-    const double vl = a.vL()[cc], vu = a.vU()[cc];
-    const double gt = gL.u.t.gt[cc];
-    if (!on) continue;
-    a.lam()[c] = lm + alpha * dl;
-    a.gv()[c] = gt;
-    const double sn = sold + alpha * dsv;
+    const int cc = c < M ? c : 0;
+    slo[sl] = a.sL()[cc]; sup[sl] = a.sU()[cc]; lm[sl] = a.lam()[cc]; dl[sl] = a.dl()[cc]; sold[sl] = a.s()[cc];
+    dsv[sl] = a.ds()[cc]; vl[sl] = a.vL()[cc]; vu[sl] = a.vU()[cc];
+    gt[sl] = gL.u.t.gt[cc];
+  }
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    MPCX_PIN(lo[sl]); MPCX_PIN(hi[sl]); MPCX_PIN(xold[sl]); MPCX_PIN(dx[sl]); MPCX_PIN(zl[sl]); MPCX_PIN(zu[sl]);
+  }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    MPCX_PIN(slo[sl]); MPCX_PIN(sup[sl]); MPCX_PIN(lm[sl]); MPCX_PIN(dl[sl]); MPCX_PIN(sold[sl]);
+    MPCX_PIN(dsv[sl]); MPCX_PIN(vl[sl]); MPCX_PIN(vu[sl]);
+  }
+#pragma unroll
+  for (int sl = 0; sl < VS; ++sl) {
+    const int i = lane + sl * WAVE;
+    const unsigned vb = vcls_slot(vw, sl);
+    if (!(vb & VFREE)) continue;  // VFREE: NX <= i < NW, lo != hi
+    a.x()[i] = xn[sl];
+    if (vb & VLO) {
+      const double r0 = MPCX_RCP(xold[sl] - lo[sl]);
+      const double dz = mu * r0 - zl[sl] - (zl[sl] * r0) * dx[sl];
+      const double zn = zl[sl] + az * dz, rn = MPCX_RCP(xn[sl] - lo[sl]);
+      a.zL()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
+    }
+    if (vb & VHI) {
+      const double r0 = MPCX_RCP(hi[sl] - xold[sl]);
+      const double dz = mu * r0 - zu[sl] + (zu[sl] * r0) * dx[sl];
+      const double zn = zu[sl] + az * dz, rn = MPCX_RCP(hi[sl] - xn[sl]);
+      a.zU()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    if (c >= M) continue;
+    a.lam()[c] = lm[sl] + alpha * dl[sl];
+    a.gv()[c] = gt[sl];
+    const double sn = sold[sl] + alpha * dsv[sl];
     a.s()[c] = sn;
     if (cls_slot(cw, sl) != 1) continue;
-    if (isfin(slo)) {
-      const double r0 = MPCX_RCP(sold - slo);
-      const double dv = mu * r0 - vl - (vl * r0) * dsv;
-      const double vn = vl + az * dv, rn = MPCX_RCP(sn - slo);
+    if (isfin(slo[sl])) {
+      const double r0 = MPCX_RCP(sold[sl] - slo[sl]);
+      const double dv = mu * r0 - vl[sl] - (vl[sl] * r0) * dsv[sl];
+      const double vn = vl[sl] + az * dv, rn = MPCX_RCP(sn - slo[sl]);
       a.vL()[c] = fmax(fmin(vn, ksm * rn), mks * rn);
     }
-    if (isfin(sup)) {
-      const double r0 = MPCX_RCP(sup - sold);
-      const double dv = mu * r0 - vu + (vu * r0) * dsv;
-      const double vn = vu + az * dv, rn = MPCX_RCP(sup - sn);
+    if (isfin(sup[sl])) {
+      const double r0 = MPCX_RCP(sup[sl] - sold[sl]);
+      const double dv = mu * r0 - vu[sl] + (vu[sl] * r0) * dsv[sl];
+      const double vn = vu[sl] + az * dv, rn = MPCX_RCP(sup[sl] - sn);
       a.vU()[c] = fmax(fmin(vn, ksm * rn), mks * rn);
     }
   }
@@ -3051,15 +3128,39 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
     double dmax = 0.0, dmax_u = 0.0, pmax = 0.0, vmax_u = 0.0, pmx = -INFINITY, pmn = INFINITY;
     double lsum = 0.0, zsum = 0.0;
     int nz = 0;
-    const unsigned vw = vcls_word();
+    const unsigned vw = vcls_word(), cw = cls_word();
+    // every operand loaded first, one batch (MPCX_PIN: one memory round trip instead of one per slot)
+    double lo_[VS], hi_[VS], xv_[VS], zl_[VS], zu_[VS], gr_[VS], jt_[VS];
 #pragma unroll
     for (int sl = 0; sl < VS; ++sl) {
       const int i = lane + sl * WAVE;
       const int ii = (i >= NX && i < NW) ? i : NX;
+      lo_[sl] = a.xL()[ii]; hi_[sl] = a.xU()[ii]; xv_[sl] = a.x()[ii]; zl_[sl] = a.zL()[ii]; zu_[sl] = a.zU()[ii];
+      gr_[sl] = acc_grad(a, ii); jt_[sl] = acc_jtl(a, ii);
+    }
+    double lb_[CS], sl_[CS], su_[CS], gs_[CS], lm_[CS], gv_[CS], sv_[CS], vl_[CS], vu_[CS];
+#pragma unroll
+    for (int sl = 0; sl < CS; ++sl) {
+      const int c = lane + sl * WAVE;
+      const int cc = c < M ? c : 0;
+      lb_[sl] = a.lb()[cc]; sl_[sl] = a.sL()[cc]; su_[sl] = a.sU()[cc]; gs_[sl] = a.gs()[cc]; lm_[sl] = a.lam()[cc];
+      gv_[sl] = a.gv()[cc]; sv_[sl] = a.s()[cc]; vl_[sl] = a.vL()[cc]; vu_[sl] = a.vU()[cc];
+    }
+#pragma unroll
+    for (int sl = 0; sl < VS; ++sl) {
+      MPCX_PIN(lo_[sl]); MPCX_PIN(hi_[sl]); MPCX_PIN(xv_[sl]); MPCX_PIN(zl_[sl]); MPCX_PIN(zu_[sl]);
+      MPCX_PIN(gr_[sl]); MPCX_PIN(jt_[sl]);
+    }
+#pragma unroll
+    for (int sl = 0; sl < CS; ++sl) {
+      MPCX_PIN(lb_[sl]); MPCX_PIN(sl_[sl]); MPCX_PIN(su_[sl]); MPCX_PIN(gs_[sl]); MPCX_PIN(lm_[sl]);
+      MPCX_PIN(gv_[sl]); MPCX_PIN(sv_[sl]); MPCX_PIN(vl_[sl]); MPCX_PIN(vu_[sl]);
+    }
+#pragma unroll
+    for (int sl = 0; sl < VS; ++sl) {
       const unsigned vb = vcls_slot(vw, sl);
-      const double lo = a.xL()[ii], hi = a.xU()[ii];
-      double xv = a.x()[ii], zl = a.zL()[ii], zu = a.zU()[ii];
-      const double gr = acc_grad(a, ii), jt = acc_jtl(a, ii);
+      const double lo = lo_[sl], hi = hi_[sl], xv = xv_[sl], zl = zl_[sl], zu = zu_[sl];
+      const double gr = gr_[sl], jt = jt_[sl];
       // on: NX <= i < NW and lo != hi; a fixed variable (lo == hi: every x_0 entry) has no barrier
       // terms (its psx is stored as 0)
       const bool on = (vb & VFREE) != 0u;
@@ -3075,14 +3176,11 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
         if (vb & VHI) { const double pr = (hi - xv) * zu; pmx = fmax(pmx, pr); pmn = fmin(pmn, pr); zsum += fabs(zu); nz++; }
       }
     }
-    const unsigned cw = cls_word();
 #pragma unroll
     for (int sl = 0; sl < CS; ++sl) {
       const int c = lane + sl * WAVE;
-      const int cc = c < M ? c : 0;
-      const double lbv = a.lb()[cc], slo = a.sL()[cc], sup = a.sU()[cc];
-      const double gsc = a.gs()[cc], lm = a.lam()[cc];
-      double gvv = a.gv()[cc], sv = a.s()[cc], vl = a.vL()[cc], vu = a.vU()[cc];
+      const double lbv = lb_[sl], slo = sl_[sl], sup = su_[sl], gsc = gs_[sl], lm = lm_[sl];
+      const double gvv = gv_[sl], sv = sv_[sl], vl = vl_[sl], vu = vu_[sl];
       const int cl = cls_slot(cw, sl);
       {
         const double rsl = rcp_or0(cl == 1 && isfin(slo), sv - slo), rsu = rcp_or0(cl == 1 && isfin(sup), sup - sv);

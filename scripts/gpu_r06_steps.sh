@@ -77,6 +77,20 @@ step_s4() {
   echo "tests exit $rc, bench exit $?"
 }
 
+step_s5() {
+  # r06/s5: each vector phase's operands in one pinned batch (MPCX_PIN: iteration head, step recovery,
+  # line search, acceptance; the solve's operator loads) against the compiler's placement (nopin) and
+  # against the no-drain kernel f70845c (rev): C3, C1, the C4 room fleet, MHE, the C2 air handler
+  mkdir -p gpurun_out/s5
+  timeout -k 10 300 python -u scripts/variants.py run base nopin rev base nopin rev > gpurun_out/s5/var_c3.txt 2>&1 || exit $?
+  AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_nopin lds_rev48 lds_base lds_nopin lds_rev48 > gpurun_out/s5/var_c1.txt 2>&1 || exit $?
+  MODEL=exchange_room AGENTS=13108 timeout -k 10 300 python -u scripts/variants.py run base nopin rev base nopin rev > gpurun_out/s5/var_c4room.txt 2>&1 || exit $?
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base nopin rev base nopin rev > gpurun_out/s5/var_mhe.txt 2>&1 || exit $?
+  MODEL=admm_ahu AGENTS=1024 timeout -k 10 300 python -u scripts/variants.py run base nopin rev base nopin rev > gpurun_out/s5/var_ahu.txt 2>&1 || exit $?
+  AGENTS=4096 timeout -k 10 400 python -u scripts/prof_phases.py > gpurun_out/s5/phases_c3.txt 2>&1
+  echo "s5 exit $?"
+}
+
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }
 "$fn"

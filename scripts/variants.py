@@ -103,6 +103,9 @@ VARIANTS = {
     # r06: a revision's small-fleet build with the working tree's filter size (48 in LDS), so that its
     # workspace matches the main build it is loaded beside (mpcx_problem_small_fleet checks it)
     "lds_rev48": (["-DMPCX_WS_LDS", "-DMPCX_MAXF=48"], "REV:" + os.environ.get("REV", "HEAD")),
+    # r06: the vector phases' operands as the compiler places them (no MPCX_PIN batches)
+    "nopin": (["-DMPCX_NO_PIN"], None),
+    "lds_nopin": (["-DMPCX_WS_LDS", "-DMPCX_NO_PIN"], None),
 }
 
 

@@ -91,6 +91,19 @@ step_s5() {
   echo "s5 exit $?"
 }
 
+step_s6() {
+  # r06/s6: the vector phases' batches within a leaf phase's register budget (recover / accept: two
+  # batches, variables then constraints) against the kernel of f70845c (rev) and without the iteration
+  # head's pinned batch (nopin_head): C3, C1, the C4 room fleet, MHE, the C2 air handler
+  mkdir -p gpurun_out/s6
+  timeout -k 10 300 python -u scripts/variants.py run base nopin_head rev base nopin_head rev > gpurun_out/s6/var_c3.txt 2>&1 || exit $?
+  AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_nopin_head lds_rev48 lds_base lds_nopin_head lds_rev48 > gpurun_out/s6/var_c1.txt 2>&1 || exit $?
+  MODEL=exchange_room AGENTS=13108 timeout -k 10 300 python -u scripts/variants.py run base nopin_head rev base nopin_head rev > gpurun_out/s6/var_c4room.txt 2>&1 || exit $?
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base nopin_head rev base nopin_head rev > gpurun_out/s6/var_mhe.txt 2>&1 || exit $?
+  MODEL=admm_ahu AGENTS=1024 timeout -k 10 300 python -u scripts/variants.py run base nopin_head rev base nopin_head rev > gpurun_out/s6/var_ahu.txt 2>&1
+  echo "s6 exit $?"
+}
+
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }
 "$fn"

@@ -1,5 +1,5 @@
 """Per-iteration view of a coordinated ADMM round from a rocprofv3 ``--kernel-trace`` run: the
-iterations are cut at ``mpcx_admm_block_stop`` (one per iteration, after the residual totals);
+iterations are cut at ``mpcx_admm_block_stop`` (kernel k_block_stop) (one per iteration, after the residual totals);
 for each iteration of the last ``ROUNDS`` rounds: wall span (from the previous stop's end), GPU busy
 time (union of kernel intervals), the solve launches' durations, and the kernel count -- is a
 straggler iteration bound by its solves or by the launches around them?
@@ -17,7 +17,7 @@ def main(d, rounds=1):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                          int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)))
     rows.sort()
-    stops = [i for i, r in enumerate(rows) if "mpcx_admm_block_stop" in r[2]]
+    stops = [i for i, r in enumerate(rows) if "k_block_stop" in r[2]]
     # a round starts with the stop of iteration 0 (the clock stamp): the stops whose previous kernel
     # is not a block_expand of the previous iteration are hard to tell apart, so rounds are cut at
     # gaps > 5 ms between consecutive stops (the untimed plant step between control steps)

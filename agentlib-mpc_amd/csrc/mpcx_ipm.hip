@@ -343,6 +343,11 @@ __device__ __forceinline__ int lane_now() {
 #else  // diagnostics (A/B): the compiler places the loads
 #define MPCX_PIN(x) (void)0
 #endif
+#ifndef MPCX_NO_PIN_HEAD  // the iteration head's batch (inlined into the kernel body)
+#define MPCX_PIN_HEAD(x) MPCX_PIN(x)
+#else  // diagnostics (A/B)
+#define MPCX_PIN_HEAD(x) (void)0
+#endif
 
 template <int GG>
 __device__ __forceinline__ double gmax(double v) {
@@ -2775,22 +2780,8 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
     gr[sl] = acc_grad(a, ii);
     sx[sl] = gL.u.sol[((ii - NX) / NP) * NB + (ii - NX) % NP];
   }
-  double lbv[CS], slo[CS], sup[CS], sv[CS], lm[CS], vl[CS], vu[CS], gvv[CS], gsc[CS], dlam[CS];
-#pragma unroll
-  for (int sl = 0; sl < CS; ++sl) {
-    const int c = lane + sl * WAVE;
-    const int cc = c < M ? c : 0;
-    lbv[sl] = a.lb()[cc]; slo[sl] = a.sL()[cc]; sup[sl] = a.sU()[cc]; sv[sl] = a.s()[cc]; lm[sl] = a.lam()[cc];
-    vl[sl] = a.vL()[cc]; vu[sl] = a.vU()[cc]; gvv[sl] = a.gv()[cc]; gsc[sl] = a.gs()[cc];
-    dlam[sl] = gL.u.sol[(cc / NG) * NB + NP + cc % NG];
-  }
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) { MPCX_PIN(lo[sl]); MPCX_PIN(hi[sl]); MPCX_PIN(xv[sl]); MPCX_PIN(zl[sl]); MPCX_PIN(zu[sl]); MPCX_PIN(gr[sl]); }
-#pragma unroll
-  for (int sl = 0; sl < CS; ++sl) {
-    MPCX_PIN(lbv[sl]); MPCX_PIN(slo[sl]); MPCX_PIN(sup[sl]); MPCX_PIN(sv[sl]); MPCX_PIN(lm[sl]);
-    MPCX_PIN(vl[sl]); MPCX_PIN(vu[sl]); MPCX_PIN(gvv[sl]); MPCX_PIN(gsc[sl]);
-  }
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     const int i = lane + sl * WAVE;
@@ -2818,6 +2809,22 @@ __device__ MPCX_HOT StepInfo recover_step(const Agent a, double mu, double tau, 
       if (!bar_cached) lb.add(s_u);
     }
     gphid += gphi * d;
+  }
+  // the constraints' operands: a second batch (both at once would need more registers than a leaf
+  // phase has without saving callee-saved ones: 22 scratch saves and restores per call, C3 +4 %, r06/s5)
+  double lbv[CS], slo[CS], sup[CS], sv[CS], lm[CS], vl[CS], vu[CS], gvv[CS], gsc[CS], dlam[CS];
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const int cc = c < M ? c : 0;
+    lbv[sl] = a.lb()[cc]; slo[sl] = a.sL()[cc]; sup[sl] = a.sU()[cc]; sv[sl] = a.s()[cc]; lm[sl] = a.lam()[cc];
+    vl[sl] = a.vL()[cc]; vu[sl] = a.vU()[cc]; gvv[sl] = a.gv()[cc]; gsc[sl] = a.gs()[cc];
+    dlam[sl] = gL.u.sol[(cc / NG) * NB + NP + cc % NG];
+  }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    MPCX_PIN(lbv[sl]); MPCX_PIN(slo[sl]); MPCX_PIN(sup[sl]); MPCX_PIN(sv[sl]); MPCX_PIN(lm[sl]);
+    MPCX_PIN(vl[sl]); MPCX_PIN(vu[sl]); MPCX_PIN(gvv[sl]); MPCX_PIN(gsc[sl]);
   }
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
@@ -3028,23 +3035,9 @@ __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, do
     zl[sl] = a.zL()[ii]; zu[sl] = a.zU()[ii];
     xn[sl] = gL.u.t.xt[ii];
   }
-  double slo[CS], sup[CS], lm[CS], dl[CS], sold[CS], dsv[CS], vl[CS], vu[CS], gt[CS];
-#pragma unroll
-  for (int sl = 0; sl < CS; ++sl) {
-    const int c = lane + sl * WAVE;
-    const int cc = c < M ? c : 0;
-    slo[sl] = a.sL()[cc]; sup[sl] = a.sU()[cc]; lm[sl] = a.lam()[cc]; dl[sl] = a.dl()[cc]; sold[sl] = a.s()[cc];
-    dsv[sl] = a.ds()[cc]; vl[sl] = a.vL()[cc]; vu[sl] = a.vU()[cc];
-    gt[sl] = gL.u.t.gt[cc];
-  }
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
     MPCX_PIN(lo[sl]); MPCX_PIN(hi[sl]); MPCX_PIN(xold[sl]); MPCX_PIN(dx[sl]); MPCX_PIN(zl[sl]); MPCX_PIN(zu[sl]);
-  }
-#pragma unroll
-  for (int sl = 0; sl < CS; ++sl) {
-    MPCX_PIN(slo[sl]); MPCX_PIN(sup[sl]); MPCX_PIN(lm[sl]); MPCX_PIN(dl[sl]); MPCX_PIN(sold[sl]);
-    MPCX_PIN(dsv[sl]); MPCX_PIN(vl[sl]); MPCX_PIN(vu[sl]);
   }
 #pragma unroll
   for (int sl = 0; sl < VS; ++sl) {
@@ -3064,6 +3057,21 @@ __device__ MPCX_HOT void accept_step(const Agent a, const double kappa_sigma, do
       const double zn = zu[sl] + az * dz, rn = MPCX_RCP(hi[sl] - xn[sl]);
       a.zU()[i] = fmax(fmin(zn, ksm * rn), mks * rn);
     }
+  }
+  // the constraints' operands: a second batch (register budget of a leaf phase, see recover_step)
+  double slo[CS], sup[CS], lm[CS], dl[CS], sold[CS], dsv[CS], vl[CS], vu[CS], gt[CS];
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    const int c = lane + sl * WAVE;
+    const int cc = c < M ? c : 0;
+    slo[sl] = a.sL()[cc]; sup[sl] = a.sU()[cc]; lm[sl] = a.lam()[cc]; dl[sl] = a.dl()[cc]; sold[sl] = a.s()[cc];
+    dsv[sl] = a.ds()[cc]; vl[sl] = a.vL()[cc]; vu[sl] = a.vU()[cc];
+    gt[sl] = gL.u.t.gt[cc];
+  }
+#pragma unroll
+  for (int sl = 0; sl < CS; ++sl) {
+    MPCX_PIN(slo[sl]); MPCX_PIN(sup[sl]); MPCX_PIN(lm[sl]); MPCX_PIN(dl[sl]); MPCX_PIN(sold[sl]);
+    MPCX_PIN(dsv[sl]); MPCX_PIN(vl[sl]); MPCX_PIN(vu[sl]);
   }
 #pragma unroll
   for (int sl = 0; sl < CS; ++sl) {
@@ -3148,13 +3156,13 @@ __device__ __attribute__((always_inline)) int iter_head(const Agent a) {
     }
 #pragma unroll
     for (int sl = 0; sl < VS; ++sl) {
-      MPCX_PIN(lo_[sl]); MPCX_PIN(hi_[sl]); MPCX_PIN(xv_[sl]); MPCX_PIN(zl_[sl]); MPCX_PIN(zu_[sl]);
-      MPCX_PIN(gr_[sl]); MPCX_PIN(jt_[sl]);
+      MPCX_PIN_HEAD(lo_[sl]); MPCX_PIN_HEAD(hi_[sl]); MPCX_PIN_HEAD(xv_[sl]); MPCX_PIN_HEAD(zl_[sl]); MPCX_PIN_HEAD(zu_[sl]);
+      MPCX_PIN_HEAD(gr_[sl]); MPCX_PIN_HEAD(jt_[sl]);
     }
 #pragma unroll
     for (int sl = 0; sl < CS; ++sl) {
-      MPCX_PIN(lb_[sl]); MPCX_PIN(sl_[sl]); MPCX_PIN(su_[sl]); MPCX_PIN(gs_[sl]); MPCX_PIN(lm_[sl]);
-      MPCX_PIN(gv_[sl]); MPCX_PIN(sv_[sl]); MPCX_PIN(vl_[sl]); MPCX_PIN(vu_[sl]);
+      MPCX_PIN_HEAD(lb_[sl]); MPCX_PIN_HEAD(sl_[sl]); MPCX_PIN_HEAD(su_[sl]); MPCX_PIN_HEAD(gs_[sl]); MPCX_PIN_HEAD(lm_[sl]);
+      MPCX_PIN_HEAD(gv_[sl]); MPCX_PIN_HEAD(sv_[sl]); MPCX_PIN_HEAD(vl_[sl]); MPCX_PIN_HEAD(vu_[sl]);
     }
 #pragma unroll
     for (int sl = 0; sl < VS; ++sl) {

@@ -106,8 +106,8 @@ VARIANTS = {
     # r06: the vector phases' operands as the compiler places them (no MPCX_PIN batches)
     "nopin": (["-DMPCX_NO_PIN"], None),
     "lds_nopin": (["-DMPCX_WS_LDS", "-DMPCX_NO_PIN"], None),
-    "nopin_head": (["-DMPCX_NO_PIN_HEAD"], None),
-    "lds_nopin_head": (["-DMPCX_WS_LDS", "-DMPCX_NO_PIN_HEAD"], None),
+    "pin_head": (["-DMPCX_PIN_HEAD_BATCH"], None),
+    "lds_pin_head": (["-DMPCX_WS_LDS", "-DMPCX_PIN_HEAD_BATCH"], None),
 }
 
 

@@ -2994,7 +2994,10 @@ __device__ MPCX_HOT void line_search(const Agent a) {
     K.ls.tr = tr;
     K.ls.bar = trial_bar;
     K.ls.trials += 1;
-    bool okt = (tr.theta <= K.theta_max) && (tr.phi == tr.phi);
+    // a trial whose barrier function is not finite (a slack rounded to 0: phi = +inf) is cut back like
+    // an evaluation error (IPOPT BacktrackingLineSearch; oracle/ipm.py rejects it) -- the theta-reduction
+    // branch below would otherwise take it and the next iterate's barrier terms are inf / NaN
+    bool okt = (tr.theta <= K.theta_max) && isfin(tr.phi);
     {  // filter test, one entry per lane (MAXF <= 64): one LDS read instead of nfilt in sequence
       const int j = lane_now();
       const bool dom = j < K.nfilt && tr.theta >= gL.fth[j < MAXF ? j : 0] && tr.phi >= gL.fph[j < MAXF ? j : 0];
@@ -3611,6 +3614,29 @@ __device__ __noinline__ void resto_start(const Agent a) {
   }
   pn = wsum(pn);
   th = wsum(th);
+#ifdef MPCX_TRACE_IT  // diagnostics: the smallest slacks at the restoration start
+  {
+    double mxl = INFINITY, mxu = INFINITY, msl = INFINITY, msu = INFINITY, mp = INFINITY, mn = INFINITY;
+    for (int i = NX + lane; i < NW; i += WAVE) {
+      const double lo = a.xL()[i], hi = a.xU()[i], xv = a.x()[i];
+      if (lo == hi) continue;
+      if (isfin(lo)) mxl = fmin(mxl, xv - lo);
+      if (isfin(hi)) mxu = fmin(mxu, hi - xv);
+    }
+    for (int c = lane; c < M; c += WAVE) {
+      const double slo = a.sL()[c], sup = a.sU()[c], sv = a.s()[c];
+      if (cls_of(a.lb()[c], a.ub()[c], slo, sup) == 1) {
+        if (isfin(slo)) msl = fmin(msl, sv - slo);
+        if (isfin(sup)) msu = fmin(msu, sup - sv);
+      }
+      mp = fmin(mp, a.rp()[c]); mn = fmin(mn, a.rn()[c]);
+    }
+    mxl = wmin(mxl); mxu = wmin(mxu); msl = wmin(msl); msu = wmin(msu); mp = wmin(mp); mn = wmin(mn);
+    if (lane == 0)
+      printf("mpcx resto-start it=%d mu_r=%.6e pn=%.6e th=%.6e min x-lo=%.3e hi-x=%.3e s-sL=%.3e sU-s=%.3e p=%.3e n=%.3e\n",
+             K.it, mu_r, pn, th, mxl, mxu, msl, msu, mp, mn);
+  }
+#endif
   K.square_r = (wsumi(nfree) + 2 * M) == wsumi(neq);
   sync();
   eval_gj_ws(a, a.x(), gL.want_sdh);  // (J~^T lambda) with lambda = 0
@@ -4172,7 +4198,10 @@ __device__ __noinline__ void line_search_resto(const Agent a) {
     tr.phi = tr.fr - mu * (K.barx + wsum(bar));
     K.ls.tr = tr;
     K.ls.trials += 1;
-    bool okt = (tr.theta <= K.theta_max) && (tr.phi == tr.phi);
+    // a trial whose barrier function is not finite (a slack rounded to 0: phi = +inf) is cut back like
+    // an evaluation error (IPOPT BacktrackingLineSearch; oracle/ipm.py rejects it) -- the theta-reduction
+    // branch below would otherwise take it and the next iterate's barrier terms are inf / NaN
+    bool okt = (tr.theta <= K.theta_max) && isfin(tr.phi);
     {  // filter test, one entry per lane (MAXF <= 64): one LDS read instead of nfilt in sequence
       const int j = lane_now();
       const bool dom = j < K.nfilt && tr.theta >= gL.fth[j < MAXF ? j : 0] && tr.phi >= gL.fph[j < MAXF ? j : 0];
@@ -4235,6 +4264,13 @@ __device__ __noinline__ int resto_tail(const Agent a) {
   line_search_resto(a);
   const LSResult ls = K.ls;
   K.n_trials += ls.trials;
+#ifdef MPCX_TRACE_IT
+  if (lane_now() == 0)
+    printf("mpcx resto-ls it=%d acc=%d mu=%.6e theta=%.6e phi=%.14e gphid=%.6e amin=%.3e amax=%.3e alpha=%.3e trials=%d "
+           "tr.theta=%.6e tr.phi=%.14e thmin=%.3e thmax=%.3e\n", K.it, ls.accepted, K.mu, K.st.theta,
+           K.fx - K.mu * K.st.barrier, K.st.gphid, K.amin, K.st.amax, ls.alpha, ls.trials, ls.tr.theta, ls.tr.phi,
+           K.theta_min, K.theta_max);
+#endif
   if (!ls.accepted) { K.status = MPCX_RESTORATION_FAILED; return 1; }
   if (!ls.ftype) filter_augment(argp);
   K.fx = ls.tr.fr;
@@ -4371,6 +4407,22 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
 #define KARGP ((KArgs*)__builtin_amdgcn_kernarg_segment_ptr())
 #pragma unroll 1
   for (;;) {
+#ifdef MPCX_TRACE_IT  // diagnostics (scripts/resto_ab.py trace): the previous iteration's step, per iteration
+    {
+      double mxl = INFINITY;
+      int arg = -1;
+      for (int i = NX + lane; i < NW; i += WAVE) {
+        const double lo = a.xL()[i];
+        if (lo != a.xU()[i] && isfin(lo) && a.x()[i] - lo < mxl) { mxl = a.x()[i] - lo; arg = i; }
+      }
+      const double m = wmin(mxl);
+      const int am = (int)wmax(mxl == m ? (double)arg : -1.0);
+      if (lane == 0 && agent == 0)
+        printf("mpcx it=%d resto=%d soft=%d mu=%.6e fx=%.14e theta=%.6e amax=%.3e alpha=%.4e trials=%d refine=%d dw=%.3e "
+               "nfilt=%d min x-lo=%.3e at %d\n", K.it, K.resto, K.soft, K.mu, K.fx, K.st.theta, K.st.amax, K.ls.alpha,
+               K.ls.trials, K.n_refine, K.dw, K.nfilt, m, am);
+    }
+#endif
     if (K.resto) {
       const int hr = iter_head_resto(a);
       if (hr == 1) break;
@@ -4488,6 +4540,9 @@ extern "C" __global__ void __launch_bounds__(64, MIN_WAVES) mpcx_ipm_solve(Args 
     PROF(9);
   }
 #undef KARGP
+#ifdef MPCX_TRACE_IT
+  if (lane == 0 && agent == 0) printf("mpcx end it=%d resto=%d status=%d\n", K.it, K.resto, K.status);
+#endif
   const double obj_scale = K.obj_scale;
 
   // ---- outputs ----------------------------------------------------------------

@@ -1234,7 +1234,7 @@ static int ipm_run(const model_t* m, const double* p, const double* lbw, const d
       for (int ls = 0; ls < 64; ++ls) {
         TRIAL(alpha, az);
         const double tht = theta_of(w, w->gt, w->st), pht = ft - mu * barrier_of(w, w->xt, w->st);
-        int okt = tht <= theta_max && pht == pht && filter_accepts(&F, tht, pht);
+        int okt = tht <= theta_max && isfin(pht) && filter_accepts(&F, tht, pht);  /* ipm.py: finite phi */
         if (okt) {
           const int sw = gphid < 0 && alpha * pow(-gphid, 2.3) > pow(theta, 1.1);
           if (theta <= theta_min && sw) { okt = pht <= phi + 1e-8 * alpha * gphid; ftype = 1; }

@@ -34,6 +34,8 @@ ZERO_PIVOT = 1e-20  # same constant as csrc/mpcx_ipm.hip
 
 #: diagnostics only: a list receives the trials of the last line search (scripts/resto_diag.py)
 LS_TRACE = None
+KKT_HOOK = None  # diagnostics: called with (iteration, in restoration, dw, dc, K, npos, nneg, nzero)
+IT_TRACE = None  # diagnostics: a list to collect (iteration, in restoration, mu, objective, refinement steps)
 
 
 @dataclasses.dataclass
@@ -442,6 +444,8 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
         counts["max_filter"] = max(counts["max_filter"], len(filt))
 
     while True:
+        if IT_TRACE is not None:  # diagnostics (scripts/resto_ab.py trace): one row per iteration
+            IT_TRACE.append((it, int(inner is not None), mu, fx, counts.get("refine", 0)))
         if inner is not None and inner.check(x, s):
             status = "Resto_Return"
             break
@@ -513,6 +517,8 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
             npos = int(np.sum(ev > 0))
             nneg = int(np.sum(ev < 0))
             nzero = len(ev) - npos - nneg
+            if KKT_HOOK is not None:  # diagnostics: the KKT matrices of an iteration's inertia tests
+                KKT_HOOK(it, inner is not None, dw, dc, K, npos, nneg, nzero)
             sol = None
             if nzero == 0:
                 rhs = np.concatenate([rhs_x, rhs_l])
@@ -546,6 +552,8 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
                         raise RuntimeError("inertia correction failed")
                     dc = o.delta_c_bar * mu ** o.kappa_c
                     dw = o.delta_w_first if delta_w_last == 0 else max(o.delta_w_min, o.kappa_w_minus * delta_w_last)
+        if IT_TRACE is not None:
+            IT_TRACE.append(("dw", it, int(inner is not None), dw, dc))
         if inner is not None:
             # IPOPT PDFullSpaceSolver: iterative refinement of the step on the full system (here
             # the restoration NLP's, p and n explicit)
@@ -640,6 +648,9 @@ def _solve(nlp, x0, lbx, ubx, lbg, ubg, o, record, inner: Optional[_Inner] = Non
                 alpha *= 0.5
                 if alpha < a_min:
                     break
+            if IT_TRACE is not None and inner is not None:
+                IT_TRACE.append(("ls", it, int(accepted), mu, theta, phi, gphi_d, a_min, a_max, alpha, theta_min,
+                                 theta_max))
             if not accepted and inner is not None:
                 # no restoration inside the restoration phase (IPOPT: "Restoration phase in
                 # the restoration phase failed")

@@ -108,6 +108,8 @@ VARIANTS = {
     "lds_nopin": (["-DMPCX_WS_LDS", "-DMPCX_NO_PIN"], None),
     "pin_head": (["-DMPCX_PIN_HEAD_BATCH"], None),
     "lds_pin_head": (["-DMPCX_WS_LDS", "-DMPCX_PIN_HEAD_BATCH"], None),
+    # r06: agents per CU past the one-round rule (MHE: 4 -> 5, two stage rounds)
+    "apc5": (["-DMPCX_APC=5"], None),
 }
 
 

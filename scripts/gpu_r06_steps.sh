@@ -104,22 +104,26 @@ step_s6() {
   echo "s6 exit $?"
 }
 
-step_s7() {
+record() {
+  local d=gpurun_out/$1
   # r06/s7: record on the committed kernel (two-batch vector phases, head left to the compiler): GPU
   # suite, smoke, PMC passes of the C3 leg, the default bench line, kernel-trace stats of the C3 / MHE /
   # NARX legs
-  mkdir -p gpurun_out/s7/pmc
-  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s7/gpu_tests.txt 2>&1
+  mkdir -p $d/pmc
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rfE --timeout 300 --timeout-method thread > $d/gpu_tests.txt 2>&1
   rc=$?
   [ $rc -ne 0 ] && [ $rc -ne 1 ] && { echo "tests exit $rc"; exit $rc; }
-  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s7/smoke.txt 2>&1 || exit $?
-  PMC_OUT=gpurun_out/s7/pmc bash scripts/gpu_pmc.sh || exit $?
-  timeout -k 10 900 python -u bench.py > gpurun_out/s7/bench.json 2> gpurun_out/s7/bench.err || exit $?
-  rm -rf gpurun_out/s7/prof
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s7/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --admm-agents 0 --c2-blocks 0 --c5-blocks 0 > gpurun_out/s7/prof_bench.json 2> gpurun_out/s7/prof.err || exit $?
-  python scripts/trace_summary.py gpurun_out/s7/prof gpurun_out/s7/kernel_trace_summary.txt > /dev/null
-  echo "tests exit $rc, s7 exit $?"
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $d/smoke.txt 2>&1 || exit $?
+  PMC_OUT=$d/pmc bash scripts/gpu_pmc.sh || exit $?
+  timeout -k 10 900 python -u bench.py > $d/bench.json 2> $d/bench.err || exit $?
+  rm -rf $d/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --admm-agents 0 --c2-blocks 0 --c5-blocks 0 > $d/prof_bench.json 2> $d/prof.err || exit $?
+  python scripts/trace_summary.py $d/prof $d/kernel_trace_summary.txt > /dev/null
+  echo "tests exit $rc, record exit $?"
 }
+
+step_s7() { record s7; }
+step_s8() { record s8; }  # the record again after the non-finite-trial fix
 
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }

@@ -331,7 +331,7 @@ __device__ __forceinline__ void wsync() {
 __device__ __forceinline__ int lane_now() {
   int l;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
+  return l & (WAVE - 1);  // the range for the compiler: lane-derived offsets are known non-negative
 }
 
 // Pin a loaded operand: the empty asm "uses" it here, so the compiler issues the load before this

@@ -122,6 +122,18 @@ record() {
   echo "tests exit $rc, record exit $?"
 }
 
+step_s9() {
+  # r06/s9: the lane id masked to its range (lane_now: l & 63 -- lane-derived offsets known
+  # non-negative, so loads take the SGPR-base + 32-bit offset form) against the committed kernel (rev)
+  mkdir -p gpurun_out/s9
+  timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s9/var_c3.txt 2>&1 || exit $?
+  AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_rev48 lds_base lds_rev48 > gpurun_out/s9/var_c1.txt 2>&1 || exit $?
+  MODEL=exchange_room AGENTS=13108 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s9/var_c4room.txt 2>&1 || exit $?
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s9/var_mhe.txt 2>&1 || exit $?
+  MODEL=admm_ahu AGENTS=1024 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s9/var_ahu.txt 2>&1
+  echo "s9 exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 

@@ -136,6 +136,7 @@ step_s9() {
 
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
+step_s10() { record s10; }  # the record on the masked-lane kernel
 
 fn="step_$1"
 declare -F "$fn" > /dev/null || { echo "unknown step $1"; exit 2; }

@@ -46,7 +46,7 @@ from typing import Dict, List, Optional, Sequence, Union
 import numpy as np
 
 from agentlib_mpc_amd.data_structures import admm_datatypes as adt
-from agentlib_mpc_amd.runtime.native import ADMM_CONTROL, ADMM_TOTALS, STATS_BYTES, admm_reduce_count
+from agentlib_mpc_amd.runtime.native import ADMM_CONTROL, ADMM_TOTALS, STATS_BYTES, admm_reduce_count, dedicated_streams
 
 CONSENSUS = "consensus"
 EXCHANGE = "exchange"
@@ -460,10 +460,19 @@ class ADMMFleet:
         #: None (the default) records nothing
         self.solve_trace = None
         #: the classes' solves of an iteration on one HIP stream each (see _solve_all);
-        #: MPCX_FLEET_STREAMS=0 keeps them on the caller's stream, one after the other
+        #: MPCX_FLEET_STREAMS=0 keeps them on the caller's stream.  MPCX_FLEET_DEDICATED=1 gives each
+        #: class stream a hardware queue of its own (C ABI v15): the classes' solves then overlap, but
+        #: every launch of the iteration's main-stream kernels waits ~15 us more with three queues
+        #: active, and the legs measured slower (r06/s11: C4 663 vs 755 it/s, C5 376 vs 420, C2
+        #: level) -- so ordinary streams (sharing the runtime's queues) stay the default
         self.concurrent_classes = (dev.type == "cuda" and len(self.classes) > 1
                                    and os.environ.get("MPCX_FLEET_STREAMS", "1") != "0")
-        self._class_streams = [t.cuda.Stream(device=dev) for _ in self.classes] if self.concurrent_classes else None
+        if not self.concurrent_classes:
+            self._class_streams = None
+        elif os.environ.get("MPCX_FLEET_DEDICATED", "0") == "1":
+            self._class_streams = dedicated_streams(len(self.classes), dev)
+        else:
+            self._class_streams = [t.cuda.Stream(device=dev) for _ in self.classes]
         self._ev_solve = t.cuda.Event() if self.concurrent_classes else None
         #: the lead class (most agents x NLP size) is issued first and the others wait for its
         #: pre-solve moves (see _solve_all); MPCX_FLEET_LEAD=0: every class starts at once

@@ -94,7 +94,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_scatter_rows_multi", "mpcx_gather_rows_multi",
     "mpcx_allreduce_register", "mpcx_allreduce_register_fn", "mpcx_allreduce_unregister", "mpcx_allreduce_kind",
     "mpcx_admm_allreduce", "mpcx_allreduce_calls", "mpcx_rccl_unique_id", "mpcx_rccl_comm_init",
-    "mpcx_rccl_comm_init_file", "mpcx_rccl_comm_destroy",
+    "mpcx_rccl_comm_init_file", "mpcx_rccl_comm_destroy", "mpcx_stream_create_dedicated", "mpcx_stream_destroy",
 ]
 MOVE_DESC = 4  # MPCX_MOVE_DESC: int64 words per descriptor of the fused row moves (C ABI v12)
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
@@ -239,10 +239,39 @@ def load_library():
         lib.mpcx_rccl_comm_init.argtypes = [ctypes.c_char_p, i32, i32, vp, ctypes.POINTER(vp)]
         lib.mpcx_rccl_comm_init_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i32, i32, i32, ctypes.POINTER(vp)]
         lib.mpcx_rccl_comm_destroy.argtypes = [ctypes.c_char_p, vp]
+        # streams with a hardware queue of their own (C ABI v15): the fleet's class streams
+        lib.mpcx_stream_create_dedicated.argtypes = [ctypes.POINTER(vp)]
+        lib.mpcx_stream_destroy.argtypes = [vp]
         for name in EXPORTED_SYMBOLS:
             getattr(lib, name)  # raises AttributeError if a symbol is missing
         _lib = lib
         return lib
+
+
+_DEDICATED: dict = {}
+
+
+def dedicated_streams(n: int, device) -> list:
+    """``n`` HIP streams with a hardware queue of their own each (C ABI v15,
+    ``mpcx_stream_create_dedicated``), as ``torch.cuda.ExternalStream``.  Ordinary streams share
+    the runtime's few hardware queues, and two classes' solves on one queue run one after the
+    other.  A per-device pool for the process: a fleet takes the first ``n``, so the process holds
+    as many dedicated queues as its widest fleet has classes (fleets of one process run one at a
+    time; sharing a stream only orders their launches).  The streams live as long as the process."""
+    import torch
+
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    pool = _DEDICATED.setdefault(idx, [])
+    lib = load_library()
+    with torch.cuda.device(idx):
+        while len(pool) < n:
+            s = ctypes.c_void_p()
+            rc = lib.mpcx_stream_create_dedicated(ctypes.byref(s))
+            if rc != 0:
+                raise NativeError(f"mpcx_stream_create_dedicated failed ({rc})")
+            pool.append(torch.cuda.ExternalStream(s.value, device=torch.device("cuda", idx)))
+    return pool[:n]
 
 
 def admm_reduce_count(n_global: int, n_global_blocks: int, T: int) -> int:

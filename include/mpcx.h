@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MPCX_API_VERSION 14
+#define MPCX_API_VERSION 15
 
 typedef enum mpcx_err {
   MPCX_OK = 0,
@@ -435,6 +435,15 @@ int mpcx_rccl_comm_init(const char* rccl_library, int32_t nranks, int32_t rank, 
 int mpcx_rccl_comm_init_file(const char* rccl_library, const char* id_path, int32_t nranks, int32_t rank,
                              int32_t timeout_ms, void** comm);
 int mpcx_rccl_comm_destroy(const char* rccl_library, void* comm);
+
+/* ---- streams (C ABI v15) --------------------------------------------------------------------
+ * A HIP stream with a hardware queue of its own (hipExtStreamCreateWithCUMask over every CU of
+ * the current device).  Ordinary streams of a process share the runtime's few hardware queues
+ * (GPU_MAX_HW_QUEUES, 4 by default): two agent classes' solves on two such streams can land on
+ * one queue and run one after the other (r06: the C2 rooms and air handlers);
+ * an ADMM fleet gives each class a dedicated stream so that their launches overlap. */
+int mpcx_stream_create_dedicated(void** stream);
+int mpcx_stream_destroy(void* stream);
 
 #ifdef __cplusplus
 }

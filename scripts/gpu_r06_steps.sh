@@ -134,6 +134,30 @@ step_s9() {
   echo "s9 exit $?"
 }
 
+step_s11() {
+  # r06/s11: the fleet's class streams with hardware queues of their own (C ABI v15) against
+  # ordinary torch streams (MPCX_FLEET_DEDICATED=0): the C2 leg (rooms + air handlers), the C5
+  # leg (zones + AHU + CCA), the C4 leg; then the ADMM GPU tests and a kernel trace of the C2 leg
+  mkdir -p gpurun_out/s11
+  local C2="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0"
+  local C5="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c2-blocks 0 --mhe-agents 0"
+  local C4="--agents 64 --no-cpu-baseline --no-e2e --nn-zones 0 --c5-blocks 0 --c2-blocks 0 --mhe-agents 0"
+  timeout -k 10 200 python -u -m pytest tests/test_gpu_admm.py -q -rfE --timeout 120 --timeout-method thread -k dedicated -s > gpurun_out/s11/test_dedicated.txt 2>&1 || exit $?
+  for run in 1 2; do
+    timeout -k 10 300 python -u bench.py $C2 > gpurun_out/s11/c2_dedicated_$run.json 2> /dev/null || exit $?
+    MPCX_FLEET_DEDICATED=0 timeout -k 10 300 python -u bench.py $C2 > gpurun_out/s11/c2_torch_$run.json 2> /dev/null || exit $?
+  done
+  timeout -k 10 300 python -u bench.py $C5 > gpurun_out/s11/c5_dedicated.json 2> /dev/null || exit $?
+  MPCX_FLEET_DEDICATED=0 timeout -k 10 300 python -u bench.py $C5 > gpurun_out/s11/c5_torch.json 2> /dev/null || exit $?
+  timeout -k 10 300 python -u bench.py $C4 > gpurun_out/s11/c4_dedicated.json 2> /dev/null || exit $?
+  MPCX_FLEET_DEDICATED=0 timeout -k 10 300 python -u bench.py $C4 > gpurun_out/s11/c4_torch.json 2> /dev/null || exit $?
+  rm -rf gpurun_out/s11/prof_c2
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/s11/prof_c2 -o run --output-format csv -- python3 bench.py $C2 > gpurun_out/s11/c2_prof.json 2> /dev/null || exit $?
+  python scripts/iter_trace.py gpurun_out/s11/prof_c2 1 > gpurun_out/s11/c2_iterations.txt
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_admm.py -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s11/gpu_admm_tests.txt 2>&1
+  echo "s11 exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 step_s10() { record s10; }  # the record on the masked-lane kernel

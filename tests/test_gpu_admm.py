@@ -732,3 +732,33 @@ def test_gpu_collective_rccl_transport_one_rank(tmp_path):
     finally:
         assert lib.mpcx_rccl_comm_destroy(cpath, comm) == 0
     assert lib.mpcx_allreduce_kind() == native.COLLECTIVE_NONE
+
+def test_gpu_dedicated_streams_overlap():
+    """C ABI v15: two streams from mpcx_stream_create_dedicated (hardware queues of their own) run
+    a spin kernel each at the same time -- ordinary streams of a process share the runtime's few
+    hardware queues, on which the C2 rooms' and air handlers' solves ran one after the other (r06,
+    scripts/queue_probe.py)."""
+    import time
+
+    from agentlib_mpc_amd.runtime.native import dedicated_streams
+
+    a, b = dedicated_streams(2, "cuda")
+    assert a.cuda_stream != b.cuda_stream
+    cycles = 4_000_000
+
+    def run(streams):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for s in streams:
+            with torch.cuda.stream(s):
+                torch.cuda._sleep(cycles)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t
+
+    run([a, b])  # warm-up (queue creation)
+    one = min(run([a]) for _ in range(3))
+    two = min(run([a, b]) for _ in range(3))
+    print(f"one spin {one * 1e3:.3f} ms, two on dedicated streams {two * 1e3:.3f} ms")
+    assert two < 1.5 * one, (one, two)
+    assert dedicated_streams(2, "cuda")[0] is a  # the process-wide pool
+

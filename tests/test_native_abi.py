@@ -28,7 +28,7 @@ def test_library_builds_loads_and_exports_all_symbols():
     lib = ctypes.CDLL(str(path))
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.mpcx_version() == 14
+    assert lib.mpcx_version() == 15
 
 
 def test_collective_goes_through_the_registered_transport():

@@ -482,6 +482,20 @@ class ADMMFleet:
         self._class_order = ([self._lead] + [i for i in range(len(self.classes)) if i != self._lead]
                              if self._lead is not None else list(range(len(self.classes))))
         self._ev_lead = t.cuda.Event() if self._lead is not None else None
+        #: the lead class's solve on the caller's stream itself, the others on their class streams:
+        #: the two overlap on two hardware queues (the class streams share one), and the iteration's
+        #: small kernels keep their back-to-back dispatch -- C2 1076 / 931 -> 1203 / 1139 ADMM it/s,
+        #: C4 level (r06/s12).  Not for a lead class whose agents fill a CU's LDS (4 per CU or fewer,
+        #: the C5 zones: 434 / 414 -> 396 / 393): the others' workgroups then split its launch.
+        #: MPCX_FLEET_LEAD_MAIN=1 / 0 forces it on / off
+        lead_env = os.environ.get("MPCX_FLEET_LEAD_MAIN", "auto")
+        if self._lead is None or lead_env == "0":
+            self._lead_on_main = False
+        elif lead_env == "1":
+            self._lead_on_main = True
+        else:
+            lds = self.classes[self._lead].native.lds_bytes_per_agent()
+            self._lead_on_main = lds > 0 and 163840 // lds > 4
         #: coordinated rounds launch only the agents still active (mpcx_active_map +
         #: mpcx_batch_solve_mapped): each class's solve is ``bound`` workgroups over the compacted
         #: agent map, the bound being the class's active count at the last stopping check (the
@@ -616,13 +630,14 @@ class ADMMFleet:
         lead = self._lead
         for ci in self._class_order:
             c = self.classes[ci]
-            with (t.cuda.stream(streams[ci]) if streams else contextlib.nullcontext()):
-                if streams:
+            own = streams[ci] if streams and not (self._lead_on_main and ci == lead) else None
+            with (t.cuda.stream(own) if own is not None else contextlib.nullcontext()):
+                if own is not None:
                     # the other classes start once the lead class's solve is next in its queue: its
                     # workgroups claim the CUs first and the smaller classes fill what they leave
                     # (a class that needs a whole generation of the LDS, the C5 zones, split into two
                     # when the others' workgroups were dispatched beside it: r05/s14)
-                    streams[ci].wait_event(self._ev_solve if ci == lead or lead is None else self._ev_lead)
+                    own.wait_event(self._ev_solve if ci == lead or lead is None else self._ev_lead)
                 if self.fused_moves:  # every move of the class in one launch (C ABI v12), prepared
                     ops.run_plan(c.scatter_plan)
                 else:
@@ -631,7 +646,7 @@ class ADMMFleet:
                 if self._mapped:  # only the agents still active, compacted (mpcx_active_map)
                     ops.active_map(c.n, c.ACTIVE, c.MAP, self._map_counts[ci:ci + 1])
                 if streams and ci == lead:
-                    self._ev_lead.record(streams[ci])
+                    self._ev_lead.record(own if own is not None else main)
                 if self._mapped:
                     ops.solve(c, c.ACTIVE, c.MAP, c.bound)
                 else:
@@ -643,8 +658,9 @@ class ADMMFleet:
                     for cols, dst, rows in self._gather_moves(c):
                         ops.gather_rows(T, c.W, cols, dst, rows)
         if streams:
-            for st_ in streams:
-                main.wait_stream(st_)
+            for ci, st_ in enumerate(streams):
+                if not (self._lead_on_main and ci == lead):
+                    main.wait_stream(st_)
         for c in self.classes:
             if self.solve_trace is not None:
                 words = c.ST.view(t.int32).view(c.n, STATS_BYTES // 4)

@@ -151,6 +151,8 @@ int mpcx_set_options(mpcx_handle* h, const mpcx_options* opts);
 int mpcx_reserve(mpcx_handle* h, int32_t n_agents);
 /* Workspace bytes per agent (for capacity planning on 288 GB HBM). */
 int64_t mpcx_workspace_bytes_per_agent(const mpcx_handle* h);
+/* LDS bytes of one agent's workgroup on the main build (C ABI v15; -1 without a handle) */
+int64_t mpcx_lds_bytes_per_agent(const mpcx_handle* h);
 /* Small-fleet specialisation of the same structure (replaces the same reference call as
  * mpcx_problem_create, for a handful of agents -- the reference's usual one MPC agent per
  * process, core/discretization.py:203): a second code object built with the agent's

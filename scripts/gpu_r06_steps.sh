@@ -158,6 +158,40 @@ step_s11() {
   echo "s11 exit $?"
 }
 
+step_s12() {
+  # r06/s12: the lead class on the caller's stream (MPCX_FLEET_LEAD_MAIN=1: two hardware queues
+  # active) against both classes on class streams (default): C2, C5, C4 legs, twice each
+  mkdir -p gpurun_out/s12
+  local C2="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0"
+  local C5="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c2-blocks 0 --mhe-agents 0"
+  local C4="--agents 64 --no-cpu-baseline --no-e2e --nn-zones 0 --c5-blocks 0 --c2-blocks 0 --mhe-agents 0"
+  for run in 1 2; do
+    for leg in C2 C5 C4; do
+      timeout -k 10 300 python -u bench.py ${!leg} > gpurun_out/s12/${leg}_default_$run.json 2> /dev/null || exit $?
+      MPCX_FLEET_LEAD_MAIN=1 timeout -k 10 300 python -u bench.py ${!leg} > gpurun_out/s12/${leg}_leadmain_$run.json 2> /dev/null || exit $?
+    done
+  done
+  rm -rf gpurun_out/s12/prof_c2
+  MPCX_FLEET_LEAD_MAIN=1 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/s12/prof_c2 -o run --output-format csv -- python3 bench.py $C2 > gpurun_out/s12/c2_prof.json 2> /dev/null
+  echo "s12 exit $?"
+}
+
+step_s13() {
+  # r06/s13: the automatic lead-class placement (lead on the caller's stream unless its agents fill a
+  # CU's LDS): C2, C5, C4 legs twice; the ADMM GPU tests
+  mkdir -p gpurun_out/s13
+  local C2="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0"
+  local C5="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c2-blocks 0 --mhe-agents 0"
+  local C4="--agents 64 --no-cpu-baseline --no-e2e --nn-zones 0 --c5-blocks 0 --c2-blocks 0 --mhe-agents 0"
+  for run in 1 2; do
+    for leg in C2 C5 C4; do
+      timeout -k 10 300 python -u bench.py ${!leg} > gpurun_out/s13/${leg}_auto_$run.json 2> /dev/null || exit $?
+    done
+  done
+  timeout -k 10 700 python -u -m pytest tests/test_gpu_admm.py -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s13/gpu_admm_tests.txt 2>&1
+  echo "s13 exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 step_s10() { record s10; }  # the record on the masked-lane kernel

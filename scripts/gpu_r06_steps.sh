@@ -192,6 +192,20 @@ step_s13() {
   echo "s13 exit $?"
 }
 
+step_s14() {
+  # r06/s14: C3 launches of 512 agents (the north-star split: 4096 rooms over 8 GPUs) and other
+  # sizes, default routing, reference settings; a kernel trace of the 512-agent leg
+  mkdir -p gpurun_out/s14
+  local ONLY="--no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --c2-blocks 0 --mhe-agents 0 --steps 20 --warmup 3"
+  for n in 256 512 1024 2048 4096; do
+    timeout -k 10 300 python -u bench.py --agents $n $ONLY > gpurun_out/s14/c3_$n.json 2> /dev/null || exit $?
+  done
+  rm -rf gpurun_out/s14/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/s14/prof -o run --output-format csv -- python3 bench.py --agents 512 $ONLY > gpurun_out/s14/c3_512_prof.json 2> /dev/null || exit $?
+  python scripts/trace_summary.py gpurun_out/s14/prof gpurun_out/s14/kernel_trace_summary_512.txt > /dev/null
+  echo "s14 exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 step_s10() { record s10; }  # the record on the masked-lane kernel

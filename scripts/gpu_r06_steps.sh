@@ -206,6 +206,13 @@ step_s14() {
   echo "s14 exit $?"
 }
 
+step_final() {
+  # r06 final record on the committed tree: record() + the 2-rank gloo rehearsal of bench.py's N>1 path
+  record final || exit $?
+  bash scripts/gpu_mgpu_rehearsal.sh && mv gpurun_out/mgpu.json gpurun_out/mgpu.err gpurun_out/final/
+  echo "final exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 step_s10() { record s10; }  # the record on the masked-lane kernel

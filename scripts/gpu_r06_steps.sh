@@ -213,6 +213,18 @@ step_final() {
   echo "final exit $?"
 }
 
+step_s15() {
+  # r06/s15: the line search's first trial x-part computed in recover_step (base) against the
+  # committed kernel (rev)
+  mkdir -p gpurun_out/s15
+  timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s15/var_c3.txt 2>&1 || exit $?
+  AGENTS=1 timeout -k 10 300 python -u scripts/variants.py run lds_base lds_rev48 lds_base lds_rev48 > gpurun_out/s15/var_c1.txt 2>&1 || exit $?
+  MODEL=exchange_room AGENTS=13108 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s15/var_c4room.txt 2>&1 || exit $?
+  MODEL=mhe_room AGENTS=4096 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s15/var_mhe.txt 2>&1 || exit $?
+  MODEL=admm_ahu AGENTS=1024 timeout -k 10 300 python -u scripts/variants.py run base rev base rev > gpurun_out/s15/var_ahu.txt 2>&1
+  echo "s15 exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 step_s10() { record s10; }  # the record on the masked-lane kernel

@@ -110,6 +110,9 @@ VARIANTS = {
     "lds_pin_head": (["-DMPCX_WS_LDS", "-DMPCX_PIN_HEAD_BATCH"], None),
     # r06: agents per CU past the one-round rule (MHE: 4 -> 5, two stage rounds)
     "apc5": (["-DMPCX_APC=5"], None),
+    "apc20": (["-DMPCX_APC=20"], None),
+    "apc24": (["-DMPCX_APC=24"], None),
+    "apc28": (["-DMPCX_APC=28"], None),
     # r06: the main build's stage elimination / assembly without the register image (MHE)
     "noreg": (["-DMPCX_ELIM_NOREG"], None),
     "asm_noreg": (["-DMPCX_ASM_NOREG"], None),

@@ -31,6 +31,15 @@ def test_library_builds_loads_and_exports_all_symbols():
     assert lib.mpcx_version() == 15
 
 
+def test_v15_entry_points_check_their_arguments():
+    """C ABI v15 without a GPU: the LDS query answers -1 for no handle, the stream functions reject
+    a null pointer before any HIP call (the GPU side: test_gpu_dedicated_streams_overlap)."""
+    lib = native.load_library()
+    assert lib.mpcx_lds_bytes_per_agent(None) == -1
+    assert lib.mpcx_stream_create_dedicated(None) == native.ERR_ARG
+    assert lib.mpcx_stream_destroy(None) == native.ERR_ARG
+
+
 def test_collective_goes_through_the_registered_transport():
     """C ABI v14: mpcx_admm_allreduce issues the ADMM iteration's one all-reduce on the
     transport registered with the library.  A stub transport (a C-callable function that "sums" over

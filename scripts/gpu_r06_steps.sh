@@ -225,6 +225,16 @@ step_s15() {
   echo "s15 exit $?"
 }
 
+step_repro() {
+  # r06: the driver's bench command three times in separate processes (leg-to-leg reproducibility,
+  # VERDICT r05 item 5)
+  mkdir -p gpurun_out/repro
+  for run in 1 2 3; do
+    timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/repro/bench_$run.json 2> /dev/null || exit $?
+  done
+  echo "repro exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 step_s10() { record s10; }  # the record on the masked-lane kernel

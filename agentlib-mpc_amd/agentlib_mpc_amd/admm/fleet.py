@@ -504,6 +504,11 @@ class ADMMFleet:
         #: a class's per-iteration row moves (means / multipliers / penalty into p, locals out of w)
         #: as one scatter and one gather launch (C ABI v12); MPCX_FLEET_FUSED=0: one launch per move
         self.fused_moves = os.environ.get("MPCX_FLEET_FUSED", "1") != "0" and hasattr(self.ops, "scatter_plan")
+        #: the per-iteration bookkeeping of all classes in one launch each (stats count, block
+        #: expansion; C ABI v15); MPCX_FLEET_BOOK=0: one launch per class (A/B)
+        self.fused_book = self.fused_moves and os.environ.get("MPCX_FLEET_BOOK", "1") != "0"
+        self._stats_plans = {}  # freeze-mask mode -> prepared mpcx_stats_count_multi launch
+        self._expand_key, self._expand_plan = None, None
         self._prepare_moves()
         self._mapped = False
         for c in self.classes:
@@ -661,12 +666,21 @@ class ADMMFleet:
             for ci, st_ in enumerate(streams):
                 if not (self._lead_on_main and ci == lead):
                     main.wait_stream(st_)
-        for c in self.classes:
-            if self.solve_trace is not None:
+        if self.solve_trace is not None:
+            for c in self.classes:
                 words = c.ST.view(t.int32).view(c.n, STATS_BYTES // 4)
                 self.solve_trace.append((c.name, words[:, _ITER_WORD:_STATUS_WORD + 1].clone()))
-            # converged solves and restoration calls: one launch per class (mpcx_stats_count)
-            ops.stats_count(c.n, c.ST, c.ACTIVE if self._masked else None, self._counts)
+        # converged solves and restoration calls: every class in one launch (mpcx_stats_count_multi,
+        # C ABI v15; the plan per freeze-mask mode), else one launch per class
+        if self.fused_book and hasattr(ops, "stats_plan"):
+            plan = self._stats_plans.get(self._masked)
+            if plan is None:
+                plan = self._stats_plans[self._masked] = ops.stats_plan(
+                    [(c.n, c.ST, c.ACTIVE if self._masked else None) for c in self.classes], self._counts)
+            ops.run_plan(plan)
+        else:
+            for c in self.classes:
+                ops.stats_count(c.n, c.ST, c.ACTIVE if self._masked else None, self._counts)
 
     def _update_means(self, rho: float, apply_multipliers: bool, per_block: bool = False,
                       keep_control: bool = False):
@@ -942,6 +956,18 @@ class ADMMFleet:
         """Per-block penalties and freeze masks (device) to the groups and the agents (with the
         participation mask) -- what the solves, means and multiplier updates read."""
         ops = self.ops
+        if self.fused_book and hasattr(ops, "expand_plan"):
+            # the groups' and every class's expansion in one launch (mpcx_admm_block_expand_multi, C ABI
+            # v15), the plan rebuilt when the round's block mask or a participation mask is new
+            key = (active_b.data_ptr(),
+                   tuple(None if getattr(c, "PART", None) is None else c.PART.data_ptr() for c in self.classes))
+            if self._expand_key != key:
+                entries = ([(self.BLOCK_G, None, self.ACTIVE_G, self.RHO_G)] if self.G else []) + \
+                          [(c.BLOCK, getattr(c, "PART", None), c.ACTIVE, None) for c in self.classes]
+                self._expand_plan = ops.expand_plan(entries, active_b, self.RHO_B)
+                self._expand_key = key
+            ops.run_plan(self._expand_plan)
+            return
         if self.G:
             ops.block_expand(self.BLOCK_G, active_b, self.RHO_B, None, self.ACTIVE_G, self.RHO_G)
         for c in self.classes:

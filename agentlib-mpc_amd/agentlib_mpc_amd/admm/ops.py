@@ -142,6 +142,31 @@ class NativeADMMOps:
                                                   _p(out_active), _p(out_rho), self.stream),
                   "mpcx_admm_block_expand")
 
+    def expand_plan(self, entries, active_b, rho_b):
+        """A prepared ``mpcx_admm_block_expand_multi`` launch (C ABI v15): ``entries`` =
+        [(idx, part, out_active, out_rho)] -- each what :meth:`block_expand` would do, in one launch;
+        :meth:`run_plan` issues it."""
+        import torch
+
+        words = []
+        for idx, part, oa, orho in entries:
+            words += [idx.shape[0]] + [0 if x is None else x.data_ptr() for x in (idx, part, oa, orho)]
+        desc = torch.tensor(words, dtype=torch.int64, device=active_b.device)
+        args = (len(entries), _p(desc), max(e[0].shape[0] for e in entries), _p(active_b), _p(rho_b))
+        return (self.lib.mpcx_admm_block_expand_multi, args, desc, "mpcx_admm_block_expand_multi")
+
+    def stats_plan(self, entries, counts):
+        """A prepared ``mpcx_stats_count_multi`` launch (C ABI v15): ``entries`` = [(n, stats,
+        active)] counted into ``counts`` in one launch."""
+        import torch
+
+        words = []
+        for n, st, act in entries:
+            words += [int(n), st.data_ptr(), 0 if act is None else act.data_ptr()]
+        desc = torch.tensor(words, dtype=torch.int64, device=counts.device)
+        args = (len(entries), _p(desc), max(int(e[0]) for e in entries), _p(counts))
+        return (self.lib.mpcx_stats_count_multi, args, desc, "mpcx_stats_count_multi")
+
     def stats_count(self, n, stats, active, counts):
         """counts[0] += converged agents, counts[1] += their restoration calls (one launch)."""
         self._chk(self.lib.mpcx_stats_count(n, _p(stats), _p(active), _p(counts), self.stream), "mpcx_stats_count")

@@ -95,7 +95,7 @@ EXPORTED_SYMBOLS = [
     "mpcx_allreduce_register", "mpcx_allreduce_register_fn", "mpcx_allreduce_unregister", "mpcx_allreduce_kind",
     "mpcx_admm_allreduce", "mpcx_allreduce_calls", "mpcx_rccl_unique_id", "mpcx_rccl_comm_init",
     "mpcx_rccl_comm_init_file", "mpcx_rccl_comm_destroy", "mpcx_stream_create_dedicated", "mpcx_stream_destroy",
-    "mpcx_lds_bytes_per_agent",
+    "mpcx_lds_bytes_per_agent", "mpcx_admm_block_expand_multi", "mpcx_stats_count_multi",
 ]
 MOVE_DESC = 4  # MPCX_MOVE_DESC: int64 words per descriptor of the fused row moves (C ABI v12)
 ADMM_TOTALS = 8  # MPCX_ADMM_TOTALS
@@ -201,6 +201,8 @@ def load_library():
         lib.mpcx_problem_mid_fleet.argtypes = [vp, ctypes.c_char_p, i32]
         lib.mpcx_problem_wide_fleet.argtypes = [vp, ctypes.c_char_p, i32]
         lib.mpcx_workspace_bytes_per_agent.restype = ctypes.c_int64
+        lib.mpcx_admm_block_expand_multi.argtypes = [i32, vp, i32, vp, vp, vp]
+        lib.mpcx_stats_count_multi.argtypes = [i32, vp, i32, vp, vp]
         lib.mpcx_lds_bytes_per_agent.argtypes = [vp]
         lib.mpcx_lds_bytes_per_agent.restype = ctypes.c_int64
         lib.mpcx_batch_solve.argtypes = [vp, i32] + [vp] * 9 + [vp, vp]

@@ -582,7 +582,66 @@ __global__ void k_stats_count(int n, const mpcx_stats* __restrict__ st, const in
     if (fb) atomicAdd(counts + 1, (unsigned long long)fb);
   }
 }
+// several classes' block expansions / stats counts in one launch (C ABI v15): blockIdx.y selects
+// the descriptor (include/mpcx.h)
+__global__ void k_block_expand_multi(const long long* __restrict__ desc, const int* __restrict__ active_b,
+                                     const double* __restrict__ rho_b) {
+  const long long* d = desc + (long)blockIdx.y * MPCX_EXPAND_DESC;
+  const int n = (int)d[0];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int* idx = (const int*)d[1];
+  const int* part = (const int*)d[2];
+  int* out_active = (int*)d[3];
+  double* out_rho = (double*)d[4];
+  const int b = idx[i];
+  if (out_active) out_active[i] = (active_b[b] != 0 && (part == nullptr || part[i] != 0)) ? 1 : 0;
+  if (out_rho) out_rho[i] = rho_b[b];
+}
+
+__global__ void k_stats_count_multi(const long long* __restrict__ desc, unsigned long long* __restrict__ counts) {
+  const long long* d = desc + (long)blockIdx.y * MPCX_STATS_DESC;
+  const int n = (int)d[0];
+  const mpcx_stats* st = (const mpcx_stats*)d[1];
+  const int* active = (const int*)d[2];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int ok = 0, fb = 0;
+  if (i < n && (active == nullptr || active[i] != 0)) {
+    const int s = st[i].status;
+    ok = (s == 0 || s == 1) ? 1 : 0;
+    fb = st[i].n_restorations;
+  }
+#pragma unroll
+  for (int o = WAVE / 2; o > 0; o >>= 1) {
+    ok += __shfl_xor(ok, o, WAVE);
+    fb += __shfl_xor(fb, o, WAVE);
+  }
+  if ((threadIdx.x & (WAVE - 1)) == 0) {
+    if (ok) atomicAdd(counts, (unsigned long long)ok);
+    if (fb) atomicAdd(counts + 1, (unsigned long long)fb);
+  }
+}
 }  // namespace
+
+extern "C" int mpcx_admm_block_expand_multi(int32_t n_desc, const int64_t* desc, int32_t max_n,
+                                            const int32_t* active_b, const double* rho_b, void* stream) {
+  if (n_desc < 0 || max_n < 0 || (n_desc > 0 && (!desc || !active_b))) return MPCX_ERR_ARG;
+  if (n_desc == 0 || max_n == 0) return MPCX_OK;
+  hipLaunchKernelGGL(k_block_expand_multi, dim3(blocks_for(max_n, 256), n_desc), dim3(256), 0, (hipStream_t)stream,
+                     (const long long*)desc, active_b, rho_b);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
+
+extern "C" int mpcx_stats_count_multi(int32_t n_desc, const int64_t* desc, int32_t max_n, int64_t* counts,
+                                      void* stream) {
+  if (n_desc < 0 || max_n < 0 || !counts || (n_desc > 0 && !desc)) return MPCX_ERR_ARG;
+  if (n_desc == 0 || max_n == 0) return MPCX_OK;
+  hipLaunchKernelGGL(k_stats_count_multi, dim3(blocks_for(max_n, 256), n_desc), dim3(256), 0, (hipStream_t)stream,
+                     (const long long*)desc, (unsigned long long*)counts);
+  LAUNCH_CHECK();
+  return MPCX_OK;
+}
 
 extern "C" int mpcx_stats_count(int32_t n, const mpcx_stats* stats, const int32_t* active, int64_t* counts,
                                 void* stream) {

@@ -370,6 +370,17 @@ int64_t mpcx_device_clock_khz(void);
  * counts: device int64[2], accumulated across calls (the converged-solve count the reference's
  * modules log per solve, `mpc.py:397-400`, summed over a round). */
 int mpcx_stats_count(int32_t n, const mpcx_stats* stats, const int32_t* active, int64_t* counts, void* stream);
+/* The per-iteration bookkeeping of several agent classes in ONE launch each (C ABI v15): desc holds
+ * n_desc descriptors in DEVICE memory (built once per round / class set).
+ * block_expand_multi: desc k = (n, idx, part or 0, out_active or 0, out_rho or 0), MPCX_EXPAND_DESC
+ *   int64 words: mpcx_admm_block_expand of each (active_b, rho_b common), n <= max_n;
+ * stats_count_multi: desc k = (n, stats, active or 0), MPCX_STATS_DESC words: mpcx_stats_count of
+ *   each into the one counts pair. */
+#define MPCX_EXPAND_DESC 5
+#define MPCX_STATS_DESC 3
+int mpcx_admm_block_expand_multi(int32_t n_desc, const int64_t* desc, int32_t max_n, const int32_t* active_b,
+                                 const double* rho_b, void* stream);
+int mpcx_stats_count_multi(int32_t n_desc, const int64_t* desc, int32_t max_n, int64_t* counts, void* stream);
 
 /* ---- NLP vector <-> trajectory moves (no host round trip) ----------------------------
  * dst[dst_rows[a]][t] <- src[a*src_ld + cols[t]]: the coupling trajectories out of the

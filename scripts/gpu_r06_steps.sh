@@ -235,6 +235,22 @@ step_repro() {
   echo "repro exit $?"
 }
 
+step_s16() {
+  # r06/s16: the per-iteration bookkeeping fused (stats count, block expansion: one launch each for
+  # all classes) against one launch per class (MPCX_FLEET_BOOK=0): ADMM GPU tests, C2 and C5 legs
+  mkdir -p gpurun_out/s16
+  timeout -k 10 700 python -u -m pytest tests/test_gpu_admm.py -q -rfE --timeout 300 --timeout-method thread > gpurun_out/s16/gpu_admm_tests.txt 2>&1 || exit $?
+  local C2="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c5-blocks 0 --mhe-agents 0"
+  local C5="--agents 64 --no-cpu-baseline --no-e2e --admm-agents 0 --nn-zones 0 --c2-blocks 0 --mhe-agents 0"
+  for run in 1 2; do
+    for leg in C2 C5; do
+      timeout -k 10 300 python -u bench.py ${!leg} > gpurun_out/s16/${leg}_book_$run.json 2> /dev/null || exit $?
+      MPCX_FLEET_BOOK=0 timeout -k 10 300 python -u bench.py ${!leg} > gpurun_out/s16/${leg}_perclass_$run.json 2> /dev/null || exit $?
+    done
+  done
+  echo "s16 exit $?"
+}
+
 step_s7() { record s7; }
 step_s8() { record s8; }  # the record again after the non-finite-trial fix
 step_s10() { record s10; }  # the record on the masked-lane kernel

@@ -762,3 +762,57 @@ def test_gpu_dedicated_streams_overlap():
     assert two < 1.5 * one, (one, two)
     assert dedicated_streams(2, "cuda")[0] is a  # the process-wide pool
 
+
+
+def test_gpu_fused_bookkeeping_matches_per_class_launches():
+    """C ABI v15: mpcx_admm_block_expand_multi / mpcx_stats_count_multi (one launch for the groups
+    and every class) give exactly what one mpcx_admm_block_expand / mpcx_stats_count per class does
+    -- random block maps, participation masks, freeze masks and solver stats."""
+    from agentlib_mpc_amd.runtime.native import STATS_BYTES
+
+    ops = NativeADMMOps()
+    rng = np.random.default_rng(7)
+    dev = torch.device("cuda")
+    nb = 37
+    active_b = torch.as_tensor(rng.integers(0, 2, nb).astype(np.int32), device=dev)
+    rho_b = torch.as_tensor(rng.uniform(0.1, 10.0, (nb, 1)), device=dev)
+    sizes = [1000, 257, 64, 1]
+    entries, ref = [], []
+    for k, n in enumerate(sizes):
+        idx = torch.as_tensor(rng.integers(0, nb, n).astype(np.int32), device=dev)
+        part = None if k % 2 else torch.as_tensor(rng.integers(0, 2, n).astype(np.int32), device=dev)
+        oa, orho = torch.full((n,), -7, dtype=torch.int32, device=dev), None
+        if k == 0:
+            orho = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+        entries.append((idx, part, oa, orho))
+        ra = torch.full((n,), -7, dtype=torch.int32, device=dev)
+        rr = None if orho is None else torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+        ops.block_expand(idx, active_b, rho_b if rr is not None else None, part, ra, rr)
+        ref.append((ra, rr))
+    ops.run_plan(ops.expand_plan(entries, active_b, rho_b))
+    torch.cuda.synchronize()
+    for (idx, part, oa, orho), (ra, rr) in zip(entries, ref):
+        assert torch.equal(oa, ra)
+        if orho is not None:
+            assert torch.equal(orho, rr)
+    stats, counts_ref = [], torch.zeros(2, dtype=torch.int64, device=dev)
+    for n in sizes:
+        raw = np.zeros((n, STATS_BYTES // 4), np.int32)
+        st = torch.as_tensor(raw.reshape(-1).view(np.uint8), device=dev)
+        words = st.view(torch.int32).view(n, STATS_BYTES // 4)
+        act = torch.as_tensor(rng.integers(0, 2, n).astype(np.int32), device=dev)
+        stats.append((n, st, act, words))
+    # statuses and restoration counts through the native stats layout (mpcx_stats: status and
+    # n_restorations fields), written via the record's dtype
+    from agentlib_mpc_amd.runtime.native import stats_array
+    for n, st, act, _ in stats:
+        arr = stats_array(st.cpu().numpy().tobytes()).copy()
+        arr["status"] = rng.integers(-3, 3, n)
+        arr["n_restorations"] = rng.integers(0, 4, n)
+        st.copy_(torch.as_tensor(np.frombuffer(arr.tobytes(), np.uint8).copy(), device=dev))
+        ops.stats_count(n, st, act, counts_ref)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    ops.run_plan(ops.stats_plan([(n, st, act) for n, st, act, _ in stats], counts))
+    torch.cuda.synchronize()
+    assert torch.equal(counts, counts_ref), (counts, counts_ref)
+    assert int(counts_ref[0]) > 0 and int(counts_ref[1]) > 0

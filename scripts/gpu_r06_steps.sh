@@ -206,6 +206,13 @@ step_s14() {
   echo "s14 exit $?"
 }
 
+step_final2() {
+  # r06 final record after the fused bookkeeping (C ABI v15 header: new code objects)
+  record final2 || exit $?
+  bash scripts/gpu_mgpu_rehearsal.sh && mv gpurun_out/mgpu.json gpurun_out/mgpu.err gpurun_out/final2/
+  echo "final2 exit $?"
+}
+
 step_final() {
   # r06 final record on the committed tree: record() + the 2-rank gloo rehearsal of bench.py's N>1 path
   record final || exit $?
